@@ -1,0 +1,234 @@
+"""bench.py — device-resident deserialize throughput of RedRock value blobs on MI355X.
+
+Headline (BASELINE.json metric): GiB/s (+ values/s) of decoding a 1M-value mixed batch
+(config-4 proportions) that is already resident in HBM, per GPU, weak-scaled:
+each rank owns its own pre-sharded 1M batch (values are independent, so there is no data-path
+collective), and `value` = all ranks' blob bytes / max-over-ranks time.
+
+A step = one rr_decode_batch call (look-back reset + one decode launch) over the whole batch.
+Also reported: encode throughput (same batch), the roofline of the decode kernel (algorithmic
+bytes per launch / launch time vs 8 TB/s HBM3E) and, on rank 0 at N=1, the CPU baseline: the
+reference-faithful desObject restatement (oracle/rro_faithful.c) on the box's host cores.
+
+Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--n VALUES] [--config 4]
+Multi-GPU: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "GiB/s + values/s device-resident serdes, 1M mixed batch @1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+CONFIG_NAMES = {1: "100K 64-byte RAW strings", 2: "1M Zipf 16B-4KiB strings", 3: "1M hash ziplists x16 pairs",
+                4: "1M mixed String/List/Set/Hash/ZSet (config-4 proportions)"}
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--n", type=int, default=1_000_000, help="values per GPU")
+    p.add_argument("--config", type=int, default=4)
+    p.add_argument("--cpu-seconds", type=float, default=12.0, help="budget for the CPU baseline leg")
+    p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--no-check", action="store_true")
+    p.add_argument("--profile-only", action="store_true", help="decode steps only (for rocprofv3)")
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    import redrock_old_amd as rr
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    dev = torch.device(f"cuda:{local}")
+    torch.cuda.set_device(dev)
+
+    # ---- this rank's shard (pre-sharded: distinct seed per rank) ----
+    seed = int(rr.lib().rr_gen_default_seed(args.config)) + 7919 * rank
+    t0 = time.perf_counter()
+    data, offs = rr.gen_batch(args.config, args.n, seed)
+    t_gen = time.perf_counter() - t0
+    n = len(offs) - 1
+    nb = int(offs[-1])
+    types, counts = np.unique(data[offs[:-1].astype(np.int64)], return_counts=True)
+
+    eng = rr.Engine(local)
+    eng.reserve(n)
+    d_data = torch.from_numpy(data).to(dev)
+    d_offs = torch.from_numpy(offs.view(np.int64)).to(dev)
+    cap = rr.elem_bound(n, nb)
+    d_vals = torch.empty(n * 16, dtype=torch.uint8, device=dev)
+    d_elems = torch.empty(cap * 16, dtype=torch.uint8, device=dev)
+    d_arena = torch.empty((nb + 15) & ~15, dtype=torch.uint8, device=dev)
+    d_tot = torch.zeros(4, dtype=torch.int64, device=dev)
+    d_out = torch.empty((nb + 15) & ~15, dtype=torch.uint8, device=dev)
+    d_ooffs = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    d_tot2 = torch.zeros(4, dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream()
+
+    def decode():
+        eng.decode_device(d_data, d_offs, d_vals, d_elems, d_arena, d_tot, stream=stream)
+
+    def encode():
+        eng.encode_device(d_vals, d_elems, d_arena, d_out, d_ooffs, d_tot2, stream=stream)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    def timed(fn, steps, warmup):
+        for _ in range(warmup):
+            fn()
+        barrier()
+        torch.cuda.synchronize()
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        t_start = time.perf_counter()
+        ev0.record(stream)
+        for _ in range(steps):
+            fn()
+        ev1.record(stream)
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - t_start
+        barrier()
+        ev_ms = ev0.elapsed_time(ev1) / steps
+        t = torch.tensor([wall], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item()), ev_ms
+
+    if args.profile_only:
+        timed(decode, args.steps, args.warmup)
+        return
+
+    wall_dec, ev_dec = timed(decode, args.steps, args.warmup)
+    tot = d_tot.cpu().numpy().view(np.uint64).copy()
+    n_elems, n_bad, payload = int(tot[0]), int(tot[2]), int(tot[3])
+    wall_enc, ev_enc = timed(encode, args.steps, args.warmup)
+    tot2 = d_tot2.cpu().numpy().view(np.uint64).copy()
+
+    # ---- correctness of what was timed ----
+    parity = None
+    if not args.no_check:
+        rt = bool(torch.equal(d_out[:nb], d_data[:nb])) and bool(
+            np.array_equal(d_ooffs.cpu().numpy().view(np.uint64), offs))
+        parity = {"roundtrip_bit_exact": rt, "n_bad": n_bad}
+        if rank == 0 and world == 1:
+            from oracle import cpu
+            ov, oe, _, ot = cpu.decode(data, offs, nthreads=min(16, cpu.nprocs()))
+            v = d_vals.cpu().numpy().view(rr.VALUE_DT)
+            e = d_elems[: n_elems * 16].cpu().numpy().view(rr.ELEM_DT)
+            parity["decode_vs_oracle_bit_exact"] = bool(np.array_equal(v, ov) and np.array_equal(e, oe))
+
+    # ---- aggregate over ranks ----
+    agg = torch.tensor([nb, n, n_elems, payload], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(agg)
+    tot_bytes, tot_vals = float(agg[0]), float(agg[1])
+    ms_step = wall_dec / args.steps * 1e3
+    gib_s = tot_bytes * args.steps / wall_dec / 2 ** 30
+    vals_s = tot_vals * args.steps / wall_dec
+    enc_gib_s = tot_bytes * args.steps / wall_enc / 2 ** 30
+
+    # roofline of the decode kernel (SURVEY.md §8d algorithmic bytes, per launch, this rank)
+    alg_bytes = nb + 16 * n + 16 * n_elems + payload
+    achieved = alg_bytes / (ev_dec * 1e-3) / 1e9
+    enc_alg = 16 * n + 16 * n_elems + int(tot2[3]) + nb + 8 * (n + 1)
+    enc_achieved = enc_alg / (ev_enc * 1e-3) / 1e9
+
+    result = {
+        "metric": METRIC,
+        "value": round(gib_s, 2),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (seeded C generator, SURVEY.md §8d shapes)",
+        "config": {"workload": f"device-resident decode, {CONFIG_NAMES.get(args.config, args.config)}",
+                   "values_per_gpu": n, "blob_bytes_per_gpu": nb, "descriptors_per_gpu": n_elems,
+                   "parallelism": f"shard{world} (pre-sharded, no data-path collective)",
+                   "type_histogram": {int(t): int(c) for t, c in zip(types, counts)}},
+        "values_per_s": round(vals_s, 1),
+        "decode": {"gib_s": round(gib_s, 2), "values_per_s": round(vals_s, 1), "ms_per_step": round(ms_step, 4),
+                   "event_ms_per_launch": round(ev_dec, 4)},
+        "encode": {"gib_s": round(enc_gib_s, 2), "ms_per_step": round(wall_enc / args.steps * 1e3, 4),
+                   "event_ms_per_launch": round(ev_enc, 4),
+                   "roofline_achieved_GBs": round(enc_achieved, 1)},
+        "roofline": {"bound": "hbm", "kernel": "decode_kernel", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "alg_bytes_per_launch": alg_bytes},
+        "parity": parity,
+        "gen_s": round(t_gen, 2),
+    }
+
+    if rank == 0 and world == 1 and not args.no_cpu:
+        result["cpu_baseline"] = cpu_baseline(data, offs, nb, args.cpu_seconds)
+
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(data, offs, nb, budget_s):
+    """Reference-faithful desObject (one thread, robj/sds/dict/skiplist/quicklist building, as
+    rock.c:468 runs it) over the same batch, repeated within ~budget_s; median pass."""
+    from oracle import cpu
+    n = len(offs) - 1
+    # bounded sample: a prefix of the same batch sized to ~1 s per pass
+    out = {}
+    _, _, _, t_dec, t_enc = cpu.faithful_roundtrip(data[: int(offs[min(n, 20000)]) + 16], offs[: min(n, 20000) + 1])
+    per_val = max(t_dec / min(n, 20000), 1e-9)
+    m = int(min(n, max(20000, 1.0 / per_val)))
+    sub_off = offs[: m + 1]
+    sub = data[: ((int(sub_off[-1]) + 15) & ~15)]
+    times_d, times_e = [], []
+    t_end = time.perf_counter() + budget_s * 0.6
+    while len(times_d) < 3 or (time.perf_counter() < t_end and len(times_d) < 9):
+        _, _, bad, td, te = cpu.faithful_roundtrip(sub, sub_off)
+        times_d.append(td)
+        times_e.append(te)
+    sb = int(sub_off[-1])
+    td = statistics.median(times_d)
+    te = statistics.median(times_e)
+    out.update({"value": round(sb / td / 2 ** 30, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+                "sample": f"first {m} values ({sb} B) of the same batch, faithful desObject, median of {len(times_d)}",
+                "values_per_s": round(m / td, 1), "encode_gib_s": round(sb / te / 2 ** 30, 4)})
+    # flat restatement (same output as the GPU), 1 thread and all threads, same sample
+    nt = min(16, cpu.nprocs())
+    for k, thr in (("flat_1t_gib_s", 1), (f"flat_{nt}t_gib_s", nt)):
+        ts = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            cpu.decode(sub, sub_off, nthreads=thr)
+            ts.append(time.perf_counter() - t0)
+        out[k] = round(sb / statistics.median(ts) / 2 ** 30, 4)
+    out["host_cpus"] = cpu.nprocs()
+    return out
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,113 @@
+/*
+ * rr_serdes.h — batch C-ABI of the MI355X value serialize/deserialize engine.
+ *
+ * Replaces, for batches, the reference hot path of RedRock:
+ *   robj *desObject(void *buf, size_t len)   rock_serdes.h:49, defined rock_serdes.c:538
+ *   sds   serObject(robj *o)                 rock_serdes.h:48, defined rock_serdes.c:512
+ *   robj *desString(char *s, size_t len)     rock_serdes.h:47, defined rock_serdes.c:133
+ * The reference is one value per call and builds Redis heap objects; a GPU cannot build robj
+ * (host pointers), so the batch entry points below decode blobs into the flat device form of
+ * rr_format.h and encode that form back into blobs, bit-exact.  The single-value legacy
+ * signatures live in rock_serdes_compat.h.
+ *
+ * Conventions:
+ *   - return value: RR_API_OK (0) or a negative RR_API_E* code for the whole call;
+ *   - per-value status in rr_value.status (0 = OK), counted into rr_totals.n_bad;
+ *   - caller-owned buffers; one rr_ctx per host thread; no hidden host synchronisation in the
+ *     device entry points (graph-capturable: memset + 1 kernel per call).
+ * Plain C: no HIP or torch types in any signature.  Streams are passed as void* (hipStream_t).
+ */
+#ifndef RR_SERDES_H
+#define RR_SERDES_H
+
+#include <stddef.h>
+#include <stdint.h>
+#include "rr_format.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RR_API_OK        0
+#define RR_API_EINVAL   -1   /* bad argument (null pointer, misaligned buffer, n too large) */
+#define RR_API_EHIP     -2   /* a HIP runtime call failed */
+#define RR_API_ENOMEM   -3   /* device/host allocation failed */
+#define RR_API_ENODEV   -4   /* no usable GPU */
+
+typedef struct rr_ctx rr_ctx;
+
+/* Blob batch: n blobs concatenated; blob i is data[offsets[i] .. offsets[i+1]). */
+typedef struct rr_blob_batch {
+    uint8_t  *data;         /* 16-byte aligned */
+    uint64_t *offsets;      /* n+1 entries, offsets[0] == 0, non-decreasing */
+    uint64_t  n;
+    uint64_t  data_cap;     /* bytes available at data (encode output capacity) */
+} rr_blob_batch;
+
+/* Flat decoded batch (rr_format.h). */
+typedef struct rr_flat_batch {
+    rr_value *values;       /* n records */
+    rr_elem  *elems;        /* elem_cap descriptors */
+    uint8_t  *arena;        /* arena_cap bytes, 16-byte aligned */
+    uint64_t  n;
+    uint64_t  elem_cap;
+    uint64_t  arena_cap;
+} rr_flat_batch;
+
+/* Written by the device at the end of every batch call. */
+typedef struct rr_totals {
+    uint64_t n_elems;       /* descriptors written (decode) / read (encode) */
+    uint64_t bytes;         /* blob bytes read (decode) / written (encode) */
+    uint64_t n_bad;         /* values whose status != RR_OK */
+    uint64_t payload;       /* payload bytes (string/ziplist bytes) copied */
+} rr_totals;
+
+/* ---- context ------------------------------------------------------------------------ */
+int  rr_ctx_create(int device, rr_ctx **out);
+void rr_ctx_destroy(rr_ctx *ctx);
+/* Make scratch space for batches up to n values (the device calls grow it on demand too,
+ * but growing allocates; call this first when capturing graphs). */
+int  rr_ctx_reserve(rr_ctx *ctx, uint64_t n_values);
+const char *rr_last_error(void);
+
+/* ---- device-resident entry points (all pointers on ctx's device) -------------------- */
+/* Decode: needs out->n == in->n, out->arena_cap >= in->offsets[n] rounded up to 16,
+ * out->elem_cap >= number of descriptors (an upper bound is rr_decode_elem_bound()). */
+int rr_decode_batch(rr_ctx *ctx, const rr_blob_batch *in, rr_flat_batch *out,
+                    rr_totals *d_totals, void *stream);
+/* Encode: writes out->offsets[0..n] and out->data; out->data_cap bounds the bytes written
+ * (values that would not fit get RR_E_CAPACITY).  in->values[i].status is ignored. */
+int rr_encode_batch(rr_ctx *ctx, const rr_flat_batch *in, rr_blob_batch *out,
+                    rr_totals *d_totals, void *stream);
+
+/* Upper bound on descriptors a decode of `bytes` blob bytes in `n` values can produce. */
+uint64_t rr_decode_elem_bound(uint64_t n, uint64_t bytes);
+
+/* ---- host entry points (host pointers; stage through the ctx's device buffers; block) */
+int rr_decode_batch_host(rr_ctx *ctx, const uint8_t *data, const uint64_t *offsets, uint64_t n,
+                         rr_value *values, rr_elem *elems, uint64_t elem_cap,
+                         uint8_t *arena, rr_totals *totals);
+/* Returns bytes via totals->bytes; data_cap bounds the output. */
+int rr_encode_batch_host(rr_ctx *ctx, const rr_value *values, const rr_elem *elems,
+                         uint64_t n_elems, const uint8_t *arena, uint64_t arena_bytes,
+                         uint64_t n, uint8_t *data, uint64_t data_cap, uint64_t *offsets,
+                         rr_totals *totals);
+
+/* ---- synthetic batches (BASELINE.json configs) ------------------------ */
+/* config: 1 = 64-B RAW strings, 2 = Zipf 16B-4KiB strings, 3 = 16-pair hash ziplists,
+ *         4 = mixed (config-4 proportions; also the 1M headline batch and config 5 shards),
+ *         10 = edge cases, 11 = mixed with large values.  Host memory, malloc'd. */
+typedef struct rr_host_batch {
+    uint8_t  *data;
+    uint64_t *offsets;
+    uint64_t  n;
+    uint64_t  bytes;
+} rr_host_batch;
+int  rr_gen_batch(int config, uint64_t n, uint64_t seed, rr_host_batch *out);
+void rr_host_batch_free(rr_host_batch *b);
+uint64_t rr_gen_default_seed(int config);   /* 0x5EED0000 + config */
+
+#ifdef __cplusplus
+}
+#endif
+#endif

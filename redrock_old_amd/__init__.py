@@ -1,0 +1,209 @@
+"""redrock_old_amd — MI355X-native batch serialize/deserialize engine for RedRock value blobs.
+
+The product is the C-ABI library ``redrock_old_amd/librr_serdes.so`` (include/rr_serdes.h):
+hand-written gfx950 HIP kernels behind a plain-C host layer.  This module is a thin ctypes
+binding used by the tests, ``bench.py`` and ``__graft_entry__``; it adds no compute of its own
+and has no CPU fallback: if the library is missing or no GPU is present, calls raise.
+
+Reference interface it mirrors (src/rock_serdes.h:47-49): ``serObject`` / ``desObject`` turn
+one Redis object into a blob and back; here ``Engine.encode*`` / ``Engine.decode*`` do the same
+for whole batches in the flat form of include/rr_format.h.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "librr_serdes.so")
+
+# --- flat form dtypes (include/rr_format.h) ---------------------------------------------
+VALUE_DT = np.dtype([("type", "u1"), ("enc", "u1"), ("status", "<u2"), ("lru", "<u4"),
+                     ("n_elems", "<u4"), ("elem_base", "<u4")])
+ELEM_DT = np.dtype([("data", "<u8"), ("len", "<u4"), ("kind", "u1"), ("zenc", "u1"), ("rsv", "<u2")])
+assert VALUE_DT.itemsize == 16 and ELEM_DT.itemsize == 16
+
+T_STRING, T_SET_HT, T_HASH_HT, T_ZSET_SKIPLIST = 0, 2, 4, 5
+T_SET_INTSET, T_ZSET_ZIPLIST, T_HASH_ZIPLIST, T_LIST_QUICKLIST = 11, 12, 13, 14
+K_STR, K_INT, K_SCORE, K_ZLRAW = 0, 1, 2, 3
+STATUS_NAMES = {0: "OK", 1: "SHORT", 2: "TYPE", 3: "STR_ENC", 4: "STR_INTLEN", 5: "EMBSTR_LEN",
+                6: "TRUNC", 7: "COUNT", 8: "INTSET", 9: "ZL_LEN", 10: "ZL_CORRUPT", 11: "CAPACITY",
+                12: "ENCODE"}
+
+CONFIG_MIXED = 4
+
+
+class RRError(RuntimeError):
+    pass
+
+
+class Totals(C.Structure):
+    _fields_ = [("n_elems", C.c_uint64), ("bytes", C.c_uint64), ("n_bad", C.c_uint64),
+                ("payload", C.c_uint64)]
+
+    def as_dict(self):
+        return {k: int(getattr(self, k)) for k, _ in self._fields_}
+
+
+class BlobBatch(C.Structure):
+    _fields_ = [("data", C.c_void_p), ("offsets", C.c_void_p), ("n", C.c_uint64), ("data_cap", C.c_uint64)]
+
+
+class FlatBatch(C.Structure):
+    _fields_ = [("values", C.c_void_p), ("elems", C.c_void_p), ("arena", C.c_void_p), ("n", C.c_uint64),
+                ("elem_cap", C.c_uint64), ("arena_cap", C.c_uint64)]
+
+
+class HostBatch(C.Structure):
+    _fields_ = [("data", C.POINTER(C.c_uint8)), ("offsets", C.POINTER(C.c_uint64)), ("n", C.c_uint64),
+                ("bytes", C.c_uint64)]
+
+
+# Every symbol include/rr_serdes.h declares (the ABI test checks they are all exported).
+EXPORTS = ["rr_ctx_create", "rr_ctx_destroy", "rr_ctx_reserve", "rr_last_error", "rr_decode_batch",
+           "rr_encode_batch", "rr_decode_elem_bound", "rr_decode_batch_host", "rr_encode_batch_host",
+           "rr_gen_batch", "rr_host_batch_free", "rr_gen_default_seed"]
+
+_lib = None
+
+
+def lib():
+    """Load the in-tree engine library (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RRError(f"{LIB_PATH} not built: run __graft_entry__.build()")
+    L = C.CDLL(LIB_PATH)
+    vp, u64 = C.c_void_p, C.c_uint64
+    L.rr_ctx_create.argtypes = [C.c_int, C.POINTER(vp)]
+    L.rr_ctx_destroy.argtypes = [vp]
+    L.rr_ctx_destroy.restype = None
+    L.rr_ctx_reserve.argtypes = [vp, u64]
+    L.rr_last_error.restype = C.c_char_p
+    L.rr_decode_batch.argtypes = [vp, C.POINTER(BlobBatch), C.POINTER(FlatBatch), vp, vp]
+    L.rr_encode_batch.argtypes = [vp, C.POINTER(FlatBatch), C.POINTER(BlobBatch), vp, vp]
+    L.rr_decode_elem_bound.argtypes = [u64, u64]
+    L.rr_decode_elem_bound.restype = u64
+    L.rr_decode_batch_host.argtypes = [vp, vp, vp, u64, vp, vp, u64, vp, C.POINTER(Totals)]
+    L.rr_encode_batch_host.argtypes = [vp, vp, vp, u64, vp, u64, u64, vp, u64, vp, C.POINTER(Totals)]
+    L.rr_gen_batch.argtypes = [C.c_int, u64, u64, C.POINTER(HostBatch)]
+    L.rr_host_batch_free.argtypes = [C.POINTER(HostBatch)]
+    L.rr_host_batch_free.restype = None
+    L.rr_gen_default_seed.argtypes = [C.c_int]
+    L.rr_gen_default_seed.restype = u64
+    _lib = L
+    return L
+
+
+def _check(rc):
+    if rc != 0:
+        raise RRError(f"rr call failed ({rc}): {lib().rr_last_error().decode()}")
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(C.c_void_p) if a is not None and a.size else None
+
+
+def gen_batch(config: int, n: int, seed: int | None = None):
+    """Synthetic blob batch: returns (data uint8 padded to 16, offsets uint64)."""
+    L = lib()
+    if seed is None:
+        seed = L.rr_gen_default_seed(config)
+    hb = HostBatch()
+    _check(L.rr_gen_batch(config, n, seed, C.byref(hb)))
+    try:
+        nbytes = int(hb.bytes)
+        padded = (nbytes + 15) & ~15
+        data = np.ctypeslib.as_array(hb.data, shape=(max(padded, 1),))[:padded].copy() if padded else \
+            np.zeros(0, np.uint8)
+        offs = np.ctypeslib.as_array(hb.offsets, shape=(n + 1,)).copy()
+    finally:
+        L.rr_host_batch_free(C.byref(hb))
+    return data, offs
+
+
+def elem_bound(n: int, nbytes: int) -> int:
+    return int(lib().rr_decode_elem_bound(n, nbytes))
+
+
+class Engine:
+    """One engine context (one per host thread) on a HIP device."""
+
+    def __init__(self, device: int = 0):
+        self._L = lib()
+        self._ctx = C.c_void_p()
+        _check(self._L.rr_ctx_create(device, C.byref(self._ctx)))
+
+    def close(self):
+        if self._ctx:
+            self._L.rr_ctx_destroy(self._ctx)
+            self._ctx = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def reserve(self, n: int):
+        _check(self._L.rr_ctx_reserve(self._ctx, n))
+
+    # ---- host entry points ------------------------------------------------------------
+    def decode_host(self, data: np.ndarray, offsets: np.ndarray, elem_cap: int | None = None):
+        n = len(offsets) - 1
+        nbytes = int(offsets[-1])
+        if elem_cap is None:
+            elem_cap = elem_bound(n, nbytes)
+        data = np.ascontiguousarray(data, np.uint8)
+        offsets = np.ascontiguousarray(offsets, np.uint64)
+        values = np.zeros(n, VALUE_DT)
+        elems = np.zeros(max(elem_cap, 1), ELEM_DT)
+        arena = np.zeros(max(nbytes, 1), np.uint8)
+        t = Totals()
+        _check(self._L.rr_decode_batch_host(self._ctx, _ptr(data), _ptr(offsets), n, _ptr(values), _ptr(elems),
+                                            elem_cap, _ptr(arena), C.byref(t)))
+        ne = min(int(t.n_elems), elem_cap)
+        return values, elems[:ne], arena[:nbytes], t.as_dict()
+
+    def encode_host(self, values: np.ndarray, elems: np.ndarray, arena: np.ndarray, data_cap: int | None = None):
+        n = len(values)
+        values = np.ascontiguousarray(values, VALUE_DT)
+        elems = np.ascontiguousarray(elems, ELEM_DT)
+        arena = np.ascontiguousarray(arena, np.uint8)
+        if data_cap is None:
+            data_cap = encode_bound(values, elems)
+        data = np.zeros(max(data_cap, 1), np.uint8)
+        offsets = np.zeros(n + 1, np.uint64)
+        t = Totals()
+        _check(self._L.rr_encode_batch_host(self._ctx, _ptr(values), _ptr(elems), len(elems), _ptr(arena),
+                                            arena.size, n, _ptr(data), data_cap, _ptr(offsets), C.byref(t)))
+        return data[:int(offsets[-1])], offsets, t.as_dict()
+
+    # ---- device entry points (torch tensors on the engine's device) ----------------------
+    def decode_device(self, data, offsets, values, elems, arena, totals, stream=None):
+        """All arguments are torch CUDA tensors; no host sync.  stream: torch stream or None."""
+        n = offsets.numel() - 1
+        inb = BlobBatch(data.data_ptr(), offsets.data_ptr(), n, data.numel())
+        outb = FlatBatch(values.data_ptr(), elems.data_ptr(), arena.data_ptr(), n, elems.numel() // 16,
+                         arena.numel())
+        s = stream.cuda_stream if stream is not None else None
+        _check(self._L.rr_decode_batch(self._ctx, C.byref(inb), C.byref(outb), C.c_void_p(totals.data_ptr()),
+                                       C.c_void_p(s) if s else None))
+
+    def encode_device(self, values, elems, arena, out_data, out_offsets, totals, stream=None):
+        n = out_offsets.numel() - 1
+        inb = FlatBatch(values.data_ptr(), elems.data_ptr(), arena.data_ptr(), n, elems.numel() // 16,
+                        arena.numel())
+        outb = BlobBatch(out_data.data_ptr(), out_offsets.data_ptr(), n, out_data.numel())
+        s = stream.cuda_stream if stream is not None else None
+        _check(self._L.rr_encode_batch(self._ctx, C.byref(inb), C.byref(outb), C.c_void_p(totals.data_ptr()),
+                                       C.c_void_p(s) if s else None))
+
+
+def encode_bound(values: np.ndarray, elems: np.ndarray) -> int:
+    """Upper bound on encoded bytes for a flat batch (decimal ints <= 20 chars + 4-byte prefix;
+    every other element costs <= 16 + len)."""
+    return int(len(values) * 13 + len(elems) * 24 + int(elems["len"].astype(np.uint64).sum()) + 16)

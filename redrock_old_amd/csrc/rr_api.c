@@ -1,0 +1,194 @@
+/*
+ * rr_api.c — the C host layer of the engine (plain C99 over the HIP runtime C API).
+ *
+ * Implements include/rr_serdes.h: contexts, argument checks, device-resident batch calls
+ * (a hipMemsetAsync of the look-back words + one kernel, no host sync) and host-pointer
+ * variants that stage through pinned buffers and the context's device buffers.
+ */
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "rr_kernels.h"
+
+struct rr_ctx {
+    int device;
+    hipStream_t stream;          /* used by the host entry points */
+    uint64_t *scratch;           /* look-back words + counters */
+    uint64_t scratch_tiles;
+    /* device staging for host entry points */
+    void *d_in, *d_off, *d_vals, *d_elems, *d_arena, *d_out, *d_ooff;
+    size_t c_in, c_off, c_vals, c_elems, c_arena, c_out, c_ooff;
+    rr_totals *d_totals;
+};
+
+static __thread char g_err[256];
+const char *rr_last_error(void) { return g_err; }
+static int fail(int code, const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof g_err, fmt, ap);
+    va_end(ap);
+    return code;
+}
+#define HIPCHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) \
+    return fail(RR_API_EHIP, "%s:%d %s: %s", __FILE__, __LINE__, #x, hipGetErrorString(e_)); } while (0)
+
+int rr_ctx_create(int device, rr_ctx **out) {
+    if (!out) return fail(RR_API_EINVAL, "out is NULL");
+    *out = NULL;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(RR_API_ENODEV, "no HIP device");
+    if (device < 0 || device >= ndev) return fail(RR_API_EINVAL, "device %d out of range", device);
+    HIPCHK(hipSetDevice(device));
+    rr_ctx *c = (rr_ctx *)calloc(1, sizeof *c);
+    if (!c) return fail(RR_API_ENOMEM, "calloc");
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        free(c);
+        return fail(RR_API_EHIP, "hipStreamCreate");
+    }
+    if (hipMalloc((void **)&c->d_totals, sizeof(rr_totals)) != hipSuccess) {
+        hipStreamDestroy(c->stream);
+        free(c);
+        return fail(RR_API_ENOMEM, "hipMalloc totals");
+    }
+    *out = c;
+    return RR_API_OK;
+}
+
+static void dfree(void **p, size_t *c) { if (*p) hipFree(*p); *p = NULL; *c = 0; }
+
+void rr_ctx_destroy(rr_ctx *c) {
+    if (!c) return;
+    hipSetDevice(c->device);
+    if (c->scratch) hipFree(c->scratch);
+    dfree(&c->d_in, &c->c_in); dfree(&c->d_off, &c->c_off); dfree(&c->d_vals, &c->c_vals);
+    dfree(&c->d_elems, &c->c_elems); dfree(&c->d_arena, &c->c_arena); dfree(&c->d_out, &c->c_out);
+    dfree(&c->d_ooff, &c->c_ooff);
+    if (c->d_totals) hipFree(c->d_totals);
+    hipStreamDestroy(c->stream);
+    free(c);
+}
+
+int rr_ctx_reserve(rr_ctx *c, uint64_t n_values) {
+    if (!c) return fail(RR_API_EINVAL, "ctx is NULL");
+    uint64_t tiles = (n_values + rr_tile_values() - 1) / rr_tile_values();
+    if (c->scratch && tiles <= c->scratch_tiles) return RR_API_OK;
+    HIPCHK(hipSetDevice(c->device));
+    if (c->scratch) { HIPCHK(hipDeviceSynchronize()); hipFree(c->scratch); c->scratch = NULL; }
+    uint64_t want = tiles + tiles / 4 + 64;
+    if (hipMalloc((void **)&c->scratch, (RR_SCRATCH_HDR + want) * sizeof(uint64_t)) != hipSuccess)
+        return fail(RR_API_ENOMEM, "hipMalloc scratch (%llu tiles)", (unsigned long long)want);
+    c->scratch_tiles = want;
+    return RR_API_OK;
+}
+
+uint64_t rr_decode_elem_bound(uint64_t n, uint64_t bytes) {
+    /* every descriptor but a value's first consumes >= 2 blob bytes (ziplist entry / intset
+     * member minimum); the first may come from the 5-byte header alone. */
+    return n + bytes / 2;
+}
+
+static int aligned16(const void *p) { return ((uintptr_t)p & 15) == 0; }
+
+int rr_decode_batch(rr_ctx *c, const rr_blob_batch *in, rr_flat_batch *out, rr_totals *d_totals, void *stream) {
+    if (!c || !in || !out) return fail(RR_API_EINVAL, "NULL argument");
+    if (out->n != in->n) return fail(RR_API_EINVAL, "out->n != in->n");
+    if (in->n >= (1ull << 37)) return fail(RR_API_EINVAL, "batch too large");
+    if (in->n && (!in->data || !in->offsets || !out->values || !out->arena))
+        return fail(RR_API_EINVAL, "NULL buffer");
+    if (!aligned16(in->data) || !aligned16(out->arena)) return fail(RR_API_EINVAL, "data/arena not 16-byte aligned");
+    int rc = rr_ctx_reserve(c, in->n);
+    if (rc) return rc;
+    HIPCHK(rr_launch_decode(in->data, in->offsets, in->n, out->values, out->elems, out->elem_cap, out->arena,
+                            c->scratch, d_totals, (hipStream_t)stream));
+    return RR_API_OK;
+}
+
+int rr_encode_batch(rr_ctx *c, const rr_flat_batch *in, rr_blob_batch *out, rr_totals *d_totals, void *stream) {
+    if (!c || !in || !out) return fail(RR_API_EINVAL, "NULL argument");
+    if (out->n != in->n) return fail(RR_API_EINVAL, "out->n != in->n");
+    if (in->n >= (1ull << 37)) return fail(RR_API_EINVAL, "batch too large");
+    if (!out->offsets) return fail(RR_API_EINVAL, "NULL offsets");
+    if (in->n && (!in->values || !out->data)) return fail(RR_API_EINVAL, "NULL buffer");
+    int rc = rr_ctx_reserve(c, in->n);
+    if (rc) return rc;
+    HIPCHK(rr_launch_encode(in->values, in->elems, in->arena, in->n, out->data, out->data_cap, out->offsets,
+                            c->scratch, d_totals, (hipStream_t)stream));
+    return RR_API_OK;
+}
+
+/* grow a device staging buffer (host entry points only) */
+static int dgrow(void **p, size_t *cap, size_t need) {
+    if (need <= *cap && *p) return RR_API_OK;
+    if (*p) hipFree(*p);
+    *p = NULL;
+    *cap = 0;
+    size_t want = need + need / 8 + 256;
+    if (hipMalloc(p, want) != hipSuccess) return fail(RR_API_ENOMEM, "hipMalloc %zu", want);
+    *cap = want;
+    return RR_API_OK;
+}
+#define GROW(P, C, N) do { int r_ = dgrow((void **)&(P), &(C), (N)); if (r_) return r_; } while (0)
+
+int rr_decode_batch_host(rr_ctx *c, const uint8_t *data, const uint64_t *offsets, uint64_t n, rr_value *values,
+                         rr_elem *elems, uint64_t elem_cap, uint8_t *arena, rr_totals *totals) {
+    if (!c || !offsets || (n && (!data || !values))) return fail(RR_API_EINVAL, "NULL argument");
+    HIPCHK(hipSetDevice(c->device));
+    uint64_t bytes = offsets[n];
+    size_t pbytes = (size_t)((bytes + 15) & ~15ull) + 16;
+    GROW(c->d_in, c->c_in, pbytes);
+    GROW(c->d_off, c->c_off, (n + 1) * sizeof(uint64_t));
+    GROW(c->d_vals, c->c_vals, (n ? n : 1) * sizeof(rr_value));
+    GROW(c->d_elems, c->c_elems, (elem_cap ? elem_cap : 1) * sizeof(rr_elem));
+    GROW(c->d_arena, c->c_arena, pbytes);
+    HIPCHK(hipMemsetAsync(c->d_in, 0, pbytes, c->stream));
+    if (bytes) HIPCHK(hipMemcpyAsync(c->d_in, data, bytes, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->d_off, offsets, (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
+    rr_blob_batch in = {(uint8_t *)c->d_in, (uint64_t *)c->d_off, n, pbytes};
+    rr_flat_batch out = {(rr_value *)c->d_vals, (rr_elem *)c->d_elems, (uint8_t *)c->d_arena, n, elem_cap, pbytes};
+    int rc = rr_decode_batch(c, &in, &out, c->d_totals, c->stream);
+    if (rc) return rc;
+    rr_totals t;
+    HIPCHK(hipMemcpyAsync(&t, c->d_totals, sizeof t, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (n) HIPCHK(hipMemcpyAsync(values, c->d_vals, n * sizeof(rr_value), hipMemcpyDeviceToHost, c->stream));
+    uint64_t ne = t.n_elems < elem_cap ? t.n_elems : elem_cap;
+    if (ne && elems) HIPCHK(hipMemcpyAsync(elems, c->d_elems, ne * sizeof(rr_elem), hipMemcpyDeviceToHost, c->stream));
+    if (bytes && arena) HIPCHK(hipMemcpyAsync(arena, c->d_arena, bytes, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (n == 0) memset(&t, 0, sizeof t);
+    if (totals) *totals = t;
+    return RR_API_OK;
+}
+
+int rr_encode_batch_host(rr_ctx *c, const rr_value *values, const rr_elem *elems, uint64_t n_elems,
+                         const uint8_t *arena, uint64_t arena_bytes, uint64_t n, uint8_t *data, uint64_t data_cap,
+                         uint64_t *offsets, rr_totals *totals) {
+    if (!c || !offsets || (n && (!values || !data))) return fail(RR_API_EINVAL, "NULL argument");
+    HIPCHK(hipSetDevice(c->device));
+    GROW(c->d_vals, c->c_vals, (n ? n : 1) * sizeof(rr_value));
+    GROW(c->d_elems, c->c_elems, (n_elems ? n_elems : 1) * sizeof(rr_elem));
+    GROW(c->d_arena, c->c_arena, arena_bytes + 16);
+    GROW(c->d_out, c->c_out, data_cap + 16);
+    GROW(c->d_ooff, c->c_ooff, (n + 1) * sizeof(uint64_t));
+    if (n) HIPCHK(hipMemcpyAsync(c->d_vals, values, n * sizeof(rr_value), hipMemcpyHostToDevice, c->stream));
+    if (n_elems) HIPCHK(hipMemcpyAsync(c->d_elems, elems, n_elems * sizeof(rr_elem), hipMemcpyHostToDevice, c->stream));
+    if (arena_bytes) HIPCHK(hipMemcpyAsync(c->d_arena, arena, arena_bytes, hipMemcpyHostToDevice, c->stream));
+    rr_flat_batch in = {(rr_value *)c->d_vals, (rr_elem *)c->d_elems, (uint8_t *)c->d_arena, n, n_elems, arena_bytes};
+    rr_blob_batch out = {(uint8_t *)c->d_out, (uint64_t *)c->d_ooff, n, data_cap};
+    int rc = rr_encode_batch(c, &in, &out, c->d_totals, c->stream);
+    if (rc) return rc;
+    rr_totals t;
+    HIPCHK(hipMemcpyAsync(&t, c->d_totals, sizeof t, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(offsets, c->d_ooff, (n + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    uint64_t nb = t.bytes < data_cap ? t.bytes : data_cap;
+    if (nb) HIPCHK(hipMemcpyAsync(data, c->d_out, nb, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (n == 0) memset(&t, 0, sizeof t);
+    if (totals) *totals = t;
+    return RR_API_OK;
+}

@@ -1,0 +1,154 @@
+// rr_device.h — device-side building blocks shared by the decode and encode kernels:
+// unaligned little-endian loads, strict integer parse / decimal render (util.c, sds.c),
+// wave64 scans and the decoupled look-back used for output offsets.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/rr_format.h"
+
+#define RR_WAVE 64
+
+namespace rr {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint32_t ld_u8(const uint8_t *p) { return *p; }
+__device__ __forceinline__ uint32_t ld_u32(const uint8_t *p) {
+    uint32_t v;
+    __builtin_memcpy(&v, p, 4);
+    return v;
+}
+__device__ __forceinline__ uint64_t ld_u64(const uint8_t *p) {
+    uint64_t v;
+    __builtin_memcpy(&v, p, 8);
+    return v;
+}
+
+// util.c:360-424 string2ll, restricted by zipTryEncoding (ziplist.c:480): 1 <= len < 32.
+__device__ __forceinline__ bool zip_try_int(const uint8_t *s, uint32_t len, int64_t &out) {
+    if (len == 0 || len >= 32) return false;
+    uint32_t c0 = ld_u8(s);
+    if (len == 1 && c0 == '0') { out = 0; return true; }
+    uint32_t i = 0;
+    bool neg = false;
+    if (c0 == '-') {
+        neg = true;
+        i = 1;
+        if (len == 1) return false;
+    }
+    uint32_t c = ld_u8(s + i);
+    if (c < '1' || c > '9') return false;
+    uint64_t v = c - '0';
+    ++i;
+    for (; i < len; ++i) {
+        c = ld_u8(s + i);
+        if (c < '0' || c > '9') return false;
+        if (v > (~0ull / 10)) return false;
+        v *= 10;
+        if (v > (~0ull - (c - '0'))) return false;
+        v += c - '0';
+    }
+    if (neg) {
+        if (v > (1ull << 63)) return false;
+        out = (int64_t)(0ull - v);
+    } else {
+        if (v > 0x7FFFFFFFFFFFFFFFull) return false;
+        out = (int64_t)v;
+    }
+    return true;
+}
+
+// Length of sdsll2str(v) (sds.c:450-479).
+__device__ __forceinline__ uint32_t dec_len(int64_t value) {
+    uint64_t v = value < 0 ? 0ull - (uint64_t)value : (uint64_t)value;
+    uint32_t l = 1;
+    while (v >= 10) { v /= 10; ++l; }
+    return l + (value < 0 ? 1u : 0u);
+}
+// Writes sdsll2str(v) at d (byte stores), returns length.
+__device__ __forceinline__ uint32_t dec_write(uint8_t *d, int64_t value) {
+    uint32_t l = dec_len(value);
+    uint64_t v = value < 0 ? 0ull - (uint64_t)value : (uint64_t)value;
+    uint32_t p = l;
+    do { d[--p] = (uint8_t)('0' + (v % 10)); v /= 10; } while (v);
+    if (value < 0) d[0] = '-';
+    return l;
+}
+
+__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+
+// Wave64 inclusive scan (u64) with shuffles.
+__device__ __forceinline__ uint64_t wave_incl_scan(uint64_t x) {
+    uint32_t lane = lane_id();
+#pragma unroll
+    for (int d = 1; d < RR_WAVE; d <<= 1) {
+        uint64_t y = __shfl_up(x, d, RR_WAVE);
+        if (lane >= (uint32_t)d) x += y;
+    }
+    return x;
+}
+__device__ __forceinline__ uint64_t wave_sum(uint64_t x) {
+#pragma unroll
+    for (int d = RR_WAVE / 2; d > 0; d >>= 1) x += __shfl_xor(x, d, RR_WAVE);
+    return x;
+}
+
+// ---- decoupled look-back (single-pass scan across wave tiles) ---------------------------
+// One 8-byte word per tile: bits 62-63 flag (0 empty, 1 aggregate, 2 inclusive prefix),
+// bits 0-61 value.  The word is the data (a self-contained granule written by one relaxed
+// agent-scope store = sc1), so no separate flag and no fence are needed
+// (cdna_hip_programming.md §6 Guideline 16, R2).  Words are zeroed by a hipMemsetAsync
+// before every launch.  Tile ids are handed out in launch order by an atomic counter, so a
+// tile only waits on tiles whose waves are already resident.
+constexpr uint64_t LB_AGG = 1ull << 62;
+constexpr uint64_t LB_INC = 2ull << 62;
+constexpr uint64_t LB_VAL = (1ull << 62) - 1;
+
+__device__ __forceinline__ void lb_store(uint64_t *p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t lb_load(uint64_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Returns the exclusive prefix of tile `tile` (wave-uniform); agg is wave-uniform.
+__device__ __forceinline__ uint64_t lookback(uint64_t *state, uint32_t tile, uint64_t agg) {
+    uint32_t lane = lane_id();
+    if (tile == 0) {
+        if (lane == 0) lb_store(&state[0], LB_INC | agg);
+        return 0;
+    }
+    if (lane == 0) lb_store(&state[tile], LB_AGG | agg);
+    uint64_t excl = 0;
+    int64_t base = (int64_t)tile - 1;
+    for (uint32_t spins = 0;; ++spins) {
+        int64_t j = base - (int64_t)lane;
+        uint64_t s = j >= 0 ? lb_load(&state[j]) : LB_INC;
+        uint64_t flag = s >> 62;
+        uint64_t inc = __ballot(flag == 2);
+        uint64_t empty = __ballot(flag == 0);
+        uint32_t first = inc ? (uint32_t)__builtin_ctzll(inc) : 64u;
+        uint64_t upto = first >= 63 ? ~0ull : ((2ull << first) - 1);
+        if (empty & upto) {
+            // bounded spin: a predecessor that never publishes must not hang the GPU
+            if (spins > (1u << 24)) { excl = LB_VAL; break; }
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        uint64_t v = lane <= first ? (s & LB_VAL) : 0;
+        excl += wave_sum(v);
+        if (first < 64) break;
+        base -= RR_WAVE;
+    }
+    if (lane == 0) lb_store(&state[tile], LB_INC | (excl + agg));
+    return excl;
+}
+
+__device__ __forceinline__ uint32_t next_tile(uint64_t *counter) {
+    uint32_t t = 0;
+    if (lane_id() == 0) t = (uint32_t)atomicAdd((unsigned long long *)counter, 1ull);
+    return __builtin_amdgcn_readfirstlane(t);
+}
+
+}  // namespace rr

@@ -1,0 +1,30 @@
+/* rr_kernels.h — launch entry points of rr_kernels.hip, called by the C host layer (rr_api.c). */
+#ifndef RR_KERNELS_H
+#define RR_KERNELS_H
+
+#include <hip/hip_runtime_api.h>
+#include <stdint.h>
+
+#include "../../include/rr_format.h"
+#include "../../include/rr_serdes.h"
+
+/* scratch layout (uint64 words): [0] tile counter, [1] done counter, [2] byte total,
+ * [8 .. 8+64) 16 shards x {bad, payload, elems, -}, then one look-back word per tile. */
+#define RR_SCRATCH_HDR 72
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+hipError_t rr_launch_decode(const uint8_t *blob, const uint64_t *offsets, uint64_t n, rr_value *values,
+                            rr_elem *elems, uint64_t elem_cap, uint8_t *arena, uint64_t *scratch,
+                            rr_totals *totals, hipStream_t stream);
+hipError_t rr_launch_encode(const rr_value *values, const rr_elem *elems, const uint8_t *arena, uint64_t n,
+                            uint8_t *out, uint64_t cap, uint64_t *offsets, uint64_t *scratch,
+                            rr_totals *totals, hipStream_t stream);
+uint64_t rr_tile_values(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

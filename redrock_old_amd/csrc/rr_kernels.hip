@@ -1,0 +1,667 @@
+// rr_kernels.hip — CDNA4 (gfx950) decode and encode kernels for RedRock value blobs.
+//
+// Decode (blob batch -> flat batch), one launch, single pass:
+//   a wave owns a TILE of 64 consecutive values (lane = value);
+//   1. the wave streams the tile's contiguous blob bytes into the MIRROR arena with aligned
+//      16-byte loads/stores (every value's payload lands at its blob offset, so no arena scan);
+//   2. each lane parses its value header/chain (count pass: validates exactly like
+//      rock_serdes.c's asserts, counts descriptors);
+//   3. wave scan + decoupled look-back across tiles -> each value's elem_base;
+//   4. each lane re-parses (L2-hot) and writes its descriptors, the wave writes the 16-byte
+//      value records coalesced.
+// Encode (flat batch -> blob batch), one launch, single pass:
+//   lane = value: size pass from the descriptors, wave scan + look-back -> blob offsets,
+//   then headers/length fields by the lane and bulk payloads by the whole wave.
+//
+// No MFMA: this is byte/record work bounded by HBM.
+#include <hip/hip_runtime.h>
+
+#include "rr_device.h"
+#include "rr_kernels.h"
+
+using namespace rr;
+
+namespace {
+
+constexpr uint32_t TILE = RR_WAVE;       // values per wave tile
+constexpr uint32_t WG = 256;             // 4 independent waves per workgroup
+
+struct Parsed {
+    uint32_t status;
+    uint32_t enc;
+    uint64_t n;        // descriptors
+    uint64_t payload;  // payload bytes (string / ziplist bytes)
+};
+
+__device__ __forceinline__ void put_elem(rr_elem *e, uint64_t data, uint32_t len, uint32_t kind, uint32_t zenc) {
+    uint4 w;
+    w.x = (uint32_t)data;
+    w.y = (uint32_t)(data >> 32);
+    w.z = len;
+    w.w = kind | (zenc << 8);
+    *reinterpret_cast<uint4 *>(e) = w;
+}
+
+// ziplist walk, ziplist.c:300-447; bounds checked.  zl points at the ziplist (L bytes),
+// zoff is its offset in the batch (arena offsets of string entries = zoff + position).
+template <bool EMIT>
+__device__ uint32_t parse_ziplist(const uint8_t *zl, uint64_t L, uint64_t zoff, rr_elem *out, uint64_t &count) {
+    count = 0;
+    if (L < 11 || ld_u32(zl) != L) return RR_E_ZL_CORRUPT;
+    uint32_t zltail = ld_u32(zl + 4);
+    uint32_t zllen = ld_u8(zl + 8) | (ld_u8(zl + 9) << 8);
+    uint64_t p = 10, prev_raw = 0, last = 10, n = 0;
+    for (;;) {
+        if (p >= L) return RR_E_ZL_CORRUPT;
+        uint32_t b0 = ld_u8(zl + p);
+        if (b0 == 0xFF) break;
+        uint64_t pl, pls;
+        if (b0 < 254) { pl = b0; pls = 1; }
+        else {
+            if (p + 5 > L - 1) return RR_E_ZL_CORRUPT;
+            pl = ld_u32(zl + p + 1);
+            pls = 5;
+        }
+        if (pl != prev_raw) return RR_E_ZL_CORRUPT;
+        uint64_t q = p + pls;
+        if (q >= L - 1) return RR_E_ZL_CORRUPT;
+        uint32_t enc = ld_u8(zl + q);
+        uint64_t end;
+        if (enc < 0xC0) {
+            uint32_t cls = enc & 0xC0;
+            uint64_t ls, sl;
+            if (cls == 0x00) { ls = 1; sl = enc & 0x3F; }
+            else if (cls == 0x40) {
+                if (q + 2 > L - 1) return RR_E_ZL_CORRUPT;
+                ls = 2;
+                sl = ((uint64_t)(enc & 0x3F) << 8) | ld_u8(zl + q + 1);
+            } else {
+                if (q + 5 > L - 1) return RR_E_ZL_CORRUPT;
+                ls = 5;
+                sl = ((uint64_t)ld_u8(zl + q + 1) << 24) | ((uint64_t)ld_u8(zl + q + 2) << 16) |
+                     ((uint64_t)ld_u8(zl + q + 3) << 8) | ld_u8(zl + q + 4);
+            }
+            uint64_t d = q + ls;
+            end = d + sl;
+            if (end > L - 1) return RR_E_ZL_CORRUPT;
+            if (EMIT) put_elem(out + n, zoff + d, (uint32_t)sl, RR_K_STR, cls);
+        } else {
+            uint64_t isz;
+            switch (enc) {
+                case 0xFE: isz = 1; break;
+                case 0xC0: isz = 2; break;
+                case 0xF0: isz = 3; break;
+                case 0xD0: isz = 4; break;
+                case 0xE0: isz = 8; break;
+                default:
+                    if (enc >= 0xF1 && enc <= 0xFD) isz = 0;
+                    else return RR_E_ZL_CORRUPT;
+            }
+            uint64_t d = q + 1;
+            end = d + isz;
+            if (end > L - 1) return RR_E_ZL_CORRUPT;
+            if (EMIT) {
+                int64_t v;
+                const uint8_t *x = zl + d;
+                if (isz == 0) v = (int64_t)(enc & 0x0F) - 1;
+                else if (isz == 1) v = (int8_t)ld_u8(x);
+                else if (isz == 2) v = (int16_t)(ld_u8(x) | (ld_u8(x + 1) << 8));
+                else if (isz == 3) v = ((int32_t)((ld_u8(x) << 8) | (ld_u8(x + 1) << 16) | (ld_u8(x + 2) << 24))) >> 8;
+                else if (isz == 4) v = (int32_t)ld_u32(x);
+                else v = (int64_t)ld_u64(x);
+                put_elem(out + n, (uint64_t)v, 0, RR_K_INT, enc);
+            }
+        }
+        ++n;
+        prev_raw = end - p;
+        last = p;
+        p = end;
+    }
+    if (p != L - 1) return RR_E_ZL_CORRUPT;
+    if (zllen != 0xFFFF && zllen != n) return RR_E_ZL_CORRUPT;
+    if (zltail != last) return RR_E_ZL_CORRUPT;
+    count = n;
+    return RR_OK;
+}
+
+// desObject rock_serdes.c:538-564 and des* :133-508, on one blob at b (batch offset off).
+template <bool EMIT>
+__device__ Parsed parse_value(const uint8_t *b, uint64_t off, uint64_t len, rr_elem *out) {
+    Parsed r{RR_OK, 0, 0, 0};
+    uint64_t n = 0, pay = 0;
+    if (len < 5) { r.status = RR_E_SHORT; return r; }
+    uint32_t type = ld_u8(b);
+    uint64_t p = 5, rem = len - 5;
+    uint32_t st = RR_OK;
+    switch (type) {
+        case RR_TYPE_STRING: {
+            if (len < 6) { st = RR_E_SHORT; break; }
+            uint32_t enc = ld_u8(b + 5);
+            r.enc = enc;
+            uint64_t rest = len - 6;
+            if (enc == RR_ENC_INT) {
+                if (rest != 8) { st = RR_E_STR_INTLEN; break; }
+                if (EMIT) put_elem(out, ld_u64(b + 6), 0, RR_K_INT, 0);
+                n = 1;
+            } else if (enc == RR_ENC_RAW || enc == RR_ENC_EMBSTR) {
+                if (enc == RR_ENC_EMBSTR && rest > RR_EMBSTR_SIZE_LIMIT) { st = RR_E_EMBSTR_LEN; break; }
+                if (rest > 0xFFFFFFFFull) { st = RR_E_CAPACITY; break; }
+                if (EMIT) put_elem(out, off + 6, (uint32_t)rest, RR_K_STR, 0);
+                n = 1;
+                pay = rest;
+            } else st = RR_E_STR_ENC;
+            break;
+        }
+        case RR_TYPE_LIST_QUICKLIST:
+            while (rem) {
+                if (rem < 4) { st = RR_E_TRUNC; break; }
+                uint64_t l = ld_u32(b + p);
+                p += 4;
+                rem -= 4;
+                if (l > rem) { st = RR_E_TRUNC; break; }
+                if (EMIT) {
+                    int64_t iv;
+                    if (zip_try_int(b + p, (uint32_t)l, iv)) put_elem(out + n, (uint64_t)iv, 0, RR_K_INT, 0);
+                    else { put_elem(out + n, off + p, (uint32_t)l, RR_K_STR, 0); pay += l; }
+                }
+                ++n;
+                p += l;
+                rem -= l;
+            }
+            break;
+        case RR_TYPE_SET_INTSET: {
+            if (rem < 8) { st = RR_E_SHORT; break; }
+            uint64_t w = ld_u32(b + p), cnt = ld_u32(b + p + 4);
+            p += 8;
+            rem -= 8;
+            if ((w != 2 && w != 4 && w != 8) || rem != w * cnt) { st = RR_E_INTSET; break; }
+            r.enc = (uint32_t)w;
+            if (EMIT) {
+                for (uint64_t i = 0; i < cnt; ++i) {
+                    const uint8_t *q = b + p + i * w;
+                    int64_t x = w == 2 ? (int64_t)(int16_t)(ld_u8(q) | (ld_u8(q + 1) << 8))
+                              : w == 4 ? (int64_t)(int32_t)ld_u32(q) : (int64_t)ld_u64(q);
+                    put_elem(out + i, (uint64_t)x, 0, RR_K_INT, 0);
+                }
+            }
+            n = cnt;
+            break;
+        }
+        case RR_TYPE_SET_HT:
+        case RR_TYPE_HASH_HT: {
+            if (rem < 8) { st = RR_E_SHORT; break; }
+            uint64_t cnt = ld_u64(b + p), got = 0;
+            uint32_t per = type == RR_TYPE_SET_HT ? 1 : 2;
+            p += 8;
+            rem -= 8;
+            while (rem && st == RR_OK) {
+                for (uint32_t k = 0; k < per; ++k) {
+                    if (rem < 8) { st = RR_E_TRUNC; break; }
+                    uint64_t l = ld_u64(b + p);
+                    p += 8;
+                    rem -= 8;
+                    if (l > rem) { st = RR_E_TRUNC; break; }
+                    if (EMIT) put_elem(out + n, off + p, (uint32_t)l, RR_K_STR, 0);
+                    ++n;
+                    pay += l;
+                    p += l;
+                    rem -= l;
+                }
+                ++got;
+            }
+            if (st == RR_OK && got != cnt) st = RR_E_COUNT;
+            break;
+        }
+        case RR_TYPE_HASH_ZIPLIST:
+        case RR_TYPE_ZSET_ZIPLIST: {
+            if (rem < 8) { st = RR_E_SHORT; break; }
+            uint64_t L = ld_u64(b + p);
+            p += 8;
+            rem -= 8;
+            if (rem != L) { st = RR_E_ZL_LEN; break; }
+            uint64_t cnt;
+            st = parse_ziplist<EMIT>(b + p, L, off + p, out + 1, cnt);
+            if (st == RR_OK && (cnt & 1)) st = RR_E_ZL_CORRUPT;
+            if (st != RR_OK) break;
+            if (EMIT) put_elem(out, off + p, (uint32_t)L, RR_K_ZLRAW, 0);
+            n = 1 + cnt;
+            pay = L;
+            break;
+        }
+        case RR_TYPE_ZSET_SKIPLIST: {
+            if (rem < 8) { st = RR_E_SHORT; break; }
+            uint64_t cnt = ld_u64(b + p);
+            p += 8;
+            rem -= 8;
+            for (uint64_t i = 0; i < cnt; ++i) {
+                if (rem < 8) { st = RR_E_TRUNC; break; }
+                uint64_t l = ld_u64(b + p);
+                p += 8;
+                rem -= 8;
+                if (l > rem) { st = RR_E_TRUNC; break; }
+                if (EMIT) put_elem(out + n, off + p, (uint32_t)l, RR_K_STR, 0);
+                pay += l;
+                p += l;
+                rem -= l;
+                if (rem < 8) { st = RR_E_TRUNC; break; }
+                if (EMIT) put_elem(out + n + 1, ld_u64(b + p), 0, RR_K_SCORE, 0);
+                n += 2;
+                p += 8;
+                rem -= 8;
+            }
+            if (st == RR_OK && rem != 0) st = RR_E_COUNT;
+            break;
+        }
+        default:
+            st = RR_E_TYPE;
+    }
+    if (st != RR_OK) { n = 0; pay = 0; }
+    r.status = st;
+    r.n = n;
+    r.payload = pay;
+    return r;
+}
+
+// Batch totals without a second launch: per-tile partials go to 16 shards (non-returning
+// atomics), the last tile id stores the byte total, and the last workgroup to finish (ticket
+// counter, agent release/acquire as in cdna_hip_programming.md §5 "In-launch split-K
+// reduction") folds the shards into *out.
+__device__ __forceinline__ void totals_add(uint64_t *scratch, uint32_t tile, uint64_t bad, uint64_t pay,
+                                           uint64_t nel, uint64_t bytes_total, bool is_last_tile,
+                                           uint32_t ntiles, rr_totals *out) {
+    // scratch[0] tile counter, [1] done counter, [2] bytes total, [8 + 4*s + k] shard s
+    if (lane_id() == 0) {
+        uint32_t s = tile & 15;
+        if (bad) atomicAdd((unsigned long long *)&scratch[8 + 4 * s + 0], (unsigned long long)bad);
+        if (pay) atomicAdd((unsigned long long *)&scratch[8 + 4 * s + 1], (unsigned long long)pay);
+        if (nel) atomicAdd((unsigned long long *)&scratch[8 + 4 * s + 2], (unsigned long long)nel);
+        if (is_last_tile) lb_store(&scratch[2], bytes_total);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        uint64_t done = atomicAdd((unsigned long long *)&scratch[1], 1ull);
+        if (done == ntiles - 1 && out) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            uint64_t b = 0, p = 0, e = 0;
+            for (int k = 0; k < 16; ++k) {
+                b += lb_load(&scratch[8 + 4 * k + 0]);
+                p += lb_load(&scratch[8 + 4 * k + 1]);
+                e += lb_load(&scratch[8 + 4 * k + 2]);
+            }
+            out->n_elems = e;
+            out->bytes = lb_load(&scratch[2]);
+            out->n_bad = b;
+            out->payload = p;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------- decode
+__global__ __launch_bounds__(WG) void decode_kernel(const uint8_t *__restrict__ blob,
+                                                    const uint64_t *__restrict__ offsets, uint64_t n,
+                                                    rr_value *__restrict__ values, rr_elem *__restrict__ elems,
+                                                    uint64_t elem_cap, uint8_t *__restrict__ arena,
+                                                    uint64_t *scratch, uint32_t ntiles, rr_totals *totals) {
+    const uint32_t lane = lane_id();
+    const uint32_t tile = next_tile(&scratch[0]);
+    if (tile >= ntiles) return;
+    uint64_t *state = scratch + RR_SCRATCH_HDR;
+    const uint64_t v0 = (uint64_t)tile * TILE;
+    const uint64_t v = v0 + lane;
+    const bool active = v < n;
+    uint64_t o_lo = 0, o_hi = 0;
+    if (active) {
+        o_lo = offsets[v];
+        o_hi = offsets[v + 1];
+    }
+    // tile byte range [B0, B1)
+    const uint64_t nv = (n - v0) < TILE ? (n - v0) : TILE;
+    const uint64_t B0 = __shfl(o_lo, 0, RR_WAVE);
+    const uint64_t B1 = offsets[v0 + nv];
+
+    // 1. mirror copy: aligned 16-byte chunks covering [B0, B1). Chunks shared with the
+    //    neighbouring tile receive identical bytes from both writers.
+    {
+        const uint64_t A0 = B0 & ~15ull, A1 = (B1 + 15) & ~15ull;
+        const u32x4 *src = reinterpret_cast<const u32x4 *>(blob);
+        u32x4 *dst = reinterpret_cast<u32x4 *>(arena);
+        uint64_t c = (A0 >> 4) + lane, ce = A1 >> 4;
+        for (; c + 3 * RR_WAVE < ce; c += 4 * RR_WAVE) {
+            u32x4 a = src[c];
+            u32x4 b = src[c + RR_WAVE];
+            u32x4 d = src[c + 2 * RR_WAVE];
+            u32x4 e = src[c + 3 * RR_WAVE];
+            __builtin_nontemporal_store(a, dst + c);
+            __builtin_nontemporal_store(b, dst + c + RR_WAVE);
+            __builtin_nontemporal_store(d, dst + c + 2 * RR_WAVE);
+            __builtin_nontemporal_store(e, dst + c + 3 * RR_WAVE);
+        }
+        for (; c < ce; c += RR_WAVE) __builtin_nontemporal_store(src[c], dst + c);
+    }
+
+    // 2. count pass
+    Parsed pr{RR_OK, 0, 0, 0};
+    if (active) pr = parse_value<false>(blob + o_lo, o_lo, o_hi - o_lo, nullptr);
+
+    // 3. scan + look-back
+    const uint64_t incl = wave_incl_scan(pr.n);
+    const uint64_t agg = __shfl(incl, RR_WAVE - 1, RR_WAVE);
+    const uint64_t prefix = lookback(state, tile, agg);
+    const uint64_t base = prefix + incl - pr.n;
+
+    // 4. emit
+    uint32_t status = pr.status;
+    uint64_t pay = 0;
+    if (active) {
+        if (status == RR_OK && base + pr.n > elem_cap) status = RR_E_CAPACITY;
+        if (status == RR_OK && pr.n) {
+            Parsed e = parse_value<true>(blob + o_lo, o_lo, o_hi - o_lo, elems + base);
+            pay = e.payload;
+        }
+        uint32_t type = o_hi > o_lo ? blob[o_lo] : 0;
+        uint32_t lru = (o_hi - o_lo >= 5) ? (ld_u32(blob + o_lo + 1) & RR_LRU_MASK) : 0;
+        uint4 w;
+        w.x = type | (pr.enc << 8) | (status << 16);
+        w.y = lru;
+        w.z = (uint32_t)pr.n;
+        w.w = (uint32_t)base;
+        reinterpret_cast<uint4 *>(values)[v] = w;
+    }
+    const uint64_t bad = wave_sum(active && status != RR_OK ? 1 : 0);
+    const uint64_t payt = wave_sum(pay);
+    totals_add(scratch, tile, bad, payt, agg, offsets[n], tile == ntiles - 1, ntiles, totals);
+}
+
+// ---------------------------------------------------------------------------------------- encode
+__device__ __forceinline__ bool fits_width(int64_t x, uint32_t w) {
+    if (w == 8) return true;
+    if (w == 4) return x >= INT32_MIN && x <= INT32_MAX;
+    return x >= INT16_MIN && x <= INT16_MAX;
+}
+
+struct ElemV {
+    uint64_t data;
+    uint32_t len;
+    uint32_t kind;
+};
+__device__ __forceinline__ ElemV get_elem(const rr_elem *e) {
+    uint4 w = *reinterpret_cast<const uint4 *>(e);
+    return ElemV{(uint64_t)w.x | ((uint64_t)w.y << 32), w.z, w.w & 0xFF};
+}
+
+// serObject rock_serdes.c:512-535: blob size of one flat value, 0 + status if unencodable.
+__device__ uint64_t encode_size(uint32_t type, uint32_t enc, uint64_t n, const rr_elem *el, uint32_t &st,
+                                uint64_t &pay) {
+    st = RR_OK;
+    pay = 0;
+    uint64_t s = 5;
+    switch (type) {
+        case RR_TYPE_STRING: {
+            if (n != 1) break;
+            ElemV e = get_elem(el);
+            if (enc == RR_ENC_INT) {
+                if (e.kind != RR_K_INT) break;
+                return 14;
+            }
+            if ((enc != RR_ENC_RAW && enc != RR_ENC_EMBSTR) || e.kind != RR_K_STR) break;
+            pay = e.len;
+            return 6 + (uint64_t)e.len;
+        }
+        case RR_TYPE_LIST_QUICKLIST: {
+            for (uint64_t i = 0; i < n; ++i) {
+                ElemV e = get_elem(el + i);
+                if (e.kind == RR_K_INT) s += 4 + dec_len((int64_t)e.data);
+                else if (e.kind == RR_K_STR) { s += 4 + (uint64_t)e.len; pay += e.len; }
+                else { st = RR_E_ENCODE; return 0; }
+            }
+            return s;
+        }
+        case RR_TYPE_SET_INTSET: {
+            if (enc != 2 && enc != 4 && enc != 8) break;
+            for (uint64_t i = 0; i < n; ++i) {
+                ElemV e = get_elem(el + i);
+                if (e.kind != RR_K_INT || !fits_width((int64_t)e.data, enc)) { st = RR_E_ENCODE; return 0; }
+            }
+            return 13 + (uint64_t)enc * n;
+        }
+        case RR_TYPE_SET_HT:
+        case RR_TYPE_HASH_HT: {
+            if (type == RR_TYPE_HASH_HT && (n & 1)) break;
+            s += 8;
+            for (uint64_t i = 0; i < n; ++i) {
+                ElemV e = get_elem(el + i);
+                if (e.kind != RR_K_STR) { st = RR_E_ENCODE; return 0; }
+                s += 8 + (uint64_t)e.len;
+                pay += e.len;
+            }
+            return s;
+        }
+        case RR_TYPE_HASH_ZIPLIST:
+        case RR_TYPE_ZSET_ZIPLIST: {
+            if (n < 1) break;
+            ElemV e = get_elem(el);
+            if (e.kind != RR_K_ZLRAW) break;
+            pay = e.len;
+            return 13 + (uint64_t)e.len;
+        }
+        case RR_TYPE_ZSET_SKIPLIST: {
+            if (n & 1) break;
+            s += 8;
+            for (uint64_t i = 0; i < n; i += 2) {
+                ElemV a = get_elem(el + i), b = get_elem(el + i + 1);
+                if (a.kind != RR_K_STR || b.kind != RR_K_SCORE) { st = RR_E_ENCODE; return 0; }
+                s += 16 + (uint64_t)a.len;
+                pay += a.len;
+            }
+            return s;
+        }
+        default:
+            break;
+    }
+    st = RR_E_ENCODE;
+    pay = 0;
+    return 0;
+}
+
+__device__ __forceinline__ void st_bytes(uint8_t *d, uint64_t v, uint32_t nb) {
+    for (uint32_t i = 0; i < nb; ++i) d[i] = (uint8_t)(v >> (8 * i));
+}
+
+constexpr uint32_t BULK = 32;        // payloads longer than this are copied by the whole wave
+constexpr uint32_t QCAP = 256;       // bulk-copy queue entries per wave
+
+struct BulkQ {
+    uint64_t dst[QCAP];
+    uint64_t src[QCAP];
+    uint32_t len[QCAP];
+};
+
+// Wave-cooperative byte copy arena[src..] -> blob[dst..]: aligned dword stores in the middle,
+// byte stores at the ends (neighbouring values own the bytes around the segment).
+__device__ __forceinline__ void wave_copy(uint8_t *__restrict__ dst, const uint8_t *__restrict__ src, uint64_t len) {
+    const uint32_t lane = lane_id();
+    uint64_t head = (4 - ((uintptr_t)dst & 3)) & 3;
+    if (head > len) head = len;
+    if (lane < head) dst[lane] = src[lane];
+    uint64_t body = (len - head) & ~3ull;
+    uint32_t *d4 = reinterpret_cast<uint32_t *>(dst + head);
+    const uint8_t *s4 = src + head;
+    for (uint64_t k = lane; k < (body >> 2); k += RR_WAVE) {
+        uint32_t w;
+        __builtin_memcpy(&w, s4 + 4 * k, 4);
+        d4[k] = w;
+    }
+    uint64_t tail = len - head - body;
+    if (lane < tail) dst[head + body + lane] = src[head + body + lane];
+}
+
+__global__ __launch_bounds__(WG) void encode_kernel(const rr_value *__restrict__ values,
+                                                    const rr_elem *__restrict__ elems,
+                                                    const uint8_t *__restrict__ arena, uint64_t n,
+                                                    uint8_t *__restrict__ out, uint64_t cap,
+                                                    uint64_t *__restrict__ offsets, uint64_t *scratch,
+                                                    uint32_t ntiles, rr_totals *totals) {
+    __shared__ BulkQ qs[WG / RR_WAVE];
+    __shared__ uint32_t qn[WG / RR_WAVE];
+    const uint32_t lane = lane_id();
+    BulkQ &q = qs[threadIdx.x / RR_WAVE];
+    const uint32_t tile = next_tile(&scratch[0]);
+    if (tile >= ntiles) return;
+    uint64_t *state = scratch + RR_SCRATCH_HDR;
+    const uint64_t v = (uint64_t)tile * TILE + lane;
+    const bool active = v < n;
+
+    uint32_t type = 0, enc = 0, lru = 0, st = RR_OK;
+    uint64_t ne = 0, eb = 0, size = 0, pay = 0;
+    if (active) {
+        uint4 w = reinterpret_cast<const uint4 *>(values)[v];
+        type = w.x & 0xFF;
+        enc = (w.x >> 8) & 0xFF;
+        lru = w.y & RR_LRU_MASK;
+        ne = w.z;
+        eb = w.w;
+        size = encode_size(type, enc, ne, elems + eb, st, pay);
+    }
+    const uint64_t incl = wave_incl_scan(size);
+    const uint64_t agg = __shfl(incl, RR_WAVE - 1, RR_WAVE);
+    const uint64_t prefix = lookback(state, tile, agg);
+    const uint64_t o = prefix + incl - size;
+    if (active) offsets[v] = o;
+    if (tile == ntiles - 1 && lane == 0) offsets[n] = prefix + agg;
+
+    bool ok = active && st == RR_OK && o + size <= cap;
+    if (lane == 0) qn[threadIdx.x / RR_WAVE] = 0;
+    __builtin_amdgcn_wave_barrier();
+    if (ok) {
+        uint8_t *d = out + o;
+        const rr_elem *el = elems + eb;
+        d[0] = (uint8_t)type;
+        st_bytes(d + 1, lru, 4);
+        uint64_t p = 5;
+        auto copy = [&](uint64_t dpos, uint64_t src, uint32_t len) {
+            if (len > BULK) {
+                uint32_t slot = atomicAdd(&qn[threadIdx.x / RR_WAVE], 1u);
+                if (slot < QCAP) { q.dst[slot] = o + dpos; q.src[slot] = src; q.len[slot] = len; return; }
+            }
+            for (uint32_t i = 0; i < len; ++i) d[dpos + i] = arena[src + i];
+        };
+        switch (type) {
+            case RR_TYPE_STRING: {
+                ElemV e = get_elem(el);
+                d[5] = (uint8_t)enc;
+                if (enc == RR_ENC_INT) st_bytes(d + 6, e.data, 8);
+                else copy(6, e.data, e.len);
+                break;
+            }
+            case RR_TYPE_LIST_QUICKLIST:
+                for (uint64_t i = 0; i < ne; ++i) {
+                    ElemV e = get_elem(el + i);
+                    if (e.kind == RR_K_INT) {
+                        uint32_t l = dec_write(d + p + 4, (int64_t)e.data);
+                        st_bytes(d + p, l, 4);
+                        p += 4 + l;
+                    } else {
+                        st_bytes(d + p, e.len, 4);
+                        copy(p + 4, e.data, e.len);
+                        p += 4 + (uint64_t)e.len;
+                    }
+                }
+                break;
+            case RR_TYPE_SET_INTSET:
+                st_bytes(d + p, enc, 4);
+                st_bytes(d + p + 4, ne, 4);
+                p += 8;
+                for (uint64_t i = 0; i < ne; ++i) {
+                    ElemV e = get_elem(el + i);
+                    st_bytes(d + p, e.data, enc);
+                    p += enc;
+                }
+                break;
+            case RR_TYPE_SET_HT:
+            case RR_TYPE_HASH_HT:
+                st_bytes(d + p, type == RR_TYPE_SET_HT ? ne : ne / 2, 8);
+                p += 8;
+                for (uint64_t i = 0; i < ne; ++i) {
+                    ElemV e = get_elem(el + i);
+                    st_bytes(d + p, e.len, 8);
+                    copy(p + 8, e.data, e.len);
+                    p += 8 + (uint64_t)e.len;
+                }
+                break;
+            case RR_TYPE_HASH_ZIPLIST:
+            case RR_TYPE_ZSET_ZIPLIST: {
+                ElemV e = get_elem(el);
+                st_bytes(d + p, e.len, 8);
+                copy(p + 8, e.data, e.len);
+                break;
+            }
+            case RR_TYPE_ZSET_SKIPLIST:
+                st_bytes(d + p, ne / 2, 8);
+                p += 8;
+                for (uint64_t i = 0; i < ne; i += 2) {
+                    ElemV a = get_elem(el + i), b = get_elem(el + i + 1);
+                    st_bytes(d + p, a.len, 8);
+                    copy(p + 8, a.data, a.len);
+                    p += 8 + (uint64_t)a.len;
+                    st_bytes(d + p, b.data, 8);
+                    p += 8;
+                }
+                break;
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    // bulk copies by the whole wave (queue overflow was copied lane-serially above)
+    uint32_t qcount = qn[threadIdx.x / RR_WAVE];
+    if (qcount > QCAP) qcount = QCAP;
+    for (uint32_t k = 0; k < qcount; ++k) wave_copy(out + q.dst[k], arena + q.src[k], q.len[k]);
+
+    const uint64_t bad = wave_sum(active && !ok ? 1 : 0);
+    const uint64_t payt = wave_sum(ok ? pay : 0);
+    const uint64_t nel = wave_sum(ne);
+    totals_add(scratch, tile, bad, payt, nel, prefix + agg, tile == ntiles - 1, ntiles, totals);
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------------- launch
+extern "C" hipError_t rr_launch_decode(const uint8_t *blob, const uint64_t *offsets, uint64_t n, rr_value *values,
+                                       rr_elem *elems, uint64_t elem_cap, uint8_t *arena, uint64_t *scratch,
+                                       rr_totals *totals, hipStream_t stream) {
+    uint32_t ntiles = (uint32_t)((n + TILE - 1) / TILE);
+    size_t zero = (RR_SCRATCH_HDR + (size_t)ntiles) * sizeof(uint64_t);
+    hipError_t e = hipMemsetAsync(scratch, 0, (zero + 15) & ~(size_t)15, stream);
+    if (e != hipSuccess) return e;
+    if (ntiles == 0) {
+        if (totals) {
+            e = hipMemsetAsync(totals, 0, sizeof(rr_totals), stream);
+        }
+        return e;
+    }
+    uint32_t waves_per_wg = WG / RR_WAVE;
+    uint32_t grid = (ntiles + waves_per_wg - 1) / waves_per_wg;
+    hipLaunchKernelGGL(decode_kernel, dim3(grid), dim3(WG), 0, stream, blob, offsets, n, values, elems, elem_cap,
+                       arena, scratch, ntiles, totals);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t rr_launch_encode(const rr_value *values, const rr_elem *elems, const uint8_t *arena,
+                                       uint64_t n, uint8_t *out, uint64_t cap, uint64_t *offsets, uint64_t *scratch,
+                                       rr_totals *totals, hipStream_t stream) {
+    uint32_t ntiles = (uint32_t)((n + TILE - 1) / TILE);
+    size_t zero = (RR_SCRATCH_HDR + (size_t)ntiles) * sizeof(uint64_t);
+    hipError_t e = hipMemsetAsync(scratch, 0, (zero + 15) & ~(size_t)15, stream);
+    if (e != hipSuccess) return e;
+    if (ntiles == 0) {
+        e = hipMemsetAsync(offsets, 0, sizeof(uint64_t), stream);
+        if (e == hipSuccess && totals) e = hipMemsetAsync(totals, 0, sizeof(rr_totals), stream);
+        return e;
+    }
+    uint32_t waves_per_wg = WG / RR_WAVE;
+    uint32_t grid = (ntiles + waves_per_wg - 1) / waves_per_wg;
+    hipLaunchKernelGGL(encode_kernel, dim3(grid), dim3(WG), 0, stream, values, elems, arena, n, out, cap, offsets,
+                       scratch, ntiles, totals);
+    return hipGetLastError();
+}
+
+extern "C" uint64_t rr_tile_values(void) { return TILE; }

@@ -1,0 +1,180 @@
+"""GPU parity tests: the HIP engine, called through the C-ABI, against the CPU oracle and the
+golden vectors.  Bit-exact everywhere (integer/byte work).  One process, one engine context."""
+import struct
+
+import numpy as np
+import pytest
+
+import redrock_old_amd as rr
+from oracle import cpu
+from oracle import pyoracle as po
+
+from helpers import assert_flat_equal, batch_from_blobs, expected_flat, golden
+
+pytestmark = pytest.mark.gpu
+G = golden()
+
+
+def reencoded(blob):
+    return blob[:1] + struct.pack("<I", struct.unpack_from("<I", blob, 1)[0] & 0xFFFFFF) + blob[5:]
+
+
+def test_golden_batch(engine):
+    fx = G["kats"] + G["edges"]
+    blobs = [bytes.fromhex(f["blob"]) for f in fx]
+    data, offs = batch_from_blobs(blobs)
+    v, e, a, t = engine.decode_host(data, offs)
+    assert_flat_equal((v, e), expected_flat(fx), "golden")
+    assert np.array_equal(a, data[:int(offs[-1])])
+    nbad = sum(1 for f in fx if f["value"].get("status", 0))
+    assert t["n_bad"] == nbad
+    ok = np.nonzero(v["status"] == 0)[0]
+    # encode the OK values only (bad values own no descriptors and are not encodable)
+    out, ooffs, t2 = engine.encode_host(v[ok], e, a)
+    assert t2["n_bad"] == 0
+    exp = b"".join(reencoded(blobs[i]) for i in ok)
+    assert bytes(out) == exp
+
+
+@pytest.mark.parametrize("cfg,n", [(1, 100000), (2, 100000), (3, 50000), (4, 100000), (10, 2400), (11, 400)])
+def test_config_parity(engine, cfg, n):
+    data, offs = rr.gen_batch(cfg, n)
+    v, e, a, t = engine.decode_host(data, offs)
+    ov, oe, oa, ot = cpu.decode(data, offs, nthreads=8)
+    assert_flat_equal((v, e), (ov, oe), f"config {cfg}")
+    assert np.array_equal(a, oa)
+    assert t == ot
+    out, ooffs, t2 = engine.encode_host(v, e, a)
+    assert np.array_equal(ooffs, offs)
+    assert np.array_equal(out, data[:int(offs[-1])])
+    assert t2["n_bad"] == 0 and t2["bytes"] == int(offs[-1]) and t2["n_elems"] == t["n_elems"]
+    assert t2["payload"] == t["payload"]
+
+
+@pytest.mark.parametrize("n", [1, 2, 63, 64, 65, 127, 128, 129, 4097])
+def test_ragged_batch_sizes(engine, n):
+    data, offs = rr.gen_batch(4, n, seed=1000 + n)
+    v, e, a, t = engine.decode_host(data, offs)
+    ov, oe, oa, ot = cpu.decode(data, offs)
+    assert_flat_equal((v, e), (ov, oe), f"n={n}")
+    out, ooffs, _ = engine.encode_host(v, e, a)
+    assert np.array_equal(out, data[:int(offs[-1])])
+
+
+def test_empty_batch(engine):
+    v, e, a, t = engine.decode_host(np.zeros(16, np.uint8), np.zeros(1, np.uint64))
+    assert len(v) == 0 and t["n_elems"] == 0 and t["n_bad"] == 0
+
+
+def test_decode_capacity(engine):
+    data, offs = rr.gen_batch(4, 3000)
+    cap = 5000
+    v, e, a, t = engine.decode_host(data, offs, elem_cap=cap)
+    ov, oe, oa, ot = cpu.decode(data, offs, elem_cap=cap)
+    assert t == ot and t["n_bad"] > 0
+    # descriptors are written only below the first value that did not fit
+    first = int(np.nonzero(ov["status"] == 11)[0][0])
+    w = int(ov["elem_base"][first])
+    assert_flat_equal((v, e[:w]), (ov, oe[:w]), "capacity")
+
+
+def test_encode_capacity(engine):
+    data, offs = rr.gen_batch(4, 3000)
+    v, e, a, t = engine.decode_host(data, offs)
+    cap = int(offs[1500])
+    out, ooffs, t2 = engine.encode_host(v, e, a, data_cap=cap)
+    assert np.array_equal(ooffs, offs)            # offsets are always complete
+    assert t2["bytes"] == int(offs[-1]) and t2["n_bad"] > 0
+    fits = int(np.searchsorted(offs[1:], cap, side="right"))
+    assert np.array_equal(out[:int(offs[fits])], data[:int(offs[fits])])
+
+
+def test_fuzzed_blobs_match_oracle(engine):
+    """Random byte flips / truncations of valid blobs: statuses and descriptors must match the
+    oracle value for value (no out-of-bounds reads: the kernel must survive every input)."""
+    rng = np.random.default_rng(7)
+    data, offs = rr.gen_batch(10, 480)
+    blobs = []
+    for i in range(len(offs) - 1):
+        b = bytearray(data[offs[i]:offs[i + 1]].tobytes())
+        for _ in range(4):
+            m = bytearray(b)
+            r = rng.integers(0, 4)
+            if r == 0 and len(m):
+                m[rng.integers(0, len(m))] ^= 1 << int(rng.integers(0, 8))
+            elif r == 1 and len(m):
+                m = m[:int(rng.integers(0, len(m)))]
+            elif r == 2 and len(m) > 6:
+                p = int(rng.integers(5, len(m)))
+                m[p] = int(rng.integers(0, 256))
+            blobs.append(bytes(m))
+    fdata, foffs = batch_from_blobs(blobs)
+    v, e, a, t = engine.decode_host(fdata, foffs)
+    ov, oe, oa, ot = cpu.decode(fdata, foffs)
+    assert_flat_equal((v, e), (ov, oe), "fuzz")
+    assert t == ot
+
+
+def test_device_api_matches_host_api(engine):
+    import torch
+    data, offs = rr.gen_batch(4, 20000)
+    n = len(offs) - 1
+    nb = int(offs[-1])
+    dev = torch.device("cuda:0")
+    d_data = torch.from_numpy(data).to(dev)
+    d_offs = torch.from_numpy(offs.view(np.int64)).to(dev)
+    cap = rr.elem_bound(n, nb)
+    d_vals = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
+    d_elems = torch.zeros(cap * 16, dtype=torch.uint8, device=dev)
+    d_arena = torch.zeros((nb + 15) & ~15, dtype=torch.uint8, device=dev)
+    d_tot = torch.zeros(4, dtype=torch.int64, device=dev)
+    s = torch.cuda.current_stream()
+    engine.decode_device(d_data, d_offs, d_vals, d_elems, d_arena, d_tot, stream=s)
+    torch.cuda.synchronize()
+    tot = d_tot.cpu().numpy().view(np.uint64)
+    v = d_vals.cpu().numpy().view(rr.VALUE_DT)
+    e = d_elems.cpu().numpy().view(rr.ELEM_DT)[:int(tot[0])]
+    hv, he, ha, ht = engine.decode_host(data, offs)
+    assert_flat_equal((v, e), (hv, he), "device api")
+    assert int(tot[0]) == ht["n_elems"] and int(tot[3]) == ht["payload"]
+    # device encode back into a second buffer
+    d_out = torch.zeros((nb + 15) & ~15, dtype=torch.uint8, device=dev)
+    d_ooffs = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    engine.encode_device(d_vals, d_elems, d_arena, d_out, d_ooffs, d_tot, stream=s)
+    torch.cuda.synchronize()
+    assert np.array_equal(d_ooffs.cpu().numpy().view(np.uint64), offs)
+    assert torch.equal(d_out[:nb], d_data[:nb])
+
+
+def test_full_size_mixed_roundtrip(engine):
+    """1M-value mixed batch (the headline size): size-independent properties on the GPU —
+    encode(decode(b)) == b byte for byte, zero bad values, descriptor count equals the oracle's,
+    per-type histogram of records matches the blobs' type bytes."""
+    import torch
+    data, offs = rr.gen_batch(4, 1_000_000)
+    n = len(offs) - 1
+    nb = int(offs[-1])
+    dev = torch.device("cuda:0")
+    d_data = torch.from_numpy(data).to(dev)
+    d_offs = torch.from_numpy(offs.view(np.int64)).to(dev)
+    cap = rr.elem_bound(n, nb)
+    d_vals = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
+    d_elems = torch.zeros(cap * 16, dtype=torch.uint8, device=dev)
+    d_arena = torch.zeros((nb + 15) & ~15, dtype=torch.uint8, device=dev)
+    d_tot = torch.zeros(4, dtype=torch.int64, device=dev)
+    engine.decode_device(d_data, d_offs, d_vals, d_elems, d_arena, d_tot)
+    torch.cuda.synchronize()
+    tot = d_tot.cpu().numpy().view(np.uint64)
+    assert int(tot[2]) == 0
+    ov, oe, _, ot = cpu.decode(data, offs, nthreads=8)
+    assert int(tot[0]) == ot["n_elems"] and int(tot[3]) == ot["payload"]
+    v = d_vals.cpu().numpy().view(rr.VALUE_DT)
+    assert np.array_equal(v, ov)
+    e = d_elems.cpu().numpy().view(rr.ELEM_DT)[:int(tot[0])]
+    assert np.array_equal(e, oe)
+    d_out = torch.zeros((nb + 15) & ~15, dtype=torch.uint8, device=dev)
+    d_ooffs = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    engine.encode_device(d_vals, d_elems, d_arena, d_out, d_ooffs, d_tot)
+    torch.cuda.synchronize()
+    assert torch.equal(d_out[:nb], d_data[:nb])
+    assert np.array_equal(d_ooffs.cpu().numpy().view(np.uint64), offs)
