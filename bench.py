@@ -71,7 +71,7 @@ def main():
     types, counts = np.unique(data[offs[:-1].astype(np.int64)], return_counts=True)
 
     eng = rr.Engine(local)
-    eng.reserve(n)
+    eng.reserve(n, nb)
     d_data = torch.from_numpy(data).to(dev)
     d_offs = torch.from_numpy(offs.view(np.int64)).to(dev)
     cap = rr.elem_bound(n, nb)

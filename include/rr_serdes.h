@@ -65,13 +65,15 @@ typedef struct rr_totals {
 /* ---- context ------------------------------------------------------------------------ */
 int  rr_ctx_create(int device, rr_ctx **out);
 void rr_ctx_destroy(rr_ctx *ctx);
-/* Make scratch space for batches up to n values (the device calls grow it on demand too,
- * but growing allocates; call this first when capturing graphs). */
-int  rr_ctx_reserve(rr_ctx *ctx, uint64_t n_values);
+/* Make scratch space for batches up to n_values values / n_bytes blob bytes (the device calls
+ * grow it on demand too, but growing allocates; call this first when capturing graphs). */
+int  rr_ctx_reserve(rr_ctx *ctx, uint64_t n_values, uint64_t n_bytes);
 const char *rr_last_error(void);
 
 /* ---- device-resident entry points (all pointers on ctx's device) -------------------- */
-/* Decode: needs out->n == in->n, out->arena_cap >= in->offsets[n] rounded up to 16,
+/* Decode: needs out->n == in->n; in->data_cap a multiple of 16 with
+ * offsets[n] <= data_cap (the work grid is sized from data_cap, so keep it tight) and
+ * in->data readable for data_cap bytes; out->arena_cap >= in->data_cap;
  * out->elem_cap >= number of descriptors (an upper bound is rr_decode_elem_bound()). */
 int rr_decode_batch(rr_ctx *ctx, const rr_blob_batch *in, rr_flat_batch *out,
                     rr_totals *d_totals, void *stream);

@@ -76,12 +76,18 @@ def lib():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise RRError(f"{LIB_PATH} not built: run __graft_entry__.build()")
+    # torch (used for device buffers and streams) ships its own libamdhip64.so.7; load it first
+    # so this library binds to the same HIP runtime instead of a second copy from /opt/rocm.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(LIB_PATH)
     vp, u64 = C.c_void_p, C.c_uint64
     L.rr_ctx_create.argtypes = [C.c_int, C.POINTER(vp)]
     L.rr_ctx_destroy.argtypes = [vp]
     L.rr_ctx_destroy.restype = None
-    L.rr_ctx_reserve.argtypes = [vp, u64]
+    L.rr_ctx_reserve.argtypes = [vp, u64, u64]
     L.rr_last_error.restype = C.c_char_p
     L.rr_decode_batch.argtypes = [vp, C.POINTER(BlobBatch), C.POINTER(FlatBatch), vp, vp]
     L.rr_encode_batch.argtypes = [vp, C.POINTER(FlatBatch), C.POINTER(BlobBatch), vp, vp]
@@ -148,8 +154,8 @@ class Engine:
         except Exception:
             pass
 
-    def reserve(self, n: int):
-        _check(self._L.rr_ctx_reserve(self._ctx, n))
+    def reserve(self, n: int, nbytes: int = 0):
+        _check(self._L.rr_ctx_reserve(self._ctx, n, nbytes))
 
     # ---- host entry points ------------------------------------------------------------
     def decode_host(self, data: np.ndarray, offsets: np.ndarray, elem_cap: int | None = None):

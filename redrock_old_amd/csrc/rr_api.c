@@ -16,7 +16,7 @@ struct rr_ctx {
     int device;
     hipStream_t stream;          /* used by the host entry points */
     uint64_t *scratch;           /* look-back words + counters */
-    uint64_t scratch_tiles;
+    uint64_t scratch_words;
     /* device staging for host entry points */
     void *d_in, *d_off, *d_vals, *d_elems, *d_arena, *d_out, *d_ooff;
     size_t c_in, c_off, c_vals, c_elems, c_arena, c_out, c_ooff;
@@ -72,17 +72,21 @@ void rr_ctx_destroy(rr_ctx *c) {
     free(c);
 }
 
-int rr_ctx_reserve(rr_ctx *c, uint64_t n_values) {
-    if (!c) return fail(RR_API_EINVAL, "ctx is NULL");
-    uint64_t tiles = (n_values + rr_tile_values() - 1) / rr_tile_values();
-    if (c->scratch && tiles <= c->scratch_tiles) return RR_API_OK;
+static int ensure_scratch(rr_ctx *c, uint64_t words) {
+    if (c->scratch && words <= c->scratch_words) return RR_API_OK;
     HIPCHK(hipSetDevice(c->device));
     if (c->scratch) { HIPCHK(hipDeviceSynchronize()); hipFree(c->scratch); c->scratch = NULL; }
-    uint64_t want = tiles + tiles / 4 + 64;
-    if (hipMalloc((void **)&c->scratch, (RR_SCRATCH_HDR + want) * sizeof(uint64_t)) != hipSuccess)
-        return fail(RR_API_ENOMEM, "hipMalloc scratch (%llu tiles)", (unsigned long long)want);
-    c->scratch_tiles = want;
+    uint64_t want = words + words / 4 + 64;
+    if (hipMalloc((void **)&c->scratch, want * sizeof(uint64_t)) != hipSuccess)
+        return fail(RR_API_ENOMEM, "hipMalloc scratch (%llu words)", (unsigned long long)want);
+    c->scratch_words = want;
     return RR_API_OK;
+}
+
+int rr_ctx_reserve(rr_ctx *c, uint64_t n_values, uint64_t n_bytes) {
+    if (!c) return fail(RR_API_EINVAL, "ctx is NULL");
+    uint64_t a = rr_encode_scratch_words(n_values), b = rr_decode_scratch_words((n_bytes + 15) & ~15ull);
+    return ensure_scratch(c, a > b ? a : b);
 }
 
 uint64_t rr_decode_elem_bound(uint64_t n, uint64_t bytes) {
@@ -100,10 +104,12 @@ int rr_decode_batch(rr_ctx *c, const rr_blob_batch *in, rr_flat_batch *out, rr_t
     if (in->n && (!in->data || !in->offsets || !out->values || !out->arena))
         return fail(RR_API_EINVAL, "NULL buffer");
     if (!aligned16(in->data) || !aligned16(out->arena)) return fail(RR_API_EINVAL, "data/arena not 16-byte aligned");
-    int rc = rr_ctx_reserve(c, in->n);
+    if (in->data_cap & 15) return fail(RR_API_EINVAL, "data_cap must be a multiple of 16");
+    if (out->arena_cap < in->data_cap) return fail(RR_API_EINVAL, "arena_cap < data_cap");
+    int rc = ensure_scratch(c, rr_decode_scratch_words(in->data_cap));
     if (rc) return rc;
     HIPCHK(rr_launch_decode(in->data, in->offsets, in->n, out->values, out->elems, out->elem_cap, out->arena,
-                            c->scratch, d_totals, (hipStream_t)stream));
+                            c->scratch, in->data_cap, d_totals, (hipStream_t)stream));
     return RR_API_OK;
 }
 
@@ -113,7 +119,7 @@ int rr_encode_batch(rr_ctx *c, const rr_flat_batch *in, rr_blob_batch *out, rr_t
     if (in->n >= (1ull << 37)) return fail(RR_API_EINVAL, "batch too large");
     if (!out->offsets) return fail(RR_API_EINVAL, "NULL offsets");
     if (in->n && (!in->values || !out->data)) return fail(RR_API_EINVAL, "NULL buffer");
-    int rc = rr_ctx_reserve(c, in->n);
+    int rc = ensure_scratch(c, rr_encode_scratch_words(in->n));
     if (rc) return rc;
     HIPCHK(rr_launch_encode(in->values, in->elems, in->arena, in->n, out->data, out->data_cap, out->offsets,
                             c->scratch, d_totals, (hipStream_t)stream));
@@ -138,15 +144,16 @@ int rr_decode_batch_host(rr_ctx *c, const uint8_t *data, const uint64_t *offsets
     if (!c || !offsets || (n && (!data || !values))) return fail(RR_API_EINVAL, "NULL argument");
     HIPCHK(hipSetDevice(c->device));
     uint64_t bytes = offsets[n];
-    size_t pbytes = (size_t)((bytes + 15) & ~15ull) + 16;
-    GROW(c->d_in, c->c_in, pbytes);
+    size_t pbytes = (size_t)((bytes + 15) & ~15ull);
+    GROW(c->d_in, c->c_in, pbytes + 16);
     GROW(c->d_off, c->c_off, (n + 1) * sizeof(uint64_t));
     GROW(c->d_vals, c->c_vals, (n ? n : 1) * sizeof(rr_value));
     GROW(c->d_elems, c->c_elems, (elem_cap ? elem_cap : 1) * sizeof(rr_elem));
-    GROW(c->d_arena, c->c_arena, pbytes);
-    HIPCHK(hipMemsetAsync(c->d_in, 0, pbytes, c->stream));
+    GROW(c->d_arena, c->c_arena, pbytes + 16);
+    HIPCHK(hipMemsetAsync(c->d_in, 0, pbytes + 16, c->stream));
     if (bytes) HIPCHK(hipMemcpyAsync(c->d_in, data, bytes, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(c->d_off, offsets, (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemsetAsync(c->d_arena, 0, pbytes ? pbytes : 16, c->stream));
     rr_blob_batch in = {(uint8_t *)c->d_in, (uint64_t *)c->d_off, n, pbytes};
     rr_flat_batch out = {(rr_value *)c->d_vals, (rr_elem *)c->d_elems, (uint8_t *)c->d_arena, n, elem_cap, pbytes};
     int rc = rr_decode_batch(c, &in, &out, c->d_totals, c->stream);

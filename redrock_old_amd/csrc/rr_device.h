@@ -13,20 +13,26 @@ namespace rr {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ uint32_t ld_u8(const uint8_t *p) { return *p; }
-__device__ __forceinline__ uint32_t ld_u32(const uint8_t *p) {
-    uint32_t v;
-    __builtin_memcpy(&v, p, 4);
-    return v;
+// Byte-composed little-endian loads.  Templated on the pointer type so the same parser runs
+// on LDS-staged bytes (address_space(3): ds_read_u8, ~100-cycle latency) and on global memory
+// (fallback for windows whose values do not fit the stage).  The byte loads of one field are
+// independent, so a field costs one memory latency, not four.
+typedef const __attribute__((address_space(3))) uint8_t *lds_cptr;
+
+template <typename P>
+__device__ __forceinline__ uint32_t ld_u8(P p) { return p[0]; }
+template <typename P>
+__device__ __forceinline__ uint32_t ld_u16(P p) { return (uint32_t)p[0] | ((uint32_t)p[1] << 8); }
+template <typename P>
+__device__ __forceinline__ uint32_t ld_u32(P p) {
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
 }
-__device__ __forceinline__ uint64_t ld_u64(const uint8_t *p) {
-    uint64_t v;
-    __builtin_memcpy(&v, p, 8);
-    return v;
-}
+template <typename P>
+__device__ __forceinline__ uint64_t ld_u64(P p) { return (uint64_t)ld_u32(p) | ((uint64_t)ld_u32(p + 4) << 32); }
 
 // util.c:360-424 string2ll, restricted by zipTryEncoding (ziplist.c:480): 1 <= len < 32.
-__device__ __forceinline__ bool zip_try_int(const uint8_t *s, uint32_t len, int64_t &out) {
+template <typename P>
+__device__ __forceinline__ bool zip_try_int(P s, uint32_t len, int64_t &out) {
     if (len == 0 || len >= 32) return false;
     uint32_t c0 = ld_u8(s);
     if (len == 1 && c0 == '0') { out = 0; return true; }

@@ -9,7 +9,8 @@
 #include "../../include/rr_serdes.h"
 
 /* scratch layout (uint64 words): [0] tile counter, [1] done counter, [2] byte total,
- * [8 .. 8+64) 16 shards x {bad, payload, elems, -}, then one look-back word per tile. */
+ * [8 .. 8+64) 16 shards x {bad, payload, elems, -}, then one look-back word per tile
+ * (decode: per byte window, followed by the u32 first-value table of the windows). */
 #define RR_SCRATCH_HDR 72
 
 #ifdef __cplusplus
@@ -18,11 +19,12 @@ extern "C" {
 
 hipError_t rr_launch_decode(const uint8_t *blob, const uint64_t *offsets, uint64_t n, rr_value *values,
                             rr_elem *elems, uint64_t elem_cap, uint8_t *arena, uint64_t *scratch,
-                            rr_totals *totals, hipStream_t stream);
+                            uint64_t data_cap, rr_totals *totals, hipStream_t stream);
 hipError_t rr_launch_encode(const rr_value *values, const rr_elem *elems, const uint8_t *arena, uint64_t n,
                             uint8_t *out, uint64_t cap, uint64_t *offsets, uint64_t *scratch,
                             rr_totals *totals, hipStream_t stream);
-uint64_t rr_tile_values(void);
+uint64_t rr_decode_scratch_words(uint64_t data_cap);
+uint64_t rr_encode_scratch_words(uint64_t n);
 
 #ifdef __cplusplus
 }

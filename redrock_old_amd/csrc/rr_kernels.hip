@@ -44,8 +44,8 @@ __device__ __forceinline__ void put_elem(rr_elem *e, uint64_t data, uint32_t len
 
 // ziplist walk, ziplist.c:300-447; bounds checked.  zl points at the ziplist (L bytes),
 // zoff is its offset in the batch (arena offsets of string entries = zoff + position).
-template <bool EMIT>
-__device__ uint32_t parse_ziplist(const uint8_t *zl, uint64_t L, uint64_t zoff, rr_elem *out, uint64_t &count) {
+template <bool EMIT, typename P>
+__device__ __forceinline__ uint32_t parse_ziplist(P zl, uint64_t L, uint64_t zoff, rr_elem *out, uint64_t &count) {
     count = 0;
     if (L < 11 || ld_u32(zl) != L) return RR_E_ZL_CORRUPT;
     uint32_t zltail = ld_u32(zl + 4);
@@ -102,7 +102,7 @@ __device__ uint32_t parse_ziplist(const uint8_t *zl, uint64_t L, uint64_t zoff, 
             if (end > L - 1) return RR_E_ZL_CORRUPT;
             if (EMIT) {
                 int64_t v;
-                const uint8_t *x = zl + d;
+                P x = zl + d;
                 if (isz == 0) v = (int64_t)(enc & 0x0F) - 1;
                 else if (isz == 1) v = (int8_t)ld_u8(x);
                 else if (isz == 2) v = (int16_t)(ld_u8(x) | (ld_u8(x + 1) << 8));
@@ -125,8 +125,8 @@ __device__ uint32_t parse_ziplist(const uint8_t *zl, uint64_t L, uint64_t zoff, 
 }
 
 // desObject rock_serdes.c:538-564 and des* :133-508, on one blob at b (batch offset off).
-template <bool EMIT>
-__device__ Parsed parse_value(const uint8_t *b, uint64_t off, uint64_t len, rr_elem *out) {
+template <bool EMIT, typename P>
+__device__ __forceinline__ Parsed parse_value(P b, uint64_t off, uint64_t len, rr_elem *out) {
     Parsed r{RR_OK, 0, 0, 0};
     uint64_t n = 0, pay = 0;
     if (len < 5) { r.status = RR_E_SHORT; return r; }
@@ -178,8 +178,8 @@ __device__ Parsed parse_value(const uint8_t *b, uint64_t off, uint64_t len, rr_e
             r.enc = (uint32_t)w;
             if (EMIT) {
                 for (uint64_t i = 0; i < cnt; ++i) {
-                    const uint8_t *q = b + p + i * w;
-                    int64_t x = w == 2 ? (int64_t)(int16_t)(ld_u8(q) | (ld_u8(q + 1) << 8))
+                    P q = b + p + i * w;
+                    int64_t x = w == 2 ? (int64_t)(int16_t)ld_u16(q)
                               : w == 4 ? (int64_t)(int32_t)ld_u32(q) : (int64_t)ld_u64(q);
                     put_elem(out + i, (uint64_t)x, 0, RR_K_INT, 0);
                 }
@@ -220,7 +220,7 @@ __device__ Parsed parse_value(const uint8_t *b, uint64_t off, uint64_t len, rr_e
             rem -= 8;
             if (rem != L) { st = RR_E_ZL_LEN; break; }
             uint64_t cnt;
-            st = parse_ziplist<EMIT>(b + p, L, off + p, out + 1, cnt);
+            st = parse_ziplist<EMIT, P>(b + p, L, off + p, out + 1, cnt);
             if (st == RR_OK && (cnt & 1)) st = RR_E_ZL_CORRUPT;
             if (st != RR_OK) break;
             if (EMIT) put_elem(out, off + p, (uint32_t)L, RR_K_ZLRAW, 0);
@@ -262,114 +262,213 @@ __device__ Parsed parse_value(const uint8_t *b, uint64_t off, uint64_t len, rr_e
     return r;
 }
 
-// Batch totals without a second launch: per-tile partials go to 16 shards (non-returning
-// atomics), the last tile id stores the byte total, and the last workgroup to finish (ticket
-// counter, agent release/acquire as in cdna_hip_programming.md §5 "In-launch split-K
-// reduction") folds the shards into *out.
-__device__ __forceinline__ void totals_add(uint64_t *scratch, uint32_t tile, uint64_t bad, uint64_t pay,
-                                           uint64_t nel, uint64_t bytes_total, bool is_last_tile,
-                                           uint32_t ntiles, rr_totals *out) {
-    // scratch[0] tile counter, [1] done counter, [2] bytes total, [8 + 4*s + k] shard s
+// Batch totals: every tile stores its partials {bad, payload, count} with plain stores into
+// its own slot; a one-workgroup finalize kernel folds them after the main launch.  (A single
+// returning atomic per tile on one word serialises at ~88/us — measured 2.8 ms at 121K tiles.)
+__device__ __forceinline__ void tile_stats(uint64_t *stats, uint32_t tile, uint64_t bad, uint64_t pay, uint64_t cnt) {
     if (lane_id() == 0) {
-        uint32_t s = tile & 15;
-        if (bad) atomicAdd((unsigned long long *)&scratch[8 + 4 * s + 0], (unsigned long long)bad);
-        if (pay) atomicAdd((unsigned long long *)&scratch[8 + 4 * s + 1], (unsigned long long)pay);
-        if (nel) atomicAdd((unsigned long long *)&scratch[8 + 4 * s + 2], (unsigned long long)nel);
-        if (is_last_tile) lb_store(&scratch[2], bytes_total);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        uint64_t done = atomicAdd((unsigned long long *)&scratch[1], 1ull);
-        if (done == ntiles - 1 && out) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            uint64_t b = 0, p = 0, e = 0;
-            for (int k = 0; k < 16; ++k) {
-                b += lb_load(&scratch[8 + 4 * k + 0]);
-                p += lb_load(&scratch[8 + 4 * k + 1]);
-                e += lb_load(&scratch[8 + 4 * k + 2]);
-            }
-            out->n_elems = e;
-            out->bytes = lb_load(&scratch[2]);
-            out->n_bad = b;
-            out->payload = p;
-        }
+        stats[3 * (uint64_t)tile + 0] = bad;
+        stats[3 * (uint64_t)tile + 1] = pay;
+        stats[3 * (uint64_t)tile + 2] = cnt;
+    }
+}
+
+// mode 0 (decode): bytes = offsets[n], n_elems = sum of counts.
+// mode 1 (encode): bytes = inclusive prefix of the last tile (total blob bytes).
+__global__ __launch_bounds__(1024) void finalize_kernel(const uint64_t *__restrict__ stats, uint64_t *state,
+                                                        uint32_t ntiles, const uint64_t *__restrict__ offsets,
+                                                        uint64_t n, int mode, rr_totals *out) {
+    __shared__ uint64_t red[3][16];
+    uint64_t b = 0, p = 0, c = 0;
+    for (uint32_t t = threadIdx.x; t < ntiles; t += blockDim.x) {
+        b += stats[3 * (uint64_t)t + 0];
+        p += stats[3 * (uint64_t)t + 1];
+        c += stats[3 * (uint64_t)t + 2];
+    }
+    b = wave_sum(b);
+    p = wave_sum(p);
+    c = wave_sum(c);
+    const uint32_t w = threadIdx.x / RR_WAVE;
+    if (lane_id() == 0) { red[0][w] = b; red[1][w] = p; red[2][w] = c; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t tb = 0, tp = 0, tc = 0;
+        for (uint32_t k = 0; k < blockDim.x / RR_WAVE; ++k) { tb += red[0][k]; tp += red[1][k]; tc += red[2][k]; }
+        out->n_bad = tb;
+        out->payload = tp;
+        out->n_elems = tc;
+        out->bytes = mode == 0 ? offsets[n] : (ntiles ? (lb_load(&state[ntiles - 1]) & LB_VAL) : 0);
     }
 }
 
 // ---------------------------------------------------------------------------------------- decode
-__global__ __launch_bounds__(WG) void decode_kernel(const uint8_t *__restrict__ blob,
-                                                    const uint64_t *__restrict__ offsets, uint64_t n,
-                                                    rr_value *__restrict__ values, rr_elem *__restrict__ elems,
-                                                    uint64_t elem_cap, uint8_t *__restrict__ arena,
-                                                    uint64_t *scratch, uint32_t ntiles, rr_totals *totals) {
-    const uint32_t lane = lane_id();
-    const uint32_t tile = next_tile(&scratch[0]);
-    if (tile >= ntiles) return;
-    uint64_t *state = scratch + RR_SCRATCH_HDR;
-    const uint64_t v0 = (uint64_t)tile * TILE;
-    const uint64_t v = v0 + lane;
-    const bool active = v < n;
-    uint64_t o_lo = 0, o_hi = 0;
-    if (active) {
-        o_lo = offsets[v];
-        o_hi = offsets[v + 1];
-    }
-    // tile byte range [B0, B1)
-    const uint64_t nv = (n - v0) < TILE ? (n - v0) : TILE;
-    const uint64_t B0 = __shfl(o_lo, 0, RR_WAVE);
-    const uint64_t B1 = offsets[v0 + nv];
+// The blob buffer is cut into fixed byte WINDOWS of WIN bytes; window t owns the values whose
+// first byte lies in [t*WIN, (t+1)*WIN) (plan_kernel finds them: first_val[t]).  One wave per
+// window:
+//   1. streams the window's bytes into the mirror arena (aligned dwordx4 loads/stores — the
+//      copy is balanced by bytes whatever the value sizes), and stages the bytes of its values
+//      (window + the tail of the last value, up to STAGE bytes) into LDS from the same loads;
+//   2. lane = value, chunks of 64: validates/counts every value from LDS (count pass);
+//   3. wave scan + decoupled look-back over windows -> elem_base of every value;
+//   4. re-parses from LDS and writes descriptors + value records.
+// Windows whose values do not fit the stage parse from global memory (L2-hot) instead.
 
-    // 1. mirror copy: aligned 16-byte chunks covering [B0, B1). Chunks shared with the
-    //    neighbouring tile receive identical bytes from both writers.
+__global__ __launch_bounds__(256) void plan_kernel(const uint64_t *__restrict__ offsets, uint64_t n,
+                                                   uint32_t *__restrict__ first_val, uint32_t nwin, uint32_t win) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i > n) return;
+    uint64_t w_lo = i == 0 ? 0 : offsets[i - 1] / win + 1;
+    uint64_t w_hi = offsets[i] / win;
+    if (i == n) w_hi = nwin;   // windows past the last value start, and the sentinel
+    for (uint64_t w = w_lo; w <= w_hi && w <= nwin; ++w) first_val[w] = (uint32_t)i;
+}
+
+template <bool EMIT, typename P>
+__device__ __forceinline__ Parsed parse_at(P base, uint64_t sbase, uint64_t o_lo, uint64_t o_hi, rr_elem *out) {
+    return parse_value<EMIT, P>(base + (uint32_t)(o_lo - sbase), o_lo, o_hi - o_lo, out);
+}
+
+template <typename P>
+__device__ __forceinline__ void decode_values(P base, uint64_t sbase, const uint64_t *__restrict__ offsets,
+                                              uint64_t v_lo, uint64_t v_hi, rr_value *__restrict__ values,
+                                              rr_elem *__restrict__ elems, uint64_t elem_cap, uint64_t *state,
+                                              uint32_t tile, uint64_t &bad_out, uint64_t &pay_out,
+                                              uint64_t &agg_out) {
+    const uint32_t lane = lane_id();
+    const uint64_t nv = v_hi - v_lo;
+    // count pass
+    uint64_t agg = 0, cnt0 = 0;
+    Parsed pr0{RR_OK, 0, 0, 0};
+    uint64_t o_lo0 = 0, o_hi0 = 0;
+    for (uint64_t c = 0; c < nv; c += RR_WAVE) {
+        uint64_t v = v_lo + c + lane;
+        Parsed pr{RR_OK, 0, 0, 0};
+        uint64_t o_lo = 0, o_hi = 0;
+        if (v < v_hi) {
+            o_lo = offsets[v];
+            o_hi = offsets[v + 1];
+            pr = parse_at<false, P>(base, sbase, o_lo, o_hi, nullptr);
+        }
+        if (c == 0) { pr0 = pr; o_lo0 = o_lo; o_hi0 = o_hi; cnt0 = pr.n; }
+        agg += wave_sum(pr.n);
+    }
+    const uint64_t prefix = lookback(state, tile, agg);
+    agg_out = agg;
+    // emit pass
+    uint64_t run = prefix, bad = 0, pay = 0;
+    for (uint64_t c = 0; c < nv; c += RR_WAVE) {
+        uint64_t v = v_lo + c + lane;
+        bool active = v < v_hi;
+        Parsed pr;
+        uint64_t o_lo, o_hi;
+        if (c == 0) { pr = pr0; o_lo = o_lo0; o_hi = o_hi0; }
+        else {
+            pr = Parsed{RR_OK, 0, 0, 0};
+            o_lo = o_hi = 0;
+            if (active) {
+                o_lo = offsets[v];
+                o_hi = offsets[v + 1];
+                pr = parse_at<false, P>(base, sbase, o_lo, o_hi, nullptr);
+            }
+        }
+        (void)cnt0;
+        const uint64_t incl = wave_incl_scan(pr.n);
+        const uint64_t elem_base = run + incl - pr.n;
+        run += __shfl(incl, RR_WAVE - 1, RR_WAVE);
+        if (active) {
+            uint32_t status = pr.status;
+            if (status == RR_OK && elem_base + pr.n > elem_cap) status = RR_E_CAPACITY;
+            if (status == RR_OK && pr.n) {
+                Parsed e = parse_at<true, P>(base, sbase, o_lo, o_hi, elems + elem_base);
+                pay += e.payload;
+            }
+            P b = base + (uint32_t)(o_lo - sbase);
+            uint32_t len = (uint32_t)(o_hi - o_lo);
+            uint32_t type = len ? ld_u8(b) : 0;
+            uint32_t lru = len >= 5 ? (ld_u32(b + 1) & RR_LRU_MASK) : 0;
+            uint4 w;
+            w.x = type | (pr.enc << 8) | (status << 16);
+            w.y = lru;
+            w.z = (uint32_t)pr.n;
+            w.w = (uint32_t)elem_base;
+            reinterpret_cast<uint4 *>(values)[v] = w;
+            bad += status != RR_OK ? 1 : 0;
+        }
+    }
+    bad_out = wave_sum(bad);
+    pay_out = wave_sum(pay);
+}
+
+template <uint32_t WIN, uint32_t STAGE>
+__global__ __launch_bounds__(RR_WAVE) void decode_kernel(const uint8_t *__restrict__ blob,
+                                                         const uint64_t *__restrict__ offsets, uint64_t n,
+                                                         const uint32_t *__restrict__ first_val, uint32_t nwin,
+                                                         rr_value *__restrict__ values, rr_elem *__restrict__ elems,
+                                                         uint64_t elem_cap, uint8_t *__restrict__ arena,
+                                                         uint64_t *scratch) {
+    __shared__ __attribute__((aligned(16))) uint8_t stage[STAGE];
+    const uint32_t lane = lane_id();
+    uint64_t *state = scratch + RR_SCRATCH_HDR;
+    uint64_t *stats = state + nwin;
+    const uint64_t nbytes = offsets[n];
+    // persistent: static round-robin over windows; every wave only ever waits on lower windows
+    // held by co-resident waves (grid <= resident capacity), so the look-back cannot deadlock.
+    for (uint32_t tile = blockIdx.x; tile < nwin; tile += gridDim.x) {
+    const uint64_t v_lo = first_val[tile], v_hi = first_val[tile + 1];
+    const uint64_t W0 = (uint64_t)tile * WIN;
+    const uint64_t padded = (nbytes + 15) & ~15ull;
+    const uint64_t W1 = W0 + WIN < padded ? W0 + WIN : padded;
+    uint64_t S0 = W0, S1 = W0;
+    if (v_hi > v_lo) {
+        S0 = offsets[v_lo];
+        S1 = offsets[v_hi];
+    }
+    const uint64_t sbase = S0 & ~15ull;
+    const uint64_t send = (S1 + 15) & ~15ull;
+    const bool staged = send - sbase <= STAGE;
+    const uint64_t L1 = staged && send > W1 ? send : W1;
+
+    // 1. copy window -> arena, stage value bytes -> LDS (one load feeds both)
     {
-        const uint64_t A0 = B0 & ~15ull, A1 = (B1 + 15) & ~15ull;
         const u32x4 *src = reinterpret_cast<const u32x4 *>(blob);
         u32x4 *dst = reinterpret_cast<u32x4 *>(arena);
-        uint64_t c = (A0 >> 4) + lane, ce = A1 >> 4;
+        u32x4 *lds = reinterpret_cast<u32x4 *>(stage);
+        const uint64_t cw1 = W1 >> 4, cs0 = sbase >> 4;
+        uint64_t c = (W0 >> 4) + lane;
+        const uint64_t ce = L1 >> 4;
         for (; c + 3 * RR_WAVE < ce; c += 4 * RR_WAVE) {
-            u32x4 a = src[c];
-            u32x4 b = src[c + RR_WAVE];
-            u32x4 d = src[c + 2 * RR_WAVE];
-            u32x4 e = src[c + 3 * RR_WAVE];
-            __builtin_nontemporal_store(a, dst + c);
-            __builtin_nontemporal_store(b, dst + c + RR_WAVE);
-            __builtin_nontemporal_store(d, dst + c + 2 * RR_WAVE);
-            __builtin_nontemporal_store(e, dst + c + 3 * RR_WAVE);
+            u32x4 x[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) x[k] = src[c + k * RR_WAVE];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                uint64_t cc = c + k * RR_WAVE;
+                if (cc < cw1) __builtin_nontemporal_store(x[k], dst + cc);
+                if (staged && cc >= cs0) lds[cc - cs0] = x[k];
+            }
         }
-        for (; c < ce; c += RR_WAVE) __builtin_nontemporal_store(src[c], dst + c);
-    }
-
-    // 2. count pass
-    Parsed pr{RR_OK, 0, 0, 0};
-    if (active) pr = parse_value<false>(blob + o_lo, o_lo, o_hi - o_lo, nullptr);
-
-    // 3. scan + look-back
-    const uint64_t incl = wave_incl_scan(pr.n);
-    const uint64_t agg = __shfl(incl, RR_WAVE - 1, RR_WAVE);
-    const uint64_t prefix = lookback(state, tile, agg);
-    const uint64_t base = prefix + incl - pr.n;
-
-    // 4. emit
-    uint32_t status = pr.status;
-    uint64_t pay = 0;
-    if (active) {
-        if (status == RR_OK && base + pr.n > elem_cap) status = RR_E_CAPACITY;
-        if (status == RR_OK && pr.n) {
-            Parsed e = parse_value<true>(blob + o_lo, o_lo, o_hi - o_lo, elems + base);
-            pay = e.payload;
+        for (; c < ce; c += RR_WAVE) {
+            u32x4 x = src[c];
+            if (c < cw1) __builtin_nontemporal_store(x, dst + c);
+            if (staged && c >= cs0) lds[c - cs0] = x;
         }
-        uint32_t type = o_hi > o_lo ? blob[o_lo] : 0;
-        uint32_t lru = (o_hi - o_lo >= 5) ? (ld_u32(blob + o_lo + 1) & RR_LRU_MASK) : 0;
-        uint4 w;
-        w.x = type | (pr.enc << 8) | (status << 16);
-        w.y = lru;
-        w.z = (uint32_t)pr.n;
-        w.w = (uint32_t)base;
-        reinterpret_cast<uint4 *>(values)[v] = w;
     }
-    const uint64_t bad = wave_sum(active && status != RR_OK ? 1 : 0);
-    const uint64_t payt = wave_sum(pay);
-    totals_add(scratch, tile, bad, payt, agg, offsets[n], tile == ntiles - 1, ntiles, totals);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+
+    uint64_t bad, pay, agg;
+    if (staged)
+        decode_values<lds_cptr>((lds_cptr)stage, sbase, offsets, v_lo, v_hi, values, elems, elem_cap, state, tile,
+                                bad, pay, agg);
+    else
+        decode_values<const uint8_t *>(blob, 0, offsets, v_lo, v_hi, values, elems, elem_cap, state, tile, bad,
+                                       pay, agg);
+    tile_stats(stats, tile, bad, pay, agg);
+    // the stage is rewritten by the next window: all lanes' LDS reads must be done
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    }
 }
 
 // ---------------------------------------------------------------------------------------- encode
@@ -500,14 +599,15 @@ __global__ __launch_bounds__(WG) void encode_kernel(const rr_value *__restrict__
                                                     const uint8_t *__restrict__ arena, uint64_t n,
                                                     uint8_t *__restrict__ out, uint64_t cap,
                                                     uint64_t *__restrict__ offsets, uint64_t *scratch,
-                                                    uint32_t ntiles, rr_totals *totals) {
+                                                    uint32_t ntiles) {
     __shared__ BulkQ qs[WG / RR_WAVE];
     __shared__ uint32_t qn[WG / RR_WAVE];
     const uint32_t lane = lane_id();
     BulkQ &q = qs[threadIdx.x / RR_WAVE];
-    const uint32_t tile = next_tile(&scratch[0]);
-    if (tile >= ntiles) return;
     uint64_t *state = scratch + RR_SCRATCH_HDR;
+    uint64_t *stats = state + ntiles;
+    const uint32_t nwaves = gridDim.x * (WG / RR_WAVE);
+    for (uint32_t tile = blockIdx.x * (WG / RR_WAVE) + threadIdx.x / RR_WAVE; tile < ntiles; tile += nwaves) {
     const uint64_t v = (uint64_t)tile * TILE + lane;
     const bool active = v < n;
 
@@ -619,36 +719,69 @@ __global__ __launch_bounds__(WG) void encode_kernel(const rr_value *__restrict__
     const uint64_t bad = wave_sum(active && !ok ? 1 : 0);
     const uint64_t payt = wave_sum(ok ? pay : 0);
     const uint64_t nel = wave_sum(ne);
-    totals_add(scratch, tile, bad, payt, nel, prefix + agg, tile == ntiles - 1, ntiles, totals);
+    tile_stats(stats, tile, bad, payt, nel);
+    }
 }
 
 }  // namespace
 
 // ---------------------------------------------------------------------------------------- launch
+constexpr uint32_t DEC_WIN = 4096;
+constexpr uint32_t DEC_STAGE = 8192;
+
+// Resident workgroup count for a persistent launch: occupancy query minus one block per CU
+// (the API over-reports by one for SGPR-heavy kernels, MI355X_MICROARCH.md §Residency).
+template <typename K>
+static uint32_t resident_grid(K kernel, int block) {
+    int dev = 0, cus = 0, occ = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kernel, block, 0) != hipSuccess || occ < 1) occ = 1;
+    if (occ > 1) occ -= 1;
+    if (cus < 1) cus = 1;
+    return (uint32_t)(cus * occ);
+}
+
+extern "C" uint64_t rr_decode_windows(uint64_t data_cap) { return data_cap / DEC_WIN + 1; }
+
+// Scratch words a decode of a data_cap-byte buffer needs: header, one look-back word and
+// three stats words per window, first_val (u32) for every window + sentinel.
+extern "C" uint64_t rr_decode_scratch_words(uint64_t data_cap) {
+    uint64_t nwin = rr_decode_windows(data_cap);
+    return RR_SCRATCH_HDR + 4 * nwin + (nwin + 2) / 2 + 1;
+}
+
+extern "C" uint64_t rr_encode_scratch_words(uint64_t n) { return RR_SCRATCH_HDR + 4 * ((n + TILE - 1) / TILE) + 1; }
+
 extern "C" hipError_t rr_launch_decode(const uint8_t *blob, const uint64_t *offsets, uint64_t n, rr_value *values,
                                        rr_elem *elems, uint64_t elem_cap, uint8_t *arena, uint64_t *scratch,
-                                       rr_totals *totals, hipStream_t stream) {
-    uint32_t ntiles = (uint32_t)((n + TILE - 1) / TILE);
-    size_t zero = (RR_SCRATCH_HDR + (size_t)ntiles) * sizeof(uint64_t);
+                                       uint64_t data_cap, rr_totals *totals, hipStream_t stream) {
+    // The window grid is sized from data_cap (>= offsets[n], host-known without a sync);
+    // windows past offsets[n] find no values and copy nothing.
+    const uint32_t nwin = (uint32_t)rr_decode_windows(data_cap);
+    uint64_t *state = scratch + RR_SCRATCH_HDR;
+    uint32_t *first_val = reinterpret_cast<uint32_t *>(state + 4 * (uint64_t)nwin);
+    size_t zero = (RR_SCRATCH_HDR + (size_t)nwin) * sizeof(uint64_t);
     hipError_t e = hipMemsetAsync(scratch, 0, (zero + 15) & ~(size_t)15, stream);
     if (e != hipSuccess) return e;
-    if (ntiles == 0) {
-        if (totals) {
-            e = hipMemsetAsync(totals, 0, sizeof(rr_totals), stream);
-        }
-        return e;
-    }
-    uint32_t waves_per_wg = WG / RR_WAVE;
-    uint32_t grid = (ntiles + waves_per_wg - 1) / waves_per_wg;
-    hipLaunchKernelGGL(decode_kernel, dim3(grid), dim3(WG), 0, stream, blob, offsets, n, values, elems, elem_cap,
-                       arena, scratch, ntiles, totals);
+    hipLaunchKernelGGL(plan_kernel, dim3((uint32_t)((n + 1 + 255) / 256)), dim3(256), 0, stream, offsets, n, first_val,
+                       nwin, DEC_WIN);
+    static uint32_t grid = 0;
+    if (!grid) grid = resident_grid(decode_kernel<DEC_WIN, DEC_STAGE>, RR_WAVE);
+    const uint32_t g = nwin < grid ? nwin : grid;
+    hipLaunchKernelGGL((decode_kernel<DEC_WIN, DEC_STAGE>), dim3(g), dim3(RR_WAVE), 0, stream, blob, offsets, n,
+                       first_val, nwin, values, elems, elem_cap, arena, scratch);
+    if (totals)
+        hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(1024), 0, stream, state + nwin, state, nwin, offsets, n, 0,
+                           totals);
     return hipGetLastError();
 }
 
 extern "C" hipError_t rr_launch_encode(const rr_value *values, const rr_elem *elems, const uint8_t *arena,
                                        uint64_t n, uint8_t *out, uint64_t cap, uint64_t *offsets, uint64_t *scratch,
                                        rr_totals *totals, hipStream_t stream) {
-    uint32_t ntiles = (uint32_t)((n + TILE - 1) / TILE);
+    const uint32_t ntiles = (uint32_t)((n + TILE - 1) / TILE);
+    uint64_t *state = scratch + RR_SCRATCH_HDR;
     size_t zero = (RR_SCRATCH_HDR + (size_t)ntiles) * sizeof(uint64_t);
     hipError_t e = hipMemsetAsync(scratch, 0, (zero + 15) & ~(size_t)15, stream);
     if (e != hipSuccess) return e;
@@ -657,11 +790,14 @@ extern "C" hipError_t rr_launch_encode(const rr_value *values, const rr_elem *el
         if (e == hipSuccess && totals) e = hipMemsetAsync(totals, 0, sizeof(rr_totals), stream);
         return e;
     }
-    uint32_t waves_per_wg = WG / RR_WAVE;
-    uint32_t grid = (ntiles + waves_per_wg - 1) / waves_per_wg;
-    hipLaunchKernelGGL(encode_kernel, dim3(grid), dim3(WG), 0, stream, values, elems, arena, n, out, cap, offsets,
-                       scratch, ntiles, totals);
+    static uint32_t grid = 0;
+    if (!grid) grid = resident_grid(encode_kernel, WG);
+    const uint32_t need = (ntiles + WG / RR_WAVE - 1) / (WG / RR_WAVE);
+    const uint32_t g = need < grid ? need : grid;
+    hipLaunchKernelGGL(encode_kernel, dim3(g), dim3(WG), 0, stream, values, elems, arena, n, out, cap, offsets,
+                       scratch, ntiles);
+    if (totals)
+        hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(1024), 0, stream, state + ntiles, state, ntiles, offsets, n,
+                           1, totals);
     return hipGetLastError();
 }
-
-extern "C" uint64_t rr_tile_values(void) { return TILE; }
