@@ -118,35 +118,78 @@ __device__ __forceinline__ uint64_t lb_load(uint64_t *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Returns the exclusive prefix of tile `tile` (wave-uniform); agg is wave-uniform.
-__device__ __forceinline__ uint64_t lookback(uint64_t *state, uint32_t tile, uint64_t agg) {
-    uint32_t lane = lane_id();
-    if (tile == 0) {
-        if (lane == 0) lb_store(&state[0], LB_INC | agg);
-        return 0;
+// Two-level look-back.  Tiles are grouped by 64 (LB_GROUP); besides its own word every tile
+// adds (1 << 48) | aggregate to its group word with one non-returning atomic, so a group word
+// says both how many of its tiles have published and their total.  A tile's exclusive prefix
+// is then found in ~2-3 round trips whatever the number of tiles in flight: one sweep of the
+// (up to 63) earlier tiles of its own group, then sweeps over 64 earlier groups at a time,
+// each lane reading a group word and the word of that group's last tile (an inclusive prefix
+// there ends the walk).  With thousands of concurrent tiles a flat 64-tile look-back needs
+// ~tiles/64 round trips per tile (measured: 3.9 ms for 121K tiles); this needs ~3.
+constexpr uint32_t LB_GROUP = 64;
+constexpr uint64_t GRP_ONE = 1ull << 48;
+constexpr uint64_t GRP_VAL = GRP_ONE - 1;
+
+__device__ __forceinline__ uint64_t lookback(uint64_t *state, uint64_t *groups, uint32_t tile, uint32_t ntiles,
+                                             uint64_t agg) {
+    const uint32_t lane = lane_id();
+    const uint32_t g = tile / LB_GROUP, p = tile % LB_GROUP;
+    if (lane == 0) {
+        lb_store(&state[tile], (tile == 0 ? LB_INC : LB_AGG) | agg);
+        atomicAdd((unsigned long long *)&groups[g], (unsigned long long)(GRP_ONE | agg));
     }
-    if (lane == 0) lb_store(&state[tile], LB_AGG | agg);
+    if (tile == 0) return 0;
     uint64_t excl = 0;
-    int64_t base = (int64_t)tile - 1;
-    for (uint32_t spins = 0;; ++spins) {
-        int64_t j = base - (int64_t)lane;
-        uint64_t s = j >= 0 ? lb_load(&state[j]) : LB_INC;
-        uint64_t flag = s >> 62;
-        uint64_t inc = __ballot(flag == 2);
-        uint64_t empty = __ballot(flag == 0);
+    uint32_t spins = 0;
+    // phase 1: earlier tiles of the same group
+    if (p) {
+        for (;;) {
+            uint64_t s = lane < p ? lb_load(&state[tile - 1 - lane]) : LB_INC;
+            uint64_t flag = s >> 62;
+            uint64_t inc = __ballot(lane < p && flag == 2);
+            uint64_t empty = __ballot(lane < p && flag == 0);
+            uint32_t first = inc ? (uint32_t)__builtin_ctzll(inc) : 64u;
+            uint64_t upto = first >= 63 ? ~0ull : ((2ull << first) - 1);
+            if (empty & upto) {
+                if (++spins > (1u << 24)) return LB_VAL;   // bounded: never hang the GPU
+                __builtin_amdgcn_s_sleep(1);
+                continue;
+            }
+            excl = wave_sum(lane < p && lane <= first ? (s & LB_VAL) : 0);
+            if (first < 64) goto done;
+            break;
+        }
+    }
+    // phase 2: whole earlier groups, 64 per sweep
+    for (int64_t gg = (int64_t)g - 1;;) {
+        const int64_t k = gg - (int64_t)lane;
+        uint64_t last = LB_INC, grp = 0;
+        bool complete = true;
+        if (k >= 0) {
+            last = lb_load(&state[(uint64_t)k * LB_GROUP + LB_GROUP - 1]);
+            grp = lb_load(&groups[k]);
+            uint64_t members = (uint64_t)ntiles - (uint64_t)k * LB_GROUP;
+            if (members > LB_GROUP) members = LB_GROUP;
+            complete = (grp >> 48) == members;
+        }
+        const bool is_inc = (last >> 62) == 2;
+        uint64_t inc = __ballot(is_inc);
         uint32_t first = inc ? (uint32_t)__builtin_ctzll(inc) : 64u;
-        uint64_t upto = first >= 63 ? ~0ull : ((2ull << first) - 1);
-        if (empty & upto) {
-            // bounded spin: a predecessor that never publishes must not hang the GPU
-            if (spins > (1u << 24)) { excl = LB_VAL; break; }
+        uint64_t upto_excl = first >= 64 ? ~0ull : ((1ull << first) - 1);   // lanes before the INC lane
+        uint64_t incomplete = __ballot(!complete);
+        if (incomplete & upto_excl) {
+            if (++spins > (1u << 24)) return LB_VAL;
             __builtin_amdgcn_s_sleep(1);
             continue;
         }
-        uint64_t v = lane <= first ? (s & LB_VAL) : 0;
+        uint64_t v = 0;
+        if (lane < first) v = grp & GRP_VAL;
+        else if (lane == first) v = last & LB_VAL;
         excl += wave_sum(v);
         if (first < 64) break;
-        base -= RR_WAVE;
+        gg -= RR_WAVE;
     }
+done:
     if (lane == 0) lb_store(&state[tile], LB_INC | (excl + agg));
     return excl;
 }

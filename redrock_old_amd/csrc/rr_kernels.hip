@@ -273,14 +273,15 @@ __device__ __forceinline__ void tile_stats(uint64_t *stats, uint32_t tile, uint6
     }
 }
 
-// mode 0 (decode): bytes = offsets[n], n_elems = sum of counts.
-// mode 1 (encode): bytes = inclusive prefix of the last tile (total blob bytes).
-__global__ __launch_bounds__(1024) void finalize_kernel(const uint64_t *__restrict__ stats, uint64_t *state,
-                                                        uint32_t ntiles, const uint64_t *__restrict__ offsets,
-                                                        uint64_t n, int mode, rr_totals *out) {
-    __shared__ uint64_t red[3][16];
+// mode 0 (decode): bytes = offsets[n]; mode 1 (encode): bytes = inclusive prefix of the last
+// tile.  Many blocks (one CU reads ~60 GB/s: a single-block fold of 121K tiles took 56 us),
+// each folding a slice and adding into *out, which the launcher zeroes first.
+__global__ __launch_bounds__(256) void finalize_kernel(const uint64_t *__restrict__ stats, uint64_t *state,
+                                                       uint32_t ntiles, const uint64_t *__restrict__ offsets,
+                                                       uint64_t n, int mode, rr_totals *out) {
+    __shared__ uint64_t red[3][4];
     uint64_t b = 0, p = 0, c = 0;
-    for (uint32_t t = threadIdx.x; t < ntiles; t += blockDim.x) {
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < ntiles; t += gridDim.x * blockDim.x) {
         b += stats[3 * (uint64_t)t + 0];
         p += stats[3 * (uint64_t)t + 1];
         c += stats[3 * (uint64_t)t + 2];
@@ -294,11 +295,23 @@ __global__ __launch_bounds__(1024) void finalize_kernel(const uint64_t *__restri
     if (threadIdx.x == 0) {
         uint64_t tb = 0, tp = 0, tc = 0;
         for (uint32_t k = 0; k < blockDim.x / RR_WAVE; ++k) { tb += red[0][k]; tp += red[1][k]; tc += red[2][k]; }
-        out->n_bad = tb;
-        out->payload = tp;
-        out->n_elems = tc;
-        out->bytes = mode == 0 ? offsets[n] : (ntiles ? (lb_load(&state[ntiles - 1]) & LB_VAL) : 0);
+        if (tb) atomicAdd((unsigned long long *)&out->n_bad, (unsigned long long)tb);
+        if (tp) atomicAdd((unsigned long long *)&out->payload, (unsigned long long)tp);
+        if (tc) atomicAdd((unsigned long long *)&out->n_elems, (unsigned long long)tc);
+        if (blockIdx.x == 0)
+            out->bytes = mode == 0 ? offsets[n] : (ntiles ? (lb_load(&state[ntiles - 1]) & LB_VAL) : 0);
     }
+}
+
+static hipError_t launch_finalize(const uint64_t *stats, uint64_t *state, uint32_t ntiles, const uint64_t *offsets,
+                                  uint64_t n, int mode, rr_totals *out, hipStream_t stream) {
+    hipError_t e = hipMemsetAsync(out, 0, sizeof(rr_totals), stream);
+    if (e != hipSuccess) return e;
+    uint32_t blocks = (ntiles + 255) / 256;
+    if (blocks > 512) blocks = 512;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(finalize_kernel, dim3(blocks), dim3(256), 0, stream, stats, state, ntiles, offsets, n, mode, out);
+    return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------------------- decode
@@ -332,7 +345,8 @@ template <typename P>
 __device__ __forceinline__ void decode_values(P base, uint64_t sbase, const uint64_t *__restrict__ offsets,
                                               uint64_t v_lo, uint64_t v_hi, rr_value *__restrict__ values,
                                               rr_elem *__restrict__ elems, uint64_t elem_cap, uint64_t *state,
-                                              uint32_t tile, uint64_t &bad_out, uint64_t &pay_out,
+                                              uint64_t *groups, uint32_t tile, uint32_t ntiles, uint64_t &bad_out,
+                                              uint64_t &pay_out,
                                               uint64_t &agg_out) {
     const uint32_t lane = lane_id();
     const uint64_t nv = v_hi - v_lo;
@@ -352,7 +366,7 @@ __device__ __forceinline__ void decode_values(P base, uint64_t sbase, const uint
         if (c == 0) { pr0 = pr; o_lo0 = o_lo; o_hi0 = o_hi; cnt0 = pr.n; }
         agg += wave_sum(pr.n);
     }
-    const uint64_t prefix = lookback(state, tile, agg);
+    const uint64_t prefix = lookback(state, groups, tile, ntiles, agg);
     agg_out = agg;
     // emit pass
     uint64_t run = prefix, bad = 0, pay = 0;
@@ -409,7 +423,8 @@ __global__ __launch_bounds__(RR_WAVE) void decode_kernel(const uint8_t *__restri
     __shared__ __attribute__((aligned(16))) uint8_t stage[STAGE];
     const uint32_t lane = lane_id();
     uint64_t *state = scratch + RR_SCRATCH_HDR;
-    uint64_t *stats = state + nwin;
+    uint64_t *groups = state + nwin;
+    uint64_t *stats = groups + (nwin + LB_GROUP - 1) / LB_GROUP;
     const uint64_t nbytes = offsets[n];
     // persistent: static round-robin over windows; every wave only ever waits on lower windows
     // held by co-resident waves (grid <= resident capacity), so the look-back cannot deadlock.
@@ -459,11 +474,11 @@ __global__ __launch_bounds__(RR_WAVE) void decode_kernel(const uint8_t *__restri
 
     uint64_t bad, pay, agg;
     if (staged)
-        decode_values<lds_cptr>((lds_cptr)stage, sbase, offsets, v_lo, v_hi, values, elems, elem_cap, state, tile,
-                                bad, pay, agg);
+        decode_values<lds_cptr>((lds_cptr)stage, sbase, offsets, v_lo, v_hi, values, elems, elem_cap, state, groups,
+                                tile, nwin, bad, pay, agg);
     else
-        decode_values<const uint8_t *>(blob, 0, offsets, v_lo, v_hi, values, elems, elem_cap, state, tile, bad,
-                                       pay, agg);
+        decode_values<const uint8_t *>(blob, 0, offsets, v_lo, v_hi, values, elems, elem_cap, state, groups, tile,
+                                       nwin, bad, pay, agg);
     tile_stats(stats, tile, bad, pay, agg);
     // the stage is rewritten by the next window: all lanes' LDS reads must be done
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -605,7 +620,8 @@ __global__ __launch_bounds__(WG) void encode_kernel(const rr_value *__restrict__
     const uint32_t lane = lane_id();
     BulkQ &q = qs[threadIdx.x / RR_WAVE];
     uint64_t *state = scratch + RR_SCRATCH_HDR;
-    uint64_t *stats = state + ntiles;
+    uint64_t *groups = state + ntiles;
+    uint64_t *stats = groups + (ntiles + LB_GROUP - 1) / LB_GROUP;
     const uint32_t nwaves = gridDim.x * (WG / RR_WAVE);
     for (uint32_t tile = blockIdx.x * (WG / RR_WAVE) + threadIdx.x / RR_WAVE; tile < ntiles; tile += nwaves) {
     const uint64_t v = (uint64_t)tile * TILE + lane;
@@ -624,7 +640,7 @@ __global__ __launch_bounds__(WG) void encode_kernel(const rr_value *__restrict__
     }
     const uint64_t incl = wave_incl_scan(size);
     const uint64_t agg = __shfl(incl, RR_WAVE - 1, RR_WAVE);
-    const uint64_t prefix = lookback(state, tile, agg);
+    const uint64_t prefix = lookback(state, groups, tile, ntiles, agg);
     const uint64_t o = prefix + incl - size;
     if (active) offsets[v] = o;
     if (tile == ntiles - 1 && lane == 0) offsets[n] = prefix + agg;
@@ -748,10 +764,13 @@ extern "C" uint64_t rr_decode_windows(uint64_t data_cap) { return data_cap / DEC
 // three stats words per window, first_val (u32) for every window + sentinel.
 extern "C" uint64_t rr_decode_scratch_words(uint64_t data_cap) {
     uint64_t nwin = rr_decode_windows(data_cap);
-    return RR_SCRATCH_HDR + 4 * nwin + (nwin + 2) / 2 + 1;
+    return RR_SCRATCH_HDR + 4 * nwin + nwin / 64 + 1 + (nwin + 2) / 2 + 1;
 }
 
-extern "C" uint64_t rr_encode_scratch_words(uint64_t n) { return RR_SCRATCH_HDR + 4 * ((n + TILE - 1) / TILE) + 1; }
+extern "C" uint64_t rr_encode_scratch_words(uint64_t n) {
+    uint64_t t = (n + TILE - 1) / TILE;
+    return RR_SCRATCH_HDR + 4 * t + t / 64 + 2;
+}
 
 extern "C" hipError_t rr_launch_decode(const uint8_t *blob, const uint64_t *offsets, uint64_t n, rr_value *values,
                                        rr_elem *elems, uint64_t elem_cap, uint8_t *arena, uint64_t *scratch,
@@ -760,8 +779,10 @@ extern "C" hipError_t rr_launch_decode(const uint8_t *blob, const uint64_t *offs
     // windows past offsets[n] find no values and copy nothing.
     const uint32_t nwin = (uint32_t)rr_decode_windows(data_cap);
     uint64_t *state = scratch + RR_SCRATCH_HDR;
-    uint32_t *first_val = reinterpret_cast<uint32_t *>(state + 4 * (uint64_t)nwin);
-    size_t zero = (RR_SCRATCH_HDR + (size_t)nwin) * sizeof(uint64_t);
+    const uint64_t ngroups = (nwin + LB_GROUP - 1) / LB_GROUP;
+    uint64_t *stats = state + nwin + ngroups;
+    uint32_t *first_val = reinterpret_cast<uint32_t *>(stats + 3 * (uint64_t)nwin);
+    size_t zero = (RR_SCRATCH_HDR + (size_t)nwin + ngroups) * sizeof(uint64_t);
     hipError_t e = hipMemsetAsync(scratch, 0, (zero + 15) & ~(size_t)15, stream);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(plan_kernel, dim3((uint32_t)((n + 1 + 255) / 256)), dim3(256), 0, stream, offsets, n, first_val,
@@ -771,10 +792,9 @@ extern "C" hipError_t rr_launch_decode(const uint8_t *blob, const uint64_t *offs
     const uint32_t g = nwin < grid ? nwin : grid;
     hipLaunchKernelGGL((decode_kernel<DEC_WIN, DEC_STAGE>), dim3(g), dim3(RR_WAVE), 0, stream, blob, offsets, n,
                        first_val, nwin, values, elems, elem_cap, arena, scratch);
-    if (totals)
-        hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(1024), 0, stream, state + nwin, state, nwin, offsets, n, 0,
-                           totals);
-    return hipGetLastError();
+    e = hipGetLastError();
+    if (e == hipSuccess && totals) e = launch_finalize(stats, state, nwin, offsets, n, 0, totals, stream);
+    return e;
 }
 
 extern "C" hipError_t rr_launch_encode(const rr_value *values, const rr_elem *elems, const uint8_t *arena,
@@ -782,7 +802,9 @@ extern "C" hipError_t rr_launch_encode(const rr_value *values, const rr_elem *el
                                        rr_totals *totals, hipStream_t stream) {
     const uint32_t ntiles = (uint32_t)((n + TILE - 1) / TILE);
     uint64_t *state = scratch + RR_SCRATCH_HDR;
-    size_t zero = (RR_SCRATCH_HDR + (size_t)ntiles) * sizeof(uint64_t);
+    const uint64_t ngroups = (ntiles + LB_GROUP - 1) / LB_GROUP;
+    uint64_t *stats = state + ntiles + ngroups;
+    size_t zero = (RR_SCRATCH_HDR + (size_t)ntiles + ngroups) * sizeof(uint64_t);
     hipError_t e = hipMemsetAsync(scratch, 0, (zero + 15) & ~(size_t)15, stream);
     if (e != hipSuccess) return e;
     if (ntiles == 0) {
@@ -796,8 +818,7 @@ extern "C" hipError_t rr_launch_encode(const rr_value *values, const rr_elem *el
     const uint32_t g = need < grid ? need : grid;
     hipLaunchKernelGGL(encode_kernel, dim3(g), dim3(WG), 0, stream, values, elems, arena, n, out, cap, offsets,
                        scratch, ntiles);
-    if (totals)
-        hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(1024), 0, stream, state + ntiles, state, ntiles, offsets, n,
-                           1, totals);
-    return hipGetLastError();
+    e = hipGetLastError();
+    if (e == hipSuccess && totals) e = launch_finalize(stats, state, ntiles, offsets, n, 1, totals, stream);
+    return e;
 }
