@@ -16,6 +16,7 @@
 // No MFMA: this is byte/record work bounded by HBM.
 #include <hip/hip_runtime.h>
 
+#include "rr_decode_fast.h"
 #include "rr_device.h"
 #include "rr_kernels.h"
 
@@ -413,14 +414,16 @@ __device__ __forceinline__ void decode_values(P base, uint64_t sbase, const uint
     pay_out = wave_sum(pay);
 }
 
-template <uint32_t WIN, uint32_t STAGE>
+template <uint32_t WIN, uint32_t STAGE, uint32_t ECAP>
 __global__ __launch_bounds__(RR_WAVE) void decode_kernel(const uint8_t *__restrict__ blob,
                                                          const uint64_t *__restrict__ offsets, uint64_t n,
                                                          const uint32_t *__restrict__ first_val, uint32_t nwin,
                                                          rr_value *__restrict__ values, rr_elem *__restrict__ elems,
                                                          uint64_t elem_cap, uint8_t *__restrict__ arena,
                                                          uint64_t *scratch) {
-    __shared__ __attribute__((aligned(16))) uint8_t stage[STAGE];
+    // +64: the fast path's aligned multi-dword reads may run past the staged bytes
+    __shared__ __attribute__((aligned(16))) uint8_t stage[STAGE + 64];
+    __shared__ uint32_t recs[ECAP];
     const uint32_t lane = lane_id();
     uint64_t *state = scratch + RR_SCRATCH_HDR;
     uint64_t *groups = state + nwin;
@@ -472,14 +475,68 @@ __global__ __launch_bounds__(RR_WAVE) void decode_kernel(const uint8_t *__restri
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 
-    uint64_t bad, pay, agg;
-    if (staged)
-        decode_values<lds_cptr>((lds_cptr)stage, sbase, offsets, v_lo, v_hi, values, elems, elem_cap, state, groups,
-                                tile, nwin, bad, pay, agg);
-    else
-        decode_values<const uint8_t *>(blob, 0, offsets, v_lo, v_hi, values, elems, elem_cap, state, groups, tile,
-                                       nwin, bad, pay, agg);
-    tile_stats(stats, tile, bad, pay, agg);
+    bool done = false;
+    const uint64_t nv = v_hi - v_lo;
+    if (staged && nv <= RR_WAVE) {
+        // fast path: unified walk -> element records -> lane-per-element emission
+        lds_cptr S = (lds_cptr)stage;
+        const bool active = lane < nv;
+        const uint64_t v = v_lo + lane;
+        uint64_t o_lo = sbase, o_hi = sbase;
+        if (active) {
+            o_lo = offsets[v];
+            o_hi = offsets[v + 1];
+        }
+        const uint32_t vb = (uint32_t)(o_lo - sbase), len = (uint32_t)(o_hi - o_lo);
+        uint32_t nrec = 0;
+        const WalkOut wo = fast_walk(S, active, vb, len, recs, ECAP, nrec);
+        if (!__ballot(active && wo.fail) && nrec <= ECAP) {
+            const uint64_t n_ = active ? wo.n : 0;
+            const uint64_t incl = wave_incl_scan(n_);
+            const uint64_t agg = __shfl(incl, RR_WAVE - 1, RR_WAVE);
+            const uint64_t prefix = lookback(state, groups, tile, nwin, agg);
+            const uint64_t ebase = prefix + incl - n_;
+            const bool capok = ebase + n_ <= elem_cap;
+            const uint32_t type = active ? s8(S, vb) : 0xFF;
+            __attribute__((address_space(3))) uint32_t *R = (__attribute__((address_space(3))) uint32_t *)recs;
+            uint64_t pay = 0;
+            for (uint32_t r = 0; r < nrec; r += RR_WAVE) {
+                const uint32_t i = r + lane;
+                const uint32_t rec = i < nrec ? R[i] : 0u;
+                const int ow = (int)((rec >> 16) & 63);
+                const uint32_t otype = __shfl(type, ow, RR_WAVE), oenc = __shfl(wo.enc, ow, RR_WAVE);
+                const uint32_t ovb = __shfl(vb, ow, RR_WAVE), olen = __shfl(len, ow, RR_WAVE);
+                const uint64_t obase = __shfl(ebase, ow, RR_WAVE);
+                const int ook = __shfl((int)capok, ow, RR_WAVE);
+                if (i < nrec && ook) {
+                    uint4 w;
+                    const uint32_t k = rec >> 22;
+                    fast_emit(S, sbase, otype, oenc, ovb, olen, rec & 0xFFFF, k, w, pay);
+                    *reinterpret_cast<uint4 *>(elems + obase + k) = w;
+                }
+            }
+            if (active) {
+                uint4 w;
+                w.x = type | (wo.enc << 8) | ((capok ? RR_OK : RR_E_CAPACITY) << 16);
+                w.y = s32(S, vb + 1) & RR_LRU_MASK;
+                w.z = wo.n;
+                w.w = (uint32_t)ebase;
+                reinterpret_cast<uint4 *>(values)[v] = w;
+            }
+            tile_stats(stats, tile, wave_sum(active && !capok ? 1 : 0), wave_sum(pay), agg);
+            done = true;
+        }
+    }
+    if (!done) {
+        uint64_t bad, pay, agg;
+        if (staged)
+            decode_values<lds_cptr>((lds_cptr)stage, sbase, offsets, v_lo, v_hi, values, elems, elem_cap, state,
+                                    groups, tile, nwin, bad, pay, agg);
+        else
+            decode_values<const uint8_t *>(blob, 0, offsets, v_lo, v_hi, values, elems, elem_cap, state, groups, tile,
+                                           nwin, bad, pay, agg);
+        tile_stats(stats, tile, bad, pay, agg);
+    }
     // the stage is rewritten by the next window: all lanes' LDS reads must be done
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
@@ -744,6 +801,8 @@ __global__ __launch_bounds__(WG) void encode_kernel(const rr_value *__restrict__
 // ---------------------------------------------------------------------------------------- launch
 constexpr uint32_t DEC_WIN = 4096;
 constexpr uint32_t DEC_STAGE = 8192;
+constexpr uint32_t DEC_ECAP = 1024;
+#define DECODE_KERNEL decode_kernel<DEC_WIN, DEC_STAGE, DEC_ECAP>
 
 // Resident workgroup count for a persistent launch: occupancy query minus one block per CU
 // (the API over-reports by one for SGPR-heavy kernels, MI355X_MICROARCH.md §Residency).
@@ -788,9 +847,9 @@ extern "C" hipError_t rr_launch_decode(const uint8_t *blob, const uint64_t *offs
     hipLaunchKernelGGL(plan_kernel, dim3((uint32_t)((n + 1 + 255) / 256)), dim3(256), 0, stream, offsets, n, first_val,
                        nwin, DEC_WIN);
     static uint32_t grid = 0;
-    if (!grid) grid = resident_grid(decode_kernel<DEC_WIN, DEC_STAGE>, RR_WAVE);
+    if (!grid) grid = resident_grid(DECODE_KERNEL, RR_WAVE);
     const uint32_t g = nwin < grid ? nwin : grid;
-    hipLaunchKernelGGL((decode_kernel<DEC_WIN, DEC_STAGE>), dim3(g), dim3(RR_WAVE), 0, stream, blob, offsets, n,
+    hipLaunchKernelGGL((DECODE_KERNEL), dim3(g), dim3(RR_WAVE), 0, stream, blob, offsets, n,
                        first_val, nwin, values, elems, elem_cap, arena, scratch);
     e = hipGetLastError();
     if (e == hipSuccess && totals) e = launch_finalize(stats, state, nwin, offsets, n, 0, totals, stream);
