@@ -344,8 +344,89 @@ def encode_one(val: dict, elems, arena: bytes) -> bytes:
     return bytes(out)
 
 
+def reserve(b: bytes) -> int:
+    """Descriptor slots a value owns in the flat batch, from its header alone (plus the length
+    chain of a List, which has no count field).  For every valid blob this equals the number of
+    descriptors decode emits; a malformed value keeps its slots, zero-filled.  It lets the GPU
+    size every value's output before parsing it (include/rr_format.h, "descriptor slots")."""
+    L = len(b)
+    if L < 5:
+        return 0
+    t = b[0]
+    if t == T_STRING:
+        return 1 if L >= 6 else 0
+    if t == T_LIST_QUICKLIST:
+        p, n = 5, 0
+        while p < L:
+            if L - p < 4:
+                break
+            ln = _u32(b, p)
+            if ln > L - p - 4:
+                break
+            n += 1
+            p += 4 + ln
+        return n
+    if L < 13:
+        return 0
+    if t == T_SET_INTSET:
+        w, c = _u32(b, 5), _u32(b, 9)
+        return c if (w in (2, 4, 8) and L - 13 == w * c) else 0
+    if t == T_SET_HT:
+        return min(_u64(b, 5), (L - 13) // 8)
+    if t == T_HASH_HT:
+        return min(2 * _u64(b, 5), (L - 13) // 8)
+    if t == T_ZSET_SKIPLIST:
+        return 2 * min(_u64(b, 5), (L - 13) // 16)
+    if t in (T_HASH_ZIPLIST, T_ZSET_ZIPLIST):
+        Lz = _u64(b, 5)
+        if Lz != L - 13 or Lz < 11:
+            return 0
+        zllen = struct.unpack_from("<H", b, 13 + 8)[0]
+        if zllen != 0xFFFF:
+            return 1 + min(zllen, (Lz - 11) // 2)
+        return 1 + _zl_walk_count(b[13:])
+    return 0
+
+
+def _zl_walk_count(zl: bytes) -> int:
+    """Entries of a ziplist whose zllen saturated at 0xFFFF: walk until the end byte or the
+    first entry that does not parse (ziplist.c:300-447)."""
+    L, p, n = len(zl), 10, 0
+    while p < L - 1 and zl[p] != 0xFF:
+        pls = 1 if zl[p] < 254 else 5
+        q = p + pls
+        if q >= L - 1:
+            break
+        enc = zl[q]
+        if enc < 0xC0:
+            cls = enc & 0xC0
+            if cls == 0x00:
+                e = q + 1 + (enc & 0x3F)
+            elif cls == 0x40:
+                if q + 2 > L - 1:
+                    break
+                e = q + 2 + (((enc & 0x3F) << 8) | zl[q + 1])
+            else:
+                if q + 5 > L - 1:
+                    break
+                e = q + 5 + struct.unpack_from(">I", zl, q + 1)[0]
+        elif enc in _INT_SIZES:
+            e = q + 1 + _INT_SIZES[enc]
+        elif 0xF1 <= enc <= 0xFD:
+            e = q + 1
+        else:
+            break
+        if e > L - 1:
+            break
+        n += 1
+        p = e
+    return n
+
+
 def decode_batch(blobs):
-    """Decode a list of blobs as one batch: returns (data, offsets, values, elems, arena)."""
+    """Decode a list of blobs as one batch: returns (data, offsets, values, elems, arena).
+    Value i owns descriptor slots [elem_base, elem_base + reserve(blob i)); a malformed value
+    leaves its slots as zero descriptors (K_STR, 0, 0, 0)."""
     offsets = [0]
     for b in blobs:
         offsets.append(offsets[-1] + len(b))
@@ -353,9 +434,12 @@ def decode_batch(blobs):
     values, elems = [], []
     for i, b in enumerate(blobs):
         v, es = decode_one(b, offsets[i])
+        r = reserve(b)
+        if v["status"] == OK and len(es) != r:
+            v["status"], v["n_elems"], es = E_COUNT, 0, []
         v["elem_base"] = len(elems)
         values.append(v)
-        elems.extend(es)
+        elems.extend(es if v["status"] == OK else [(K_STR, 0, 0, 0)] * r)
     return data, offsets, values, elems, data  # mirror arena == blob bytes
 
 

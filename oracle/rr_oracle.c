@@ -277,6 +277,75 @@ done:
     return st;
 }
 
+/* Descriptor slots a value owns (rr_format.h "descriptor slots"): from the header alone, plus
+ * the length chain of a List.  Equals the decoded count for every valid blob; a malformed
+ * value keeps its slots zero-filled. */
+static uint64_t zl_walk_count(const uint8_t *zl, uint64_t L) {
+    uint64_t p = 10, n = 0;
+    while (p < L - 1 && zl[p] != 0xFF) {
+        uint64_t q = p + (zl[p] < 254 ? 1 : 5), e;
+        if (q >= L - 1) break;
+        uint8_t enc = zl[q];
+        if (enc < 0xC0) {
+            uint8_t cls = enc & 0xC0;
+            if (cls == 0x00) e = q + 1 + (enc & 0x3F);
+            else if (cls == 0x40) { if (q + 2 > L - 1) break; e = q + 2 + (((uint64_t)(enc & 0x3F) << 8) | zl[q + 1]); }
+            else {
+                if (q + 5 > L - 1) break;
+                e = q + 5 + (((uint64_t)zl[q + 1] << 24) | ((uint64_t)zl[q + 2] << 16) | ((uint64_t)zl[q + 3] << 8) | zl[q + 4]);
+            }
+        } else if (enc == 0xFE) e = q + 2;
+        else if (enc == 0xC0) e = q + 3;
+        else if (enc == 0xF0) e = q + 4;
+        else if (enc == 0xD0) e = q + 5;
+        else if (enc == 0xE0) e = q + 9;
+        else if (enc >= 0xF1 && enc <= 0xFD) e = q + 1;
+        else break;
+        if (e > L - 1) break;
+        n++;
+        p = e;
+    }
+    return n;
+}
+
+uint64_t rro_reserve(const uint8_t *b, uint64_t L) {
+    if (L < 5) return 0;
+    switch (b[0]) {
+    case RR_TYPE_STRING: return L >= 6 ? 1 : 0;
+    case RR_TYPE_LIST_QUICKLIST: {
+        uint64_t p = 5, n = 0;
+        while (p < L) {
+            if (L - p < 4) break;
+            uint64_t l = ld32(b + p);
+            if (l > L - p - 4) break;
+            n++;
+            p += 4 + l;
+        }
+        return n;
+    }
+    default: break;
+    }
+    if (L < 13) return 0;
+    switch (b[0]) {
+    case RR_TYPE_SET_INTSET: {
+        uint64_t w = ld32(b + 5), c = ld32(b + 9);
+        return ((w == 2 || w == 4 || w == 8) && L - 13 == w * c) ? c : 0;
+    }
+    case RR_TYPE_SET_HT: { uint64_t c = ld64(b + 5), m = (L - 13) / 8; return c < m ? c : m; }
+    case RR_TYPE_HASH_HT: { uint64_t c = ld64(b + 5), m = (L - 13) / 8; return c > m / 2 ? m : 2 * c; }
+    case RR_TYPE_ZSET_SKIPLIST: { uint64_t c = ld64(b + 5), m = (L - 13) / 16; return 2 * (c < m ? c : m); }
+    case RR_TYPE_HASH_ZIPLIST:
+    case RR_TYPE_ZSET_ZIPLIST: {
+        uint64_t Lz = ld64(b + 5);
+        if (Lz != L - 13 || Lz < 11) return 0;
+        uint64_t zllen = (uint64_t)b[21] | ((uint64_t)b[22] << 8);
+        if (zllen != 0xFFFF) { uint64_t m = (Lz - 11) / 2; return 1 + (zllen < m ? zllen : m); }
+        return 1 + zl_walk_count(b + 13, Lz);
+    }
+    default: return 0;
+    }
+}
+
 /* ---------------------------------------------------------------- batch, pthreads */
 
 typedef struct {
@@ -297,21 +366,27 @@ static void *dec_worker(void *arg) {
         uint64_t o = j->off[i], len = j->off[i + 1] - o, ne, pl;
         rr_value *v = &j->values[i];
         if (j->pass == 1) {
-            rro_decode_one(j->data, o, len, v, NULL, &ne, &pl);
-            v->n_elems = (uint32_t)ne;
-            cnt += ne;
+            uint64_t r = rro_reserve(j->data + o, len);
+            v->elem_base = (uint32_t)r;          /* stash the reservation for pass 2 */
+            cnt += r;
         } else {
-            ne = v->n_elems;
+            uint64_t r = v->elem_base;
+            rro_decode_one(j->data, o, len, v, NULL, &ne, &pl);
+            if (v->status == RR_OK && ne != r) { v->status = RR_E_COUNT; ne = 0; }
             v->elem_base = (uint32_t)base;
-            if (v->status == RR_OK) {
-                if (base + ne > j->cap) { v->status = RR_E_CAPACITY; }
-                else {
-                    rro_decode_one(j->data, o, len, v, j->elems + base, &ne, &pl);
-                    pay += pl;
-                }
+            if (v->status != RR_OK) {
+                /* malformed: its slots are zero-filled (when they fit) and it owns no descriptors */
+                if (base + r <= j->cap) memset(j->elems + base, 0, sizeof(rr_elem) * r);
+                ne = 0;
+            } else if (base + r > j->cap) {
+                v->status = RR_E_CAPACITY;                 /* keeps its count, writes nothing */
+            } else {
+                rro_decode_one(j->data, o, len, v, j->elems + base, &ne, &pl);
+                pay += pl;
             }
+            v->n_elems = (uint32_t)ne;
             if (v->status != RR_OK) bad++;
-            base += ne;
+            base += r;
         }
     }
     j->count = cnt; j->payload = pay; j->bad = bad;

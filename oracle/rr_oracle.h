@@ -40,6 +40,9 @@ int rro_parse_ziplist(const uint8_t *zl, uint64_t L, uint64_t base, rr_elem *out
 int rro_decode_one(const uint8_t *data, uint64_t off, uint64_t len, rr_value *v,
                    rr_elem *out, uint64_t *n_elems, uint64_t *payload);
 
+/* Descriptor slots value b[0, L) owns in a decoded batch (== its descriptor count if valid). */
+uint64_t rro_reserve(const uint8_t *b, uint64_t L);
+
 /* Flat batch decode; arena receives the mirror copy of data[0, offsets[n]). */
 int rro_decode(const uint8_t *data, const uint64_t *offsets, uint64_t n, rr_value *values,
                rr_elem *elems, uint64_t elem_cap, uint8_t *arena, rr_totals *t, int nthreads);

@@ -85,7 +85,7 @@ static int ensure_scratch(rr_ctx *c, uint64_t words) {
 
 int rr_ctx_reserve(rr_ctx *c, uint64_t n_values, uint64_t n_bytes) {
     if (!c) return fail(RR_API_EINVAL, "ctx is NULL");
-    uint64_t a = rr_encode_scratch_words(n_values), b = rr_decode_scratch_words((n_bytes + 15) & ~15ull);
+    uint64_t a = rr_encode_scratch_words(n_values), b = rr_decode_scratch_words((n_bytes + 15) & ~15ull, n_values);
     return ensure_scratch(c, a > b ? a : b);
 }
 
@@ -106,7 +106,7 @@ int rr_decode_batch(rr_ctx *c, const rr_blob_batch *in, rr_flat_batch *out, rr_t
     if (!aligned16(in->data) || !aligned16(out->arena)) return fail(RR_API_EINVAL, "data/arena not 16-byte aligned");
     if (in->data_cap & 15) return fail(RR_API_EINVAL, "data_cap must be a multiple of 16");
     if (out->arena_cap < in->data_cap) return fail(RR_API_EINVAL, "arena_cap < data_cap");
-    int rc = ensure_scratch(c, rr_decode_scratch_words(in->data_cap));
+    int rc = ensure_scratch(c, rr_decode_scratch_words(in->data_cap, in->n));
     if (rc) return rc;
     HIPCHK(rr_launch_decode(in->data, in->offsets, in->n, out->values, out->elems, out->elem_cap, out->arena,
                             c->scratch, in->data_cap, d_totals, (hipStream_t)stream));

@@ -299,8 +299,13 @@ __global__ __launch_bounds__(256) void finalize_kernel(const uint64_t *__restric
         if (tb) atomicAdd((unsigned long long *)&out->n_bad, (unsigned long long)tb);
         if (tp) atomicAdd((unsigned long long *)&out->payload, (unsigned long long)tp);
         if (tc) atomicAdd((unsigned long long *)&out->n_elems, (unsigned long long)tc);
-        if (blockIdx.x == 0)
-            out->bytes = mode == 0 ? offsets[n] : (ntiles ? (lb_load(&state[ntiles - 1]) & LB_VAL) : 0);
+        if (blockIdx.x == 0) {
+            if (mode == 2) {   // decode: descriptor slots = scanned total, bytes = offsets[n]
+                out->bytes = offsets[n];
+                atomicAdd((unsigned long long *)&out->n_elems, (unsigned long long)state[0]);
+            } else
+                out->bytes = mode == 0 ? offsets[n] : (ntiles ? (lb_load(&state[ntiles - 1]) & LB_VAL) : 0);
+        }
     }
 }
 
@@ -327,219 +332,297 @@ static hipError_t launch_finalize(const uint64_t *stats, uint64_t *state, uint32
 //   4. re-parses from LDS and writes descriptors + value records.
 // Windows whose values do not fit the stage parse from global memory (L2-hot) instead.
 
-__global__ __launch_bounds__(256) void plan_kernel(const uint64_t *__restrict__ offsets, uint64_t n,
-                                                   uint32_t *__restrict__ first_val, uint32_t nwin, uint32_t win) {
-    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// ---- K1: plan windows + descriptor reservation per value -------------------------------
+// Thread per value i in [0, n]: first_val for the byte windows whose first value is i, and
+// reserve(i) = the descriptor slots value i owns (rr_format.h): header fields only, plus the
+// length chain of a List.  Equal to the decoded count for every valid blob.
+__device__ __forceinline__ uint64_t zl_walk_count_g(const uint8_t *zl, uint64_t L) {
+    uint64_t p = 10, n = 0;
+    while (p < L - 1 && zl[p] != 0xFF) {
+        const uint64_t q = p + (zl[p] < 254 ? 1 : 5);
+        if (q >= L - 1) break;
+        const uint32_t enc = zl[q];
+        uint64_t e;
+        if (enc < 0xC0) {
+            const uint32_t cls = enc & 0xC0;
+            if (cls == 0x00) e = q + 1 + (enc & 0x3F);
+            else if (cls == 0x40) { if (q + 2 > L - 1) break; e = q + 2 + (((uint64_t)(enc & 0x3F) << 8) | zl[q + 1]); }
+            else { if (q + 5 > L - 1) break; e = q + 5 + __builtin_bswap32(ld_u32(zl + q + 1)); }
+        } else if (enc == 0xFE) e = q + 2;
+        else if (enc == 0xC0) e = q + 3;
+        else if (enc == 0xF0) e = q + 4;
+        else if (enc == 0xD0) e = q + 5;
+        else if (enc == 0xE0) e = q + 9;
+        else if (enc >= 0xF1 && enc <= 0xFD) e = q + 1;
+        else break;
+        if (e > L - 1) break;
+        ++n;
+        p = e;
+    }
+    return n;
+}
+
+__device__ __forceinline__ uint64_t reserve_g(const uint8_t *b, uint64_t L) {
+    if (L < 5) return 0;
+    const uint32_t t = b[0];
+    if (t == RR_TYPE_STRING) return L >= 6 ? 1 : 0;
+    if (t == RR_TYPE_LIST_QUICKLIST) {
+        uint64_t p = 5, n = 0;
+        while (p < L) {
+            if (L - p < 4) break;
+            const uint64_t l = ld_u32(b + p);
+            if (l > L - p - 4) break;
+            ++n;
+            p += 4 + l;
+        }
+        return n;
+    }
+    if (L < 13) return 0;
+    switch (t) {
+        case RR_TYPE_SET_INTSET: {
+            const uint64_t w = ld_u32(b + 5), c = ld_u32(b + 9);
+            return ((w == 2 || w == 4 || w == 8) && L - 13 == w * c) ? c : 0;
+        }
+        case RR_TYPE_SET_HT: { const uint64_t c = ld_u64(b + 5), m = (L - 13) / 8; return c < m ? c : m; }
+        case RR_TYPE_HASH_HT: { const uint64_t c = ld_u64(b + 5), m = (L - 13) / 8; return c > m / 2 ? m : 2 * c; }
+        case RR_TYPE_ZSET_SKIPLIST: { const uint64_t c = ld_u64(b + 5), m = (L - 13) / 16; return 2 * (c < m ? c : m); }
+        case RR_TYPE_HASH_ZIPLIST:
+        case RR_TYPE_ZSET_ZIPLIST: {
+            const uint64_t Lz = ld_u64(b + 5);
+            if (Lz != L - 13 || Lz < 11) return 0;
+            const uint64_t zllen = ld_u16(b + 21);
+            if (zllen != 0xFFFF) { const uint64_t m = (Lz - 11) / 2; return 1 + (zllen < m ? zllen : m); }
+            return 1 + zl_walk_count_g(b + 13, Lz);
+        }
+        default:
+            return 0;
+    }
+}
+
+__global__ __launch_bounds__(256) void count_kernel(const uint8_t *__restrict__ blob,
+                                                    const uint64_t *__restrict__ offsets, uint64_t n,
+                                                    uint32_t *__restrict__ first_val, uint32_t nwin, uint32_t win,
+                                                    uint64_t *__restrict__ counts) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i > n) return;
-    uint64_t w_lo = i == 0 ? 0 : offsets[i - 1] / win + 1;
-    uint64_t w_hi = offsets[i] / win;
+    const uint64_t o_hi = offsets[i];
+    const uint64_t o_lo = i == 0 ? 0 : offsets[i - 1];
+    uint64_t w_lo = i == 0 ? 0 : o_lo / win + 1;
+    uint64_t w_hi = o_hi / win;
     if (i == n) w_hi = nwin;   // windows past the last value start, and the sentinel
     for (uint64_t w = w_lo; w <= w_hi && w <= nwin; ++w) first_val[w] = (uint32_t)i;
+    if (i < n) {
+        const uint64_t b0 = o_hi, b1 = offsets[i + 1];
+        counts[i] = reserve_g(blob + b0, b1 - b0);
+    }
 }
 
-template <bool EMIT, typename P>
-__device__ __forceinline__ Parsed parse_at(P base, uint64_t sbase, uint64_t o_lo, uint64_t o_hi, rr_elem *out) {
-    return parse_value<EMIT, P>(base + (uint32_t)(o_lo - sbase), o_lo, o_hi - o_lo, out);
+// ---- K2: exclusive scan of the reservations -> elem_base -------------------------------
+// 4096 values per 256-thread workgroup, tile ids from an atomic ticket (so a tile only waits
+// on tiles already running), decoupled look-back between tiles (two-level, rr_device.h).
+constexpr uint32_t SCAN_PER_THREAD = 16;
+constexpr uint32_t SCAN_TILE = 256 * SCAN_PER_THREAD;
+
+__global__ __launch_bounds__(256) void scan_kernel(uint64_t *__restrict__ counts, uint64_t n, uint64_t *lb,
+                                                   uint32_t ntiles) {
+    __shared__ uint64_t wsum[4];
+    __shared__ uint64_t sh_prefix;
+    __shared__ uint32_t sh_tile;
+    uint64_t *ticket = lb;
+    uint64_t *state = lb + 1;
+    uint64_t *groups = state + ntiles;
+    if (threadIdx.x == 0) sh_tile = (uint32_t)atomicAdd((unsigned long long *)ticket, 1ull);
+    __syncthreads();
+    const uint32_t tile = sh_tile;
+    const uint64_t base = (uint64_t)tile * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_PER_THREAD;
+    uint64_t x[SCAN_PER_THREAD];
+    uint64_t sum = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < SCAN_PER_THREAD; ++k) {
+        x[k] = base + k < n ? counts[base + k] : 0;
+        sum += x[k];
+    }
+    const uint64_t incl = wave_incl_scan(sum);
+    const uint32_t w = threadIdx.x / RR_WAVE;
+    if (lane_id() == RR_WAVE - 1) wsum[w] = incl;
+    __syncthreads();
+    uint64_t wpre = 0, agg = 0;
+    for (uint32_t k = 0; k < 4; ++k) {
+        if (k < w) wpre += wsum[k];
+        agg += wsum[k];
+    }
+    if (w == 0) {
+        const uint64_t pre = lookback(state, groups, tile, ntiles, agg);
+        if (lane_id() == 0) sh_prefix = pre;
+    }
+    __syncthreads();
+    uint64_t run = sh_prefix + wpre + incl - sum;
+#pragma unroll
+    for (uint32_t k = 0; k < SCAN_PER_THREAD; ++k) {
+        if (base + k < n) counts[base + k] = run;
+        run += x[k];
+    }
+    if (tile == ntiles - 1 && threadIdx.x == 255) counts[n] = sh_prefix + agg;
 }
 
+// ---- K3: windows: mirror copy + stage + walk + emit ------------------------------------
+// The blob buffer is cut into fixed byte WINDOWS; window t owns the values whose first byte
+// lies in [t*WIN, (t+1)*WIN).  Output positions come from K2, so windows are independent:
+// no inter-window wait, a slow window delays only itself.
 template <typename P>
-__device__ __forceinline__ void decode_values(P base, uint64_t sbase, const uint64_t *__restrict__ offsets,
-                                              uint64_t v_lo, uint64_t v_hi, rr_value *__restrict__ values,
-                                              rr_elem *__restrict__ elems, uint64_t elem_cap, uint64_t *state,
-                                              uint64_t *groups, uint32_t tile, uint32_t ntiles, uint64_t &bad_out,
-                                              uint64_t &pay_out,
-                                              uint64_t &agg_out) {
-    const uint32_t lane = lane_id();
-    const uint64_t nv = v_hi - v_lo;
-    // count pass
-    uint64_t agg = 0, cnt0 = 0;
-    Parsed pr0{RR_OK, 0, 0, 0};
-    uint64_t o_lo0 = 0, o_hi0 = 0;
-    for (uint64_t c = 0; c < nv; c += RR_WAVE) {
-        uint64_t v = v_lo + c + lane;
-        Parsed pr{RR_OK, 0, 0, 0};
-        uint64_t o_lo = 0, o_hi = 0;
-        if (v < v_hi) {
-            o_lo = offsets[v];
-            o_hi = offsets[v + 1];
-            pr = parse_at<false, P>(base, sbase, o_lo, o_hi, nullptr);
-        }
-        if (c == 0) { pr0 = pr; o_lo0 = o_lo; o_hi0 = o_hi; cnt0 = pr.n; }
-        agg += wave_sum(pr.n);
+__device__ __forceinline__ void exact_chunk(P base, uint64_t sbase, const uint64_t *__restrict__ offsets,
+                                            const uint64_t *__restrict__ ebase, uint64_t v0, uint64_t v_hi,
+                                            rr_value *__restrict__ values, rr_elem *__restrict__ elems,
+                                            uint64_t elem_cap, uint64_t &bad, uint64_t &pay) {
+    // the exact parser, lane = value: assigns the reference's status codes to malformed values
+    const uint64_t v = v0 + lane_id();
+    if (v >= v_hi) return;
+    const uint64_t o_lo = offsets[v], o_hi = offsets[v + 1];
+    const uint64_t eb = ebase[v], r = ebase[v + 1] - eb;
+    P b = base + (uint32_t)(o_lo - sbase);
+    Parsed pr = parse_value<false, P>(b, o_lo, o_hi - o_lo, nullptr);
+    uint32_t status = pr.status;
+    uint64_t ne = pr.n;
+    if (status == RR_OK && ne != r) status = RR_E_COUNT;
+    const bool fits = eb + r <= elem_cap && eb + r <= 0xFFFFFFFFull;
+    if (status != RR_OK) {
+        ne = 0;
+        if (fits)
+            for (uint64_t k = 0; k < r; ++k) put_elem(elems + eb + k, 0, 0, 0, 0);
+    } else if (!fits) {
+        status = RR_E_CAPACITY;
+    } else {
+        Parsed e = parse_value<true, P>(b, o_lo, o_hi - o_lo, elems + eb);
+        pay += e.payload;
     }
-    const uint64_t prefix = lookback(state, groups, tile, ntiles, agg);
-    agg_out = agg;
-    // emit pass
-    uint64_t run = prefix, bad = 0, pay = 0;
-    for (uint64_t c = 0; c < nv; c += RR_WAVE) {
-        uint64_t v = v_lo + c + lane;
-        bool active = v < v_hi;
-        Parsed pr;
-        uint64_t o_lo, o_hi;
-        if (c == 0) { pr = pr0; o_lo = o_lo0; o_hi = o_hi0; }
-        else {
-            pr = Parsed{RR_OK, 0, 0, 0};
-            o_lo = o_hi = 0;
-            if (active) {
-                o_lo = offsets[v];
-                o_hi = offsets[v + 1];
-                pr = parse_at<false, P>(base, sbase, o_lo, o_hi, nullptr);
-            }
-        }
-        (void)cnt0;
-        const uint64_t incl = wave_incl_scan(pr.n);
-        const uint64_t elem_base = run + incl - pr.n;
-        run += __shfl(incl, RR_WAVE - 1, RR_WAVE);
-        if (active) {
-            uint32_t status = pr.status;
-            if (status == RR_OK && elem_base + pr.n > elem_cap) status = RR_E_CAPACITY;
-            if (status == RR_OK && pr.n) {
-                Parsed e = parse_at<true, P>(base, sbase, o_lo, o_hi, elems + elem_base);
-                pay += e.payload;
-            }
-            P b = base + (uint32_t)(o_lo - sbase);
-            uint32_t len = (uint32_t)(o_hi - o_lo);
-            uint32_t type = len ? ld_u8(b) : 0;
-            uint32_t lru = len >= 5 ? (ld_u32(b + 1) & RR_LRU_MASK) : 0;
-            uint4 w;
-            w.x = type | (pr.enc << 8) | (status << 16);
-            w.y = lru;
-            w.z = (uint32_t)pr.n;
-            w.w = (uint32_t)elem_base;
-            reinterpret_cast<uint4 *>(values)[v] = w;
-            bad += status != RR_OK ? 1 : 0;
-        }
-    }
-    bad_out = wave_sum(bad);
-    pay_out = wave_sum(pay);
+    const uint32_t len = (uint32_t)(o_hi - o_lo);
+    uint4 w;
+    w.x = (len ? ld_u8(b) : 0) | (pr.enc << 8) | (status << 16);
+    w.y = len >= 5 ? (ld_u32(b + 1) & RR_LRU_MASK) : 0;
+    w.z = (uint32_t)ne;
+    w.w = (uint32_t)eb;
+    reinterpret_cast<uint4 *>(values)[v] = w;
+    bad += status != RR_OK ? 1 : 0;
 }
 
 template <uint32_t WIN, uint32_t STAGE, uint32_t ECAP>
 __global__ __launch_bounds__(RR_WAVE) void decode_kernel(const uint8_t *__restrict__ blob,
                                                          const uint64_t *__restrict__ offsets, uint64_t n,
                                                          const uint32_t *__restrict__ first_val, uint32_t nwin,
+                                                         const uint64_t *__restrict__ ebase,
                                                          rr_value *__restrict__ values, rr_elem *__restrict__ elems,
                                                          uint64_t elem_cap, uint8_t *__restrict__ arena,
-                                                         uint64_t *scratch) {
+                                                         uint64_t *__restrict__ stats) {
     // +64: the fast path's aligned multi-dword reads may run past the staged bytes
     __shared__ __attribute__((aligned(16))) uint8_t stage[STAGE + 64];
     __shared__ uint32_t recs[ECAP];
     const uint32_t lane = lane_id();
-    uint64_t *state = scratch + RR_SCRATCH_HDR;
-    uint64_t *groups = state + nwin;
-    uint64_t *stats = groups + (nwin + LB_GROUP - 1) / LB_GROUP;
     const uint64_t nbytes = offsets[n];
-    // persistent: static round-robin over windows; every wave only ever waits on lower windows
-    // held by co-resident waves (grid <= resident capacity), so the look-back cannot deadlock.
+    const uint64_t cap = elem_cap < 0xFFFFFFFFull ? elem_cap : 0xFFFFFFFFull;   // elem_base is 32-bit
     for (uint32_t tile = blockIdx.x; tile < nwin; tile += gridDim.x) {
-    const uint64_t v_lo = first_val[tile], v_hi = first_val[tile + 1];
-    const uint64_t W0 = (uint64_t)tile * WIN;
-    const uint64_t padded = (nbytes + 15) & ~15ull;
-    const uint64_t W1 = W0 + WIN < padded ? W0 + WIN : padded;
-    uint64_t S0 = W0, S1 = W0;
-    if (v_hi > v_lo) {
-        S0 = offsets[v_lo];
-        S1 = offsets[v_hi];
-    }
-    const uint64_t sbase = S0 & ~15ull;
-    const uint64_t send = (S1 + 15) & ~15ull;
-    const bool staged = send - sbase <= STAGE;
-    const uint64_t L1 = staged && send > W1 ? send : W1;
+        const uint64_t v_lo = first_val[tile], v_hi = first_val[tile + 1];
+        const uint64_t W0 = (uint64_t)tile * WIN;
+        const uint64_t padded = (nbytes + 15) & ~15ull;
+        const uint64_t W1 = W0 + WIN < padded ? W0 + WIN : padded;
+        uint64_t S0 = W0, S1 = W0;
+        if (v_hi > v_lo) {
+            S0 = offsets[v_lo];
+            S1 = offsets[v_hi];
+        }
+        const uint64_t sbase = S0 & ~15ull;
+        const uint64_t send = (S1 + 15) & ~15ull;
+        const bool staged = send - sbase <= STAGE;
+        const uint64_t L1 = staged && send > W1 ? send : W1;
 
-    // 1. copy window -> arena, stage value bytes -> LDS (one load feeds both)
-    {
-        const u32x4 *src = reinterpret_cast<const u32x4 *>(blob);
-        u32x4 *dst = reinterpret_cast<u32x4 *>(arena);
-        u32x4 *lds = reinterpret_cast<u32x4 *>(stage);
-        const uint64_t cw1 = W1 >> 4, cs0 = sbase >> 4;
-        uint64_t c = (W0 >> 4) + lane;
-        const uint64_t ce = L1 >> 4;
-        for (; c + 3 * RR_WAVE < ce; c += 4 * RR_WAVE) {
-            u32x4 x[4];
+        // 1. copy window -> arena, stage value bytes -> LDS (one load feeds both)
+        {
+            const u32x4 *src = reinterpret_cast<const u32x4 *>(blob);
+            u32x4 *dst = reinterpret_cast<u32x4 *>(arena);
+            u32x4 *lds = reinterpret_cast<u32x4 *>(stage);
+            const uint64_t cw1 = W1 >> 4, cs0 = sbase >> 4;
+            uint64_t c = (W0 >> 4) + lane;
+            const uint64_t ce = L1 >> 4;
+            for (; c + 3 * RR_WAVE < ce; c += 4 * RR_WAVE) {
+                u32x4 x[4];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) x[k] = src[c + k * RR_WAVE];
+                for (int k = 0; k < 4; ++k) x[k] = src[c + k * RR_WAVE];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                uint64_t cc = c + k * RR_WAVE;
-                if (cc < cw1) __builtin_nontemporal_store(x[k], dst + cc);
-                if (staged && cc >= cs0) lds[cc - cs0] = x[k];
-            }
-        }
-        for (; c < ce; c += RR_WAVE) {
-            u32x4 x = src[c];
-            if (c < cw1) __builtin_nontemporal_store(x, dst + c);
-            if (staged && c >= cs0) lds[c - cs0] = x;
-        }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-
-    bool done = false;
-    const uint64_t nv = v_hi - v_lo;
-    if (staged && nv <= RR_WAVE) {
-        // fast path: unified walk -> element records -> lane-per-element emission
-        lds_cptr S = (lds_cptr)stage;
-        const bool active = lane < nv;
-        const uint64_t v = v_lo + lane;
-        uint64_t o_lo = sbase, o_hi = sbase;
-        if (active) {
-            o_lo = offsets[v];
-            o_hi = offsets[v + 1];
-        }
-        const uint32_t vb = (uint32_t)(o_lo - sbase), len = (uint32_t)(o_hi - o_lo);
-        uint32_t nrec = 0;
-        const WalkOut wo = fast_walk(S, active, vb, len, recs, ECAP, nrec);
-        if (!__ballot(active && wo.fail) && nrec <= ECAP) {
-            const uint64_t n_ = active ? wo.n : 0;
-            const uint64_t incl = wave_incl_scan(n_);
-            const uint64_t agg = __shfl(incl, RR_WAVE - 1, RR_WAVE);
-            const uint64_t prefix = lookback(state, groups, tile, nwin, agg);
-            const uint64_t ebase = prefix + incl - n_;
-            const bool capok = ebase + n_ <= elem_cap;
-            const uint32_t type = active ? s8(S, vb) : 0xFF;
-            __attribute__((address_space(3))) uint32_t *R = (__attribute__((address_space(3))) uint32_t *)recs;
-            uint64_t pay = 0;
-            for (uint32_t r = 0; r < nrec; r += RR_WAVE) {
-                const uint32_t i = r + lane;
-                const uint32_t rec = i < nrec ? R[i] : 0u;
-                const int ow = (int)((rec >> 16) & 63);
-                const uint32_t otype = __shfl(type, ow, RR_WAVE), oenc = __shfl(wo.enc, ow, RR_WAVE);
-                const uint32_t ovb = __shfl(vb, ow, RR_WAVE), olen = __shfl(len, ow, RR_WAVE);
-                const uint64_t obase = __shfl(ebase, ow, RR_WAVE);
-                const int ook = __shfl((int)capok, ow, RR_WAVE);
-                if (i < nrec && ook) {
-                    uint4 w;
-                    const uint32_t k = rec >> 22;
-                    fast_emit(S, sbase, otype, oenc, ovb, olen, rec & 0xFFFF, k, w, pay);
-                    *reinterpret_cast<uint4 *>(elems + obase + k) = w;
+                for (int k = 0; k < 4; ++k) {
+                    const uint64_t cc = c + k * RR_WAVE;
+                    if (cc < cw1) __builtin_nontemporal_store(x[k], dst + cc);
+                    if (staged && cc >= cs0) lds[cc - cs0] = x[k];
                 }
             }
-            if (active) {
-                uint4 w;
-                w.x = type | (wo.enc << 8) | ((capok ? RR_OK : RR_E_CAPACITY) << 16);
-                w.y = s32(S, vb + 1) & RR_LRU_MASK;
-                w.z = wo.n;
-                w.w = (uint32_t)ebase;
-                reinterpret_cast<uint4 *>(values)[v] = w;
+            for (; c < ce; c += RR_WAVE) {
+                const u32x4 x = src[c];
+                if (c < cw1) __builtin_nontemporal_store(x, dst + c);
+                if (staged && c >= cs0) lds[c - cs0] = x;
             }
-            tile_stats(stats, tile, wave_sum(active && !capok ? 1 : 0), wave_sum(pay), agg);
-            done = true;
         }
-    }
-    if (!done) {
-        uint64_t bad, pay, agg;
-        if (staged)
-            decode_values<lds_cptr>((lds_cptr)stage, sbase, offsets, v_lo, v_hi, values, elems, elem_cap, state,
-                                    groups, tile, nwin, bad, pay, agg);
-        else
-            decode_values<const uint8_t *>(blob, 0, offsets, v_lo, v_hi, values, elems, elem_cap, state, groups, tile,
-                                           nwin, bad, pay, agg);
-        tile_stats(stats, tile, bad, pay, agg);
-    }
-    // the stage is rewritten by the next window: all lanes' LDS reads must be done
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+
+        uint64_t bad = 0, pay = 0;
+        for (uint64_t v0 = v_lo; v0 < v_hi; v0 += RR_WAVE) {
+            bool done = false;
+            if (staged) {
+                // fast path: unified walk -> element records -> lane-per-element emission
+                lds_cptr S = (lds_cptr)stage;
+                const bool active = v0 + lane < v_hi;
+                const uint64_t v = v0 + lane;
+                uint64_t o_lo = sbase, o_hi = sbase, eb = 0, r = 0;
+                if (active) {
+                    o_lo = offsets[v];
+                    o_hi = offsets[v + 1];
+                    eb = ebase[v];
+                    r = ebase[v + 1] - eb;
+                }
+                const uint32_t vb = (uint32_t)(o_lo - sbase), len = (uint32_t)(o_hi - o_lo);
+                uint32_t nrec = 0;
+                const WalkOut wo = fast_walk(S, active, vb, len, recs, ECAP, nrec);
+                if (!__ballot(active && (wo.fail || wo.n != r)) && nrec <= ECAP) {
+                    const bool capok = eb + r <= cap;
+                    const uint32_t type = active ? s8(S, vb) : 0xFF;
+                    __attribute__((address_space(3))) uint32_t *R = (__attribute__((address_space(3))) uint32_t *)recs;
+                    for (uint32_t q = 0; q < nrec; q += RR_WAVE) {
+                        const uint32_t i = q + lane;
+                        const uint32_t rec = i < nrec ? R[i] : 0u;
+                        const int ow = (int)((rec >> 16) & 63);
+                        const uint32_t otype = __shfl(type, ow, RR_WAVE), oenc = __shfl(wo.enc, ow, RR_WAVE);
+                        const uint32_t ovb = __shfl(vb, ow, RR_WAVE), olen = __shfl(len, ow, RR_WAVE);
+                        const uint64_t obase = __shfl(eb, ow, RR_WAVE);
+                        const int ook = __shfl((int)capok, ow, RR_WAVE);
+                        if (i < nrec && ook) {
+                            uint4 w;
+                            const uint32_t k = rec >> 22;
+                            fast_emit(S, sbase, otype, oenc, ovb, olen, rec & 0xFFFF, k, w, pay);
+                            *reinterpret_cast<uint4 *>(elems + obase + k) = w;
+                        }
+                    }
+                    if (active) {
+                        uint4 w;
+                        w.x = type | (wo.enc << 8) | ((capok ? RR_OK : RR_E_CAPACITY) << 16);
+                        w.y = s32(S, vb + 1) & RR_LRU_MASK;
+                        w.z = wo.n;
+                        w.w = (uint32_t)eb;
+                        reinterpret_cast<uint4 *>(values)[v] = w;
+                        bad += capok ? 0 : 1;
+                    }
+                    done = true;
+                }
+            }
+            if (!done) {
+                if (staged)
+                    exact_chunk<lds_cptr>((lds_cptr)stage, sbase, offsets, ebase, v0, v_hi, values, elems, cap, bad, pay);
+                else
+                    exact_chunk<const uint8_t *>(blob, 0, offsets, ebase, v0, v_hi, values, elems, cap, bad, pay);
+            }
+            // records and stage are rewritten by the next chunk / window
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_wave_barrier();
+        }
+        tile_stats(stats, tile, wave_sum(bad), wave_sum(pay), 0);
     }
 }
 
@@ -819,16 +902,13 @@ static uint32_t resident_grid(K kernel, int block) {
 
 extern "C" uint64_t rr_decode_windows(uint64_t data_cap) { return data_cap / DEC_WIN + 1; }
 
-// Scratch words a decode of a data_cap-byte buffer needs: header, one look-back word and
-// three stats words per window, first_val (u32) for every window + sentinel.
-extern "C" uint64_t rr_decode_scratch_words(uint64_t data_cap) {
-    uint64_t nwin = rr_decode_windows(data_cap);
-    return RR_SCRATCH_HDR + 4 * nwin + nwin / 64 + 1 + (nwin + 2) / 2 + 1;
-}
+static uint64_t scan_tiles(uint64_t n) { return (n + SCAN_TILE - 1) / SCAN_TILE; }
 
-extern "C" uint64_t rr_encode_scratch_words(uint64_t n) {
-    uint64_t t = (n + TILE - 1) / TILE;
-    return RR_SCRATCH_HDR + 4 * t + t / 64 + 2;
+// Decode scratch (uint64 words): [HDR] [scan: ticket, look-back state + groups]
+// [counts -> elem_base, n+1] [window stats, 3 per window] [first_val u32, nwin+1].
+extern "C" uint64_t rr_decode_scratch_words(uint64_t data_cap, uint64_t n) {
+    const uint64_t nwin = rr_decode_windows(data_cap), st = scan_tiles(n);
+    return RR_SCRATCH_HDR + 1 + st + st / 64 + 1 + (n + 1) + 3 * nwin + (nwin + 2) / 2 + 2;
 }
 
 extern "C" hipError_t rr_launch_decode(const uint8_t *blob, const uint64_t *offsets, uint64_t n, rr_value *values,
@@ -837,22 +917,28 @@ extern "C" hipError_t rr_launch_decode(const uint8_t *blob, const uint64_t *offs
     // The window grid is sized from data_cap (>= offsets[n], host-known without a sync);
     // windows past offsets[n] find no values and copy nothing.
     const uint32_t nwin = (uint32_t)rr_decode_windows(data_cap);
-    uint64_t *state = scratch + RR_SCRATCH_HDR;
-    const uint64_t ngroups = (nwin + LB_GROUP - 1) / LB_GROUP;
-    uint64_t *stats = state + nwin + ngroups;
+    const uint32_t st = (uint32_t)scan_tiles(n);
+    uint64_t *lb = scratch + RR_SCRATCH_HDR;
+    const uint64_t lb_words = 1 + st + (st + LB_GROUP - 1) / LB_GROUP;
+    uint64_t *counts = lb + lb_words;
+    uint64_t *stats = counts + n + 1;
     uint32_t *first_val = reinterpret_cast<uint32_t *>(stats + 3 * (uint64_t)nwin);
-    size_t zero = (RR_SCRATCH_HDR + (size_t)nwin + ngroups) * sizeof(uint64_t);
-    hipError_t e = hipMemsetAsync(scratch, 0, (zero + 15) & ~(size_t)15, stream);
+    hipError_t e = hipMemsetAsync(lb, 0, ((lb_words * 8) + 15) & ~(size_t)15, stream);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(plan_kernel, dim3((uint32_t)((n + 1 + 255) / 256)), dim3(256), 0, stream, offsets, n, first_val,
-                       nwin, DEC_WIN);
+    hipLaunchKernelGGL(count_kernel, dim3((uint32_t)((n + 1 + 255) / 256)), dim3(256), 0, stream, blob, offsets, n,
+                       first_val, nwin, DEC_WIN, counts);
+    if (st) hipLaunchKernelGGL(scan_kernel, dim3(st), dim3(256), 0, stream, counts, n, lb, st);
+    else {
+        e = hipMemsetAsync(counts, 0, sizeof(uint64_t), stream);
+        if (e != hipSuccess) return e;
+    }
     static uint32_t grid = 0;
     if (!grid) grid = resident_grid(DECODE_KERNEL, RR_WAVE);
     const uint32_t g = nwin < grid ? nwin : grid;
-    hipLaunchKernelGGL((DECODE_KERNEL), dim3(g), dim3(RR_WAVE), 0, stream, blob, offsets, n,
-                       first_val, nwin, values, elems, elem_cap, arena, scratch);
+    hipLaunchKernelGGL((DECODE_KERNEL), dim3(g), dim3(RR_WAVE), 0, stream, blob, offsets, n, first_val, nwin, counts,
+                       values, elems, elem_cap, arena, stats);
     e = hipGetLastError();
-    if (e == hipSuccess && totals) e = launch_finalize(stats, state, nwin, offsets, n, 0, totals, stream);
+    if (e == hipSuccess && totals) e = launch_finalize(stats, counts + n, nwin, offsets, n, 2, totals, stream);
     return e;
 }
 

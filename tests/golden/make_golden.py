@@ -168,13 +168,14 @@ def edge_blobs():
 def main():
     kats = []
     for k in KATS:
+        assert po.reserve(h(k["blob"])) == len(k["elems"])
         kats.append(dict(k, blob=h(k["blob"]).hex()))
     edges = []
     for name, blob in edge_blobs():
         v, es = po.decode_one(blob, 0)
         edges.append(dict(name=name, blob=blob.hex(),
                           value=dict(type=v["type"], enc=v["enc"], lru=v["lru"], status=v["status"],
-                                     n_elems=v["n_elems"]),
+                                     n_elems=v["n_elems"], reserve=po.reserve(blob)),
                           elems=[[e[0], e[1] & 0xFFFFFFFFFFFFFFFF, e[2], e[3]] for e in es]))
     doc = dict(generator="tests/golden/make_golden.py", kats=kats, edges=edges, string2ll=STRING2LL,
                ll2string=LL2STRING, ziplist_example=ZIPLIST_EXAMPLE, intset_encoding=INTSET_ENC)

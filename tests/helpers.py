@@ -43,6 +43,8 @@ def expected_flat(fixtures):
         for kind, data, ln, zenc in fx["elems"]:
             d = data + off if kind in (rr.K_STR, rr.K_ZLRAW) else data
             elems.append((d & 0xFFFFFFFFFFFFFFFF, ln, kind, zenc, 0))
+        if v.get("status", 0):   # a malformed value keeps its reserved slots, zero-filled
+            elems.extend([(0, 0, 0, 0, 0)] * v["reserve"])
         off += len(blob)
     return values, np.array(elems, dtype=rr.ELEM_DT)
 
