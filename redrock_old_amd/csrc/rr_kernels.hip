@@ -904,6 +904,11 @@ extern "C" uint64_t rr_decode_windows(uint64_t data_cap) { return data_cap / DEC
 
 static uint64_t scan_tiles(uint64_t n) { return (n + SCAN_TILE - 1) / SCAN_TILE; }
 
+extern "C" uint64_t rr_encode_scratch_words(uint64_t n) {
+    uint64_t t = (n + TILE - 1) / TILE;
+    return RR_SCRATCH_HDR + 4 * t + t / 64 + 2;
+}
+
 // Decode scratch (uint64 words): [HDR] [scan: ticket, look-back state + groups]
 // [counts -> elem_base, n+1] [window stats, 3 per window] [first_val u32, nwin+1].
 extern "C" uint64_t rr_decode_scratch_words(uint64_t data_cap, uint64_t n) {
