@@ -17,7 +17,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "librr_serdes.so")
+# RR_LIB selects an alternative in-tree build (e.g. the probe build librr_serdes_probe.so).
+LIB_PATH = os.path.join(_HERE, os.environ.get("RR_LIB", "librr_serdes.so"))
 
 # --- flat form dtypes (include/rr_format.h) ---------------------------------------------
 VALUE_DT = np.dtype([("type", "u1"), ("enc", "u1"), ("status", "<u2"), ("lru", "<u4"),

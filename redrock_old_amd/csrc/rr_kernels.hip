@@ -15,6 +15,7 @@
 //
 // No MFMA: this is byte/record work bounded by HBM.
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 
 #include "rr_decode_fast.h"
 #include "rr_device.h"
@@ -25,6 +26,16 @@ using namespace rr;
 namespace {
 
 constexpr uint32_t TILE = RR_WAVE;       // values per wave tile
+
+// Probe build (make PROBE=1 -> librr_serdes_probe.so): per-phase cycle and path counters
+// accumulated into scratch words [8, 40) (diagnostics only; the product build compiles them out).
+#ifdef RR_PROBE
+#define PROBE_ADD(P, I, V) do { if (lane_id() == 0) atomicAdd((unsigned long long *)&(P)[8 + (I)], (unsigned long long)(V)); } while (0)
+#define PROBE_T() __builtin_amdgcn_s_memtime()
+#else
+#define PROBE_ADD(P, I, V) do { } while (0)
+#define PROBE_T() 0ull
+#endif
 constexpr uint32_t WG = 256;             // 4 independent waves per workgroup
 
 struct Parsed {
@@ -505,18 +516,30 @@ __device__ __forceinline__ void exact_chunk(P base, uint64_t sbase, const uint64
     bad += status != RR_OK ? 1 : 0;
 }
 
-template <uint32_t WIN, uint32_t STAGE, uint32_t ECAP>
-__global__ __launch_bounds__(RR_WAVE) void decode_kernel(const uint8_t *__restrict__ blob,
-                                                         const uint64_t *__restrict__ offsets, uint64_t n,
-                                                         const uint32_t *__restrict__ first_val, uint32_t nwin,
-                                                         const uint64_t *__restrict__ ebase,
-                                                         rr_value *__restrict__ values, rr_elem *__restrict__ elems,
-                                                         uint64_t elem_cap, uint8_t *__restrict__ arena,
-                                                         uint64_t *__restrict__ stats) {
+// One workgroup of NW waves per window (persistent, grid-stride over windows).  All waves copy
+// the window to the arena and stage it (+ the tail of its last value, up to SLACK bytes) in
+// LDS; the window's values are then cut into chunks of 64 (one per lane), chunk j walked and
+// emitted by wave j % NW.  A walk that fills all 64 lanes amortises its ~max-elements steps
+// over 64 values; the window size is chosen so a typical window holds about 64 values.
+template <uint32_t NW, uint32_t WIN, uint32_t SLACK, uint32_t ECAPW>
+__global__ __launch_bounds__(NW * RR_WAVE) void decode_kernel(const uint8_t *__restrict__ blob,
+                                                              const uint64_t *__restrict__ offsets, uint64_t n,
+                                                              const uint32_t *__restrict__ first_val, uint32_t nwin,
+                                                              const uint64_t *__restrict__ ebase,
+                                                              rr_value *__restrict__ values,
+                                                              rr_elem *__restrict__ elems, uint64_t elem_cap,
+                                                              uint8_t *__restrict__ arena,
+                                                              uint64_t *__restrict__ stats, uint64_t *probe, int mode) {
+    constexpr uint32_t STAGE = WIN + SLACK;
     // +64: the fast path's aligned multi-dword reads may run past the staged bytes
     __shared__ __attribute__((aligned(16))) uint8_t stage[STAGE + 64];
-    __shared__ uint32_t recs[ECAP];
+    __shared__ uint32_t recs_all[NW][ECAPW];
+    __shared__ uint64_t red[NW][2];
+    (void)probe;
+    (void)mode;
     const uint32_t lane = lane_id();
+    const uint32_t wave = threadIdx.x / RR_WAVE;
+    lds_u32w recs = (lds_u32w)recs_all[wave];
     const uint64_t nbytes = offsets[n];
     const uint64_t cap = elem_cap < 0xFFFFFFFFull ? elem_cap : 0xFFFFFFFFull;   // elem_base is 32-bit
     for (uint32_t tile = blockIdx.x; tile < nwin; tile += gridDim.x) {
@@ -539,32 +562,34 @@ __global__ __launch_bounds__(RR_WAVE) void decode_kernel(const uint8_t *__restri
             const u32x4 *src = reinterpret_cast<const u32x4 *>(blob);
             u32x4 *dst = reinterpret_cast<u32x4 *>(arena);
             u32x4 *lds = reinterpret_cast<u32x4 *>(stage);
+            constexpr uint32_t T = NW * RR_WAVE;
             const uint64_t cw1 = W1 >> 4, cs0 = sbase >> 4;
-            uint64_t c = (W0 >> 4) + lane;
+            uint64_t c = (W0 >> 4) + threadIdx.x;
             const uint64_t ce = L1 >> 4;
-            for (; c + 3 * RR_WAVE < ce; c += 4 * RR_WAVE) {
+            for (; c + 3 * T < ce; c += 4 * T) {
                 u32x4 x[4];
 #pragma unroll
-                for (int k = 0; k < 4; ++k) x[k] = src[c + k * RR_WAVE];
+                for (int k = 0; k < 4; ++k) x[k] = src[c + k * T];
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
-                    const uint64_t cc = c + k * RR_WAVE;
+                    const uint64_t cc = c + k * T;
                     if (cc < cw1) __builtin_nontemporal_store(x[k], dst + cc);
                     if (staged && cc >= cs0) lds[cc - cs0] = x[k];
                 }
             }
-            for (; c < ce; c += RR_WAVE) {
+            for (; c < ce; c += T) {
                 const u32x4 x = src[c];
                 if (c < cw1) __builtin_nontemporal_store(x, dst + c);
                 if (staged && c >= cs0) lds[c - cs0] = x;
             }
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        __syncthreads();
 
         uint64_t bad = 0, pay = 0;
-        for (uint64_t v0 = v_lo; v0 < v_hi; v0 += RR_WAVE) {
+#ifdef RR_PROBE
+        if (mode == 1) { __syncthreads(); continue; }   // ablation: copy + stage only
+#endif
+        for (uint64_t v0 = v_lo + (uint64_t)wave * RR_WAVE; v0 < v_hi; v0 += NW * RR_WAVE) {
             bool done = false;
             if (staged) {
                 // fast path: unified walk -> element records -> lane-per-element emission
@@ -580,14 +605,21 @@ __global__ __launch_bounds__(RR_WAVE) void decode_kernel(const uint8_t *__restri
                 }
                 const uint32_t vb = (uint32_t)(o_lo - sbase), len = (uint32_t)(o_hi - o_lo);
                 uint32_t nrec = 0;
-                const WalkOut wo = fast_walk(S, active, vb, len, recs, ECAP, nrec);
-                if (!__ballot(active && (wo.fail || wo.n != r)) && nrec <= ECAP) {
+                const WalkOut wo = fast_walk(S, active, vb, len, recs, ECAPW, nrec);
+#ifdef RR_PROBE
+                if (mode == 2) { asm volatile("" ::"v"(wo.n), "v"(nrec)); continue; }   // ablation: no emission
+#endif
+                if (!__ballot(active && (wo.fail || wo.n != r)) && nrec <= ECAPW) {
                     const bool capok = eb + r <= cap;
-                    const uint32_t type = active ? s8(S, vb) : 0xFF;
-                    __attribute__((address_space(3))) uint32_t *R = (__attribute__((address_space(3))) uint32_t *)recs;
+                    uint32_t h0 = 0, h1 = 0;
+                    if (active) {
+                        h0 = s32(S, vb);
+                        h1 = s32(S, vb + 1);
+                    }
+                    const uint32_t type = active ? (h0 & 0xFF) : 0xFF;
                     for (uint32_t q = 0; q < nrec; q += RR_WAVE) {
                         const uint32_t i = q + lane;
-                        const uint32_t rec = i < nrec ? R[i] : 0u;
+                        const uint32_t rec = i < nrec ? recs[i] : 0u;
                         const int ow = (int)((rec >> 16) & 63);
                         const uint32_t otype = __shfl(type, ow, RR_WAVE), oenc = __shfl(wo.enc, ow, RR_WAVE);
                         const uint32_t ovb = __shfl(vb, ow, RR_WAVE), olen = __shfl(len, ow, RR_WAVE);
@@ -603,7 +635,7 @@ __global__ __launch_bounds__(RR_WAVE) void decode_kernel(const uint8_t *__restri
                     if (active) {
                         uint4 w;
                         w.x = type | (wo.enc << 8) | ((capok ? RR_OK : RR_E_CAPACITY) << 16);
-                        w.y = s32(S, vb + 1) & RR_LRU_MASK;
+                        w.y = h1 & RR_LRU_MASK;
                         w.z = wo.n;
                         w.w = (uint32_t)eb;
                         reinterpret_cast<uint4 *>(values)[v] = w;
@@ -618,11 +650,21 @@ __global__ __launch_bounds__(RR_WAVE) void decode_kernel(const uint8_t *__restri
                 else
                     exact_chunk<const uint8_t *>(blob, 0, offsets, ebase, v0, v_hi, values, elems, cap, bad, pay);
             }
-            // records and stage are rewritten by the next chunk / window
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            // this wave's records are rewritten by its next chunk
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
         }
-        tile_stats(stats, tile, wave_sum(bad), wave_sum(pay), 0);
+        bad = wave_sum(bad);
+        pay = wave_sum(pay);
+        if (lane == 0) { red[wave][0] = bad; red[wave][1] = pay; }
+        __syncthreads();   // also: the stage is rewritten by the next window
+        if (threadIdx.x == 0) {
+            uint64_t tb = 0, tp = 0;
+            for (uint32_t k = 0; k < NW; ++k) { tb += red[k][0]; tp += red[k][1]; }
+            stats[3 * (uint64_t)tile + 0] = tb;
+            stats[3 * (uint64_t)tile + 1] = tp;
+            stats[3 * (uint64_t)tile + 2] = 0;
+        }
     }
 }
 
@@ -882,20 +924,33 @@ __global__ __launch_bounds__(WG) void encode_kernel(const rr_value *__restrict__
 }  // namespace
 
 // ---------------------------------------------------------------------------------------- launch
-constexpr uint32_t DEC_WIN = 4096;
-constexpr uint32_t DEC_STAGE = 8192;
-constexpr uint32_t DEC_ECAP = 1024;
-#define DECODE_KERNEL decode_kernel<DEC_WIN, DEC_STAGE, DEC_ECAP>
+#ifndef RR_DEC_NW
+#define RR_DEC_NW 4
+#endif
+#ifndef RR_DEC_WIN
+#define RR_DEC_WIN 32768
+#endif
+#ifndef RR_DEC_SLACK
+#define RR_DEC_SLACK 4096
+#endif
+#ifndef RR_DEC_ECAPW
+#define RR_DEC_ECAPW 1024
+#endif
+constexpr uint32_t DEC_NW = RR_DEC_NW;
+constexpr uint32_t DEC_WIN = RR_DEC_WIN;
+constexpr uint32_t DEC_SLACK = RR_DEC_SLACK;
+constexpr uint32_t DEC_ECAPW = RR_DEC_ECAPW;
+#define DECODE_KERNEL decode_kernel<DEC_NW, DEC_WIN, DEC_SLACK, DEC_ECAPW>
 
 // Resident workgroup count for a persistent launch: occupancy query minus one block per CU
 // (the API over-reports by one for SGPR-heavy kernels, MI355X_MICROARCH.md §Residency).
 template <typename K>
-static uint32_t resident_grid(K kernel, int block) {
+static uint32_t resident_grid(K kernel, int block, bool margin = true) {
     int dev = 0, cus = 0, occ = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kernel, block, 0) != hipSuccess || occ < 1) occ = 1;
-    if (occ > 1) occ -= 1;
+    if (margin && occ > 1) occ -= 1;
     if (cus < 1) cus = 1;
     return (uint32_t)(cus * occ);
 }
@@ -938,10 +993,18 @@ extern "C" hipError_t rr_launch_decode(const uint8_t *blob, const uint64_t *offs
         if (e != hipSuccess) return e;
     }
     static uint32_t grid = 0;
-    if (!grid) grid = resident_grid(DECODE_KERNEL, RR_WAVE);
+    if (!grid) grid = resident_grid(DECODE_KERNEL, DEC_NW * RR_WAVE, false);   // no inter-window waits
     const uint32_t g = nwin < grid ? nwin : grid;
-    hipLaunchKernelGGL((DECODE_KERNEL), dim3(g), dim3(RR_WAVE), 0, stream, blob, offsets, n, first_val, nwin, counts,
-                       values, elems, elem_cap, arena, stats);
+#ifdef RR_PROBE
+    e = hipMemsetAsync(scratch, 0, RR_SCRATCH_HDR * sizeof(uint64_t), stream);
+    if (e != hipSuccess) return e;
+#endif
+    int mode = 0;
+#ifdef RR_PROBE
+    if (const char *m = getenv("RR_DECODE_MODE")) mode = atoi(m);
+#endif
+    hipLaunchKernelGGL((DECODE_KERNEL), dim3(g), dim3(DEC_NW * RR_WAVE), 0, stream, blob, offsets, n, first_val, nwin, counts,
+                       values, elems, elem_cap, arena, stats, scratch, mode);
     e = hipGetLastError();
     if (e == hipSuccess && totals) e = launch_finalize(stats, counts + n, nwin, offsets, n, 2, totals, stream);
     return e;
