@@ -17,7 +17,7 @@
 #include <hip/hip_runtime.h>
 #include <stdlib.h>
 
-#include "rr_decode_fast.h"
+#include "rr_decode_walk.h"
 #include "rr_device.h"
 #include "rr_kernels.h"
 
@@ -516,13 +516,12 @@ __device__ __forceinline__ void exact_chunk(P base, uint64_t sbase, const uint64
     bad += status != RR_OK ? 1 : 0;
 }
 
-// One workgroup of NW waves per window (persistent, grid-stride over windows).  All waves copy
-// the window to the arena and stage it (+ the tail of its last value, up to SLACK bytes) in
-// LDS; the window's values are then cut into chunks of 64 (one per lane), chunk j walked and
-// emitted by wave j % NW.  A walk that fills all 64 lanes amortises its ~max-elements steps
-// over 64 values; the window size is chosen so a typical window holds about 64 values.
-template <uint32_t NW, uint32_t WIN, uint32_t SLACK, uint32_t ECAPW>
-__global__ __launch_bounds__(NW * RR_WAVE) void decode_kernel(const uint8_t *__restrict__ blob,
+// Independent waves (NW per workgroup, no LDS, no barriers): each wave takes windows of WIN
+// bytes (grid-stride), copies the window to the arena with streaming dwordx4 loads/stores, then
+// walks + emits the values that start in it, 64 per chunk (rr_decode_walk.h), from the same
+// just-loaded bytes.  A chunk the fast walk rejects goes to the exact parser.
+template <uint32_t NW, uint32_t WIN>
+__global__ __launch_bounds__(NW * RR_WAVE) void decode_kernel(const uint8_t *__restrict__ blob, uint64_t data_cap,
                                                               const uint64_t *__restrict__ offsets, uint64_t n,
                                                               const uint32_t *__restrict__ first_val, uint32_t nwin,
                                                               const uint64_t *__restrict__ ebase,
@@ -530,139 +529,69 @@ __global__ __launch_bounds__(NW * RR_WAVE) void decode_kernel(const uint8_t *__r
                                                               rr_elem *__restrict__ elems, uint64_t elem_cap,
                                                               uint8_t *__restrict__ arena,
                                                               uint64_t *__restrict__ stats, uint64_t *probe, int mode) {
-    constexpr uint32_t STAGE = WIN + SLACK;
-    // +64: the fast path's aligned multi-dword reads may run past the staged bytes
-    __shared__ __attribute__((aligned(16))) uint8_t stage[STAGE + 64];
-    __shared__ uint32_t recs_all[NW][ECAPW];
-    __shared__ uint64_t red[NW][2];
     (void)probe;
     (void)mode;
     const uint32_t lane = lane_id();
-    const uint32_t wave = threadIdx.x / RR_WAVE;
-    lds_u32w recs = (lds_u32w)recs_all[wave];
+    const uint32_t gw = blockIdx.x * NW + threadIdx.x / RR_WAVE, nw = gridDim.x * NW;
     const uint64_t nbytes = offsets[n];
+    const uint64_t padded = (nbytes + 15) & ~15ull;
     const uint64_t cap = elem_cap < 0xFFFFFFFFull ? elem_cap : 0xFFFFFFFFull;   // elem_base is 32-bit
-    for (uint32_t tile = blockIdx.x; tile < nwin; tile += gridDim.x) {
-        const uint64_t v_lo = first_val[tile], v_hi = first_val[tile + 1];
+    for (uint32_t tile = gw; tile < nwin; tile += nw) {
         const uint64_t W0 = (uint64_t)tile * WIN;
-        const uint64_t padded = (nbytes + 15) & ~15ull;
         const uint64_t W1 = W0 + WIN < padded ? W0 + WIN : padded;
-        uint64_t S0 = W0, S1 = W0;
-        if (v_hi > v_lo) {
-            S0 = offsets[v_lo];
-            S1 = offsets[v_hi];
-        }
-        const uint64_t sbase = S0 & ~15ull;
-        const uint64_t send = (S1 + 15) & ~15ull;
-        const bool staged = send - sbase <= STAGE;
-        const uint64_t L1 = staged && send > W1 ? send : W1;
-
-        // 1. copy window -> arena, stage value bytes -> LDS (one load feeds both)
+        // 1. copy window -> arena
         {
             const u32x4 *src = reinterpret_cast<const u32x4 *>(blob);
             u32x4 *dst = reinterpret_cast<u32x4 *>(arena);
-            u32x4 *lds = reinterpret_cast<u32x4 *>(stage);
-            constexpr uint32_t T = NW * RR_WAVE;
-            const uint64_t cw1 = W1 >> 4, cs0 = sbase >> 4;
-            uint64_t c = (W0 >> 4) + threadIdx.x;
-            const uint64_t ce = L1 >> 4;
-            for (; c + 3 * T < ce; c += 4 * T) {
-                u32x4 x[4];
+            uint64_t c = (W0 >> 4) + lane;
+            const uint64_t ce = W1 >> 4;
+            for (; c + 7 * RR_WAVE < ce; c += 8 * RR_WAVE) {
+                u32x4 x[8];
 #pragma unroll
-                for (int k = 0; k < 4; ++k) x[k] = src[c + k * T];
+                for (int k = 0; k < 8; ++k) x[k] = src[c + k * RR_WAVE];
 #pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const uint64_t cc = c + k * T;
-                    if (cc < cw1) __builtin_nontemporal_store(x[k], dst + cc);
-                    if (staged && cc >= cs0) lds[cc - cs0] = x[k];
-                }
+                for (int k = 0; k < 8; ++k) __builtin_nontemporal_store(x[k], dst + c + k * RR_WAVE);
             }
-            for (; c < ce; c += T) {
-                const u32x4 x = src[c];
-                if (c < cw1) __builtin_nontemporal_store(x, dst + c);
-                if (staged && c >= cs0) lds[c - cs0] = x;
-            }
+            for (; c < ce; c += RR_WAVE) __builtin_nontemporal_store(src[c], dst + c);
         }
-        __syncthreads();
-
+#ifdef RR_PROBE
+        if (mode == 1) continue;   // ablation: copy only
+#endif
+        // 2. walk + emit the window's values
+        const uint64_t v_lo = first_val[tile], v_hi = first_val[tile + 1];
         uint64_t bad = 0, pay = 0;
-#ifdef RR_PROBE
-        if (mode == 1) { __syncthreads(); continue; }   // ablation: copy + stage only
-#endif
-        for (uint64_t v0 = v_lo + (uint64_t)wave * RR_WAVE; v0 < v_hi; v0 += NW * RR_WAVE) {
-            bool done = false;
-            if (staged) {
-                // fast path: unified walk -> element records -> lane-per-element emission
-                lds_cptr S = (lds_cptr)stage;
-                const bool active = v0 + lane < v_hi;
-                const uint64_t v = v0 + lane;
-                uint64_t o_lo = sbase, o_hi = sbase, eb = 0, r = 0;
+        for (uint64_t v0 = v_lo; v0 < v_hi; v0 += RR_WAVE) {
+            const uint64_t v = v0 + lane;
+            const bool active = v < v_hi;
+            uint64_t o_lo = 0, o_hi = 0, eb = 0, r = 0;
+            if (active) {
+                o_lo = offsets[v];
+                o_hi = offsets[v + 1];
+                eb = ebase[v];
+                r = ebase[v + 1] - eb;
+            }
+            const bool capok = eb + r <= cap;
+            const ChunkOut co = walk_value(blob, data_cap, active, o_lo, o_hi, elems, eb, r, capok);
+            if (!__ballot(active && (co.fail || co.n != r))) {
                 if (active) {
-                    o_lo = offsets[v];
-                    o_hi = offsets[v + 1];
-                    eb = ebase[v];
-                    r = ebase[v + 1] - eb;
+                    uint4 w;
+                    w.x = co.type | (co.enc << 8) | ((capok ? RR_OK : RR_E_CAPACITY) << 16);
+                    w.y = co.lru;
+                    w.z = co.n;
+                    w.w = (uint32_t)eb;
+                    reinterpret_cast<uint4 *>(values)[v] = w;
+                    bad += capok ? 0 : 1;
+                    pay += capok ? co.pay : 0;
                 }
-                const uint32_t vb = (uint32_t)(o_lo - sbase), len = (uint32_t)(o_hi - o_lo);
-                uint32_t nrec = 0;
-                const WalkOut wo = fast_walk(S, active, vb, len, recs, ECAPW, nrec);
-#ifdef RR_PROBE
-                if (mode == 2) { asm volatile("" ::"v"(wo.n), "v"(nrec)); continue; }   // ablation: no emission
-#endif
-                if (!__ballot(active && (wo.fail || wo.n != r)) && nrec <= ECAPW) {
-                    const bool capok = eb + r <= cap;
-                    uint32_t h0 = 0, h1 = 0;
-                    if (active) {
-                        h0 = s32(S, vb);
-                        h1 = s32(S, vb + 1);
-                    }
-                    const uint32_t type = active ? (h0 & 0xFF) : 0xFF;
-                    for (uint32_t q = 0; q < nrec; q += RR_WAVE) {
-                        const uint32_t i = q + lane;
-                        const uint32_t rec = i < nrec ? recs[i] : 0u;
-                        const int ow = (int)((rec >> 16) & 63);
-                        const uint32_t otype = __shfl(type, ow, RR_WAVE), oenc = __shfl(wo.enc, ow, RR_WAVE);
-                        const uint32_t ovb = __shfl(vb, ow, RR_WAVE), olen = __shfl(len, ow, RR_WAVE);
-                        const uint64_t obase = __shfl(eb, ow, RR_WAVE);
-                        const int ook = __shfl((int)capok, ow, RR_WAVE);
-                        if (i < nrec && ook) {
-                            uint4 w;
-                            const uint32_t k = rec >> 22;
-                            fast_emit(S, sbase, otype, oenc, ovb, olen, rec & 0xFFFF, k, w, pay);
-                            *reinterpret_cast<uint4 *>(elems + obase + k) = w;
-                        }
-                    }
-                    if (active) {
-                        uint4 w;
-                        w.x = type | (wo.enc << 8) | ((capok ? RR_OK : RR_E_CAPACITY) << 16);
-                        w.y = h1 & RR_LRU_MASK;
-                        w.z = wo.n;
-                        w.w = (uint32_t)eb;
-                        reinterpret_cast<uint4 *>(values)[v] = w;
-                        bad += capok ? 0 : 1;
-                    }
-                    done = true;
-                }
+            } else {
+                exact_chunk<const uint8_t *>(blob, 0, offsets, ebase, v0, v_hi, values, elems, cap, bad, pay);
             }
-            if (!done) {
-                if (staged)
-                    exact_chunk<lds_cptr>((lds_cptr)stage, sbase, offsets, ebase, v0, v_hi, values, elems, cap, bad, pay);
-                else
-                    exact_chunk<const uint8_t *>(blob, 0, offsets, ebase, v0, v_hi, values, elems, cap, bad, pay);
-            }
-            // this wave's records are rewritten by its next chunk
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
         }
         bad = wave_sum(bad);
         pay = wave_sum(pay);
-        if (lane == 0) { red[wave][0] = bad; red[wave][1] = pay; }
-        __syncthreads();   // also: the stage is rewritten by the next window
-        if (threadIdx.x == 0) {
-            uint64_t tb = 0, tp = 0;
-            for (uint32_t k = 0; k < NW; ++k) { tb += red[k][0]; tp += red[k][1]; }
-            stats[3 * (uint64_t)tile + 0] = tb;
-            stats[3 * (uint64_t)tile + 1] = tp;
+        if (lane == 0) {
+            stats[3 * (uint64_t)tile + 0] = bad;
+            stats[3 * (uint64_t)tile + 1] = pay;
             stats[3 * (uint64_t)tile + 2] = 0;
         }
     }
@@ -930,17 +859,9 @@ __global__ __launch_bounds__(WG) void encode_kernel(const rr_value *__restrict__
 #ifndef RR_DEC_WIN
 #define RR_DEC_WIN 32768
 #endif
-#ifndef RR_DEC_SLACK
-#define RR_DEC_SLACK 4096
-#endif
-#ifndef RR_DEC_ECAPW
-#define RR_DEC_ECAPW 1024
-#endif
 constexpr uint32_t DEC_NW = RR_DEC_NW;
 constexpr uint32_t DEC_WIN = RR_DEC_WIN;
-constexpr uint32_t DEC_SLACK = RR_DEC_SLACK;
-constexpr uint32_t DEC_ECAPW = RR_DEC_ECAPW;
-#define DECODE_KERNEL decode_kernel<DEC_NW, DEC_WIN, DEC_SLACK, DEC_ECAPW>
+#define DECODE_KERNEL decode_kernel<DEC_NW, DEC_WIN>
 
 // Resident workgroup count for a persistent launch: occupancy query minus one block per CU
 // (the API over-reports by one for SGPR-heavy kernels, MI355X_MICROARCH.md §Residency).
@@ -994,7 +915,8 @@ extern "C" hipError_t rr_launch_decode(const uint8_t *blob, const uint64_t *offs
     }
     static uint32_t grid = 0;
     if (!grid) grid = resident_grid(DECODE_KERNEL, DEC_NW * RR_WAVE, false);   // no inter-window waits
-    const uint32_t g = nwin < grid ? nwin : grid;
+    const uint32_t gneed = (nwin + DEC_NW - 1) / DEC_NW;
+    const uint32_t g = gneed < grid ? gneed : grid;
 #ifdef RR_PROBE
     e = hipMemsetAsync(scratch, 0, RR_SCRATCH_HDR * sizeof(uint64_t), stream);
     if (e != hipSuccess) return e;
@@ -1003,8 +925,8 @@ extern "C" hipError_t rr_launch_decode(const uint8_t *blob, const uint64_t *offs
 #ifdef RR_PROBE
     if (const char *m = getenv("RR_DECODE_MODE")) mode = atoi(m);
 #endif
-    hipLaunchKernelGGL((DECODE_KERNEL), dim3(g), dim3(DEC_NW * RR_WAVE), 0, stream, blob, offsets, n, first_val, nwin, counts,
-                       values, elems, elem_cap, arena, stats, scratch, mode);
+    hipLaunchKernelGGL((DECODE_KERNEL), dim3(g), dim3(DEC_NW * RR_WAVE), 0, stream, blob, data_cap, offsets, n, first_val,
+                       nwin, counts, values, elems, elem_cap, arena, stats, scratch, mode);
     e = hipGetLastError();
     if (e == hipSuccess && totals) e = launch_finalize(stats, counts + n, nwin, offsets, n, 2, totals, stream);
     return e;
