@@ -103,18 +103,18 @@ struct WalkOut {
 
 constexpr uint32_t REC_KMAX = 1024;
 
-__device__ __forceinline__ void rec_append(lds_u32w recs, uint32_t ecap, uint32_t &nrec, bool emit, uint32_t rec) {
-    const uint64_t m = __ballot(emit);
-    const uint32_t idx = nrec + (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
-    if (emit && idx < ecap) recs[idx] = rec;
-    nrec += (uint32_t)__builtin_popcountll(m);
+// Records are written at their DESTINATION slot: value's slot base rb (= its elem_base minus
+// the chunk's) + element index.  Emission then walks the slots in order, so consecutive lanes
+// store consecutive descriptors (coalesced) and a 64-slot round spans only a few values.
+// Slots past the value's reservation r are not written (the value then fails anyway).
+__device__ __forceinline__ void rec_put(lds_u32w recs, bool emit, uint32_t rb, uint32_t k, uint32_t r, uint32_t rec) {
+    if (emit && k < r) recs[rb + k] = rec;
 }
 
-// Unified walker.  vb/len: the lane's value in the stage; recs/ecap: this wave's record list;
-// nrec: wave-uniform record count (updated).  Inactive lanes pass active = false.
+// Unified walker.  vb/len: the lane's value in the stage; recs: the wave's slot table; rb/r:
+// the lane's slot base and reservation.  Inactive lanes pass active = false.
 __device__ __forceinline__ WalkOut fast_walk(lds_cptr S, bool active, uint32_t vb, uint32_t len, lds_u32w recs,
-                                             uint32_t ecap, uint32_t &nrec) {
+                                             uint32_t rb, uint32_t r) {
     const uint32_t lane = lane_id();
     WalkOut o{0, 0, false};
     uint32_t type = 0xFF, p = 0, end = vb + len, zl0 = 0, zlL = 0, prev_raw = 0, last = 0, nint = 0;
@@ -183,7 +183,7 @@ __device__ __forceinline__ WalkOut fast_walk(lds_cptr S, bool active, uint32_t v
                 o.fail = true;
         }
     }
-    rec_append(recs, ecap, nrec, pre, prepos | (lane << 16));
+    rec_put(recs, pre, rb, 0, r, prepos | (lane << 16));
     while (__ballot(walking)) {
         bool emit = false;
         const uint32_t rpos = p, k = o.n;
@@ -276,7 +276,7 @@ __device__ __forceinline__ WalkOut fast_walk(lds_cptr S, bool active, uint32_t v
             if (o.fail) walking = false;
             if (emit && k >= REC_KMAX) { o.fail = true; walking = false; emit = false; }
         }
-        rec_append(recs, ecap, nrec, emit, rpos | (lane << 16) | (k << 22));
+        rec_put(recs, emit, rb, k, r, rpos | (lane << 16) | (k << 22));
     }
     // end-of-value checks (rock_serdes.c counts; ziplist header fields)
     if (active && !o.fail) {
@@ -344,19 +344,26 @@ __device__ __forceinline__ void fast_emit(lds_cptr S, uint64_t sbase, uint32_t t
         default:   // ziplists
             if (k == 0) { data = sbase + pos; elen = len - 13; kind = RR_K_ZLRAW; pay += elen; }
             else {
-                const uint32_t qo = (b[0] & 0xFF) < 254 ? 1u : 5u;     // enc offset from pos
-                const uint32_t e = byte_at(b, qo);
+                // entry header: prevlen 1 byte (enc at +1) or 5 bytes (enc at +5); every field is
+                // extracted with static byte offsets from the 32 bytes read (no indexed arrays)
+                const bool big = (b[0] & 0xFF) >= 254;
+                const uint32_t qo = big ? 5u : 1u;
+                const uint32_t e = big ? ((b[1] >> 8) & 0xFF) : ((b[0] >> 8) & 0xFF);
+                const uint32_t x1 = big ? ((b[1] >> 16) & 0xFF) : ((b[0] >> 16) & 0xFF);   // byte qo+1
+                const uint32_t lo = big ? __builtin_amdgcn_alignbyte(b[2], b[1], 2)
+                                        : __builtin_amdgcn_alignbyte(b[1], b[0], 2);        // bytes qo+1..qo+4
+                const uint32_t hi = big ? __builtin_amdgcn_alignbyte(b[3], b[2], 2)
+                                        : __builtin_amdgcn_alignbyte(b[2], b[1], 2);        // bytes qo+5..qo+8
                 if (e < 0xC0) {
                     const uint32_t cls = e & 0xC0;
                     uint32_t ls, sl;
                     if (cls == 0x00) { ls = 1; sl = e & 0x3F; }
-                    else if (cls == 0x40) { ls = 2; sl = ((e & 0x3F) << 8) | byte_at(b, qo + 1); }
-                    else { ls = 5; sl = __builtin_bswap32(dword_at(b, qo + 1)); }
+                    else if (cls == 0x40) { ls = 2; sl = ((e & 0x3F) << 8) | x1; }
+                    else { ls = 5; sl = __builtin_bswap32(lo); }
                     data = sbase + pos + qo + ls;
                     elen = sl;
                     zenc = cls;
                 } else {
-                    const uint32_t lo = dword_at(b, qo + 1), hi = dword_at(b, qo + 5);
                     int64_t v;
                     if (e >= 0xF1 && e <= 0xFD) v = (int64_t)(e & 0x0F) - 1;
                     else if (e == 0xFE) v = (int8_t)(lo & 0xFF);

@@ -17,7 +17,7 @@
 #include <hip/hip_runtime.h>
 #include <stdlib.h>
 
-#include "rr_decode_walk.h"
+#include "rr_decode_fast.h"
 #include "rr_device.h"
 #include "rr_kernels.h"
 
@@ -516,76 +516,146 @@ __device__ __forceinline__ void exact_chunk(P base, uint64_t sbase, const uint64
     bad += status != RR_OK ? 1 : 0;
 }
 
-// Independent waves (NW per workgroup, no LDS, no barriers): each wave takes windows of WIN
-// bytes (grid-stride), copies the window to the arena with streaming dwordx4 loads/stores, then
-// walks + emits the values that start in it, 64 per chunk (rr_decode_walk.h), from the same
-// just-loaded bytes.  A chunk the fast walk rejects goes to the exact parser.
-template <uint32_t NW, uint32_t WIN>
-__global__ __launch_bounds__(NW * RR_WAVE) void decode_kernel(const uint8_t *__restrict__ blob, uint64_t data_cap,
-                                                              const uint64_t *__restrict__ offsets, uint64_t n,
-                                                              const uint32_t *__restrict__ first_val, uint32_t nwin,
-                                                              const uint64_t *__restrict__ ebase,
-                                                              rr_value *__restrict__ values,
-                                                              rr_elem *__restrict__ elems, uint64_t elem_cap,
-                                                              uint8_t *__restrict__ arena,
-                                                              uint64_t *__restrict__ stats, uint64_t *probe, int mode) {
+// One wave per workgroup, each with its own LDS window (no sharing, no barriers): the wave
+// copies its window to the arena and stages it (+ the tail of its last value, up to SLACK
+// bytes), then per chunk of 64 values: walk from LDS (lane = value, rr_decode_fast.h) writing
+// element records into a table indexed by destination slot, then emit lane-per-slot (coalesced
+// descriptor stores).  Chunks the fast path cannot take (malformed values, slot table
+// overflow, unstaged windows) go to the exact parser.
+template <uint32_t WIN, uint32_t SLACK, uint32_t ECAP>
+__global__ __launch_bounds__(RR_WAVE) void decode_kernel(const uint8_t *__restrict__ blob, uint64_t data_cap,
+                                                         const uint64_t *__restrict__ offsets, uint64_t n,
+                                                         const uint32_t *__restrict__ first_val, uint32_t nwin,
+                                                         const uint64_t *__restrict__ ebase,
+                                                         rr_value *__restrict__ values, rr_elem *__restrict__ elems,
+                                                         uint64_t elem_cap, uint8_t *__restrict__ arena,
+                                                         uint64_t *__restrict__ stats, uint64_t *probe, int mode) {
+    constexpr uint32_t STAGE = WIN + SLACK;
+    // +64: the fast path's aligned multi-dword reads may run past the staged bytes
+    __shared__ __attribute__((aligned(16))) uint8_t stage[STAGE + 64];
+    __shared__ uint32_t slot_tab[ECAP];
     (void)probe;
     (void)mode;
+    (void)data_cap;
     const uint32_t lane = lane_id();
-    const uint32_t gw = blockIdx.x * NW + threadIdx.x / RR_WAVE, nw = gridDim.x * NW;
+    lds_u32w recs = (lds_u32w)slot_tab;
     const uint64_t nbytes = offsets[n];
     const uint64_t padded = (nbytes + 15) & ~15ull;
     const uint64_t cap = elem_cap < 0xFFFFFFFFull ? elem_cap : 0xFFFFFFFFull;   // elem_base is 32-bit
-    for (uint32_t tile = gw; tile < nwin; tile += nw) {
+    for (uint32_t tile = blockIdx.x; tile < nwin; tile += gridDim.x) {
+        const uint64_t v_lo = first_val[tile], v_hi = first_val[tile + 1];
         const uint64_t W0 = (uint64_t)tile * WIN;
         const uint64_t W1 = W0 + WIN < padded ? W0 + WIN : padded;
-        // 1. copy window -> arena
+        uint64_t S0 = W0, S1 = W0;
+        if (v_hi > v_lo) {
+            S0 = offsets[v_lo];
+            S1 = offsets[v_hi];
+        }
+        const uint64_t sbase = S0 & ~15ull;
+        const uint64_t send = (S1 + 15) & ~15ull;
+        const bool staged = send - sbase <= STAGE;
+        const uint64_t L1 = staged && send > W1 ? send : W1;
+
+        // 1. copy window -> arena, stage value bytes -> LDS (one load feeds both)
         {
             const u32x4 *src = reinterpret_cast<const u32x4 *>(blob);
             u32x4 *dst = reinterpret_cast<u32x4 *>(arena);
+            u32x4 *lds = reinterpret_cast<u32x4 *>(stage);
+            const uint64_t cw1 = W1 >> 4, cs0 = sbase >> 4;
             uint64_t c = (W0 >> 4) + lane;
-            const uint64_t ce = W1 >> 4;
+            const uint64_t ce = L1 >> 4;
             for (; c + 7 * RR_WAVE < ce; c += 8 * RR_WAVE) {
                 u32x4 x[8];
 #pragma unroll
                 for (int k = 0; k < 8; ++k) x[k] = src[c + k * RR_WAVE];
 #pragma unroll
-                for (int k = 0; k < 8; ++k) __builtin_nontemporal_store(x[k], dst + c + k * RR_WAVE);
+                for (int k = 0; k < 8; ++k) {
+                    const uint64_t cc = c + k * RR_WAVE;
+                    if (cc < cw1) __builtin_nontemporal_store(x[k], dst + cc);
+                    if (staged && cc >= cs0) lds[cc - cs0] = x[k];
+                }
             }
-            for (; c < ce; c += RR_WAVE) __builtin_nontemporal_store(src[c], dst + c);
+            for (; c < ce; c += RR_WAVE) {
+                const u32x4 x = src[c];
+                if (c < cw1) __builtin_nontemporal_store(x, dst + c);
+                if (staged && c >= cs0) lds[c - cs0] = x;
+            }
         }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #ifdef RR_PROBE
-        if (mode == 1) continue;   // ablation: copy only
+        if (mode == 1) continue;   // ablation: copy + stage only
 #endif
-        // 2. walk + emit the window's values
-        const uint64_t v_lo = first_val[tile], v_hi = first_val[tile + 1];
         uint64_t bad = 0, pay = 0;
         for (uint64_t v0 = v_lo; v0 < v_hi; v0 += RR_WAVE) {
-            const uint64_t v = v0 + lane;
-            const bool active = v < v_hi;
-            uint64_t o_lo = 0, o_hi = 0, eb = 0, r = 0;
-            if (active) {
-                o_lo = offsets[v];
-                o_hi = offsets[v + 1];
-                eb = ebase[v];
-                r = ebase[v + 1] - eb;
-            }
-            const bool capok = eb + r <= cap;
-            const ChunkOut co = walk_value(blob, data_cap, active, o_lo, o_hi, elems, eb, r, capok);
-            if (!__ballot(active && (co.fail || co.n != r))) {
+            const uint64_t v1 = v0 + RR_WAVE < v_hi ? v0 + RR_WAVE : v_hi;
+            const uint64_t cb = ebase[v0], nslots = ebase[v1] - cb;
+            bool done = false;
+            if (staged && nslots <= ECAP) {
+                lds_cptr S = (lds_cptr)stage;
+                const bool active = v0 + lane < v1;
+                const uint64_t v = v0 + lane;
+                uint64_t o_lo = sbase, o_hi = sbase, eb = cb, r = 0;
                 if (active) {
-                    uint4 w;
-                    w.x = co.type | (co.enc << 8) | ((capok ? RR_OK : RR_E_CAPACITY) << 16);
-                    w.y = co.lru;
-                    w.z = co.n;
-                    w.w = (uint32_t)eb;
-                    reinterpret_cast<uint4 *>(values)[v] = w;
-                    bad += capok ? 0 : 1;
-                    pay += capok ? co.pay : 0;
+                    o_lo = offsets[v];
+                    o_hi = offsets[v + 1];
+                    eb = ebase[v];
+                    r = ebase[v + 1] - eb;
                 }
-            } else {
-                exact_chunk<const uint8_t *>(blob, 0, offsets, ebase, v0, v_hi, values, elems, cap, bad, pay);
+                const uint32_t vb = (uint32_t)(o_lo - sbase), len = (uint32_t)(o_hi - o_lo);
+                const WalkOut wo = fast_walk(S, active, vb, len, recs, (uint32_t)(eb - cb), (uint32_t)r);
+#ifdef RR_PROBE
+                if (mode == 2) { asm volatile("" ::"v"(wo.n)); continue; }   // ablation: no emission
+#endif
+                if (!__ballot(active && (wo.fail || wo.n != r))) {
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    const bool capok = eb + r <= cap;
+                    uint32_t h0 = 0, h1 = 0;
+                    if (active) {
+                        h0 = s32(S, vb);
+                        h1 = s32(S, vb + 1);
+                    }
+                    const uint32_t type = active ? (h0 & 0xFF) : 0xFF;
+                    const bool chunk_ok = cb + nslots <= cap;   // every value of the chunk fits
+                    // lane-per-slot emission: slot j holds the record of descriptor cb + j
+                    for (uint32_t q = 0; q < (uint32_t)nslots; q += RR_WAVE) {
+                        const uint32_t j = q + lane;
+                        const uint32_t rec = j < nslots ? recs[j] : 0u;
+                        const int ow = (int)((rec >> 16) & 63);
+                        const uint32_t otype = __shfl(type, ow, RR_WAVE), oenc = __shfl(wo.enc, ow, RR_WAVE);
+                        const uint32_t ovb = __shfl(vb, ow, RR_WAVE), olen = __shfl(len, ow, RR_WAVE);
+                        const int ook = chunk_ok ? 1 : __shfl((int)capok, ow, RR_WAVE);
+                        if (j < nslots && ook) {
+                            uint4 w;
+                            fast_emit(S, sbase, otype, oenc, ovb, olen, rec & 0xFFFF, rec >> 22, w, pay);
+                            *reinterpret_cast<uint4 *>(elems + cb + j) = w;
+                        }
+                    }
+                    if (active) {
+                        uint4 w;
+                        w.x = type | (wo.enc << 8) | ((capok ? RR_OK : RR_E_CAPACITY) << 16);
+                        w.y = h1 & RR_LRU_MASK;
+                        w.z = wo.n;
+                        w.w = (uint32_t)eb;
+                        reinterpret_cast<uint4 *>(values)[v] = w;
+                        bad += capok ? 0 : 1;
+                    }
+                    done = true;
+                }
             }
+            if (!done) {
+                if (staged)
+                    exact_chunk<lds_cptr>((lds_cptr)stage, sbase, offsets, ebase, v0, v1, values, elems, cap, bad, pay);
+                else
+                    exact_chunk<const uint8_t *>(blob, 0, offsets, ebase, v0, v1, values, elems, cap, bad, pay);
+            }
+            // the slot table is rewritten by the next chunk
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
         bad = wave_sum(bad);
         pay = wave_sum(pay);
@@ -594,6 +664,9 @@ __global__ __launch_bounds__(NW * RR_WAVE) void decode_kernel(const uint8_t *__r
             stats[3 * (uint64_t)tile + 1] = pay;
             stats[3 * (uint64_t)tile + 2] = 0;
         }
+        // the stage is rewritten by the next window
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
     }
 }
 
@@ -853,15 +926,18 @@ __global__ __launch_bounds__(WG) void encode_kernel(const rr_value *__restrict__
 }  // namespace
 
 // ---------------------------------------------------------------------------------------- launch
-#ifndef RR_DEC_NW
-#define RR_DEC_NW 4
-#endif
 #ifndef RR_DEC_WIN
-#define RR_DEC_WIN 32768
+#define RR_DEC_WIN 16384
 #endif
-constexpr uint32_t DEC_NW = RR_DEC_NW;
+#ifndef RR_DEC_SLACK
+#define RR_DEC_SLACK 4096
+#endif
+#ifndef RR_DEC_ECAP
+#define RR_DEC_ECAP 1024
+#endif
+constexpr uint32_t DEC_NW = 1;
 constexpr uint32_t DEC_WIN = RR_DEC_WIN;
-#define DECODE_KERNEL decode_kernel<DEC_NW, DEC_WIN>
+#define DECODE_KERNEL decode_kernel<DEC_WIN, RR_DEC_SLACK, RR_DEC_ECAP>
 
 // Resident workgroup count for a persistent launch: occupancy query minus one block per CU
 // (the API over-reports by one for SGPR-heavy kernels, MI355X_MICROARCH.md §Residency).
