@@ -111,191 +111,153 @@ __device__ __forceinline__ void rec_put(lds_u32w recs, bool emit, uint32_t rb, u
     if (emit && k < r) recs[rb + k] = rec;
 }
 
+// Walk classes (one per lane, fixed for the walk)
+constexpr uint32_t WC_NONE = 0, WC_LIST = 1, WC_HT = 2, WC_SL = 3, WC_ZL = 4, WC_IS = 5;
+
 // Unified walker.  vb/len: the lane's value in the stage; recs: the wave's slot table; rb/r:
 // the lane's slot base and reservation.  Inactive lanes pass active = false.
+//
+// The step is straight-line select arithmetic: every class's element size and validity are
+// computed from the same 12 bytes and the lane's class picks its own (v_cndmask), so a wave
+// whose lanes hold different types runs ~one step's worth of instructions per step instead of
+// the sum of every type's branches (a switch here compiled to ~870 instructions per step).
 __device__ __forceinline__ WalkOut fast_walk(lds_cptr S, bool active, uint32_t vb, uint32_t len, lds_u32w recs,
                                              uint32_t rb, uint32_t r) {
     const uint32_t lane = lane_id();
     WalkOut o{0, 0, false};
-    uint32_t type = 0xFF, p = 0, end = vb + len, zl0 = 0, zlL = 0, prev_raw = 0, last = 0, nint = 0;
+    uint32_t cls = WC_NONE, p = vb, end = vb + len, zl0 = 0, zend = 0, prev_raw = 0, last = 0, nint = 0, w = 0;
     uint64_t cnt = 0;
-    bool walking = false, pre = false;
+    bool pre = false;
     uint32_t prepos = 0;
     if (active) {
         uint32_t h[4];   // header: type, lru, enc / count fields (bytes vb .. vb+15)
         s_read<4>(S, vb, h);
-        type = h[0] & 0xFF;
-        if (len < 5) { o.fail = true; type = 0xFF; }
-        else switch (type) {
-            case RR_TYPE_STRING: {
-                if (len < 6) { o.fail = true; break; }
-                const uint32_t enc = (h[1] >> 8) & 0xFF;
-                o.enc = enc;
-                if (enc == RR_ENC_INT) o.fail = len != 14;
-                else if (enc == RR_ENC_RAW) o.fail = false;
-                else if (enc == RR_ENC_EMBSTR) o.fail = len - 6 > RR_EMBSTR_SIZE_LIMIT;
-                else o.fail = true;
-                if (!o.fail) { pre = true; prepos = vb; o.n = 1; }
-                break;
-            }
-            case RR_TYPE_SET_INTSET: {
-                if (len < 13) { o.fail = true; break; }
-                const uint32_t w = __builtin_amdgcn_alignbyte(h[2], h[1], 1);
-                const uint32_t c = __builtin_amdgcn_alignbyte(h[3], h[2], 1);
-                if ((w != 2 && w != 4 && w != 8) || (uint64_t)(len - 13) != (uint64_t)w * c) { o.fail = true; break; }
-                o.enc = w;
-                nint = c;
-                p = vb + 13;
-                walking = true;
-                break;
-            }
-            case RR_TYPE_LIST_QUICKLIST:
-                p = vb + 5;
-                walking = true;
-                break;
-            case RR_TYPE_SET_HT:
-            case RR_TYPE_HASH_HT:
-            case RR_TYPE_ZSET_SKIPLIST:
-                if (len < 13) { o.fail = true; break; }
-                cnt = (uint64_t)__builtin_amdgcn_alignbyte(h[2], h[1], 1) |
-                      ((uint64_t)__builtin_amdgcn_alignbyte(h[3], h[2], 1) << 32);
-                p = vb + 13;
-                walking = true;
-                break;
-            case RR_TYPE_HASH_ZIPLIST:
-            case RR_TYPE_ZSET_ZIPLIST: {
-                if (len < 13) { o.fail = true; break; }
-                const uint64_t L = (uint64_t)__builtin_amdgcn_alignbyte(h[2], h[1], 1) |
-                                   ((uint64_t)__builtin_amdgcn_alignbyte(h[3], h[2], 1) << 32);
-                if ((uint64_t)(len - 13) != L || L < 11) { o.fail = true; break; }
-                zl0 = vb + 13;
-                zlL = len - 13;
-                if (s32(S, zl0) != zlL) { o.fail = true; break; }
-                pre = true;
-                prepos = zl0;
-                o.n = 1;
-                p = zl0 + 10;
-                last = zl0 + 10;
-                walking = true;
-                break;
-            }
-            default:
-                o.fail = true;
+        const uint32_t type = len >= 5 ? (h[0] & 0xFF) : 0xFFu;
+        const uint32_t f5 = __builtin_amdgcn_alignbyte(h[2], h[1], 1);   // bytes 5..8
+        const uint32_t f9 = __builtin_amdgcn_alignbyte(h[3], h[2], 1);   // bytes 9..12
+        const uint64_t u5 = (uint64_t)f5 | ((uint64_t)f9 << 32);
+        if (type == RR_TYPE_STRING) {
+            const uint32_t enc = f5 & 0xFF;
+            o.enc = enc;
+            o.fail = len < 6 || !(enc == RR_ENC_RAW || (enc == RR_ENC_INT && len == 14) ||
+                                  (enc == RR_ENC_EMBSTR && len - 6 <= RR_EMBSTR_SIZE_LIMIT));
+            pre = !o.fail;
+            prepos = vb;
+            o.n = pre ? 1 : 0;
+        } else if (type == RR_TYPE_SET_INTSET) {
+            o.fail = len < 13 || (f5 != 2 && f5 != 4 && f5 != 8) || (uint64_t)(len - 13) != (uint64_t)f5 * f9;
+            o.enc = f5;
+            w = f5;
+            nint = f9;
+            cls = o.fail ? WC_NONE : WC_IS;
+            p = vb + 13;
+        } else if (type == RR_TYPE_LIST_QUICKLIST) {
+            cls = WC_LIST;
+            p = vb + 5;
+        } else if (type == RR_TYPE_SET_HT || type == RR_TYPE_HASH_HT || type == RR_TYPE_ZSET_SKIPLIST) {
+            o.fail = len < 13;
+            cnt = u5;
+            cls = o.fail ? WC_NONE : (type == RR_TYPE_ZSET_SKIPLIST ? WC_SL : WC_HT);
+            p = vb + 13;
+        } else if (type == RR_TYPE_HASH_ZIPLIST || type == RR_TYPE_ZSET_ZIPLIST) {
+            zl0 = vb + 13;
+            const uint32_t zlbytes = __builtin_amdgcn_alignbyte(h[4 - 1], h[3], 1);   // bytes 13..16 (h[3] bytes 12..15)
+            (void)zlbytes;
+            o.fail = len < 13 || (uint64_t)(len - 13) != u5 || u5 < 11 || s32(S, zl0) != len - 13;
+            zend = vb + len;
+            pre = !o.fail;
+            prepos = zl0;
+            o.n = pre ? 1 : 0;
+            cls = o.fail ? WC_NONE : WC_ZL;
+            p = zl0 + 10;
+            last = zl0 + 10;
+        } else {
+            o.fail = true;
         }
     }
     rec_put(recs, pre, rb, 0, r, prepos | (lane << 16));
+    bool walking = cls != WC_NONE;
     while (__ballot(walking)) {
-        bool emit = false;
-        const uint32_t rpos = p, k = o.n;
-        if (walking) {
-            uint32_t b[3];   // bytes p .. p+11: every element header of every type fits
-            s_read<3>(S, p, b);
-            const uint64_t u64v = (uint64_t)b[0] | ((uint64_t)b[1] << 32);
-            switch (type) {
-                case RR_TYPE_SET_INTSET:
-                    if (k < nint) { emit = true; ++o.n; p += o.enc; }
-                    else walking = false;
-                    break;
-                case RR_TYPE_LIST_QUICKLIST:
-                    if (p == end) { walking = false; break; }
-                    if (end - p < 4 || b[0] > end - p - 4) { o.fail = true; break; }
-                    emit = true;
-                    ++o.n;
-                    p += 4 + b[0];
-                    break;
-                case RR_TYPE_SET_HT:
-                case RR_TYPE_HASH_HT:
-                    if (p == end) { walking = false; break; }
-                    if (end - p < 8 || u64v > (uint64_t)(end - p - 8)) { o.fail = true; break; }
-                    emit = true;
-                    ++o.n;
-                    p += 8 + b[0];
-                    break;
-                case RR_TYPE_ZSET_SKIPLIST:
-                    if ((k & 1) == 0) {
-                        if (p == end) { walking = false; break; }
-                        if ((uint64_t)(k >> 1) == cnt) { o.fail = true; break; }   // bytes after the last node
-                        if (end - p < 8 || u64v > (uint64_t)(end - p - 8)) { o.fail = true; break; }
-                        p += 8 + b[0];
-                    } else {
-                        if (end - p < 8) { o.fail = true; break; }
-                        p += 8;
-                    }
-                    emit = true;
-                    ++o.n;
-                    break;
-                default: {   // ziplist entry, ziplist.c:300-447
-                    const uint32_t zend = zl0 + zlL;
-                    if (p >= zend) { o.fail = true; break; }
-                    const uint32_t b0 = b[0] & 0xFF;
-                    if (b0 == 0xFF) { walking = false; break; }
-                    const bool big = b0 >= 254;
-                    if (big && p + 5 > zend - 1) { o.fail = true; break; }
-                    const uint32_t pl = big ? __builtin_amdgcn_alignbyte(b[1], b[0], 1) : b0;
-                    const uint32_t pls = big ? 5u : 1u;
-                    if (pl != prev_raw) { o.fail = true; break; }
-                    const uint32_t q = p + pls;
-                    if (q >= zend - 1) { o.fail = true; break; }
-                    // bytes q .. q+4 (enc + up to 4 length bytes)
-                    const uint32_t qe = big ? __builtin_amdgcn_alignbyte(b[2], b[1], 1) : __builtin_amdgcn_alignbyte(b[1], b[0], 1);
-                    const uint32_t qe4 = big ? ((b[2] >> 8) & 0xFF) : ((b[1] >> 8) & 0xFF);
-                    const uint32_t enc = qe & 0xFF;
-                    uint64_t e64;
-                    if (enc < 0xC0) {
-                        const uint32_t cls = enc & 0xC0;
-                        if (cls == 0x00) e64 = (uint64_t)q + 1 + (enc & 0x3F);
-                        else if (cls == 0x40) {
-                            if (q + 2 > zend - 1) { o.fail = true; break; }
-                            e64 = (uint64_t)q + 2 + (((enc & 0x3F) << 8) | ((qe >> 8) & 0xFF));
-                        } else {
-                            if (q + 5 > zend - 1) { o.fail = true; break; }
-                            const uint32_t sl = ((qe >> 8) & 0xFF) << 24 | ((qe >> 16) & 0xFF) << 16 | ((qe >> 24) & 0xFF) << 8 | qe4;
-                            e64 = (uint64_t)q + 5 + sl;
-                        }
-                    } else {
-                        uint32_t isz;
-                        if (enc == 0xFE) isz = 1;
-                        else if (enc == 0xC0) isz = 2;
-                        else if (enc == 0xF0) isz = 3;
-                        else if (enc == 0xD0) isz = 4;
-                        else if (enc == 0xE0) isz = 8;
-                        else if (enc >= 0xF1 && enc <= 0xFD) isz = 0;
-                        else { o.fail = true; break; }
-                        e64 = (uint64_t)q + 1 + isz;
-                    }
-                    if (e64 > zend - 1) { o.fail = true; break; }
-                    const uint32_t e = (uint32_t)e64;
-                    emit = true;
-                    ++o.n;
-                    prev_raw = e - p;
-                    last = p;
-                    p = e;
-                    break;
-                }
-            }
-            if (o.fail) walking = false;
-            if (emit && k >= REC_KMAX) { o.fail = true; walking = false; emit = false; }
+        uint32_t b[3];   // bytes p .. p+11: every element header of every class fits
+        s_read<3>(S, p, b);
+        const uint32_t k = o.n;
+        const uint32_t L32 = b[0];
+        const uint64_t L64 = (uint64_t)b[0] | ((uint64_t)b[1] << 32);
+        const uint32_t rem = end - p;
+        // ---- LIST: u32 length + bytes
+        const bool chain_end = p == end;
+        const bool l_bad = rem < 4 || L32 > rem - 4;
+        // ---- HT / skiplist member: u64 length + bytes; skiplist score: 8 bytes
+        const bool h_bad = rem < 8 || L64 > (uint64_t)(rem - 8);
+        const bool sl_score = (k & 1) != 0;
+        const bool sl_extra = !sl_score && (uint64_t)(k >> 1) == cnt;   // bytes after the last node
+        // ---- ziplist entry (ziplist.c:300-447)
+        const uint32_t b0 = L32 & 0xFF;
+        const bool z_end = b0 == 0xFF;
+        const bool big = b0 >= 254;
+        const uint32_t pl = big ? __builtin_amdgcn_alignbyte(b[1], b[0], 1) : b0;
+        const uint32_t pls = big ? 5u : 1u;
+        const uint32_t qe = big ? __builtin_amdgcn_alignbyte(b[2], b[1], 1) : __builtin_amdgcn_alignbyte(b[1], b[0], 1);
+        const uint32_t qe4 = big ? ((b[2] >> 8) & 0xFF) : ((b[1] >> 8) & 0xFF);
+        const uint32_t enc = qe & 0xFF;
+        const bool zstr = enc < 0xC0;
+        const uint32_t scls = enc >> 6;
+        const uint32_t ls = scls == 0 ? 1u : (scls == 1 ? 2u : 5u);
+        const uint32_t sl = scls == 0 ? (enc & 0x3F)
+                          : scls == 1 ? (((enc & 0x3F) << 8) | ((qe >> 8) & 0xFF))
+                                      : ((((qe >> 8) & 0xFF) << 24) | (((qe >> 16) & 0xFF) << 16) |
+                                         (((qe >> 24) & 0xFF) << 8) | qe4);
+        const bool imm = enc >= 0xF1 && enc <= 0xFD;
+        const uint32_t isz = enc == 0xFE ? 1u : enc == 0xC0 ? 2u : enc == 0xF0 ? 3u : enc == 0xD0 ? 4u : enc == 0xE0 ? 8u : 0u;
+        const bool int_ok = imm || enc == 0xFE || enc == 0xC0 || enc == 0xF0 || enc == 0xD0 || enc == 0xE0;
+        const uint64_t q = (uint64_t)p + pls;
+        const uint64_t zsize = zstr ? (uint64_t)pls + ls + sl : (uint64_t)pls + 1 + isz;
+        const bool z_bad = p >= zend || (big && p + 5 > zend - 1) || pl != prev_raw || q >= zend - 1 ||
+                           (zstr && scls == 1 && q + 2 > zend - 1) || (zstr && scls >= 2 && q + 5 > zend - 1) ||
+                           (!zstr && !int_ok) || (uint64_t)p + zsize > zend - 1;
+        // ---- pick this lane's class
+        bool at_end, bad;
+        uint32_t size;
+        if (cls == WC_LIST) { at_end = chain_end; bad = l_bad; size = 4 + L32; }
+        else if (cls == WC_HT) { at_end = chain_end; bad = h_bad; size = 8 + L32; }
+        else if (cls == WC_SL) {
+            at_end = !sl_score && chain_end;
+            bad = sl_score ? rem < 8 : (sl_extra || h_bad);
+            size = sl_score ? 8u : 8 + L32;
+        } else if (cls == WC_ZL) {
+            at_end = p < zend && z_end;
+            bad = z_bad;
+            size = (uint32_t)zsize;
+        } else {   // WC_IS
+            at_end = k >= nint;
+            bad = false;
+            size = w;
         }
-        rec_put(recs, emit, rb, k, r, rpos | (lane << 16) | (k << 22));
+        const bool emit = walking && !at_end && !bad;
+        o.fail |= walking && !at_end && bad;
+        rec_put(recs, emit, rb, k, r, p | (lane << 16) | (k << 22));
+        if (emit) {
+            prev_raw = size;
+            last = p;
+            p += size;
+            o.n = k + 1;
+        }
+        walking = emit && o.n <= r && k + 1 < REC_KMAX;
+        o.fail |= emit && (o.n > r || k + 1 >= REC_KMAX);
     }
     // end-of-value checks (rock_serdes.c counts; ziplist header fields)
     if (active && !o.fail) {
-        switch (type) {
-            case RR_TYPE_SET_HT: o.fail = (uint64_t)o.n != cnt; break;
-            case RR_TYPE_HASH_HT:
-            case RR_TYPE_ZSET_SKIPLIST: o.fail = (o.n & 1) || (uint64_t)(o.n >> 1) != cnt; break;
-            case RR_TYPE_HASH_ZIPLIST:
-            case RR_TYPE_ZSET_ZIPLIST: {
-                uint32_t z[3];
-                s_read<3>(S, zl0, z);   // zlbytes, zltail, zllen
-                const uint32_t entries = o.n - 1;
-                const uint32_t zllen = z[2] & 0xFFFF;
-                o.fail = p != zl0 + zlL - 1 || (zllen != 0xFFFF && zllen != entries) || z[1] != last - zl0 ||
-                         (entries & 1);
-                break;
-            }
-            default:
-                break;
+        if (cls == WC_HT) {
+            const uint32_t type = s8(S, vb);
+            o.fail = type == RR_TYPE_SET_HT ? (uint64_t)o.n != cnt : ((o.n & 1) || (uint64_t)(o.n >> 1) != cnt);
+        } else if (cls == WC_SL) {
+            o.fail = (o.n & 1) || (uint64_t)(o.n >> 1) != cnt;
+        } else if (cls == WC_ZL) {
+            uint32_t z[3];
+            s_read<3>(S, zl0, z);   // zlbytes, zltail, zllen
+            const uint32_t entries = o.n - 1;
+            const uint32_t zllen = z[2] & 0xFFFF;
+            o.fail = p != zend - 1 || (zllen != 0xFFFF && zllen != entries) || z[1] != last - zl0 || (entries & 1);
         }
     }
     return o;
