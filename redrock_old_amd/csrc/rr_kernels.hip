@@ -17,7 +17,7 @@
 #include <hip/hip_runtime.h>
 #include <stdlib.h>
 
-#include "rr_decode_fast.h"
+#include "rr_decode_class.h"
 #include "rr_device.h"
 #include "rr_kernels.h"
 
@@ -27,15 +27,6 @@ namespace {
 
 constexpr uint32_t TILE = RR_WAVE;       // values per wave tile
 
-// Probe build (make PROBE=1 -> librr_serdes_probe.so): per-phase cycle and path counters
-// accumulated into scratch words [8, 40) (diagnostics only; the product build compiles them out).
-#ifdef RR_PROBE
-#define PROBE_ADD(P, I, V) do { if (lane_id() == 0) atomicAdd((unsigned long long *)&(P)[8 + (I)], (unsigned long long)(V)); } while (0)
-#define PROBE_T() __builtin_amdgcn_s_memtime()
-#else
-#define PROBE_ADD(P, I, V) do { } while (0)
-#define PROBE_T() 0ull
-#endif
 constexpr uint32_t WG = 256;             // 4 independent waves per workgroup
 
 struct Parsed {
@@ -332,19 +323,17 @@ static hipError_t launch_finalize(const uint64_t *stats, uint64_t *state, uint32
 }
 
 // ---------------------------------------------------------------------------------------- decode
-// The blob buffer is cut into fixed byte WINDOWS of WIN bytes; window t owns the values whose
-// first byte lies in [t*WIN, (t+1)*WIN) (plan_kernel finds them: first_val[t]).  One wave per
-// window:
-//   1. streams the window's bytes into the mirror arena (aligned dwordx4 loads/stores — the
-//      copy is balanced by bytes whatever the value sizes), and stages the bytes of its values
-//      (window + the tail of the last value, up to STAGE bytes) into LDS from the same loads;
-//   2. lane = value, chunks of 64: validates/counts every value from LDS (count pass);
-//   3. wave scan + decoupled look-back over windows -> elem_base of every value;
-//   4. re-parses from LDS and writes descriptors + value records.
-// Windows whose values do not fit the stage parse from global memory (L2-hot) instead.
+// Four launches, no inter-workgroup waits except the scan's look-back:
+//   K1 count_kernel   thread per value: its descriptor reservation (rr_format.h) and its walk
+//                     class (rr_decode_class.h; header checks done here);
+//   K2 scan_kernel    exclusive scan of the reservations -> elem_base of every value;
+//   K3 decode_kernel  workgroup per tile of DEC_T values: streams the tile's bytes into the
+//                     mirror arena, sorts the tile's values by class in LDS, then its waves take
+//                     64-value single-class batches (heaviest class first) and walk + emit them
+//                     from L2-hot global memory;
+//   K4 finalize       totals.
 
-// ---- K1: plan windows + descriptor reservation per value -------------------------------
-// Thread per value i in [0, n]: first_val for the byte windows whose first value is i, and
+// ---- K1: reservation + class per value ------------------------------------------------
 // reserve(i) = the descriptor slots value i owns (rr_format.h): header fields only, plus the
 // length chain of a List.  Equal to the decoded count for every valid blob.
 __device__ __forceinline__ uint64_t zl_walk_count_g(const uint8_t *zl, uint64_t L) {
@@ -410,22 +399,51 @@ __device__ __forceinline__ uint64_t reserve_g(const uint8_t *b, uint64_t L) {
     }
 }
 
+// The class of a value: which single-class walk decodes it.  Every check that needs only the
+// header is made here; values failing one (and unknown types) go to the exact parser.
+__device__ __forceinline__ uint32_t classify_g(const uint8_t *b, uint64_t L) {
+    if (L < 5) return C_EXACT;
+    switch (b[0]) {
+        case RR_TYPE_STRING: {
+            if (L < 6) return C_EXACT;
+            const uint32_t enc = b[5];
+            const uint64_t rest = L - 6;
+            if (enc == RR_ENC_INT) return rest == 8 ? C_STR : C_EXACT;
+            if (enc == RR_ENC_EMBSTR) return rest <= RR_EMBSTR_SIZE_LIMIT ? C_STR : C_EXACT;
+            if (enc == RR_ENC_RAW) return rest <= 0xFFFFFFFFull ? C_STR : C_EXACT;
+            return C_EXACT;
+        }
+        case RR_TYPE_LIST_QUICKLIST:
+            return C_LIST;
+        case RR_TYPE_SET_INTSET: {
+            if (L < 13) return C_EXACT;
+            const uint64_t w = ld_u32(b + 5), c = ld_u32(b + 9);
+            return ((w == 2 || w == 4 || w == 8) && L - 13 == w * c) ? C_IS : C_EXACT;
+        }
+        case RR_TYPE_SET_HT:
+        case RR_TYPE_HASH_HT:
+            return L < 13 ? C_EXACT : C_HT;
+        case RR_TYPE_ZSET_SKIPLIST:
+            return L < 13 ? C_EXACT : C_SL;
+        case RR_TYPE_HASH_ZIPLIST:
+        case RR_TYPE_ZSET_ZIPLIST: {
+            if (L < 24) return C_EXACT;   // 13-byte header + the 11-byte empty ziplist
+            const uint64_t Lz = ld_u64(b + 5);
+            return (Lz == L - 13 && ld_u32(b + 13) == Lz) ? C_ZL : C_EXACT;
+        }
+        default:
+            return C_EXACT;
+    }
+}
+
 __global__ __launch_bounds__(256) void count_kernel(const uint8_t *__restrict__ blob,
                                                     const uint64_t *__restrict__ offsets, uint64_t n,
-                                                    uint32_t *__restrict__ first_val, uint32_t nwin, uint32_t win,
-                                                    uint64_t *__restrict__ counts) {
+                                                    uint64_t *__restrict__ counts, uint8_t *__restrict__ cls) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i > n) return;
-    const uint64_t o_hi = offsets[i];
-    const uint64_t o_lo = i == 0 ? 0 : offsets[i - 1];
-    uint64_t w_lo = i == 0 ? 0 : o_lo / win + 1;
-    uint64_t w_hi = o_hi / win;
-    if (i == n) w_hi = nwin;   // windows past the last value start, and the sentinel
-    for (uint64_t w = w_lo; w <= w_hi && w <= nwin; ++w) first_val[w] = (uint32_t)i;
-    if (i < n) {
-        const uint64_t b0 = o_hi, b1 = offsets[i + 1];
-        counts[i] = reserve_g(blob + b0, b1 - b0);
-    }
+    if (i >= n) return;
+    const uint64_t b0 = offsets[i], b1 = offsets[i + 1];
+    counts[i] = reserve_g(blob + b0, b1 - b0);
+    cls[i] = (uint8_t)classify_g(blob + b0, b1 - b0);
 }
 
 // ---- K2: exclusive scan of the reservations -> elem_base -------------------------------
@@ -476,26 +494,21 @@ __global__ __launch_bounds__(256) void scan_kernel(uint64_t *__restrict__ counts
     if (tile == ntiles - 1 && threadIdx.x == 255) counts[n] = sh_prefix + agg;
 }
 
-// ---- K3: windows: mirror copy + stage + walk + emit ------------------------------------
-// The blob buffer is cut into fixed byte WINDOWS; window t owns the values whose first byte
-// lies in [t*WIN, (t+1)*WIN).  Output positions come from K2, so windows are independent:
-// no inter-window wait, a slow window delays only itself.
-template <typename P>
-__device__ __forceinline__ void exact_chunk(P base, uint64_t sbase, const uint64_t *__restrict__ offsets,
-                                            const uint64_t *__restrict__ ebase, uint64_t v0, uint64_t v_hi,
+// ---- K3: tiles: mirror copy + class sort + single-class batches ------------------------
+// The exact parser, lane = value v (from global memory): the reference's status codes for
+// malformed values, zero-filled slots, capacity handling.
+__device__ __forceinline__ void exact_value(const uint8_t *__restrict__ blob, uint64_t v,
+                                            const uint64_t *__restrict__ offsets, const uint64_t *__restrict__ ebase,
                                             rr_value *__restrict__ values, rr_elem *__restrict__ elems,
-                                            uint64_t elem_cap, uint64_t &bad, uint64_t &pay) {
-    // the exact parser, lane = value: assigns the reference's status codes to malformed values
-    const uint64_t v = v0 + lane_id();
-    if (v >= v_hi) return;
+                                            uint64_t cap, uint64_t &bad, uint64_t &pay) {
     const uint64_t o_lo = offsets[v], o_hi = offsets[v + 1];
     const uint64_t eb = ebase[v], r = ebase[v + 1] - eb;
-    P b = base + (uint32_t)(o_lo - sbase);
-    Parsed pr = parse_value<false, P>(b, o_lo, o_hi - o_lo, nullptr);
+    const uint8_t *b = blob + o_lo;
+    Parsed pr = parse_value<false, const uint8_t *>(b, o_lo, o_hi - o_lo, nullptr);
     uint32_t status = pr.status;
     uint64_t ne = pr.n;
     if (status == RR_OK && ne != r) status = RR_E_COUNT;
-    const bool fits = eb + r <= elem_cap && eb + r <= 0xFFFFFFFFull;
+    const bool fits = eb + r <= cap;
     if (status != RR_OK) {
         ne = 0;
         if (fits)
@@ -503,170 +516,170 @@ __device__ __forceinline__ void exact_chunk(P base, uint64_t sbase, const uint64
     } else if (!fits) {
         status = RR_E_CAPACITY;
     } else {
-        Parsed e = parse_value<true, P>(b, o_lo, o_hi - o_lo, elems + eb);
+        Parsed e = parse_value<true, const uint8_t *>(b, o_lo, o_hi - o_lo, elems + eb);
         pay += e.payload;
     }
     const uint32_t len = (uint32_t)(o_hi - o_lo);
-    uint4 w;
-    w.x = (len ? ld_u8(b) : 0) | (pr.enc << 8) | (status << 16);
-    w.y = len >= 5 ? (ld_u32(b + 1) & RR_LRU_MASK) : 0;
-    w.z = (uint32_t)ne;
-    w.w = (uint32_t)eb;
-    reinterpret_cast<uint4 *>(values)[v] = w;
+    put_value(values + v, len ? ld_u8(b) : 0, pr.enc, status, len >= 5 ? ld_u32(b + 1) : 0, (uint32_t)ne,
+              (uint32_t)eb);
     bad += status != RR_OK ? 1 : 0;
 }
 
-// One wave per workgroup, each with its own LDS window (no sharing, no barriers): the wave
-// copies its window to the arena and stages it (+ the tail of its last value, up to SLACK
-// bytes), then per chunk of 64 values: walk from LDS (lane = value, rr_decode_fast.h) writing
-// element records into a table indexed by destination slot, then emit lane-per-slot (coalesced
-// descriptor stores).  Chunks the fast path cannot take (malformed values, slot table
-// overflow, unstaged windows) go to the exact parser.
-template <uint32_t WIN, uint32_t SLACK, uint32_t ECAP>
-__global__ __launch_bounds__(RR_WAVE) void decode_kernel(const uint8_t *__restrict__ blob, uint64_t data_cap,
-                                                         const uint64_t *__restrict__ offsets, uint64_t n,
-                                                         const uint32_t *__restrict__ first_val, uint32_t nwin,
-                                                         const uint64_t *__restrict__ ebase,
-                                                         rr_value *__restrict__ values, rr_elem *__restrict__ elems,
-                                                         uint64_t elem_cap, uint8_t *__restrict__ arena,
-                                                         uint64_t *__restrict__ stats, uint64_t *probe, int mode) {
-    constexpr uint32_t STAGE = WIN + SLACK;
-    // +64: the fast path's aligned multi-dword reads may run past the staged bytes
-    __shared__ __attribute__((aligned(16))) uint8_t stage[STAGE + 64];
-    __shared__ uint32_t slot_tab[ECAP];
-    (void)probe;
-    (void)mode;
-    (void)data_cap;
-    const uint32_t lane = lane_id();
-    lds_u32w recs = (lds_u32w)slot_tab;
-    const uint64_t nbytes = offsets[n];
-    const uint64_t padded = (nbytes + 15) & ~15ull;
-    const uint64_t cap = elem_cap < 0xFFFFFFFFull ? elem_cap : 0xFFFFFFFFull;   // elem_base is 32-bit
-    for (uint32_t tile = blockIdx.x; tile < nwin; tile += gridDim.x) {
-        const uint64_t v_lo = first_val[tile], v_hi = first_val[tile + 1];
-        const uint64_t W0 = (uint64_t)tile * WIN;
-        const uint64_t W1 = W0 + WIN < padded ? W0 + WIN : padded;
-        uint64_t S0 = W0, S1 = W0;
-        if (v_hi > v_lo) {
-            S0 = offsets[v_lo];
-            S1 = offsets[v_hi];
-        }
-        const uint64_t sbase = S0 & ~15ull;
-        const uint64_t send = (S1 + 15) & ~15ull;
-        const bool staged = send - sbase <= STAGE;
-        const uint64_t L1 = staged && send > W1 ? send : W1;
+// class batch order: heaviest walks first (longest-job-first over the tile's waves)
+__constant__ uint32_t CLASS_ORDER[C_N] = {C_ZL, C_SL, C_HT, C_LIST, C_EXACT, C_IS, C_STR};
 
-        // 1. copy window -> arena, stage value bytes -> LDS (one load feeds both)
-        {
-            const u32x4 *src = reinterpret_cast<const u32x4 *>(blob);
-            u32x4 *dst = reinterpret_cast<u32x4 *>(arena);
-            u32x4 *lds = reinterpret_cast<u32x4 *>(stage);
-            const uint64_t cw1 = W1 >> 4, cs0 = sbase >> 4;
-            uint64_t c = (W0 >> 4) + lane;
-            const uint64_t ce = L1 >> 4;
-            for (; c + 7 * RR_WAVE < ce; c += 8 * RR_WAVE) {
-                u32x4 x[8];
+template <uint32_t T, uint32_t NW>
+__global__ __launch_bounds__(NW * RR_WAVE) void decode_kernel(const uint8_t *__restrict__ blob, uint64_t data_cap,
+                                                              const uint64_t *__restrict__ offsets, uint64_t n,
+                                                              const uint8_t *__restrict__ cls,
+                                                              const uint64_t *__restrict__ ebase,
+                                                              rr_value *__restrict__ values,
+                                                              rr_elem *__restrict__ elems, uint64_t elem_cap,
+                                                              uint8_t *__restrict__ arena, uint64_t *__restrict__ stats) {
+    constexpr uint32_t NT = NW * RR_WAVE;
+    __shared__ uint16_t perm[T];
+    __shared__ uint32_t ccount[C_N], cbase[C_N], ccur[C_N], bpre[C_N + 1];
+    __shared__ uint32_t next_batch;
+    __shared__ uint64_t red[2][NW];
+    const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid / RR_WAVE;
+    const uint32_t tile = blockIdx.x;
+    const uint64_t v0 = (uint64_t)tile * T;
+    const uint32_t nv = (uint32_t)(n - v0 < T ? n - v0 : T);
+    const uint64_t o_first = offsets[v0], o_end = offsets[v0 + nv];
+    const uint64_t cap = elem_cap < 0xFFFFFFFFull ? elem_cap : 0xFFFFFFFFull;   // elem_base is 32-bit
+
+    // 1. mirror copy of the tile's bytes (16-byte chunks; tile t owns [A_t, A_t+1) with
+    //    A_t = offsets[t*T] rounded down, A_0 = 0, the last tile ending at offsets[n] rounded up)
+    {
+        const uint64_t A0 = tile ? (o_first >> 4) : 0;
+        const uint64_t A1 = v0 + nv == n ? (o_end + 15) >> 4 : o_end >> 4;
+        const u32x4 *src = reinterpret_cast<const u32x4 *>(blob);
+        u32x4 *dst = reinterpret_cast<u32x4 *>(arena);
+        uint64_t c = A0 + tid;
+        for (; c + 3 * NT < A1; c += 4 * NT) {
+            u32x4 x[4];
 #pragma unroll
-                for (int k = 0; k < 8; ++k) x[k] = src[c + k * RR_WAVE];
+            for (int k = 0; k < 4; ++k) x[k] = src[c + k * NT];
 #pragma unroll
-                for (int k = 0; k < 8; ++k) {
-                    const uint64_t cc = c + k * RR_WAVE;
-                    if (cc < cw1) __builtin_nontemporal_store(x[k], dst + cc);
-                    if (staged && cc >= cs0) lds[cc - cs0] = x[k];
-                }
-            }
-            for (; c < ce; c += RR_WAVE) {
-                const u32x4 x = src[c];
-                if (c < cw1) __builtin_nontemporal_store(x, dst + c);
-                if (staged && c >= cs0) lds[c - cs0] = x;
+            for (int k = 0; k < 4; ++k) __builtin_nontemporal_store(x[k], dst + c + k * NT);
+        }
+        for (; c < A1; c += NT) __builtin_nontemporal_store(src[c], dst + c);
+    }
+
+    // 2. counting sort of the tile's values by class (ballot per class, one LDS atomic per
+    //    class per wave-round)
+    if (tid < C_N) { ccount[tid] = 0; ccur[tid] = 0; }
+    if (tid == 0) next_batch = 0;
+    // values whose tile-relative offsets could overflow 32 bits all go to the exact parser
+    const uint64_t B = o_first & ~15ull;
+    const bool tile_big = o_end - B > 0xFFFFFF00ull;
+    __syncthreads();
+    uint32_t myc[T / NT];
+#pragma unroll
+    for (uint32_t j = 0; j < T / NT; ++j) {
+        const uint32_t i = j * NT + tid;
+        myc[j] = i < nv ? (tile_big ? C_EXACT : (uint32_t)cls[v0 + i]) : C_N;
+#pragma unroll
+        for (uint32_t c = 0; c < C_N; ++c) {
+            const uint64_t m = __ballot(myc[j] == c);
+            if (m && lane == 0) atomicAdd(&ccount[c], (uint32_t)__popcll(m));
+        }
+    }
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t s = 0, bs = 0;
+        for (uint32_t k = 0; k < C_N; ++k) {
+            const uint32_t c = CLASS_ORDER[k];
+            cbase[c] = s;
+            bpre[k] = bs;
+            s += ccount[c];
+            bs += (ccount[c] + RR_WAVE - 1) / RR_WAVE;
+        }
+        bpre[C_N] = bs;
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t j = 0; j < T / NT; ++j) {
+        const uint32_t i = j * NT + tid;
+#pragma unroll
+        for (uint32_t c = 0; c < C_N; ++c) {
+            const uint64_t m = __ballot(myc[j] == c);
+            if (m) {
+                uint32_t at = 0;
+                if (lane == 0) at = atomicAdd(&ccur[c], (uint32_t)__popcll(m));
+                at = __shfl(at, 0, RR_WAVE);
+                if (myc[j] == c) perm[cbase[c] + at + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = (uint16_t)i;
             }
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#ifdef RR_PROBE
-        if (mode == 1) continue;   // ablation: copy + stage only
-#endif
-        uint64_t bad = 0, pay = 0;
-        for (uint64_t v0 = v_lo; v0 < v_hi; v0 += RR_WAVE) {
-            const uint64_t v1 = v0 + RR_WAVE < v_hi ? v0 + RR_WAVE : v_hi;
-            const uint64_t cb = ebase[v0], nslots = ebase[v1] - cb;
-            bool done = false;
-            if (staged && nslots <= ECAP) {
-                lds_cptr S = (lds_cptr)stage;
-                const bool active = v0 + lane < v1;
-                const uint64_t v = v0 + lane;
-                uint64_t o_lo = sbase, o_hi = sbase, eb = cb, r = 0;
-                if (active) {
-                    o_lo = offsets[v];
-                    o_hi = offsets[v + 1];
-                    eb = ebase[v];
-                    r = ebase[v + 1] - eb;
+    }
+    __syncthreads();
+
+    // 3. single-class batches of <= 64 values, taken dynamically by the waves
+    const rsrc_t R = make_rsrc(blob + B, (uint32_t)(data_cap - B < 0xFFFFFFFFull ? data_cap - B : 0xFFFFFFFFull));
+    uint64_t bad = 0, pay = 0;
+    const uint32_t nb = bpre[C_N];
+    for (;;) {
+        uint32_t bi = 0;
+        if (lane == 0) bi = atomicAdd(&next_batch, 1u);
+        bi = __builtin_amdgcn_readfirstlane(__shfl(bi, 0, RR_WAVE));
+        if (bi >= nb) break;
+        uint32_t k = 0;
+        while (bi >= bpre[k + 1]) ++k;
+        const uint32_t c = CLASS_ORDER[k];
+        const uint32_t first = cbase[c] + (bi - bpre[k]) * RR_WAVE;
+        const uint32_t cnt = min(ccount[c] - (bi - bpre[k]) * RR_WAVE, (uint32_t)RR_WAVE);
+        if (lane < cnt) {
+            const uint64_t v = v0 + perm[first + lane];
+            if (c == C_EXACT) {
+                exact_value(blob, v, offsets, ebase, values, elems, cap, bad, pay);
+            } else {
+                const uint64_t o = offsets[v], o1 = offsets[v + 1], eb = ebase[v], r = ebase[v + 1] - eb;
+                Lane l;
+                l.q = (uint32_t)(o - B);
+                l.L = (uint32_t)(o1 - o);
+                l.B = B;
+                l.el = elems + eb;
+                l.r = (uint32_t)r;
+                l.ok = eb + r <= cap;
+                Head H;
+                gread<4>(R, l.q, H.h);
+                uint32_t ne = 1, enc = 0;
+                bool fail = false;
+                if (c == C_STR) {
+                    do_string(H, l, pay);
+                    enc = H.b5();
+                } else if (c == C_IS) {
+                    do_intset(R, H, l);
+                    ne = H.f9();
+                    enc = H.f5();
+                } else if (c == C_LIST) {
+                    fail = do_list(R, l, ne, pay);
+                } else if (c == C_HT) {
+                    fail = do_ht(R, H, l, ne, pay);
+                } else if (c == C_SL) {
+                    fail = do_skiplist(R, H, l, ne, pay);
+                } else {
+                    fail = do_ziplist(R, l, ne, pay);
                 }
-                const uint32_t vb = (uint32_t)(o_lo - sbase), len = (uint32_t)(o_hi - o_lo);
-                const WalkOut wo = fast_walk(S, active, vb, len, recs, (uint32_t)(eb - cb), (uint32_t)r);
-#ifdef RR_PROBE
-                if (mode == 2) { asm volatile("" ::"v"(wo.n)); continue; }   // ablation: no emission
-#endif
-                if (!__ballot(active && (wo.fail || wo.n != r))) {
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                    __builtin_amdgcn_wave_barrier();
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                    const bool capok = eb + r <= cap;
-                    uint32_t h0 = 0, h1 = 0;
-                    if (active) {
-                        h0 = s32(S, vb);
-                        h1 = s32(S, vb + 1);
-                    }
-                    const uint32_t type = active ? (h0 & 0xFF) : 0xFF;
-                    const bool chunk_ok = cb + nslots <= cap;   // every value of the chunk fits
-                    // lane-per-slot emission: slot j holds the record of descriptor cb + j
-                    for (uint32_t q = 0; q < (uint32_t)nslots; q += RR_WAVE) {
-                        const uint32_t j = q + lane;
-                        const uint32_t rec = j < nslots ? recs[j] : 0u;
-                        const int ow = (int)((rec >> 16) & 63);
-                        const uint32_t otype = __shfl(type, ow, RR_WAVE), oenc = __shfl(wo.enc, ow, RR_WAVE);
-                        const uint32_t ovb = __shfl(vb, ow, RR_WAVE), olen = __shfl(len, ow, RR_WAVE);
-                        const int ook = chunk_ok ? 1 : __shfl((int)capok, ow, RR_WAVE);
-                        if (j < nslots && ook) {
-                            uint4 w;
-                            fast_emit(S, sbase, otype, oenc, ovb, olen, rec & 0xFFFF, rec >> 22, w, pay);
-                            *reinterpret_cast<uint4 *>(elems + cb + j) = w;
-                        }
-                    }
-                    if (active) {
-                        uint4 w;
-                        w.x = type | (wo.enc << 8) | ((capok ? RR_OK : RR_E_CAPACITY) << 16);
-                        w.y = h1 & RR_LRU_MASK;
-                        w.z = wo.n;
-                        w.w = (uint32_t)eb;
-                        reinterpret_cast<uint4 *>(values)[v] = w;
-                        bad += capok ? 0 : 1;
-                    }
-                    done = true;
+                if (fail) {
+                    exact_value(blob, v, offsets, ebase, values, elems, cap, bad, pay);
+                } else {
+                    put_value(values + v, H.type(), enc, l.ok ? RR_OK : RR_E_CAPACITY, H.lru(), ne, (uint32_t)eb);
+                    bad += l.ok ? 0 : 1;
                 }
             }
-            if (!done) {
-                if (staged)
-                    exact_chunk<lds_cptr>((lds_cptr)stage, sbase, offsets, ebase, v0, v1, values, elems, cap, bad, pay);
-                else
-                    exact_chunk<const uint8_t *>(blob, 0, offsets, ebase, v0, v1, values, elems, cap, bad, pay);
-            }
-            // the slot table is rewritten by the next chunk
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
-        bad = wave_sum(bad);
-        pay = wave_sum(pay);
-        if (lane == 0) {
-            stats[3 * (uint64_t)tile + 0] = bad;
-            stats[3 * (uint64_t)tile + 1] = pay;
-            stats[3 * (uint64_t)tile + 2] = 0;
-        }
-        // the stage is rewritten by the next window
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
+    }
+    bad = wave_sum(bad);
+    pay = wave_sum(pay);
+    if (lane == 0) { red[0][wave] = bad; red[1][wave] = pay; }
+    __syncthreads();
+    if (tid == 0) {
+        uint64_t tb = 0, tp = 0;
+        for (uint32_t w = 0; w < NW; ++w) { tb += red[0][w]; tp += red[1][w]; }
+        stats[3 * (uint64_t)tile + 0] = tb;
+        stats[3 * (uint64_t)tile + 1] = tp;
+        stats[3 * (uint64_t)tile + 2] = 0;
     }
 }
 
@@ -926,18 +939,13 @@ __global__ __launch_bounds__(WG) void encode_kernel(const rr_value *__restrict__
 }  // namespace
 
 // ---------------------------------------------------------------------------------------- launch
-#ifndef RR_DEC_WIN
-#define RR_DEC_WIN 16384
+#ifndef RR_DEC_T
+#define RR_DEC_T 2048
 #endif
-#ifndef RR_DEC_SLACK
-#define RR_DEC_SLACK 4096
+#ifndef RR_DEC_NW
+#define RR_DEC_NW 8
 #endif
-#ifndef RR_DEC_ECAP
-#define RR_DEC_ECAP 1024
-#endif
-constexpr uint32_t DEC_NW = 1;
-constexpr uint32_t DEC_WIN = RR_DEC_WIN;
-#define DECODE_KERNEL decode_kernel<DEC_WIN, RR_DEC_SLACK, RR_DEC_ECAP>
+constexpr uint32_t DEC_T = RR_DEC_T, DEC_NW = RR_DEC_NW;
 
 // Resident workgroup count for a persistent launch: occupancy query minus one block per CU
 // (the API over-reports by one for SGPR-heavy kernels, MI355X_MICROARCH.md §Residency).
@@ -952,8 +960,6 @@ static uint32_t resident_grid(K kernel, int block, bool margin = true) {
     return (uint32_t)(cus * occ);
 }
 
-extern "C" uint64_t rr_decode_windows(uint64_t data_cap) { return data_cap / DEC_WIN + 1; }
-
 static uint64_t scan_tiles(uint64_t n) { return (n + SCAN_TILE - 1) / SCAN_TILE; }
 
 extern "C" uint64_t rr_encode_scratch_words(uint64_t n) {
@@ -961,50 +967,39 @@ extern "C" uint64_t rr_encode_scratch_words(uint64_t n) {
     return RR_SCRATCH_HDR + 4 * t + t / 64 + 2;
 }
 
+static uint64_t dec_tiles(uint64_t n) { return (n + DEC_T - 1) / DEC_T; }
+
 // Decode scratch (uint64 words): [HDR] [scan: ticket, look-back state + groups]
-// [counts -> elem_base, n+1] [window stats, 3 per window] [first_val u32, nwin+1].
+// [counts -> elem_base, n+1] [tile stats, 3 per tile] [class bytes, n].
 extern "C" uint64_t rr_decode_scratch_words(uint64_t data_cap, uint64_t n) {
-    const uint64_t nwin = rr_decode_windows(data_cap), st = scan_tiles(n);
-    return RR_SCRATCH_HDR + 1 + st + st / 64 + 1 + (n + 1) + 3 * nwin + (nwin + 2) / 2 + 2;
+    (void)data_cap;
+    const uint64_t st = scan_tiles(n);
+    return RR_SCRATCH_HDR + 1 + st + (st + LB_GROUP - 1) / LB_GROUP + (n + 1) + 3 * dec_tiles(n) + (n + 7) / 8 + 2;
 }
 
 extern "C" hipError_t rr_launch_decode(const uint8_t *blob, const uint64_t *offsets, uint64_t n, rr_value *values,
                                        rr_elem *elems, uint64_t elem_cap, uint8_t *arena, uint64_t *scratch,
                                        uint64_t data_cap, rr_totals *totals, hipStream_t stream) {
-    // The window grid is sized from data_cap (>= offsets[n], host-known without a sync);
-    // windows past offsets[n] find no values and copy nothing.
-    const uint32_t nwin = (uint32_t)rr_decode_windows(data_cap);
-    const uint32_t st = (uint32_t)scan_tiles(n);
+    const uint32_t st = (uint32_t)scan_tiles(n), nt = (uint32_t)dec_tiles(n);
     uint64_t *lb = scratch + RR_SCRATCH_HDR;
     const uint64_t lb_words = 1 + st + (st + LB_GROUP - 1) / LB_GROUP;
     uint64_t *counts = lb + lb_words;
     uint64_t *stats = counts + n + 1;
-    uint32_t *first_val = reinterpret_cast<uint32_t *>(stats + 3 * (uint64_t)nwin);
+    uint8_t *cls = reinterpret_cast<uint8_t *>(stats + 3 * (uint64_t)nt);
     hipError_t e = hipMemsetAsync(lb, 0, ((lb_words * 8) + 15) & ~(size_t)15, stream);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(count_kernel, dim3((uint32_t)((n + 1 + 255) / 256)), dim3(256), 0, stream, blob, offsets, n,
-                       first_val, nwin, DEC_WIN, counts);
-    if (st) hipLaunchKernelGGL(scan_kernel, dim3(st), dim3(256), 0, stream, counts, n, lb, st);
-    else {
+    if (n) {
+        hipLaunchKernelGGL(count_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, stream, blob, offsets, n,
+                           counts, cls);
+        hipLaunchKernelGGL(scan_kernel, dim3(st), dim3(256), 0, stream, counts, n, lb, st);
+        hipLaunchKernelGGL((decode_kernel<DEC_T, DEC_NW>), dim3(nt), dim3(DEC_NW * RR_WAVE), 0, stream, blob,
+                           data_cap, offsets, n, cls, counts, values, elems, elem_cap, arena, stats);
+    } else {
         e = hipMemsetAsync(counts, 0, sizeof(uint64_t), stream);
         if (e != hipSuccess) return e;
     }
-    static uint32_t grid = 0;
-    if (!grid) grid = resident_grid(DECODE_KERNEL, DEC_NW * RR_WAVE, false);   // no inter-window waits
-    const uint32_t gneed = (nwin + DEC_NW - 1) / DEC_NW;
-    const uint32_t g = gneed < grid ? gneed : grid;
-#ifdef RR_PROBE
-    e = hipMemsetAsync(scratch, 0, RR_SCRATCH_HDR * sizeof(uint64_t), stream);
-    if (e != hipSuccess) return e;
-#endif
-    int mode = 0;
-#ifdef RR_PROBE
-    if (const char *m = getenv("RR_DECODE_MODE")) mode = atoi(m);
-#endif
-    hipLaunchKernelGGL((DECODE_KERNEL), dim3(g), dim3(DEC_NW * RR_WAVE), 0, stream, blob, data_cap, offsets, n, first_val,
-                       nwin, counts, values, elems, elem_cap, arena, stats, scratch, mode);
     e = hipGetLastError();
-    if (e == hipSuccess && totals) e = launch_finalize(stats, counts + n, nwin, offsets, n, 2, totals, stream);
+    if (e == hipSuccess && totals) e = launch_finalize(stats, counts + n, nt, offsets, n, 2, totals, stream);
     return e;
 }
 
