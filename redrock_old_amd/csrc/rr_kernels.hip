@@ -644,28 +644,30 @@ __global__ __launch_bounds__(NW * RR_WAVE) void decode_kernel(const uint8_t *__r
                 Head H;
                 gread<4>(R, l.q, H.h);
                 uint32_t ne = 1, enc = 0;
+                uint64_t vp = 0;   // this value's payload bytes (counted once it is emitted)
                 bool fail = false;
                 if (c == C_STR) {
-                    do_string(H, l, pay);
+                    do_string(H, l, vp);
                     enc = H.b5();
                 } else if (c == C_IS) {
                     do_intset(R, H, l);
                     ne = H.f9();
                     enc = H.f5();
                 } else if (c == C_LIST) {
-                    fail = do_list(R, l, ne, pay);
+                    fail = do_list(R, l, ne, vp);
                 } else if (c == C_HT) {
-                    fail = do_ht(R, H, l, ne, pay);
+                    fail = do_ht(R, H, l, ne, vp);
                 } else if (c == C_SL) {
-                    fail = do_skiplist(R, H, l, ne, pay);
+                    fail = do_skiplist(R, H, l, ne, vp);
                 } else {
-                    fail = do_ziplist(R, l, ne, pay);
+                    fail = do_ziplist(R, l, ne, vp);
                 }
                 if (fail) {
                     exact_value(blob, v, offsets, ebase, values, elems, cap, bad, pay);
                 } else {
                     put_value(values + v, H.type(), enc, l.ok ? RR_OK : RR_E_CAPACITY, H.lru(), ne, (uint32_t)eb);
                     bad += l.ok ? 0 : 1;
+                    pay += l.ok ? vp : 0;
                 }
             }
         }
