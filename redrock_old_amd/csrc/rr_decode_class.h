@@ -6,10 +6,10 @@
 // mixed wave would hold (a mixed walk measured ~200 wave-instructions per step, ~60 % of
 // them branch/exec-mask SALU).
 //
-// Bytes come from global memory (L2 / Infinity-Cache hot: the workgroup has just streamed its
-// tile through for the mirror copy) via buffer loads against a per-tile descriptor: offsets
-// are 32-bit and tile-relative, and a read past the end of the blob buffer returns zeros
-// instead of faulting, so every step can load a fixed 16-32 bytes at its cursor.
+// Bytes come from the workgroup's LDS-staged byte window (LdsSrc), or, for a window whose
+// values run too far past it, from global memory through a buffer descriptor (GlbSrc:
+// window-relative 32-bit offsets; a read past the blob buffer returns zeros instead of
+// faulting).  Either way every step reads a fixed 8-28 bytes at its cursor.
 //
 // Each routine applies the checks of rock_serdes.c / ziplist.c that the exact parser
 // (parse_value) applies; a lane whose value fails any of them reports `fail`, and the caller
@@ -55,6 +55,27 @@ __device__ __forceinline__ void gread(rsrc_t R, uint32_t p, uint32_t (&o)[N]) {
 #pragma unroll
     for (int i = 0; i < N; ++i) o[i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], sh);
 }
+
+// Byte sources for the walks.  p is relative to the source's base; get<N> returns bytes
+// [p, p + 4N) as N dwords (N+1 aligned reads + alignbyte).
+struct GlbSrc {   // global memory through a buffer descriptor: reads past its range give zeros
+    rsrc_t R;
+    template <int N>
+    __device__ __forceinline__ void get(uint32_t p, uint32_t (&o)[N]) const { gread<N>(R, p, o); }
+};
+struct LdsSrc {   // the workgroup's staged window; reads may run up to 64 bytes past it
+    lds_cptr S;
+    template <int N>
+    __device__ __forceinline__ void get(uint32_t p, uint32_t (&o)[N]) const {
+        const __attribute__((address_space(3))) uint32_t *W = (const __attribute__((address_space(3))) uint32_t *)S;
+        const uint32_t a = p >> 2, sh = p & 3;
+        uint32_t w[N + 1];
+#pragma unroll
+        for (int i = 0; i <= N; ++i) w[i] = W[a + i];
+#pragma unroll
+        for (int i = 0; i < N; ++i) o[i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], sh);
+    }
+};
 
 __device__ __forceinline__ uint32_t ab(uint32_t hi, uint32_t lo, uint32_t s) { return __builtin_amdgcn_alignbyte(hi, lo, s); }
 
@@ -142,13 +163,14 @@ __device__ __forceinline__ void do_string(const Head &H, const Lane &l, uint64_t
 }
 
 // ---- intset (rock_serdes.c:217-245, intset.c:45-52): fixed-width members, no walk
-__device__ __forceinline__ void do_intset(rsrc_t R, const Head &H, const Lane &l) {
+template <class Src>
+__device__ __forceinline__ void do_intset(const Src &R, const Head &H, const Lane &l) {
     const uint32_t w = H.f5(), cnt = H.f9();
     if (!l.ok) return;
     uint32_t p = l.q + 13;
     for (uint32_t k = 0; k < cnt; ++k, p += w) {
         uint32_t x[2];
-        gread<2>(R, p, x);
+        R.template get<2>(p, x);
         const int64_t v = w == 2 ? (int64_t)(int16_t)(x[0] & 0xFFFF)
                         : w == 4 ? (int64_t)(int32_t)x[0] : (int64_t)((uint64_t)x[0] | ((uint64_t)x[1] << 32));
         put_desc(l.el + k, (uint64_t)v, 0, RR_K_INT, 0);
@@ -157,13 +179,14 @@ __device__ __forceinline__ void do_intset(rsrc_t R, const Head &H, const Lane &l
 
 // ---- List (rock_serdes.c:162-214): {u32 len, bytes}* to the end; integer-looking entries
 // become INT (quicklistPushTail re-encodes them, ziplist.c:480)
-__device__ __forceinline__ bool do_list(rsrc_t R, const Lane &l, uint32_t &n, uint64_t &pay) {
+template <class Src>
+__device__ __forceinline__ bool do_list(const Src &R, const Lane &l, uint32_t &n, uint64_t &pay) {
     uint32_t p = l.q + 5, k = 0;
     const uint32_t end = l.q + l.L;
     bool fail = false;
     while (p != end) {
         uint32_t b[6];   // len + 20 bytes
-        gread<6>(R, p, b);
+        R.template get<6>(p, b);
         const uint32_t rem = end - p, len = b[0];
         if (rem < 4 || len > rem - 4 || k >= l.r) { fail = true; break; }
         const uint32_t d[5] = {b[1], b[2], b[3], b[4], b[5]};
@@ -182,14 +205,15 @@ __device__ __forceinline__ bool do_list(rsrc_t R, const Lane &l, uint32_t &n, ui
 }
 
 // ---- Set / Hash hash tables (rock_serdes.c:248-311, :349-414): u64 count, {u64 len, bytes}*
-__device__ __forceinline__ bool do_ht(rsrc_t R, const Head &H, const Lane &l, uint32_t &n, uint64_t &pay) {
+template <class Src>
+__device__ __forceinline__ bool do_ht(const Src &R, const Head &H, const Lane &l, uint32_t &n, uint64_t &pay) {
     const uint64_t cnt = H.u5();
     uint32_t p = l.q + 13, k = 0;
     const uint32_t end = l.q + l.L;
     bool fail = false;
     while (p != end) {
         uint32_t b[2];
-        gread<2>(R, p, b);
+        R.template get<2>(p, b);
         const uint32_t rem = end - p;
         if (rem < 8 || b[1] != 0 || b[0] > rem - 8 || k >= l.r) { fail = true; break; }
         if (l.ok) put_desc(l.el + k, l.B + p + 8, b[0], RR_K_STR, 0);
@@ -203,14 +227,15 @@ __device__ __forceinline__ bool do_ht(rsrc_t R, const Head &H, const Lane &l, ui
 }
 
 // ---- ZSet skiplist (rock_serdes.c:448-508): u64 count, {u64 len, member, f64 score}*
-__device__ __forceinline__ bool do_skiplist(rsrc_t R, const Head &H, const Lane &l, uint32_t &n, uint64_t &pay) {
+template <class Src>
+__device__ __forceinline__ bool do_skiplist(const Src &R, const Head &H, const Lane &l, uint32_t &n, uint64_t &pay) {
     const uint64_t cnt = H.u5();
     uint32_t p = l.q + 13, k = 0;
     const uint32_t end = l.q + l.L;
     bool fail = false;
     while (p != end) {
         uint32_t b[2];
-        gread<2>(R, p, b);
+        R.template get<2>(p, b);
         const uint32_t rem = end - p;
         if (rem < 8 || k >= l.r) { fail = true; break; }
         if (k & 1) {
@@ -230,17 +255,18 @@ __device__ __forceinline__ bool do_skiplist(rsrc_t R, const Head &H, const Lane 
 
 // ---- Hash / ZSet ziplists (rock_serdes.c:314-346, :417-446; ziplist.c:300-447): element 0
 // is the raw ziplist, then one descriptor per entry
-__device__ __forceinline__ bool do_ziplist(rsrc_t R, const Lane &l, uint32_t &n, uint64_t &pay) {
+template <class Src>
+__device__ __forceinline__ bool do_ziplist(const Src &R, const Lane &l, uint32_t &n, uint64_t &pay) {
     const uint32_t zl0 = l.q + 13, zend = l.q + l.L, zlast = zend - 1;   // zlast: the 0xFF byte
     uint32_t z[3];
-    gread<3>(R, zl0, z);   // zlbytes, zltail, zllen
+    R.template get<3>(zl0, z);   // zlbytes, zltail, zllen
     if (l.ok) put_desc(l.el, l.B + zl0, l.L - 13, RR_K_ZLRAW, 0);
     pay += l.L - 13;
     uint32_t p = zl0 + 10, prev_raw = 0, last = zl0 + 10, k = 1;
     bool fail = false;
     for (;;) {
         uint32_t b[4];   // prevlen (1 or 5) + encoding + up to 9 more bytes
-        gread<4>(R, p, b);
+        R.template get<4>(p, b);
         const uint32_t b0 = b[0] & 0xFF;
         if (p >= zend) { fail = true; break; }
         if (b0 == 0xFF) break;

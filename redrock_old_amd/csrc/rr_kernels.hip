@@ -438,12 +438,21 @@ __device__ __forceinline__ uint32_t classify_g(const uint8_t *b, uint64_t L) {
 
 __global__ __launch_bounds__(256) void count_kernel(const uint8_t *__restrict__ blob,
                                                     const uint64_t *__restrict__ offsets, uint64_t n,
+                                                    uint32_t *__restrict__ first_val, uint32_t nwin, uint32_t win,
                                                     uint64_t *__restrict__ counts, uint8_t *__restrict__ cls) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint64_t b0 = offsets[i], b1 = offsets[i + 1];
-    counts[i] = reserve_g(blob + b0, b1 - b0);
-    cls[i] = (uint8_t)classify_g(blob + b0, b1 - b0);
+    if (i > n) return;
+    // first_val[w] = first value whose first byte is at or after w*win (windows past the
+    // last value start, and the sentinel nwin, get n)
+    const uint64_t o_hi = offsets[i];
+    const uint64_t w_lo = i == 0 ? 0 : offsets[i - 1] / win + 1;
+    const uint64_t w_hi = i == n ? nwin : o_hi / win;
+    for (uint64_t w = w_lo; w <= w_hi && w <= nwin; ++w) first_val[w] = (uint32_t)i;
+    if (i < n) {
+        const uint64_t b1 = offsets[i + 1];
+        counts[i] = reserve_g(blob + o_hi, b1 - o_hi);
+        cls[i] = (uint8_t)classify_g(blob + o_hi, b1 - o_hi);
+    }
 }
 
 // ---- K2: exclusive scan of the reservations -> elem_base -------------------------------
@@ -525,150 +534,191 @@ __device__ __forceinline__ void exact_value(const uint8_t *__restrict__ blob, ui
     bad += status != RR_OK ? 1 : 0;
 }
 
-// class batch order: heaviest walks first (longest-job-first over the tile's waves)
+// class batch order: heaviest walks first (longest-job-first over the window's waves)
 __constant__ uint32_t CLASS_ORDER[C_N] = {C_ZL, C_SL, C_HT, C_LIST, C_EXACT, C_IS, C_STR};
 
-template <uint32_t T, uint32_t NW>
+// One single-class batch: lane < cnt decodes value v (byte offsets relative to the source,
+// whose byte 0 is batch offset B).
+template <class Src>
+__device__ __forceinline__ void run_batch(const Src &src, uint32_t c, uint64_t v, uint64_t B,
+                                          const uint8_t *__restrict__ blob, const uint64_t *__restrict__ offsets,
+                                          const uint64_t *__restrict__ ebase, rr_value *__restrict__ values,
+                                          rr_elem *__restrict__ elems, uint64_t cap, uint64_t &bad, uint64_t &pay) {
+    if (c == C_EXACT) {
+        exact_value(blob, v, offsets, ebase, values, elems, cap, bad, pay);
+        return;
+    }
+    const uint64_t o = offsets[v], o1 = offsets[v + 1], eb = ebase[v], r = ebase[v + 1] - eb;
+    Lane l;
+    l.q = (uint32_t)(o - B);
+    l.L = (uint32_t)(o1 - o);
+    l.B = B;
+    l.el = elems + eb;
+    l.r = (uint32_t)r;
+    l.ok = eb + r <= cap;
+    Head H;
+    src.template get<4>(l.q, H.h);
+    uint32_t ne = 1, enc = 0;
+    uint64_t vp = 0;   // this value's payload bytes (counted once it is emitted)
+    bool fail = false;
+    if (c == C_STR) {
+        do_string(H, l, vp);
+        enc = H.b5();
+    } else if (c == C_IS) {
+        do_intset(src, H, l);
+        ne = H.f9();
+        enc = H.f5();
+    } else if (c == C_LIST) {
+        fail = do_list(src, l, ne, vp);
+    } else if (c == C_HT) {
+        fail = do_ht(src, H, l, ne, vp);
+    } else if (c == C_SL) {
+        fail = do_skiplist(src, H, l, ne, vp);
+    } else {
+        fail = do_ziplist(src, l, ne, vp);
+    }
+    if (fail) {
+        exact_value(blob, v, offsets, ebase, values, elems, cap, bad, pay);
+    } else {
+        put_value(values + v, H.type(), enc, l.ok ? RR_OK : RR_E_CAPACITY, H.lru(), ne, (uint32_t)eb);
+        bad += l.ok ? 0 : 1;
+        pay += l.ok ? vp : 0;
+    }
+}
+
+// Workgroup per byte WINDOW of W bytes: window t owns the values whose first byte lies in
+// [t*W, (t+1)*W) (first_val from K1).  The workgroup
+//   1. streams the window into the mirror arena and, from the same loads, stages the bytes of
+//      its values (the window + the tail of its last value, up to SLACK more) into LDS;
+//   2. per chunk of <= PMAX of its values: counting-sorts them by class in LDS;
+//   3. its waves take single-class batches of <= 64 values, heaviest class first, and walk +
+//      emit them from LDS (from global memory when the values did not fit the stage).
+template <uint32_t W, uint32_t SLACK, uint32_t NW, uint32_t PMAX>
 __global__ __launch_bounds__(NW * RR_WAVE) void decode_kernel(const uint8_t *__restrict__ blob, uint64_t data_cap,
                                                               const uint64_t *__restrict__ offsets, uint64_t n,
+                                                              const uint32_t *__restrict__ first_val,
                                                               const uint8_t *__restrict__ cls,
                                                               const uint64_t *__restrict__ ebase,
                                                               rr_value *__restrict__ values,
                                                               rr_elem *__restrict__ elems, uint64_t elem_cap,
                                                               uint8_t *__restrict__ arena, uint64_t *__restrict__ stats) {
-    constexpr uint32_t NT = NW * RR_WAVE;
-    __shared__ uint16_t perm[T];
+    constexpr uint32_t NT = NW * RR_WAVE, STAGE = W + SLACK;
+    static_assert(PMAX % NT == 0 && W % 16 == 0 && SLACK % 16 == 0, "tile shape");
+    __shared__ __attribute__((aligned(16))) uint8_t stage[STAGE + 64];
+    __shared__ uint16_t perm[PMAX];
     __shared__ uint32_t ccount[C_N], cbase[C_N], ccur[C_N], bpre[C_N + 1];
     __shared__ uint32_t next_batch;
     __shared__ uint64_t red[2][NW];
     const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid / RR_WAVE;
     const uint32_t tile = blockIdx.x;
-    const uint64_t v0 = (uint64_t)tile * T;
-    const uint32_t nv = (uint32_t)(n - v0 < T ? n - v0 : T);
-    const uint64_t o_first = offsets[v0], o_end = offsets[v0 + nv];
+    const uint64_t v_lo = first_val[tile], v_hi = first_val[tile + 1];
+    const uint64_t padded = (offsets[n] + 15) & ~15ull;
+    const uint64_t W0 = (uint64_t)tile * W;
+    const uint64_t W1 = W0 + W < padded ? W0 + W : padded;
+    uint64_t S0 = W0, S1 = W0;
+    if (v_hi > v_lo) {
+        S0 = offsets[v_lo] & ~15ull;
+        S1 = (offsets[v_hi] + 15) & ~15ull;
+    }
+    const bool staged = S1 - S0 <= STAGE;
     const uint64_t cap = elem_cap < 0xFFFFFFFFull ? elem_cap : 0xFFFFFFFFull;   // elem_base is 32-bit
 
-    // 1. mirror copy of the tile's bytes (16-byte chunks; tile t owns [A_t, A_t+1) with
-    //    A_t = offsets[t*T] rounded down, A_0 = 0, the last tile ending at offsets[n] rounded up)
+    // 1. window -> arena, value bytes -> LDS (one load feeds both)
     {
-        const uint64_t A0 = tile ? (o_first >> 4) : 0;
-        const uint64_t A1 = v0 + nv == n ? (o_end + 15) >> 4 : o_end >> 4;
         const u32x4 *src = reinterpret_cast<const u32x4 *>(blob);
         u32x4 *dst = reinterpret_cast<u32x4 *>(arena);
-        uint64_t c = A0 + tid;
-        for (; c + 3 * NT < A1; c += 4 * NT) {
+        u32x4 *lds = reinterpret_cast<u32x4 *>(stage);
+        const uint64_t cw1 = W1 >> 4, cs0 = S0 >> 4;
+        const uint64_t ce = (staged && S1 > W1 ? S1 : W1) >> 4;
+        uint64_t c = (W0 >> 4) + tid;
+        for (; c + 3 * NT < ce; c += 4 * NT) {
             u32x4 x[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) x[k] = src[c + k * NT];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) __builtin_nontemporal_store(x[k], dst + c + k * NT);
-        }
-        for (; c < A1; c += NT) __builtin_nontemporal_store(src[c], dst + c);
-    }
-
-    // 2. counting sort of the tile's values by class (ballot per class, one LDS atomic per
-    //    class per wave-round)
-    if (tid < C_N) { ccount[tid] = 0; ccur[tid] = 0; }
-    if (tid == 0) next_batch = 0;
-    // values whose tile-relative offsets could overflow 32 bits all go to the exact parser
-    const uint64_t B = o_first & ~15ull;
-    const bool tile_big = o_end - B > 0xFFFFFF00ull;
-    __syncthreads();
-    uint32_t myc[T / NT];
-#pragma unroll
-    for (uint32_t j = 0; j < T / NT; ++j) {
-        const uint32_t i = j * NT + tid;
-        myc[j] = i < nv ? (tile_big ? C_EXACT : (uint32_t)cls[v0 + i]) : C_N;
-#pragma unroll
-        for (uint32_t c = 0; c < C_N; ++c) {
-            const uint64_t m = __ballot(myc[j] == c);
-            if (m && lane == 0) atomicAdd(&ccount[c], (uint32_t)__popcll(m));
-        }
-    }
-    __syncthreads();
-    if (tid == 0) {
-        uint32_t s = 0, bs = 0;
-        for (uint32_t k = 0; k < C_N; ++k) {
-            const uint32_t c = CLASS_ORDER[k];
-            cbase[c] = s;
-            bpre[k] = bs;
-            s += ccount[c];
-            bs += (ccount[c] + RR_WAVE - 1) / RR_WAVE;
-        }
-        bpre[C_N] = bs;
-    }
-    __syncthreads();
-#pragma unroll
-    for (uint32_t j = 0; j < T / NT; ++j) {
-        const uint32_t i = j * NT + tid;
-#pragma unroll
-        for (uint32_t c = 0; c < C_N; ++c) {
-            const uint64_t m = __ballot(myc[j] == c);
-            if (m) {
-                uint32_t at = 0;
-                if (lane == 0) at = atomicAdd(&ccur[c], (uint32_t)__popcll(m));
-                at = __shfl(at, 0, RR_WAVE);
-                if (myc[j] == c) perm[cbase[c] + at + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = (uint16_t)i;
+            for (int k = 0; k < 4; ++k) {
+                const uint64_t cc = c + k * NT;
+                if (cc < cw1) __builtin_nontemporal_store(x[k], dst + cc);
+                if (staged && cc >= cs0) lds[cc - cs0] = x[k];
             }
         }
+        for (; c < ce; c += NT) {
+            const u32x4 x = src[c];
+            if (c < cw1) __builtin_nontemporal_store(x, dst + c);
+            if (staged && c >= cs0) lds[c - cs0] = x;
+        }
     }
-    __syncthreads();
+    // values that do not fit the stage are read from global memory; if even their 32-bit
+    // window-relative offsets could overflow, the exact parser takes them
+    const bool far = !staged && S1 - S0 > 0xFFFFFF00ull;
+    const LdsSrc lsrc{(lds_cptr)stage};
+    const GlbSrc gsrc{make_rsrc(blob + S0, (uint32_t)(data_cap - S0 < 0xFFFFFFFFull ? data_cap - S0 : 0xFFFFFFFFull))};
 
-    // 3. single-class batches of <= 64 values, taken dynamically by the waves
-    const rsrc_t R = make_rsrc(blob + B, (uint32_t)(data_cap - B < 0xFFFFFFFFull ? data_cap - B : 0xFFFFFFFFull));
     uint64_t bad = 0, pay = 0;
-    const uint32_t nb = bpre[C_N];
-    for (;;) {
-        uint32_t bi = 0;
-        if (lane == 0) bi = atomicAdd(&next_batch, 1u);
-        bi = __builtin_amdgcn_readfirstlane(__shfl(bi, 0, RR_WAVE));
-        if (bi >= nb) break;
-        uint32_t k = 0;
-        while (bi >= bpre[k + 1]) ++k;
-        const uint32_t c = CLASS_ORDER[k];
-        const uint32_t first = cbase[c] + (bi - bpre[k]) * RR_WAVE;
-        const uint32_t cnt = min(ccount[c] - (bi - bpre[k]) * RR_WAVE, (uint32_t)RR_WAVE);
-        if (lane < cnt) {
-            const uint64_t v = v0 + perm[first + lane];
-            if (c == C_EXACT) {
-                exact_value(blob, v, offsets, ebase, values, elems, cap, bad, pay);
-            } else {
-                const uint64_t o = offsets[v], o1 = offsets[v + 1], eb = ebase[v], r = ebase[v + 1] - eb;
-                Lane l;
-                l.q = (uint32_t)(o - B);
-                l.L = (uint32_t)(o1 - o);
-                l.B = B;
-                l.el = elems + eb;
-                l.r = (uint32_t)r;
-                l.ok = eb + r <= cap;
-                Head H;
-                gread<4>(R, l.q, H.h);
-                uint32_t ne = 1, enc = 0;
-                uint64_t vp = 0;   // this value's payload bytes (counted once it is emitted)
-                bool fail = false;
-                if (c == C_STR) {
-                    do_string(H, l, vp);
-                    enc = H.b5();
-                } else if (c == C_IS) {
-                    do_intset(R, H, l);
-                    ne = H.f9();
-                    enc = H.f5();
-                } else if (c == C_LIST) {
-                    fail = do_list(R, l, ne, vp);
-                } else if (c == C_HT) {
-                    fail = do_ht(R, H, l, ne, vp);
-                } else if (c == C_SL) {
-                    fail = do_skiplist(R, H, l, ne, vp);
-                } else {
-                    fail = do_ziplist(R, l, ne, vp);
+    for (uint64_t c0 = v_lo; c0 < v_hi; c0 += PMAX) {
+        const uint32_t nv = (uint32_t)(v_hi - c0 < PMAX ? v_hi - c0 : PMAX);
+        // 2. counting sort by class (ballot per class, one LDS atomic per class per wave-round)
+        if (tid < C_N) { ccount[tid] = 0; ccur[tid] = 0; }
+        if (tid == 0) next_batch = 0;
+        __syncthreads();   // also: the stage is complete; the previous chunk's batches are done
+        uint32_t myc[PMAX / NT];
+#pragma unroll
+        for (uint32_t j = 0; j < PMAX / NT; ++j) {
+            const uint32_t i = j * NT + tid;
+            myc[j] = i < nv ? (far ? C_EXACT : (uint32_t)cls[c0 + i]) : C_N;
+#pragma unroll
+            for (uint32_t c = 0; c < C_N; ++c) {
+                const uint64_t m = __ballot(myc[j] == c);
+                if (m && lane == 0) atomicAdd(&ccount[c], (uint32_t)__popcll(m));
+            }
+        }
+        __syncthreads();
+        if (tid == 0) {
+            uint32_t s = 0, bs = 0;
+            for (uint32_t k = 0; k < C_N; ++k) {
+                const uint32_t c = CLASS_ORDER[k];
+                cbase[c] = s;
+                bpre[k] = bs;
+                s += ccount[c];
+                bs += (ccount[c] + RR_WAVE - 1) / RR_WAVE;
+            }
+            bpre[C_N] = bs;
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t j = 0; j < PMAX / NT; ++j) {
+            const uint32_t i = j * NT + tid;
+#pragma unroll
+            for (uint32_t c = 0; c < C_N; ++c) {
+                const uint64_t m = __ballot(myc[j] == c);
+                if (m) {
+                    uint32_t at = 0;
+                    if (lane == 0) at = atomicAdd(&ccur[c], (uint32_t)__popcll(m));
+                    at = __shfl(at, 0, RR_WAVE);
+                    if (myc[j] == c) perm[cbase[c] + at + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = (uint16_t)i;
                 }
-                if (fail) {
-                    exact_value(blob, v, offsets, ebase, values, elems, cap, bad, pay);
-                } else {
-                    put_value(values + v, H.type(), enc, l.ok ? RR_OK : RR_E_CAPACITY, H.lru(), ne, (uint32_t)eb);
-                    bad += l.ok ? 0 : 1;
-                    pay += l.ok ? vp : 0;
-                }
+            }
+        }
+        __syncthreads();
+
+        // 3. single-class batches, taken dynamically by the waves
+        const uint32_t nb = bpre[C_N];
+        for (;;) {
+            uint32_t bi = 0;
+            if (lane == 0) bi = atomicAdd(&next_batch, 1u);
+            bi = __builtin_amdgcn_readfirstlane(__shfl(bi, 0, RR_WAVE));
+            if (bi >= nb) break;
+            uint32_t k = 0;
+            while (bi >= bpre[k + 1]) ++k;
+            const uint32_t c = CLASS_ORDER[k];
+            const uint32_t first = cbase[c] + (bi - bpre[k]) * RR_WAVE;
+            const uint32_t cnt = min(ccount[c] - (bi - bpre[k]) * RR_WAVE, (uint32_t)RR_WAVE);
+            if (lane < cnt) {
+                const uint64_t v = c0 + perm[first + lane];
+                if (staged)
+                    run_batch(lsrc, c, v, S0, blob, offsets, ebase, values, elems, cap, bad, pay);
+                else
+                    run_batch(gsrc, c, v, S0, blob, offsets, ebase, values, elems, cap, bad, pay);
             }
         }
     }
@@ -941,13 +991,20 @@ __global__ __launch_bounds__(WG) void encode_kernel(const rr_value *__restrict__
 }  // namespace
 
 // ---------------------------------------------------------------------------------------- launch
-#ifndef RR_DEC_T
-#define RR_DEC_T 2048
+#ifndef RR_DEC_W
+#define RR_DEC_W 65536
+#endif
+#ifndef RR_DEC_SLACK
+#define RR_DEC_SLACK 8192
 #endif
 #ifndef RR_DEC_NW
 #define RR_DEC_NW 8
 #endif
-constexpr uint32_t DEC_T = RR_DEC_T, DEC_NW = RR_DEC_NW;
+#ifndef RR_DEC_PMAX
+#define RR_DEC_PMAX 2048
+#endif
+constexpr uint32_t DEC_W = RR_DEC_W, DEC_NW = RR_DEC_NW;
+#define DECODE_KERNEL decode_kernel<RR_DEC_W, RR_DEC_SLACK, RR_DEC_NW, RR_DEC_PMAX>
 
 // Resident workgroup count for a persistent launch: occupancy query minus one block per CU
 // (the API over-reports by one for SGPR-heavy kernels, MI355X_MICROARCH.md §Residency).
@@ -969,39 +1026,41 @@ extern "C" uint64_t rr_encode_scratch_words(uint64_t n) {
     return RR_SCRATCH_HDR + 4 * t + t / 64 + 2;
 }
 
-static uint64_t dec_tiles(uint64_t n) { return (n + DEC_T - 1) / DEC_T; }
+// windows: sized from data_cap (>= offsets[n], host-known without a sync); windows past
+// offsets[n] own no values and copy nothing
+static uint64_t dec_windows(uint64_t data_cap) { return data_cap / DEC_W + 1; }
 
 // Decode scratch (uint64 words): [HDR] [scan: ticket, look-back state + groups]
-// [counts -> elem_base, n+1] [tile stats, 3 per tile] [class bytes, n].
+// [counts -> elem_base, n+1] [window stats, 3 per window] [first_val u32, nwin+1]
+// [class bytes, n].
 extern "C" uint64_t rr_decode_scratch_words(uint64_t data_cap, uint64_t n) {
-    (void)data_cap;
-    const uint64_t st = scan_tiles(n);
-    return RR_SCRATCH_HDR + 1 + st + (st + LB_GROUP - 1) / LB_GROUP + (n + 1) + 3 * dec_tiles(n) + (n + 7) / 8 + 2;
+    const uint64_t st = scan_tiles(n), nw = dec_windows(data_cap);
+    return RR_SCRATCH_HDR + 1 + st + (st + LB_GROUP - 1) / LB_GROUP + (n + 1) + 3 * nw + (nw + 2) / 2 + (n + 7) / 8 + 2;
 }
 
 extern "C" hipError_t rr_launch_decode(const uint8_t *blob, const uint64_t *offsets, uint64_t n, rr_value *values,
                                        rr_elem *elems, uint64_t elem_cap, uint8_t *arena, uint64_t *scratch,
                                        uint64_t data_cap, rr_totals *totals, hipStream_t stream) {
-    const uint32_t st = (uint32_t)scan_tiles(n), nt = (uint32_t)dec_tiles(n);
+    const uint32_t st = (uint32_t)scan_tiles(n), nw = (uint32_t)dec_windows(data_cap);
     uint64_t *lb = scratch + RR_SCRATCH_HDR;
     const uint64_t lb_words = 1 + st + (st + LB_GROUP - 1) / LB_GROUP;
     uint64_t *counts = lb + lb_words;
     uint64_t *stats = counts + n + 1;
-    uint8_t *cls = reinterpret_cast<uint8_t *>(stats + 3 * (uint64_t)nt);
+    uint32_t *first_val = reinterpret_cast<uint32_t *>(stats + 3 * (uint64_t)nw);
+    uint8_t *cls = reinterpret_cast<uint8_t *>(first_val + ((nw + 2) & ~1u));
     hipError_t e = hipMemsetAsync(lb, 0, ((lb_words * 8) + 15) & ~(size_t)15, stream);
     if (e != hipSuccess) return e;
-    if (n) {
-        hipLaunchKernelGGL(count_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, stream, blob, offsets, n,
-                           counts, cls);
-        hipLaunchKernelGGL(scan_kernel, dim3(st), dim3(256), 0, stream, counts, n, lb, st);
-        hipLaunchKernelGGL((decode_kernel<DEC_T, DEC_NW>), dim3(nt), dim3(DEC_NW * RR_WAVE), 0, stream, blob,
-                           data_cap, offsets, n, cls, counts, values, elems, elem_cap, arena, stats);
-    } else {
+    hipLaunchKernelGGL(count_kernel, dim3((uint32_t)((n + 1 + 255) / 256)), dim3(256), 0, stream, blob, offsets, n,
+                       first_val, nw, DEC_W, counts, cls);
+    if (st) hipLaunchKernelGGL(scan_kernel, dim3(st), dim3(256), 0, stream, counts, n, lb, st);
+    else {
         e = hipMemsetAsync(counts, 0, sizeof(uint64_t), stream);
         if (e != hipSuccess) return e;
     }
+    hipLaunchKernelGGL((DECODE_KERNEL), dim3(nw), dim3(DEC_NW * RR_WAVE), 0, stream, blob, data_cap, offsets, n,
+                       first_val, cls, counts, values, elems, elem_cap, arena, stats);
     e = hipGetLastError();
-    if (e == hipSuccess && totals) e = launch_finalize(stats, counts + n, nt, offsets, n, 2, totals, stream);
+    if (e == hipSuccess && totals) e = launch_finalize(stats, counts + n, nw, offsets, n, 2, totals, stream);
     return e;
 }
 
