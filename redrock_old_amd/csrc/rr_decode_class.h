@@ -84,40 +84,39 @@ __device__ __forceinline__ uint32_t ab(uint32_t hi, uint32_t lo, uint32_t s) { r
 // A 20-digit magnitude is always >= 1e19 > 2^63, so more than 20 bytes fails; up to 19 digits
 // cannot overflow uint64 while accumulating.
 __device__ __forceinline__ bool regs_try_int(const uint32_t (&b)[5], uint32_t len, int64_t &out) {
-    if (len == 0 || len > 20) return false;
+    // straight-line (selects only): every digit position is evaluated, out-of-range ones are
+    // masked, so a wave pays one pass whatever mix of lengths its lanes hold
     const uint32_t c0 = b[0] & 0xFF;
-    if (len == 1 && c0 == '0') { out = 0; return true; }
     const uint32_t neg = c0 == '-' ? 1u : 0u;
-    const uint32_t nd = len - neg;
-    if (nd == 0 || nd > 19) return false;
     bool ok = true;
     uint64_t v = 0;
 #pragma unroll
     for (uint32_t j = 0; j < 20; ++j) {
-        const uint32_t c = (b[j >> 2] >> (8 * (j & 3))) & 0xFF;
-        if (j >= neg && j < len) {
-            ok &= j == neg ? (c - '1' <= 8u) : (c - '0' <= 9u);
-            v = v * 10 + (c - '0');
-        }
+        const uint32_t d = ((b[j >> 2] >> (8 * (j & 3))) & 0xFF) - '0';
+        const bool in = j >= neg && j < len;
+        ok &= !in | (j == neg ? d - 1u <= 8u : d <= 9u);
+        v = v * (in ? 10u : 1u) + (in ? d : 0u);   // (a select of the product would compile to a branch)
     }
-    if (!ok) return false;
-    if (neg) {
-        if (v > (1ull << 63)) return false;
-        out = (int64_t)(0ull - v);
-    } else {
-        if (v > 0x7FFFFFFFFFFFFFFFull) return false;
-        out = (int64_t)v;
-    }
-    return true;
+    const uint32_t nd = len - neg;
+    const bool zero = len == 1 && c0 == '0';
+    ok = zero | (ok & (len <= 20) & (nd - 1u <= 18u) & (v <= 0x7FFFFFFFFFFFFFFFull + neg));
+    out = zero ? 0 : neg ? (int64_t)(0ull - v) : (int64_t)v;
+    return ok;
 }
 
-__device__ __forceinline__ void put_desc(rr_elem *e, uint64_t data, uint32_t len, uint32_t kind, uint32_t zenc) {
-    uint4 w;
+// Descriptor stores go through a buffer descriptor over the window's slot range: a slot
+// offset of NOSLOT (lanes whose value does not fit the caller's capacity) is out of range and
+// the hardware drops the store, so no store needs a branch.
+constexpr uint32_t NOSLOT = 0xFFFFFFF0u;
+__device__ __forceinline__ void put_desc(rsrc_t E, uint32_t off, uint64_t data, uint32_t len, uint32_t kind,
+                                         uint32_t zenc) {
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    v4u w;
     w.x = (uint32_t)data;
     w.y = (uint32_t)(data >> 32);
     w.z = len;
     w.w = kind | (zenc << 8);
-    *reinterpret_cast<uint4 *>(e) = w;
+    __builtin_amdgcn_raw_buffer_store_b128(w, E, (int)off, 0, 0);
 }
 
 __device__ __forceinline__ void put_value(rr_value *v, uint32_t type, uint32_t enc, uint32_t status, uint32_t lru,
@@ -130,15 +129,18 @@ __device__ __forceinline__ void put_value(rr_value *v, uint32_t type, uint32_t e
     *reinterpret_cast<uint4 *>(v) = w;
 }
 
-// One lane's value in a batch.  q: tile-relative offset of the blob, L: its length; B: batch
-// offset of tile byte 0 (descriptor data = B + tile position, the mirror-arena offset);
-// eb / r: slot base and reservation; ok: the reservation fits the caller's capacity.
+// One lane's value in a batch.  q: source-relative offset of the blob, L: its length; B: batch
+// offset of source byte 0 (descriptor data = B + source position, the mirror-arena offset);
+// r: its reservation; ok: the reservation fits the caller's capacity.
 struct Lane {
     uint32_t q, L;
     uint64_t B;
-    rr_elem *el;       // elems + eb
+    rsrc_t E;          // descriptors of the window
+    uint32_t so;       // byte offset of slot eb in E
     uint32_t r;
     bool ok;
+    // byte offset of the value's slot k, or NOSLOT when its slots do not fit
+    __device__ __forceinline__ uint32_t slot(uint32_t k) const { return ok ? so + 16 * k : NOSLOT; }
 };
 
 // header bytes 0..15 of the value: type | lru (bytes 1..4) | byte 5 | bytes 5..8 | bytes 9..12
@@ -155,9 +157,9 @@ struct Head {
 // ---- String (rock_serdes.c:114-158): enc INT -> inline i64, RAW/EMBSTR -> bytes 6..L
 __device__ __forceinline__ void do_string(const Head &H, const Lane &l, uint64_t &pay) {
     if (H.b5() == RR_ENC_INT) {
-        if (l.ok) put_desc(l.el, (uint64_t)ab(H.h[2], H.h[1], 2) | ((uint64_t)ab(H.h[3], H.h[2], 2) << 32), 0, RR_K_INT, 0);
+        put_desc(l.E, l.slot(0), (uint64_t)ab(H.h[2], H.h[1], 2) | ((uint64_t)ab(H.h[3], H.h[2], 2) << 32), 0, RR_K_INT, 0);
     } else {
-        if (l.ok) put_desc(l.el, l.B + l.q + 6, l.L - 6, RR_K_STR, 0);
+        put_desc(l.E, l.slot(0), l.B + l.q + 6, l.L - 6, RR_K_STR, 0);
         pay += l.L - 6;
     }
 }
@@ -166,16 +168,20 @@ __device__ __forceinline__ void do_string(const Head &H, const Lane &l, uint64_t
 template <class Src>
 __device__ __forceinline__ void do_intset(const Src &R, const Head &H, const Lane &l) {
     const uint32_t w = H.f5(), cnt = H.f9();
-    if (!l.ok) return;
+    if (!l.ok) return;   // (no stores: loop-invariant per lane)
     uint32_t p = l.q + 13;
     for (uint32_t k = 0; k < cnt; ++k, p += w) {
         uint32_t x[2];
         R.template get<2>(p, x);
         const int64_t v = w == 2 ? (int64_t)(int16_t)(x[0] & 0xFFFF)
                         : w == 4 ? (int64_t)(int32_t)x[0] : (int64_t)((uint64_t)x[0] | ((uint64_t)x[1] << 32));
-        put_desc(l.el + k, (uint64_t)v, 0, RR_K_INT, 0);
+        put_desc(l.E, l.so + 16 * k, (uint64_t)v, 0, RR_K_INT, 0);
     }
 }
+
+// The walks are software-pipelined: a step computes the next cursor from the bytes it holds
+// and issues the read there (clamped into the value) BEFORE its checks and descriptor store,
+// so the read's latency overlaps them; the loop-carried chain is read -> size -> next read.
 
 // ---- List (rock_serdes.c:162-214): {u32 len, bytes}* to the end; integer-looking entries
 // become INT (quicklistPushTail re-encodes them, ziplist.c:480)
@@ -184,21 +190,26 @@ __device__ __forceinline__ bool do_list(const Src &R, const Lane &l, uint32_t &n
     uint32_t p = l.q + 5, k = 0;
     const uint32_t end = l.q + l.L;
     bool fail = false;
-    while (p != end) {
-        uint32_t b[6];   // len + 20 bytes
-        R.template get<6>(p, b);
+    uint32_t b[6];   // len + 20 bytes
+    R.template get<6>(p, b);
+    for (;;) {
         const uint32_t rem = end - p, len = b[0];
-        if (rem < 4 || len > rem - 4 || k >= l.r) { fail = true; break; }
+        const uint64_t nx = (uint64_t)p + 4 + len;
+        const uint32_t pn = nx < end ? (uint32_t)nx : end;
+        uint32_t bn[6];
+        R.template get<6>(pn, bn);
+        const bool done = p == end;
+        const bool bad = rem < 4 || len > rem - 4 || k >= l.r;
+        if (done || bad) { fail = !done; break; }
         const uint32_t d[5] = {b[1], b[2], b[3], b[4], b[5]};
         int64_t iv;
-        if (regs_try_int(d, len, iv)) {
-            if (l.ok) put_desc(l.el + k, (uint64_t)iv, 0, RR_K_INT, 0);
-        } else {
-            if (l.ok) put_desc(l.el + k, l.B + p + 4, len, RR_K_STR, 0);
-            pay += len;
-        }
+        const bool isint = regs_try_int(d, len, iv);
+        put_desc(l.E, l.slot(k), isint ? (uint64_t)iv : l.B + p + 4, isint ? 0 : len, isint ? RR_K_INT : RR_K_STR, 0);
+        pay += isint ? 0 : len;
         ++k;
-        p += 4 + len;
+        p = pn;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) b[i] = bn[i];
     }
     n = k;
     return fail || k != l.r;
@@ -211,15 +222,23 @@ __device__ __forceinline__ bool do_ht(const Src &R, const Head &H, const Lane &l
     uint32_t p = l.q + 13, k = 0;
     const uint32_t end = l.q + l.L;
     bool fail = false;
-    while (p != end) {
-        uint32_t b[2];
-        R.template get<2>(p, b);
+    uint32_t b[2];
+    R.template get<2>(p, b);
+    for (;;) {
         const uint32_t rem = end - p;
-        if (rem < 8 || b[1] != 0 || b[0] > rem - 8 || k >= l.r) { fail = true; break; }
-        if (l.ok) put_desc(l.el + k, l.B + p + 8, b[0], RR_K_STR, 0);
+        const uint64_t nx = (uint64_t)p + 8 + b[0];
+        const uint32_t pn = (nx < end && b[1] == 0) ? (uint32_t)nx : end;
+        uint32_t bn[2];
+        R.template get<2>(pn, bn);
+        const bool done = p == end;
+        const bool bad = rem < 8 || b[1] != 0 || b[0] > rem - 8 || k >= l.r;
+        if (done || bad) { fail = !done; break; }
+        put_desc(l.E, l.slot(k), l.B + p + 8, b[0], RR_K_STR, 0);
         pay += b[0];
         ++k;
-        p += 8 + b[0];
+        p = pn;
+        b[0] = bn[0];
+        b[1] = bn[1];
     }
     n = k;
     const bool cnt_ok = H.type() == RR_TYPE_SET_HT ? (uint64_t)k == cnt : ((k & 1) == 0 && (uint64_t)(k >> 1) == cnt);
@@ -233,21 +252,25 @@ __device__ __forceinline__ bool do_skiplist(const Src &R, const Head &H, const L
     uint32_t p = l.q + 13, k = 0;
     const uint32_t end = l.q + l.L;
     bool fail = false;
-    while (p != end) {
-        uint32_t b[2];
-        R.template get<2>(p, b);
+    uint32_t b[2];
+    R.template get<2>(p, b);
+    for (;;) {
         const uint32_t rem = end - p;
-        if (rem < 8 || k >= l.r) { fail = true; break; }
-        if (k & 1) {
-            if (l.ok) put_desc(l.el + k, (uint64_t)b[0] | ((uint64_t)b[1] << 32), 0, RR_K_SCORE, 0);
-            p += 8;
-        } else {
-            if (b[1] != 0 || b[0] > rem - 8) { fail = true; break; }
-            if (l.ok) put_desc(l.el + k, l.B + p + 8, b[0], RR_K_STR, 0);
-            pay += b[0];
-            p += 8 + b[0];
-        }
+        const bool score = (k & 1) != 0;
+        const uint64_t nx = (uint64_t)p + 8 + (score ? 0u : b[0]);
+        const uint32_t pn = (nx < end && (score || b[1] == 0)) ? (uint32_t)nx : end;
+        uint32_t bn[2];
+        R.template get<2>(pn, bn);
+        const bool done = p == end;
+        const bool bad = rem < 8 || k >= l.r || (!score && (b[1] != 0 || b[0] > rem - 8));
+        if (done || bad) { fail = !done; break; }
+        put_desc(l.E, l.slot(k), score ? ((uint64_t)b[0] | ((uint64_t)b[1] << 32)) : l.B + p + 8, score ? 0 : b[0],
+                 score ? RR_K_SCORE : RR_K_STR, 0);
+        pay += score ? 0 : b[0];
         ++k;
+        p = pn;
+        b[0] = bn[0];
+        b[1] = bn[1];
     }
     n = k;
     return fail || (k & 1) || (uint64_t)(k >> 1) != cnt || k != l.r;
@@ -260,16 +283,14 @@ __device__ __forceinline__ bool do_ziplist(const Src &R, const Lane &l, uint32_t
     const uint32_t zl0 = l.q + 13, zend = l.q + l.L, zlast = zend - 1;   // zlast: the 0xFF byte
     uint32_t z[3];
     R.template get<3>(zl0, z);   // zlbytes, zltail, zllen
-    if (l.ok) put_desc(l.el, l.B + zl0, l.L - 13, RR_K_ZLRAW, 0);
+    put_desc(l.E, l.slot(0), l.B + zl0, l.L - 13, RR_K_ZLRAW, 0);
     pay += l.L - 13;
     uint32_t p = zl0 + 10, prev_raw = 0, last = zl0 + 10, k = 1;
     bool fail = false;
+    uint32_t b[4];   // prevlen (1 or 5) + encoding + up to 9 more bytes
+    R.template get<4>(p, b);
     for (;;) {
-        uint32_t b[4];   // prevlen (1 or 5) + encoding + up to 9 more bytes
-        R.template get<4>(p, b);
         const uint32_t b0 = b[0] & 0xFF;
-        if (p >= zend) { fail = true; break; }
-        if (b0 == 0xFF) break;
         // every field of the entry header from registers, as selects (no per-encoding branches)
         const bool big = b0 >= 254;
         const uint32_t pl = big ? ab(b[1], b[0], 1) : b0;
@@ -278,25 +299,37 @@ __device__ __forceinline__ bool do_ziplist(const Src &R, const Lane &l, uint32_t
         const uint32_t x1 = big ? (b[1] >> 16) & 0xFF : (b[0] >> 16) & 0xFF;
         const uint32_t lo = big ? ab(b[2], b[1], 2) : ab(b[1], b[0], 2);   // bytes after the encoding byte
         const uint32_t hi = big ? ab(b[3], b[2], 2) : ab(b[2], b[1], 2);
+        // (bitwise | and arithmetic selects, not || / ?: chains: the compiler turns those into
+        // exec-mask branches, ~60 % of the step's instructions)
         const bool zstr = e < 0xC0;
-        const uint32_t scls = e >> 6;   // string length class 0 / 1 / 2
-        const uint32_t ls = scls == 0 ? 1u : scls == 1 ? 2u : 5u;
-        const uint32_t sl = scls == 0 ? (e & 0x3F) : scls == 1 ? (((e & 0x3F) << 8) | x1) : __builtin_bswap32(lo);
+        const uint32_t scls = e >> 6;                        // string length class 0 / 1 / 2
+        const uint32_t ls = 1 + scls + 2 * (scls >> 1);      // 1 / 2 / 5 length bytes
+        const uint32_t sl1 = scls == 0 ? (e & 0x3F) : (((e & 0x3F) << 8) | x1);
+        const uint32_t sl = scls >= 2 ? __builtin_bswap32(lo) : sl1;
         const bool imm = e - 0xF1u <= 0xFDu - 0xF1u;
-        const uint32_t isz = e == 0xFE ? 1u : e == 0xC0 ? 2u : e == 0xF0 ? 3u : e == 0xD0 ? 4u : e == 0xE0 ? 8u : 0u;
-        const int64_t i8 = (int8_t)(lo & 0xFF), i16 = (int16_t)(lo & 0xFFFF), i24 = ((int32_t)(lo << 8)) >> 8;
-        const int64_t i32 = (int32_t)lo, i64 = (int64_t)((uint64_t)lo | ((uint64_t)hi << 32));
-        const int64_t iv = imm ? (int64_t)(e & 0x0F) - 1 : isz == 1 ? i8 : isz == 2 ? i16 : isz == 3 ? i24 : isz == 4 ? i32 : i64;
-        const uint64_t endp = zstr ? (uint64_t)qp + ls + sl : (uint64_t)qp + 1 + isz;
-        const bool bad = (big && p + 5 > zlast) || pl != prev_raw || qp >= zlast || k >= l.r ||
-                         (!zstr && !imm && isz == 0) || (zstr && qp + ls > zlast) || endp > zlast;
-        if (bad) { fail = true; break; }
-        if (l.ok) put_desc(l.el + k, zstr ? l.B + qp + ls : (uint64_t)iv, zstr ? sl : 0, zstr ? RR_K_STR : RR_K_INT,
-                           zstr ? (e & 0xC0) : e);
+        const uint32_t isz = (uint32_t)(e == 0xFE) + 2 * (uint32_t)(e == 0xC0) + 3 * (uint32_t)(e == 0xF0) +
+                             4 * (uint32_t)(e == 0xD0) + 8 * (uint32_t)(e == 0xE0);
+        const uint64_t endp = (uint64_t)qp + (zstr ? ls + sl : 1 + isz);
+        const uint32_t pn = endp < zlast ? (uint32_t)endp : zlast;
+        uint32_t bn[4];
+        R.template get<4>(pn, bn);
+        const bool done = (b0 == 0xFF) & (p < zend);
+        const bool bad = (p >= zend) | (big & (p + 5 > zlast)) | (pl != prev_raw) | (qp >= zlast) | (k >= l.r) |
+                         (!zstr & !imm & (isz == 0)) | (zstr & (qp + ls > zlast)) | (endp > zlast);
+        if (done | bad) { fail = !done; break; }
+        // little-endian integer of isz (1..4) bytes, sign-extended by a shift pair; 8 bytes; or
+        // the 4-bit immediate
+        const uint32_t sh = (32 - 8 * isz) & 31;
+        const int64_t v32 = (int32_t)(lo << sh) >> sh;
+        const int64_t iv = isz == 8 ? (int64_t)((uint64_t)lo | ((uint64_t)hi << 32)) : imm ? (int64_t)(e & 0x0F) - 1 : v32;
+        put_desc(l.E, l.slot(k), zstr ? l.B + qp + ls : (uint64_t)iv, zstr ? sl : 0, zstr ? RR_K_STR : RR_K_INT,
+                 zstr ? (e & 0xC0) : e);
         prev_raw = (uint32_t)endp - p;
         last = p;
-        p = (uint32_t)endp;
+        p = pn;
         ++k;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) b[i] = bn[i];
     }
     n = k;
     const uint32_t entries = k - 1, zllen = z[2] & 0xFFFF;

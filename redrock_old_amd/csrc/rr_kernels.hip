@@ -506,10 +506,17 @@ __global__ __launch_bounds__(256) void scan_kernel(uint64_t *__restrict__ counts
 // ---- K3: tiles: mirror copy + class sort + single-class batches ------------------------
 // The exact parser, lane = value v (from global memory): the reference's status codes for
 // malformed values, zero-filled slots, capacity handling.
-__device__ __forceinline__ void exact_value(const uint8_t *__restrict__ blob, uint64_t v,
-                                            const uint64_t *__restrict__ offsets, const uint64_t *__restrict__ ebase,
-                                            rr_value *__restrict__ values, rr_elem *__restrict__ elems,
-                                            uint64_t cap, uint64_t &bad, uint64_t &pay) {
+// per-value contribution to the window totals (returned by value: accumulators passed by
+// reference were merged into one dynamically-addressed update and spilled to scratch)
+struct Acc {
+    uint32_t bad;
+    uint64_t pay;
+};
+
+__device__ __forceinline__ Acc exact_value(const uint8_t *__restrict__ blob, uint64_t v,
+                                           const uint64_t *__restrict__ offsets, const uint64_t *__restrict__ ebase,
+                                           rr_value *__restrict__ values, rr_elem *__restrict__ elems, uint64_t cap) {
+    uint64_t pay = 0;
     const uint64_t o_lo = offsets[v], o_hi = offsets[v + 1];
     const uint64_t eb = ebase[v], r = ebase[v + 1] - eb;
     const uint8_t *b = blob + o_lo;
@@ -531,7 +538,7 @@ __device__ __forceinline__ void exact_value(const uint8_t *__restrict__ blob, ui
     const uint32_t len = (uint32_t)(o_hi - o_lo);
     put_value(values + v, len ? ld_u8(b) : 0, pr.enc, status, len >= 5 ? ld_u32(b + 1) : 0, (uint32_t)ne,
               (uint32_t)eb);
-    bad += status != RR_OK ? 1 : 0;
+    return Acc{status != RR_OK ? 1u : 0u, pay};
 }
 
 // class batch order: heaviest walks first (longest-job-first over the window's waves)
@@ -540,20 +547,18 @@ __constant__ uint32_t CLASS_ORDER[C_N] = {C_ZL, C_SL, C_HT, C_LIST, C_EXACT, C_I
 // One single-class batch: lane < cnt decodes value v (byte offsets relative to the source,
 // whose byte 0 is batch offset B).
 template <class Src>
-__device__ __forceinline__ void run_batch(const Src &src, uint32_t c, uint64_t v, uint64_t B,
-                                          const uint8_t *__restrict__ blob, const uint64_t *__restrict__ offsets,
-                                          const uint64_t *__restrict__ ebase, rr_value *__restrict__ values,
-                                          rr_elem *__restrict__ elems, uint64_t cap, uint64_t &bad, uint64_t &pay) {
-    if (c == C_EXACT) {
-        exact_value(blob, v, offsets, ebase, values, elems, cap, bad, pay);
-        return;
-    }
+__device__ __forceinline__ Acc run_batch(const Src &src, uint32_t c, uint64_t v, uint64_t B, rsrc_t E, uint64_t eb0,
+                                         const uint8_t *__restrict__ blob, const uint64_t *__restrict__ offsets,
+                                         const uint64_t *__restrict__ ebase, rr_value *__restrict__ values,
+                                         rr_elem *__restrict__ elems, uint64_t cap) {
+    if (c == C_EXACT) return exact_value(blob, v, offsets, ebase, values, elems, cap);
     const uint64_t o = offsets[v], o1 = offsets[v + 1], eb = ebase[v], r = ebase[v + 1] - eb;
     Lane l;
     l.q = (uint32_t)(o - B);
     l.L = (uint32_t)(o1 - o);
     l.B = B;
-    l.el = elems + eb;
+    l.E = E;
+    l.so = (uint32_t)(eb - eb0) * 16;
     l.r = (uint32_t)r;
     l.ok = eb + r <= cap;
     Head H;
@@ -577,13 +582,9 @@ __device__ __forceinline__ void run_batch(const Src &src, uint32_t c, uint64_t v
     } else {
         fail = do_ziplist(src, l, ne, vp);
     }
-    if (fail) {
-        exact_value(blob, v, offsets, ebase, values, elems, cap, bad, pay);
-    } else {
-        put_value(values + v, H.type(), enc, l.ok ? RR_OK : RR_E_CAPACITY, H.lru(), ne, (uint32_t)eb);
-        bad += l.ok ? 0 : 1;
-        pay += l.ok ? vp : 0;
-    }
+    if (fail) return exact_value(blob, v, offsets, ebase, values, elems, cap);
+    put_value(values + v, H.type(), enc, l.ok ? RR_OK : RR_E_CAPACITY, H.lru(), ne, (uint32_t)eb);
+    return Acc{l.ok ? 0u : 1u, l.ok ? vp : 0};
 }
 
 // Workgroup per byte WINDOW of W bytes: window t owns the values whose first byte lies in
@@ -593,8 +594,13 @@ __device__ __forceinline__ void run_batch(const Src &src, uint32_t c, uint64_t v
 //   2. per chunk of <= PMAX of its values: counting-sorts them by class in LDS;
 //   3. its waves take single-class batches of <= 64 values, heaviest class first, and walk +
 //      emit them from LDS (from global memory when the values did not fit the stage).
+#ifdef RR_DEC_WPE   // tuning: ask the register allocator for this many waves per SIMD
+#define DEC_WPE_ATTR __attribute__((amdgpu_waves_per_eu(RR_DEC_WPE)))
+#else
+#define DEC_WPE_ATTR
+#endif
 template <uint32_t W, uint32_t SLACK, uint32_t NW, uint32_t PMAX>
-__global__ __launch_bounds__(NW * RR_WAVE) void decode_kernel(const uint8_t *__restrict__ blob, uint64_t data_cap,
+__global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const uint8_t *__restrict__ blob, uint64_t data_cap,
                                                               const uint64_t *__restrict__ offsets, uint64_t n,
                                                               const uint32_t *__restrict__ first_val,
                                                               const uint8_t *__restrict__ cls,
@@ -649,13 +655,23 @@ __global__ __launch_bounds__(NW * RR_WAVE) void decode_kernel(const uint8_t *__r
         }
     }
     // values that do not fit the stage are read from global memory; if even their 32-bit
-    // window-relative offsets could overflow, the exact parser takes them
-    const bool far = !staged && S1 - S0 > 0xFFFFFF00ull;
+    // window-relative byte or slot offsets could overflow, the exact parser takes them
+    const uint64_t eb0 = ebase[v_lo], eb1 = ebase[v_hi];
+    const bool far = (!staged && S1 - S0 > 0xFFFFFF00ull) || (eb1 - eb0) * 16 >= NOSLOT;
     const LdsSrc lsrc{(lds_cptr)stage};
     const GlbSrc gsrc{make_rsrc(blob + S0, (uint32_t)(data_cap - S0 < 0xFFFFFFFFull ? data_cap - S0 : 0xFFFFFFFFull))};
+    // the window's descriptor slots [eb0, eb1), cut at the capacity
+    const uint64_t ecut = eb1 < cap ? eb1 : cap;
+    const rsrc_t E = make_rsrc(reinterpret_cast<const uint8_t *>(elems + eb0),
+                               far || ecut <= eb0 ? 0u : (uint32_t)((ecut - eb0) * 16));
 
     uint64_t bad = 0, pay = 0;
-    for (uint64_t c0 = v_lo; c0 < v_hi; c0 += PMAX) {
+#ifdef RR_ABLATE   // timing-only builds (tools/): 1 = copy + stage only, 2 = + class sort, no batches
+    const uint64_t v_end = RR_ABLATE == 1 ? v_lo : v_hi;
+#else
+    const uint64_t v_end = v_hi;
+#endif
+    for (uint64_t c0 = v_lo; c0 < v_end; c0 += PMAX) {
         const uint32_t nv = (uint32_t)(v_hi - c0 < PMAX ? v_hi - c0 : PMAX);
         // 2. counting sort by class (ballot per class, one LDS atomic per class per wave-round)
         if (tid < C_N) { ccount[tid] = 0; ccur[tid] = 0; }
@@ -702,7 +718,11 @@ __global__ __launch_bounds__(NW * RR_WAVE) void decode_kernel(const uint8_t *__r
         __syncthreads();
 
         // 3. single-class batches, taken dynamically by the waves
+#if defined(RR_ABLATE) && RR_ABLATE == 2
+        const uint32_t nb = 0;
+#else
         const uint32_t nb = bpre[C_N];
+#endif
         for (;;) {
             uint32_t bi = 0;
             if (lane == 0) bi = atomicAdd(&next_batch, 1u);
@@ -715,10 +735,10 @@ __global__ __launch_bounds__(NW * RR_WAVE) void decode_kernel(const uint8_t *__r
             const uint32_t cnt = min(ccount[c] - (bi - bpre[k]) * RR_WAVE, (uint32_t)RR_WAVE);
             if (lane < cnt) {
                 const uint64_t v = c0 + perm[first + lane];
-                if (staged)
-                    run_batch(lsrc, c, v, S0, blob, offsets, ebase, values, elems, cap, bad, pay);
-                else
-                    run_batch(gsrc, c, v, S0, blob, offsets, ebase, values, elems, cap, bad, pay);
+                const Acc a = staged ? run_batch(lsrc, c, v, S0, E, eb0, blob, offsets, ebase, values, elems, cap)
+                                     : run_batch(gsrc, c, v, S0, E, eb0, blob, offsets, ebase, values, elems, cap);
+                bad += a.bad;
+                pay += a.pay;
             }
         }
     }
