@@ -89,13 +89,6 @@ int rr_ctx_reserve(rr_ctx *c, uint64_t n_values, uint64_t n_bytes) {
     return ensure_scratch(c, a > b ? a : b);
 }
 
-/* Diagnostics: copy the probe counters of the last call (probe build only; zeros otherwise). */
-int rr_probe_counters(rr_ctx *c, uint64_t *out, int n) {
-    if (!c || !c->scratch || n > 32) return RR_API_EINVAL;
-    HIPCHK(hipDeviceSynchronize());
-    HIPCHK(hipMemcpy(out, c->scratch + 8, (size_t)n * sizeof(uint64_t), hipMemcpyDeviceToHost));
-    return RR_API_OK;
-}
 
 uint64_t rr_decode_elem_bound(uint64_t n, uint64_t bytes) {
     /* every descriptor but a value's first consumes >= 2 blob bytes (ziplist entry / intset

@@ -594,6 +594,18 @@ __device__ __forceinline__ Acc run_batch(const Src &src, uint32_t c, uint64_t v,
 //   2. per chunk of <= PMAX of its values: counting-sorts them by class in LDS;
 //   3. its waves take single-class batches of <= 64 values, heaviest class first, and walk +
 //      emit them from LDS (from global memory when the values did not fit the stage).
+// Probe build (make VARIANT=probe EXTRA=-DRR_PROBE, tools/probe_decode.py): per-window phase
+// cycles and per-class batch cycles / counts / lanes into a buffer set by rr_probe_set
+// (PROBE_WORDS u64 per window).  Diagnostics only; the product build has none of it.
+constexpr uint32_t PROBE_WORDS = 32;
+#ifdef RR_PROBE
+__device__ uint64_t *g_probe;
+extern "C" int rr_probe_set(void *p) { return hipMemcpyToSymbol(HIP_SYMBOL(g_probe), &p, sizeof(p)) == hipSuccess ? 0 : -1; }
+#define PROBE(...) __VA_ARGS__
+#else
+#define PROBE(...)
+#endif
+
 #ifdef RR_DEC_WPE   // tuning: ask the register allocator for this many waves per SIMD
 #define DEC_WPE_ATTR __attribute__((amdgpu_waves_per_eu(RR_DEC_WPE)))
 #else
@@ -615,6 +627,8 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
     __shared__ uint32_t ccount[C_N], cbase[C_N], ccur[C_N], bpre[C_N + 1];
     __shared__ uint32_t next_batch;
     __shared__ uint64_t red[2][NW];
+    PROBE(__shared__ uint64_t prb[PROBE_WORDS]; uint64_t pt0 = __builtin_amdgcn_s_memtime(), pt1 = 0, pt2 = 0;
+          if (threadIdx.x < PROBE_WORDS) prb[threadIdx.x] = 0;)
     const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid / RR_WAVE;
     const uint32_t tile = blockIdx.x;
     const uint64_t v_lo = first_val[tile], v_hi = first_val[tile + 1];
@@ -677,6 +691,7 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
         if (tid < C_N) { ccount[tid] = 0; ccur[tid] = 0; }
         if (tid == 0) next_batch = 0;
         __syncthreads();   // also: the stage is complete; the previous chunk's batches are done
+        PROBE(if (c0 == v_lo) pt1 = __builtin_amdgcn_s_memtime();)
         uint32_t myc[PMAX / NT];
 #pragma unroll
         for (uint32_t j = 0; j < PMAX / NT; ++j) {
@@ -717,6 +732,7 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
         }
         __syncthreads();
 
+        PROBE(if (c0 == v_lo) pt2 = __builtin_amdgcn_s_memtime();)
         // 3. single-class batches, taken dynamically by the waves
 #if defined(RR_ABLATE) && RR_ABLATE == 2
         const uint32_t nb = 0;
@@ -733,6 +749,10 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
             const uint32_t c = CLASS_ORDER[k];
             const uint32_t first = cbase[c] + (bi - bpre[k]) * RR_WAVE;
             const uint32_t cnt = min(ccount[c] - (bi - bpre[k]) * RR_WAVE, (uint32_t)RR_WAVE);
+#ifdef RR_SKIP_CLASSES   // timing-only builds (tools/): skip the batches of these classes
+            if ((RR_SKIP_CLASSES >> c) & 1) continue;
+#endif
+            PROBE(const uint64_t tb0 = __builtin_amdgcn_s_memtime();)
             if (lane < cnt) {
                 const uint64_t v = c0 + perm[first + lane];
                 const Acc a = staged ? run_batch(lsrc, c, v, S0, E, eb0, blob, offsets, ebase, values, elems, cap)
@@ -740,6 +760,11 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
                 bad += a.bad;
                 pay += a.pay;
             }
+            PROBE(if (lane == 0) {
+                atomicAdd((unsigned long long *)&prb[3 + c], (unsigned long long)(__builtin_amdgcn_s_memtime() - tb0));
+                atomicAdd((unsigned long long *)&prb[10 + c], 1ull);
+                atomicAdd((unsigned long long *)&prb[17 + c], (unsigned long long)cnt);
+            })
         }
     }
     bad = wave_sum(bad);
@@ -752,6 +777,8 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
         stats[3 * (uint64_t)tile + 0] = tb;
         stats[3 * (uint64_t)tile + 1] = tp;
         stats[3 * (uint64_t)tile + 2] = 0;
+        PROBE(prb[0] = pt1 - pt0; prb[1] = pt2 - pt1; prb[2] = __builtin_amdgcn_s_memtime() - pt2; prb[24] = v_hi - v_lo;
+              prb[25] = staged; for (uint32_t i = 0; i < PROBE_WORDS; ++i) g_probe[(uint64_t)tile * PROBE_WORDS + i] = prb[i];)
     }
 }
 

@@ -1,0 +1,47 @@
+"""Diagnostics: per-window phase cycles and per-class batch cycles of the decode kernel.
+Build:  make -C redrock_old_amd/csrc VARIANT=probe EXTRA=-DRR_PROBE
+Run (GPU box):  RR_LIB=librr_serdes_probe.so python tools/probe_decode.py [config] [n]"""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+import redrock_old_amd as rr  # noqa: E402
+
+cfg = int(sys.argv[1]) if len(sys.argv) > 1 else 4
+n = int(sys.argv[2]) if len(sys.argv) > 2 else 1_000_000
+data, offs = rr.gen_batch(cfg, n)
+nb = int(offs[-1])
+dev = torch.device("cuda:0")
+eng = rr.Engine(0)
+eng.reserve(n, nb)
+d_data = torch.from_numpy(data).to(dev)
+d_offs = torch.from_numpy(offs.view(np.int64)).to(dev)
+cap = rr.elem_bound(n, nb)
+d_vals = torch.empty(n * 16, dtype=torch.uint8, device=dev)
+d_elems = torch.empty(cap * 16, dtype=torch.uint8, device=dev)
+d_arena = torch.empty((nb + 15) & ~15, dtype=torch.uint8, device=dev)
+d_tot = torch.zeros(4, dtype=torch.int64, device=dev)
+W = int(os.environ.get("RR_DEC_W", 65536))
+nwin = len(data) // W + 1
+probe = torch.zeros(nwin * 32, dtype=torch.int64, device=dev)
+L = rr.lib()
+L.rr_probe_set.argtypes = [C.c_void_p]
+assert L.rr_probe_set(C.c_void_p(probe.data_ptr())) == 0
+for _ in range(3):
+    eng.decode_device(d_data, d_offs, d_vals, d_elems, d_arena, d_tot)
+torch.cuda.synchronize()
+p = probe.cpu().numpy().reshape(nwin, 32).astype(np.float64)
+names = ["STR", "IS", "LIST", "HT", "SL", "ZL", "EXACT"]
+print(f"cfg {cfg}: {nwin} windows, staged {int(p[:, 25].sum())}, values/window {p[:, 24].mean():.1f}")
+print("phase cycles per window (mean / p90):  copy %.0f / %.0f   sort %.0f / %.0f   batches %.0f / %.0f" % (
+    p[:, 0].mean(), np.percentile(p[:, 0], 90), p[:, 1].mean(), np.percentile(p[:, 1], 90),
+    p[:, 2].mean(), np.percentile(p[:, 2], 90)))
+for c, nm in enumerate(names):
+    nbat = p[:, 10 + c].sum()
+    if nbat:
+        print(f"{nm:6s} batches {int(nbat):8d}  cycles/batch {p[:, 3 + c].sum() / nbat:9.0f}  lanes/batch {p[:, 17 + c].sum() / nbat:5.1f}")
