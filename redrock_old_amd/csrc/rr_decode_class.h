@@ -56,25 +56,63 @@ __device__ __forceinline__ void gread(rsrc_t R, uint32_t p, uint32_t (&o)[N]) {
     for (int i = 0; i < N; ++i) o[i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], sh);
 }
 
-// Byte sources for the walks.  p is relative to the source's base; get<N> returns bytes
-// [p, p + 4N) as N dwords (N+1 aligned reads + alignbyte).
+// Byte sources for the walks.  p is relative to the source's base.  fetch<N>(p) issues the
+// N+1 aligned dword reads covering bytes [p, p + 4N) and returns them raw; Raw::align turns
+// them into N dwords.  The walks fetch the NEXT cursor's bytes and align them only at the top
+// of the next step, so the read's latency overlaps the current step's checks and stores (an
+// align right after the read would make the compiler wait for it there).
+template <int N>
+struct Raw {
+    uint32_t w[N + 1];
+    uint32_t sh;
+    __device__ __forceinline__ void align(uint32_t (&o)[N]) const {
+#pragma unroll
+        for (int i = 0; i < N; ++i) o[i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], sh);
+    }
+};
+
 struct GlbSrc {   // global memory through a buffer descriptor: reads past its range give zeros
     rsrc_t R;
     template <int N>
-    __device__ __forceinline__ void get(uint32_t p, uint32_t (&o)[N]) const { gread<N>(R, p, o); }
+    __device__ __forceinline__ Raw<N> fetch(uint32_t p) const {
+        constexpr int D = N + 1;
+        Raw<N> r;
+        const uint32_t a = p & ~3u;
+        r.sh = p & 3u;
+#pragma unroll
+        for (int i = 0; i < D; i += 4) {
+            if (D - i >= 4) {
+                const auto v = __builtin_amdgcn_raw_buffer_load_b128(R, (int)(a + 4 * i), 0, 0);
+                r.w[i] = v[0]; r.w[i + 1] = v[1]; r.w[i + 2] = v[2]; r.w[i + 3] = v[3];
+            } else if (D - i == 3) {
+                const auto v = __builtin_amdgcn_raw_buffer_load_b96(R, (int)(a + 4 * i), 0, 0);
+                r.w[i] = v[0]; r.w[i + 1] = v[1]; r.w[i + 2] = v[2];
+            } else if (D - i == 2) {
+                const auto v = __builtin_amdgcn_raw_buffer_load_b64(R, (int)(a + 4 * i), 0, 0);
+                r.w[i] = v[0]; r.w[i + 1] = v[1];
+            } else {
+                r.w[i] = __builtin_amdgcn_raw_buffer_load_b32(R, (int)(a + 4 * i), 0, 0);
+            }
+        }
+        return r;
+    }
+    template <int N>
+    __device__ __forceinline__ void get(uint32_t p, uint32_t (&o)[N]) const { fetch<N>(p).align(o); }
 };
 struct LdsSrc {   // the workgroup's staged window; reads may run up to 64 bytes past it
     lds_cptr S;
     template <int N>
-    __device__ __forceinline__ void get(uint32_t p, uint32_t (&o)[N]) const {
+    __device__ __forceinline__ Raw<N> fetch(uint32_t p) const {
         const __attribute__((address_space(3))) uint32_t *W = (const __attribute__((address_space(3))) uint32_t *)S;
-        const uint32_t a = p >> 2, sh = p & 3;
-        uint32_t w[N + 1];
+        Raw<N> r;
+        const uint32_t a = p >> 2;
+        r.sh = p & 3;
 #pragma unroll
-        for (int i = 0; i <= N; ++i) w[i] = W[a + i];
-#pragma unroll
-        for (int i = 0; i < N; ++i) o[i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], sh);
+        for (int i = 0; i <= N; ++i) r.w[i] = W[a + i];
+        return r;
     }
+    template <int N>
+    __device__ __forceinline__ void get(uint32_t p, uint32_t (&o)[N]) const { fetch<N>(p).align(o); }
 };
 
 __device__ __forceinline__ uint32_t ab(uint32_t hi, uint32_t lo, uint32_t s) { return __builtin_amdgcn_alignbyte(hi, lo, s); }
@@ -164,24 +202,39 @@ __device__ __forceinline__ void do_string(const Head &H, const Lane &l, uint64_t
     }
 }
 
+// The walks are software-pipelined: a step computes the next cursor from the bytes it holds
+// and issues the read there (clamped into the value) BEFORE its checks and descriptor store,
+// so the read's latency overlaps them; the loop-carried chain is read -> size -> next read.
+// The loop body is two steps with the raw read buffers swapping roles (ping-pong): a single
+// step per iteration needs a register copy of the in-flight buffer at the back-edge, and the
+// compiler waits for the read to land before that copy.
+#define RR_PINGPONG(RA, RB, STEP)  \
+    for (;;) {                     \
+        if (STEP(RA, RB)) break;   \
+        if (STEP(RB, RA)) break;   \
+    }
+
 // ---- intset (rock_serdes.c:217-245, intset.c:45-52): fixed-width members, no walk
 template <class Src>
 __device__ __forceinline__ void do_intset(const Src &R, const Head &H, const Lane &l) {
     const uint32_t w = H.f5(), cnt = H.f9();
     if (!l.ok) return;   // (no stores: loop-invariant per lane)
-    uint32_t p = l.q + 13;
-    for (uint32_t k = 0; k < cnt; ++k, p += w) {
+    uint32_t p = l.q + 13, k = 0;
+    Raw<2> ra = R.template fetch<2>(p), rb;
+    auto step = [&](const Raw<2> &cur, Raw<2> &nxt) __attribute__((always_inline)) {
+        if (k >= cnt) return true;
         uint32_t x[2];
-        R.template get<2>(p, x);
+        cur.align(x);
+        nxt = R.template fetch<2>(p + w);   // (reads may run past the value: in range of the source)
         const int64_t v = w == 2 ? (int64_t)(int16_t)(x[0] & 0xFFFF)
                         : w == 4 ? (int64_t)(int32_t)x[0] : (int64_t)((uint64_t)x[0] | ((uint64_t)x[1] << 32));
         put_desc(l.E, l.so + 16 * k, (uint64_t)v, 0, RR_K_INT, 0);
-    }
+        ++k;
+        p += w;
+        return false;
+    };
+    RR_PINGPONG(ra, rb, step)
 }
-
-// The walks are software-pipelined: a step computes the next cursor from the bytes it holds
-// and issues the read there (clamped into the value) BEFORE its checks and descriptor store,
-// so the read's latency overlaps them; the loop-carried chain is read -> size -> next read.
 
 // ---- List (rock_serdes.c:162-214): {u32 len, bytes}* to the end; integer-looking entries
 // become INT (quicklistPushTail re-encodes them, ziplist.c:480)
@@ -190,17 +243,17 @@ __device__ __forceinline__ bool do_list(const Src &R, const Lane &l, uint32_t &n
     uint32_t p = l.q + 5, k = 0;
     const uint32_t end = l.q + l.L;
     bool fail = false;
-    uint32_t b[6];   // len + 20 bytes
-    R.template get<6>(p, b);
-    for (;;) {
+    Raw<6> ra = R.template fetch<6>(p), rb;   // len + 20 bytes
+    auto step = [&](const Raw<6> &cur, Raw<6> &nxt) __attribute__((always_inline)) {
+        uint32_t b[6];
+        cur.align(b);
         const uint32_t rem = end - p, len = b[0];
         const uint64_t nx = (uint64_t)p + 4 + len;
         const uint32_t pn = nx < end ? (uint32_t)nx : end;
-        uint32_t bn[6];
-        R.template get<6>(pn, bn);
+        nxt = R.template fetch<6>(pn);
         const bool done = p == end;
-        const bool bad = rem < 4 || len > rem - 4 || k >= l.r;
-        if (done || bad) { fail = !done; break; }
+        const bool bad = (rem < 4) | (len > rem - 4) | (k >= l.r);
+        if (done | bad) { fail = !done; return true; }
         const uint32_t d[5] = {b[1], b[2], b[3], b[4], b[5]};
         int64_t iv;
         const bool isint = regs_try_int(d, len, iv);
@@ -208,9 +261,9 @@ __device__ __forceinline__ bool do_list(const Src &R, const Lane &l, uint32_t &n
         pay += isint ? 0 : len;
         ++k;
         p = pn;
-#pragma unroll
-        for (int i = 0; i < 6; ++i) b[i] = bn[i];
-    }
+        return false;
+    };
+    RR_PINGPONG(ra, rb, step)
     n = k;
     return fail || k != l.r;
 }
@@ -222,24 +275,24 @@ __device__ __forceinline__ bool do_ht(const Src &R, const Head &H, const Lane &l
     uint32_t p = l.q + 13, k = 0;
     const uint32_t end = l.q + l.L;
     bool fail = false;
-    uint32_t b[2];
-    R.template get<2>(p, b);
-    for (;;) {
+    Raw<2> ra = R.template fetch<2>(p), rb;
+    auto step = [&](const Raw<2> &cur, Raw<2> &nxt) __attribute__((always_inline)) {
+        uint32_t b[2];
+        cur.align(b);
         const uint32_t rem = end - p;
         const uint64_t nx = (uint64_t)p + 8 + b[0];
-        const uint32_t pn = (nx < end && b[1] == 0) ? (uint32_t)nx : end;
-        uint32_t bn[2];
-        R.template get<2>(pn, bn);
+        const uint32_t pn = ((nx < end) & (b[1] == 0)) ? (uint32_t)nx : end;
+        nxt = R.template fetch<2>(pn);
         const bool done = p == end;
-        const bool bad = rem < 8 || b[1] != 0 || b[0] > rem - 8 || k >= l.r;
-        if (done || bad) { fail = !done; break; }
+        const bool bad = (rem < 8) | (b[1] != 0) | (b[0] > rem - 8) | (k >= l.r);
+        if (done | bad) { fail = !done; return true; }
         put_desc(l.E, l.slot(k), l.B + p + 8, b[0], RR_K_STR, 0);
         pay += b[0];
         ++k;
         p = pn;
-        b[0] = bn[0];
-        b[1] = bn[1];
-    }
+        return false;
+    };
+    RR_PINGPONG(ra, rb, step)
     n = k;
     const bool cnt_ok = H.type() == RR_TYPE_SET_HT ? (uint64_t)k == cnt : ((k & 1) == 0 && (uint64_t)(k >> 1) == cnt);
     return fail || !cnt_ok || k != l.r;
@@ -252,26 +305,26 @@ __device__ __forceinline__ bool do_skiplist(const Src &R, const Head &H, const L
     uint32_t p = l.q + 13, k = 0;
     const uint32_t end = l.q + l.L;
     bool fail = false;
-    uint32_t b[2];
-    R.template get<2>(p, b);
-    for (;;) {
+    Raw<2> ra = R.template fetch<2>(p), rb;
+    auto step = [&](const Raw<2> &cur, Raw<2> &nxt) __attribute__((always_inline)) {
+        uint32_t b[2];
+        cur.align(b);
         const uint32_t rem = end - p;
         const bool score = (k & 1) != 0;
         const uint64_t nx = (uint64_t)p + 8 + (score ? 0u : b[0]);
-        const uint32_t pn = (nx < end && (score || b[1] == 0)) ? (uint32_t)nx : end;
-        uint32_t bn[2];
-        R.template get<2>(pn, bn);
+        const uint32_t pn = ((nx < end) & (score | (b[1] == 0))) ? (uint32_t)nx : end;
+        nxt = R.template fetch<2>(pn);
         const bool done = p == end;
-        const bool bad = rem < 8 || k >= l.r || (!score && (b[1] != 0 || b[0] > rem - 8));
-        if (done || bad) { fail = !done; break; }
+        const bool bad = (rem < 8) | (k >= l.r) | (!score & ((b[1] != 0) | (b[0] > rem - 8)));
+        if (done | bad) { fail = !done; return true; }
         put_desc(l.E, l.slot(k), score ? ((uint64_t)b[0] | ((uint64_t)b[1] << 32)) : l.B + p + 8, score ? 0 : b[0],
                  score ? RR_K_SCORE : RR_K_STR, 0);
         pay += score ? 0 : b[0];
         ++k;
         p = pn;
-        b[0] = bn[0];
-        b[1] = bn[1];
-    }
+        return false;
+    };
+    RR_PINGPONG(ra, rb, step)
     n = k;
     return fail || (k & 1) || (uint64_t)(k >> 1) != cnt || k != l.r;
 }
@@ -287,9 +340,10 @@ __device__ __forceinline__ bool do_ziplist(const Src &R, const Lane &l, uint32_t
     pay += l.L - 13;
     uint32_t p = zl0 + 10, prev_raw = 0, last = zl0 + 10, k = 1;
     bool fail = false;
-    uint32_t b[4];   // prevlen (1 or 5) + encoding + up to 9 more bytes
-    R.template get<4>(p, b);
-    for (;;) {
+    Raw<4> ra = R.template fetch<4>(p), rb;   // prevlen (1 or 5) + encoding + up to 9 more bytes
+    auto step = [&](const Raw<4> &cur, Raw<4> &nxt) __attribute__((always_inline)) {
+        uint32_t b[4];
+        cur.align(b);
         const uint32_t b0 = b[0] & 0xFF;
         // every field of the entry header from registers, as selects (no per-encoding branches)
         const bool big = b0 >= 254;
@@ -311,12 +365,11 @@ __device__ __forceinline__ bool do_ziplist(const Src &R, const Lane &l, uint32_t
                              4 * (uint32_t)(e == 0xD0) + 8 * (uint32_t)(e == 0xE0);
         const uint64_t endp = (uint64_t)qp + (zstr ? ls + sl : 1 + isz);
         const uint32_t pn = endp < zlast ? (uint32_t)endp : zlast;
-        uint32_t bn[4];
-        R.template get<4>(pn, bn);
+        nxt = R.template fetch<4>(pn);
         const bool done = (b0 == 0xFF) & (p < zend);
         const bool bad = (p >= zend) | (big & (p + 5 > zlast)) | (pl != prev_raw) | (qp >= zlast) | (k >= l.r) |
                          (!zstr & !imm & (isz == 0)) | (zstr & (qp + ls > zlast)) | (endp > zlast);
-        if (done | bad) { fail = !done; break; }
+        if (done | bad) { fail = !done; return true; }
         // little-endian integer of isz (1..4) bytes, sign-extended by a shift pair; 8 bytes; or
         // the 4-bit immediate
         const uint32_t sh = (32 - 8 * isz) & 31;
@@ -328,9 +381,9 @@ __device__ __forceinline__ bool do_ziplist(const Src &R, const Lane &l, uint32_t
         last = p;
         p = pn;
         ++k;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) b[i] = bn[i];
-    }
+        return false;
+    };
+    RR_PINGPONG(ra, rb, step)
     n = k;
     const uint32_t entries = k - 1, zllen = z[2] & 0xFFFF;
     return fail || p != zlast || (zllen != 0xFFFF && zllen != entries) || z[1] != last - zl0 || (entries & 1) ||

@@ -597,8 +597,8 @@ __device__ __forceinline__ Acc run_batch(const Src &src, uint32_t c, uint64_t v,
 // Probe build (make VARIANT=probe EXTRA=-DRR_PROBE, tools/probe_decode.py): per-window phase
 // cycles and per-class batch cycles / counts / lanes into a buffer set by rr_probe_set
 // (PROBE_WORDS u64 per window).  Diagnostics only; the product build has none of it.
-constexpr uint32_t PROBE_WORDS = 32;
 #ifdef RR_PROBE
+constexpr uint32_t PROBE_WORDS = 32;
 __device__ uint64_t *g_probe;
 extern "C" int rr_probe_set(void *p) { return hipMemcpyToSymbol(HIP_SYMBOL(g_probe), &p, sizeof(p)) == hipSuccess ? 0 : -1; }
 #define PROBE(...) __VA_ARGS__
@@ -642,6 +642,14 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
     }
     const bool staged = S1 - S0 <= STAGE;
     const uint64_t cap = elem_cap < 0xFFFFFFFFull ? elem_cap : 0xFFFFFFFFull;   // elem_base is 32-bit
+
+    // the first chunk's class bytes, loaded before the copy so their latency hides under it
+    uint32_t cls0[PMAX / NT];
+#pragma unroll
+    for (uint32_t j = 0; j < PMAX / NT; ++j) {
+        const uint64_t v = v_lo + j * NT + tid;
+        cls0[j] = v < v_hi ? (uint32_t)cls[v] : C_N;
+    }
 
     // 1. window -> arena, value bytes -> LDS (one load feeds both)
     {
@@ -688,6 +696,7 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
     for (uint64_t c0 = v_lo; c0 < v_end; c0 += PMAX) {
         const uint32_t nv = (uint32_t)(v_hi - c0 < PMAX ? v_hi - c0 : PMAX);
         // 2. counting sort by class (ballot per class, one LDS atomic per class per wave-round)
+        if (c0 != v_lo) __syncthreads();   // every wave is done with the previous chunk's batches
         if (tid < C_N) { ccount[tid] = 0; ccur[tid] = 0; }
         if (tid == 0) next_batch = 0;
         __syncthreads();   // also: the stage is complete; the previous chunk's batches are done
@@ -696,7 +705,8 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
 #pragma unroll
         for (uint32_t j = 0; j < PMAX / NT; ++j) {
             const uint32_t i = j * NT + tid;
-            myc[j] = i < nv ? (far ? C_EXACT : (uint32_t)cls[c0 + i]) : C_N;
+            const uint32_t ci = c0 == v_lo ? cls0[j] : i < nv ? (uint32_t)cls[c0 + i] : C_N;
+            myc[j] = i < nv ? (far ? C_EXACT : ci) : C_N;
 #pragma unroll
             for (uint32_t c = 0; c < C_N; ++c) {
                 const uint64_t m = __ballot(myc[j] == c);
