@@ -788,7 +788,7 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
         stats[3 * (uint64_t)tile + 1] = tp;
         stats[3 * (uint64_t)tile + 2] = 0;
         PROBE(prb[0] = pt1 - pt0; prb[1] = pt2 - pt1; prb[2] = __builtin_amdgcn_s_memtime() - pt2; prb[24] = v_hi - v_lo;
-              prb[25] = staged; for (uint32_t i = 0; i < PROBE_WORDS; ++i) g_probe[(uint64_t)tile * PROBE_WORDS + i] = prb[i];)
+              prb[25] = staged; if (g_probe) for (uint32_t i = 0; i < PROBE_WORDS; ++i) g_probe[(uint64_t)tile * PROBE_WORDS + i] = prb[i];)
     }
 }
 
