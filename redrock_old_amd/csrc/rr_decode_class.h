@@ -25,7 +25,6 @@ namespace rr {
 constexpr uint32_t C_STR = 0, C_IS = 1, C_LIST = 2, C_HT = 3, C_SL = 4, C_ZL = 5, C_EXACT = 6, C_N = 7;
 
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
-typedef __attribute__((address_space(3))) uint32_t *lds_u32w;
 
 __device__ __forceinline__ rsrc_t make_rsrc(const uint8_t *base, uint32_t bytes) {
     return __builtin_amdgcn_make_buffer_rsrc((void *)base, 0, (int)bytes, 0x00020000);
@@ -389,208 +388,6 @@ __device__ __forceinline__ bool do_ziplist(const Src &R, const Lane &l, uint32_t
     const uint32_t entries = k - 1, zllen = z[2] & 0xFFFF;
     return fail || p != zlast || (zllen != 0xFFFF && zllen != entries) || z[1] != last - zl0 || (entries & 1) ||
            k != l.r;
-}
-
-// ============================================================================================
-// Two-phase batches (staged windows): the walks above do a value's whole decode per step at
-// one lane per value, so a batch of few values (a window holds ~5-30 values of a class) runs
-// most of its instructions on idle lanes, and the kernel is issue-bound.  Here the walk only
-// validates and records each element's position in an LDS table indexed by window-local slot
-// (a few instructions per step); the descriptors are then built lane-per-SLOT over the batch's
-// slots, 64 at a time, with full lanes and stores that are contiguous per value.
-
-// position walks: same checks as the walks above; tab = &table[first slot of the value]
-template <class Src>
-__device__ __forceinline__ bool pos_list(const Src &R, const Lane &l, lds_u32w tab, uint32_t &n) {
-    uint32_t p = l.q + 5, k = 0;
-    const uint32_t end = l.q + l.L;
-    bool fail = false;
-    Raw<1> ra = R.template fetch<1>(p), rb;
-    auto step = [&](const Raw<1> &cur, Raw<1> &nxt) __attribute__((always_inline)) {
-        uint32_t b[1];
-        cur.align(b);
-        const uint32_t rem = end - p, len = b[0];
-        const uint64_t nx = (uint64_t)p + 4 + len;
-        const uint32_t pn = nx < end ? (uint32_t)nx : end;
-        nxt = R.template fetch<1>(pn);
-        const bool done = p == end;
-        const bool bad = (rem < 4) | (len > rem - 4) | (k >= l.r);
-        if (done | bad) { fail = !done; return true; }
-        tab[k] = p;
-        ++k;
-        p = pn;
-        return false;
-    };
-    RR_PINGPONG(ra, rb, step)
-    n = k;
-    return fail || k != l.r;
-}
-
-template <class Src>
-__device__ __forceinline__ bool pos_ht(const Src &R, const Head &H, const Lane &l, lds_u32w tab, uint32_t &n) {
-    const uint64_t cnt = H.u5();
-    uint32_t p = l.q + 13, k = 0;
-    const uint32_t end = l.q + l.L;
-    bool fail = false;
-    Raw<2> ra = R.template fetch<2>(p), rb;
-    auto step = [&](const Raw<2> &cur, Raw<2> &nxt) __attribute__((always_inline)) {
-        uint32_t b[2];
-        cur.align(b);
-        const uint32_t rem = end - p;
-        const uint64_t nx = (uint64_t)p + 8 + b[0];
-        const uint32_t pn = ((nx < end) & (b[1] == 0)) ? (uint32_t)nx : end;
-        nxt = R.template fetch<2>(pn);
-        const bool done = p == end;
-        const bool bad = (rem < 8) | (b[1] != 0) | (b[0] > rem - 8) | (k >= l.r);
-        if (done | bad) { fail = !done; return true; }
-        tab[k] = p;
-        ++k;
-        p = pn;
-        return false;
-    };
-    RR_PINGPONG(ra, rb, step)
-    n = k;
-    const bool cnt_ok = H.type() == RR_TYPE_SET_HT ? (uint64_t)k == cnt : ((k & 1) == 0 && (uint64_t)(k >> 1) == cnt);
-    return fail || !cnt_ok || k != l.r;
-}
-
-template <class Src>
-__device__ __forceinline__ bool pos_skiplist(const Src &R, const Head &H, const Lane &l, lds_u32w tab, uint32_t &n) {
-    const uint64_t cnt = H.u5();
-    uint32_t p = l.q + 13, k = 0;
-    const uint32_t end = l.q + l.L;
-    bool fail = false;
-    Raw<2> ra = R.template fetch<2>(p), rb;
-    auto step = [&](const Raw<2> &cur, Raw<2> &nxt) __attribute__((always_inline)) {
-        uint32_t b[2];
-        cur.align(b);
-        const uint32_t rem = end - p;
-        const bool score = (k & 1) != 0;
-        const uint64_t nx = (uint64_t)p + 8 + (score ? 0u : b[0]);
-        const uint32_t pn = ((nx < end) & (score | (b[1] == 0))) ? (uint32_t)nx : end;
-        nxt = R.template fetch<2>(pn);
-        const bool done = p == end;
-        const bool bad = (rem < 8) | (k >= l.r) | (!score & ((b[1] != 0) | (b[0] > rem - 8)));
-        if (done | bad) { fail = !done; return true; }
-        tab[k] = p;
-        ++k;
-        p = pn;
-        return false;
-    };
-    RR_PINGPONG(ra, rb, step)
-    n = k;
-    return fail || (k & 1) || (uint64_t)(k >> 1) != cnt || k != l.r;
-}
-
-// ziplist entry header fields (ziplist.c:300-447) from the 16 bytes at the entry
-struct ZlEntry {
-    bool big, zstr, imm;
-    uint32_t b0, pl, hdr, e, sl, ls, isz, lo, hi;
-    __device__ __forceinline__ ZlEntry(const uint32_t (&b)[4]) {
-        b0 = b[0] & 0xFF;
-        big = b0 >= 254;
-        pl = big ? ab(b[1], b[0], 1) : b0;
-        hdr = big ? 5u : 1u;   // prevlen bytes
-        e = big ? (b[1] >> 8) & 0xFF : (b[0] >> 8) & 0xFF;
-        const uint32_t x1 = big ? (b[1] >> 16) & 0xFF : (b[0] >> 16) & 0xFF;
-        lo = big ? ab(b[2], b[1], 2) : ab(b[1], b[0], 2);   // bytes after the encoding byte
-        hi = big ? ab(b[3], b[2], 2) : ab(b[2], b[1], 2);
-        zstr = e < 0xC0;
-        const uint32_t scls = e >> 6;                        // string length class 0 / 1 / 2
-        ls = 1 + scls + 2 * (scls >> 1);                     // 1 / 2 / 5 length bytes
-        const uint32_t sl1 = scls == 0 ? (e & 0x3F) : (((e & 0x3F) << 8) | x1);
-        sl = scls >= 2 ? __builtin_bswap32(lo) : sl1;
-        imm = e - 0xF1u <= 0xFDu - 0xF1u;
-        isz = (uint32_t)(e == 0xFE) + 2 * (uint32_t)(e == 0xC0) + 3 * (uint32_t)(e == 0xF0) +
-              4 * (uint32_t)(e == 0xD0) + 8 * (uint32_t)(e == 0xE0);
-    }
-    // bytes from the entry start to the next entry
-    __device__ __forceinline__ uint64_t size() const { return (uint64_t)hdr + (zstr ? ls + sl : 1 + isz); }
-};
-
-template <class Src>
-__device__ __forceinline__ bool pos_ziplist(const Src &R, const Lane &l, lds_u32w tab, uint32_t &n) {
-    const uint32_t zl0 = l.q + 13, zend = l.q + l.L, zlast = zend - 1;   // zlast: the 0xFF byte
-    uint32_t z[3];
-    R.template get<3>(zl0, z);   // zlbytes, zltail, zllen
-    uint32_t p = zl0 + 10, prev_raw = 0, last = zl0 + 10, k = 1;
-    bool fail = false;
-    Raw<4> ra = R.template fetch<4>(p), rb;
-    auto step = [&](const Raw<4> &cur, Raw<4> &nxt) __attribute__((always_inline)) {
-        uint32_t b[4];
-        cur.align(b);
-        const ZlEntry x(b);
-        const uint64_t endp = (uint64_t)p + x.size();
-        const uint32_t pn = endp < zlast ? (uint32_t)endp : zlast;
-        nxt = R.template fetch<4>(pn);
-        const uint32_t qp = p + x.hdr;
-        const bool done = (x.b0 == 0xFF) & (p < zend);
-        const bool bad = (p >= zend) | (x.big & (p + 5 > zlast)) | (x.pl != prev_raw) | (qp >= zlast) | (k >= l.r) |
-                         (!x.zstr & !x.imm & (x.isz == 0)) | (x.zstr & (qp + x.ls > zlast)) | (endp > zlast);
-        if (done | bad) { fail = !done; return true; }
-        tab[k] = p;
-        prev_raw = (uint32_t)endp - p;
-        last = p;
-        p = pn;
-        ++k;
-        return false;
-    };
-    RR_PINGPONG(ra, rb, step)
-    n = k;
-    const uint32_t entries = k - 1, zllen = z[2] & 0xFFFF;
-    return fail || p != zlast || (zllen != 0xFFFF && zllen != entries) || z[1] != last - zl0 || (entries & 1) ||
-           k != l.r;
-}
-
-// descriptor k of a value of class c whose element starts at pos (q, L: the value; w: intset
-// width); adds its payload bytes
-template <class Src>
-__device__ __forceinline__ void emit_slot(const Src &R, uint32_t c, uint64_t B, uint32_t q, uint32_t L, uint32_t w,
-                                          uint32_t pos, uint32_t k, rsrc_t E, uint32_t off, uint64_t &pay) {
-    if (c == C_IS) {
-        uint32_t x[2];
-        R.template get<2>(pos, x);
-        const int64_t v = w == 2 ? (int64_t)(int16_t)(x[0] & 0xFFFF)
-                        : w == 4 ? (int64_t)(int32_t)x[0] : (int64_t)((uint64_t)x[0] | ((uint64_t)x[1] << 32));
-        put_desc(E, off, (uint64_t)v, 0, RR_K_INT, 0);
-    } else if (c == C_LIST) {
-        uint32_t b[6];
-        R.template get<6>(pos, b);
-        const uint32_t len = b[0];
-        const uint32_t d[5] = {b[1], b[2], b[3], b[4], b[5]};
-        int64_t iv;
-        const bool isint = regs_try_int(d, len, iv);
-        put_desc(E, off, isint ? (uint64_t)iv : B + pos + 4, isint ? 0 : len, isint ? RR_K_INT : RR_K_STR, 0);
-        pay += isint ? 0 : len;
-    } else if (c == C_HT) {
-        uint32_t b[1];
-        R.template get<1>(pos, b);
-        put_desc(E, off, B + pos + 8, b[0], RR_K_STR, 0);
-        pay += b[0];
-    } else if (c == C_SL) {
-        uint32_t b[2];
-        R.template get<2>(pos, b);
-        const bool score = (k & 1) != 0;
-        put_desc(E, off, score ? ((uint64_t)b[0] | ((uint64_t)b[1] << 32)) : B + pos + 8, score ? 0 : b[0],
-                 score ? RR_K_SCORE : RR_K_STR, 0);
-        pay += score ? 0 : b[0];
-    } else {   // C_ZL
-        if (k == 0) {
-            put_desc(E, off, B + q + 13, L - 13, RR_K_ZLRAW, 0);
-            pay += L - 13;
-        } else {
-            uint32_t b[4];
-            R.template get<4>(pos, b);
-            const ZlEntry x(b);
-            const uint32_t sh = (32 - 8 * x.isz) & 31;
-            const int64_t v32 = (int32_t)(x.lo << sh) >> sh;
-            const int64_t iv = x.isz == 8 ? (int64_t)((uint64_t)x.lo | ((uint64_t)x.hi << 32))
-                             : x.imm      ? (int64_t)(x.e & 0x0F) - 1
-                                          : v32;
-            put_desc(E, off, x.zstr ? B + pos + x.hdr + x.ls : (uint64_t)iv, x.zstr ? x.sl : 0,
-                     x.zstr ? RR_K_STR : RR_K_INT, x.zstr ? (x.e & 0xC0) : x.e);
-        }
-    }
 }
 
 }  // namespace rr

@@ -587,89 +587,6 @@ __device__ __forceinline__ Acc run_batch(const Src &src, uint32_t c, uint64_t v,
     return Acc{l.ok ? 0u : 1u, l.ok ? vp : 0};
 }
 
-// A batch of a staged window, run by the whole wave (lanes >= the batch size inactive).
-// String and exact-parser batches stay lane-per-value; the walk classes go two-phase
-// (rr_decode_class.h): position walk + checks lane-per-value into the window's slot table,
-// then descriptors lane-per-slot.  A batch whose slots reach past the table runs the one-phase
-// walks.
-template <uint32_t ECAP>
-__device__ __forceinline__ Acc batch_staged(const LdsSrc &src, lds_u32w tab, uint32_t c, bool active, uint64_t v,
-                                            uint64_t B, rsrc_t E, uint64_t eb0, const uint8_t *__restrict__ blob,
-                                            const uint64_t *__restrict__ offsets, const uint64_t *__restrict__ ebase,
-                                            rr_value *__restrict__ values, rr_elem *__restrict__ elems, uint64_t cap) {
-    Acc acc{0, 0};
-    if (c == C_EXACT || c == C_STR) {
-        if (active) acc = run_batch(src, c, v, B, E, eb0, blob, offsets, ebase, values, elems, cap);
-        return acc;
-    }
-    uint64_t eb = eb0, r = 0;
-    Lane l{};
-    Head H{};
-    if (active) {
-        const uint64_t o = offsets[v], o1 = offsets[v + 1];
-        eb = ebase[v];
-        r = ebase[v + 1] - eb;
-        l.q = (uint32_t)(o - B);
-        l.L = (uint32_t)(o1 - o);
-        l.B = B;
-        l.E = E;
-        l.so = (uint32_t)(eb - eb0) * 16;
-        l.r = (uint32_t)r;
-        l.ok = eb + r <= cap;
-        src.template get<4>(l.q, H.h);
-    }
-    if (__ballot(active && (eb - eb0) + r > ECAP)) {
-        if (active) acc = run_batch(src, c, v, B, E, eb0, blob, offsets, ebase, values, elems, cap);
-        return acc;
-    }
-    // 1. walk: checks + element positions (lane = value)
-    uint32_t n = 0;
-    bool fail = false;
-    if (active) {
-        const lds_u32w t = tab + (l.so >> 4);
-        if (c == C_IS) n = H.f9();
-        else if (c == C_LIST) fail = pos_list(src, l, t, n);
-        else if (c == C_HT) fail = pos_ht(src, H, l, t, n);
-        else if (c == C_SL) fail = pos_skiplist(src, H, l, t, n);
-        else fail = pos_ziplist(src, l, t, n);
-        if (fail) {
-            acc = exact_value(blob, v, offsets, ebase, values, elems, cap);
-        } else {
-            put_value(values + v, H.type(), c == C_IS ? H.f5() : 0, l.ok ? RR_OK : RR_E_CAPACITY, H.lru(), n,
-                      (uint32_t)eb);
-            acc.bad = l.ok ? 0 : 1;
-        }
-    }
-    // 2. descriptors, lane = slot over the batch's emitted slots (value-major)
-    const uint32_t lane = lane_id();
-    const uint32_t en = active && !fail && l.ok ? n : 0;
-    uint32_t P = en;   // inclusive prefix over the lanes
-#pragma unroll
-    for (uint32_t d = 1; d < RR_WAVE; d <<= 1) {
-        const uint32_t t = __shfl_up(P, d, RR_WAVE);
-        if (lane >= d) P += t;
-    }
-    const uint32_t T = __shfl(P, RR_WAVE - 1, RR_WAVE), X = P - en;
-    const uint32_t w = c == C_IS ? H.f5() : 0;
-    uint64_t pay = 0;
-    for (uint32_t base = 0; base < T; base += RR_WAVE) {
-        const uint32_t si = base + lane;
-        uint32_t o = 0;   // owner lane: the number of lanes whose inclusive prefix is <= si
-#pragma unroll
-        for (uint32_t step = RR_WAVE / 2; step; step >>= 1)
-            if (__shfl(P, (int)(o + step - 1), RR_WAVE) <= si) o += step;
-        const uint32_t k = si - __shfl(X, (int)o, RR_WAVE);
-        const uint32_t oso = __shfl(l.so, (int)o, RR_WAVE), oq = __shfl(l.q, (int)o, RR_WAVE);
-        const uint32_t oL = __shfl(l.L, (int)o, RR_WAVE), ow = __shfl(w, (int)o, RR_WAVE);
-        if (si < T) {
-            const uint32_t pos = c == C_IS ? oq + 13 + k * ow : (c == C_ZL && k == 0) ? 0u : tab[(oso >> 4) + k];
-            emit_slot(src, c, B, oq, oL, ow, pos, k, E, oso + 16 * k, pay);
-        }
-    }
-    acc.pay += pay;
-    return acc;
-}
-
 // Workgroup per byte WINDOW of W bytes: window t owns the values whose first byte lies in
 // [t*W, (t+1)*W) (first_val from K1).  The workgroup
 //   1. streams the window into the mirror arena and, from the same loads, stages the bytes of
@@ -694,7 +611,7 @@ extern "C" int rr_probe_set(void *p) { return hipMemcpyToSymbol(HIP_SYMBOL(g_pro
 #else
 #define DEC_WPE_ATTR
 #endif
-template <uint32_t W, uint32_t SLACK, uint32_t NW, uint32_t PMAX, uint32_t ECAP>
+template <uint32_t W, uint32_t SLACK, uint32_t NW, uint32_t PMAX>
 __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const uint8_t *__restrict__ blob, uint64_t data_cap,
                                                               const uint64_t *__restrict__ offsets, uint64_t n,
                                                               const uint32_t *__restrict__ first_val,
@@ -707,7 +624,6 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
     static_assert(PMAX % NT == 0 && W % 16 == 0 && SLACK % 16 == 0, "tile shape");
     __shared__ __attribute__((aligned(16))) uint8_t stage[STAGE + 64];
     __shared__ uint16_t perm[PMAX];
-    __shared__ uint32_t slot_pos[ECAP];   // element positions by window-local slot (two-phase batches)
     __shared__ uint32_t ccount[C_N], cbase[C_N], ccur[C_N], bpre[C_N + 1];
     __shared__ uint32_t next_batch;
     __shared__ uint64_t red[2][NW];
@@ -791,7 +707,6 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
             const uint32_t i = j * NT + tid;
             const uint32_t ci = c0 == v_lo ? cls0[j] : i < nv ? (uint32_t)cls[c0 + i] : C_N;
             myc[j] = i < nv ? (far ? C_EXACT : ci) : C_N;
-            if (j * NT + wave * RR_WAVE >= nv) continue;   // (wave-uniform) no values in this round
 #pragma unroll
             for (uint32_t c = 0; c < C_N; ++c) {
                 const uint64_t m = __ballot(myc[j] == c);
@@ -814,7 +729,6 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
 #pragma unroll
         for (uint32_t j = 0; j < PMAX / NT; ++j) {
             const uint32_t i = j * NT + tid;
-            if (j * NT + wave * RR_WAVE >= nv) continue;
 #pragma unroll
             for (uint32_t c = 0; c < C_N; ++c) {
                 const uint64_t m = __ballot(myc[j] == c);
@@ -849,16 +763,13 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
             if ((RR_SKIP_CLASSES >> c) & 1) continue;
 #endif
             PROBE(const uint64_t tb0 = __builtin_amdgcn_s_memtime();)
-            const bool active = lane < cnt;
-            const uint64_t v = c0 + (active ? perm[first + lane] : 0u);
-            Acc a{0, 0};
-            if (staged)
-                a = batch_staged<ECAP>(lsrc, (lds_u32w)slot_pos, c, active, v, S0, E, eb0, blob, offsets, ebase,
-                                       values, elems, cap);
-            else if (active)
-                a = run_batch(gsrc, c, v, S0, E, eb0, blob, offsets, ebase, values, elems, cap);
-            bad += a.bad;
-            pay += a.pay;
+            if (lane < cnt) {
+                const uint64_t v = c0 + perm[first + lane];
+                const Acc a = staged ? run_batch(lsrc, c, v, S0, E, eb0, blob, offsets, ebase, values, elems, cap)
+                                     : run_batch(gsrc, c, v, S0, E, eb0, blob, offsets, ebase, values, elems, cap);
+                bad += a.bad;
+                pay += a.pay;
+            }
             PROBE(if (lane == 0) {
                 atomicAdd((unsigned long long *)&prb[3 + c], (unsigned long long)(__builtin_amdgcn_s_memtime() - tb0));
                 atomicAdd((unsigned long long *)&prb[10 + c], 1ull);
@@ -1138,22 +1049,19 @@ __global__ __launch_bounds__(WG) void encode_kernel(const rr_value *__restrict__
 
 // ---------------------------------------------------------------------------------------- launch
 #ifndef RR_DEC_W
-#define RR_DEC_W 32768
+#define RR_DEC_W 65536
 #endif
 #ifndef RR_DEC_SLACK
-#define RR_DEC_SLACK 4096
+#define RR_DEC_SLACK 8192
 #endif
 #ifndef RR_DEC_NW
-#define RR_DEC_NW 4
+#define RR_DEC_NW 8
 #endif
 #ifndef RR_DEC_PMAX
-#define RR_DEC_PMAX 1024
-#endif
-#ifndef RR_DEC_ECAP
-#define RR_DEC_ECAP 2048
+#define RR_DEC_PMAX 2048
 #endif
 constexpr uint32_t DEC_W = RR_DEC_W, DEC_NW = RR_DEC_NW;
-#define DECODE_KERNEL decode_kernel<RR_DEC_W, RR_DEC_SLACK, RR_DEC_NW, RR_DEC_PMAX, RR_DEC_ECAP>
+#define DECODE_KERNEL decode_kernel<RR_DEC_W, RR_DEC_SLACK, RR_DEC_NW, RR_DEC_PMAX>
 
 // Resident workgroup count for a persistent launch: occupancy query minus one block per CU
 // (the API over-reports by one for SGPR-heavy kernels, MI355X_MICROARCH.md §Residency).
