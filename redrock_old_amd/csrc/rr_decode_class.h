@@ -202,12 +202,16 @@ __device__ __forceinline__ void do_string(const Head &H, const Lane &l, uint64_t
     }
 }
 
-// The walks are software-pipelined: a step computes the next cursor from the bytes it holds
-// and issues the read there (clamped into the value) BEFORE its checks and descriptor store,
-// so the read's latency overlaps them; the loop-carried chain is read -> size -> next read.
-// The loop body is two steps with the raw read buffers swapping roles (ping-pong): a single
-// step per iteration needs a register copy of the in-flight buffer at the back-edge, and the
-// compiler waits for the read to land before that copy.
+// The walks run the whole wave in lock-step: every lane executes every step, a lane that is
+// done or failed is masked by selects (its cursor frozen, its descriptor store sent to NOSLOT),
+// and the loop exits when a ballot finds no lane still walking.  Divergent per-lane loop exits
+// instead cost ~10 exec-mask SALU instructions per step, half of all issued instructions.
+//
+// They are also software-pipelined: a step computes the next cursor from the bytes it holds
+// and issues the read there BEFORE its checks and descriptor store, so the read's latency
+// overlaps them.  The loop body is two steps with the raw read buffers swapping roles
+// (ping-pong): one step per iteration needs a register copy of the in-flight buffer at the
+// back-edge, and the compiler waits for the read to land before that copy.
 #define RR_PINGPONG(RA, RB, STEP)  \
     for (;;) {                     \
         if (STEP(RA, RB)) break;   \
@@ -216,22 +220,21 @@ __device__ __forceinline__ void do_string(const Head &H, const Lane &l, uint64_t
 
 // ---- intset (rock_serdes.c:217-245, intset.c:45-52): fixed-width members, no walk
 template <class Src>
-__device__ __forceinline__ void do_intset(const Src &R, const Head &H, const Lane &l) {
-    const uint32_t w = H.f5(), cnt = H.f9();
-    if (!l.ok) return;   // (no stores: loop-invariant per lane)
+__device__ __forceinline__ void do_intset(const Src &R, const Head &H, const Lane &l, bool active) {
+    const uint32_t w = H.f5(), cnt = active && l.ok ? H.f9() : 0;
     uint32_t p = l.q + 13, k = 0;
     Raw<2> ra = R.template fetch<2>(p), rb;
     auto step = [&](const Raw<2> &cur, Raw<2> &nxt) __attribute__((always_inline)) {
-        if (k >= cnt) return true;
+        const bool live = k < cnt;
         uint32_t x[2];
         cur.align(x);
         nxt = R.template fetch<2>(p + w);   // (reads may run past the value: in range of the source)
         const int64_t v = w == 2 ? (int64_t)(int16_t)(x[0] & 0xFFFF)
                         : w == 4 ? (int64_t)(int32_t)x[0] : (int64_t)((uint64_t)x[0] | ((uint64_t)x[1] << 32));
-        put_desc(l.E, l.so + 16 * k, (uint64_t)v, 0, RR_K_INT, 0);
-        ++k;
+        put_desc(l.E, live ? l.so + 16 * k : NOSLOT, (uint64_t)v, 0, RR_K_INT, 0);
+        k += live;
         p += w;
-        return false;
+        return __ballot(k < cnt) == 0;
     };
     RR_PINGPONG(ra, rb, step)
 }
@@ -239,10 +242,10 @@ __device__ __forceinline__ void do_intset(const Src &R, const Head &H, const Lan
 // ---- List (rock_serdes.c:162-214): {u32 len, bytes}* to the end; integer-looking entries
 // become INT (quicklistPushTail re-encodes them, ziplist.c:480)
 template <class Src>
-__device__ __forceinline__ bool do_list(const Src &R, const Lane &l, uint32_t &n, uint64_t &pay) {
+__device__ __forceinline__ bool do_list(const Src &R, const Lane &l, bool active, uint32_t &n, uint64_t &pay) {
     uint32_t p = l.q + 5, k = 0;
     const uint32_t end = l.q + l.L;
-    bool fail = false;
+    bool fail = false, live = active;
     Raw<6> ra = R.template fetch<6>(p), rb;   // len + 20 bytes
     auto step = [&](const Raw<6> &cur, Raw<6> &nxt) __attribute__((always_inline)) {
         uint32_t b[6];
@@ -250,18 +253,21 @@ __device__ __forceinline__ bool do_list(const Src &R, const Lane &l, uint32_t &n
         const uint32_t rem = end - p, len = b[0];
         const uint64_t nx = (uint64_t)p + 4 + len;
         const uint32_t pn = nx < end ? (uint32_t)nx : end;
-        nxt = R.template fetch<6>(pn);
+        nxt = R.template fetch<6>(live ? pn : p);
         const bool done = p == end;
         const bool bad = (rem < 4) | (len > rem - 4) | (k >= l.r);
-        if (done | bad) { fail = !done; return true; }
+        const bool emit = live & !done & !bad;
+        fail |= live & !done & bad;
         const uint32_t d[5] = {b[1], b[2], b[3], b[4], b[5]};
         int64_t iv;
         const bool isint = regs_try_int(d, len, iv);
-        put_desc(l.E, l.slot(k), isint ? (uint64_t)iv : l.B + p + 4, isint ? 0 : len, isint ? RR_K_INT : RR_K_STR, 0);
-        pay += isint ? 0 : len;
-        ++k;
-        p = pn;
-        return false;
+        put_desc(l.E, emit ? l.slot(k) : NOSLOT, isint ? (uint64_t)iv : l.B + p + 4, isint ? 0 : len,
+                 isint ? RR_K_INT : RR_K_STR, 0);
+        pay += emit && !isint ? len : 0;
+        k += emit;
+        p = emit ? pn : p;
+        live = emit;
+        return __ballot(live) == 0;
     };
     RR_PINGPONG(ra, rb, step)
     n = k;
@@ -270,11 +276,12 @@ __device__ __forceinline__ bool do_list(const Src &R, const Lane &l, uint32_t &n
 
 // ---- Set / Hash hash tables (rock_serdes.c:248-311, :349-414): u64 count, {u64 len, bytes}*
 template <class Src>
-__device__ __forceinline__ bool do_ht(const Src &R, const Head &H, const Lane &l, uint32_t &n, uint64_t &pay) {
+__device__ __forceinline__ bool do_ht(const Src &R, const Head &H, const Lane &l, bool active, uint32_t &n,
+                                      uint64_t &pay) {
     const uint64_t cnt = H.u5();
     uint32_t p = l.q + 13, k = 0;
     const uint32_t end = l.q + l.L;
-    bool fail = false;
+    bool fail = false, live = active;
     Raw<2> ra = R.template fetch<2>(p), rb;
     auto step = [&](const Raw<2> &cur, Raw<2> &nxt) __attribute__((always_inline)) {
         uint32_t b[2];
@@ -282,15 +289,17 @@ __device__ __forceinline__ bool do_ht(const Src &R, const Head &H, const Lane &l
         const uint32_t rem = end - p;
         const uint64_t nx = (uint64_t)p + 8 + b[0];
         const uint32_t pn = ((nx < end) & (b[1] == 0)) ? (uint32_t)nx : end;
-        nxt = R.template fetch<2>(pn);
+        nxt = R.template fetch<2>(live ? pn : p);
         const bool done = p == end;
         const bool bad = (rem < 8) | (b[1] != 0) | (b[0] > rem - 8) | (k >= l.r);
-        if (done | bad) { fail = !done; return true; }
-        put_desc(l.E, l.slot(k), l.B + p + 8, b[0], RR_K_STR, 0);
-        pay += b[0];
-        ++k;
-        p = pn;
-        return false;
+        const bool emit = live & !done & !bad;
+        fail |= live & !done & bad;
+        put_desc(l.E, emit ? l.slot(k) : NOSLOT, l.B + p + 8, b[0], RR_K_STR, 0);
+        pay += emit ? b[0] : 0;
+        k += emit;
+        p = emit ? pn : p;
+        live = emit;
+        return __ballot(live) == 0;
     };
     RR_PINGPONG(ra, rb, step)
     n = k;
@@ -300,11 +309,12 @@ __device__ __forceinline__ bool do_ht(const Src &R, const Head &H, const Lane &l
 
 // ---- ZSet skiplist (rock_serdes.c:448-508): u64 count, {u64 len, member, f64 score}*
 template <class Src>
-__device__ __forceinline__ bool do_skiplist(const Src &R, const Head &H, const Lane &l, uint32_t &n, uint64_t &pay) {
+__device__ __forceinline__ bool do_skiplist(const Src &R, const Head &H, const Lane &l, bool active, uint32_t &n,
+                                            uint64_t &pay) {
     const uint64_t cnt = H.u5();
     uint32_t p = l.q + 13, k = 0;
     const uint32_t end = l.q + l.L;
-    bool fail = false;
+    bool fail = false, live = active;
     Raw<2> ra = R.template fetch<2>(p), rb;
     auto step = [&](const Raw<2> &cur, Raw<2> &nxt) __attribute__((always_inline)) {
         uint32_t b[2];
@@ -313,16 +323,18 @@ __device__ __forceinline__ bool do_skiplist(const Src &R, const Head &H, const L
         const bool score = (k & 1) != 0;
         const uint64_t nx = (uint64_t)p + 8 + (score ? 0u : b[0]);
         const uint32_t pn = ((nx < end) & (score | (b[1] == 0))) ? (uint32_t)nx : end;
-        nxt = R.template fetch<2>(pn);
+        nxt = R.template fetch<2>(live ? pn : p);
         const bool done = p == end;
         const bool bad = (rem < 8) | (k >= l.r) | (!score & ((b[1] != 0) | (b[0] > rem - 8)));
-        if (done | bad) { fail = !done; return true; }
-        put_desc(l.E, l.slot(k), score ? ((uint64_t)b[0] | ((uint64_t)b[1] << 32)) : l.B + p + 8, score ? 0 : b[0],
-                 score ? RR_K_SCORE : RR_K_STR, 0);
-        pay += score ? 0 : b[0];
-        ++k;
-        p = pn;
-        return false;
+        const bool emit = live & !done & !bad;
+        fail |= live & !done & bad;
+        put_desc(l.E, emit ? l.slot(k) : NOSLOT, score ? ((uint64_t)b[0] | ((uint64_t)b[1] << 32)) : l.B + p + 8,
+                 score ? 0 : b[0], score ? RR_K_SCORE : RR_K_STR, 0);
+        pay += emit && !score ? b[0] : 0;
+        k += emit;
+        p = emit ? pn : p;
+        live = emit;
+        return __ballot(live) == 0;
     };
     RR_PINGPONG(ra, rb, step)
     n = k;
@@ -332,14 +344,14 @@ __device__ __forceinline__ bool do_skiplist(const Src &R, const Head &H, const L
 // ---- Hash / ZSet ziplists (rock_serdes.c:314-346, :417-446; ziplist.c:300-447): element 0
 // is the raw ziplist, then one descriptor per entry
 template <class Src>
-__device__ __forceinline__ bool do_ziplist(const Src &R, const Lane &l, uint32_t &n, uint64_t &pay) {
+__device__ __forceinline__ bool do_ziplist(const Src &R, const Lane &l, bool active, uint32_t &n, uint64_t &pay) {
     const uint32_t zl0 = l.q + 13, zend = l.q + l.L, zlast = zend - 1;   // zlast: the 0xFF byte
     uint32_t z[3];
     R.template get<3>(zl0, z);   // zlbytes, zltail, zllen
-    put_desc(l.E, l.slot(0), l.B + zl0, l.L - 13, RR_K_ZLRAW, 0);
-    pay += l.L - 13;
+    put_desc(l.E, active ? l.slot(0) : NOSLOT, l.B + zl0, l.L - 13, RR_K_ZLRAW, 0);
+    pay += active ? l.L - 13 : 0;
     uint32_t p = zl0 + 10, prev_raw = 0, last = zl0 + 10, k = 1;
-    bool fail = false;
+    bool fail = false, live = active;
     Raw<4> ra = R.template fetch<4>(p), rb;   // prevlen (1 or 5) + encoding + up to 9 more bytes
     auto step = [&](const Raw<4> &cur, Raw<4> &nxt) __attribute__((always_inline)) {
         uint32_t b[4];
@@ -354,7 +366,7 @@ __device__ __forceinline__ bool do_ziplist(const Src &R, const Lane &l, uint32_t
         const uint32_t lo = big ? ab(b[2], b[1], 2) : ab(b[1], b[0], 2);   // bytes after the encoding byte
         const uint32_t hi = big ? ab(b[3], b[2], 2) : ab(b[2], b[1], 2);
         // (bitwise | and arithmetic selects, not || / ?: chains: the compiler turns those into
-        // exec-mask branches, ~60 % of the step's instructions)
+        // exec-mask branches)
         const bool zstr = e < 0xC0;
         const uint32_t scls = e >> 6;                        // string length class 0 / 1 / 2
         const uint32_t ls = 1 + scls + 2 * (scls >> 1);      // 1 / 2 / 5 length bytes
@@ -365,23 +377,25 @@ __device__ __forceinline__ bool do_ziplist(const Src &R, const Lane &l, uint32_t
                              4 * (uint32_t)(e == 0xD0) + 8 * (uint32_t)(e == 0xE0);
         const uint64_t endp = (uint64_t)qp + (zstr ? ls + sl : 1 + isz);
         const uint32_t pn = endp < zlast ? (uint32_t)endp : zlast;
-        nxt = R.template fetch<4>(pn);
+        nxt = R.template fetch<4>(live ? pn : p);
         const bool done = (b0 == 0xFF) & (p < zend);
         const bool bad = (p >= zend) | (big & (p + 5 > zlast)) | (pl != prev_raw) | (qp >= zlast) | (k >= l.r) |
                          (!zstr & !imm & (isz == 0)) | (zstr & (qp + ls > zlast)) | (endp > zlast);
-        if (done | bad) { fail = !done; return true; }
+        const bool emit = live & !done & !bad;
+        fail |= live & !done & bad;
         // little-endian integer of isz (1..4) bytes, sign-extended by a shift pair; 8 bytes; or
         // the 4-bit immediate
         const uint32_t sh = (32 - 8 * isz) & 31;
         const int64_t v32 = (int32_t)(lo << sh) >> sh;
         const int64_t iv = isz == 8 ? (int64_t)((uint64_t)lo | ((uint64_t)hi << 32)) : imm ? (int64_t)(e & 0x0F) - 1 : v32;
-        put_desc(l.E, l.slot(k), zstr ? l.B + qp + ls : (uint64_t)iv, zstr ? sl : 0, zstr ? RR_K_STR : RR_K_INT,
-                 zstr ? (e & 0xC0) : e);
-        prev_raw = (uint32_t)endp - p;
-        last = p;
-        p = pn;
-        ++k;
-        return false;
+        put_desc(l.E, emit ? l.slot(k) : NOSLOT, zstr ? l.B + qp + ls : (uint64_t)iv, zstr ? sl : 0,
+                 zstr ? RR_K_STR : RR_K_INT, zstr ? (e & 0xC0) : e);
+        prev_raw = emit ? (uint32_t)endp - p : prev_raw;
+        last = emit ? p : last;
+        p = emit ? pn : p;
+        k += emit;
+        live = emit;
+        return __ballot(live) == 0;
     };
     RR_PINGPONG(ra, rb, step)
     n = k;

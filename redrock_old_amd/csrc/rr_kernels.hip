@@ -546,42 +546,52 @@ __constant__ uint32_t CLASS_ORDER[C_N] = {C_ZL, C_SL, C_HT, C_LIST, C_EXACT, C_I
 
 // One single-class batch: lane < cnt decodes value v (byte offsets relative to the source,
 // whose byte 0 is batch offset B).
+// One single-class batch, run by the whole wave: lane < cnt (active) decodes value v (byte
+// offsets relative to the source, whose byte 0 is batch offset B).  The walks run the wave in
+// lock-step (rr_decode_class.h); values they reject, and the EXACT class, go to the exact
+// parser lane by lane.
 template <class Src>
-__device__ __forceinline__ Acc run_batch(const Src &src, uint32_t c, uint64_t v, uint64_t B, rsrc_t E, uint64_t eb0,
-                                         const uint8_t *__restrict__ blob, const uint64_t *__restrict__ offsets,
-                                         const uint64_t *__restrict__ ebase, rr_value *__restrict__ values,
-                                         rr_elem *__restrict__ elems, uint64_t cap) {
-    if (c == C_EXACT) return exact_value(blob, v, offsets, ebase, values, elems, cap);
-    const uint64_t o = offsets[v], o1 = offsets[v + 1], eb = ebase[v], r = ebase[v + 1] - eb;
-    Lane l;
-    l.q = (uint32_t)(o - B);
-    l.L = (uint32_t)(o1 - o);
+__device__ __forceinline__ Acc run_batch(const Src &src, uint32_t c, bool active, uint64_t v, uint64_t B, rsrc_t E,
+                                         uint64_t eb0, const uint8_t *__restrict__ blob,
+                                         const uint64_t *__restrict__ offsets, const uint64_t *__restrict__ ebase,
+                                         rr_value *__restrict__ values, rr_elem *__restrict__ elems, uint64_t cap) {
+    if (c == C_EXACT) return active ? exact_value(blob, v, offsets, ebase, values, elems, cap) : Acc{0, 0};
+    uint64_t eb = eb0, r = 0;
+    Lane l{};
     l.B = B;
     l.E = E;
-    l.so = (uint32_t)(eb - eb0) * 16;
-    l.r = (uint32_t)r;
-    l.ok = eb + r <= cap;
+    if (active) {
+        const uint64_t o = offsets[v], o1 = offsets[v + 1];
+        eb = ebase[v];
+        r = ebase[v + 1] - eb;
+        l.q = (uint32_t)(o - B);
+        l.L = (uint32_t)(o1 - o);
+        l.so = (uint32_t)(eb - eb0) * 16;
+        l.r = (uint32_t)r;
+        l.ok = eb + r <= cap;
+    }
     Head H;
     src.template get<4>(l.q, H.h);
     uint32_t ne = 1, enc = 0;
     uint64_t vp = 0;   // this value's payload bytes (counted once it is emitted)
     bool fail = false;
     if (c == C_STR) {
-        do_string(H, l, vp);
+        if (active) do_string(H, l, vp);
         enc = H.b5();
     } else if (c == C_IS) {
-        do_intset(src, H, l);
+        do_intset(src, H, l, active);
         ne = H.f9();
         enc = H.f5();
     } else if (c == C_LIST) {
-        fail = do_list(src, l, ne, vp);
+        fail = do_list(src, l, active, ne, vp);
     } else if (c == C_HT) {
-        fail = do_ht(src, H, l, ne, vp);
+        fail = do_ht(src, H, l, active, ne, vp);
     } else if (c == C_SL) {
-        fail = do_skiplist(src, H, l, ne, vp);
+        fail = do_skiplist(src, H, l, active, ne, vp);
     } else {
-        fail = do_ziplist(src, l, ne, vp);
+        fail = do_ziplist(src, l, active, ne, vp);
     }
+    if (!active) return Acc{0, 0};
     if (fail) return exact_value(blob, v, offsets, ebase, values, elems, cap);
     put_value(values + v, H.type(), enc, l.ok ? RR_OK : RR_E_CAPACITY, H.lru(), ne, (uint32_t)eb);
     return Acc{l.ok ? 0u : 1u, l.ok ? vp : 0};
@@ -707,6 +717,7 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
             const uint32_t i = j * NT + tid;
             const uint32_t ci = c0 == v_lo ? cls0[j] : i < nv ? (uint32_t)cls[c0 + i] : C_N;
             myc[j] = i < nv ? (far ? C_EXACT : ci) : C_N;
+            if (j * NT + wave * RR_WAVE >= nv) continue;   // (wave-uniform) no values in this round
 #pragma unroll
             for (uint32_t c = 0; c < C_N; ++c) {
                 const uint64_t m = __ballot(myc[j] == c);
@@ -729,6 +740,7 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
 #pragma unroll
         for (uint32_t j = 0; j < PMAX / NT; ++j) {
             const uint32_t i = j * NT + tid;
+            if (j * NT + wave * RR_WAVE >= nv) continue;
 #pragma unroll
             for (uint32_t c = 0; c < C_N; ++c) {
                 const uint64_t m = __ballot(myc[j] == c);
@@ -763,13 +775,12 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
             if ((RR_SKIP_CLASSES >> c) & 1) continue;
 #endif
             PROBE(const uint64_t tb0 = __builtin_amdgcn_s_memtime();)
-            if (lane < cnt) {
-                const uint64_t v = c0 + perm[first + lane];
-                const Acc a = staged ? run_batch(lsrc, c, v, S0, E, eb0, blob, offsets, ebase, values, elems, cap)
-                                     : run_batch(gsrc, c, v, S0, E, eb0, blob, offsets, ebase, values, elems, cap);
-                bad += a.bad;
-                pay += a.pay;
-            }
+            const bool active = lane < cnt;
+            const uint64_t v = c0 + (active ? perm[first + lane] : 0u);
+            const Acc a = staged ? run_batch(lsrc, c, active, v, S0, E, eb0, blob, offsets, ebase, values, elems, cap)
+                                 : run_batch(gsrc, c, active, v, S0, E, eb0, blob, offsets, ebase, values, elems, cap);
+            bad += a.bad;
+            pay += a.pay;
             PROBE(if (lane == 0) {
                 atomicAdd((unsigned long long *)&prb[3 + c], (unsigned long long)(__builtin_amdgcn_s_memtime() - tb0));
                 atomicAdd((unsigned long long *)&prb[10 + c], 1ull);
