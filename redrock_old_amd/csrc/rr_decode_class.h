@@ -154,7 +154,11 @@ __device__ __forceinline__ void put_desc(rsrc_t E, uint32_t off, uint64_t data, 
     w.y = (uint32_t)(data >> 32);
     w.z = len;
     w.w = kind | (zenc << 8);
+#ifndef RR_ABLATE_NOSTORE   // timing-only builds (tools/)
     __builtin_amdgcn_raw_buffer_store_b128(w, E, (int)off, 0, 0);
+#else
+    asm volatile("" ::"v"(w.x), "v"(w.y), "v"(w.z), "v"(w.w), "v"(off));
+#endif
 }
 
 __device__ __forceinline__ void put_value(rr_value *v, uint32_t type, uint32_t enc, uint32_t status, uint32_t lru,
@@ -229,6 +233,7 @@ __device__ __forceinline__ void do_intset(const Src &R, const Head &H, const Lan
         uint32_t x[2];
         cur.align(x);
         nxt = R.template fetch<2>(p + w);   // (reads may run past the value: in range of the source)
+        __builtin_amdgcn_sched_barrier(0);   // keep the read ahead of the checks and the store
         const int64_t v = w == 2 ? (int64_t)(int16_t)(x[0] & 0xFFFF)
                         : w == 4 ? (int64_t)(int32_t)x[0] : (int64_t)((uint64_t)x[0] | ((uint64_t)x[1] << 32));
         put_desc(l.E, live ? l.so + 16 * k : NOSLOT, (uint64_t)v, 0, RR_K_INT, 0);
@@ -254,6 +259,7 @@ __device__ __forceinline__ bool do_list(const Src &R, const Lane &l, bool active
         const uint64_t nx = (uint64_t)p + 4 + len;
         const uint32_t pn = nx < end ? (uint32_t)nx : end;
         nxt = R.template fetch<6>(live ? pn : p);
+        __builtin_amdgcn_sched_barrier(0);   // keep the read ahead of the checks and the store
         const bool done = p == end;
         const bool bad = (rem < 4) | (len > rem - 4) | (k >= l.r);
         const bool emit = live & !done & !bad;
@@ -290,6 +296,7 @@ __device__ __forceinline__ bool do_ht(const Src &R, const Head &H, const Lane &l
         const uint64_t nx = (uint64_t)p + 8 + b[0];
         const uint32_t pn = ((nx < end) & (b[1] == 0)) ? (uint32_t)nx : end;
         nxt = R.template fetch<2>(live ? pn : p);
+        __builtin_amdgcn_sched_barrier(0);   // keep the read ahead of the checks and the store
         const bool done = p == end;
         const bool bad = (rem < 8) | (b[1] != 0) | (b[0] > rem - 8) | (k >= l.r);
         const bool emit = live & !done & !bad;
@@ -324,6 +331,7 @@ __device__ __forceinline__ bool do_skiplist(const Src &R, const Head &H, const L
         const uint64_t nx = (uint64_t)p + 8 + (score ? 0u : b[0]);
         const uint32_t pn = ((nx < end) & (score | (b[1] == 0))) ? (uint32_t)nx : end;
         nxt = R.template fetch<2>(live ? pn : p);
+        __builtin_amdgcn_sched_barrier(0);   // keep the read ahead of the checks and the store
         const bool done = p == end;
         const bool bad = (rem < 8) | (k >= l.r) | (!score & ((b[1] != 0) | (b[0] > rem - 8)));
         const bool emit = live & !done & !bad;
@@ -378,6 +386,7 @@ __device__ __forceinline__ bool do_ziplist(const Src &R, const Lane &l, bool act
         const uint64_t endp = (uint64_t)qp + (zstr ? ls + sl : 1 + isz);
         const uint32_t pn = endp < zlast ? (uint32_t)endp : zlast;
         nxt = R.template fetch<4>(live ? pn : p);
+        __builtin_amdgcn_sched_barrier(0);   // keep the read ahead of the checks and the store
         const bool done = (b0 == 0xFF) & (p < zend);
         const bool bad = (p >= zend) | (big & (p + 5 > zlast)) | (pl != prev_raw) | (qp >= zlast) | (k >= l.r) |
                          (!zstr & !imm & (isz == 0)) | (zstr & (qp + ls > zlast)) | (endp > zlast);

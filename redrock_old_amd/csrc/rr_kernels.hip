@@ -676,13 +676,17 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const uint64_t cc = c + k * NT;
+#ifndef RR_ABLATE_NOCOPY   // timing-only builds (tools/)
                 if (cc < cw1) __builtin_nontemporal_store(x[k], dst + cc);
+#endif
                 if (staged && cc >= cs0) lds[cc - cs0] = x[k];
             }
         }
         for (; c < ce; c += NT) {
             const u32x4 x = src[c];
+#ifndef RR_ABLATE_NOCOPY
             if (c < cw1) __builtin_nontemporal_store(x, dst + c);
+#endif
             if (staged && c >= cs0) lds[c - cs0] = x;
         }
     }

@@ -1,0 +1,44 @@
+"""Turn a tools/profile_bench.sh directory into the committed profile summary:
+per-kernel average durations (kernel trace) and per-launch HBM traffic of one
+rr_decode_batch call (FETCH_SIZE x2, the MI355X_MICROARCH.md gfx950 correction for 16 B/lane
+streaming reads, + WRITE_SIZE; both in KB per dispatch), summed over the pipeline's kernels.
+Usage: python tools/traffic_summary.py PROFDIR OUT.json"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+d, out = sys.argv[1], sys.argv[2]
+
+
+def short(name):
+    return name.split("(")[0].split("::")[-1].split("<")[0].strip()
+
+
+res = {"kernels": {}, "traffic_bytes_per_call": None}
+for p in glob.glob(os.path.join(d, "trace", "*kernel_stats.csv")):
+    for r in csv.DictReader(open(p)):
+        res["kernels"][short(r["Name"])] = {"calls": int(r["Calls"]), "avg_us": float(r["AverageNs"]) / 1e3}
+per = collections.defaultdict(dict)
+for c in ("FETCH_SIZE", "WRITE_SIZE"):
+    for p in glob.glob(os.path.join(d, c, "*counter_collection.csv")):
+        acc = collections.defaultdict(float)
+        disp = collections.defaultdict(set)
+        for r in csv.DictReader(open(p)):
+            k = short(r["Kernel_Name"])
+            acc[k] += float(r["Counter_Value"])
+            disp[k].add(r["Dispatch_Id"])
+        for k in acc:
+            per[k][c] = acc[k] / len(disp[k]) * 1024   # KB -> bytes, per dispatch
+pipeline = ("count_kernel", "scan_kernel", "decode_kernel", "finalize_kernel")
+tot = 0.0
+for k in pipeline:
+    if k in per:
+        f, w = per[k].get("FETCH_SIZE", 0.0), per[k].get("WRITE_SIZE", 0.0)
+        res["kernels"].setdefault(k, {}).update({"fetch_bytes": f, "write_bytes": w, "hbm_bytes": 2 * f + w})
+        tot += 2 * f + w
+res["traffic_bytes_per_call"] = tot if per else None
+json.dump(res, open(out, "w"), indent=1)
+print(json.dumps(res, indent=1))
