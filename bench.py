@@ -177,8 +177,9 @@ def main():
         "encode": {"gib_s": round(enc_gib_s, 2), "ms_per_step": round(wall_enc / args.steps * 1e3, 4),
                    "event_ms_per_launch": round(ev_enc, 4),
                    "roofline_achieved_GBs": round(enc_achieved, 1)},
-        "roofline": {"bound": "hbm", "kernel": "decode_kernel", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+        "roofline": {"bound": "hbm", "kernel": "rr_decode_batch (count+scan+decode+finalize kernels)",
+                     "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": measured_traffic(args.config, n, nb),
                      "alg_bytes_per_launch": alg_bytes},
         "parity": parity,
         "gen_s": round(t_gen, 2),
@@ -191,6 +192,22 @@ def main():
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def measured_traffic(config, n, nb):
+    """HBM bytes per decode call from the committed rocprofv3 PMC summary of this workload
+    (tools/profile_bench.sh + tools/traffic_summary.py), or None if none matches."""
+    import glob
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_decode_summary.json")), reverse=True):
+        try:
+            with open(p) as f:
+                d = json.load(f)
+            w = d.get("workload", {})
+            if (w.get("config"), w.get("n"), w.get("blob_bytes")) == (config, n, nb) and d.get("traffic_bytes_per_call"):
+                return int(d["traffic_bytes_per_call"])
+        except (OSError, ValueError):
+            continue
+    return None
 
 
 def cpu_baseline(data, offs, nb, budget_s):

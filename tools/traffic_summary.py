@@ -8,13 +8,15 @@ import csv
 import glob
 import json
 import os
+import re
 import sys
 
 d, out = sys.argv[1], sys.argv[2]
 
 
 def short(name):
-    return name.split("(")[0].split("::")[-1].split("<")[0].strip()
+    m = re.search(r"(\w+_kernel)\b", name)
+    return m.group(1) if m else name.split("(")[0].strip()
 
 
 res = {"kernels": {}, "traffic_bytes_per_call": None}
