@@ -85,7 +85,7 @@ static int ensure_scratch(rr_ctx *c, uint64_t words) {
 
 int rr_ctx_reserve(rr_ctx *c, uint64_t n_values, uint64_t n_bytes) {
     if (!c) return fail(RR_API_EINVAL, "ctx is NULL");
-    uint64_t a = rr_encode_scratch_words(n_values), b = rr_decode_scratch_words((n_bytes + 15) & ~15ull, n_values);
+    uint64_t a = rr_encode_scratch_words(n_values, (n_bytes + 15) & ~15ull), b = rr_decode_scratch_words((n_bytes + 15) & ~15ull, n_values);
     return ensure_scratch(c, a > b ? a : b);
 }
 
@@ -120,7 +120,8 @@ int rr_encode_batch(rr_ctx *c, const rr_flat_batch *in, rr_blob_batch *out, rr_t
     if (in->n >= (1ull << 37)) return fail(RR_API_EINVAL, "batch too large");
     if (!out->offsets) return fail(RR_API_EINVAL, "NULL offsets");
     if (in->n && (!in->values || !out->data)) return fail(RR_API_EINVAL, "NULL buffer");
-    int rc = ensure_scratch(c, rr_encode_scratch_words(in->n));
+    if ((uintptr_t)out->data & 15) return fail(RR_API_EINVAL, "out->data must be 16-byte aligned");
+    int rc = ensure_scratch(c, rr_encode_scratch_words(in->n, out->data_cap));
     if (rc) return rc;
     HIPCHK(rr_launch_encode(in->values, in->elems, in->arena, in->n, out->data, out->data_cap, out->offsets,
                             c->scratch, d_totals, (hipStream_t)stream));

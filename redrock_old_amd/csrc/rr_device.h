@@ -84,6 +84,15 @@ __device__ __forceinline__ uint32_t dec_write(uint8_t *d, int64_t value) {
 
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
 
+// Workgroup barrier that orders LDS only.  __syncthreads() is a workgroup-scope fence for all
+// memory: it makes every wave wait for the acknowledgement of its outstanding global stores
+// (s_waitcnt vmcnt(0)), ~1-2 us behind a burst of streaming stores.
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // Wave64 inclusive scan (u64) with shuffles.
 __device__ __forceinline__ uint64_t wave_incl_scan(uint64_t x) {
     uint32_t lane = lane_id();

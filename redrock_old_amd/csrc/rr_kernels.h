@@ -24,7 +24,7 @@ hipError_t rr_launch_encode(const rr_value *values, const rr_elem *elems, const 
                             uint8_t *out, uint64_t cap, uint64_t *offsets, uint64_t *scratch,
                             rr_totals *totals, hipStream_t stream);
 uint64_t rr_decode_scratch_words(uint64_t data_cap, uint64_t n);
-uint64_t rr_encode_scratch_words(uint64_t n);
+uint64_t rr_encode_scratch_words(uint64_t n, uint64_t data_cap);
 
 #ifdef __cplusplus
 }

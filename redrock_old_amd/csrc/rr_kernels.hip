@@ -25,9 +25,7 @@ using namespace rr;
 
 namespace {
 
-constexpr uint32_t TILE = RR_WAVE;       // values per wave tile
 
-constexpr uint32_t WG = 256;             // 4 independent waves per workgroup
 
 struct Parsed {
     uint32_t status;
@@ -898,166 +896,331 @@ __device__ uint64_t encode_size(uint32_t type, uint32_t enc, uint64_t n, const r
     return 0;
 }
 
-__device__ __forceinline__ void st_bytes(uint8_t *d, uint64_t v, uint32_t nb) {
-    for (uint32_t i = 0; i < nb; ++i) d[i] = (uint8_t)(v >> (8 * i));
-}
+// Encode runs as five launches (one memset, no inter-workgroup waits beyond the scan's
+// look-back):
+//   E1 enc_size_kernel  thread per value: blob size (0 for an unencodable value) into
+//                       offsets[v], per-tile {bad, payload, descriptors};
+//   E2 scan_kernel      in-place exclusive scan -> offsets[0..n];
+//   E3 enc_index_kernel thread per value: first value of every W-byte output window, and the
+//                       values that would cross data_cap (RR_E_CAPACITY, payload taken back);
+//   E4 enc_emit_kernel  workgroup per W-byte output window: builds the window's bytes in an
+//                       LDS image (headers and length fields by element-parallel tasks,
+//                       payloads by 64-byte copy pieces), then stores it with 16-byte
+//                       coalesced stores;
+//   E5 finalize         totals.
+// Output bytes past the last value that fits (and of a value that does not fit) are zero.
 
-constexpr uint32_t BULK = 32;        // payloads longer than this are copied by the whole wave
-constexpr uint32_t QCAP = 256;       // bulk-copy queue entries per wave
-
-struct BulkQ {
-    uint64_t dst[QCAP];
-    uint64_t src[QCAP];
-    uint32_t len[QCAP];
-};
-
-// Wave-cooperative byte copy arena[src..] -> blob[dst..]: aligned dword stores in the middle,
-// byte stores at the ends (neighbouring values own the bytes around the segment).
-__device__ __forceinline__ void wave_copy(uint8_t *__restrict__ dst, const uint8_t *__restrict__ src, uint64_t len) {
-    const uint32_t lane = lane_id();
-    uint64_t head = (4 - ((uintptr_t)dst & 3)) & 3;
-    if (head > len) head = len;
-    if (lane < head) dst[lane] = src[lane];
-    uint64_t body = (len - head) & ~3ull;
-    uint32_t *d4 = reinterpret_cast<uint32_t *>(dst + head);
-    const uint8_t *s4 = src + head;
-    for (uint64_t k = lane; k < (body >> 2); k += RR_WAVE) {
-        uint32_t w;
-        __builtin_memcpy(&w, s4 + 4 * k, 4);
-        d4[k] = w;
-    }
-    uint64_t tail = len - head - body;
-    if (lane < tail) dst[head + body + lane] = src[head + body + lane];
-}
-
-__global__ __launch_bounds__(WG) void encode_kernel(const rr_value *__restrict__ values,
-                                                    const rr_elem *__restrict__ elems,
-                                                    const uint8_t *__restrict__ arena, uint64_t n,
-                                                    uint8_t *__restrict__ out, uint64_t cap,
-                                                    uint64_t *__restrict__ offsets, uint64_t *scratch,
-                                                    uint32_t ntiles) {
-    __shared__ BulkQ qs[WG / RR_WAVE];
-    __shared__ uint32_t qn[WG / RR_WAVE];
-    const uint32_t lane = lane_id();
-    BulkQ &q = qs[threadIdx.x / RR_WAVE];
-    uint64_t *state = scratch + RR_SCRATCH_HDR;
-    uint64_t *groups = state + ntiles;
-    uint64_t *stats = groups + (ntiles + LB_GROUP - 1) / LB_GROUP;
-    const uint32_t nwaves = gridDim.x * (WG / RR_WAVE);
-    for (uint32_t tile = blockIdx.x * (WG / RR_WAVE) + threadIdx.x / RR_WAVE; tile < ntiles; tile += nwaves) {
-    const uint64_t v = (uint64_t)tile * TILE + lane;
-    const bool active = v < n;
-
-    uint32_t type = 0, enc = 0, lru = 0, st = RR_OK;
-    uint64_t ne = 0, eb = 0, size = 0, pay = 0;
-    if (active) {
-        uint4 w = reinterpret_cast<const uint4 *>(values)[v];
-        type = w.x & 0xFF;
-        enc = (w.x >> 8) & 0xFF;
-        lru = w.y & RR_LRU_MASK;
+// ---- E1: blob size per value -----------------------------------------------------------
+__global__ __launch_bounds__(256) void enc_size_kernel(const rr_value *__restrict__ values,
+                                                       const rr_elem *__restrict__ elems, uint64_t n,
+                                                       uint64_t *__restrict__ sizes, uint64_t *__restrict__ stats) {
+    __shared__ uint64_t red[3][4];
+    const uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint64_t size = 0, pay = 0, ne = 0, bad = 0;
+    if (v < n) {
+        const uint4 w = reinterpret_cast<const uint4 *>(values)[v];
+        uint32_t st;
         ne = w.z;
-        eb = w.w;
-        size = encode_size(type, enc, ne, elems + eb, st, pay);
+        size = encode_size(w.x & 0xFF, (w.x >> 8) & 0xFF, ne, elems + w.w, st, pay);
+        bad = st != RR_OK;
+        sizes[v] = size;
     }
-    const uint64_t incl = wave_incl_scan(size);
-    const uint64_t agg = __shfl(incl, RR_WAVE - 1, RR_WAVE);
-    const uint64_t prefix = lookback(state, groups, tile, ntiles, agg);
-    const uint64_t o = prefix + incl - size;
-    if (active) offsets[v] = o;
-    if (tile == ntiles - 1 && lane == 0) offsets[n] = prefix + agg;
+    bad = wave_sum(bad);
+    pay = wave_sum(pay);
+    ne = wave_sum(ne);
+    const uint32_t wv = threadIdx.x / RR_WAVE;
+    if (lane_id() == 0) { red[0][wv] = bad; red[1][wv] = pay; red[2][wv] = ne; }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        uint64_t s = 0;
+        for (uint32_t k = 0; k < blockDim.x / RR_WAVE; ++k) s += red[threadIdx.x][k];
+        stats[3 * (uint64_t)blockIdx.x + threadIdx.x] = s;
+    }
+}
 
-    bool ok = active && st == RR_OK && o + size <= cap;
-    if (lane == 0) qn[threadIdx.x / RR_WAVE] = 0;
-    __builtin_amdgcn_wave_barrier();
-    if (ok) {
-        uint8_t *d = out + o;
-        const rr_elem *el = elems + eb;
-        d[0] = (uint8_t)type;
-        st_bytes(d + 1, lru, 4);
-        uint64_t p = 5;
-        auto copy = [&](uint64_t dpos, uint64_t src, uint32_t len) {
-            if (len > BULK) {
-                uint32_t slot = atomicAdd(&qn[threadIdx.x / RR_WAVE], 1u);
-                if (slot < QCAP) { q.dst[slot] = o + dpos; q.src[slot] = src; q.len[slot] = len; return; }
+// ---- E3: window index + capacity check ---------------------------------------------------
+// fv[w] = the value holding output byte w*W (values of size 0 hold none).  A value whose end
+// passes data_cap is not written (rock_serdes has no such case: sds grows; the batch API
+// bounds the output): it counts as bad and its payload is taken back out of the totals
+// (stored as a two's-complement negative, folded by the same modular sum).
+template <uint32_t W>
+__global__ __launch_bounds__(256) void enc_index_kernel(const rr_value *__restrict__ values,
+                                                        const rr_elem *__restrict__ elems, uint64_t n,
+                                                        const uint64_t *__restrict__ offsets, uint64_t cap,
+                                                        uint32_t *__restrict__ fv, uint64_t nwin,
+                                                        uint64_t *__restrict__ stats) {
+    __shared__ uint64_t red[2][4];
+    const uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint64_t bad = 0, pay = 0;
+    if (v < n) {
+        const uint64_t a = offsets[v], b = offsets[v + 1];
+        if (b > a) {
+            uint64_t w_hi = (b - 1) / W;
+            if (w_hi > nwin) w_hi = nwin;
+            for (uint64_t w = (a + W - 1) / W; w <= w_hi; ++w) fv[w] = (uint32_t)v;
+            if (b > cap) {
+                const uint4 x = reinterpret_cast<const uint4 *>(values)[v];
+                uint32_t st;
+                encode_size(x.x & 0xFF, (x.x >> 8) & 0xFF, x.z, elems + x.w, st, pay);
+                bad = 1;
+                pay = 0ull - pay;
             }
-            for (uint32_t i = 0; i < len; ++i) d[dpos + i] = arena[src + i];
-        };
-        switch (type) {
-            case RR_TYPE_STRING: {
-                ElemV e = get_elem(el);
-                d[5] = (uint8_t)enc;
-                if (enc == RR_ENC_INT) st_bytes(d + 6, e.data, 8);
-                else copy(6, e.data, e.len);
-                break;
-            }
-            case RR_TYPE_LIST_QUICKLIST:
-                for (uint64_t i = 0; i < ne; ++i) {
-                    ElemV e = get_elem(el + i);
-                    if (e.kind == RR_K_INT) {
-                        uint32_t l = dec_write(d + p + 4, (int64_t)e.data);
-                        st_bytes(d + p, l, 4);
-                        p += 4 + l;
-                    } else {
-                        st_bytes(d + p, e.len, 4);
-                        copy(p + 4, e.data, e.len);
-                        p += 4 + (uint64_t)e.len;
-                    }
-                }
-                break;
-            case RR_TYPE_SET_INTSET:
-                st_bytes(d + p, enc, 4);
-                st_bytes(d + p + 4, ne, 4);
-                p += 8;
-                for (uint64_t i = 0; i < ne; ++i) {
-                    ElemV e = get_elem(el + i);
-                    st_bytes(d + p, e.data, enc);
-                    p += enc;
-                }
-                break;
-            case RR_TYPE_SET_HT:
-            case RR_TYPE_HASH_HT:
-                st_bytes(d + p, type == RR_TYPE_SET_HT ? ne : ne / 2, 8);
-                p += 8;
-                for (uint64_t i = 0; i < ne; ++i) {
-                    ElemV e = get_elem(el + i);
-                    st_bytes(d + p, e.len, 8);
-                    copy(p + 8, e.data, e.len);
-                    p += 8 + (uint64_t)e.len;
-                }
-                break;
-            case RR_TYPE_HASH_ZIPLIST:
-            case RR_TYPE_ZSET_ZIPLIST: {
-                ElemV e = get_elem(el);
-                st_bytes(d + p, e.len, 8);
-                copy(p + 8, e.data, e.len);
-                break;
-            }
-            case RR_TYPE_ZSET_SKIPLIST:
-                st_bytes(d + p, ne / 2, 8);
-                p += 8;
-                for (uint64_t i = 0; i < ne; i += 2) {
-                    ElemV a = get_elem(el + i), b = get_elem(el + i + 1);
-                    st_bytes(d + p, a.len, 8);
-                    copy(p + 8, a.data, a.len);
-                    p += 8 + (uint64_t)a.len;
-                    st_bytes(d + p, b.data, 8);
-                    p += 8;
-                }
-                break;
         }
     }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    // bulk copies by the whole wave (queue overflow was copied lane-serially above)
-    uint32_t qcount = qn[threadIdx.x / RR_WAVE];
-    if (qcount > QCAP) qcount = QCAP;
-    for (uint32_t k = 0; k < qcount; ++k) wave_copy(out + q.dst[k], arena + q.src[k], q.len[k]);
-
-    const uint64_t bad = wave_sum(active && !ok ? 1 : 0);
-    const uint64_t payt = wave_sum(ok ? pay : 0);
-    const uint64_t nel = wave_sum(ne);
-    tile_stats(stats, tile, bad, payt, nel);
+    bad = wave_sum(bad);
+    pay = wave_sum(pay);
+    const uint32_t wv = threadIdx.x / RR_WAVE;
+    if (lane_id() == 0) { red[0][wv] = bad; red[1][wv] = pay; }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        uint64_t s = 0;
+        if (threadIdx.x < 2)
+            for (uint32_t k = 0; k < blockDim.x / RR_WAVE; ++k) s += red[threadIdx.x][k];
+        stats[3 * (uint64_t)blockIdx.x + threadIdx.x] = s;
     }
+}
+
+// ---- E4: window emission -------------------------------------------------------------------
+// Blob layout per type (serObject rock_serdes.c:512-535): a value is a header of h bytes then
+// one "task" per descriptor, each task writing es bytes:
+//   STRING    h=6  (type, lru, enc)            INT: 8 (i64)           STR: len (payload)
+//   LIST      h=5                              INT: 4 + decimal       STR: 4 + len
+//   INTSET    h=13 (+ u32 enc, u32 count)      enc bytes of the int
+//   SET/HASH HT  h=13 (+ u64 count)            8 + len
+//   ZIPLIST   h=5,  one task (descriptor 0, the raw ziplist): 8 + len
+//   SKIPLIST  h=13 (+ u64 count)               member: 8 + len        score: 8 (raw f64)
+__device__ __forceinline__ uint32_t enc_hdr(uint32_t type) {
+    return type == RR_TYPE_STRING ? 6u : (type == RR_TYPE_LIST_QUICKLIST || type == RR_TYPE_HASH_ZIPLIST ||
+                                          type == RR_TYPE_ZSET_ZIPLIST) ? 5u : 13u;
+}
+
+// Decimal digits of an unsigned magnitude (sdsll2str's length without the sign).
+__device__ __forceinline__ uint32_t udigits(uint64_t v) {
+    uint32_t l = 1;
+    uint64_t p = 10;
+#pragma unroll
+    for (int k = 1; k < 20; ++k) {
+        l += v >= p ? 1u : 0u;
+        p = k < 19 ? p * 10 : p;
+    }
+    return l;
+}
+
+// The window image: byte writes at absolute output positions, clipped to [w0, w0 + span).
+struct Img {
+    uint8_t *img;
+    uint64_t w0;
+    uint64_t span;
+    __device__ __forceinline__ void put(uint64_t pos, uint32_t b) const {
+        const uint64_t d = pos - w0;
+        if (d < span) img[d] = (uint8_t)b;
+    }
+    // little-endian field of nb bytes
+    __device__ __forceinline__ void field(uint64_t pos, uint64_t v, uint32_t nb) const {
+        const uint64_t d = pos - w0;
+        if (d < span && d + nb <= span) {
+            if (nb == 8) __builtin_memcpy(img + d, &v, 8);
+            else if (nb == 4) { const uint32_t x = (uint32_t)v; __builtin_memcpy(img + d, &x, 4); }
+            else if (nb == 2) { const uint16_t x = (uint16_t)v; __builtin_memcpy(img + d, &x, 2); }
+            else img[d] = (uint8_t)v;
+        } else {
+            for (uint32_t i = 0; i < nb; ++i) put(pos + i, (uint32_t)(v >> (8 * i)) & 0xFF);
+        }
+    }
+    // sdsll2str(x) (sds.c:450-479) of l characters at pos
+    __device__ __forceinline__ void decimal(uint64_t pos, int64_t x, uint32_t l) const {
+        uint64_t u = x < 0 ? 0ull - (uint64_t)x : (uint64_t)x;
+        uint64_t p = pos + l;
+        if (x < 0) put(pos, '-');
+        while (u >= (1ull << 32)) { put(--p, '0' + (uint32_t)(u % 10)); u /= 10; }
+        uint32_t s = (uint32_t)u;
+        do { put(--p, '0' + s % 10); s /= 10; } while (s);
+    }
+};
+
+// 64-byte copy piece: arena bytes [src, src+len) -> image bytes [dst, dst+len), len <= 64.
+// Unaligned 16-byte global loads and LDS stores (gfx950 allows both), exact byte extent.
+__device__ __forceinline__ void copy_piece(uint8_t *img, uint32_t dst, const uint8_t *__restrict__ src, uint32_t len) {
+    uint4 x[4];
+    const uint32_t full = len >> 4;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k)
+        if (k < full) __builtin_memcpy(&x[k], src + 16 * k, 16);
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k)
+        if (k < full) __builtin_memcpy(img + dst + 16 * k, &x[k], 16);
+    for (uint32_t i = full << 4; i < len; ++i) img[dst + i] = src[i];
+}
+
+template <uint32_t NT>
+__device__ __forceinline__ uint64_t block_excl_scan(uint64_t x, uint64_t *wsum, uint64_t &total) {
+    const uint64_t incl = wave_incl_scan(x);
+    const uint32_t wv = threadIdx.x / RR_WAVE;
+    if (lane_id() == RR_WAVE - 1) wsum[wv] = incl;
+    lds_barrier();
+    uint64_t pre = 0, t = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < NT / RR_WAVE; ++k) {
+        const uint64_t s = wsum[k];
+        pre += k < wv ? s : 0;
+        t += s;
+    }
+    total = t;
+    return pre + incl - x;
+}
+
+template <uint32_t W, uint32_t NT, uint32_t JCAP>
+__global__ __launch_bounds__(NT) void enc_emit_kernel(const rr_value *__restrict__ values,
+                                                      const rr_elem *__restrict__ elems,
+                                                      const uint8_t *__restrict__ arena, uint64_t n,
+                                                      uint8_t *__restrict__ out, uint64_t cap,
+                                                      const uint64_t *__restrict__ offsets,
+                                                      const uint32_t *__restrict__ fv) {
+    __shared__ uint4 img4[W / 16];
+    __shared__ uint64_t j_src[JCAP];
+    __shared__ uint16_t j_dst[JCAP];
+    __shared__ uint8_t j_len[JCAP];
+    __shared__ uint32_t tb[NT + 1];        // task base of each value of the round
+    __shared__ uint64_t sv_pos[NT];        // output position of the value's first task
+    __shared__ uint64_t sv_eb[NT];         // element-byte scan at the value's first task
+    __shared__ uint32_t sv_el[NT];         // elem_base
+    __shared__ uint32_t sv_te[NT];         // type | enc << 8
+    __shared__ uint64_t wsum[2][NT / RR_WAVE];
+    __shared__ uint32_t sh_nj;
+    uint8_t *img = reinterpret_cast<uint8_t *>(img4);
+    const uint32_t tid = threadIdx.x;
+    const uint64_t total = offsets[n];
+    const uint64_t lim = total < cap ? total : cap;
+    const uint64_t w0 = (uint64_t)blockIdx.x * W;
+    if (w0 >= lim) return;
+    const uint64_t span = lim - w0 < W ? lim - w0 : W;
+    const Img I{img, w0, span};
+#pragma unroll
+    for (uint32_t k = tid; k < W / 16; k += NT) img4[k] = make_uint4(0, 0, 0, 0);
+    if (tid == 0) sh_nj = 0;
+    const uint64_t v0 = fv[blockIdx.x];
+    const uint64_t vend = w0 + W < total ? (uint64_t)fv[blockIdx.x + 1] + 1 : n;
+    lds_barrier();
+
+    auto payload = [&](uint64_t pos, uint64_t src, uint64_t len) {
+        // clip to the window, then 64-byte pieces into the queue (inline when it is full)
+        uint64_t d0 = pos < w0 ? w0 : pos, d1 = pos + len;
+        if (d1 > w0 + span) d1 = w0 + span;
+        if (d0 >= d1) return;
+        src += d0 - pos;
+        const uint32_t dst = (uint32_t)(d0 - w0), l = (uint32_t)(d1 - d0);
+        const uint32_t np = (l + 63) >> 6;
+        const uint32_t j = atomicAdd(&sh_nj, np);
+        for (uint32_t k = 0; k < np; ++k) {
+            const uint32_t pl = k + 1 < np ? 64u : l - 64u * k;
+            if (j + k < JCAP) {
+                j_src[j + k] = src + 64u * k;
+                j_dst[j + k] = (uint16_t)(dst + 64u * k);
+                j_len[j + k] = (uint8_t)pl;
+            } else
+                copy_piece(img, dst + 64u * k, arena + src + 64u * k, pl);
+        }
+    };
+
+    for (uint64_t vb = v0; vb < vend; vb += NT) {
+        const uint64_t v = vb + tid;
+        uint32_t tasks = 0;
+        if (v < vend) {
+            const uint64_t a = offsets[v], b = offsets[v + 1];
+            if (b > a && b <= cap) {
+                const uint4 x = reinterpret_cast<const uint4 *>(values)[v];
+                const uint32_t type = x.x & 0xFF, enc = (x.x >> 8) & 0xFF, ne = x.z;
+                I.put(a, type);
+                I.field(a + 1, x.y & RR_LRU_MASK, 4);
+                if (type == RR_TYPE_STRING) I.put(a + 5, enc);
+                else if (type == RR_TYPE_SET_INTSET) { I.field(a + 5, enc, 4); I.field(a + 9, ne, 4); }
+                else if (type == RR_TYPE_SET_HT) I.field(a + 5, ne, 8);
+                else if (type == RR_TYPE_HASH_HT || type == RR_TYPE_ZSET_SKIPLIST) I.field(a + 5, ne / 2, 8);
+                tasks = (type == RR_TYPE_HASH_ZIPLIST || type == RR_TYPE_ZSET_ZIPLIST) ? 1u : ne;
+                sv_pos[tid] = a + enc_hdr(type);
+                sv_el[tid] = x.w;
+                sv_te[tid] = type | (enc << 8);
+            }
+        }
+        uint64_t tt;
+        const uint32_t base = (uint32_t)block_excl_scan<NT>(tasks, wsum[0], tt);
+        tb[tid] = base;
+        if (tid == NT - 1) tb[NT] = base + tasks;
+        lds_barrier();
+        uint64_t run = 0;   // element bytes of the earlier task rounds
+        for (uint64_t r0 = 0; r0 < tt; r0 += NT) {
+            const uint64_t t = r0 + tid;
+            const bool act = t < tt;
+            uint32_t j = 0;
+            uint64_t es = 0;
+            ElemV e{0, 0, 0};
+            uint32_t type = 0, enc = 0, k = 0;
+            if (act) {
+                // last value j with tb[j] <= t
+                uint32_t lo = 0;
+#pragma unroll
+                for (uint32_t s = NT / 2; s > 0; s >>= 1)
+                    if (tb[lo + s] <= t) lo += s;
+                j = lo;
+                k = (uint32_t)(t - tb[j]);
+                type = sv_te[j] & 0xFF;
+                enc = sv_te[j] >> 8;
+                e = get_elem(elems + sv_el[j] + k);
+                switch (type) {
+                    case RR_TYPE_STRING: es = enc == RR_ENC_INT ? 8 : e.len; break;
+                    case RR_TYPE_LIST_QUICKLIST:
+                        es = 4 + (e.kind == RR_K_INT ? udigits((int64_t)e.data < 0 ? 0ull - e.data : e.data) +
+                                                           ((int64_t)e.data < 0 ? 1u : 0u)
+                                                     : e.len);
+                        break;
+                    case RR_TYPE_SET_INTSET: es = enc; break;
+                    case RR_TYPE_ZSET_SKIPLIST: es = (k & 1) ? 8 : 8 + (uint64_t)e.len; break;
+                    default: es = 8 + (uint64_t)e.len; break;   // HT members, ziplist raw
+                }
+            }
+            uint64_t rt;
+            const uint64_t ex = run + block_excl_scan<NT>(es, wsum[1], rt);
+            if (act && k == 0) sv_eb[j] = ex;
+            lds_barrier();
+            if (act) {
+                const uint64_t p = sv_pos[j] + ex - sv_eb[j];
+                switch (type) {
+                    case RR_TYPE_STRING:
+                        if (enc == RR_ENC_INT) I.field(p, e.data, 8);
+                        else payload(p, e.data, e.len);
+                        break;
+                    case RR_TYPE_LIST_QUICKLIST:
+                        I.field(p, es - 4, 4);
+                        if (e.kind == RR_K_INT) I.decimal(p + 4, (int64_t)e.data, (uint32_t)(es - 4));
+                        else payload(p + 4, e.data, e.len);
+                        break;
+                    case RR_TYPE_SET_INTSET: I.field(p, e.data, enc); break;
+                    case RR_TYPE_ZSET_SKIPLIST:
+                        if (k & 1) { I.field(p, e.data, 8); break; }
+                        [[fallthrough]];
+                    default:
+                        I.field(p, e.len, 8);
+                        payload(p + 8, e.data, e.len);
+                        break;
+                }
+            }
+            run += rt;
+        }
+        lds_barrier();
+    }
+
+    // payload pieces
+    const uint32_t nj = sh_nj < JCAP ? sh_nj : JCAP;
+    for (uint32_t j = tid; j < nj; j += NT) copy_piece(img, j_dst[j], arena + j_src[j], j_len[j]);
+    lds_barrier();
+
+    // store the image: 16-byte chunks, bytes at a partial end
+    u32x4 *dst4 = reinterpret_cast<u32x4 *>(out + w0);
+    const u32x4 *src4 = reinterpret_cast<const u32x4 *>(img4);
+    const uint32_t full = (uint32_t)(span >> 4);
+    for (uint32_t c = tid; c < full; c += NT) __builtin_nontemporal_store(src4[c], dst4 + c);
+    const uint32_t tail = (uint32_t)(span & 15);
+    if (tid < tail) out[w0 + 16ull * full + tid] = img[16u * full + tid];
 }
 
 }  // namespace
@@ -1092,11 +1255,6 @@ static uint32_t resident_grid(K kernel, int block, bool margin = true) {
 }
 
 static uint64_t scan_tiles(uint64_t n) { return (n + SCAN_TILE - 1) / SCAN_TILE; }
-
-extern "C" uint64_t rr_encode_scratch_words(uint64_t n) {
-    uint64_t t = (n + TILE - 1) / TILE;
-    return RR_SCRATCH_HDR + 4 * t + t / 64 + 2;
-}
 
 // windows: sized from data_cap (>= offsets[n], host-known without a sync); windows past
 // offsets[n] own no values and copy nothing
@@ -1136,28 +1294,40 @@ extern "C" hipError_t rr_launch_decode(const uint8_t *blob, const uint64_t *offs
     return e;
 }
 
+// Encode scratch (uint64 words): [HDR] [scan: ticket, look-back state + groups]
+// [tile stats, 3 per 256 values, twice] [first value per output window u32, nwin+1].
+constexpr uint32_t ENC_W = 16384, ENC_NT = 256, ENC_JCAP = 1024;
+static uint64_t enc_windows(uint64_t data_cap) { return data_cap / ENC_W + 1; }
+
+extern "C" uint64_t rr_encode_scratch_words(uint64_t n, uint64_t data_cap) {
+    const uint64_t st = scan_tiles(n), t = (n + 255) / 256, nw = enc_windows(data_cap);
+    return RR_SCRATCH_HDR + 1 + st + (st + LB_GROUP - 1) / LB_GROUP + 6 * t + (nw + 2) / 2 + 2;
+}
+
 extern "C" hipError_t rr_launch_encode(const rr_value *values, const rr_elem *elems, const uint8_t *arena,
                                        uint64_t n, uint8_t *out, uint64_t cap, uint64_t *offsets, uint64_t *scratch,
                                        rr_totals *totals, hipStream_t stream) {
-    const uint32_t ntiles = (uint32_t)((n + TILE - 1) / TILE);
-    uint64_t *state = scratch + RR_SCRATCH_HDR;
-    const uint64_t ngroups = (ntiles + LB_GROUP - 1) / LB_GROUP;
-    uint64_t *stats = state + ntiles + ngroups;
-    size_t zero = (RR_SCRATCH_HDR + (size_t)ntiles + ngroups) * sizeof(uint64_t);
-    hipError_t e = hipMemsetAsync(scratch, 0, (zero + 15) & ~(size_t)15, stream);
-    if (e != hipSuccess) return e;
-    if (ntiles == 0) {
+    hipError_t e;
+    if (n == 0) {
         e = hipMemsetAsync(offsets, 0, sizeof(uint64_t), stream);
         if (e == hipSuccess && totals) e = hipMemsetAsync(totals, 0, sizeof(rr_totals), stream);
         return e;
     }
-    static uint32_t grid = 0;
-    if (!grid) grid = resident_grid(encode_kernel, WG);
-    const uint32_t need = (ntiles + WG / RR_WAVE - 1) / (WG / RR_WAVE);
-    const uint32_t g = need < grid ? need : grid;
-    hipLaunchKernelGGL(encode_kernel, dim3(g), dim3(WG), 0, stream, values, elems, arena, n, out, cap, offsets,
-                       scratch, ntiles);
+    const uint32_t st = (uint32_t)scan_tiles(n), t = (uint32_t)((n + 255) / 256);
+    const uint64_t nw = enc_windows(cap);
+    uint64_t *lb = scratch + RR_SCRATCH_HDR;
+    const uint64_t lb_words = 1 + st + (st + LB_GROUP - 1) / LB_GROUP;
+    uint64_t *stats = lb + lb_words;
+    uint32_t *fv = reinterpret_cast<uint32_t *>(stats + 6 * (uint64_t)t);
+    e = hipMemsetAsync(lb, 0, ((lb_words * 8) + 15) & ~(size_t)15, stream);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(enc_size_kernel, dim3(t), dim3(256), 0, stream, values, elems, n, offsets, stats);
+    hipLaunchKernelGGL(scan_kernel, dim3(st), dim3(256), 0, stream, offsets, n, lb, st);
+    hipLaunchKernelGGL(enc_index_kernel<ENC_W>, dim3(t), dim3(256), 0, stream, values, elems, n, offsets, cap, fv,
+                       nw, stats + 3 * (uint64_t)t);
+    hipLaunchKernelGGL((enc_emit_kernel<ENC_W, ENC_NT, ENC_JCAP>), dim3((uint32_t)nw), dim3(ENC_NT), 0, stream,
+                       values, elems, arena, n, out, cap, offsets, fv);
     e = hipGetLastError();
-    if (e == hipSuccess && totals) e = launch_finalize(stats, state, ntiles, offsets, n, 1, totals, stream);
+    if (e == hipSuccess && totals) e = launch_finalize(stats, lb, 2 * t, offsets, n, 0, totals, stream);
     return e;
 }
