@@ -42,6 +42,7 @@ def parse():
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-check", action="store_true")
     p.add_argument("--profile-only", action="store_true", help="decode steps only (for rocprofv3)")
+    p.add_argument("--profile-encode", action="store_true", help="one decode, then encode steps only (for rocprofv3)")
     return p.parse_args()
 
 
@@ -117,6 +118,10 @@ def main():
 
     if args.profile_only:
         timed(decode, args.steps, args.warmup)
+        return
+    if args.profile_encode:
+        decode()
+        timed(encode, args.steps, args.warmup)
         return
 
     wall_dec, ev_dec = timed(decode, args.steps, args.warmup)

@@ -822,12 +822,50 @@ __device__ __forceinline__ ElemV get_elem(const rr_elem *e) {
     return ElemV{(uint64_t)w.x | ((uint64_t)w.y << 32), w.z, w.w & 0xFF};
 }
 
+// Decimal digits of an unsigned magnitude (sdsll2str's length without the sign): compares,
+// no divisions.
+__device__ __forceinline__ uint32_t udigits(uint64_t v) {
+    uint32_t l = 1;
+    uint64_t p = 10;
+#pragma unroll
+    for (int k = 1; k < 20; ++k) {
+        l += v >= p ? 1u : 0u;
+        p = k < 19 ? p * 10 : p;
+    }
+    return l;
+}
+// Length of sdsll2str(x) (sds.c:450-479).
+__device__ __forceinline__ uint32_t sdec_len(int64_t x) {
+    return x < 0 ? 1u + udigits(0ull - (uint64_t)x) : udigits((uint64_t)x);
+}
+
+// Per-descriptor contribution to a value's blob bytes and payload, and whether the
+// descriptor kind is legal for the value type (see enc_emit_kernel's layout table).
+struct ElemCost {
+    uint64_t bytes, pay;
+    bool bad;
+};
+__device__ __forceinline__ ElemCost elem_cost(uint32_t type, uint32_t enc, uint64_t i, const ElemV &e) {
+    switch (type) {
+        case RR_TYPE_LIST_QUICKLIST:
+            if (e.kind == RR_K_INT) return {4 + (uint64_t)sdec_len((int64_t)e.data), 0, false};
+            return {4 + (uint64_t)e.len, e.len, e.kind != RR_K_STR};
+        case RR_TYPE_SET_INTSET:
+            return {enc, 0, e.kind != RR_K_INT || !fits_width((int64_t)e.data, enc)};
+        case RR_TYPE_ZSET_SKIPLIST:
+            if (i & 1) return {8, 0, e.kind != RR_K_SCORE};
+            return {8 + (uint64_t)e.len, e.len, e.kind != RR_K_STR};
+        default:   // SET_HT / HASH_HT members
+            return {8 + (uint64_t)e.len, e.len, e.kind != RR_K_STR};
+    }
+}
+
 // serObject rock_serdes.c:512-535: blob size of one flat value, 0 + status if unencodable.
+// Descriptors are read four at a time (independent 16-byte loads in flight per lane).
 __device__ uint64_t encode_size(uint32_t type, uint32_t enc, uint64_t n, const rr_elem *el, uint32_t &st,
                                 uint64_t &pay) {
     st = RR_OK;
     pay = 0;
-    uint64_t s = 5;
     switch (type) {
         case RR_TYPE_STRING: {
             if (n != 1) break;
@@ -840,35 +878,6 @@ __device__ uint64_t encode_size(uint32_t type, uint32_t enc, uint64_t n, const r
             pay = e.len;
             return 6 + (uint64_t)e.len;
         }
-        case RR_TYPE_LIST_QUICKLIST: {
-            for (uint64_t i = 0; i < n; ++i) {
-                ElemV e = get_elem(el + i);
-                if (e.kind == RR_K_INT) s += 4 + dec_len((int64_t)e.data);
-                else if (e.kind == RR_K_STR) { s += 4 + (uint64_t)e.len; pay += e.len; }
-                else { st = RR_E_ENCODE; return 0; }
-            }
-            return s;
-        }
-        case RR_TYPE_SET_INTSET: {
-            if (enc != 2 && enc != 4 && enc != 8) break;
-            for (uint64_t i = 0; i < n; ++i) {
-                ElemV e = get_elem(el + i);
-                if (e.kind != RR_K_INT || !fits_width((int64_t)e.data, enc)) { st = RR_E_ENCODE; return 0; }
-            }
-            return 13 + (uint64_t)enc * n;
-        }
-        case RR_TYPE_SET_HT:
-        case RR_TYPE_HASH_HT: {
-            if (type == RR_TYPE_HASH_HT && (n & 1)) break;
-            s += 8;
-            for (uint64_t i = 0; i < n; ++i) {
-                ElemV e = get_elem(el + i);
-                if (e.kind != RR_K_STR) { st = RR_E_ENCODE; return 0; }
-                s += 8 + (uint64_t)e.len;
-                pay += e.len;
-            }
-            return s;
-        }
         case RR_TYPE_HASH_ZIPLIST:
         case RR_TYPE_ZSET_ZIPLIST: {
             if (n < 1) break;
@@ -877,16 +886,33 @@ __device__ uint64_t encode_size(uint32_t type, uint32_t enc, uint64_t n, const r
             pay = e.len;
             return 13 + (uint64_t)e.len;
         }
+        case RR_TYPE_SET_INTSET:
+            if (enc != 2 && enc != 4 && enc != 8) break;
+            [[fallthrough]];
+        case RR_TYPE_LIST_QUICKLIST:
+        case RR_TYPE_SET_HT:
+        case RR_TYPE_HASH_HT:
         case RR_TYPE_ZSET_SKIPLIST: {
-            if (n & 1) break;
-            s += 8;
-            for (uint64_t i = 0; i < n; i += 2) {
-                ElemV a = get_elem(el + i), b = get_elem(el + i + 1);
-                if (a.kind != RR_K_STR || b.kind != RR_K_SCORE) { st = RR_E_ENCODE; return 0; }
-                s += 16 + (uint64_t)a.len;
-                pay += a.len;
+            if ((type == RR_TYPE_HASH_HT || type == RR_TYPE_ZSET_SKIPLIST) && (n & 1)) break;
+            uint64_t sz = type == RR_TYPE_LIST_QUICKLIST ? 5 : 13, p = 0;
+            bool bad = false;
+            for (uint64_t i = 0; i < n; i += 4) {
+                ElemV e[4];
+#pragma unroll
+                for (uint32_t k = 0; k < 4; ++k) e[k] = i + k < n ? get_elem(el + i + k) : ElemV{0, 0, RR_K_INT};
+#pragma unroll
+                for (uint32_t k = 0; k < 4; ++k) {
+                    if (i + k < n) {
+                        const ElemCost c = elem_cost(type, enc, i + k, e[k]);
+                        sz += c.bytes;
+                        p += c.pay;
+                        bad |= c.bad;
+                    }
+                }
             }
-            return s;
+            if (bad) { st = RR_E_ENCODE; return 0; }
+            pay = p;
+            return sz;
         }
         default:
             break;
@@ -980,6 +1006,28 @@ __global__ __launch_bounds__(256) void enc_index_kernel(const rr_value *__restri
     }
 }
 
+#ifdef RR_PROBE
+// Encode probe (tools/probe_encode.py): per window {init, headers, tasks, copy, store, total,
+// values, tasks, pieces} in s_memrealtime ticks (100 MHz); diagnostics only.
+constexpr uint32_t EPROBE_WORDS = 13;
+__device__ uint64_t *g_eprobe;
+extern "C" int rr_eprobe_set(void *p) { return hipMemcpyToSymbol(HIP_SYMBOL(g_eprobe), &p, sizeof(p)) == hipSuccess ? 0 : -1; }
+__device__ __forceinline__ uint64_t rr_stamp() {
+    uint64_t t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#define EPROBE(...) __VA_ARGS__
+#else
+#define EPROBE(...)
+#endif
+
+#ifndef RR_ENC_TPF
+#define RR_ENC_TPF 1
+#endif
+
 // ---- E4: window emission -------------------------------------------------------------------
 // Blob layout per type (serObject rock_serdes.c:512-535): a value is a header of h bytes then
 // one "task" per descriptor, each task writing es bytes:
@@ -994,19 +1042,23 @@ __device__ __forceinline__ uint32_t enc_hdr(uint32_t type) {
                                           type == RR_TYPE_ZSET_ZIPLIST) ? 5u : 13u;
 }
 
-// Decimal digits of an unsigned magnitude (sdsll2str's length without the sign).
-__device__ __forceinline__ uint32_t udigits(uint64_t v) {
-    uint32_t l = 1;
-    uint64_t p = 10;
-#pragma unroll
-    for (int k = 1; k < 20; ++k) {
-        l += v >= p ? 1u : 0u;
-        p = k < 19 ? p * 10 : p;
-    }
-    return l;
+// The window image: byte writes at absolute output positions, clipped to [w0, w0 + span).
+// Naturally aligned LDS stores only: a misaligned ds_write costs ~7 aligned ones on gfx950
+// (tools/micro/lds_align.hip: misaligned b32/b64/b128 all ~0.45 ms vs 0.06-0.10 ms aligned).
+// lds_put writes the low nb (<= 8) bytes of v at image offset d: ascending alignment steps
+// (1, 2, 4), then descending sizes (8, 4, 2, 1); every store lands on its natural alignment.
+__device__ __forceinline__ void lds_put(uint8_t *img, uint32_t d, uint64_t v, uint32_t nb) {
+    uint32_t r = nb;
+    if ((d & 1) && r >= 1) { img[d] = (uint8_t)v; v >>= 8; d += 1; r -= 1; }
+    if ((d & 2) && r >= 2) { *reinterpret_cast<uint16_t *>(img + d) = (uint16_t)v; v >>= 16; d += 2; r -= 2; }
+    if ((d & 4) && r >= 4) { *reinterpret_cast<uint32_t *>(img + d) = (uint32_t)v; v >>= 32; d += 4; r -= 4; }
+    if (r & 8) { *reinterpret_cast<uint64_t *>(img + d) = v; return; }
+    if (r & 4) { *reinterpret_cast<uint32_t *>(img + d) = (uint32_t)v; v >>= 32; d += 4; }
+    if (r & 2) { *reinterpret_cast<uint16_t *>(img + d) = (uint16_t)v; v >>= 16; d += 2; }
+    if (r & 1) img[d] = (uint8_t)v;
 }
 
-// The window image: byte writes at absolute output positions, clipped to [w0, w0 + span).
+// The window image: writes at absolute output positions, clipped to [w0, w0 + span).
 struct Img {
     uint8_t *img;
     uint64_t w0;
@@ -1015,42 +1067,93 @@ struct Img {
         const uint64_t d = pos - w0;
         if (d < span) img[d] = (uint8_t)b;
     }
-    // little-endian field of nb bytes
+    // little-endian field of nb (<= 8) bytes
     __device__ __forceinline__ void field(uint64_t pos, uint64_t v, uint32_t nb) const {
         const uint64_t d = pos - w0;
-        if (d < span && d + nb <= span) {
-            if (nb == 8) __builtin_memcpy(img + d, &v, 8);
-            else if (nb == 4) { const uint32_t x = (uint32_t)v; __builtin_memcpy(img + d, &x, 4); }
-            else if (nb == 2) { const uint16_t x = (uint16_t)v; __builtin_memcpy(img + d, &x, 2); }
-            else img[d] = (uint8_t)v;
-        } else {
+        if (d < span && d + nb <= span) lds_put(img, (uint32_t)d, v, nb);
+        else
             for (uint32_t i = 0; i < nb; ++i) put(pos + i, (uint32_t)(v >> (8 * i)) & 0xFF);
-        }
     }
-    // sdsll2str(x) (sds.c:450-479) of l characters at pos
+    // sdsll2str(x) (sds.c:450-479), l characters at pos: the characters are shifted into a
+    // 24-byte register string (last digit first, so the first character ends in byte 0),
+    // then stored as up to three fields
     __device__ __forceinline__ void decimal(uint64_t pos, int64_t x, uint32_t l) const {
         uint64_t u = x < 0 ? 0ull - (uint64_t)x : (uint64_t)x;
-        uint64_t p = pos + l;
-        if (x < 0) put(pos, '-');
-        while (u >= (1ull << 32)) { put(--p, '0' + (uint32_t)(u % 10)); u /= 10; }
-        uint32_t s = (uint32_t)u;
-        do { put(--p, '0' + s % 10); s /= 10; } while (s);
+        uint64_t a0 = 0, a1 = 0, a2 = 0;
+        auto push = [&](uint32_t c) {
+            a2 = (a2 << 8) | (a1 >> 56);
+            a1 = (a1 << 8) | (a0 >> 56);
+            a0 = (a0 << 8) | c;
+        };
+        // base-1e9 chunks, then 32-bit digit steps
+        const uint64_t t = u / 1000000000ull;
+        uint32_t c[3] = {(uint32_t)(u - t * 1000000000ull), (uint32_t)(t % 1000000000ull), (uint32_t)(t / 1000000000ull)};
+        const uint32_t nd = l - (x < 0 ? 1u : 0u);
+        uint32_t cur = c[0];
+        for (uint32_t k = 0; k < nd; ++k) {
+            if (k == 9) cur = c[1];
+            if (k == 18) cur = c[2];
+            push('0' + cur % 10);
+            cur /= 10;
+        }
+        if (x < 0) push('-');
+        for (uint32_t w = 0; 8 * w < l; ++w)
+            field(pos + 8 * w, w == 0 ? a0 : w == 1 ? a1 : a2, l - 8 * w < 8 ? l - 8 * w : 8);
     }
 };
 
-// 64-byte copy piece: arena bytes [src, src+len) -> image bytes [dst, dst+len), len <= 64.
-// Unaligned 16-byte global loads and LDS stores (gfx950 allows both), exact byte extent.
-__device__ __forceinline__ void copy_piece(uint8_t *img, uint32_t dst, const uint8_t *__restrict__ src, uint32_t len) {
-    uint4 x[4];
-    const uint32_t full = len >> 4;
-#pragma unroll
-    for (uint32_t k = 0; k < 4; ++k)
-        if (k < full) __builtin_memcpy(&x[k], src + 16 * k, 16);
-#pragma unroll
-    for (uint32_t k = 0; k < 4; ++k)
-        if (k < full) __builtin_memcpy(img + dst + 16 * k, &x[k], 16);
-    for (uint32_t i = full << 4; i < len; ++i) img[dst + i] = src[i];
-}
+// Copy piece: arena bytes [src, src+len) -> image bytes [d, d+len), the piece inside one
+// 64-byte aligned image block.  Destination-aligned plan: ascending head steps (1, 2, 4, 8)
+// to a 16-byte boundary, up to four 16-byte chunks, descending tail (8, 4, 2, 1).  Source
+// loads are unaligned (allowed for global memory) and all issued before the stores.  Macros
+// over plain locals: the same code on struct members went through scratch memory.
+#define RR_PIECE_LOAD(P, SRC, DST, LEN)                                                          \
+    uint4 P##m0, P##m1, P##m2, P##m3;                                                            \
+    uint64_t P##h8 = 0, P##t8 = 0;                                                               \
+    uint32_t P##h4 = 0, P##t4 = 0, P##h2 = 0, P##t2 = 0, P##h1 = 0, P##t1 = 0;                   \
+    {                                                                                            \
+        uint32_t p_ = (DST), r_ = (LEN);                                                         \
+        const uint8_t *q_ = (SRC);                                                               \
+        if ((p_ & 1) && r_ >= 1) { P##h1 = q_[0]; p_ += 1; r_ -= 1; q_ += 1; }                   \
+        if ((p_ & 2) && r_ >= 2) { uint16_t x_; __builtin_memcpy(&x_, q_, 2); P##h2 = x_; p_ += 2; r_ -= 2; q_ += 2; } \
+        if ((p_ & 4) && r_ >= 4) { __builtin_memcpy(&P##h4, q_, 4); p_ += 4; r_ -= 4; q_ += 4; } \
+        if ((p_ & 8) && r_ >= 8) { __builtin_memcpy(&P##h8, q_, 8); p_ += 8; r_ -= 8; q_ += 8; } \
+        const uint32_t nm_ = r_ >> 4;                                                            \
+        if (nm_ > 0) __builtin_memcpy(&P##m0, q_, 16);                                           \
+        if (nm_ > 1) __builtin_memcpy(&P##m1, q_ + 16, 16);                                      \
+        if (nm_ > 2) __builtin_memcpy(&P##m2, q_ + 32, 16);                                      \
+        if (nm_ > 3) __builtin_memcpy(&P##m3, q_ + 48, 16);                                      \
+        q_ += 16 * nm_;                                                                          \
+        r_ &= 15;                                                                                \
+        if (r_ & 8) { __builtin_memcpy(&P##t8, q_, 8); q_ += 8; }                                \
+        if (r_ & 4) { __builtin_memcpy(&P##t4, q_, 4); q_ += 4; }                                \
+        if (r_ & 2) { uint16_t x_; __builtin_memcpy(&x_, q_, 2); P##t2 = x_; q_ += 2; }          \
+        if (r_ & 1) P##t1 = q_[0];                                                               \
+    }
+#define RR_PIECE_STORE(P, IMG, DST, LEN)                                                         \
+    {                                                                                            \
+        uint8_t *i_ = (IMG);                                                                     \
+        uint32_t p_ = (DST), r_ = (LEN);                                                         \
+        if ((p_ & 1) && r_ >= 1) { i_[p_] = (uint8_t)P##h1; p_ += 1; r_ -= 1; }                  \
+        if ((p_ & 2) && r_ >= 2) { *reinterpret_cast<uint16_t *>(i_ + p_) = (uint16_t)P##h2; p_ += 2; r_ -= 2; } \
+        if ((p_ & 4) && r_ >= 4) { *reinterpret_cast<uint32_t *>(i_ + p_) = P##h4; p_ += 4; r_ -= 4; } \
+        if ((p_ & 8) && r_ >= 8) { *reinterpret_cast<uint64_t *>(i_ + p_) = P##h8; p_ += 8; r_ -= 8; } \
+        const uint32_t nm_ = r_ >> 4;                                                            \
+        uint4 *m_ = reinterpret_cast<uint4 *>(i_ + p_);                                          \
+        if (nm_ > 0) m_[0] = P##m0;                                                              \
+        if (nm_ > 1) m_[1] = P##m1;                                                              \
+        if (nm_ > 2) m_[2] = P##m2;                                                              \
+        if (nm_ > 3) m_[3] = P##m3;                                                              \
+        p_ += 16 * nm_;                                                                          \
+        r_ &= 15;                                                                                \
+        if (r_ & 8) { *reinterpret_cast<uint64_t *>(i_ + p_) = P##t8; p_ += 8; }                 \
+        if (r_ & 4) { *reinterpret_cast<uint32_t *>(i_ + p_) = P##t4; p_ += 4; }                 \
+        if (r_ & 2) { *reinterpret_cast<uint16_t *>(i_ + p_) = (uint16_t)P##t2; p_ += 2; }       \
+        if (r_ & 1) i_[p_] = (uint8_t)P##t1;                                                     \
+    }
+
+// Copy-queue entry: arena offset (40 bits) | image offset << 40 (16 bits) | (len - 1) << 56.
+constexpr uint64_t JQ_SRC = (1ull << 40) - 1;
 
 template <uint32_t NT>
 __device__ __forceinline__ uint64_t block_excl_scan(uint64_t x, uint64_t *wsum, uint64_t &total) {
@@ -1076,10 +1179,9 @@ __global__ __launch_bounds__(NT) void enc_emit_kernel(const rr_value *__restrict
                                                       uint8_t *__restrict__ out, uint64_t cap,
                                                       const uint64_t *__restrict__ offsets,
                                                       const uint32_t *__restrict__ fv) {
+    static_assert(W <= 65536 && W % 64 == 0, "image offsets are 16-bit, pieces 64-byte blocks");
     __shared__ uint4 img4[W / 16];
-    __shared__ uint64_t j_src[JCAP];
-    __shared__ uint16_t j_dst[JCAP];
-    __shared__ uint8_t j_len[JCAP];
+    __shared__ uint64_t jq[JCAP];
     __shared__ uint32_t tb[NT + 1];        // task base of each value of the round
     __shared__ uint64_t sv_pos[NT];        // output position of the value's first task
     __shared__ uint64_t sv_eb[NT];         // element-byte scan at the value's first task
@@ -1093,6 +1195,7 @@ __global__ __launch_bounds__(NT) void enc_emit_kernel(const rr_value *__restrict
     const uint64_t lim = total < cap ? total : cap;
     const uint64_t w0 = (uint64_t)blockIdx.x * W;
     if (w0 >= lim) return;
+    EPROBE(uint64_t et0 = rr_stamp(), etk = 0, ent = 0, tf = 0, tsc = 0, twr = 0, tw1 = 0, tw2 = 0;)
     const uint64_t span = lim - w0 < W ? lim - w0 : W;
     const Img I{img, w0, span};
 #pragma unroll
@@ -1101,24 +1204,37 @@ __global__ __launch_bounds__(NT) void enc_emit_kernel(const rr_value *__restrict
     const uint64_t v0 = fv[blockIdx.x];
     const uint64_t vend = w0 + W < total ? (uint64_t)fv[blockIdx.x + 1] + 1 : n;
     lds_barrier();
+    EPROBE(const uint64_t et1 = rr_stamp();)
 
-    auto payload = [&](uint64_t pos, uint64_t src, uint64_t len) {
-        // clip to the window, then 64-byte pieces into the queue (inline when it is full)
+    // Payload bytes [pos, pos+len) <- arena[src..]: clipped to the window, split into the
+    // 64-byte aligned image blocks it touches, queued for the copy phase.  Called by every
+    // lane of the wave (want = false for none): queue slots are reserved with one LDS atomic
+    // per wave over a wave prefix sum.
+    auto payload = [&](bool want, uint64_t pos, uint64_t src, uint64_t len) {
         uint64_t d0 = pos < w0 ? w0 : pos, d1 = pos + len;
         if (d1 > w0 + span) d1 = w0 + span;
-        if (d0 >= d1) return;
-        src += d0 - pos;
-        const uint32_t dst = (uint32_t)(d0 - w0), l = (uint32_t)(d1 - d0);
-        const uint32_t np = (l + 63) >> 6;
-        const uint32_t j = atomicAdd(&sh_nj, np);
-        for (uint32_t k = 0; k < np; ++k) {
-            const uint32_t pl = k + 1 < np ? 64u : l - 64u * k;
-            if (j + k < JCAP) {
-                j_src[j + k] = src + 64u * k;
-                j_dst[j + k] = (uint16_t)(dst + 64u * k);
-                j_len[j + k] = (uint8_t)pl;
-            } else
-                copy_piece(img, dst + 64u * k, arena + src + 64u * k, pl);
+        want = want && d0 < d1;
+        src += want ? d0 - pos : 0;
+        const uint32_t dst = want ? (uint32_t)(d0 - w0) : 0, l = want ? (uint32_t)(d1 - d0) : 0;
+        const bool queued = want && src + l <= JQ_SRC;
+        const uint32_t np = queued ? ((dst + l - 1) >> 6) - (dst >> 6) + 1 : 0;
+        const uint32_t incl = (uint32_t)wave_incl_scan(np);
+        const uint32_t wtot = __shfl(incl, RR_WAVE - 1, RR_WAVE);
+        uint32_t base = 0;
+        if (wtot && lane_id() == RR_WAVE - 1) base = atomicAdd(&sh_nj, wtot);
+        base = __shfl(base, RR_WAVE - 1, RR_WAVE);
+        if (!want) return;
+        const uint32_t j = queued ? base + incl - np : JCAP;
+        const uint32_t npc = queued ? np : 1;
+        uint32_t pd = dst;
+        for (uint32_t k = 0; k < npc; ++k) {
+            const uint32_t pe = k + 1 < npc ? (pd | 63u) + 1 : dst + l;
+            const uint64_t ps = src + (pd - dst);
+            if (j + k < JCAP)
+                jq[j + k] = ps | ((uint64_t)pd << 40) | ((uint64_t)(pe - pd - 1) << 56);
+            else   // queue full: byte copy (rare; keeps the kernel small)
+                for (uint32_t i = pd; i < pe; ++i) img[i] = arena[ps + (i - pd)];
+            pd = pe;
         }
     };
 
@@ -1127,15 +1243,19 @@ __global__ __launch_bounds__(NT) void enc_emit_kernel(const rr_value *__restrict
         uint32_t tasks = 0;
         if (v < vend) {
             const uint64_t a = offsets[v], b = offsets[v + 1];
+            const uint4 x = reinterpret_cast<const uint4 *>(values)[v];
             if (b > a && b <= cap) {
-                const uint4 x = reinterpret_cast<const uint4 *>(values)[v];
                 const uint32_t type = x.x & 0xFF, enc = (x.x >> 8) & 0xFF, ne = x.z;
-                I.put(a, type);
-                I.field(a + 1, x.y & RR_LRU_MASK, 4);
-                if (type == RR_TYPE_STRING) I.put(a + 5, enc);
-                else if (type == RR_TYPE_SET_INTSET) { I.field(a + 5, enc, 4); I.field(a + 9, ne, 4); }
-                else if (type == RR_TYPE_SET_HT) I.field(a + 5, ne, 8);
-                else if (type == RR_TYPE_HASH_HT || type == RR_TYPE_ZSET_SKIPLIST) I.field(a + 5, ne / 2, 8);
+                // type, lru (5 bytes) then the type's fixed field: STRING enc (1), INTSET enc +
+                // count (8), HT / skiplist count (8)
+                const uint32_t fnb = type == RR_TYPE_STRING ? 1u : (type == RR_TYPE_SET_INTSET || type == RR_TYPE_SET_HT ||
+                                                                    type == RR_TYPE_HASH_HT || type == RR_TYPE_ZSET_SKIPLIST) ? 8u : 0u;
+                const uint64_t fv8 = type == RR_TYPE_STRING ? enc : type == RR_TYPE_SET_INTSET ? (enc | ((uint64_t)ne << 32))
+                                   : type == RR_TYPE_SET_HT ? ne : (uint64_t)(ne / 2);
+                for (uint32_t f = 0; f < 2; ++f) {
+                    const uint32_t nb = f == 0 ? 5u : fnb;
+                    if (nb) I.field(a + 5 * f, f == 0 ? (type | ((uint64_t)(x.y & RR_LRU_MASK) << 8)) : fv8, nb);
+                }
                 tasks = (type == RR_TYPE_HASH_ZIPLIST || type == RR_TYPE_ZSET_ZIPLIST) ? 1u : ne;
                 sv_pos[tid] = a + enc_hdr(type);
                 sv_el[tid] = x.w;
@@ -1147,31 +1267,37 @@ __global__ __launch_bounds__(NT) void enc_emit_kernel(const rr_value *__restrict
         tb[tid] = base;
         if (tid == NT - 1) tb[NT] = base + tasks;
         lds_barrier();
+        EPROBE(const uint64_t eth = rr_stamp(); ent += tt;)
         uint64_t run = 0;   // element bytes of the earlier task rounds
-        for (uint64_t r0 = 0; r0 < tt; r0 += NT) {
-            const uint64_t t = r0 + tid;
-            const bool act = t < tt;
-            uint32_t j = 0;
-            uint64_t es = 0;
-            ElemV e{0, 0, 0};
-            uint32_t type = 0, enc = 0, k = 0;
-            if (act) {
+        // task rounds in groups of TPF: every round's descriptor is loaded up front, so a
+        // group costs one memory round trip
+        auto fetch = [&](uint64_t t, uint32_t &pj, ElemV &pe) {
+            pj = 0;
+            pe = ElemV{0, 0, 0};
+            if (t < tt) {
                 // last value j with tb[j] <= t
                 uint32_t lo = 0;
 #pragma unroll
                 for (uint32_t s = NT / 2; s > 0; s >>= 1)
                     if (tb[lo + s] <= t) lo += s;
-                j = lo;
+                pj = lo;
+                pe = get_elem(elems + sv_el[lo] + (uint32_t)(t - tb[lo]));
+            }
+        };
+        auto round = [&](uint64_t r0, const uint32_t j, const ElemV &e) {
+            EPROBE(const uint64_t rs0 = rr_stamp();)
+            const uint64_t t = r0 + tid;
+            const bool act = t < tt;
+            uint64_t es = 0;
+            uint32_t type = 0, enc = 0, k = 0;
+            if (act) {
                 k = (uint32_t)(t - tb[j]);
                 type = sv_te[j] & 0xFF;
                 enc = sv_te[j] >> 8;
-                e = get_elem(elems + sv_el[j] + k);
                 switch (type) {
                     case RR_TYPE_STRING: es = enc == RR_ENC_INT ? 8 : e.len; break;
                     case RR_TYPE_LIST_QUICKLIST:
-                        es = 4 + (e.kind == RR_K_INT ? udigits((int64_t)e.data < 0 ? 0ull - e.data : e.data) +
-                                                           ((int64_t)e.data < 0 ? 1u : 0u)
-                                                     : e.len);
+                        es = 4 + (e.kind == RR_K_INT ? sdec_len((int64_t)e.data) : e.len);
                         break;
                     case RR_TYPE_SET_INTSET: es = enc; break;
                     case RR_TYPE_ZSET_SKIPLIST: es = (k & 1) ? 8 : 8 + (uint64_t)e.len; break;
@@ -1182,37 +1308,73 @@ __global__ __launch_bounds__(NT) void enc_emit_kernel(const rr_value *__restrict
             const uint64_t ex = run + block_excl_scan<NT>(es, wsum[1], rt);
             if (act && k == 0) sv_eb[j] = ex;
             lds_barrier();
+            EPROBE(const uint64_t rs1 = rr_stamp(); tsc += rs1 - rs0;)
+            bool pay = false;
+            uint64_t ppos = 0;
             if (act) {
                 const uint64_t p = sv_pos[j] + ex - sv_eb[j];
-                switch (type) {
-                    case RR_TYPE_STRING:
-                        if (enc == RR_ENC_INT) I.field(p, e.data, 8);
-                        else payload(p, e.data, e.len);
-                        break;
-                    case RR_TYPE_LIST_QUICKLIST:
-                        I.field(p, es - 4, 4);
-                        if (e.kind == RR_K_INT) I.decimal(p + 4, (int64_t)e.data, (uint32_t)(es - 4));
-                        else payload(p + 4, e.data, e.len);
-                        break;
-                    case RR_TYPE_SET_INTSET: I.field(p, e.data, enc); break;
-                    case RR_TYPE_ZSET_SKIPLIST:
-                        if (k & 1) { I.field(p, e.data, 8); break; }
-                        [[fallthrough]];
-                    default:
-                        I.field(p, e.len, 8);
-                        payload(p + 8, e.data, e.len);
-                        break;
-                }
+                // one fixed field, then a decimal or a payload (single call sites keep the
+                // kernel small enough for the instruction cache)
+                uint64_t fval = e.len;
+                uint32_t fnb = 8, hdr = 8;
+                pay = true;
+                if (type == RR_TYPE_STRING) { fnb = 0; hdr = 0; if (enc == RR_ENC_INT) { fval = e.data; fnb = 8; pay = false; } }
+                else if (type == RR_TYPE_LIST_QUICKLIST) { fval = es - 4; fnb = 4; hdr = 4; pay = e.kind != RR_K_INT; }
+                else if (type == RR_TYPE_SET_INTSET) { fval = e.data; fnb = enc; pay = false; }
+                else if (type == RR_TYPE_ZSET_SKIPLIST && (k & 1)) { fval = e.data; pay = false; }
+                if (fnb) I.field(p, fval, fnb);
+                EPROBE(asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); const uint64_t rw1 = rr_stamp(); tw1 += rw1 - rs1;)
+                if (type == RR_TYPE_LIST_QUICKLIST && !pay) I.decimal(p + 4, (int64_t)e.data, (uint32_t)(es - 4));
+                EPROBE(asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); const uint64_t rw2 = rr_stamp(); tw2 += rw2 - rw1;)
+                ppos = p + hdr;
             }
+            payload(pay, ppos, e.data, e.len);
             run += rt;
+            EPROBE(asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); const uint64_t rs2 = rr_stamp(); twr += rs2 - rs1;)
+        };
+        // task rounds in groups of four: the group's descriptors are loaded up front, so a
+        // group costs one memory round trip
+#if RR_ENC_TPF == 1
+        for (uint64_t g0 = 0; g0 < tt; g0 += NT) {
+            uint32_t j0;
+            ElemV e0;
+            fetch(g0 + tid, j0, e0);
+            round(g0, j0, e0);
         }
+#else
+        for (uint64_t g0 = 0; g0 < tt; g0 += 4 * NT) {
+            uint32_t j0, j1, j2, j3;
+            ElemV e0, e1, e2, e3;
+            fetch(g0 + tid, j0, e0);
+            fetch(g0 + NT + tid, j1, e1);
+            fetch(g0 + 2 * NT + tid, j2, e2);
+            fetch(g0 + 3 * NT + tid, j3, e3);
+            EPROBE(asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); tf += rr_stamp() - eth;)
+            round(g0, j0, e0);
+            if (g0 + NT < tt) round(g0 + NT, j1, e1);
+            if (g0 + 2 * NT < tt) round(g0 + 2 * NT, j2, e2);
+            if (g0 + 3 * NT < tt) round(g0 + 3 * NT, j3, e3);
+        }
+#endif
         lds_barrier();
+        EPROBE(const uint64_t ett = rr_stamp(); etk += ett - eth;)
     }
+    EPROBE(const uint64_t et2 = rr_stamp();)
 
     // payload pieces
     const uint32_t nj = sh_nj < JCAP ? sh_nj : JCAP;
-    for (uint32_t j = tid; j < nj; j += NT) copy_piece(img, j_dst[j], arena + j_src[j], j_len[j]);
+    for (uint32_t j = tid; j < nj; j += 2 * NT) {
+        const bool two = j + NT < nj;
+        const uint64_t q0 = jq[j], q1 = two ? jq[j + NT] : 0;
+        const uint32_t d0 = (uint32_t)(q0 >> 40) & 0xFFFF, l0 = (uint32_t)(q0 >> 56) + 1;
+        const uint32_t d1 = (uint32_t)(q1 >> 40) & 0xFFFF, l1 = two ? (uint32_t)(q1 >> 56) + 1 : 0;
+        RR_PIECE_LOAD(a_, arena + (q0 & JQ_SRC), d0, l0)
+        RR_PIECE_LOAD(b_, arena + (q1 & JQ_SRC), d1, l1)
+        RR_PIECE_STORE(a_, img, d0, l0)
+        RR_PIECE_STORE(b_, img, d1, l1)
+    }
     lds_barrier();
+    EPROBE(const uint64_t et3 = rr_stamp();)
 
     // store the image: 16-byte chunks, bytes at a partial end
     u32x4 *dst4 = reinterpret_cast<u32x4 *>(out + w0);
@@ -1221,6 +1383,13 @@ __global__ __launch_bounds__(NT) void enc_emit_kernel(const rr_value *__restrict
     for (uint32_t c = tid; c < full; c += NT) __builtin_nontemporal_store(src4[c], dst4 + c);
     const uint32_t tail = (uint32_t)(span & 15);
     if (tid < tail) out[w0 + 16ull * full + tid] = img[16u * full + tid];
+    EPROBE(const uint64_t et4 = rr_stamp();
+           if (tid == 0 && g_eprobe) {
+               uint64_t *o = g_eprobe + (uint64_t)blockIdx.x * EPROBE_WORDS;
+               o[0] = et1 - et0; o[1] = (et2 - et1) - etk; o[2] = etk; o[3] = et3 - et2; o[4] = et4 - et3;
+               o[5] = et4 - et0; o[6] = vend - v0; o[7] = ent; o[8] = sh_nj;
+               o[9] = tw1; o[10] = tsc; o[11] = twr; o[12] = tw2;
+           })
 }
 
 }  // namespace
@@ -1296,7 +1465,10 @@ extern "C" hipError_t rr_launch_decode(const uint8_t *blob, const uint64_t *offs
 
 // Encode scratch (uint64 words): [HDR] [scan: ticket, look-back state + groups]
 // [tile stats, 3 per 256 values, twice] [first value per output window u32, nwin+1].
-constexpr uint32_t ENC_W = 16384, ENC_NT = 256, ENC_JCAP = 1024;
+#ifndef RR_ENC_W
+#define RR_ENC_W 16384
+#endif
+constexpr uint32_t ENC_W = RR_ENC_W, ENC_NT = 256, ENC_JCAP = 1024;
 static uint64_t enc_windows(uint64_t data_cap) { return data_cap / ENC_W + 1; }
 
 extern "C" uint64_t rr_encode_scratch_words(uint64_t n, uint64_t data_cap) {
