@@ -1,0 +1,133 @@
+"""GPU encode tests: the window/emit encode pipeline (rr_kernels.hip E1-E5) against the CPU
+oracle's encode (oracle/rr_oracle.c rro_encode, rock_serdes.c:512-535 restated) on flat batches
+the decoder never produces: relocated arenas and permuted descriptor ranges, values far larger
+than one output window, zero-length members, unencodable descriptors and a data_cap that cuts a
+value.  Bit-exact: bytes, offsets and totals."""
+import struct
+
+import numpy as np
+import pytest
+
+import redrock_old_amd as rr
+from oracle import cpu
+
+from helpers import batch_from_blobs
+
+pytestmark = pytest.mark.gpu
+
+
+def _lru(i):
+    return (i * 2654435761) & 0xFFFFFF
+
+
+def s_raw(i, payload):
+    return bytes([rr.T_STRING]) + struct.pack("<I", _lru(i)) + b"\x00" + payload
+
+
+def l_list(i, items):
+    return bytes([rr.T_LIST_QUICKLIST]) + struct.pack("<I", _lru(i)) + b"".join(
+        struct.pack("<I", len(x)) + x for x in items)
+
+
+def s_ht(i, members, t=rr.T_SET_HT):
+    n = len(members) if t == rr.T_SET_HT else len(members) // 2
+    return bytes([t]) + struct.pack("<I", _lru(i)) + struct.pack("<Q", n) + b"".join(
+        struct.pack("<Q", len(x)) + x for x in members)
+
+
+def z_sl(i, pairs):
+    return bytes([rr.T_ZSET_SKIPLIST]) + struct.pack("<I", _lru(i)) + struct.pack("<Q", len(pairs)) + b"".join(
+        struct.pack("<Q", len(m)) + m + struct.pack("<d", s) for m, s in pairs)
+
+
+def _check_against_oracle(engine, v, e, a, data_cap=None):
+    out, ooffs, t = engine.encode_host(v, e, a, data_cap=data_cap)
+    xo, xoffs, xt = cpu.encode(v, e, a, data_cap=data_cap)
+    assert np.array_equal(ooffs, xoffs)
+    assert t == xt
+    n = min(len(out), len(xo))
+    if data_cap is not None:
+        n = min(n, data_cap)
+    assert np.array_equal(out[:n], xo[:n])
+    return out, ooffs, t
+
+
+def test_values_larger_than_a_window(engine):
+    """Values of 40-300 KB span many 16 KiB output windows; each window writes only its slice."""
+    rng = np.random.default_rng(11)
+    blobs = []
+    for i in range(12):
+        k = i % 4
+        if k == 0:
+            blobs.append(s_raw(i, rng.integers(0, 256, 40000 + 9973 * i, dtype=np.uint8).tobytes()))
+        elif k == 1:
+            items = [str(int(x)).encode() if j % 3 == 0 else rng.integers(0, 256, int(rng.integers(0, 90)),
+                                                                          dtype=np.uint8).tobytes()
+                     for j, x in enumerate(rng.integers(-10**18, 10**18, 5000))]
+            blobs.append(l_list(i, items))
+        elif k == 2:
+            blobs.append(s_ht(i, [b""] + [rng.integers(0, 256, int(rng.integers(0, 70)), dtype=np.uint8).tobytes()
+                                          for _ in range(3001)]))
+        else:
+            blobs.append(z_sl(i, [(rng.integers(65, 91, int(rng.integers(1, 40)), dtype=np.uint8).tobytes(),
+                                   float(rng.standard_normal())) for _ in range(2000)]))
+        blobs.append(s_raw(i + 100, b"x" * int(rng.integers(0, 50))))   # small neighbours
+    data, offs = batch_from_blobs(blobs)
+    v, e, a, t = engine.decode_host(data, offs)
+    assert t["n_bad"] == 0
+    out, ooffs, t2 = _check_against_oracle(engine, v, e, a)
+    assert np.array_equal(ooffs, offs)
+    assert np.array_equal(out, data[:int(offs[-1])])
+
+
+def test_relocated_arena_and_permuted_ranges(engine):
+    """Descriptor ranges in shuffled order and payloads moved to odd offsets in a new arena:
+    the encoder must follow elem_base / data, not assume the decoder's layout."""
+    rng = np.random.default_rng(5)
+    data, offs = rr.gen_batch(4, 6000, seed=77)
+    v, e, a, t = engine.decode_host(data, offs)
+    n = len(v)
+    order = rng.permutation(n)
+    e2 = np.zeros_like(e)
+    v2 = v.copy()
+    arena2 = bytearray()
+    pos = 0
+    for i in order:
+        b, c = int(v["elem_base"][i]), int(v["n_elems"][i])
+        seg = e[b:b + c].copy()
+        for k in range(c):
+            if seg["kind"][k] in (rr.K_STR, rr.K_ZLRAW):
+                ln = int(seg["len"][k])
+                arena2 += bytes(int(rng.integers(0, 7)))          # misalign the next payload
+                seg["data"][k] = len(arena2)
+                src = int(e["data"][b + k])
+                arena2 += a[src:src + ln].tobytes()
+        e2[pos:pos + c] = seg
+        v2["elem_base"][i] = pos
+        pos += c
+    a2 = np.frombuffer(bytes(arena2) + bytes(16), np.uint8)
+    out, ooffs, t2 = _check_against_oracle(engine, v2, e2, a2)
+    assert np.array_equal(out, data[:int(offs[-1])])
+
+
+def test_unencodable_descriptors_and_capacity_cut(engine):
+    """Wrong descriptor kinds / intset widths are RR_E_ENCODE (size 0); a data_cap that cuts a
+    value leaves it and every later value unwritten, with the same totals as the oracle."""
+    data, offs = rr.gen_batch(4, 4000, seed=3)
+    v, e, a, t = engine.decode_host(data, offs)
+    rng = np.random.default_rng(9)
+    e = e.copy()
+    for i in rng.choice(len(v), 60, replace=False):
+        c = int(v["n_elems"][i])
+        if c:
+            e["kind"][int(v["elem_base"][i]) + int(rng.integers(0, c))] = rr.K_SCORE
+    for cap in (None, int(offs[2000]) + 7, int(offs[len(v) // 3]), 100):
+        _check_against_oracle(engine, v, e, a, data_cap=cap)
+
+
+@pytest.mark.parametrize("cfg,n", [(1, 300000), (2, 20000), (3, 20000), (11, 400)])
+def test_encode_configs_match_oracle(engine, cfg, n):
+    data, offs = rr.gen_batch(cfg, n)
+    v, e, a, t = engine.decode_host(data, offs)
+    out, ooffs, t2 = _check_against_oracle(engine, v, e, a)
+    assert np.array_equal(out, data[:int(offs[-1])])
