@@ -14,7 +14,8 @@
  *   - return value: RR_API_OK (0) or a negative RR_API_E* code for the whole call;
  *   - per-value status in rr_value.status (0 = OK), counted into rr_totals.n_bad;
  *   - caller-owned buffers; one rr_ctx per host thread; no hidden host synchronisation in the
- *     device entry points (graph-capturable: memset + 1 kernel per call).
+ *     device entry points (graph-capturable: decode = memset + 4 kernels, encode = memset +
+ *     5 kernels, all on the caller's stream).
  * Plain C: no HIP or torch types in any signature.  Streams are passed as void* (hipStream_t).
  */
 #ifndef RR_SERDES_H

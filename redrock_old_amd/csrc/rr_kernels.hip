@@ -1,17 +1,14 @@
 // rr_kernels.hip — CDNA4 (gfx950) decode and encode kernels for RedRock value blobs.
 //
-// Decode (blob batch -> flat batch), one launch, single pass:
-//   a wave owns a TILE of 64 consecutive values (lane = value);
-//   1. the wave streams the tile's contiguous blob bytes into the MIRROR arena with aligned
-//      16-byte loads/stores (every value's payload lands at its blob offset, so no arena scan);
-//   2. each lane parses its value header/chain (count pass: validates exactly like
-//      rock_serdes.c's asserts, counts descriptors);
-//   3. wave scan + decoupled look-back across tiles -> each value's elem_base;
-//   4. each lane re-parses (L2-hot) and writes its descriptors, the wave writes the 16-byte
-//      value records coalesced.
-// Encode (flat batch -> blob batch), one launch, single pass:
-//   lane = value: size pass from the descriptors, wave scan + look-back -> blob offsets,
-//   then headers/length fields by the lane and bulk payloads by the whole wave.
+// Decode (blob batch -> flat batch): memset + count / scan / decode / finalize launches.
+//   count: thread per value, descriptor reservation + walk class; scan: reservations ->
+//   elem_base; decode: workgroup per 64 KiB blob window, streams the window into the MIRROR
+//   arena (every payload lands at its blob offset) and into LDS, sorts the window's values by
+//   class, walks + emits single-class 64-value batches (lane = value).  Details at K1-K4.
+// Encode (flat batch -> blob batch): memset + size / scan / index / emit / finalize launches.
+//   size: thread per value; scan: sizes -> offsets; index: first value of each 16 KiB output
+//   window; emit: workgroup per output window builds the window's bytes in LDS
+//   (element-parallel tasks, aligned stores) and stores it coalesced.  Details at E1-E5.
 //
 // No MFMA: this is byte/record work bounded by HBM.
 #include <hip/hip_runtime.h>
@@ -511,7 +508,12 @@ struct Acc {
     uint64_t pay;
 };
 
-__device__ __forceinline__ Acc exact_value(const uint8_t *__restrict__ blob, uint64_t v,
+#ifdef RR_DEC_NOINL
+#define RR_COLD __noinline__
+#else
+#define RR_COLD __forceinline__
+#endif
+__device__ RR_COLD Acc exact_value(const uint8_t *__restrict__ blob, uint64_t v,
                                            const uint64_t *__restrict__ offsets, const uint64_t *__restrict__ ebase,
                                            rr_value *__restrict__ values, rr_elem *__restrict__ elems, uint64_t cap) {
     uint64_t pay = 0;
@@ -593,6 +595,15 @@ __device__ __forceinline__ Acc run_batch(const Src &src, uint32_t c, bool active
     if (fail) return exact_value(blob, v, offsets, ebase, values, elems, cap);
     put_value(values + v, H.type(), enc, l.ok ? RR_OK : RR_E_CAPACITY, H.lru(), ne, (uint32_t)eb);
     return Acc{l.ok ? 0u : 1u, l.ok ? vp : 0};
+}
+
+// the unstaged (global-memory) instantiation: cold path, kept out of line in RR_DEC_NOINL
+// builds so the hot staged code stays small
+__device__ RR_COLD Acc run_batch_g(const GlbSrc &src, uint32_t c, bool active, uint64_t v, uint64_t B, rsrc_t E,
+                                   uint64_t eb0, const uint8_t *__restrict__ blob,
+                                   const uint64_t *__restrict__ offsets, const uint64_t *__restrict__ ebase,
+                                   rr_value *__restrict__ values, rr_elem *__restrict__ elems, uint64_t cap) {
+    return run_batch(src, c, active, v, B, E, eb0, blob, offsets, ebase, values, elems, cap);
 }
 
 // Workgroup per byte WINDOW of W bytes: window t owns the values whose first byte lies in
@@ -780,7 +791,7 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
             const bool active = lane < cnt;
             const uint64_t v = c0 + (active ? perm[first + lane] : 0u);
             const Acc a = staged ? run_batch(lsrc, c, active, v, S0, E, eb0, blob, offsets, ebase, values, elems, cap)
-                                 : run_batch(gsrc, c, active, v, S0, E, eb0, blob, offsets, ebase, values, elems, cap);
+                                 : run_batch_g(gsrc, c, active, v, S0, E, eb0, blob, offsets, ebase, values, elems, cap);
             bad += a.bad;
             pay += a.pay;
             PROBE(if (lane == 0) {
