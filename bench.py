@@ -41,6 +41,7 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="budget for the CPU baseline leg")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-check", action="store_true")
+    p.add_argument("--no-host", action="store_true", help="skip the PCIe-inclusive host leg and the copy reference")
     p.add_argument("--profile-only", action="store_true", help="decode steps only (for rocprofv3)")
     p.add_argument("--profile-encode", action="store_true", help="one decode, then encode steps only (for rocprofv3)")
     return p.parse_args()
@@ -130,6 +131,37 @@ def main():
     wall_enc, ev_enc = timed(encode, args.steps, args.warmup)
     tot2 = d_tot2.cpu().numpy().view(np.uint64).copy()
 
+    # ---- reference legs (not the headline): device copy bandwidth, PCIe-inclusive decode ----
+    host = None
+    if not args.no_host:
+        d_copy = torch.empty_like(d_data)
+        _, ev_copy = timed(lambda: d_copy.copy_(d_data), args.steps, args.warmup)
+        copy_gbs = 2 * d_data.numel() / (ev_copy * 1e-3) / 1e9          # read + write
+        del d_copy
+        # one step = pinned H2D of blobs + offsets, the decode, pinned D2H of records,
+        # descriptors and arena (what rr_decode_batch_host does, through pinned buffers)
+        h_data = torch.from_numpy(data).pin_memory()
+        h_offs = torch.from_numpy(offs.view(np.int64)).pin_memory()
+        h_vals = torch.empty(d_vals.numel(), dtype=torch.uint8).pin_memory()
+        h_elems = torch.empty(n_elems * 16, dtype=torch.uint8).pin_memory()
+        h_arena = torch.empty(nb, dtype=torch.uint8).pin_memory()
+
+        def e2e():
+            d_data.copy_(h_data, non_blocking=True)
+            d_offs.copy_(h_offs, non_blocking=True)
+            decode()
+            h_vals.copy_(d_vals, non_blocking=True)
+            h_elems.copy_(d_elems[: n_elems * 16], non_blocking=True)
+            h_arena.copy_(d_arena[:nb], non_blocking=True)
+
+        wall_e2e, _ = timed(e2e, 5, 1)
+        host = {"copy_ref": {"GBs": round(copy_gbs, 1), "frac_of_peak": round(copy_gbs / HBM_PEAK_GBS, 4),
+                             "what": "torch device-to-device copy of the blob buffer (read + write bytes)"},
+                "host_e2e": {"gib_s": round(nb * 5 / wall_e2e / 2 ** 30, 2),
+                             "ms_per_step": round(wall_e2e / 5 * 1e3, 3),
+                             "what": "pinned H2D blobs+offsets, decode, pinned D2H records+descriptors+arena"}}
+        del h_data, h_offs, h_vals, h_elems, h_arena
+
     # ---- correctness of what was timed ----
     parity = None
     if not args.no_check:
@@ -187,6 +219,7 @@ def main():
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": measured_traffic(args.config, n, nb),
                      "alg_bytes_per_launch": alg_bytes},
         "parity": parity,
+        **(host or {}),
         "gen_s": round(t_gen, 2),
     }
 
