@@ -625,6 +625,13 @@ extern "C" int rr_probe_set(void *p) { return hipMemcpyToSymbol(HIP_SYMBOL(g_pro
 #define PROBE(...)
 #endif
 
+// lanes per walk batch: a class's values in a chunk are cut into batches of at most DEC_BL, so
+// a class with few values per window can still spread over several waves
+#ifndef RR_DEC_BL
+#define RR_DEC_BL 64
+#endif
+constexpr uint32_t DEC_BL = RR_DEC_BL;
+static_assert(DEC_BL >= 1 && DEC_BL <= RR_WAVE, "batch lanes");
 #ifdef RR_DEC_WPE   // tuning: ask the register allocator for this many waves per SIMD
 #define DEC_WPE_ATTR __attribute__((amdgpu_waves_per_eu(RR_DEC_WPE)))
 #else
@@ -745,7 +752,7 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
                 cbase[c] = s;
                 bpre[k] = bs;
                 s += ccount[c];
-                bs += (ccount[c] + RR_WAVE - 1) / RR_WAVE;
+                bs += (ccount[c] + DEC_BL - 1) / DEC_BL;
             }
             bpre[C_N] = bs;
         }
@@ -782,8 +789,8 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
             uint32_t k = 0;
             while (bi >= bpre[k + 1]) ++k;
             const uint32_t c = CLASS_ORDER[k];
-            const uint32_t first = cbase[c] + (bi - bpre[k]) * RR_WAVE;
-            const uint32_t cnt = min(ccount[c] - (bi - bpre[k]) * RR_WAVE, (uint32_t)RR_WAVE);
+            const uint32_t first = cbase[c] + (bi - bpre[k]) * DEC_BL;
+            const uint32_t cnt = min(ccount[c] - (bi - bpre[k]) * DEC_BL, DEC_BL);
 #ifdef RR_SKIP_CLASSES   // timing-only builds (tools/): skip the batches of these classes
             if ((RR_SKIP_CLASSES >> c) & 1) continue;
 #endif

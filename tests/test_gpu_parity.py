@@ -61,6 +61,48 @@ def test_ragged_batch_sizes(engine, n):
     assert np.array_equal(out, data[:int(offs[-1])])
 
 
+def _int_like_strings(rng, n):
+    """Strings near string2ll's accept/reject boundaries: every length 0..24, signs, leading
+    zeros, int64 limits +-1, and stray non-digit bytes at random positions."""
+    out = [s.encode() for s, _ in G["string2ll"]]
+    for lim in (2**63 - 1, 2**63, 2**63 + 1, 10**18, 10**19 - 1, 10**19, 2**31, 2**24, 10**7, 10**14):
+        for d in (-1, 0, 1):
+            out += [str(lim + d).encode(), b"-" + str(lim + d).encode()]
+    for _ in range(n):
+        ln = int(rng.integers(0, 25))
+        s = bytearray(rng.integers(ord("0"), ord("9") + 1, size=ln).astype(np.uint8).tobytes())
+        r = rng.random()
+        if ln and r < 0.3:
+            s[0] = ord("-")
+        if ln > 1 and rng.random() < 0.1:
+            s[int(rng.integers(0, ln))] = int(rng.integers(0, 256))
+        if ln > 1 and rng.random() < 0.1:
+            s[1 if s[0] == ord("-") else 0] = ord("0")
+        out.append(bytes(s))
+    return out
+
+
+def test_list_integer_parsing(engine):
+    """List elements go through zipTryEncoding + string2ll (ziplist.c:480, util.c:360): the
+    GPU's integer/string decision and value must equal the oracle's for every element."""
+    rng = np.random.default_rng(11)
+    items = _int_like_strings(rng, 6000)
+    blobs = []
+    for k in range(0, len(items), 16):
+        b = bytes([14]) + struct.pack("<I", k & 0xFFFFFF)
+        for it in items[k:k + 16]:
+            b += struct.pack("<I", len(it)) + it
+        blobs.append(b)
+    data, offs = batch_from_blobs(blobs)
+    v, e, a, t = engine.decode_host(data, offs)
+    ov, oe, oa, ot = cpu.decode(data, offs)
+    assert t == ot and t["n_bad"] == 0
+    assert_flat_equal((v, e), (ov, oe), "list ints")
+    out, ooffs, t2 = engine.encode_host(v, e, a)
+    assert t2["n_bad"] == 0
+    assert np.array_equal(out, data[:int(offs[-1])])
+
+
 def test_empty_batch(engine):
     v, e, a, t = engine.decode_host(np.zeros(16, np.uint8), np.zeros(1, np.uint64))
     assert len(v) == 0 and t["n_elems"] == 0 and t["n_bad"] == 0
