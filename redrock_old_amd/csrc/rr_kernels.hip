@@ -431,6 +431,100 @@ __device__ __forceinline__ uint32_t classify_g(const uint8_t *b, uint64_t L) {
     }
 }
 
+// The first 24 bytes of a value as six dwords, from at most three aligned 16-byte loads
+// (granules past the value's end are not read: they may lie past the padded batch), instead
+// of one scattered byte load per header byte.  Bytes past the value's end are don't-cares:
+// every use below is guarded by a length check, as in reserve_g / classify_g.
+__device__ __forceinline__ void head24(const uint8_t *blob, uint64_t o, uint64_t b1, uint32_t (&d)[6]) {
+    const uint64_t a = o & ~15ull;
+    const u32x4 *g = reinterpret_cast<const u32x4 *>(blob + a);
+    uint32_t h[12];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const u32x4 x = a + 16 * k < b1 ? g[k] : u32x4{0u, 0u, 0u, 0u};
+        h[4 * k] = x[0]; h[4 * k + 1] = x[1]; h[4 * k + 2] = x[2]; h[4 * k + 3] = x[3];
+    }
+    const uint32_t q = (uint32_t)(o >> 2) & 3, sh = (uint32_t)o & 3;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+        const uint32_t lo = q == 0 ? h[j] : q == 1 ? h[j + 1] : q == 2 ? h[j + 2] : h[j + 3];
+        const uint32_t hi = q == 0 ? h[j + 1] : q == 1 ? h[j + 2] : q == 2 ? h[j + 3] : h[j + 4];
+        d[j] = __builtin_amdgcn_alignbyte(hi, lo, sh);
+    }
+}
+// dword at byte p of the value b (p + 4 <= its length): aligned loads only
+__device__ __forceinline__ uint32_t ld_u32_al(const uint8_t *b, uint64_t p) {
+    const uintptr_t x = reinterpret_cast<uintptr_t>(b) + p;
+    const uint32_t *w = reinterpret_cast<const uint32_t *>(x & ~(uintptr_t)3);
+    const uint32_t s = (uint32_t)x & 3;
+    const uint32_t lo = w[0], hi = s ? w[1] : 0u;
+    return __builtin_amdgcn_alignbyte(hi, lo, s);
+}
+
+// reserve_g + classify_g from the header dwords (same results, byte for byte)
+__device__ __forceinline__ void reserve_classify(const uint8_t *b, uint64_t L, const uint32_t (&d)[6],
+                                                 uint64_t &r, uint32_t &c) {
+    r = 0;
+    c = C_EXACT;
+    if (L < 5) return;
+    const uint32_t t = d[0] & 0xFF;
+    const uint32_t f5 = __builtin_amdgcn_alignbyte(d[2], d[1], 1), f9 = __builtin_amdgcn_alignbyte(d[3], d[2], 1);
+    const uint32_t f13 = __builtin_amdgcn_alignbyte(d[4], d[3], 1);
+    const uint64_t u5 = (uint64_t)f5 | ((uint64_t)f9 << 32);
+    switch (t) {
+        case RR_TYPE_STRING: {
+            if (L < 6) return;
+            r = 1;
+            const uint32_t enc = (d[1] >> 8) & 0xFF;
+            const uint64_t rest = L - 6;
+            if (enc == RR_ENC_INT) c = rest == 8 ? C_STR : C_EXACT;
+            else if (enc == RR_ENC_EMBSTR) c = rest <= RR_EMBSTR_SIZE_LIMIT ? C_STR : C_EXACT;
+            else if (enc == RR_ENC_RAW) c = rest <= 0xFFFFFFFFull ? C_STR : C_EXACT;
+            return;
+        }
+        case RR_TYPE_LIST_QUICKLIST: {
+            c = C_LIST;
+            uint64_t p = 5, n = 0;
+            while (p < L) {
+                if (L - p < 4) break;
+                const uint64_t l = ld_u32_al(b, p);
+                if (l > L - p - 4) break;
+                ++n;
+                p += 4 + l;
+            }
+            r = n;
+            return;
+        }
+        default:
+            break;
+    }
+    if (L < 13) return;
+    switch (t) {
+        case RR_TYPE_SET_INTSET: {
+            const uint64_t w = f5, cnt = f9;
+            const bool ok = (w == 2 || w == 4 || w == 8) && L - 13 == w * cnt;
+            r = ok ? cnt : 0;
+            c = ok ? C_IS : C_EXACT;
+            return;
+        }
+        case RR_TYPE_SET_HT: { const uint64_t m = (L - 13) / 8; r = u5 < m ? u5 : m; c = C_HT; return; }
+        case RR_TYPE_HASH_HT: { const uint64_t m = (L - 13) / 8; r = u5 > m / 2 ? m : 2 * u5; c = C_HT; return; }
+        case RR_TYPE_ZSET_SKIPLIST: { const uint64_t m = (L - 13) / 16; r = 2 * (u5 < m ? u5 : m); c = C_SL; return; }
+        case RR_TYPE_HASH_ZIPLIST:
+        case RR_TYPE_ZSET_ZIPLIST: {
+            const uint64_t Lz = u5;
+            c = (L >= 24 && Lz == L - 13 && f13 == Lz) ? C_ZL : C_EXACT;
+            if (Lz != L - 13 || Lz < 11) return;
+            const uint64_t zllen = (d[5] >> 8) & 0xFFFF;
+            if (zllen != 0xFFFF) { const uint64_t m = (Lz - 11) / 2; r = 1 + (zllen < m ? zllen : m); return; }
+            r = 1 + zl_walk_count_g(b + 13, Lz);
+            return;
+        }
+        default:
+            return;
+    }
+}
+
 __global__ __launch_bounds__(256) void count_kernel(const uint8_t *__restrict__ blob,
                                                     const uint64_t *__restrict__ offsets, uint64_t n,
                                                     uint32_t *__restrict__ first_val, uint32_t nwin, uint32_t win,
@@ -445,8 +539,18 @@ __global__ __launch_bounds__(256) void count_kernel(const uint8_t *__restrict__ 
     for (uint64_t w = w_lo; w <= w_hi && w <= nwin; ++w) first_val[w] = (uint32_t)i;
     if (i < n) {
         const uint64_t b1 = offsets[i + 1];
+#ifdef RR_COUNT_BYTES   // the byte-load formulation (diagnostics)
         counts[i] = reserve_g(blob + o_hi, b1 - o_hi);
         cls[i] = (uint8_t)classify_g(blob + o_hi, b1 - o_hi);
+#else
+        uint32_t d[6];
+        head24(blob, o_hi, b1, d);
+        uint64_t r;
+        uint32_t c;
+        reserve_classify(blob + o_hi, b1 - o_hi, d, r, c);
+        counts[i] = r;
+        cls[i] = (uint8_t)c;
+#endif
     }
 }
 
@@ -632,6 +736,19 @@ extern "C" int rr_probe_set(void *p) { return hipMemcpyToSymbol(HIP_SYMBOL(g_pro
 #endif
 constexpr uint32_t DEC_BL = RR_DEC_BL;
 static_assert(DEC_BL >= 1 && DEC_BL <= RR_WAVE, "batch lanes");
+// 1: the mirror-arena copy is written by waves that ran out of walk batches (step 4), not
+// during staging
+#ifndef RR_DEC_LATECOPY
+#define RR_DEC_LATECOPY 0
+#endif
+#ifndef RR_DEC_SU   // 16-byte staging loads in flight per thread (late-copy staging)
+#define RR_DEC_SU 4
+#endif
+#if RR_DEC_LATECOPY
+#define PROBE_OR_LATE(...) __VA_ARGS__
+#else
+#define PROBE_OR_LATE(...)
+#endif
 #ifdef RR_DEC_WPE   // tuning: ask the register allocator for this many waves per SIMD
 #define DEC_WPE_ATTR __attribute__((amdgpu_waves_per_eu(RR_DEC_WPE)))
 #else
@@ -652,6 +769,7 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
     __shared__ uint16_t perm[PMAX];
     __shared__ uint32_t ccount[C_N], cbase[C_N], ccur[C_N], bpre[C_N + 1];
     __shared__ uint32_t next_batch;
+    PROBE_OR_LATE(__shared__ uint32_t next_copy;)
     __shared__ uint64_t red[2][NW];
     PROBE(__shared__ uint64_t prb[PROBE_WORDS]; uint64_t pt0 = __builtin_amdgcn_s_memtime(), pt1 = 0, pt2 = 0;
           if (threadIdx.x < PROBE_WORDS) prb[threadIdx.x] = 0;)
@@ -677,6 +795,25 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
         cls0[j] = v < v_hi ? (uint32_t)cls[v] : C_N;
     }
 
+#if RR_DEC_LATECOPY
+    // 1. value bytes -> LDS only; the window's arena copy is written in step 4 by waves that
+    //    have run out of batches, overlapping the longest walks
+    if (tid == 0) next_copy = 0;
+    if (staged) {
+        const u32x4 *src = reinterpret_cast<const u32x4 *>(blob);
+        u32x4 *lds = reinterpret_cast<u32x4 *>(stage);
+        const uint64_t cs0 = S0 >> 4, cs1 = S1 >> 4;
+        uint64_t c = cs0 + tid;
+        for (; c + (RR_DEC_SU - 1) * NT < cs1; c += RR_DEC_SU * NT) {
+            u32x4 x[RR_DEC_SU];
+#pragma unroll
+            for (int k = 0; k < RR_DEC_SU; ++k) x[k] = src[c + k * NT];
+#pragma unroll
+            for (int k = 0; k < RR_DEC_SU; ++k) lds[c + k * NT - cs0] = x[k];
+        }
+        for (; c < cs1; c += NT) lds[c - cs0] = src[c];
+    }
+#else
     // 1. window -> arena, value bytes -> LDS (one load feeds both)
     {
         const u32x4 *src = reinterpret_cast<const u32x4 *>(blob);
@@ -706,6 +843,7 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
             if (staged && c >= cs0) lds[c - cs0] = x;
         }
     }
+#endif
     // values that do not fit the stage are read from global memory; if even their 32-bit
     // window-relative byte or slot offsets could overflow, the exact parser takes them
     const uint64_t eb0 = ebase[v_lo], eb1 = ebase[v_hi];
@@ -808,6 +946,37 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
             })
         }
     }
+#if RR_DEC_LATECOPY
+    // 4. the window's mirror-arena copy in 4 KiB tasks, taken by each wave as soon as it has no
+    //    batch left (from the LDS stage where the window's bytes are staged, else from global)
+    {
+        if (v_end == v_lo) __syncthreads();   // (no chunk ran: order next_copy's reset)
+        const u32x4 *src = reinterpret_cast<const u32x4 *>(blob);
+        u32x4 *dst = reinterpret_cast<u32x4 *>(arena);
+        const u32x4 *lds = reinterpret_cast<const u32x4 *>(stage);
+        const uint64_t cw0 = W0 >> 4, cw1 = W1 >> 4, cs0 = S0 >> 4, cs1 = staged ? S1 >> 4 : cs0;
+        constexpr uint32_t TASK = 4 * RR_WAVE;   // 16-byte granules per task
+        const uint32_t ntask = (uint32_t)((cw1 - cw0 + TASK - 1) / TASK);
+        for (;;) {
+            uint32_t ti = 0;
+            if (lane == 0) ti = atomicAdd(&next_copy, 1u);
+            ti = __builtin_amdgcn_readfirstlane(__shfl(ti, 0, RR_WAVE));
+            if (ti >= ntask) break;
+            const uint64_t g0 = cw0 + (uint64_t)ti * TASK + lane;
+            u32x4 x[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint64_t g = g0 + k * RR_WAVE;
+                if (g < cw1) x[k] = g >= cs0 && g < cs1 ? lds[g - cs0] : src[g];
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint64_t g = g0 + k * RR_WAVE;
+                if (g < cw1) __builtin_nontemporal_store(x[k], dst + g);
+            }
+        }
+    }
+#endif
     bad = wave_sum(bad);
     pay = wave_sum(pay);
     if (lane == 0) { red[0][wave] = bad; red[1][wave] = pay; }
