@@ -46,5 +46,10 @@ for k in pipeline:
         res["kernels"].setdefault(k, {}).update({"fetch_bytes": f, "write_bytes": w, "hbm_bytes": 2 * f + w})
         tot += 2 * f + w
 res["traffic_bytes_per_call"] = tot if per else None
+if os.path.exists(out):   # keep the workload tag bench.py matches the summary by
+    try:
+        res.setdefault("workload", json.load(open(out)).get("workload"))
+    except ValueError:
+        pass
 json.dump(res, open(out, "w"), indent=1)
 print(json.dumps(res, indent=1))
