@@ -485,6 +485,9 @@ __device__ __forceinline__ void reserve_classify(const uint8_t *b, uint64_t L, c
         case RR_TYPE_LIST_QUICKLIST: {
             c = C_LIST;
             uint64_t p = 5, n = 0;
+#ifdef RR_COUNT_NOLIST   // timing-only builds (tools/): no list walk (wrong reservations)
+            p = L;
+#endif
             while (p < L) {
                 if (L - p < 4) break;
                 const uint64_t l = ld_u32_al(b, p);
