@@ -125,8 +125,8 @@ __device__ __forceinline__ uint32_t ab(uint32_t hi, uint32_t lo, uint32_t s) { r
 // Straight-line (selects only): every digit position is evaluated and out-of-range ones are
 // masked, so a wave pays one pass whatever mix of lengths its lanes hold.  The digits are
 // accumulated in three 24-bit chunks (byte positions [0,7), [7,14), [14,20); < 10^7 each) with
-// full-rate v_mad_u32_u24 steps; only the final combine uses 64-bit multiplies.  (A 64-bit
-// multiply-accumulate per digit is three quarter-rate multiplies: ~2 K cycles per list step.)
+// full-rate v_mad_u32_u24 steps; only the final combine uses 64-bit multiplies (a 64-bit
+// multiply-accumulate per digit is three quarter-rate multiplies).
 __device__ __forceinline__ uint32_t pow10_u24(uint32_t n) {   // 10^n, n in [0, 7]
     const uint32_t a = (n & 1) ? 10u : 1u, b = (n & 2) ? 100u : 1u, c = (n & 4) ? 10000u : 1u;
     return __umul24(__umul24(a, b), c);
@@ -266,14 +266,22 @@ __device__ __forceinline__ bool do_list(const Src &R, const Lane &l, bool active
     uint32_t p = l.q + 5, k = 0;
     const uint32_t end = l.q + l.L;
     bool fail = false, live = active;
-    Raw<6> ra = R.template fetch<6>(p), rb;   // len + 20 bytes
-    auto step = [&](const Raw<6> &cur, Raw<6> &nxt) __attribute__((always_inline)) {
-        uint32_t b[6];
-        cur.align(b);
+#ifndef RR_LIST_RAW   // timing-only builds (tools/) narrow the step's read (wrong int decisions)
+#define RR_LIST_RAW 6
+#endif
+    Raw<RR_LIST_RAW> ra = R.template fetch<RR_LIST_RAW>(p), rb;   // len + 20 bytes
+    auto step = [&](const Raw<RR_LIST_RAW> &cur, Raw<RR_LIST_RAW> &nxt) __attribute__((always_inline)) {
+        uint32_t b[6] = {0u, 0u, 0u, 0u, 0u, 0u};
+        {
+            uint32_t t[RR_LIST_RAW];
+            cur.align(t);
+#pragma unroll
+            for (int i = 0; i < RR_LIST_RAW; ++i) b[i] = t[i];
+        }
         const uint32_t rem = end - p, len = b[0];
         const uint64_t nx = (uint64_t)p + 4 + len;
         const uint32_t pn = nx < end ? (uint32_t)nx : end;
-        nxt = R.template fetch<6>(live ? pn : p);
+        nxt = R.template fetch<RR_LIST_RAW>(live ? pn : p);
         __builtin_amdgcn_sched_barrier(0);   // keep the read ahead of the checks and the store
         const bool done = p == end;
         const bool bad = (rem < 4) | (len > rem - 4) | (k >= l.r);
@@ -281,7 +289,11 @@ __device__ __forceinline__ bool do_list(const Src &R, const Lane &l, bool active
         fail |= live & !done & bad;
         const uint32_t d[5] = {b[1], b[2], b[3], b[4], b[5]};
         int64_t iv;
+#ifdef RR_LIST_NOINT   // timing-only builds (tools/): no integer check (wrong int decisions)
+        const bool isint = false; iv = 0; (void)d;
+#else
         const bool isint = regs_try_int(d, len, iv);
+#endif
         put_desc(l.E, emit ? l.slot(k) : NOSLOT, isint ? (uint64_t)iv : l.B + p + 4, isint ? 0 : len,
                  isint ? RR_K_INT : RR_K_STR, 0);
         pay += emit && !isint ? len : 0;
