@@ -134,13 +134,25 @@ __device__ __forceinline__ uint32_t pow10_u24(uint32_t n) {   // 10^n, n in [0, 
 __device__ __forceinline__ bool regs_try_int(const uint32_t (&b)[5], uint32_t len, int64_t &out) {
     const uint32_t c0 = b[0] & 0xFF;
     const uint32_t neg = c0 == '-' ? 1u : 0u;
-    bool ok = true;
+    // digit check of bytes [neg, len) four at a time (SWAR, VALU only): a byte is a digit iff
+    // its high nibble is 3 and its low nibble + 6 does not carry into bit 4.  (Per-byte compares
+    // folded into an SGPR mask cost a VALU->SALU dependency per digit.)
+    uint32_t nondig = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 5; ++k) {
+        const uint32_t x = b[k];
+        const uint32_t nd = ((x & 0xF0F0F0F0u) ^ 0x30303030u) | (((x & 0x0F0F0F0Fu) + 0x06060606u) & 0x10101010u);
+        const uint32_t cnt = len > 4 * k + 4 ? 4u : len > 4 * k ? len - 4 * k : 0u;
+        uint32_t m = cnt ? 0xFFFFFFFFu >> (32 - 8 * cnt) : 0u;
+        if (k == 0) m &= neg ? 0xFFFFFF00u : 0xFFFFFFFFu;
+        nondig |= nd & m;
+    }
+    bool ok = nondig == 0;
     uint32_t acc[3] = {0u, 0u, 0u};
 #pragma unroll
     for (uint32_t j = 0; j < 20; ++j) {
         const uint32_t d = ((b[j >> 2] >> (8 * (j & 3))) & 0xFF) - '0';
         const bool in = (j == 0 ? neg == 0 : true) & (j < len);
-        ok &= !in | (d <= 9u);
         const uint32_t c = j < 7 ? 0 : j < 14 ? 1 : 2;
         const uint32_t t = __umul24(acc[c], 10u) + d;
         acc[c] = in ? t : acc[c];
