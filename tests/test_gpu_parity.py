@@ -188,12 +188,13 @@ def test_device_api_matches_host_api(engine):
     assert torch.equal(d_out[:nb], d_data[:nb])
 
 
-def test_full_size_mixed_roundtrip(engine):
-    """1M-value mixed batch (the headline size): size-independent properties on the GPU —
-    encode(decode(b)) == b byte for byte, zero bad values, descriptor count equals the oracle's,
-    per-type histogram of records matches the blobs' type bytes."""
+@pytest.mark.parametrize("cfg", [4, 3, 2])
+def test_full_size_mixed_roundtrip(engine, cfg):
+    """1M-value batches at BASELINE.json's sizes (config 4 mixed = the headline, config 3 Hash
+    ziplists, config 2 Zipf Strings): records and descriptors equal the oracle's, zero bad
+    values, and encode(decode(b)) == b byte for byte on the GPU."""
     import torch
-    data, offs = rr.gen_batch(4, 1_000_000)
+    data, offs = rr.gen_batch(cfg, 1_000_000)
     n = len(offs) - 1
     nb = int(offs[-1])
     dev = torch.device("cuda:0")
