@@ -29,11 +29,16 @@
  *                   (ziplist.c:480: 1<=len<32 and string2ll, util.c:360) — exactly what
  *                   desList's quicklistPushTail stores — else STR
  *   SET_INTSET      n INT elems; rr_value.enc = intset width
- *   SET_HT          n STR elems (blob order)
+ *   SET_HT          STR elems in blob order, later duplicates of a member dropped (desSet's
+ *                   dictAdd keeps the first and ignores the rest, rock_serdes.c:297); the
+ *                   value still owns one slot per blob member, the unused tail is zero
  *   HASH_ZIPLIST    ZLRAW{arena off, L} then one elem per ziplist entry (STR or INT,
  *   ZSET_ZIPLIST    zenc = the entry's encoding byte); encode only needs ZLRAW
- *   HASH_HT         2n STR elems: field, value, field, value, ...
- *   ZSET_SKIPLIST   2n elems: STR member, SCORE{f64 bits}, ... (blob order = descending)
+ *   HASH_HT         2n STR elems: field, value, field, value, ... (duplicate field: RR_E_DUP)
+ *   ZSET_SKIPLIST   2n elems: STR member, SCORE{f64 bits}, ... in the order serZset writes
+ *                   the skiplist desZset builds: descending (score, member) (zslInsert,
+ *                   t_zset.c:132-180, then the tail->head walk rock_serdes.c:430-440), equal
+ *                   keys in blob order.  A blob serZset wrote is already in that order.
  */
 #ifndef RR_FORMAT_H
 #define RR_FORMAT_H
@@ -68,8 +73,13 @@ extern "C" {
 #define RR_K_SCORE  2
 #define RR_K_ZLRAW  3
 
-/* Per-value decode status (0 = OK). Nonzero codes correspond to the reference's
- * serverAssert/serverPanic sites; the compat shim turns any of them into abort(). */
+/* Per-value decode status (0 = OK).  Codes 1-7, 9, 13 and 14 are the reference's own
+ * serverAssert/serverPanic sites; the compat shim turns any nonzero status into abort().
+ * Codes marked [stricter] reject blobs the reference would load into a broken object (it
+ * never validates those bytes); see DESIGN.md "Deviations" for the full table.
+ * When one blob has several defects the engine reports the structural one (SHORT / TRUNC /
+ * COUNT) before DUP / NAN; the reference may hit a different assert first — either way the
+ * value is rejected. */
 #define RR_OK               0
 #define RR_E_SHORT          1   /* blob shorter than its fixed header (rock_serdes.c:134,192,249,350,449,539-542) */
 #define RR_E_TYPE           2   /* unknown type tag (rock_serdes.c:561) */
@@ -78,11 +88,18 @@ extern "C" {
 #define RR_E_EMBSTR_LEN     5   /* EMBSTR longer than 44 (rock_serdes.c:152) */
 #define RR_E_TRUNC          6   /* a length field runs past the blob (rock_serdes.c:202-206,288-295,...) */
 #define RR_E_COUNT          7   /* element count disagrees with the header (rock_serdes.c:303,404,501) */
-#define RR_E_INTSET         8   /* intset width not 2/4/8 or contents length mismatch (rock_serdes.c:274) */
+#define RR_E_INTSET         8   /* contents length != width*count (rock_serdes.c:274); [stricter]
+                                   also width not 2/4/8 and the u32 wrap of width*count */
 #define RR_E_ZL_LEN         9   /* ziplist byte count != remaining blob (rock_serdes.c:360,459) */
-#define RR_E_ZL_CORRUPT     10  /* ziplist entries do not parse (ziplist.c:300-447 rules) */
-#define RR_E_CAPACITY       11  /* output descriptor / byte capacity exceeded */
-#define RR_E_ENCODE         12  /* flat value cannot be encoded (bad kind / missing ZLRAW) */
+#define RR_E_ZL_CORRUPT     10  /* [stricter] ziplist entries / zltail / zllen / odd pair count do
+                                   not parse by ziplist.c:300-447 (the reference copies them blind) */
+#define RR_E_CAPACITY       11  /* output descriptor / byte capacity exceeded (batch API only) */
+#define RR_E_ENCODE         12  /* flat value cannot be encoded (bad kind / missing ZLRAW / status
+                                   != 0 / descriptor or payload outside the caller's buffers) */
+#define RR_E_DUP            13  /* HASH_HT duplicate field: dictAdd != DICT_OK, rock_serdes.c:399-400 */
+#define RR_E_NAN            14  /* ZSET_SKIPLIST NaN score: zslInsert serverAssert(!isnan(score)),
+                                   t_zset.c:137 reached from rock_serdes.c:498 */
+#define RR_N_STATUS         15
 
 typedef struct rr_value {   /* 16 bytes */
     uint8_t  type;          /* RR_TYPE_* */

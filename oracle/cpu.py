@@ -30,7 +30,7 @@ def lib():
         L = C.CDLL(LIB_PATH)
         vp, u64 = C.c_void_p, C.c_uint64
         L.rro_decode.argtypes = [vp, vp, u64, vp, vp, u64, vp, C.POINTER(_Totals), C.c_int]
-        L.rro_encode.argtypes = [vp, vp, vp, u64, vp, u64, vp, C.POINTER(_Totals), C.c_int]
+        L.rro_encode.argtypes = [vp, vp, u64, vp, u64, u64, vp, u64, vp, C.POINTER(_Totals), C.c_int]
         L.rro_string2ll.argtypes = [C.c_char_p, C.c_size_t, C.POINTER(C.c_longlong)]
         L.rro_ll2str.argtypes = [C.c_char_p, C.c_longlong]
         L.rro_parse_ziplist.argtypes = [vp, u64, u64, vp, u64, C.POINTER(C.c_uint64)]
@@ -78,7 +78,10 @@ def encode(values, elems, arena, data_cap=None, nthreads=1):
     data = np.zeros(max(data_cap, 1), np.uint8)
     offsets = np.zeros(n + 1, np.uint64)
     t = _Totals()
-    lib().rro_encode(_p(values), _p(elems), _p(np.ascontiguousarray(arena, np.uint8)), n, _p(data), data_cap,
+    values = np.ascontiguousarray(values)
+    elems = np.ascontiguousarray(elems)
+    arena = np.ascontiguousarray(arena, np.uint8)
+    lib().rro_encode(_p(values), _p(elems), len(elems), _p(arena), arena.size, n, _p(data), data_cap,
                      _p(offsets), C.byref(t), nthreads)
     return data[:int(offsets[-1])], offsets, _tot(t)
 

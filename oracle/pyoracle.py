@@ -32,6 +32,7 @@ K_STR, K_INT, K_SCORE, K_ZLRAW = 0, 1, 2, 3
 
 OK, E_SHORT, E_TYPE, E_STR_ENC, E_STR_INTLEN, E_EMBSTR_LEN = 0, 1, 2, 3, 4, 5
 E_TRUNC, E_COUNT, E_INTSET, E_ZL_LEN, E_ZL_CORRUPT, E_CAPACITY, E_ENCODE = 6, 7, 8, 9, 10, 11, 12
+E_DUP, E_NAN = 13, 14
 
 LLONG_MIN, LLONG_MAX = -(1 << 63), (1 << 63) - 1
 
@@ -180,6 +181,9 @@ def decode_one(blob: bytes, off: int = 0):
         val["status"] = e.code
         elems = []
     val["n_elems"] = len(elems)
+    val.setdefault("n_slots", len(elems))
+    if val["status"] != OK:
+        val["n_slots"] = 0
     return val, elems
 
 
@@ -240,6 +244,7 @@ def _decode_body(b, off, val):
         rem -= 8
         per = 1 if t == T_SET_HT else 2
         got = 0
+        members = []   # (batch offset, length) in blob order
         while rem:
             for _ in range(per):
                 if rem < 8:
@@ -249,12 +254,24 @@ def _decode_body(b, off, val):
                 rem -= 8
                 if ln > rem:
                     raise DecodeError(E_TRUNC)
-                out.append((K_STR, off + p, ln, 0))
+                members.append((off + p, ln, bytes(b[p:p + ln])))
                 p += ln
                 rem -= ln
             got += 1
         if got != cnt:
             raise DecodeError(E_COUNT)
+        val["n_slots"] = len(members)
+        seen = set()
+        for i, (o, ln, key) in enumerate(members):
+            if per == 2 and i % 2:            # hash values are not keys
+                out.append((K_STR, o, ln, 0))
+                continue
+            if key in seen:                   # dictAdd != DICT_OK
+                if per == 2:
+                    raise DecodeError(E_DUP)  # rock_serdes.c:399-400 serverAssert
+                continue                      # desSet ignores it (rock_serdes.c:297)
+            seen.add(key)
+            out.append((K_STR, o, ln, 0))
     elif t in (T_HASH_ZIPLIST, T_ZSET_ZIPLIST):
         if rem < 8:
             raise DecodeError(E_SHORT)
@@ -274,6 +291,7 @@ def _decode_body(b, off, val):
         cnt = _u64(b, p)
         p += 8
         rem -= 8
+        pairs = []
         for _ in range(cnt):
             if rem < 8:
                 raise DecodeError(E_TRUNC)
@@ -282,16 +300,26 @@ def _decode_body(b, off, val):
             rem -= 8
             if ln > rem:
                 raise DecodeError(E_TRUNC)
-            out.append((K_STR, off + p, ln, 0))
+            mo, ele = off + p, bytes(b[p:p + ln])
             p += ln
             rem -= ln
             if rem < 8:
                 raise DecodeError(E_TRUNC)
-            out.append((K_SCORE, _u64(b, p), 0, 0))
+            bits = _u64(b, p)
+            pairs.append((struct.unpack_from("<d", b, p)[0], ele, mo, ln, bits))
             p += 8
             rem -= 8
         if rem != 0:
             raise DecodeError(E_COUNT)
+        if any(x[0] != x[0] for x in pairs):  # zslInsert serverAssert(!isnan(score)) t_zset.c:137
+            raise DecodeError(E_NAN)
+        # desZset rebuilds a skiplist ascending by (score, member) and serZset writes it tail to
+        # head: descending, equal keys kept in blob order (Python's sort is stable, also with
+        # reverse=True; -0.0 == 0.0 as in zslInsert's double compares)
+        pairs.sort(key=lambda x: (x[0], x[1]), reverse=True)
+        for sc, ele, mo, ln, bits in pairs:
+            out.append((K_STR, mo, ln, 0))
+            out.append((K_SCORE, bits, 0, 0))
     else:
         raise DecodeError(E_TYPE)
     return out
@@ -435,11 +463,13 @@ def decode_batch(blobs):
     for i, b in enumerate(blobs):
         v, es = decode_one(b, offsets[i])
         r = reserve(b)
-        if v["status"] == OK and len(es) != r:
+        if v["status"] == OK and v["n_slots"] != r:
             v["status"], v["n_elems"], es = E_COUNT, 0, []
         v["elem_base"] = len(elems)
         values.append(v)
-        elems.extend(es if v["status"] == OK else [(K_STR, 0, 0, 0)] * r)
+        # a malformed value keeps its slots zero-filled; a de-duplicated set zero-fills its tail
+        elems.extend(es if v["status"] == OK else [])
+        elems.extend([(K_STR, 0, 0, 0)] * (r - (len(es) if v["status"] == OK else 0)))
     return data, offsets, values, elems, data  # mirror arena == blob bytes
 
 

@@ -156,16 +156,86 @@ int rro_parse_ziplist(const uint8_t *zl, uint64_t L, uint64_t base, rr_elem *out
                    e_->kind = (K); e_->zenc = (Z); e_->rsv = 0; } \
         n++; } while (0)
 
+/* Members of one HT / skiplist value while it is parsed: batch offset + length of the string,
+ * the raw score bits (skiplist), the position in the blob, and a duplicate mark. */
+typedef struct { uint64_t off, len, score; uint64_t idx; int dup; } mem_t;
+static __thread mem_t *g_mem;
+static __thread uint64_t g_mem_cap;
+static __thread const uint8_t *g_base;   /* batch base for the qsort comparators */
+
+static mem_t *mem_slot(uint64_t i) {
+    if (i >= g_mem_cap) {
+        uint64_t c = g_mem_cap ? g_mem_cap * 2 : 64;
+        while (c <= i) c *= 2;
+        g_mem = (mem_t *)realloc(g_mem, c * sizeof(mem_t));
+        g_mem_cap = c;
+    }
+    return &g_mem[i];
+}
+
+/* sdscmp (sds.c:814-824): memcmp of the common prefix, then the shorter string first */
+static int sdscmp_raw(const uint8_t *a, uint64_t la, const uint8_t *b, uint64_t lb) {
+    uint64_t m = la < lb ? la : lb;
+    int c = m ? memcmp(a, b, m) : 0;
+    if (c) return c;
+    return la < lb ? -1 : la > lb ? 1 : 0;
+}
+
+/* content order for duplicate detection: (len, bytes), then blob position */
+static int key_cmp(const void *x, const void *y) {
+    const mem_t *a = *(mem_t *const *)x, *b = *(mem_t *const *)y;
+    if (a->len != b->len) return a->len < b->len ? -1 : 1;
+    int c = a->len ? memcmp(g_base + a->off, g_base + b->off, a->len) : 0;
+    if (c) return c;
+    return a->idx < b->idx ? -1 : a->idx > b->idx;
+}
+
+/* Marks every key equal to an earlier key (dictAdd's DICT_ERR, dict.c:265 via
+ * dictAddRaw/_dictKeyIndex); returns how many.  keys[] point into the member table. */
+static uint64_t mark_dups(mem_t **keys, uint64_t k) {
+    if (k < 2) return 0;
+    qsort(keys, k, sizeof(mem_t *), key_cmp);
+    uint64_t d = 0;
+    for (uint64_t i = 1; i < k; i++)
+        if (keys[i]->len == keys[i - 1]->len &&
+            (!keys[i]->len || !memcmp(g_base + keys[i]->off, g_base + keys[i - 1]->off, keys[i]->len))) {
+            keys[i]->dup = 1;   /* the earlier blob position sorted first: it is the one dictAdd kept */
+            d++;
+        }
+    return d;
+}
+
+/* The order serZset writes the skiplist desZset rebuilt: zslInsert (t_zset.c:132-180) keeps
+ * the list ascending by (score, sdscmp(ele)) with a new node placed before equal ones, and
+ * serZset walks it tail->head (rock_serdes.c:430-440) — i.e. descending by (score, ele),
+ * equal keys in blob order.  Scores compare as doubles (-0.0 == 0.0); NaN never gets here. */
+static int sl_cmp(const void *x, const void *y) {
+    const mem_t *a = (const mem_t *)x, *b = (const mem_t *)y;
+    double sa, sb;
+    memcpy(&sa, &a->score, 8);
+    memcpy(&sb, &b->score, 8);
+    if (sa > sb) return -1;
+    if (sa < sb) return 1;
+    int c = sdscmp_raw(g_base + a->off, a->len, g_base + b->off, b->len);
+    if (c) return c > 0 ? -1 : 1;
+    return a->idx < b->idx ? -1 : a->idx > b->idx;
+}
+
+static int is_nan_bits(uint64_t s) {
+    return (s & 0x7FF0000000000000ull) == 0x7FF0000000000000ull && (s & 0x000FFFFFFFFFFFFFull);
+}
+
 /* desObject rock_serdes.c:538-564 and des{String,List,Set,Hash,Zset} :133-508. */
 int rro_decode_one(const uint8_t *data, uint64_t off, uint64_t len, rr_value *v,
-                   rr_elem *out, uint64_t *n_elems, uint64_t *payload) {
+                   rr_elem *out, uint64_t *n_elems, uint64_t *n_slots, uint64_t *payload) {
     const uint8_t *b = data + off;
-    uint64_t n = 0, pay = 0;
+    uint64_t n = 0, pay = 0, slots = 0;
     int st = RR_OK;
+    g_base = data;
     v->type = len ? b[0] : 0;
     v->enc = 0;
     v->lru = len >= 5 ? (ld32(b + 1) & RR_LRU_MASK) : 0;
-    *n_elems = 0; *payload = 0;
+    *n_elems = 0; *payload = 0; *n_slots = 0;
     if (len < 5) { st = RR_E_SHORT; goto done; }                       /* :539-542 */
     uint64_t p = 5, rem = len - 5;
     switch (b[0]) {
@@ -213,7 +283,7 @@ int rro_decode_one(const uint8_t *data, uint64_t off, uint64_t len, rr_value *v,
     case RR_TYPE_SET_HT:                                                 /* :277-303 */
     case RR_TYPE_HASH_HT: {                                              /* :368-404 */
         if (rem < 8) { st = RR_E_SHORT; break; }
-        uint64_t cnt = ld64(b + p), got = 0;
+        uint64_t cnt = ld64(b + p), got = 0, m = 0;
         int per = b[0] == RR_TYPE_SET_HT ? 1 : 2;
         p += 8; rem -= 8;
         while (rem && st == RR_OK) {
@@ -222,13 +292,28 @@ int rro_decode_one(const uint8_t *data, uint64_t off, uint64_t len, rr_value *v,
                 uint64_t l = ld64(b + p);
                 p += 8; rem -= 8;
                 if (l > rem) { st = RR_E_TRUNC; break; }
-                EMIT(RR_K_STR, off + p, l, 0);
-                pay += l;
+                mem_t *e = mem_slot(m);
+                e->off = off + p; e->len = l; e->idx = m; e->dup = 0;
+                m++;
                 p += l; rem -= l;
             }
             got++;
         }
         if (st == RR_OK && got != cnt) st = RR_E_COUNT;
+        if (st != RR_OK) break;
+        slots = m;
+        /* keys: every member of a set, the fields (even positions) of a hash */
+        uint64_t nk = per == 1 ? m : m / 2;
+        mem_t **keys = (mem_t **)malloc(sizeof(mem_t *) * (nk ? nk : 1));
+        for (uint64_t i = 0; i < nk; i++) keys[i] = &g_mem[i * (uint64_t)per];
+        uint64_t d = mark_dups(keys, nk);
+        free(keys);
+        if (d && per == 2) { st = RR_E_DUP; break; }                   /* :399-400 */
+        for (uint64_t i = 0; i < m; i++) {                               /* :297 keeps the first */
+            if (g_mem[i].dup) continue;
+            EMIT(RR_K_STR, g_mem[i].off, g_mem[i].len, 0);
+            pay += g_mem[i].len;
+        }
         break;
     }
     case RR_TYPE_HASH_ZIPLIST:                                           /* :356-366 */
@@ -249,30 +334,46 @@ int rro_decode_one(const uint8_t *data, uint64_t off, uint64_t len, rr_value *v,
     }
     case RR_TYPE_ZSET_SKIPLIST: {                                        /* :467-501 */
         if (rem < 8) { st = RR_E_SHORT; break; }
-        uint64_t cnt = ld64(b + p);
+        uint64_t cnt = ld64(b + p), m = 0;
         p += 8; rem -= 8;
         for (uint64_t i = 0; i < cnt; i++) {
             if (rem < 8) { st = RR_E_TRUNC; break; }
             uint64_t l = ld64(b + p);
             p += 8; rem -= 8;
             if (l > rem) { st = RR_E_TRUNC; break; }
-            EMIT(RR_K_STR, off + p, l, 0);
-            pay += l;
+            mem_t *e = mem_slot(m);
+            e->off = off + p; e->len = l; e->idx = m; e->dup = 0;
             p += l; rem -= l;
             if (rem < 8) { st = RR_E_TRUNC; break; }
-            EMIT(RR_K_SCORE, ld64(b + p), 0, 0);
+            e->score = ld64(b + p);
+            m++;
             p += 8; rem -= 8;
         }
         if (st == RR_OK && rem != 0) st = RR_E_COUNT;
+        if (st != RR_OK) break;
+        for (uint64_t i = 0; i < m; i++)
+            if (is_nan_bits(g_mem[i].score)) { st = RR_E_NAN; break; }  /* t_zset.c:137 */
+        if (st != RR_OK) break;
+        int sorted = 1;
+        for (uint64_t i = 1; i < m && sorted; i++) sorted = sl_cmp(&g_mem[i - 1], &g_mem[i]) < 0;
+        if (!sorted) qsort(g_mem, m, sizeof(mem_t), sl_cmp);
+        slots = 2 * m;
+        for (uint64_t i = 0; i < m; i++) {
+            EMIT(RR_K_STR, g_mem[i].off, g_mem[i].len, 0);
+            EMIT(RR_K_SCORE, g_mem[i].score, 0, 0);
+            pay += g_mem[i].len;
+        }
         break;
     }
     default:
         st = RR_E_TYPE;                                                  /* :560-562 */
     }
 done:
-    if (st != RR_OK) { n = 0; pay = 0; }
+    if (st != RR_OK) { n = 0; pay = 0; slots = 0; }
+    else if (b[0] != RR_TYPE_SET_HT && b[0] != RR_TYPE_HASH_HT && b[0] != RR_TYPE_ZSET_SKIPLIST) slots = n;
     v->status = (uint16_t)st;
     *n_elems = n;
+    *n_slots = slots;
     *payload = pay;
     return st;
 }
@@ -356,6 +457,7 @@ typedef struct {
     uint64_t base;        /* in: running base for pass 2 */
     uint64_t count, payload, bad;
     uint64_t *sizes;
+    uint64_t ecap, acap;  /* encode: elem_cap / arena_cap of the flat input */
     int pass;
 } job_t;
 
@@ -363,7 +465,7 @@ static void *dec_worker(void *arg) {
     job_t *j = (job_t *)arg;
     uint64_t base = j->base, cnt = 0, pay = 0, bad = 0;
     for (uint64_t i = j->v0; i < j->v1; i++) {
-        uint64_t o = j->off[i], len = j->off[i + 1] - o, ne, pl;
+        uint64_t o = j->off[i], len = j->off[i + 1] - o, ne, ns, pl;
         rr_value *v = &j->values[i];
         if (j->pass == 1) {
             uint64_t r = rro_reserve(j->data + o, len);
@@ -371,8 +473,8 @@ static void *dec_worker(void *arg) {
             cnt += r;
         } else {
             uint64_t r = v->elem_base;
-            rro_decode_one(j->data, o, len, v, NULL, &ne, &pl);
-            if (v->status == RR_OK && ne != r) { v->status = RR_E_COUNT; ne = 0; }
+            rro_decode_one(j->data, o, len, v, NULL, &ne, &ns, &pl);
+            if (v->status == RR_OK && ns != r) { v->status = RR_E_COUNT; ne = 0; }
             v->elem_base = (uint32_t)base;
             if (v->status != RR_OK) {
                 /* malformed: its slots are zero-filled (when they fit) and it owns no descriptors */
@@ -381,7 +483,8 @@ static void *dec_worker(void *arg) {
             } else if (base + r > j->cap) {
                 v->status = RR_E_CAPACITY;                 /* keeps its count, writes nothing */
             } else {
-                rro_decode_one(j->data, o, len, v, j->elems + base, &ne, &pl);
+                rro_decode_one(j->data, o, len, v, j->elems + base, &ne, &ns, &pl);
+                if (ne < r) memset(j->elems + base + ne, 0, sizeof(rr_elem) * (r - ne));   /* SET_HT dedup */
                 pay += pl;
             }
             v->n_elems = (uint32_t)ne;
@@ -452,20 +555,26 @@ static int fits_width(int64_t x, unsigned w) {
     return x >= INT16_MIN && x <= INT16_MAX;
 }
 
-/* serObject rock_serdes.c:512-535 sizes. */
-uint64_t rro_encode_size(const rr_value *v, const rr_elem *el, int *status) {
+/* serObject rock_serdes.c:512-535 sizes.  A value is unencodable (RR_E_ENCODE, size 0) when
+ * its status is not RR_OK, its descriptor range passes elem_cap, a payload it references
+ * passes arena_cap, or its descriptors do not have the kinds its type needs. */
+#define ARENA_OK(E) ((E).data <= arena_cap && (uint64_t)(E).len <= arena_cap - (E).data)
+uint64_t rro_encode_size(const rr_value *v, const rr_elem *elems, uint64_t elem_cap, uint64_t arena_cap,
+                         int *status) {
     uint64_t n = v->n_elems, s = 5;
     *status = RR_OK;
+    if (v->status != RR_OK || (uint64_t)v->elem_base + n > elem_cap) goto bad;
+    const rr_elem *el = elems + v->elem_base;
     switch (v->type) {
     case RR_TYPE_STRING:
         if (n != 1) goto bad;
         if (v->enc == RR_ENC_INT) { if (el[0].kind != RR_K_INT) goto bad; return 14; }
-        if ((v->enc != RR_ENC_RAW && v->enc != RR_ENC_EMBSTR) || el[0].kind != RR_K_STR) goto bad;
+        if ((v->enc != RR_ENC_RAW && v->enc != RR_ENC_EMBSTR) || el[0].kind != RR_K_STR || !ARENA_OK(el[0])) goto bad;
         return 6 + el[0].len;
     case RR_TYPE_LIST_QUICKLIST:
         for (uint64_t i = 0; i < n; i++) {
             if (el[i].kind == RR_K_INT) s += 4 + dec_len((long long)el[i].data);
-            else if (el[i].kind == RR_K_STR) s += 4 + el[i].len;
+            else if (el[i].kind == RR_K_STR && ARENA_OK(el[i])) s += 4 + el[i].len;
             else goto bad;
         }
         return s;
@@ -478,17 +587,20 @@ uint64_t rro_encode_size(const rr_value *v, const rr_elem *el, int *status) {
     case RR_TYPE_HASH_HT:
         if (v->type == RR_TYPE_HASH_HT && (n & 1)) goto bad;
         s += 8;
-        for (uint64_t i = 0; i < n; i++) { if (el[i].kind != RR_K_STR) goto bad; s += 8 + el[i].len; }
+        for (uint64_t i = 0; i < n; i++) {
+            if (el[i].kind != RR_K_STR || !ARENA_OK(el[i])) goto bad;
+            s += 8 + el[i].len;
+        }
         return s;
     case RR_TYPE_HASH_ZIPLIST:
     case RR_TYPE_ZSET_ZIPLIST:
-        if (n < 1 || el[0].kind != RR_K_ZLRAW) goto bad;
+        if (n < 1 || el[0].kind != RR_K_ZLRAW || !ARENA_OK(el[0])) goto bad;
         return 13 + el[0].len;
     case RR_TYPE_ZSET_SKIPLIST:
         if (n & 1) goto bad;
         s += 8;
         for (uint64_t i = 0; i < n; i += 2) {
-            if (el[i].kind != RR_K_STR || el[i + 1].kind != RR_K_SCORE) goto bad;
+            if (el[i].kind != RR_K_STR || !ARENA_OK(el[i]) || el[i + 1].kind != RR_K_SCORE) goto bad;
             s += 16 + el[i].len;
         }
         return s;
@@ -559,13 +671,13 @@ static void *enc_worker(void *arg) {
         const rr_value *v = &j->values[i];
         int st;
         if (j->pass == 1) {
-            uint64_t s = rro_encode_size(v, j->ielems + v->elem_base, &st);
+            uint64_t s = rro_encode_size(v, j->ielems, j->ecap, j->acap, &st);
             j->sizes[i] = s;
             tot += s;
         } else {
             uint64_t s = j->sizes[i];
             j->ooff[i] = base;
-            rro_encode_size(v, j->ielems + v->elem_base, &st);
+            rro_encode_size(v, j->ielems, j->ecap, j->acap, &st);
             if (st != RR_OK || base + s > j->cap) bad++;
             else {
                 encode_one(v, j->ielems + v->elem_base, j->arena, j->odata + base);
@@ -583,8 +695,9 @@ static void *enc_worker(void *arg) {
     return NULL;
 }
 
-int rro_encode(const rr_value *values, const rr_elem *elems, const uint8_t *arena, uint64_t n,
-               uint8_t *data, uint64_t data_cap, uint64_t *offsets, rr_totals *t, int nthreads) {
+int rro_encode(const rr_value *values, const rr_elem *elems, uint64_t elem_cap, const uint8_t *arena,
+               uint64_t arena_cap, uint64_t n, uint8_t *data, uint64_t data_cap, uint64_t *offsets, rr_totals *t,
+               int nthreads) {
     if (nthreads < 1) nthreads = 1;
     uint64_t *sizes = (uint64_t *)malloc(sizeof(uint64_t) * (n ? n : 1));
     job_t *jobs = (job_t *)calloc((size_t)nthreads, sizeof(job_t));
@@ -599,6 +712,7 @@ int rro_encode(const rr_value *values, const rr_elem *elems, const uint8_t *aren
         jobs[k].v0 = v; jobs[k].v1 = v1; v = v1;
         jobs[k].values = (rr_value *)values; jobs[k].ielems = elems; jobs[k].arena = arena;
         jobs[k].odata = data; jobs[k].ooff = offsets; jobs[k].cap = data_cap; jobs[k].sizes = sizes;
+        jobs[k].ecap = elem_cap; jobs[k].acap = arena_cap;
         jobs[k].pass = 1;
     }
     run_jobs(jobs, nthreads, enc_worker);

@@ -36,9 +36,11 @@ int rro_zip_try_encoding(const uint8_t *s, uint64_t len, long long *v); /* zipli
 int rro_parse_ziplist(const uint8_t *zl, uint64_t L, uint64_t base, rr_elem *out, uint64_t cap,
                       uint64_t *count);
 
-/* Decode blob at data[off, off+len).  Counting mode when out == NULL. */
+/* Decode blob at data[off, off+len).  Counting mode when out == NULL.  *n_slots = descriptors
+ * the blob's members occupy before SET_HT de-duplication (== its reservation when valid);
+ * *n_elems = descriptors the value keeps. */
 int rro_decode_one(const uint8_t *data, uint64_t off, uint64_t len, rr_value *v,
-                   rr_elem *out, uint64_t *n_elems, uint64_t *payload);
+                   rr_elem *out, uint64_t *n_elems, uint64_t *n_slots, uint64_t *payload);
 
 /* Descriptor slots value b[0, L) owns in a decoded batch (== its descriptor count if valid). */
 uint64_t rro_reserve(const uint8_t *b, uint64_t L);
@@ -47,10 +49,13 @@ uint64_t rro_reserve(const uint8_t *b, uint64_t L);
 int rro_decode(const uint8_t *data, const uint64_t *offsets, uint64_t n, rr_value *values,
                rr_elem *elems, uint64_t elem_cap, uint8_t *arena, rr_totals *t, int nthreads);
 
-/* Blob size of one flat value (0 and *status != 0 if it cannot be encoded). */
-uint64_t rro_encode_size(const rr_value *v, const rr_elem *elems, int *status);
-int rro_encode(const rr_value *values, const rr_elem *elems, const uint8_t *arena, uint64_t n,
-               uint8_t *data, uint64_t data_cap, uint64_t *offsets, rr_totals *t, int nthreads);
+/* Blob size of one flat value (0 and *status != 0 if it cannot be encoded); elems is the
+ * batch's descriptor array (elem_cap entries), arena_cap the arena's size. */
+uint64_t rro_encode_size(const rr_value *v, const rr_elem *elems, uint64_t elem_cap, uint64_t arena_cap,
+                         int *status);
+int rro_encode(const rr_value *values, const rr_elem *elems, uint64_t elem_cap, const uint8_t *arena,
+               uint64_t arena_cap, uint64_t n, uint8_t *data, uint64_t data_cap, uint64_t *offsets, rr_totals *t,
+               int nthreads);
 
 /* Reference-faithful single-thread mode (rro_faithful.c). Returns 0 on success.
  * decode: blobs -> heap objects (kept alive in an opaque store), then encode them back. */

@@ -155,37 +155,44 @@ static int sdscmp(const sds a, const sds b) {
     if (c) return c;
     return l1 < l2 ? -1 : l1 > l2;
 }
-static zskiplistNode *zslInsert(zskiplist *zsl, double score, sds ele) {
-    zskiplistNode *update[ZSKIPLIST_MAXLEVEL], *x;
-    unsigned long rank[ZSKIPLIST_MAXLEVEL];
-    int i, level;
-    x = zsl->header;
-    for (i = zsl->level - 1; i >= 0; i--) {
-        rank[i] = i == (zsl->level - 1) ? 0 : rank[i + 1];
-        while (x->level[i].forward && (x->level[i].forward->score < score ||
-               (x->level[i].forward->score == score && sdscmp(x->level[i].forward->ele, ele) < 0))) {
-            rank[i] += x->level[i].span;
-            x = x->level[i].forward;
-        }
-        update[i] = x;
+/* (score, ele) of node x sorts before (score, ele): zslInsert's walk predicate */
+static int node_before(const zskiplistNode *x, double score, const sds ele) {
+    return x->score < score || (x->score == score && sdscmp(x->ele, ele) < 0);
+}
+/* zslInsert (t_zset.c:132-180) restated: on every level find the last node before the new key
+ * (and how many level-0 nodes precede it), draw the node's height, splice it in on each of its
+ * levels with the spans split, then fix the backward link.  A NaN score is the assert at
+ * t_zset.c:137: the caller rejects it before calling. */
+static zskiplistNode *zslInsert(zskiplist *sl, double score, sds ele) {
+    zskiplistNode *prev[ZSKIPLIST_MAXLEVEL], *cur = sl->header;
+    unsigned long pos[ZSKIPLIST_MAXLEVEL], walked = 0;
+    for (int lv = sl->level - 1; lv >= 0; lv--) {
+        for (zskiplistNode *nx; (nx = cur->level[lv].forward) != NULL && node_before(nx, score, ele); cur = nx)
+            walked += cur->level[lv].span;
+        prev[lv] = cur;
+        pos[lv] = walked;
     }
-    level = zslRandomLevel();
-    if (level > zsl->level) {
-        for (i = zsl->level; i < level; i++) { rank[i] = 0; update[i] = zsl->header; update[i]->level[i].span = zsl->length; }
-        zsl->level = level;
+    const int h = zslRandomLevel();
+    for (int lv = sl->level; lv < h; lv++) {
+        prev[lv] = sl->header;
+        pos[lv] = 0;
+        sl->header->level[lv].span = sl->length;
     }
-    x = zslCreateNode(level, score, ele);
-    for (i = 0; i < level; i++) {
-        x->level[i].forward = update[i]->level[i].forward;
-        update[i]->level[i].forward = x;
-        x->level[i].span = update[i]->level[i].span - (rank[0] - rank[i]);
-        update[i]->level[i].span = (rank[0] - rank[i]) + 1;
+    if (h > sl->level) sl->level = h;
+    zskiplistNode *node = zslCreateNode(h, score, ele);
+    for (int lv = 0; lv < h; lv++) {
+        const unsigned long gap = pos[0] - pos[lv];
+        node->level[lv].forward = prev[lv]->level[lv].forward;
+        prev[lv]->level[lv].forward = node;
+        node->level[lv].span = prev[lv]->level[lv].span - gap;
+        prev[lv]->level[lv].span = gap + 1;
     }
-    for (i = level; i < zsl->level; i++) update[i]->level[i].span++;
-    x->backward = (update[0] == zsl->header) ? NULL : update[0];
-    if (x->level[0].forward) x->level[0].forward->backward = x; else zsl->tail = x;
-    zsl->length++;
-    return x;
+    for (int lv = h; lv < sl->level; lv++) prev[lv]->level[lv].span++;
+    node->backward = prev[0] == sl->header ? NULL : prev[0];
+    if (node->level[0].forward) node->level[0].forward->backward = node;
+    else sl->tail = node;
+    sl->length++;
+    return node;
 }
 static void zslFree(zskiplist *zsl) {
     zskiplistNode *node = zsl->header->level[0].forward, *next;
@@ -316,10 +323,11 @@ static robj *desObject(const uint8_t *b, uint64_t len) {
     case RR_TYPE_SET_INTSET: {
         if (rem < 8) return NULL;
         uint32_t w = L32(s), cnt = L32(s + 4);
-        if (rem - 8 != (uint64_t)w * cnt) return NULL;
+        uint32_t content = w * cnt;                               /* u32 product, rock_serdes.c:268 */
+        if (rem - 8 != (uint64_t)content) return NULL;            /* :274 */
         uint8_t *is = (uint8_t *)malloc(8);                     /* createIntsetObject */
-        is = (uint8_t *)realloc(is, 8 + (size_t)w * cnt);       /* zrealloc */
-        memcpy(is, s, 8 + (size_t)w * cnt);
+        is = (uint8_t *)realloc(is, 8 + (size_t)content);       /* zrealloc */
+        memcpy(is, s, 8 + (size_t)content);
         o = createObject(OBJ_SET, is); o->encoding = ENC_INTSET;
         break;
     }
@@ -342,7 +350,10 @@ static robj *desObject(const uint8_t *b, uint64_t len) {
                 if (vl > rem) return NULL;
                 v = sdsnewlen(s, vl); s += vl; rem -= vl;
             }
-            if (dictAdd(d, k, v)) { sdsfree(k); sdsfree(v); }
+            if (dictAdd(d, k, v)) {
+                sdsfree(k); sdsfree(v);
+                if (hash) return NULL;   /* serverAssert(ret == DICT_OK), rock_serdes.c:399-400 */
+            }                            /* a set ignores the duplicate (rock_serdes.c:297) */
             cnt--;
         }
         if (cnt) return NULL;
@@ -372,6 +383,7 @@ static robj *desObject(const uint8_t *b, uint64_t len) {
             sds e = sdsnewlen(s, l); s += l; rem -= l;
             if (rem < 8) return NULL;
             double sc; memcpy(&sc, s, 8); s += 8; rem -= 8;
+            if (isnan(sc)) return NULL;  /* zslInsert's serverAssert(!isnan(score)), t_zset.c:137 */
             zskiplistNode *zn = zslInsert(zs->zsl, sc, e);
             dictAdd(zs->dict, e, &zn->score);
         }
@@ -434,7 +446,7 @@ static sds serObject(robj *o) {
         uint32_t w = L32(is), cnt = L32(is + 4);
         dst = sdscatlen(dst, is, 4);
         dst = sdscatlen(dst, is + 4, 4);
-        dst = sdscatlen(dst, is + 8, (uint64_t)w * cnt);
+        dst = sdscatlen(dst, is + 8, (uint32_t)(w * cnt));       /* u32 product, rock_serdes.c:224 */
         break;
     }
     case RR_TYPE_SET_HT:

@@ -43,8 +43,10 @@ def expected_flat(fixtures):
         for kind, data, ln, zenc in fx["elems"]:
             d = data + off if kind in (rr.K_STR, rr.K_ZLRAW) else data
             elems.append((d & 0xFFFFFFFFFFFFFFFF, ln, kind, zenc, 0))
-        if v.get("status", 0):   # a malformed value keeps its reserved slots, zero-filled
-            elems.extend([(0, 0, 0, 0, 0)] * v["reserve"])
+        # a malformed value keeps its reserved slots zero-filled; so does the unused tail of a
+        # de-duplicated set
+        used = len(fx["elems"]) if v.get("status", 0) == 0 else 0
+        elems.extend([(0, 0, 0, 0, 0)] * (v.get("reserve", used) - used))
         off += len(blob)
     return values, np.array(elems, dtype=rr.ELEM_DT)
 
