@@ -14,8 +14,10 @@
  *   - return value: RR_API_OK (0) or a negative RR_API_E* code for the whole call;
  *   - per-value status in rr_value.status (0 = OK), counted into rr_totals.n_bad;
  *   - caller-owned buffers; one rr_ctx per host thread; no hidden host synchronisation in the
- *     device entry points (graph-capturable: decode = memset + 4 kernels, encode = memset +
- *     5 kernels, all on the caller's stream).
+ *     device entry points (graph-capturable after rr_ctx_reserve: decode = memset + 5 kernels,
+ *     encode = memset + 5 kernels, all on the caller's stream).  The only wait is when the
+ *     context's scratch must grow: it waits for the context's previous call to finish (an
+ *     event, not a device sync) — and under graph capture it fails instead.
  * Plain C: no HIP or torch types in any signature.  Streams are passed as void* (hipStream_t).
  */
 #ifndef RR_SERDES_H
@@ -34,6 +36,11 @@ extern "C" {
 #define RR_API_EHIP     -2   /* a HIP runtime call failed */
 #define RR_API_ENOMEM   -3   /* device/host allocation failed */
 #define RR_API_ENODEV   -4   /* no usable GPU */
+#define RR_API_EDEVICE  -5   /* the device reported a failure (rr_totals.bytes == UINT64_MAX) */
+
+/* Value indices and descriptor positions are 32-bit: a batch holds fewer than 2^32 - 1 values
+ * (larger n is RR_API_EINVAL) and at most 2^32 - 1 descriptors (later values: RR_E_CAPACITY). */
+#define RR_MAX_VALUES   0xFFFFFFFFull
 
 typedef struct rr_ctx rr_ctx;
 
@@ -55,7 +62,9 @@ typedef struct rr_flat_batch {
     uint64_t  arena_cap;
 } rr_flat_batch;
 
-/* Written by the device at the end of every batch call. */
+/* Written by the device at the end of every batch call.  bytes == UINT64_MAX means the call
+ * failed on the device (a look-back wait was cut off) and its outputs must not be used; the
+ * host entry points return RR_API_EDEVICE then. */
 typedef struct rr_totals {
     uint64_t n_elems;       /* descriptors written (decode) / read (encode) */
     uint64_t bytes;         /* blob bytes read (decode) / written (encode) */
@@ -79,7 +88,11 @@ const char *rr_last_error(void);
 int rr_decode_batch(rr_ctx *ctx, const rr_blob_batch *in, rr_flat_batch *out,
                     rr_totals *d_totals, void *stream);
 /* Encode: writes out->offsets[0..n] and out->data; out->data_cap bounds the bytes written
- * (values that would not fit get RR_E_CAPACITY).  in->values[i].status is ignored. */
+ * (values that would not fit are counted bad and not written).  A value is unencodable —
+ * size 0, counted in rr_totals.n_bad — when its status is not RR_OK, when its descriptors
+ * [elem_base, elem_base + n_elems) pass in->elem_cap, when a payload it references passes
+ * in->arena_cap, or when its descriptor kinds do not fit its type (RR_E_ENCODE rules,
+ * rr_format.h).  Nothing outside [elems, elems + elem_cap) or [arena, arena + arena_cap) is read. */
 int rr_encode_batch(rr_ctx *ctx, const rr_flat_batch *in, rr_blob_batch *out,
                     rr_totals *d_totals, void *stream);
 

@@ -17,6 +17,8 @@ struct rr_ctx {
     hipStream_t stream;          /* used by the host entry points */
     uint64_t *scratch;           /* look-back words + counters */
     uint64_t scratch_words;
+    hipEvent_t scratch_done;     /* recorded after every call's last use of the scratch */
+    int scratch_used;
     /* device staging for host entry points */
     void *d_in, *d_off, *d_vals, *d_elems, *d_arena, *d_out, *d_ooff;
     size_t c_in, c_off, c_vals, c_elems, c_arena, c_out, c_ooff;
@@ -54,6 +56,12 @@ int rr_ctx_create(int device, rr_ctx **out) {
         free(c);
         return fail(RR_API_ENOMEM, "hipMalloc totals");
     }
+    if (hipEventCreateWithFlags(&c->scratch_done, hipEventDisableTiming) != hipSuccess) {
+        hipFree(c->d_totals);
+        hipStreamDestroy(c->stream);
+        free(c);
+        return fail(RR_API_EHIP, "hipEventCreate");
+    }
     *out = c;
     return RR_API_OK;
 }
@@ -68,25 +76,49 @@ void rr_ctx_destroy(rr_ctx *c) {
     dfree(&c->d_elems, &c->c_elems); dfree(&c->d_arena, &c->c_arena); dfree(&c->d_out, &c->c_out);
     dfree(&c->d_ooff, &c->c_ooff);
     if (c->d_totals) hipFree(c->d_totals);
+    hipEventDestroy(c->scratch_done);
     hipStreamDestroy(c->stream);
     free(c);
 }
 
-static int ensure_scratch(rr_ctx *c, uint64_t words) {
+/* Grow the scratch.  Only the previous call's kernels can still be using the old buffer, and
+ * scratch_done marks their end (whatever stream they ran on), so only that wait is needed — no
+ * device-wide synchronisation.  Growing allocates, which a stream under graph capture cannot do:
+ * size the scratch with rr_ctx_reserve before capturing. */
+static int ensure_scratch(rr_ctx *c, uint64_t words, hipStream_t stream) {
     if (c->scratch && words <= c->scratch_words) return RR_API_OK;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (stream && hipStreamIsCapturing(stream, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
+        return fail(RR_API_EINVAL, "scratch too small under graph capture: call rr_ctx_reserve first");
     HIPCHK(hipSetDevice(c->device));
-    if (c->scratch) { HIPCHK(hipDeviceSynchronize()); hipFree(c->scratch); c->scratch = NULL; }
+    if (c->scratch) {
+        if (c->scratch_used) HIPCHK(hipEventSynchronize(c->scratch_done));
+        hipFree(c->scratch);
+        c->scratch = NULL;
+    }
     uint64_t want = words + words / 4 + 64;
     if (hipMalloc((void **)&c->scratch, want * sizeof(uint64_t)) != hipSuccess)
         return fail(RR_API_ENOMEM, "hipMalloc scratch (%llu words)", (unsigned long long)want);
     c->scratch_words = want;
+    c->scratch_used = 0;
+    return RR_API_OK;
+}
+
+/* after a call's launches: remember where its use of the scratch ends (not under capture: the
+ * captured graph replays later, and capture never grows the scratch) */
+static int mark_scratch(rr_ctx *c, hipStream_t stream) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (stream && hipStreamIsCapturing(stream, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
+        return RR_API_OK;
+    HIPCHK(hipEventRecord(c->scratch_done, stream));
+    c->scratch_used = 1;
     return RR_API_OK;
 }
 
 int rr_ctx_reserve(rr_ctx *c, uint64_t n_values, uint64_t n_bytes) {
     if (!c) return fail(RR_API_EINVAL, "ctx is NULL");
     uint64_t a = rr_encode_scratch_words(n_values, (n_bytes + 15) & ~15ull), b = rr_decode_scratch_words((n_bytes + 15) & ~15ull, n_values);
-    return ensure_scratch(c, a > b ? a : b);
+    return ensure_scratch(c, a > b ? a : b, NULL);
 }
 
 
@@ -101,31 +133,31 @@ static int aligned16(const void *p) { return ((uintptr_t)p & 15) == 0; }
 int rr_decode_batch(rr_ctx *c, const rr_blob_batch *in, rr_flat_batch *out, rr_totals *d_totals, void *stream) {
     if (!c || !in || !out) return fail(RR_API_EINVAL, "NULL argument");
     if (out->n != in->n) return fail(RR_API_EINVAL, "out->n != in->n");
-    if (in->n >= (1ull << 37)) return fail(RR_API_EINVAL, "batch too large");
+    if (in->n >= RR_MAX_VALUES) return fail(RR_API_EINVAL, "batch too large (value indices are 32-bit)");
     if (in->n && (!in->data || !in->offsets || !out->values || !out->arena))
         return fail(RR_API_EINVAL, "NULL buffer");
     if (!aligned16(in->data) || !aligned16(out->arena)) return fail(RR_API_EINVAL, "data/arena not 16-byte aligned");
     if (in->data_cap & 15) return fail(RR_API_EINVAL, "data_cap must be a multiple of 16");
     if (out->arena_cap < in->data_cap) return fail(RR_API_EINVAL, "arena_cap < data_cap");
-    int rc = ensure_scratch(c, rr_decode_scratch_words(in->data_cap, in->n));
+    int rc = ensure_scratch(c, rr_decode_scratch_words(in->data_cap, in->n), (hipStream_t)stream);
     if (rc) return rc;
     HIPCHK(rr_launch_decode(in->data, in->offsets, in->n, out->values, out->elems, out->elem_cap, out->arena,
                             c->scratch, in->data_cap, d_totals, (hipStream_t)stream));
-    return RR_API_OK;
+    return mark_scratch(c, (hipStream_t)stream);
 }
 
 int rr_encode_batch(rr_ctx *c, const rr_flat_batch *in, rr_blob_batch *out, rr_totals *d_totals, void *stream) {
     if (!c || !in || !out) return fail(RR_API_EINVAL, "NULL argument");
     if (out->n != in->n) return fail(RR_API_EINVAL, "out->n != in->n");
-    if (in->n >= (1ull << 37)) return fail(RR_API_EINVAL, "batch too large");
+    if (in->n >= RR_MAX_VALUES) return fail(RR_API_EINVAL, "batch too large (value indices are 32-bit)");
     if (!out->offsets) return fail(RR_API_EINVAL, "NULL offsets");
     if (in->n && (!in->values || !out->data)) return fail(RR_API_EINVAL, "NULL buffer");
     if ((uintptr_t)out->data & 15) return fail(RR_API_EINVAL, "out->data must be 16-byte aligned");
-    int rc = ensure_scratch(c, rr_encode_scratch_words(in->n, out->data_cap));
+    int rc = ensure_scratch(c, rr_encode_scratch_words(in->n, out->data_cap), (hipStream_t)stream);
     if (rc) return rc;
-    HIPCHK(rr_launch_encode(in->values, in->elems, in->arena, in->n, out->data, out->data_cap, out->offsets,
-                            c->scratch, d_totals, (hipStream_t)stream));
-    return RR_API_OK;
+    HIPCHK(rr_launch_encode(in->values, in->elems, in->elem_cap, in->arena, in->arena_cap, in->n, out->data,
+                            out->data_cap, out->offsets, c->scratch, d_totals, (hipStream_t)stream));
+    return mark_scratch(c, (hipStream_t)stream);
 }
 
 /* grow a device staging buffer (host entry points only) */
@@ -144,6 +176,7 @@ static int dgrow(void **p, size_t *cap, size_t need) {
 int rr_decode_batch_host(rr_ctx *c, const uint8_t *data, const uint64_t *offsets, uint64_t n, rr_value *values,
                          rr_elem *elems, uint64_t elem_cap, uint8_t *arena, rr_totals *totals) {
     if (!c || !offsets || (n && (!data || !values))) return fail(RR_API_EINVAL, "NULL argument");
+    if (n >= RR_MAX_VALUES) return fail(RR_API_EINVAL, "batch too large (value indices are 32-bit)");
     HIPCHK(hipSetDevice(c->device));
     uint64_t bytes = offsets[n];
     size_t pbytes = (size_t)((bytes + 15) & ~15ull);
@@ -163,6 +196,7 @@ int rr_decode_batch_host(rr_ctx *c, const uint8_t *data, const uint64_t *offsets
     rr_totals t;
     HIPCHK(hipMemcpyAsync(&t, c->d_totals, sizeof t, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
+    if (t.bytes == ~0ull) return fail(RR_API_EDEVICE, "decode: device-side failure (look-back timeout)");
     if (n) HIPCHK(hipMemcpyAsync(values, c->d_vals, n * sizeof(rr_value), hipMemcpyDeviceToHost, c->stream));
     uint64_t ne = t.n_elems < elem_cap ? t.n_elems : elem_cap;
     if (ne && elems) HIPCHK(hipMemcpyAsync(elems, c->d_elems, ne * sizeof(rr_elem), hipMemcpyDeviceToHost, c->stream));
@@ -194,6 +228,7 @@ int rr_encode_batch_host(rr_ctx *c, const rr_value *values, const rr_elem *elems
     HIPCHK(hipMemcpyAsync(&t, c->d_totals, sizeof t, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipMemcpyAsync(offsets, c->d_ooff, (n + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
+    if (t.bytes == ~0ull) return fail(RR_API_EDEVICE, "encode: device-side failure (look-back timeout)");
     uint64_t nb = t.bytes < data_cap ? t.bytes : data_cap;
     if (nb) HIPCHK(hipMemcpyAsync(data, c->d_out, nb, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));

@@ -21,8 +21,9 @@
 
 namespace rr {
 
-// value classes (count_kernel -> decode sort); the decode kernel runs them heaviest first
-constexpr uint32_t C_STR = 0, C_IS = 1, C_LIST = 2, C_HT = 3, C_SL = 4, C_ZL = 5, C_EXACT = 6, C_N = 7;
+// value classes (count_kernel -> decode sort); the decode kernel runs them heaviest first.
+// Sets and hashes are separate classes so a batch knows wave-uniformly which members are keys.
+constexpr uint32_t C_STR = 0, C_IS = 1, C_LIST = 2, C_HT = 3, C_SL = 4, C_ZL = 5, C_EXACT = 6, C_HH = 7, C_N = 8;
 
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 
@@ -319,29 +320,74 @@ __device__ __forceinline__ bool do_list(const Src &R, const Lane &l, bool active
     return fail || k != l.r;
 }
 
+// ---- duplicate keys of hash tables (desSet's dictAdd keeps the first copy, rock_serdes.c:297;
+// desHash asserts there is none, :399-400).  The walk fingerprints every key member (set members,
+// hash fields) of a value with at most HT_FP_KEYS keys into 16 bits and keeps them in a packed
+// register shift register (no LDS: the stage fills it); a repeated fingerprint, or a value with
+// more keys, goes on the fixup list, where fixup_kernel compares the actual bytes.
+// A member's fingerprint hashes its length and the 8 bytes that end it.  For a member shorter
+// than 8 bytes those include the tail of its own length field — a function of the length — so
+// equal members always hash equal, and the bytes come with the read of the next length field.
+constexpr uint32_t HT_FP_KEYS = 16;
+__device__ __forceinline__ uint32_t member_fp16(uint32_t len, uint32_t lo, uint32_t hi) {
+    uint32_t h = (lo ^ __builtin_amdgcn_alignbit(hi, hi, 13) ^ len) * 0x9E3779B1u;
+    h = (h ^ hi ^ (h >> 15)) * 0x85EBCA6Bu;
+    h = (h >> 16) ^ (h & 0xFFFFu);
+    return h == 0xFFFFu ? 0xFFFEu : h;   // 0xFFFF marks an empty slot
+}
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
 // ---- Set / Hash hash tables (rock_serdes.c:248-311, :349-414): u64 count, {u64 len, bytes}*
+// Every step reads 16 bytes at p - 8: the 8 bytes ending the previous member (its fingerprint)
+// and this member's length field.  HASH is wave-uniform (sets and hashes are separate classes),
+// so a hash batch skips the fingerprint work on the steps that end a value, not a field.
 template <class Src>
 __device__ __forceinline__ bool do_ht(const Src &R, const Head &H, const Lane &l, bool active, uint32_t &n,
-                                      uint64_t &pay) {
+                                      uint64_t &pay, bool &fix, const bool hash) {
     const uint64_t cnt = H.u5();
-    uint32_t p = l.q + 13, k = 0;
+#ifndef RR_HT_NOFP
+    const bool chk = active && cnt <= HT_FP_KEYS;
+#else   // timing-only builds (tools/): no fingerprints (duplicates go undetected)
+    const bool chk = false;
+#endif
+    bool dupfp = active && cnt > HT_FP_KEYS;
+    uint32_t p = l.q + 13, k = 0, it = 0, plen = 0;
     const uint32_t end = l.q + l.L;
     bool fail = false, live = active;
-    Raw<2> ra = R.template fetch<2>(p), rb;
-    auto step = [&](const Raw<2> &cur, Raw<2> &nxt) __attribute__((always_inline)) {
-        uint32_t b[2];
+    uint32_t fpr[HT_FP_KEYS / 2];
+#pragma unroll
+    for (uint32_t j = 0; j < HT_FP_KEYS / 2; ++j) fpr[j] = 0xFFFFFFFFu;
+    Raw<4> ra = R.template fetch<4>(p - 8), rb;
+    auto step = [&](const Raw<4> &cur, Raw<4> &nxt) __attribute__((always_inline)) {
+        uint32_t b[4];
         cur.align(b);
         const uint32_t rem = end - p;
-        const uint64_t nx = (uint64_t)p + 8 + b[0];
-        const uint32_t pn = ((nx < end) & (b[1] == 0)) ? (uint32_t)nx : end;
-        nxt = R.template fetch<2>(live ? pn : p);
+        const uint64_t nx = (uint64_t)p + 8 + b[2];
+        const uint32_t pn = ((nx < end) & (b[3] == 0)) ? (uint32_t)nx : end;
+        nxt = R.template fetch<4>((live ? pn : p) - 8);
         __builtin_amdgcn_sched_barrier(0);   // keep the read ahead of the checks and the store
         const bool done = p == end;
-        const bool bad = (rem < 8) | (b[1] != 0) | (b[0] > rem - 8) | (k >= l.r);
+        const bool bad = (rem < 8) | (b[3] != 0) | (b[2] > rem - 8) | (k >= l.r);
         const bool emit = live & !done & !bad;
         fail |= live & !done & bad;
-        put_desc(l.E, emit ? l.slot(k) : NOSLOT, l.B + p + 8, b[0], RR_K_STR, 0);
-        pay += emit ? b[0] : 0;
+        put_desc(l.E, emit ? l.slot(k) : NOSLOT, l.B + p + 8, b[2], RR_K_STR, 0);
+        pay += emit ? b[2] : 0;
+        // the member before p (member it - 1 of every live lane) is a key: fingerprint it, test
+        // it against the earlier keys, shift it in (lanes that stopped walking no longer care)
+        if (it > 0 && (!hash || (it & 1))) {
+            const uint32_t f = member_fp16(plen, b[0], b[1]);
+            const uint32_t pat = f | (f << 16);
+            u16x2 m = __builtin_bit_cast(u16x2, fpr[0] ^ pat);
+#pragma unroll
+            for (uint32_t j = 1; j < HT_FP_KEYS / 2; ++j)
+                m = __builtin_elementwise_min(m, __builtin_bit_cast(u16x2, fpr[j] ^ pat));
+            dupfp |= chk & live & ((m.x == 0) | (m.y == 0));
+#pragma unroll
+            for (uint32_t j = HT_FP_KEYS / 2 - 1; j > 0; --j) fpr[j] = __builtin_amdgcn_alignbit(fpr[j], fpr[j - 1], 16);
+            fpr[0] = (fpr[0] << 16) | f;
+        }
+        plen = b[2];
+        ++it;
         k += emit;
         p = emit ? pn : p;
         live = emit;
@@ -349,11 +395,16 @@ __device__ __forceinline__ bool do_ht(const Src &R, const Head &H, const Lane &l
     };
     RR_PINGPONG(ra, rb, step)
     n = k;
-    const bool cnt_ok = H.type() == RR_TYPE_SET_HT ? (uint64_t)k == cnt : ((k & 1) == 0 && (uint64_t)(k >> 1) == cnt);
+    const bool cnt_ok = !hash ? (uint64_t)k == cnt : ((k & 1) == 0 && (uint64_t)(k >> 1) == cnt);
+    fix = dupfp && k >= (hash ? 4u : 2u);
     return fail || !cnt_ok || k != l.r;
 }
 
 // ---- ZSet skiplist (rock_serdes.c:448-508): u64 count, {u64 len, member, f64 score}*
+// desZset rebuilds a skiplist and serZset writes it tail->head, so the flat form lists the pairs
+// descending by (score, member).  The walk accepts a blob already in that order with all scores
+// distinct (what serZset writes); a NaN score (t_zset.c:137), a tie or an ascent sends the value
+// to the exact parser, which assigns the status or checks ties by member and queues a re-sort.
 template <class Src>
 __device__ __forceinline__ bool do_skiplist(const Src &R, const Head &H, const Lane &l, bool active, uint32_t &n,
                                             uint64_t &pay) {
@@ -361,6 +412,7 @@ __device__ __forceinline__ bool do_skiplist(const Src &R, const Head &H, const L
     uint32_t p = l.q + 13, k = 0;
     const uint32_t end = l.q + l.L;
     bool fail = false, live = active;
+    double prev = __builtin_inf();
     Raw<2> ra = R.template fetch<2>(p), rb;
     auto step = [&](const Raw<2> &cur, Raw<2> &nxt) __attribute__((always_inline)) {
         uint32_t b[2];
@@ -372,12 +424,17 @@ __device__ __forceinline__ bool do_skiplist(const Src &R, const Head &H, const L
         nxt = R.template fetch<2>(live ? pn : p);
         __builtin_amdgcn_sched_barrier(0);   // keep the read ahead of the checks and the store
         const bool done = p == end;
-        const bool bad = (rem < 8) | (k >= l.r) | (!score & ((b[1] != 0) | (b[0] > rem - 8)));
+        const uint64_t bits = (uint64_t)b[0] | ((uint64_t)b[1] << 32);
+        const double sc = __longlong_as_double((long long)bits);
+        // strictly below the previous score (k == 1: below +inf, i.e. not NaN / +inf after none)
+        const bool order = (k == 1) ? !(sc != sc) : (sc < prev);
+        const bool bad = (rem < 8) | (k >= l.r) | (!score & ((b[1] != 0) | (b[0] > rem - 8))) | (score & !order);
         const bool emit = live & !done & !bad;
         fail |= live & !done & bad;
-        put_desc(l.E, emit ? l.slot(k) : NOSLOT, score ? ((uint64_t)b[0] | ((uint64_t)b[1] << 32)) : l.B + p + 8,
-                 score ? 0 : b[0], score ? RR_K_SCORE : RR_K_STR, 0);
+        put_desc(l.E, emit ? l.slot(k) : NOSLOT, score ? bits : l.B + p + 8, score ? 0 : b[0],
+                 score ? RR_K_SCORE : RR_K_STR, 0);
         pay += emit && !score ? b[0] : 0;
+        prev = (emit & score) ? sc : prev;
         k += emit;
         p = emit ? pn : p;
         live = emit;

@@ -139,8 +139,11 @@ constexpr uint32_t LB_GROUP = 64;
 constexpr uint64_t GRP_ONE = 1ull << 48;
 constexpr uint64_t GRP_VAL = GRP_ONE - 1;
 
+// A wait that never ends (a tile that never publishes: a hardware or scheduling fault) is cut
+// after 2^24 sleeps: the call's error word *err is set and the prefix returned is 0 — the host
+// sees rr_totals.bytes == UINT64_MAX (rr_serdes.h) instead of silently wrong offsets.
 __device__ __forceinline__ uint64_t lookback(uint64_t *state, uint64_t *groups, uint32_t tile, uint32_t ntiles,
-                                             uint64_t agg) {
+                                             uint64_t agg, uint64_t *err) {
     const uint32_t lane = lane_id();
     const uint32_t g = tile / LB_GROUP, p = tile % LB_GROUP;
     if (lane == 0) {
@@ -160,7 +163,7 @@ __device__ __forceinline__ uint64_t lookback(uint64_t *state, uint64_t *groups, 
             uint32_t first = inc ? (uint32_t)__builtin_ctzll(inc) : 64u;
             uint64_t upto = first >= 63 ? ~0ull : ((2ull << first) - 1);
             if (empty & upto) {
-                if (++spins > (1u << 24)) return LB_VAL;   // bounded: never hang the GPU
+                if (++spins > (1u << 24)) { lb_store(err, 1); return 0; }   // bounded: never hang the GPU
                 __builtin_amdgcn_s_sleep(1);
                 continue;
             }
@@ -187,7 +190,7 @@ __device__ __forceinline__ uint64_t lookback(uint64_t *state, uint64_t *groups, 
         uint64_t upto_excl = first >= 64 ? ~0ull : ((1ull << first) - 1);   // lanes before the INC lane
         uint64_t incomplete = __ballot(!complete);
         if (incomplete & upto_excl) {
-            if (++spins > (1u << 24)) return LB_VAL;
+            if (++spins > (1u << 24)) { lb_store(err, 1); return 0; }
             __builtin_amdgcn_s_sleep(1);
             continue;
         }

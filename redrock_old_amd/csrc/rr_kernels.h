@@ -20,9 +20,9 @@ extern "C" {
 hipError_t rr_launch_decode(const uint8_t *blob, const uint64_t *offsets, uint64_t n, rr_value *values,
                             rr_elem *elems, uint64_t elem_cap, uint8_t *arena, uint64_t *scratch,
                             uint64_t data_cap, rr_totals *totals, hipStream_t stream);
-hipError_t rr_launch_encode(const rr_value *values, const rr_elem *elems, const uint8_t *arena, uint64_t n,
-                            uint8_t *out, uint64_t cap, uint64_t *offsets, uint64_t *scratch,
-                            rr_totals *totals, hipStream_t stream);
+hipError_t rr_launch_encode(const rr_value *values, const rr_elem *elems, uint64_t elem_cap, const uint8_t *arena,
+                            uint64_t arena_cap, uint64_t n, uint8_t *out, uint64_t cap, uint64_t *offsets,
+                            uint64_t *scratch, rr_totals *totals, hipStream_t stream);
 uint64_t rr_decode_scratch_words(uint64_t data_cap, uint64_t n);
 uint64_t rr_encode_scratch_words(uint64_t n, uint64_t data_cap);
 

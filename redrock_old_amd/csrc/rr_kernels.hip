@@ -29,7 +29,19 @@ struct Parsed {
     uint32_t enc;
     uint64_t n;        // descriptors
     uint64_t payload;  // payload bytes (string / ziplist bytes)
+    bool unsorted;     // EMIT, skiplist: pairs not in serZset's order (descending (score, member))
 };
+
+// sdscmp (sds.c:814-824) of two byte strings
+template <typename P>
+__device__ __forceinline__ int sdscmp_p(P a, uint64_t la, P b, uint64_t lb) {
+    const uint64_t m = la < lb ? la : lb;
+    for (uint64_t x = 0; x < m; ++x) {
+        const uint32_t ca = ld_u8(a + x), cb = ld_u8(b + x);
+        if (ca != cb) return ca < cb ? -1 : 1;
+    }
+    return la < lb ? -1 : la > lb ? 1 : 0;
+}
 
 __device__ __forceinline__ void put_elem(rr_elem *e, uint64_t data, uint32_t len, uint32_t kind, uint32_t zenc) {
     uint4 w;
@@ -125,7 +137,7 @@ __device__ __forceinline__ uint32_t parse_ziplist(P zl, uint64_t L, uint64_t zof
 // desObject rock_serdes.c:538-564 and des* :133-508, on one blob at b (batch offset off).
 template <bool EMIT, typename P>
 __device__ __forceinline__ Parsed parse_value(P b, uint64_t off, uint64_t len, rr_elem *out) {
-    Parsed r{RR_OK, 0, 0, 0};
+    Parsed r{RR_OK, 0, 0, 0, false};
     uint64_t n = 0, pay = 0;
     if (len < 5) { r.status = RR_E_SHORT; return r; }
     uint32_t type = ld_u8(b);
@@ -231,6 +243,9 @@ __device__ __forceinline__ Parsed parse_value(P b, uint64_t off, uint64_t len, r
             uint64_t cnt = ld_u64(b + p);
             p += 8;
             rem -= 8;
+            bool nan = false;
+            double prev = 0.0;
+            uint64_t pm = 0, pl = 0;   // previous member (position in b, length)
             for (uint64_t i = 0; i < cnt; ++i) {
                 if (rem < 8) { st = RR_E_TRUNC; break; }
                 uint64_t l = ld_u64(b + p);
@@ -238,16 +253,29 @@ __device__ __forceinline__ Parsed parse_value(P b, uint64_t off, uint64_t len, r
                 rem -= 8;
                 if (l > rem) { st = RR_E_TRUNC; break; }
                 if (EMIT) put_elem(out + n, off + p, (uint32_t)l, RR_K_STR, 0);
+                const uint64_t mp = p;
                 pay += l;
                 p += l;
                 rem -= l;
                 if (rem < 8) { st = RR_E_TRUNC; break; }
-                if (EMIT) put_elem(out + n + 1, ld_u64(b + p), 0, RR_K_SCORE, 0);
+                const uint64_t bits = ld_u64(b + p);
+                const double sc = __longlong_as_double((long long)bits);
+                nan |= sc != sc;   // zslInsert serverAssert(!isnan(score)), t_zset.c:137
+                if (EMIT) {
+                    put_elem(out + n + 1, bits, 0, RR_K_SCORE, 0);
+                    // serZset's order: descending score, then descending member (equal keys stay)
+                    if (i > 0 && !r.unsorted)
+                        r.unsorted = sc > prev || (sc == prev && sdscmp_p(b + pm, pl, b + mp, l) < 0);
+                }
+                prev = sc;
+                pm = mp;
+                pl = l;
                 n += 2;
                 p += 8;
                 rem -= 8;
             }
             if (st == RR_OK && rem != 0) st = RR_E_COUNT;
+            if (st == RR_OK && nan) st = RR_E_NAN;
             break;
         }
         default:
@@ -276,7 +304,8 @@ __device__ __forceinline__ void tile_stats(uint64_t *stats, uint32_t tile, uint6
 // each folding a slice and adding into *out, which the launcher zeroes first.
 __global__ __launch_bounds__(256) void finalize_kernel(const uint64_t *__restrict__ stats, uint64_t *state,
                                                        uint32_t ntiles, const uint64_t *__restrict__ offsets,
-                                                       uint64_t n, int mode, rr_totals *out) {
+                                                       uint64_t n, int mode, rr_totals *out,
+                                                       const uint64_t *__restrict__ extra, uint64_t *err) {
     __shared__ uint64_t red[3][4];
     uint64_t b = 0, p = 0, c = 0;
     for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < ntiles; t += gridDim.x * blockDim.x) {
@@ -297,23 +326,30 @@ __global__ __launch_bounds__(256) void finalize_kernel(const uint64_t *__restric
         if (tp) atomicAdd((unsigned long long *)&out->payload, (unsigned long long)tp);
         if (tc) atomicAdd((unsigned long long *)&out->n_elems, (unsigned long long)tc);
         if (blockIdx.x == 0) {
+            if (extra) {   // decode: {bad, payload} changes of the fixup pass
+                atomicAdd((unsigned long long *)&out->n_bad, (unsigned long long)extra[0]);
+                atomicAdd((unsigned long long *)&out->payload, (unsigned long long)extra[1]);
+            }
             if (mode == 2) {   // decode: descriptor slots = scanned total, bytes = offsets[n]
                 out->bytes = offsets[n];
                 atomicAdd((unsigned long long *)&out->n_elems, (unsigned long long)state[0]);
             } else
                 out->bytes = mode == 0 ? offsets[n] : (ntiles ? (lb_load(&state[ntiles - 1]) & LB_VAL) : 0);
+            if (err && lb_load(err)) out->bytes = ~0ull;   // device-side failure: outputs invalid
         }
     }
 }
 
 static hipError_t launch_finalize(const uint64_t *stats, uint64_t *state, uint32_t ntiles, const uint64_t *offsets,
-                                  uint64_t n, int mode, rr_totals *out, hipStream_t stream) {
+                                  uint64_t n, int mode, rr_totals *out, hipStream_t stream, uint64_t *err,
+                                  const uint64_t *extra = nullptr) {
     hipError_t e = hipMemsetAsync(out, 0, sizeof(rr_totals), stream);
     if (e != hipSuccess) return e;
     uint32_t blocks = (ntiles + 255) / 256;
     if (blocks > 512) blocks = 512;
     if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL(finalize_kernel, dim3(blocks), dim3(256), 0, stream, stats, state, ntiles, offsets, n, mode, out);
+    hipLaunchKernelGGL(finalize_kernel, dim3(blocks), dim3(256), 0, stream, stats, state, ntiles, offsets, n, mode, out,
+                       extra, err);
     return hipGetLastError();
 }
 
@@ -416,8 +452,9 @@ __device__ __forceinline__ uint32_t classify_g(const uint8_t *b, uint64_t L) {
             return ((w == 2 || w == 4 || w == 8) && L - 13 == w * c) ? C_IS : C_EXACT;
         }
         case RR_TYPE_SET_HT:
-        case RR_TYPE_HASH_HT:
             return L < 13 ? C_EXACT : C_HT;
+        case RR_TYPE_HASH_HT:
+            return L < 13 ? C_EXACT : C_HH;
         case RR_TYPE_ZSET_SKIPLIST:
             return L < 13 ? C_EXACT : C_SL;
         case RR_TYPE_HASH_ZIPLIST:
@@ -511,7 +548,7 @@ __device__ __forceinline__ void reserve_classify(const uint8_t *b, uint64_t L, c
             return;
         }
         case RR_TYPE_SET_HT: { const uint64_t m = (L - 13) / 8; r = u5 < m ? u5 : m; c = C_HT; return; }
-        case RR_TYPE_HASH_HT: { const uint64_t m = (L - 13) / 8; r = u5 > m / 2 ? m : 2 * u5; c = C_HT; return; }
+        case RR_TYPE_HASH_HT: { const uint64_t m = (L - 13) / 8; r = u5 > m / 2 ? m : 2 * u5; c = C_HH; return; }
         case RR_TYPE_ZSET_SKIPLIST: { const uint64_t m = (L - 13) / 16; r = 2 * (u5 < m ? u5 : m); c = C_SL; return; }
         case RR_TYPE_HASH_ZIPLIST:
         case RR_TYPE_ZSET_ZIPLIST: {
@@ -564,7 +601,7 @@ constexpr uint32_t SCAN_PER_THREAD = 16;
 constexpr uint32_t SCAN_TILE = 256 * SCAN_PER_THREAD;
 
 __global__ __launch_bounds__(256) void scan_kernel(uint64_t *__restrict__ counts, uint64_t n, uint64_t *lb,
-                                                   uint32_t ntiles) {
+                                                   uint32_t ntiles, uint64_t *err) {
     __shared__ uint64_t wsum[4];
     __shared__ uint64_t sh_prefix;
     __shared__ uint32_t sh_tile;
@@ -592,7 +629,7 @@ __global__ __launch_bounds__(256) void scan_kernel(uint64_t *__restrict__ counts
         agg += wsum[k];
     }
     if (w == 0) {
-        const uint64_t pre = lookback(state, groups, tile, ntiles, agg);
+        const uint64_t pre = lookback(state, groups, tile, ntiles, agg, err);
         if (lane_id() == 0) sh_prefix = pre;
     }
     __syncthreads();
@@ -620,9 +657,19 @@ struct Acc {
 #else
 #define RR_COLD __forceinline__
 #endif
+// Values whose descriptors need a whole-value pass the walks cannot make (duplicate keys of a
+// hash table, re-sorting a skiplist) are queued for fixup_kernel: fix[0] counts them, their
+// indices follow the FIX_HDR header words (capacity n: a value is queued at most once).
+constexpr uint32_t FIX_HDR = 4;   // [0] queued, [1] error word, [2] bad delta, [3] payload delta
+__device__ __forceinline__ void queue_fixup(uint64_t *fix, uint64_t v) {
+    const uint64_t i = atomicAdd((unsigned long long *)fix, 1ull);
+    reinterpret_cast<uint32_t *>(fix + FIX_HDR)[i] = (uint32_t)v;
+}
+
 __device__ RR_COLD Acc exact_value(const uint8_t *__restrict__ blob, uint64_t v,
                                            const uint64_t *__restrict__ offsets, const uint64_t *__restrict__ ebase,
-                                           rr_value *__restrict__ values, rr_elem *__restrict__ elems, uint64_t cap) {
+                                           rr_value *__restrict__ values, rr_elem *__restrict__ elems, uint64_t cap,
+                                           uint64_t *fix) {
     uint64_t pay = 0;
     const uint64_t o_lo = offsets[v], o_hi = offsets[v + 1];
     const uint64_t eb = ebase[v], r = ebase[v + 1] - eb;
@@ -641,6 +688,9 @@ __device__ RR_COLD Acc exact_value(const uint8_t *__restrict__ blob, uint64_t v,
     } else {
         Parsed e = parse_value<true, const uint8_t *>(b, o_lo, o_hi - o_lo, elems + eb);
         pay += e.payload;
+        const uint32_t t = ld_u8(b);
+        const uint64_t keys = t == RR_TYPE_HASH_HT ? ne / 2 : ne;
+        if (((t == RR_TYPE_SET_HT || t == RR_TYPE_HASH_HT) && keys >= 2) || e.unsorted) queue_fixup(fix, v);
     }
     const uint32_t len = (uint32_t)(o_hi - o_lo);
     put_value(values + v, len ? ld_u8(b) : 0, pr.enc, status, len >= 5 ? ld_u32(b + 1) : 0, (uint32_t)ne,
@@ -649,7 +699,7 @@ __device__ RR_COLD Acc exact_value(const uint8_t *__restrict__ blob, uint64_t v,
 }
 
 // class batch order: heaviest walks first (longest-job-first over the window's waves)
-__constant__ uint32_t CLASS_ORDER[C_N] = {C_ZL, C_SL, C_HT, C_LIST, C_EXACT, C_IS, C_STR};
+__constant__ uint32_t CLASS_ORDER[C_N] = {C_ZL, C_SL, C_HH, C_HT, C_LIST, C_EXACT, C_IS, C_STR};
 
 // One single-class batch: lane < cnt decodes value v (byte offsets relative to the source,
 // whose byte 0 is batch offset B).
@@ -661,8 +711,9 @@ template <class Src>
 __device__ __forceinline__ Acc run_batch(const Src &src, uint32_t c, bool active, uint64_t v, uint64_t B, rsrc_t E,
                                          uint64_t eb0, const uint8_t *__restrict__ blob,
                                          const uint64_t *__restrict__ offsets, const uint64_t *__restrict__ ebase,
-                                         rr_value *__restrict__ values, rr_elem *__restrict__ elems, uint64_t cap) {
-    if (c == C_EXACT) return active ? exact_value(blob, v, offsets, ebase, values, elems, cap) : Acc{0, 0};
+                                         rr_value *__restrict__ values, rr_elem *__restrict__ elems, uint64_t cap,
+                                         uint64_t *fix) {
+    if (c == C_EXACT) return active ? exact_value(blob, v, offsets, ebase, values, elems, cap, fix) : Acc{0, 0};
     uint64_t eb = eb0, r = 0;
     Lane l{};
     l.B = B;
@@ -681,7 +732,7 @@ __device__ __forceinline__ Acc run_batch(const Src &src, uint32_t c, bool active
     src.template get<4>(l.q, H.h);
     uint32_t ne = 1, enc = 0;
     uint64_t vp = 0;   // this value's payload bytes (counted once it is emitted)
-    bool fail = false;
+    bool fail = false, fixup = false;
     if (c == C_STR) {
         if (active) do_string(H, l, vp);
         enc = H.b5();
@@ -691,15 +742,16 @@ __device__ __forceinline__ Acc run_batch(const Src &src, uint32_t c, bool active
         enc = H.f5();
     } else if (c == C_LIST) {
         fail = do_list(src, l, active, ne, vp);
-    } else if (c == C_HT) {
-        fail = do_ht(src, H, l, active, ne, vp);
+    } else if (c == C_HT || c == C_HH) {
+        fail = do_ht(src, H, l, active, ne, vp, fixup, c == C_HH);
     } else if (c == C_SL) {
         fail = do_skiplist(src, H, l, active, ne, vp);
     } else {
         fail = do_ziplist(src, l, active, ne, vp);
     }
     if (!active) return Acc{0, 0};
-    if (fail) return exact_value(blob, v, offsets, ebase, values, elems, cap);
+    if (fail) return exact_value(blob, v, offsets, ebase, values, elems, cap, fix);
+    if (fixup && l.ok) queue_fixup(fix, v);
     put_value(values + v, H.type(), enc, l.ok ? RR_OK : RR_E_CAPACITY, H.lru(), ne, (uint32_t)eb);
     return Acc{l.ok ? 0u : 1u, l.ok ? vp : 0};
 }
@@ -709,8 +761,9 @@ __device__ __forceinline__ Acc run_batch(const Src &src, uint32_t c, bool active
 __device__ RR_COLD Acc run_batch_g(const GlbSrc &src, uint32_t c, bool active, uint64_t v, uint64_t B, rsrc_t E,
                                    uint64_t eb0, const uint8_t *__restrict__ blob,
                                    const uint64_t *__restrict__ offsets, const uint64_t *__restrict__ ebase,
-                                   rr_value *__restrict__ values, rr_elem *__restrict__ elems, uint64_t cap) {
-    return run_batch(src, c, active, v, B, E, eb0, blob, offsets, ebase, values, elems, cap);
+                                   rr_value *__restrict__ values, rr_elem *__restrict__ elems, uint64_t cap,
+                                   uint64_t *fix) {
+    return run_batch(src, c, active, v, B, E, eb0, blob, offsets, ebase, values, elems, cap, fix);
 }
 
 // Workgroup per byte WINDOW of W bytes: window t owns the values whose first byte lies in
@@ -752,7 +805,12 @@ static_assert(DEC_BL >= 1 && DEC_BL <= RR_WAVE, "batch lanes");
 #else
 #define PROBE_OR_LATE(...)
 #endif
-#ifdef RR_DEC_WPE   // tuning: ask the register allocator for this many waves per SIMD
+// Two 512-thread workgroups per CU = 4 waves per SIMD, so at most 128 VGPRs: the allocator is
+// told so (left to itself it takes 137 for the hash-table walk and the CU holds one workgroup).
+#ifndef RR_DEC_WPE
+#define RR_DEC_WPE 4
+#endif
+#if RR_DEC_WPE > 0
 #define DEC_WPE_ATTR __attribute__((amdgpu_waves_per_eu(RR_DEC_WPE)))
 #else
 #define DEC_WPE_ATTR
@@ -765,7 +823,8 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
                                                               const uint64_t *__restrict__ ebase,
                                                               rr_value *__restrict__ values,
                                                               rr_elem *__restrict__ elems, uint64_t elem_cap,
-                                                              uint8_t *__restrict__ arena, uint64_t *__restrict__ stats) {
+                                                              uint8_t *__restrict__ arena, uint64_t *__restrict__ stats,
+                                                              uint64_t *fix) {
     constexpr uint32_t NT = NW * RR_WAVE, STAGE = W + SLACK;
     static_assert(PMAX % NT == 0 && W % 16 == 0 && SLACK % 16 == 0, "tile shape");
     __shared__ __attribute__((aligned(16))) uint8_t stage[STAGE + 64];
@@ -938,14 +997,15 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
             PROBE(const uint64_t tb0 = __builtin_amdgcn_s_memtime();)
             const bool active = lane < cnt;
             const uint64_t v = c0 + (active ? perm[first + lane] : 0u);
-            const Acc a = staged ? run_batch(lsrc, c, active, v, S0, E, eb0, blob, offsets, ebase, values, elems, cap)
-                                 : run_batch_g(gsrc, c, active, v, S0, E, eb0, blob, offsets, ebase, values, elems, cap);
+            const Acc a = staged ? run_batch(lsrc, c, active, v, S0, E, eb0, blob, offsets, ebase, values, elems, cap, fix)
+                                 : run_batch_g(gsrc, c, active, v, S0, E, eb0, blob, offsets, ebase, values, elems, cap,
+                                               fix);
             bad += a.bad;
             pay += a.pay;
             PROBE(if (lane == 0) {
                 atomicAdd((unsigned long long *)&prb[3 + c], (unsigned long long)(__builtin_amdgcn_s_memtime() - tb0));
-                atomicAdd((unsigned long long *)&prb[10 + c], 1ull);
-                atomicAdd((unsigned long long *)&prb[17 + c], (unsigned long long)cnt);
+                atomicAdd((unsigned long long *)&prb[3 + C_N + c], 1ull);
+                atomicAdd((unsigned long long *)&prb[3 + 2 * C_N + c], (unsigned long long)cnt);
             })
         }
     }
@@ -990,16 +1050,9 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
         stats[3 * (uint64_t)tile + 0] = tb;
         stats[3 * (uint64_t)tile + 1] = tp;
         stats[3 * (uint64_t)tile + 2] = 0;
-        PROBE(prb[0] = pt1 - pt0; prb[1] = pt2 - pt1; prb[2] = __builtin_amdgcn_s_memtime() - pt2; prb[24] = v_hi - v_lo;
-              prb[25] = staged; if (g_probe) for (uint32_t i = 0; i < PROBE_WORDS; ++i) g_probe[(uint64_t)tile * PROBE_WORDS + i] = prb[i];)
+        PROBE(prb[0] = pt1 - pt0; prb[1] = pt2 - pt1; prb[2] = __builtin_amdgcn_s_memtime() - pt2; prb[28] = v_hi - v_lo;
+              prb[29] = staged; if (g_probe) for (uint32_t i = 0; i < PROBE_WORDS; ++i) g_probe[(uint64_t)tile * PROBE_WORDS + i] = prb[i];)
     }
-}
-
-// ---------------------------------------------------------------------------------------- encode
-__device__ __forceinline__ bool fits_width(int64_t x, uint32_t w) {
-    if (w == 8) return true;
-    if (w == 4) return x >= INT32_MIN && x <= INT32_MAX;
-    return x >= INT16_MIN && x <= INT16_MAX;
 }
 
 struct ElemV {
@@ -1011,6 +1064,221 @@ __device__ __forceinline__ ElemV get_elem(const rr_elem *e) {
     uint4 w = *reinterpret_cast<const uint4 *>(e);
     return ElemV{(uint64_t)w.x | ((uint64_t)w.y << 32), w.z, w.w & 0xFF};
 }
+
+template <uint32_t NT>
+__device__ __forceinline__ uint64_t block_excl_scan(uint64_t x, uint64_t *wsum, uint64_t &total) {
+    const uint64_t incl = wave_incl_scan(x);
+    const uint32_t wv = threadIdx.x / RR_WAVE;
+    if (lane_id() == RR_WAVE - 1) wsum[wv] = incl;
+    lds_barrier();
+    uint64_t pre = 0, t = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < NT / RR_WAVE; ++k) {
+        const uint64_t s = wsum[k];
+        pre += k < wv ? s : 0;
+        t += s;
+    }
+    total = t;
+    return pre + incl - x;
+}
+
+// ---- K4: fixup of queued values ----------------------------------------------------------
+// A workgroup per queued value (atomic ticket over the list the walks filled):
+//   SET_HT / HASH_HT  exact duplicate-key test — fingerprints of (length, first and last 8
+//                     bytes) in an LDS open-addressing table, byte comparison on a fingerprint
+//                     match; a value with more keys than fit runs in several passes, each over
+//                     one residue class of the fingerprints.  A hash with a repeated field gets
+//                     RR_E_DUP (desHash's serverAssert, rock_serdes.c:399-400); a set keeps the
+//                     first copy of each member (desSet's dictAdd, :297): later copies are marked
+//                     and the descriptors compacted in place, the freed tail slots zeroed.
+//   ZSET_SKIPLIST     pairs re-sorted in place into serZset's order (descending score, then
+//                     member, equal keys in blob order — the skiplist desZset builds, t_zset.c:
+//                     132-180) by a bitonic network over the descriptor pairs in global memory.
+// Totals changes go to fix[2] (bad values) / fix[3] (payload, two's complement), folded by the
+// finalize kernel.  Only values the walks could not clear arrive here: none in a batch of
+// serObject output whose hash tables hold at most HT_FP_KEYS keys, barring 16-bit fingerprint
+// collisions.
+constexpr uint32_t FIX_NT = 256, FIX_TAB = 8192, FIX_TAB_BITS = 13, FIX_PASS_KEYS = 2048;
+
+// 32-bit fingerprint of a member: length, first and last 8 bytes (bytes of the member only)
+__device__ __forceinline__ uint32_t member_fp(const uint8_t *__restrict__ blob, uint64_t off, uint32_t len) {
+    uint64_t a = 0, z = 0;
+    if (len >= 8) {
+        __builtin_memcpy(&a, blob + off, 8);
+        __builtin_memcpy(&z, blob + off + len - 8, 8);
+    } else {
+        for (uint32_t i = 0; i < len; ++i) a |= (uint64_t)blob[off + i] << (8 * i);
+    }
+    uint64_t h = (a ^ 0x9E3779B97F4A7C15ull) * 0xBF58476D1CE4E5B9ull;
+    h = (h ^ (h >> 31) ^ z ^ ((uint64_t)len << 32)) * 0x94D049BB133111EBull;
+    return (uint32_t)(h ^ (h >> 32));
+}
+__device__ __forceinline__ bool bytes_equal(const uint8_t *__restrict__ blob, uint64_t a, uint64_t b, uint32_t len) {
+    uint32_t i = 0;
+    for (; i + 8 <= len; i += 8) {
+        uint64_t x, y;
+        __builtin_memcpy(&x, blob + a + i, 8);
+        __builtin_memcpy(&y, blob + b + i, 8);
+        if (x != y) return false;
+    }
+    for (; i < len; ++i)
+        if (blob[a + i] != blob[b + i]) return false;
+    return true;
+}
+
+// pair a sorts before pair b in serZset's order
+__device__ __forceinline__ bool pair_before(const uint8_t *__restrict__ blob, const uint4 &am, uint64_t as,
+                                            const uint4 &bm, uint64_t bs) {
+    const double sa = __longlong_as_double((long long)as), sb = __longlong_as_double((long long)bs);
+    if (sa != sb) return sa > sb;
+    const uint64_t oa = (uint64_t)am.x | ((uint64_t)am.y << 32), ob = (uint64_t)bm.x | ((uint64_t)bm.y << 32);
+    const int c = sdscmp_p(blob + oa, am.z, blob + ob, bm.z);
+    if (c) return c > 0;
+    return oa < ob;   // equal keys: blob order (the member's arena offset is its blob offset)
+}
+
+__device__ void fix_sort_skiplist(const uint8_t *__restrict__ blob, rr_elem *__restrict__ el, uint32_t np) {
+    uint4 *P = reinterpret_cast<uint4 *>(el);   // pair i = P[2i] (member), P[2i + 1] (score)
+    uint32_t m = 1;
+    while (m < np) m <<= 1;
+    // bitonic network with every comparator ascending (first step of each merge compares
+    // mirrored positions): positions >= np act as +infinity and are never touched
+    for (uint32_t k = 2; k <= m; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t t = threadIdx.x; t < m / 2; t += FIX_NT) {
+                uint32_t lo, hi;
+                if (j == k >> 1) {
+                    const uint32_t blk = t / j, o = t % j;
+                    lo = blk * k + o;
+                    hi = blk * k + k - 1 - o;
+                } else {
+                    const uint32_t blk = t / j, o = t % j;
+                    lo = blk * 2 * j + o;
+                    hi = lo + j;
+                }
+                if (hi >= np) continue;
+                const uint4 am = P[2 * lo], as = P[2 * lo + 1], bm = P[2 * hi], bs = P[2 * hi + 1];
+                const uint64_t sa = (uint64_t)as.x | ((uint64_t)as.y << 32), sb = (uint64_t)bs.x | ((uint64_t)bs.y << 32);
+                if (pair_before(blob, bm, sb, am, sa)) {
+                    P[2 * lo] = bm; P[2 * lo + 1] = bs;
+                    P[2 * hi] = am; P[2 * hi + 1] = as;
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+__global__ __launch_bounds__(FIX_NT) void fixup_kernel(const uint8_t *__restrict__ blob, uint64_t *fix,
+                                                       rr_value *__restrict__ values, rr_elem *__restrict__ elems) {
+    __shared__ unsigned long long tab[FIX_TAB];
+    __shared__ uint64_t wsum[FIX_NT / RR_WAVE];
+    __shared__ uint32_t sh_flag;   // bit 0: a duplicate key, bit 1: a pass overflowed the table
+    const uint32_t tid = threadIdx.x;
+    const uint64_t nq = fix[0];
+    const uint32_t *list = reinterpret_cast<const uint32_t *>(fix + FIX_HDR);
+    // queued values are rare (none in serObject output with small hash tables): a static
+    // stride over the queue, no ticket atomics on an empty one
+    for (uint64_t t = blockIdx.x; t < nq; t += gridDim.x) {
+        if (tid == 0) sh_flag = 0;
+        __syncthreads();
+        const uint32_t v = list[t];
+        const uint4 rv = reinterpret_cast<const uint4 *>(values)[v];
+        const uint32_t type = rv.x & 0xFF, n = rv.z;
+        rr_elem *el = elems + rv.w;
+        if (type == RR_TYPE_ZSET_SKIPLIST) {
+            fix_sort_skiplist(blob, el, n / 2);
+        } else {
+            const uint32_t per = type == RR_TYPE_SET_HT ? 1 : 2, nk = n / per;
+            uint32_t K = (nk + FIX_PASS_KEYS - 1) / FIX_PASS_KEYS;
+            for (;;) {
+                for (uint32_t r = 0; r < K; ++r) {
+                    for (uint32_t j = tid; j < FIX_TAB; j += FIX_NT) tab[j] = 0;
+                    __syncthreads();
+                    for (uint32_t i = tid; i < nk; i += FIX_NT) {
+                        const ElemV e = get_elem(el + (uint64_t)i * per);
+                        const uint32_t fp = member_fp(blob, e.data, e.len);
+                        if (fp % K != r) continue;
+                        const unsigned long long ent = ((unsigned long long)fp << 32) | (i + 1u);
+                        uint32_t h = (fp * 0x9E3779B1u) >> (32 - FIX_TAB_BITS), probes = 0;
+                        for (;;) {
+                            unsigned long long cur = tab[h];
+                            if (cur == 0) {
+                                cur = atomicCAS(&tab[h], 0ull, ent);
+                                if (cur == 0) break;   // first of its key so far
+                            }
+                            if ((uint32_t)(cur >> 32) == fp) {
+                                const uint32_t j = (uint32_t)cur - 1u;
+                                const ElemV o = get_elem(el + (uint64_t)j * per);
+                                if (o.len == e.len && bytes_equal(blob, o.data, e.data, e.len)) {
+                                    uint32_t later = i;
+                                    if (i < j) {   // this copy comes first: it takes the slot
+                                        if (atomicCAS(&tab[h], cur, ent) != cur) continue;
+                                        later = j;
+                                    }
+                                    // mark the later copy (rsv = 1) for compaction
+                                    reinterpret_cast<uint16_t *>(el + (uint64_t)later * per)[7] = 1;
+                                    atomicOr(&sh_flag, 1u);
+                                    break;
+                                }
+                            }
+                            h = (h + 1) & (FIX_TAB - 1);
+                            if (++probes == FIX_TAB) { atomicOr(&sh_flag, 2u); break; }
+                        }
+                    }
+                    __syncthreads();
+                    if (sh_flag & 2) break;
+                }
+                if (!(sh_flag & 2)) break;
+                K *= 2;   // a residue class overflowed the table: finer classes (marks stay valid)
+                __syncthreads();
+                if (tid == 0) sh_flag &= ~2u;
+                __syncthreads();
+            }
+            if (sh_flag & 1) {
+                // compact the kept descriptors forward (a chunk is read before it is written,
+                // and writes never pass the chunk's own positions), zero the freed tail
+                uint64_t kept = 0, dropped = 0;
+                for (uint32_t c0 = 0; c0 < n; c0 += FIX_NT) {
+                    const uint32_t i = c0 + tid;
+                    uint4 d = make_uint4(0, 0, 0, 0);
+                    if (i < n) d = reinterpret_cast<const uint4 *>(el)[i];
+                    const bool keep = i < n && (per == 2 || (d.w >> 16) == 0);
+                    uint64_t tot;
+                    const uint64_t pos = block_excl_scan<FIX_NT>(keep ? 1u : 0u, wsum, tot);
+                    dropped += i < n && !keep ? d.z : 0;
+                    __syncthreads();
+                    if (keep && per == 1) reinterpret_cast<uint4 *>(el)[kept + pos] = d;
+                    if (per == 2 && i < n) dropped += d.z;   // a hash with a repeated field loses all
+                    kept += tot;
+                    __syncthreads();
+                }
+                const uint32_t nk2 = per == 2 ? 0u : (uint32_t)kept;
+                for (uint32_t i = nk2 + tid; i < n; i += FIX_NT) reinterpret_cast<uint4 *>(el)[i] = make_uint4(0, 0, 0, 0);
+                dropped = wave_sum(dropped);
+                if (lane_id() == 0 && dropped) atomicAdd((unsigned long long *)&fix[3], (unsigned long long)(0ull - dropped));
+                if (tid == 0) {
+                    uint4 w = rv;
+                    w.z = nk2;
+                    if (per == 2) {
+                        w.x = (rv.x & 0xFFFFu) | ((uint32_t)RR_E_DUP << 16);
+                        atomicAdd((unsigned long long *)&fix[2], 1ull);
+                    }
+                    reinterpret_cast<uint4 *>(values)[v] = w;
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------------------- encode
+__device__ __forceinline__ bool fits_width(int64_t x, uint32_t w) {
+    if (w == 8) return true;
+    if (w == 4) return x >= INT32_MIN && x <= INT32_MAX;
+    return x >= INT16_MIN && x <= INT16_MAX;
+}
+
 
 // Decimal digits of an unsigned magnitude (sdsll2str's length without the sign): compares,
 // no divisions.
@@ -1035,27 +1303,33 @@ struct ElemCost {
     uint64_t bytes, pay;
     bool bad;
 };
-__device__ __forceinline__ ElemCost elem_cost(uint32_t type, uint32_t enc, uint64_t i, const ElemV &e) {
+// a STR / ZLRAW descriptor's payload lies inside the caller's arena
+__device__ __forceinline__ bool in_arena(const ElemV &e, uint64_t acap) { return e.data <= acap && e.len <= acap - e.data; }
+__device__ __forceinline__ ElemCost elem_cost(uint32_t type, uint32_t enc, uint64_t i, const ElemV &e, uint64_t acap) {
     switch (type) {
         case RR_TYPE_LIST_QUICKLIST:
             if (e.kind == RR_K_INT) return {4 + (uint64_t)sdec_len((int64_t)e.data), 0, false};
-            return {4 + (uint64_t)e.len, e.len, e.kind != RR_K_STR};
+            return {4 + (uint64_t)e.len, e.len, e.kind != RR_K_STR || !in_arena(e, acap)};
         case RR_TYPE_SET_INTSET:
             return {enc, 0, e.kind != RR_K_INT || !fits_width((int64_t)e.data, enc)};
         case RR_TYPE_ZSET_SKIPLIST:
             if (i & 1) return {8, 0, e.kind != RR_K_SCORE};
-            return {8 + (uint64_t)e.len, e.len, e.kind != RR_K_STR};
+            return {8 + (uint64_t)e.len, e.len, e.kind != RR_K_STR || !in_arena(e, acap)};
         default:   // SET_HT / HASH_HT members
-            return {8 + (uint64_t)e.len, e.len, e.kind != RR_K_STR};
+            return {8 + (uint64_t)e.len, e.len, e.kind != RR_K_STR || !in_arena(e, acap)};
     }
 }
 
-// serObject rock_serdes.c:512-535: blob size of one flat value, 0 + status if unencodable.
-// Descriptors are read four at a time (independent 16-byte loads in flight per lane).
-__device__ uint64_t encode_size(uint32_t type, uint32_t enc, uint64_t n, const rr_elem *el, uint32_t &st,
-                                uint64_t &pay) {
+// serObject rock_serdes.c:512-535: blob size of one flat value, 0 + status if unencodable:
+// a value whose status is not RR_OK, whose descriptor range passes elem_cap or whose payloads
+// pass arena_cap is never read further (RR_E_ENCODE).  Descriptors are read four at a time
+// (independent 16-byte loads in flight per lane).
+__device__ uint64_t encode_size(uint32_t type, uint32_t enc, uint32_t vstatus, uint64_t eb, uint64_t n,
+                                const rr_elem *elems, uint64_t ecap, uint64_t acap, uint32_t &st, uint64_t &pay) {
     st = RR_OK;
     pay = 0;
+    const rr_elem *el = elems + eb;
+    if (vstatus != RR_OK || eb + n > ecap) type = 0xFF;   // falls to the unencodable default
     switch (type) {
         case RR_TYPE_STRING: {
             if (n != 1) break;
@@ -1064,7 +1338,7 @@ __device__ uint64_t encode_size(uint32_t type, uint32_t enc, uint64_t n, const r
                 if (e.kind != RR_K_INT) break;
                 return 14;
             }
-            if ((enc != RR_ENC_RAW && enc != RR_ENC_EMBSTR) || e.kind != RR_K_STR) break;
+            if ((enc != RR_ENC_RAW && enc != RR_ENC_EMBSTR) || e.kind != RR_K_STR || !in_arena(e, acap)) break;
             pay = e.len;
             return 6 + (uint64_t)e.len;
         }
@@ -1072,7 +1346,7 @@ __device__ uint64_t encode_size(uint32_t type, uint32_t enc, uint64_t n, const r
         case RR_TYPE_ZSET_ZIPLIST: {
             if (n < 1) break;
             ElemV e = get_elem(el);
-            if (e.kind != RR_K_ZLRAW) break;
+            if (e.kind != RR_K_ZLRAW || !in_arena(e, acap)) break;
             pay = e.len;
             return 13 + (uint64_t)e.len;
         }
@@ -1093,7 +1367,7 @@ __device__ uint64_t encode_size(uint32_t type, uint32_t enc, uint64_t n, const r
 #pragma unroll
                 for (uint32_t k = 0; k < 4; ++k) {
                     if (i + k < n) {
-                        const ElemCost c = elem_cost(type, enc, i + k, e[k]);
+                        const ElemCost c = elem_cost(type, enc, i + k, e[k], acap);
                         sz += c.bytes;
                         p += c.pay;
                         bad |= c.bad;
@@ -1129,6 +1403,7 @@ __device__ uint64_t encode_size(uint32_t type, uint32_t enc, uint64_t n, const r
 // ---- E1: blob size per value -----------------------------------------------------------
 __global__ __launch_bounds__(256) void enc_size_kernel(const rr_value *__restrict__ values,
                                                        const rr_elem *__restrict__ elems, uint64_t n,
+                                                       uint64_t ecap, uint64_t acap,
                                                        uint64_t *__restrict__ sizes, uint64_t *__restrict__ stats) {
     __shared__ uint64_t red[3][4];
     const uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1137,7 +1412,7 @@ __global__ __launch_bounds__(256) void enc_size_kernel(const rr_value *__restric
         const uint4 w = reinterpret_cast<const uint4 *>(values)[v];
         uint32_t st;
         ne = w.z;
-        size = encode_size(w.x & 0xFF, (w.x >> 8) & 0xFF, ne, elems + w.w, st, pay);
+        size = encode_size(w.x & 0xFF, (w.x >> 8) & 0xFF, w.x >> 16, w.w, ne, elems, ecap, acap, st, pay);
         bad = st != RR_OK;
         sizes[v] = size;
     }
@@ -1162,6 +1437,7 @@ __global__ __launch_bounds__(256) void enc_size_kernel(const rr_value *__restric
 template <uint32_t W>
 __global__ __launch_bounds__(256) void enc_index_kernel(const rr_value *__restrict__ values,
                                                         const rr_elem *__restrict__ elems, uint64_t n,
+                                                        uint64_t ecap, uint64_t acap,
                                                         const uint64_t *__restrict__ offsets, uint64_t cap,
                                                         uint32_t *__restrict__ fv, uint64_t nwin,
                                                         uint64_t *__restrict__ stats) {
@@ -1177,7 +1453,7 @@ __global__ __launch_bounds__(256) void enc_index_kernel(const rr_value *__restri
             if (b > cap) {
                 const uint4 x = reinterpret_cast<const uint4 *>(values)[v];
                 uint32_t st;
-                encode_size(x.x & 0xFF, (x.x >> 8) & 0xFF, x.z, elems + x.w, st, pay);
+                encode_size(x.x & 0xFF, (x.x >> 8) & 0xFF, x.x >> 16, x.w, x.z, elems, ecap, acap, st, pay);
                 bad = 1;
                 pay = 0ull - pay;
             }
@@ -1345,22 +1621,6 @@ struct Img {
 // Copy-queue entry: arena offset (40 bits) | image offset << 40 (16 bits) | (len - 1) << 56.
 constexpr uint64_t JQ_SRC = (1ull << 40) - 1;
 
-template <uint32_t NT>
-__device__ __forceinline__ uint64_t block_excl_scan(uint64_t x, uint64_t *wsum, uint64_t &total) {
-    const uint64_t incl = wave_incl_scan(x);
-    const uint32_t wv = threadIdx.x / RR_WAVE;
-    if (lane_id() == RR_WAVE - 1) wsum[wv] = incl;
-    lds_barrier();
-    uint64_t pre = 0, t = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < NT / RR_WAVE; ++k) {
-        const uint64_t s = wsum[k];
-        pre += k < wv ? s : 0;
-        t += s;
-    }
-    total = t;
-    return pre + incl - x;
-}
 
 template <uint32_t W, uint32_t NT, uint32_t JCAP>
 __global__ __launch_bounds__(NT) void enc_emit_kernel(const rr_value *__restrict__ values,
@@ -1619,12 +1879,14 @@ static uint64_t scan_tiles(uint64_t n) { return (n + SCAN_TILE - 1) / SCAN_TILE;
 // offsets[n] own no values and copy nothing
 static uint64_t dec_windows(uint64_t data_cap) { return data_cap / DEC_W + 1; }
 
-// Decode scratch (uint64 words): [HDR] [scan: ticket, look-back state + groups]
-// [counts -> elem_base, n+1] [window stats, 3 per window] [first_val u32, nwin+1]
-// [class bytes, n].
+// Decode scratch (uint64 words): [HDR] [scan: ticket, look-back state + groups] [fixup header,
+// then its u32 list of up to n values] [counts -> elem_base, n+1] [window stats, 3 per window]
+// [first_val u32, nwin+1] [class bytes, n].  The look-back words and the fixup header are
+// zeroed by one memset per call.
 extern "C" uint64_t rr_decode_scratch_words(uint64_t data_cap, uint64_t n) {
     const uint64_t st = scan_tiles(n), nw = dec_windows(data_cap);
-    return RR_SCRATCH_HDR + 1 + st + (st + LB_GROUP - 1) / LB_GROUP + (n + 1) + 3 * nw + (nw + 2) / 2 + (n + 7) / 8 + 2;
+    return RR_SCRATCH_HDR + 1 + st + (st + LB_GROUP - 1) / LB_GROUP + FIX_HDR + (n + 2) / 2 + (n + 1) + 3 * nw +
+           (nw + 2) / 2 + (n + 7) / 8 + 2;
 }
 
 extern "C" hipError_t rr_launch_decode(const uint8_t *blob, const uint64_t *offsets, uint64_t n, rr_value *values,
@@ -1633,23 +1895,28 @@ extern "C" hipError_t rr_launch_decode(const uint8_t *blob, const uint64_t *offs
     const uint32_t st = (uint32_t)scan_tiles(n), nw = (uint32_t)dec_windows(data_cap);
     uint64_t *lb = scratch + RR_SCRATCH_HDR;
     const uint64_t lb_words = 1 + st + (st + LB_GROUP - 1) / LB_GROUP;
-    uint64_t *counts = lb + lb_words;
+    uint64_t *fix = lb + lb_words;                      // header words, then the u32 list
+    uint64_t *counts = fix + FIX_HDR + (n + 2) / 2;
     uint64_t *stats = counts + n + 1;
     uint32_t *first_val = reinterpret_cast<uint32_t *>(stats + 3 * (uint64_t)nw);
     uint8_t *cls = reinterpret_cast<uint8_t *>(first_val + ((nw + 2) & ~1u));
-    hipError_t e = hipMemsetAsync(lb, 0, ((lb_words * 8) + 15) & ~(size_t)15, stream);
+    hipError_t e = hipMemsetAsync(lb, 0, (((lb_words + FIX_HDR) * 8) + 15) & ~(size_t)15, stream);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(count_kernel, dim3((uint32_t)((n + 1 + 255) / 256)), dim3(256), 0, stream, blob, offsets, n,
                        first_val, nw, DEC_W, counts, cls);
-    if (st) hipLaunchKernelGGL(scan_kernel, dim3(st), dim3(256), 0, stream, counts, n, lb, st);
+    if (st) hipLaunchKernelGGL(scan_kernel, dim3(st), dim3(256), 0, stream, counts, n, lb, st, fix + 1);
     else {
         e = hipMemsetAsync(counts, 0, sizeof(uint64_t), stream);
         if (e != hipSuccess) return e;
     }
     hipLaunchKernelGGL((DECODE_KERNEL), dim3(nw), dim3(DEC_NW * RR_WAVE), 0, stream, blob, data_cap, offsets, n,
-                       first_val, cls, counts, values, elems, elem_cap, arena, stats);
+                       first_val, cls, counts, values, elems, elem_cap, arena, stats, fix);
+    static uint32_t fix_grid = 0;
+    if (!fix_grid) fix_grid = resident_grid(fixup_kernel, FIX_NT, false);
+    hipLaunchKernelGGL(fixup_kernel, dim3(fix_grid), dim3(FIX_NT), 0, stream, blob, fix, values, elems);
     e = hipGetLastError();
-    if (e == hipSuccess && totals) e = launch_finalize(stats, counts + n, nw, offsets, n, 2, totals, stream);
+    if (e == hipSuccess && totals)
+        e = launch_finalize(stats, counts + n, nw, offsets, n, 2, totals, stream, fix + 1, fix + 2);
     return e;
 }
 
@@ -1663,12 +1930,13 @@ static uint64_t enc_windows(uint64_t data_cap) { return data_cap / ENC_W + 1; }
 
 extern "C" uint64_t rr_encode_scratch_words(uint64_t n, uint64_t data_cap) {
     const uint64_t st = scan_tiles(n), t = (n + 255) / 256, nw = enc_windows(data_cap);
-    return RR_SCRATCH_HDR + 1 + st + (st + LB_GROUP - 1) / LB_GROUP + 6 * t + (nw + 2) / 2 + 2;
+    return RR_SCRATCH_HDR + 1 + st + (st + LB_GROUP - 1) / LB_GROUP + 1 + 6 * t + (nw + 2) / 2 + 2;
 }
 
-extern "C" hipError_t rr_launch_encode(const rr_value *values, const rr_elem *elems, const uint8_t *arena,
-                                       uint64_t n, uint8_t *out, uint64_t cap, uint64_t *offsets, uint64_t *scratch,
-                                       rr_totals *totals, hipStream_t stream) {
+extern "C" hipError_t rr_launch_encode(const rr_value *values, const rr_elem *elems, uint64_t elem_cap,
+                                       const uint8_t *arena, uint64_t arena_cap, uint64_t n, uint8_t *out,
+                                       uint64_t cap, uint64_t *offsets, uint64_t *scratch, rr_totals *totals,
+                                       hipStream_t stream) {
     hipError_t e;
     if (n == 0) {
         e = hipMemsetAsync(offsets, 0, sizeof(uint64_t), stream);
@@ -1679,17 +1947,19 @@ extern "C" hipError_t rr_launch_encode(const rr_value *values, const rr_elem *el
     const uint64_t nw = enc_windows(cap);
     uint64_t *lb = scratch + RR_SCRATCH_HDR;
     const uint64_t lb_words = 1 + st + (st + LB_GROUP - 1) / LB_GROUP;
-    uint64_t *stats = lb + lb_words;
+    uint64_t *err = lb + lb_words;   // device error word (look-back timeout)
+    uint64_t *stats = err + 1;
     uint32_t *fv = reinterpret_cast<uint32_t *>(stats + 6 * (uint64_t)t);
-    e = hipMemsetAsync(lb, 0, ((lb_words * 8) + 15) & ~(size_t)15, stream);
+    e = hipMemsetAsync(lb, 0, (((lb_words + 1) * 8) + 15) & ~(size_t)15, stream);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(enc_size_kernel, dim3(t), dim3(256), 0, stream, values, elems, n, offsets, stats);
-    hipLaunchKernelGGL(scan_kernel, dim3(st), dim3(256), 0, stream, offsets, n, lb, st);
-    hipLaunchKernelGGL(enc_index_kernel<ENC_W>, dim3(t), dim3(256), 0, stream, values, elems, n, offsets, cap, fv,
-                       nw, stats + 3 * (uint64_t)t);
+    hipLaunchKernelGGL(enc_size_kernel, dim3(t), dim3(256), 0, stream, values, elems, n, elem_cap, arena_cap, offsets,
+                       stats);
+    hipLaunchKernelGGL(scan_kernel, dim3(st), dim3(256), 0, stream, offsets, n, lb, st, err);
+    hipLaunchKernelGGL(enc_index_kernel<ENC_W>, dim3(t), dim3(256), 0, stream, values, elems, n, elem_cap, arena_cap,
+                       offsets, cap, fv, nw, stats + 3 * (uint64_t)t);
     hipLaunchKernelGGL((enc_emit_kernel<ENC_W, ENC_NT, ENC_JCAP>), dim3((uint32_t)nw), dim3(ENC_NT), 0, stream,
                        values, elems, arena, n, out, cap, offsets, fv);
     e = hipGetLastError();
-    if (e == hipSuccess && totals) e = launch_finalize(stats, lb, 2 * t, offsets, n, 0, totals, stream);
+    if (e == hipSuccess && totals) e = launch_finalize(stats, lb, 2 * t, offsets, n, 0, totals, stream, err);
     return e;
 }

@@ -66,11 +66,15 @@ def test_values_larger_than_a_window(engine):
                      for j, x in enumerate(rng.integers(-10**18, 10**18, 5000))]
             blobs.append(l_list(i, items))
         elif k == 2:
-            blobs.append(s_ht(i, [b""] + [rng.integers(0, 256, int(rng.integers(0, 70)), dtype=np.uint8).tobytes()
-                                          for _ in range(3001)]))
+            # distinct members (a repeated member would be dropped: desSet de-duplicates)
+            blobs.append(s_ht(i, [b""] + [b"%d:" % j + rng.integers(0, 256, int(rng.integers(0, 70)),
+                                                                      dtype=np.uint8).tobytes()
+                                          for j in range(3001)]))
         else:
-            blobs.append(z_sl(i, [(rng.integers(65, 91, int(rng.integers(1, 40)), dtype=np.uint8).tobytes(),
-                                   float(rng.standard_normal())) for _ in range(2000)]))
+            # in serZset's order (descending score, member), as a serialized skiplist is
+            pairs = [(rng.integers(65, 91, int(rng.integers(1, 40)), dtype=np.uint8).tobytes(),
+                      float(rng.standard_normal())) for _ in range(2000)]
+            blobs.append(z_sl(i, sorted(pairs, key=lambda x: (x[1], x[0]), reverse=True)))
         blobs.append(s_raw(i + 100, b"x" * int(rng.integers(0, 50))))   # small neighbours
     data, offs = batch_from_blobs(blobs)
     v, e, a, t = engine.decode_host(data, offs)
@@ -131,3 +135,29 @@ def test_encode_configs_match_oracle(engine, cfg, n):
     v, e, a, t = engine.decode_host(data, offs)
     out, ooffs, t2 = _check_against_oracle(engine, v, e, a)
     assert np.array_equal(out, data[:int(offs[-1])])
+
+
+def test_encode_rejects_bad_status_and_out_of_range(engine):
+    """decode with a short elem_cap, then encode that flat batch: the values that
+    got RR_E_CAPACITY (and malformed ones) are unencodable — size 0, counted bad — and no
+    descriptor past elem_cap nor payload past arena_cap is read.  Matches the oracle."""
+    data, offs = rr.gen_batch(4, 3000, seed=12)
+    blobs = [bytes(data[offs[i]:offs[i + 1]]) for i in range(len(offs) - 1)]
+    blobs[7] = blobs[7][:3]                      # one malformed value (RR_E_SHORT)
+    data, offs = batch_from_blobs(blobs)
+    cap = 9000
+    v, e, a, t = engine.decode_host(data, offs, elem_cap=cap)
+    ov, oe, oa, ot = cpu.decode(data, offs, elem_cap=cap)
+    assert t == ot and (v["status"] == 11).any() and v["status"][7] == 1
+    _check_against_oracle(engine, v, e, a)
+    # descriptors pointing past the arena, and a value whose range passes elem_cap
+    v2, e2 = v.copy(), e.copy()
+    ok = np.nonzero((v2["status"] == 0) & (v2["n_elems"] > 0))[0]
+    for i in ok[:40]:
+        k = int(v2["elem_base"][i])
+        if e2["kind"][k] in (rr.K_STR, rr.K_ZLRAW):
+            e2["data"][k] = len(a) - 2
+            e2["len"][k] = 5
+    v2["elem_base"][ok[50]] = len(e2) - 1
+    out, ooffs, t2 = _check_against_oracle(engine, v2, e2, a)
+    assert t2["n_bad"] > t["n_bad"]

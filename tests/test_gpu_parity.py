@@ -221,3 +221,101 @@ def test_full_size_mixed_roundtrip(engine, cfg):
     torch.cuda.synchronize()
     assert torch.equal(d_out[:nb], d_data[:nb])
     assert np.array_equal(d_ooffs.cpu().numpy().view(np.uint64), offs)
+
+
+def _ht_blob(t, members, lru=7):
+    n = len(members) if t == rr.T_SET_HT else len(members) // 2
+    return bytes([t]) + struct.pack("<I", lru) + struct.pack("<Q", n) + b"".join(
+        struct.pack("<Q", len(m)) + m for m in members)
+
+
+def _sl_blob(pairs, lru=9):
+    return bytes([rr.T_ZSET_SKIPLIST]) + struct.pack("<I", lru) + struct.pack("<Q", len(pairs)) + b"".join(
+        struct.pack("<Q", len(m)) + m + (s if isinstance(s, bytes) else struct.pack("<d", s)) for m, s in pairs)
+
+
+def _fixup_blobs(rng):
+    """Blobs for the fixup pass (fixup_kernel): hash tables with repeated keys below and above the
+    in-register fingerprint limit (16 keys) and past one LDS table pass (2048 keys), skiplists
+    out of serZset's order, with tied scores, -0.0 / 0.0 ties, repeated members and NaN."""
+    def word(lo, hi):
+        return rng.integers(97, 123, int(rng.integers(lo, hi + 1)), dtype=np.uint8).tobytes()
+    B = []
+    for n, ndup in ((5, 2), (16, 1), (16, 0), (17, 3), (40, 10), (300, 0), (3000, 400), (9000, 50)):
+        base = [word(0, 24) + str(i).encode() for i in range(n - ndup)]
+        mem = list(base)
+        for _ in range(ndup):
+            mem.insert(int(rng.integers(0, len(mem) + 1)), base[int(rng.integers(0, len(base)))])
+        B.append(_ht_blob(rr.T_SET_HT, mem))
+    B.append(_ht_blob(rr.T_SET_HT, [b""] * 5 + [b"x"]))
+    B.append(_ht_blob(rr.T_SET_HT, [b"same-prefix-0123456789-" + bytes([65 + i % 3]) for i in range(30)]))
+    for n, dup_at in ((4, None), (8, 7), (16, 15), (16, None), (40, 39), (200, 3), (2600, 2599), (2600, None)):
+        fields = [b"f%05d" % i for i in range(n)]
+        if dup_at is not None:
+            fields[dup_at] = fields[int(rng.integers(0, dup_at))]
+        mem = []
+        for f in fields:
+            mem += [f, word(0, 40)]
+        B.append(_ht_blob(rr.T_HASH_HT, mem))
+    B.append(_ht_blob(rr.T_HASH_HT, [b"a", b"v", b"b", b"v", b"c", b"v"]))   # repeated values only
+    for n in (2, 3, 16, 17, 100, 1000, 5000):
+        pairs = [(word(1, 12), float(rng.integers(-50, 50))) for _ in range(n)]
+        B.append(_sl_blob(pairs))                                                    # random order
+        B.append(_sl_blob(sorted(pairs, key=lambda x: (x[1], x[0]), reverse=True)))  # serZset order
+    B.append(_sl_blob([(b"a", 0.0), (b"m", -0.0), (b"m", 0.0), (b"m", -0.0), (b"b", 0.0)]))
+    B.append(_sl_blob([(b"x", 1.0), (b"x", 1.0), (b"x", 2.0)]))
+    B.append(_sl_blob([(b"x", 3.0), (b"y", float("nan")), (b"z", 1.0)]))
+    B.append(_sl_blob([(b"x", struct.pack("<Q", 0xFFF8000000000001))]))
+    B.append(_sl_blob([(b"q", float("inf")), (b"p", float("-inf")), (b"r", float("inf"))]))
+    return B
+
+
+def test_fixup_pass_matches_oracle(engine):
+    """desSet de-duplication, desHash's duplicate-field assert, desZset's re-sort and NaN assert:
+    GPU records, descriptors, totals and re-encoded bytes equal the C oracle's."""
+    rng = np.random.default_rng(31)
+    blobs = _fixup_blobs(rng)
+    # interleave with ordinary values so fixed-up values share windows with fast-path ones
+    data0, offs0 = rr.gen_batch(4, 400, seed=5)
+    mixed = []
+    for i, b in enumerate(blobs):
+        mixed.append(b)
+        mixed.append(bytes(data0[offs0[i]:offs0[i + 1]]))
+    data, offs = batch_from_blobs(mixed)
+    v, e, a, t = engine.decode_host(data, offs)
+    ov, oe, oa, ot = cpu.decode(data, offs, nthreads=4)
+    assert_flat_equal((v, e), (ov, oe), "fixup")
+    assert t == ot
+    st = ov["status"]
+    assert (st == 13).sum() == 5 and (st == 14).sum() == 2       # the dup-field hashes, the NaN zsets
+    ok = np.nonzero(st == 0)[0]
+    out, ooffs, t2 = engine.encode_host(v, e, a)
+    xo, xoffs, xt = cpu.encode(ov, oe, oa)
+    assert t2 == xt and np.array_equal(ooffs, xoffs) and np.array_equal(out, xo)
+    assert t2["n_bad"] == len(v) - len(ok)
+
+
+def test_fixup_pass_device_entry_repeatable(engine):
+    """The same batch decoded twice through the device entry point (the fixup queue and its
+    ticket are reset per call) gives identical results."""
+    import torch
+    blobs = _fixup_blobs(np.random.default_rng(2))
+    data, offs = batch_from_blobs(blobs)
+    n, nb = len(offs) - 1, int(offs[-1])
+    dev = torch.device("cuda:0")
+    d_data = torch.from_numpy(data).to(dev)
+    d_offs = torch.from_numpy(offs.view(np.int64)).to(dev)
+    cap = rr.elem_bound(n, nb)
+    res = []
+    for _ in range(2):
+        d_vals = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
+        d_elems = torch.zeros(cap * 16, dtype=torch.uint8, device=dev)
+        d_arena = torch.zeros((nb + 15) & ~15, dtype=torch.uint8, device=dev)
+        d_tot = torch.zeros(4, dtype=torch.int64, device=dev)
+        engine.decode_device(d_data, d_offs, d_vals, d_elems, d_arena, d_tot)
+        torch.cuda.synchronize()
+        res.append((d_vals.cpu().numpy().copy(), d_elems.cpu().numpy().copy(), d_tot.cpu().numpy().copy()))
+    assert all(np.array_equal(x, y) for x, y in zip(res[0], res[1]))
+    ov, oe, _, ot = cpu.decode(data, offs)
+    assert np.array_equal(res[0][0].view(rr.VALUE_DT), ov)
+    assert np.array_equal(res[0][1].view(rr.ELEM_DT)[:len(oe)], oe)

@@ -36,12 +36,14 @@ for _ in range(3):
     eng.decode_device(d_data, d_offs, d_vals, d_elems, d_arena, d_tot)
 torch.cuda.synchronize()
 p = probe.cpu().numpy().reshape(nwin, 32).astype(np.float64)
-names = ["STR", "IS", "LIST", "HT", "SL", "ZL", "EXACT"]
-print(f"cfg {cfg}: {nwin} windows, staged {int(p[:, 25].sum())}, values/window {p[:, 24].mean():.1f}")
+names = ["STR", "IS", "LIST", "HTSET", "SL", "ZL", "EXACT", "HTHASH"]   # rr_decode_class.h classes
+NC = len(names)
+print(f"cfg {cfg}: {nwin} windows, staged {int(p[:, 29].sum())}, values/window {p[:, 28].mean():.1f}")
 print("phase cycles per window (mean / p90):  copy %.0f / %.0f   sort %.0f / %.0f   batches %.0f / %.0f" % (
     p[:, 0].mean(), np.percentile(p[:, 0], 90), p[:, 1].mean(), np.percentile(p[:, 1], 90),
     p[:, 2].mean(), np.percentile(p[:, 2], 90)))
 for c, nm in enumerate(names):
-    nbat = p[:, 10 + c].sum()
+    nbat = p[:, 3 + NC + c].sum()
     if nbat:
-        print(f"{nm:6s} batches {int(nbat):8d}  cycles/batch {p[:, 3 + c].sum() / nbat:9.0f}  lanes/batch {p[:, 17 + c].sum() / nbat:5.1f}")
+        print(f"{nm:6s} batches {int(nbat):8d}  cycles/batch {p[:, 3 + c].sum() / nbat:9.0f}  "
+              f"lanes/batch {p[:, 3 + 2 * NC + c].sum() / nbat:5.1f}")
