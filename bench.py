@@ -170,7 +170,7 @@ def main():
         parity = {"roundtrip_bit_exact": rt, "n_bad": n_bad}
         if rank == 0 and world == 1:
             from oracle import cpu
-            ov, oe, _, ot = cpu.decode(data, offs, nthreads=min(16, cpu.nprocs()))
+            ov, oe, _, ot = cpu.decode(data, offs, elem_cap=n_elems, nthreads=min(16, cpu.nprocs()))
             v = d_vals.cpu().numpy().view(rr.VALUE_DT)
             e = d_elems[: n_elems * 16].cpu().numpy().view(rr.ELEM_DT)
             parity["decode_vs_oracle_bit_exact"] = bool(np.array_equal(v, ov) and np.array_equal(e, oe))

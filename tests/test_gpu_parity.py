@@ -319,3 +319,45 @@ def test_fixup_pass_device_entry_repeatable(engine):
     ov, oe, _, ot = cpu.decode(data, offs)
     assert np.array_equal(res[0][0].view(rr.VALUE_DT), ov)
     assert np.array_equal(res[0][1].view(rr.ELEM_DT)[:len(oe)], oe)
+
+
+def test_config4_at_baseline_size_10m(engine):
+    """BASELINE.json config 4 at its own size: 10M mixed values (~5 GB of blobs, ~150M
+    descriptors) decoded and encoded with the device entry points.  Exercises the 64-bit
+    offsets, 32-bit elem_base / first-value tables and buffer-resource clamps at scale:
+    records and descriptors equal the C oracle's (16 host threads), encode(decode(b)) == b."""
+    import torch
+    n = 10_000_000
+    data, offs = rr.gen_batch(4, n)
+    nb = int(offs[-1])
+    assert nb > (1 << 32)                         # offsets and arena offsets past 32 bits
+    ov, oe, _, ot = cpu.decode(data, offs, elem_cap=34 * n, nthreads=16)
+    assert ot["n_bad"] == 0
+    cap = ot["n_elems"] + 64
+    dev = torch.device("cuda:0")
+    d_data = torch.from_numpy(data).to(dev)
+    d_offs = torch.from_numpy(offs.view(np.int64)).to(dev)
+    del data
+    d_vals = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
+    d_elems = torch.zeros(cap * 16, dtype=torch.uint8, device=dev)
+    d_arena = torch.zeros((nb + 15) & ~15, dtype=torch.uint8, device=dev)
+    d_tot = torch.zeros(4, dtype=torch.int64, device=dev)
+    engine.decode_device(d_data, d_offs, d_vals, d_elems, d_arena, d_tot)
+    torch.cuda.synchronize()
+    tot = d_tot.cpu().numpy().view(np.uint64)
+    assert int(tot[2]) == 0 and int(tot[0]) == ot["n_elems"] and int(tot[3]) == ot["payload"]
+    assert int(tot[1]) == nb
+    assert np.array_equal(d_vals.cpu().numpy().view(rr.VALUE_DT), ov)
+    assert np.array_equal(d_elems[:ot["n_elems"] * 16].cpu().numpy().view(rr.ELEM_DT), oe)
+    del ov, oe
+    assert torch.equal(d_arena[:nb], d_data[:nb])
+    del d_arena
+    d_out = torch.zeros((nb + 15) & ~15, dtype=torch.uint8, device=dev)
+    d_ooffs = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    d_arena2 = d_data                               # the arena mirrors the blob buffer
+    engine.encode_device(d_vals, d_elems, d_arena2, d_out, d_ooffs, d_tot)
+    torch.cuda.synchronize()
+    tot = d_tot.cpu().numpy().view(np.uint64)
+    assert int(tot[2]) == 0 and int(tot[1]) == nb
+    assert torch.equal(d_out[:nb], d_data[:nb])
+    assert np.array_equal(d_ooffs.cpu().numpy().view(np.uint64), offs)
