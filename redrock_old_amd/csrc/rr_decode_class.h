@@ -446,17 +446,33 @@ __device__ __forceinline__ bool do_skiplist(const Src &R, const Head &H, const L
 }
 
 // ---- Hash / ZSet ziplists (rock_serdes.c:314-346, :417-446; ziplist.c:300-447): element 0
-// is the raw ziplist, then one descriptor per entry
+// is the raw ziplist, then one descriptor per entry.
+// Two lanes per value walk it from both ends (ziplist.c:300-330: an entry's prevlen field gives
+// the start of the entry before it): the even lane forward from the first entry through entries
+// [0, m), the odd lane backward from zltail through entries [m, N) (N = zllen, m = ceil(N/2)),
+// each descriptor stored at its own slot.  The walks meet: the forward lane's end position and
+// last entry size must be the backward lane's last entry start and its prevlen.  Together the
+// checks are those of one forward walk (every prevlen == the size of the entry before it, the
+// entries tile [10, zlbytes-1) exactly, the last one starts at zltail, the byte after it is
+// 0xFF, N entries) with half the chained steps.  A ziplist whose zllen saturated (0xFFFF) is
+// walked forward to its end marker by the even lane alone.
 template <class Src>
-__device__ __forceinline__ bool do_ziplist(const Src &R, const Lane &l, bool active, uint32_t &n, uint64_t &pay) {
+__device__ __forceinline__ bool do_ziplist(const Src &R, const Lane &l, bool active, const bool back, uint32_t &n,
+                                           uint64_t &pay) {
     const uint32_t zl0 = l.q + 13, zend = l.q + l.L, zlast = zend - 1;   // zlast: the 0xFF byte
     uint32_t z[3];
     R.template get<3>(zl0, z);   // zlbytes, zltail, zllen
-    put_desc(l.E, active ? l.slot(0) : NOSLOT, l.B + zl0, l.L - 13, RR_K_ZLRAW, 0);
-    pay += active ? l.L - 13 : 0;
-    uint32_t p = zl0 + 10, prev_raw = 0, last = zl0 + 10, k = 1;
-    bool fail = false, live = active;
-    Raw<4> ra = R.template fetch<4>(p), rb;   // prevlen (1 or 5) + encoding + up to 9 more bytes
+    const uint32_t zllen = z[2] & 0xFFFF;
+    const bool two = zllen != 0xFFFF;
+    const uint32_t mf = two ? (zllen + 1) / 2 : 0xFFFFFFFFu, nb = two ? zllen - (zllen + 1) / 2 : 0;
+    const uint32_t endbyte = R.template fetch<1>(zlast).w[0];   // (aligned dword holding zlast)
+    put_desc(l.E, active && !back ? l.slot(0) : NOSLOT, l.B + zl0, l.L - 13, RR_K_ZLRAW, 0);
+    pay += active && !back ? l.L - 13 : 0;
+    const uint32_t lim = back ? nb : mf;
+    uint32_t p = back ? zl0 + z[1] : zl0 + 10;
+    uint32_t prev_raw = 0, last = zl0 + 10, k = 0, expect = zlast, plm = 0;
+    bool fail = false, live = active && lim > 0;
+    Raw<4> ra = R.template fetch<4>(p < zend ? p : zl0), rb;   // prevlen (1 or 5) + encoding + up to 9 more bytes
     auto step = [&](const Raw<4> &cur, Raw<4> &nxt) __attribute__((always_inline)) {
         uint32_t b[4];
         cur.align(b);
@@ -480,12 +496,15 @@ __device__ __forceinline__ bool do_ziplist(const Src &R, const Lane &l, bool act
         const uint32_t isz = (uint32_t)(e == 0xFE) + 2 * (uint32_t)(e == 0xC0) + 3 * (uint32_t)(e == 0xF0) +
                              4 * (uint32_t)(e == 0xD0) + 8 * (uint32_t)(e == 0xE0);
         const uint64_t endp = (uint64_t)qp + (zstr ? ls + sl : 1 + isz);
-        const uint32_t pn = endp < zlast ? (uint32_t)endp : zlast;
-        nxt = R.template fetch<4>(live ? pn : p);
+        // next entry: forward past this one; backward to the one this prevlen describes
+        const uint32_t pn = back ? p - pl : (endp < zlast ? (uint32_t)endp : zlast);
+        nxt = R.template fetch<4>((live & (pn < zend)) ? pn : zl0);
         __builtin_amdgcn_sched_barrier(0);   // keep the read ahead of the checks and the store
-        const bool done = (b0 == 0xFF) & (p < zend);
-        const bool bad = (p >= zend) | (big & (p + 5 > zlast)) | (pl != prev_raw) | (qp >= zlast) | (k >= l.r) |
-                         (!zstr & !imm & (isz == 0)) | (zstr & (qp + ls > zlast)) | (endp > zlast);
+        const uint32_t idx = back ? zllen - 1 - k : k;       // entry index
+        const bool done = !two & (b0 == 0xFF) & (p < zend);   // forward to the end marker
+        const bool bad = (p >= zend) | (p < zl0 + 10) | (b0 == 0xFF) | (big & (p + 5 > zlast)) | (qp >= zlast) |
+                         (idx + 1 >= l.r) | (!zstr & !imm & (isz == 0)) | (zstr & (qp + ls > zlast)) |
+                         (endp > zlast) | (back ? endp != expect : pl != prev_raw);
         const bool emit = live & !done & !bad;
         fail |= live & !done & bad;
         // little-endian integer of isz (1..4) bytes, sign-extended by a shift pair; 8 bytes; or
@@ -493,20 +512,34 @@ __device__ __forceinline__ bool do_ziplist(const Src &R, const Lane &l, bool act
         const uint32_t sh = (32 - 8 * isz) & 31;
         const int64_t v32 = (int32_t)(lo << sh) >> sh;
         const int64_t iv = isz == 8 ? (int64_t)((uint64_t)lo | ((uint64_t)hi << 32)) : imm ? (int64_t)(e & 0x0F) - 1 : v32;
-        put_desc(l.E, emit ? l.slot(k) : NOSLOT, zstr ? l.B + qp + ls : (uint64_t)iv, zstr ? sl : 0,
+        put_desc(l.E, emit ? l.slot(idx + 1) : NOSLOT, zstr ? l.B + qp + ls : (uint64_t)iv, zstr ? sl : 0,
                  zstr ? RR_K_STR : RR_K_INT, zstr ? (e & 0xC0) : e);
         prev_raw = emit ? (uint32_t)endp - p : prev_raw;
         last = emit ? p : last;
+        plm = emit ? pl : plm;
+        expect = emit ? p : expect;
         p = emit ? pn : p;
         k += emit;
-        live = emit;
+        live = emit & (k < lim);
         return __ballot(live) == 0;
     };
     RR_PINGPONG(ra, rb, step)
-    n = k;
-    const uint32_t entries = k - 1, zllen = z[2] & 0xFFFF;
-    return fail || p != zlast || (zllen != 0xFFFF && zllen != entries) || z[1] != last - zl0 || (entries & 1) ||
-           k != l.r;
+    // the meeting: the backward lane's last entry must start where the forward lane stopped,
+    // and its prevlen must be the size of the forward lane's last entry
+    const uint32_t o_k = __shfl_xor(k, 1, RR_WAVE), o_last = __shfl_xor(last, 1, RR_WAVE);
+    const uint32_t o_plm = __shfl_xor(plm, 1, RR_WAVE);
+    const bool o_fail = __shfl_xor((uint32_t)fail, 1, RR_WAVE) != 0;
+    bool ok;
+    if (two) {
+        ok = !fail && k == mf && (zllen & 1) == 0 && (endbyte >> (8 * (zlast & 3)) & 0xFF) == 0xFF &&
+             (nb > 0 ? (!o_fail && o_k == nb && p == o_last && prev_raw == o_plm)
+                     : (p == zlast && z[1] == last - zl0));
+        n = 1 + zllen;
+    } else {   // one forward walk to the end marker (ziplist.c:300-447)
+        ok = !fail && p == zlast && z[1] == last - zl0 && (k & 1) == 0;
+        n = 1 + k;
+    }
+    return !ok || n != l.r;
 }
 
 }  // namespace rr

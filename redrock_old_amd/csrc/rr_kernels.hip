@@ -746,8 +746,10 @@ __device__ __forceinline__ Acc run_batch(const Src &src, uint32_t c, bool active
         fail = do_ht(src, H, l, active, ne, vp, fixup, c == C_HH);
     } else if (c == C_SL) {
         fail = do_skiplist(src, H, l, active, ne, vp);
-    } else {
-        fail = do_ziplist(src, l, active, ne, vp);
+    } else {   // C_ZL: two lanes per value, the odd one walks backward (its results are unused)
+        const bool back = (lane_id() & 1) != 0;
+        fail = do_ziplist(src, l, active, back, ne, vp);
+        if (back) return Acc{0, 0};
     }
     if (!active) return Acc{0, 0};
     if (fail) return exact_value(blob, v, offsets, ebase, values, elems, cap, fix);
@@ -791,7 +793,7 @@ extern "C" int rr_probe_set(void *p) { return hipMemcpyToSymbol(HIP_SYMBOL(g_pro
 #define RR_DEC_BL 64
 #endif
 constexpr uint32_t DEC_BL = RR_DEC_BL;
-static_assert(DEC_BL >= 1 && DEC_BL <= RR_WAVE, "batch lanes");
+static_assert(DEC_BL >= 2 && DEC_BL <= RR_WAVE && DEC_BL % 2 == 0, "batch lanes");
 // 1: the mirror-arena copy is written by waves that ran out of walk batches (step 4), not
 // during staging
 #ifndef RR_DEC_LATECOPY
@@ -949,10 +951,11 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
             uint32_t s = 0, bs = 0;
             for (uint32_t k = 0; k < C_N; ++k) {
                 const uint32_t c = CLASS_ORDER[k];
+                const uint32_t vpb = c == C_ZL ? DEC_BL / 2 : DEC_BL;   // ziplists: two lanes each
                 cbase[c] = s;
                 bpre[k] = bs;
                 s += ccount[c];
-                bs += (ccount[c] + DEC_BL - 1) / DEC_BL;
+                bs += (ccount[c] + vpb - 1) / vpb;
             }
             bpre[C_N] = bs;
         }
@@ -989,14 +992,16 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
             uint32_t k = 0;
             while (bi >= bpre[k + 1]) ++k;
             const uint32_t c = CLASS_ORDER[k];
-            const uint32_t first = cbase[c] + (bi - bpre[k]) * DEC_BL;
-            const uint32_t cnt = min(ccount[c] - (bi - bpre[k]) * DEC_BL, DEC_BL);
+            const uint32_t vpb = c == C_ZL ? DEC_BL / 2 : DEC_BL;
+            const uint32_t first = cbase[c] + (bi - bpre[k]) * vpb;
+            const uint32_t cnt = min(ccount[c] - (bi - bpre[k]) * vpb, vpb);
 #ifdef RR_SKIP_CLASSES   // timing-only builds (tools/): skip the batches of these classes
             if ((RR_SKIP_CLASSES >> c) & 1) continue;
 #endif
             PROBE(const uint64_t tb0 = __builtin_amdgcn_s_memtime();)
-            const bool active = lane < cnt;
-            const uint64_t v = c0 + (active ? perm[first + lane] : 0u);
+            const uint32_t li = c == C_ZL ? lane >> 1 : lane;   // the value's index in the batch
+            const bool active = li < cnt;
+            const uint64_t v = c0 + (active ? perm[first + li] : 0u);
             const Acc a = staged ? run_batch(lsrc, c, active, v, S0, E, eb0, blob, offsets, ebase, values, elems, cap, fix)
                                  : run_batch_g(gsrc, c, active, v, S0, E, eb0, blob, offsets, ebase, values, elems, cap,
                                                fix);
