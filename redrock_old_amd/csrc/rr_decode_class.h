@@ -121,23 +121,23 @@ __device__ __forceinline__ uint32_t ab(uint32_t hi, uint32_t lo, uint32_t s) { r
 // zipTryEncoding (ziplist.c:480) + string2ll (util.c:360) over bytes d[0, len) given as 5
 // dwords: an entry of 1..31 bytes is an integer iff it is "0" or [-]?[1-9][0-9]* within int64.
 // A 20-digit magnitude is always >= 1e19 > 2^63, so more than 20 bytes fails; up to 19 digits
-// cannot overflow uint64 while accumulating.
+// cannot overflow uint64.
 //
-// Straight-line (selects only): every digit position is evaluated and out-of-range ones are
-// masked, so a wave pays one pass whatever mix of lengths its lanes hold.  The digits are
-// accumulated in three 24-bit chunks (byte positions [0,7), [7,14), [14,20); < 10^7 each) with
-// full-rate v_mad_u32_u24 steps; only the final combine uses 64-bit multiplies (a 64-bit
-// multiply-accumulate per digit is three quarter-rate multiplies).
-__device__ __forceinline__ uint32_t pow10_u24(uint32_t n) {   // 10^n, n in [0, 7]
-    const uint32_t a = (n & 1) ? 10u : 1u, b = (n & 2) ? 100u : 1u, c = (n & 4) ? 10000u : 1u;
-    return __umul24(__umul24(a, b), c);
+// Straight-line SWAR (selects only, so a wave pays one pass whatever mix of lengths its lanes
+// hold): the digit check runs four bytes at a time; the digits are turned into values 0-9 by
+// one subtraction per dword and RIGHT-aligned in a 20-byte field (a funnel shift by 20 - len
+// bytes: dwords by three conditional moves, bytes by alignbyte), which leaves leading zeros and
+// pushes the bytes past the entry out; each dword then converts as 4 digits with two multiply-
+// add steps (pairs, then the two pairs), and five 4-digit chunks combine with two 64-bit MADs.
+__device__ __forceinline__ uint32_t swar4(uint32_t x) {   // bytes d0..d3 (d0 most significant) -> value
+    const uint32_t t = x * 10u + (x >> 8);                  // bytes 0 / 2: 10*d0+d1, 10*d2+d3
+    return __umul24(t & 0xFFu, 100u) + ((t >> 16) & 0xFFu);
 }
 __device__ __forceinline__ bool regs_try_int(const uint32_t (&b)[5], uint32_t len, int64_t &out) {
     const uint32_t c0 = b[0] & 0xFF;
     const uint32_t neg = c0 == '-' ? 1u : 0u;
     // digit check of bytes [neg, len) four at a time (SWAR, VALU only): a byte is a digit iff
-    // its high nibble is 3 and its low nibble + 6 does not carry into bit 4.  (Per-byte compares
-    // folded into an SGPR mask cost a VALU->SALU dependency per digit.)
+    // its high nibble is 3 and its low nibble + 6 does not carry into bit 4
     uint32_t nondig = 0;
 #pragma unroll
     for (uint32_t k = 0; k < 5; ++k) {
@@ -148,24 +148,36 @@ __device__ __forceinline__ bool regs_try_int(const uint32_t (&b)[5], uint32_t le
         if (k == 0) m &= neg ? 0xFFFFFF00u : 0xFFFFFFFFu;
         nondig |= nd & m;
     }
-    bool ok = nondig == 0;
-    uint32_t acc[3] = {0u, 0u, 0u};
+    // digit values: '-' becomes a leading 0; borrows of non-digit bytes past the entry only run
+    // upward, into bytes the shift drops
+    uint32_t x[5];
 #pragma unroll
-    for (uint32_t j = 0; j < 20; ++j) {
-        const uint32_t d = ((b[j >> 2] >> (8 * (j & 3))) & 0xFF) - '0';
-        const bool in = (j == 0 ? neg == 0 : true) & (j < len);
-        const uint32_t c = j < 7 ? 0 : j < 14 ? 1 : 2;
-        const uint32_t t = __umul24(acc[c], 10u) + d;
-        acc[c] = in ? t : acc[c];
+    for (uint32_t k = 0; k < 5; ++k) x[k] = b[k];
+    x[0] = neg ? (x[0] & 0xFFFFFF00u) | 0x30u : x[0];
+#pragma unroll
+    for (uint32_t k = 0; k < 5; ++k) x[k] -= 0x30303030u;
+    // right-align: byte i -> byte i + s, s = 20 - len (len > 20 never passes the checks)
+    const uint32_t s = len <= 20 ? 20 - len : 0;
+    const uint32_t q = s >> 2, r = s & 3;
+    if (q & 1) { x[4] = x[3]; x[3] = x[2]; x[2] = x[1]; x[1] = x[0]; x[0] = 0; }
+    if (q & 2) { x[4] = x[2]; x[3] = x[1]; x[2] = x[0]; x[1] = 0; x[0] = 0; }
+    if (q & 4) { x[4] = x[0]; x[3] = 0; x[2] = 0; x[1] = 0; x[0] = 0; }
+    uint32_t y[5];
+#pragma unroll
+    for (uint32_t k = 0; k < 5; ++k) {
+        const uint32_t lo = k ? x[k - 1] : 0u;
+        y[k] = r ? __builtin_amdgcn_alignbyte(x[k], lo, 4 - r) : x[k];
     }
-    const uint32_t nB = len > 14 ? 7u : len > 7 ? len - 7 : 0u;   // digits in chunk 1
-    const uint32_t nC = len > 20 ? 6u : len > 14 ? len - 14 : 0u;  // digits in chunk 2
-    const uint64_t v = ((uint64_t)acc[0] * pow10_u24(nB) + acc[1]) * pow10_u24(nC) + acc[2];
+    const uint32_t h8 = __umul24(swar4(y[0]), 10000u) + swar4(y[1]);   // < 1e8
+    const uint32_t m8 = __umul24(swar4(y[2]), 10000u) + swar4(y[3]);
+    const uint64_t v16 = (uint64_t)h8 * 100000000ull + m8;              // < 1e16
+    const uint64_t v = (uint64_t)(uint32_t)v16 * 10000ull + swar4(y[4]) + ((uint64_t)((uint32_t)(v16 >> 32) * 10000u) << 32);
     const uint32_t c1 = (b[0] >> 8) & 0xFF;
     const uint32_t dfirst = (neg ? c1 : c0) - '0';
     const uint32_t nd = len - neg;
     const bool zero = len == 1 && c0 == '0';
-    ok = zero | (ok & (dfirst - 1u <= 8u) & (len <= 20) & (nd - 1u <= 18u) & (v <= 0x7FFFFFFFFFFFFFFFull + neg));
+    const bool ok = zero | ((nondig == 0) & (dfirst - 1u <= 8u) & (len <= 20) & (nd - 1u <= 18u) &
+                           (v <= 0x7FFFFFFFFFFFFFFFull + neg));
     out = zero ? 0 : neg ? (int64_t)(0ull - v) : (int64_t)v;
     return ok;
 }
