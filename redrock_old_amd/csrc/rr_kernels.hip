@@ -713,49 +713,56 @@ __device__ __forceinline__ Acc run_batch(const Src &src, uint32_t c, bool active
                                          const uint64_t *__restrict__ offsets, const uint64_t *__restrict__ ebase,
                                          rr_value *__restrict__ values, rr_elem *__restrict__ elems, uint64_t cap,
                                          uint64_t *fix) {
-    if (c == C_EXACT) return active ? exact_value(blob, v, offsets, ebase, values, elems, cap, fix) : Acc{0, 0};
-    uint64_t eb = eb0, r = 0;
-    Lane l{};
-    l.B = B;
-    l.E = E;
-    if (active) {
-        const uint64_t o = offsets[v], o1 = offsets[v + 1];
-        eb = ebase[v];
-        r = ebase[v + 1] - eb;
-        l.q = (uint32_t)(o - B);
-        l.L = (uint32_t)(o1 - o);
-        l.so = (uint32_t)(eb - eb0) * 16;
-        l.r = (uint32_t)r;
-        l.ok = eb + r <= cap;
+    // (one exact_value call site: the parser is large and every inlined copy costs I-cache)
+    bool exact = c == C_EXACT;
+    Acc acc{0, 0};
+    if (!exact) {
+        uint64_t eb = eb0, r = 0;
+        Lane l{};
+        l.B = B;
+        l.E = E;
+        if (active) {
+            const uint64_t o = offsets[v], o1 = offsets[v + 1];
+            eb = ebase[v];
+            r = ebase[v + 1] - eb;
+            l.q = (uint32_t)(o - B);
+            l.L = (uint32_t)(o1 - o);
+            l.so = (uint32_t)(eb - eb0) * 16;
+            l.r = (uint32_t)r;
+            l.ok = eb + r <= cap;
+        }
+        Head H;
+        src.template get<4>(l.q, H.h);
+        uint32_t ne = 1, enc = 0;
+        uint64_t vp = 0;   // this value's payload bytes (counted once it is emitted)
+        bool fail = false, fixup = false;
+        if (c == C_STR) {
+            if (active) do_string(H, l, vp);
+            enc = H.b5();
+        } else if (c == C_IS) {
+            do_intset(src, H, l, active);
+            ne = H.f9();
+            enc = H.f5();
+        } else if (c == C_LIST) {
+            fail = do_list(src, l, active, ne, vp);
+        } else if (c == C_HT || c == C_HH) {
+            fail = do_ht(src, H, l, active, ne, vp, fixup, c == C_HH);
+        } else if (c == C_SL) {
+            fail = do_skiplist(src, H, l, active, ne, vp);
+        } else {   // C_ZL: two lanes per value, the odd one walks backward (its results are unused)
+            const bool back = (lane_id() & 1) != 0;
+            fail = do_ziplist(src, l, active, back, ne, vp);
+            active &= !back;
+        }
+        exact = fail;
+        if (active && !fail) {
+            if (fixup && l.ok) queue_fixup(fix, v);
+            put_value(values + v, H.type(), enc, l.ok ? RR_OK : RR_E_CAPACITY, H.lru(), ne, (uint32_t)eb);
+            acc = Acc{l.ok ? 0u : 1u, l.ok ? vp : 0};
+        }
     }
-    Head H;
-    src.template get<4>(l.q, H.h);
-    uint32_t ne = 1, enc = 0;
-    uint64_t vp = 0;   // this value's payload bytes (counted once it is emitted)
-    bool fail = false, fixup = false;
-    if (c == C_STR) {
-        if (active) do_string(H, l, vp);
-        enc = H.b5();
-    } else if (c == C_IS) {
-        do_intset(src, H, l, active);
-        ne = H.f9();
-        enc = H.f5();
-    } else if (c == C_LIST) {
-        fail = do_list(src, l, active, ne, vp);
-    } else if (c == C_HT || c == C_HH) {
-        fail = do_ht(src, H, l, active, ne, vp, fixup, c == C_HH);
-    } else if (c == C_SL) {
-        fail = do_skiplist(src, H, l, active, ne, vp);
-    } else {   // C_ZL: two lanes per value, the odd one walks backward (its results are unused)
-        const bool back = (lane_id() & 1) != 0;
-        fail = do_ziplist(src, l, active, back, ne, vp);
-        if (back) return Acc{0, 0};
-    }
-    if (!active) return Acc{0, 0};
-    if (fail) return exact_value(blob, v, offsets, ebase, values, elems, cap, fix);
-    if (fixup && l.ok) queue_fixup(fix, v);
-    put_value(values + v, H.type(), enc, l.ok ? RR_OK : RR_E_CAPACITY, H.lru(), ne, (uint32_t)eb);
-    return Acc{l.ok ? 0u : 1u, l.ok ? vp : 0};
+    if (active && exact) acc = exact_value(blob, v, offsets, ebase, values, elems, cap, fix);
+    return acc;
 }
 
 // the unstaged (global-memory) instantiation: cold path, kept out of line in RR_DEC_NOINL
@@ -1002,9 +1009,14 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
             const uint32_t li = c == C_ZL ? lane >> 1 : lane;   // the value's index in the batch
             const bool active = li < cnt;
             const uint64_t v = c0 + (active ? perm[first + li] : 0u);
+#ifndef RR_DEC_NOGLOBAL
             const Acc a = staged ? run_batch(lsrc, c, active, v, S0, E, eb0, blob, offsets, ebase, values, elems, cap, fix)
                                  : run_batch_g(gsrc, c, active, v, S0, E, eb0, blob, offsets, ebase, values, elems, cap,
                                                fix);
+#else   // timing-only builds (tools/): no unstaged walks (wrong for windows that overflow the stage)
+            const Acc a = run_batch(lsrc, c, active, v, S0, E, eb0, blob, offsets, ebase, values, elems, cap, fix);
+            (void)gsrc;
+#endif
             bad += a.bad;
             pay += a.pay;
             PROBE(if (lane == 0) {
