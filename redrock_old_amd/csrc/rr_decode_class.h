@@ -457,6 +457,182 @@ __device__ __forceinline__ bool do_skiplist(const Src &R, const Head &H, const L
     return fail || (k & 1) || (uint64_t)(k >> 1) != cnt || k != l.r;
 }
 
+// ---- grouped walks ---------------------------------------------------------------------
+// A batch of cnt values gives each value G = 64 / cnt lanes (G <= GMAX, uniform per batch;
+// lane g of its group).  Every lane of a group walks the value's chain — the length fields, a
+// read and an add per element, the same LDS address for the whole group — and the per-element
+// work that does not feed the chain (integer parse, descriptor store, score checks) is split:
+// lane g takes elements g, g + G, g + 2G, ...  A walk step costs ~4 cycles per wave-instruction
+// whatever the number of active lanes, so with ~20 Lists or ~4 skiplists per window this cuts
+// the wave-instructions of a batch 2-8x.  Every lane of a group sees every element, so checks
+// over the whole value (counts, fingerprints, score order) come out the same on all of them;
+// the group's lane 0 records the value.
+constexpr uint32_t GMAX = 16;
+
+// ---- List (rock_serdes.c:162-214), grouped: {u32 len, bytes}* to the end
+template <class Src>
+__device__ __forceinline__ bool do_list_g(const Src &R, const Lane &l, bool active, uint32_t G, uint32_t g,
+                                          uint32_t &n, uint64_t &pay) {
+    uint32_t p = l.q + 5, k = 0;   // k: index of the element that starts at p
+    const uint32_t end = l.q + l.L;
+    bool fail = false, walk = active && p != end;
+    for (;;) {
+        uint32_t mp = 0, ml = 0, mk = 0;
+        bool mine = false;
+        for (uint32_t j = 0; j < G; ++j) {
+            uint32_t x[1];
+            R.template get<1>(p, x);
+            const uint32_t len = x[0], rem = end - p;
+            const bool bad = (rem < 4) | (len > rem - 4) | (k >= l.r);
+            fail |= walk & bad;
+            const bool ok = walk & !bad;
+            mine = j == g ? ok : mine;
+            mp = j == g ? p : mp;
+            ml = j == g ? len : ml;
+            mk = j == g ? k : mk;
+            p = ok ? p + 4 + len : p;
+            k += ok;
+            walk = ok & (p != end);
+        }
+        // my element: integer or string (zipTryEncoding, as quicklistPushTail stores it)
+        uint32_t b[6];
+        R.template get<6>(mp, b);
+        const uint32_t d[5] = {b[1], b[2], b[3], b[4], b[5]};
+        int64_t iv;
+        const bool isint = regs_try_int(d, ml, iv);
+        put_desc(l.E, mine ? l.slot(mk) : NOSLOT, isint ? (uint64_t)iv : l.B + mp + 4, isint ? 0 : ml,
+                 isint ? RR_K_INT : RR_K_STR, 0);
+        pay += mine && !isint ? ml : 0;
+        if (__ballot(walk) == 0) break;
+    }
+    n = k;
+    return fail || k != l.r;
+}
+
+// ---- Set / Hash hash tables, grouped.  A step reads the 8 bytes before p (they finish the
+// previous member's fingerprint) and the length field at p; the step at p == end only finishes
+// the last member.  Every lane of a group keeps the whole fingerprint register.
+template <class Src>
+__device__ __forceinline__ bool do_ht_g(const Src &R, const Head &H, const Lane &l, bool active, uint32_t G,
+                                        uint32_t g, uint32_t &n, uint64_t &pay, bool &fix, const bool hash) {
+    const uint64_t cnt = H.u5();
+#ifndef RR_HT_NOFP
+    const bool chk = active && cnt <= HT_FP_KEYS;
+#else   // timing-only builds (tools/): no fingerprints (duplicates go undetected)
+    const bool chk = false;
+#endif
+    bool dupfp = active && cnt > HT_FP_KEYS;
+    uint32_t p = l.q + 13, k = 0, plen = 0, s = 0;   // s: steps taken (k of every walking lane)
+    const uint32_t end = l.q + l.L;
+    bool fail = false, walk = active;
+    uint32_t fpr[HT_FP_KEYS / 2];
+#pragma unroll
+    for (uint32_t j = 0; j < HT_FP_KEYS / 2; ++j) fpr[j] = 0xFFFFFFFFu;
+    for (;;) {
+        uint32_t mp = 0, ml = 0, mk = 0;
+        bool mine = false;
+        for (uint32_t j = 0; j < G; ++j, ++s) {
+            uint32_t b[4];
+            R.template get<4>(p - 8, b);
+            if (s > 0 && (!hash || (s & 1))) {   // member s-1 is a key (s is wave-uniform)
+                const uint32_t f = member_fp16(plen, b[0], b[1]);
+                const uint32_t pat = f | (f << 16);
+                u16x2 m = __builtin_bit_cast(u16x2, fpr[0] ^ pat);
+#pragma unroll
+                for (uint32_t i = 1; i < HT_FP_KEYS / 2; ++i)
+                    m = __builtin_elementwise_min(m, __builtin_bit_cast(u16x2, fpr[i] ^ pat));
+                dupfp |= chk & walk & ((m.x == 0) | (m.y == 0));
+#pragma unroll
+                for (uint32_t i = HT_FP_KEYS / 2 - 1; i > 0; --i) fpr[i] = __builtin_amdgcn_alignbit(fpr[i], fpr[i - 1], 16);
+                fpr[0] = (fpr[0] << 16) | f;
+            }
+            const uint32_t rem = end - p;
+            const bool done = p == end;
+            const bool bad = (rem < 8) | (b[3] != 0) | (b[2] > rem - 8) | (k >= l.r);
+            fail |= walk & !done & bad;
+            const bool ok = walk & !done & !bad;
+            mine = j == g ? ok : mine;
+            mp = j == g ? p : mp;
+            ml = j == g ? b[2] : ml;
+            mk = j == g ? k : mk;
+            plen = b[2];
+            p = ok ? p + 8 + b[2] : p;
+            k += ok;
+            walk = ok;
+        }
+        put_desc(l.E, mine ? l.slot(mk) : NOSLOT, l.B + mp + 8, ml, RR_K_STR, 0);
+        pay += mine ? ml : 0;
+        if (__ballot(walk) == 0) break;
+    }
+    n = k;
+    const bool cnt_ok = !hash ? (uint64_t)k == cnt : ((k & 1) == 0 && (uint64_t)(k >> 1) == cnt);
+    fix = dupfp && k >= (hash ? 4u : 2u);
+    return fail || !cnt_ok || k != l.r;
+}
+
+// ---- ZSet skiplist, grouped: a step takes one (member, score) pair — the member's length
+// field, then the score after it (a second, dependent read); the order and NaN checks run on
+// every lane (see do_skiplist)
+template <class Src>
+__device__ __forceinline__ bool do_skiplist_g(const Src &R, const Head &H, const Lane &l, bool active, uint32_t G,
+                                              uint32_t g, uint32_t &n, uint64_t &pay) {
+    const uint64_t cnt = H.u5();
+    uint32_t p = l.q + 13, k = 0;   // k: pairs
+    const uint32_t end = l.q + l.L;
+    bool fail = false, walk = active && p != end;
+    double prev = 0.0;
+    for (;;) {
+        uint32_t mp = 0, ml = 0, mk = 0, s0 = 0, s1 = 0;
+        bool mine = false;
+        for (uint32_t j = 0; j < G; ++j) {
+            uint32_t a[2], c[2];
+            R.template get<2>(p, a);
+            const uint32_t rem = end - p;
+            const bool bad1 = (rem < 16) | (a[1] != 0) | (a[0] > rem - 16) | (2 * k + 1 >= l.r);
+            const uint32_t sp = p + 8 + a[0];
+            R.template get<2>(bad1 ? p : sp, c);
+            const double sc = __longlong_as_double((long long)((uint64_t)c[0] | ((uint64_t)c[1] << 32)));
+            const bool order = k == 0 ? !(sc != sc) : sc < prev;
+            const bool bad = bad1 | !order;
+            fail |= walk & bad;
+            const bool ok = walk & !bad;
+            mine = j == g ? ok : mine;
+            mp = j == g ? p : mp;
+            ml = j == g ? a[0] : ml;
+            mk = j == g ? k : mk;
+            s0 = j == g ? c[0] : s0;
+            s1 = j == g ? c[1] : s1;
+            prev = ok ? sc : prev;
+            p = ok ? sp + 8 : p;
+            k += ok;
+            walk = ok & (p != end);
+        }
+        put_desc(l.E, mine ? l.slot(2 * mk) : NOSLOT, l.B + mp + 8, ml, RR_K_STR, 0);
+        put_desc(l.E, mine ? l.slot(2 * mk + 1) : NOSLOT, (uint64_t)s0 | ((uint64_t)s1 << 32), 0, RR_K_SCORE, 0);
+        pay += mine ? ml : 0;
+        if (__ballot(walk) == 0) break;
+    }
+    n = 2 * k;
+    return fail || (uint64_t)k != cnt || 2 * k != l.r;
+}
+
+// ---- intset, grouped: members at fixed positions, lane g takes members g, g + G, ...; the
+// width (2 / 4 / 8, per lane) is a bit-field width, not a branch
+template <class Src>
+__device__ __forceinline__ void do_intset_g(const Src &R, const Head &H, const Lane &l, bool active, uint32_t G,
+                                            uint32_t g) {
+    const uint32_t w = H.f5(), cnt = active && l.ok ? H.f9() : 0;
+    for (uint32_t k0 = 0; __ballot(k0 + g < cnt) != 0; k0 += G) {
+        const uint32_t k = k0 + g;
+        const bool live = k < cnt;
+        uint32_t x[2];
+        R.template get<2>(l.q + 13 + (live ? w * k : 0u), x);
+        const uint32_t lo = w == 2 ? (uint32_t)__builtin_amdgcn_sbfe((int)x[0], 0, 16) : x[0];
+        const uint32_t hi = w == 8 ? x[1] : (uint32_t)((int32_t)lo >> 31);
+        put_desc(l.E, live ? l.so + 16 * k : NOSLOT, (uint64_t)lo | ((uint64_t)hi << 32), 0, RR_K_INT, 0);
+    }
+}
+
 // ---- Hash / ZSet ziplists (rock_serdes.c:314-346, :417-446; ziplist.c:300-447): element 0
 // is the raw ziplist, then one descriptor per entry.
 // Two lanes per value walk it from both ends (ziplist.c:300-330: an entry's prevlen field gives

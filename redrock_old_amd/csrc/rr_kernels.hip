@@ -707,8 +707,12 @@ __constant__ uint32_t CLASS_ORDER[C_N] = {C_ZL, C_SL, C_HH, C_HT, C_LIST, C_EXAC
 // offsets relative to the source, whose byte 0 is batch offset B).  The walks run the wave in
 // lock-step (rr_decode_class.h); values they reject, and the EXACT class, go to the exact
 // parser lane by lane.
+// G lanes per value (grouped walks, rr_decode_class.h), this lane being lane g of its group;
+// the group's lane 0 records the value (or runs the exact parser), every lane returns the
+// payload of the elements it stored.
 template <class Src>
-__device__ __forceinline__ Acc run_batch(const Src &src, uint32_t c, bool active, uint64_t v, uint64_t B, rsrc_t E,
+__device__ __forceinline__ Acc run_batch(const Src &src, uint32_t c, bool active, uint64_t v, uint32_t G, uint32_t g,
+                                         uint64_t B, rsrc_t E,
                                          uint64_t eb0, const uint8_t *__restrict__ blob,
                                          const uint64_t *__restrict__ offsets, const uint64_t *__restrict__ ebase,
                                          rr_value *__restrict__ values, rr_elem *__restrict__ elems, uint64_t cap,
@@ -740,26 +744,28 @@ __device__ __forceinline__ Acc run_batch(const Src &src, uint32_t c, bool active
             if (active) do_string(H, l, vp);
             enc = H.b5();
         } else if (c == C_IS) {
-            do_intset(src, H, l, active);
+            do_intset_g(src, H, l, active, G, g);
             ne = H.f9();
             enc = H.f5();
         } else if (c == C_LIST) {
-            fail = do_list(src, l, active, ne, vp);
-        } else if (c == C_HT || c == C_HH) {
+            fail = do_list_g(src, l, active, G, g, ne, vp);
+        } else if (c == C_HT || c == C_HH) {   // (lane per value: the fingerprints are chain work)
             fail = do_ht(src, H, l, active, ne, vp, fixup, c == C_HH);
         } else if (c == C_SL) {
-            fail = do_skiplist(src, H, l, active, ne, vp);
-        } else {   // C_ZL: two lanes per value, the odd one walks backward (its results are unused)
-            const bool back = (lane_id() & 1) != 0;
-            fail = do_ziplist(src, l, active, back, ne, vp);
-            active &= !back;
+            fail = do_skiplist_g(src, H, l, active, G, g, ne, vp);
+        } else {   // C_ZL: G == 2, lane 1 of the pair walks backward
+            fail = do_ziplist(src, l, active, g != 0, ne, vp);
         }
         exact = fail;
         if (active && !fail) {
-            if (fixup && l.ok) queue_fixup(fix, v);
-            put_value(values + v, H.type(), enc, l.ok ? RR_OK : RR_E_CAPACITY, H.lru(), ne, (uint32_t)eb);
-            acc = Acc{l.ok ? 0u : 1u, l.ok ? vp : 0};
+            if (g == 0) {
+                if (fixup && l.ok) queue_fixup(fix, v);
+                put_value(values + v, H.type(), enc, l.ok ? RR_OK : RR_E_CAPACITY, H.lru(), ne, (uint32_t)eb);
+                acc.bad = l.ok ? 0u : 1u;
+            }
+            acc.pay = l.ok ? vp : 0;
         }
+        active &= g == 0;   // the exact parser runs once per value, on the group's lane 0
     }
     if (active && exact) acc = exact_value(blob, v, offsets, ebase, values, elems, cap, fix);
     return acc;
@@ -767,12 +773,12 @@ __device__ __forceinline__ Acc run_batch(const Src &src, uint32_t c, bool active
 
 // the unstaged (global-memory) instantiation: cold path, kept out of line in RR_DEC_NOINL
 // builds so the hot staged code stays small
-__device__ RR_COLD Acc run_batch_g(const GlbSrc &src, uint32_t c, bool active, uint64_t v, uint64_t B, rsrc_t E,
-                                   uint64_t eb0, const uint8_t *__restrict__ blob,
+__device__ RR_COLD Acc run_batch_g(const GlbSrc &src, uint32_t c, bool active, uint64_t v, uint32_t G, uint32_t g,
+                                   uint64_t B, rsrc_t E, uint64_t eb0, const uint8_t *__restrict__ blob,
                                    const uint64_t *__restrict__ offsets, const uint64_t *__restrict__ ebase,
                                    rr_value *__restrict__ values, rr_elem *__restrict__ elems, uint64_t cap,
                                    uint64_t *fix) {
-    return run_batch(src, c, active, v, B, E, eb0, blob, offsets, ebase, values, elems, cap, fix);
+    return run_batch(src, c, active, v, G, g, B, E, eb0, blob, offsets, ebase, values, elems, cap, fix);
 }
 
 // Workgroup per byte WINDOW of W bytes: window t owns the values whose first byte lies in
@@ -1006,15 +1012,20 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
             if ((RR_SKIP_CLASSES >> c) & 1) continue;
 #endif
             PROBE(const uint64_t tb0 = __builtin_amdgcn_s_memtime();)
-            const uint32_t li = c == C_ZL ? lane >> 1 : lane;   // the value's index in the batch
+            // lanes per value: ziplists 2 (two-ended walk), chained classes 64 / cnt (grouped walks)
+            const bool grouped = c == C_LIST || c == C_SL || c == C_IS;
+            const uint32_t G = __builtin_amdgcn_readfirstlane(
+                c == C_ZL ? 2u : grouped ? max(1u, min(GMAX, (uint32_t)RR_WAVE / cnt)) : 1u);
+            const uint32_t li = lane / G, g = lane - li * G;   // the value's index in the batch
             const bool active = li < cnt;
             const uint64_t v = c0 + (active ? perm[first + li] : 0u);
 #ifndef RR_DEC_NOGLOBAL
-            const Acc a = staged ? run_batch(lsrc, c, active, v, S0, E, eb0, blob, offsets, ebase, values, elems, cap, fix)
-                                 : run_batch_g(gsrc, c, active, v, S0, E, eb0, blob, offsets, ebase, values, elems, cap,
-                                               fix);
+            const Acc a = staged ? run_batch(lsrc, c, active, v, G, g, S0, E, eb0, blob, offsets, ebase, values, elems,
+                                             cap, fix)
+                                 : run_batch_g(gsrc, c, active, v, G, g, S0, E, eb0, blob, offsets, ebase, values,
+                                               elems, cap, fix);
 #else   // timing-only builds (tools/): no unstaged walks (wrong for windows that overflow the stage)
-            const Acc a = run_batch(lsrc, c, active, v, S0, E, eb0, blob, offsets, ebase, values, elems, cap, fix);
+            const Acc a = run_batch(lsrc, c, active, v, G, g, S0, E, eb0, blob, offsets, ebase, values, elems, cap, fix);
             (void)gsrc;
 #endif
             bad += a.bad;
