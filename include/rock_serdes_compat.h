@@ -1,14 +1,24 @@
 /*
- * rock_serdes_compat.h — the legacy single-value signatures of RedRock's serdes
- * (src/rock_serdes.h:47-49), kept for a drop-in build inside a Redis tree.
+ * rock_serdes_compat.h — RedRock's legacy serdes entry points (src/rock_serdes.h:47-49) on
+ * the MI355X engine, for a build inside a Redis tree.
  *
- * These need Redis's robj/sds types (server.h), so they are only declared when the file is
- * compiled inside a RedRock tree (-DRR_REDIS_TREE, after #include "server.h").  Their bodies
- * flatten an robj into the rr_format.h form, run a batch of one through rr_serdes.h and turn
- * any nonzero per-value status into serverPanic() — the reference's abort-on-malformed
- * semantics (rock_serdes.c asserts).  Status: SURVEY.md §8f row f1 ("next"); see
- * INTEGRATION.md for the patch to rock.c (:468, :538, :691) that switches callers to the
- * batch entry points instead.
+ * The bodies are redrock_old_amd/compat/rock_serdes_compat.c.  They need Redis's robj / sds /
+ * dict / quicklist / intset / skiplist (server.h), so this header declares them only when
+ * compiled inside a RedRock tree: -DRR_REDIS_TREE, after #include "server.h".
+ *
+ *   desObject / desString   the blob goes through rr_decode_batch_host (the GPU decode), the
+ *                           robj is built on the host from the flat records — heap objects
+ *                           cannot be built on the device;
+ *   serObject               the robj is flattened on the host, rr_encode_batch_host writes
+ *                           the blob (the GPU encode), returned as a fresh zmalloc'd sds;
+ *   any nonzero per-value status, and any engine error, ends in serverPanic() — the
+ *   reference aborts through serverAssert/serverPanic on the same inputs (rock_serdes.c).
+ *
+ * One value per call pays a kernel launch; the batch forms below are what the RedRock call
+ * sites should use: the rock thread's restore queue (rock.c:302-383, one key per RockJob
+ * today, server.h:1013-1019) and the fork child's snapshot loads (rock.c:527-540) restore
+ * many keys per call, and the evictor (rock_hotkey.c:315-455) dumps many victims per call.
+ * INTEGRATION.md shows the patches.
  */
 #ifndef ROCK_SERDES_COMPAT_H
 #define ROCK_SERDES_COMPAT_H
@@ -16,10 +26,19 @@
 #include "rr_serdes.h"
 
 #ifdef RR_REDIS_TREE
-/* rock_serdes.h:47 declares 2 args; the definition (rock_serdes.c:133) takes the lru too. */
-robj *desString(char *s, size_t len);
+/* rock_serdes.h:47 declares 2 args; the definition (rock_serdes.c:133) takes the lru too, and
+ * that is the one provided (nothing outside rock_serdes.c calls it). */
+robj *desString(char *s, size_t len, uint32_t lru);
 sds serObject(robj *o);                 /* rock_serdes.h:48, rock_serdes.c:512 */
 robj *desObject(void *buf, size_t len); /* rock_serdes.h:49, rock_serdes.c:538 */
+
+/* Batch forms: n blobs -> n robj (out[i] == desObject(bufs[i], lens[i])), n robj -> n sds
+ * (out[i] == serObject(objs[i])), one engine call each. */
+void rr_compat_des_batch(void *const *bufs, const size_t *lens, size_t n, robj **out);
+void rr_compat_ser_batch(robj *const *objs, size_t n, sds *out);
+
+/* GPU the calling thread's engine context is created on (default 0; set before first use). */
+void rr_compat_set_device(int device);
 #endif
 
 #endif

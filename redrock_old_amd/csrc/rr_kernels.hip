@@ -302,10 +302,9 @@ __device__ __forceinline__ void tile_stats(uint64_t *stats, uint32_t tile, uint6
 // mode 0 (decode): bytes = offsets[n]; mode 1 (encode): bytes = inclusive prefix of the last
 // tile.  Many blocks (one CU reads ~60 GB/s: a single-block fold of 121K tiles took 56 us),
 // each folding a slice and adding into *out, which the launcher zeroes first.
-__global__ __launch_bounds__(256) void finalize_kernel(const uint64_t *__restrict__ stats, uint64_t *state,
-                                                       uint32_t ntiles, const uint64_t *__restrict__ offsets,
-                                                       uint64_t n, int mode, rr_totals *out,
-                                                       const uint64_t *__restrict__ extra, uint64_t *err) {
+__device__ __forceinline__ void fold_totals(const uint64_t *__restrict__ stats, uint64_t *state, uint32_t ntiles,
+                                            const uint64_t *__restrict__ offsets, uint64_t n, int mode, rr_totals *out,
+                                            const uint64_t *__restrict__ extra, uint64_t *err) {
     __shared__ uint64_t red[3][4];
     uint64_t b = 0, p = 0, c = 0;
     for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < ntiles; t += gridDim.x * blockDim.x) {
@@ -340,11 +339,17 @@ __global__ __launch_bounds__(256) void finalize_kernel(const uint64_t *__restric
     }
 }
 
+__global__ __launch_bounds__(256) void finalize_kernel(const uint64_t *__restrict__ stats, uint64_t *state,
+                                                       uint32_t ntiles, const uint64_t *__restrict__ offsets,
+                                                       uint64_t n, int mode, rr_totals *out,
+                                                       const uint64_t *__restrict__ extra, uint64_t *err) {
+    fold_totals(stats, state, ntiles, offsets, n, mode, out, extra, err);
+}
+
+// (the totals were zeroed by the pipeline's first kernel)
 static hipError_t launch_finalize(const uint64_t *stats, uint64_t *state, uint32_t ntiles, const uint64_t *offsets,
                                   uint64_t n, int mode, rr_totals *out, hipStream_t stream, uint64_t *err,
                                   const uint64_t *extra = nullptr) {
-    hipError_t e = hipMemsetAsync(out, 0, sizeof(rr_totals), stream);
-    if (e != hipSuccess) return e;
     uint32_t blocks = (ntiles + 255) / 256;
     if (blocks > 512) blocks = 512;
     if (blocks < 1) blocks = 1;
@@ -565,12 +570,23 @@ __device__ __forceinline__ void reserve_classify(const uint8_t *b, uint64_t L, c
     }
 }
 
+// Block 0 also zeroes the pipeline's per-call words (look-back state, fixup header) and the
+// totals: later kernels of the same stream use them, so no separate memset launch is needed.
+__device__ __forceinline__ void zero_call_words(uint64_t *words, uint32_t nwords, rr_totals *tot) {
+    if (blockIdx.x != 0) return;
+    for (uint32_t k = threadIdx.x; k < nwords; k += blockDim.x) words[k] = 0;
+    if (tot && threadIdx.x < 4) reinterpret_cast<uint64_t *>(tot)[threadIdx.x] = 0;
+}
+
 __global__ __launch_bounds__(256) void count_kernel(const uint8_t *__restrict__ blob,
                                                     const uint64_t *__restrict__ offsets, uint64_t n,
                                                     uint32_t *__restrict__ first_val, uint32_t nwin, uint32_t win,
-                                                    uint64_t *__restrict__ counts, uint8_t *__restrict__ cls) {
+                                                    uint64_t *__restrict__ counts, uint8_t *__restrict__ cls,
+                                                    uint64_t *zero_words, uint32_t nzero, rr_totals *tot) {
+    zero_call_words(zero_words, nzero, tot);
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i > n) return;
+    if (i == n) counts[n] = 0;   // (the scan writes the total here when there are values)
     // first_val[w] = first value whose first byte is at or after w*win (windows past the
     // last value start, and the sentinel nwin, get n)
     const uint64_t o_hi = offsets[i];
@@ -1197,8 +1213,9 @@ __device__ void fix_sort_skiplist(const uint8_t *__restrict__ blob, rr_elem *__r
     }
 }
 
-__global__ __launch_bounds__(FIX_NT) void fixup_kernel(const uint8_t *__restrict__ blob, uint64_t *fix,
-                                                       rr_value *__restrict__ values, rr_elem *__restrict__ elems) {
+__device__ __forceinline__ void fixup_values(const uint8_t *__restrict__ blob, uint64_t *fix,
+                                             rr_value *__restrict__ values, rr_elem *__restrict__ elems,
+                                             rr_totals *out) {
     __shared__ unsigned long long tab[FIX_TAB];
     __shared__ uint64_t wsum[FIX_NT / RR_WAVE];
     __shared__ uint32_t sh_flag;   // bit 0: a duplicate key, bit 1: a pass overflowed the table
@@ -1284,13 +1301,14 @@ __global__ __launch_bounds__(FIX_NT) void fixup_kernel(const uint8_t *__restrict
                 const uint32_t nk2 = per == 2 ? 0u : (uint32_t)kept;
                 for (uint32_t i = nk2 + tid; i < n; i += FIX_NT) reinterpret_cast<uint4 *>(el)[i] = make_uint4(0, 0, 0, 0);
                 dropped = wave_sum(dropped);
-                if (lane_id() == 0 && dropped) atomicAdd((unsigned long long *)&fix[3], (unsigned long long)(0ull - dropped));
+                if (lane_id() == 0 && dropped && out)
+                    atomicAdd((unsigned long long *)&out->payload, (unsigned long long)(0ull - dropped));
                 if (tid == 0) {
                     uint4 w = rv;
                     w.z = nk2;
                     if (per == 2) {
                         w.x = (rv.x & 0xFFFFu) | ((uint32_t)RR_E_DUP << 16);
-                        atomicAdd((unsigned long long *)&fix[2], 1ull);
+                        if (out) atomicAdd((unsigned long long *)&out->n_bad, 1ull);
                     }
                     reinterpret_cast<uint4 *>(values)[v] = w;
                 }
@@ -1298,6 +1316,18 @@ __global__ __launch_bounds__(FIX_NT) void fixup_kernel(const uint8_t *__restrict
         }
         __syncthreads();
     }
+}
+
+// ---- K4: the decode's last kernel: the fixup pass over the queued values (their totals
+// changes added straight into the zeroed totals), then the fold of the windows' totals
+__global__ __launch_bounds__(FIX_NT) void decode_post_kernel(const uint8_t *__restrict__ blob, uint64_t *fix,
+                                                             rr_value *__restrict__ values,
+                                                             rr_elem *__restrict__ elems,
+                                                             const uint64_t *__restrict__ stats, uint64_t *state,
+                                                             uint32_t ntiles, const uint64_t *__restrict__ offsets,
+                                                             uint64_t n, rr_totals *out) {
+    fixup_values(blob, fix, values, elems, out);
+    if (out) fold_totals(stats, state, ntiles, offsets, n, 2, out, nullptr, fix + 1);
 }
 
 // ---------------------------------------------------------------------------------------- encode
@@ -1432,7 +1462,9 @@ __device__ uint64_t encode_size(uint32_t type, uint32_t enc, uint32_t vstatus, u
 __global__ __launch_bounds__(256) void enc_size_kernel(const rr_value *__restrict__ values,
                                                        const rr_elem *__restrict__ elems, uint64_t n,
                                                        uint64_t ecap, uint64_t acap,
-                                                       uint64_t *__restrict__ sizes, uint64_t *__restrict__ stats) {
+                                                       uint64_t *__restrict__ sizes, uint64_t *__restrict__ stats,
+                                                       uint64_t *zero_words, uint32_t nzero, rr_totals *tot) {
+    zero_call_words(zero_words, nzero, tot);
     __shared__ uint64_t red[3][4];
     const uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint64_t size = 0, pay = 0, ne = 0, bad = 0;
@@ -1928,24 +1960,16 @@ extern "C" hipError_t rr_launch_decode(const uint8_t *blob, const uint64_t *offs
     uint64_t *stats = counts + n + 1;
     uint32_t *first_val = reinterpret_cast<uint32_t *>(stats + 3 * (uint64_t)nw);
     uint8_t *cls = reinterpret_cast<uint8_t *>(first_val + ((nw + 2) & ~1u));
-    hipError_t e = hipMemsetAsync(lb, 0, (((lb_words + FIX_HDR) * 8) + 15) & ~(size_t)15, stream);
-    if (e != hipSuccess) return e;
     hipLaunchKernelGGL(count_kernel, dim3((uint32_t)((n + 1 + 255) / 256)), dim3(256), 0, stream, blob, offsets, n,
-                       first_val, nw, DEC_W, counts, cls);
+                       first_val, nw, DEC_W, counts, cls, lb, (uint32_t)(lb_words + FIX_HDR), totals);
     if (st) hipLaunchKernelGGL(scan_kernel, dim3(st), dim3(256), 0, stream, counts, n, lb, st, fix + 1);
-    else {
-        e = hipMemsetAsync(counts, 0, sizeof(uint64_t), stream);
-        if (e != hipSuccess) return e;
-    }
     hipLaunchKernelGGL((DECODE_KERNEL), dim3(nw), dim3(DEC_NW * RR_WAVE), 0, stream, blob, data_cap, offsets, n,
                        first_val, cls, counts, values, elems, elem_cap, arena, stats, fix);
-    static uint32_t fix_grid = 0;
-    if (!fix_grid) fix_grid = resident_grid(fixup_kernel, FIX_NT, false);
-    hipLaunchKernelGGL(fixup_kernel, dim3(fix_grid), dim3(FIX_NT), 0, stream, blob, fix, values, elems);
-    e = hipGetLastError();
-    if (e == hipSuccess && totals)
-        e = launch_finalize(stats, counts + n, nw, offsets, n, 2, totals, stream, fix + 1, fix + 2);
-    return e;
+    static uint32_t post_grid = 0;
+    if (!post_grid) post_grid = resident_grid(decode_post_kernel, FIX_NT, false);
+    hipLaunchKernelGGL(decode_post_kernel, dim3(post_grid), dim3(FIX_NT), 0, stream, blob, fix, values, elems, stats,
+                       counts + n, nw, offsets, n, totals);
+    return hipGetLastError();
 }
 
 // Encode scratch (uint64 words): [HDR] [scan: ticket, look-back state + groups]
@@ -1978,10 +2002,8 @@ extern "C" hipError_t rr_launch_encode(const rr_value *values, const rr_elem *el
     uint64_t *err = lb + lb_words;   // device error word (look-back timeout)
     uint64_t *stats = err + 1;
     uint32_t *fv = reinterpret_cast<uint32_t *>(stats + 6 * (uint64_t)t);
-    e = hipMemsetAsync(lb, 0, (((lb_words + 1) * 8) + 15) & ~(size_t)15, stream);
-    if (e != hipSuccess) return e;
     hipLaunchKernelGGL(enc_size_kernel, dim3(t), dim3(256), 0, stream, values, elems, n, elem_cap, arena_cap, offsets,
-                       stats);
+                       stats, lb, (uint32_t)(lb_words + 1), totals);
     hipLaunchKernelGGL(scan_kernel, dim3(st), dim3(256), 0, stream, offsets, n, lb, st, err);
     hipLaunchKernelGGL(enc_index_kernel<ENC_W>, dim3(t), dim3(256), 0, stream, values, elems, n, elem_cap, arena_cap,
                        offsets, cap, fv, nw, stats + 3 * (uint64_t)t);

@@ -1,0 +1,73 @@
+/*
+ * test_compat.c — unit test of the legacy-signature shim (redrock_old_amd/compat/
+ * rock_serdes_compat.c) through desObject / desString / serObject and the batch forms,
+ * over the golden fixtures (tests/golden/kat.json, K1-K9 + edge cases; written into
+ * fixtures.h by tests/test_compat.py).  Links the engine library (the decode / encode run on
+ * the GPU) and the minimal Redis model (tests/c/miniredis).
+ *
+ * Every fixture:  status != 0  -> desObject must panic (the reference's serverAssert site);
+ *                 status == 0  -> serObject(desObject(b)) must be the blob serObject writes for
+ *                                 the object desObject built (the fixture's "reencoded", lru
+ *                                 masked to 24 bits), and desString must keep the caller's lru.
+ * Exit status 0 when every check passes.
+ */
+#include <stdio.h>
+#include <string.h>
+
+#include "server.h"
+#include "rock_serdes_compat.h"
+#include "fixtures.h"
+
+static int fails;
+#define CHECK(c, ...) do { if (!(c)) { fails++; printf("FAIL %s: ", fx->name); printf(__VA_ARGS__); printf("\n"); } } while (0)
+
+int main(void) {
+    int checked = 0, panics = 0;
+    robj *objs[N_FIXTURES];
+    void *bufs[N_FIXTURES];
+    size_t lens[N_FIXTURES], nok = 0;
+    const fixture_t *okfx[N_FIXTURES];
+    for (int i = 0; i < N_FIXTURES; i++) {
+        const fixture_t *fx = &FIXTURES[i];
+        jmp_buf jb;
+        mr_panic_jmp = &jb;
+        robj *volatile o = NULL;
+        if (setjmp(jb) == 0) {
+            o = desObject((void *)fx->blob, fx->len);
+        } else {
+            CHECK(fx->status != 0, "desObject panicked on a valid blob: %s", mr_panic_msg);
+            if (fx->status) panics++;
+            continue;
+        }
+        CHECK(fx->status == 0, "desObject accepted a blob the reference rejects (status %d)", fx->status);
+        if (fx->status) continue;
+        sds s = serObject(o);
+        CHECK(sdslen(s) == fx->out_len && !memcmp(s, fx->out, fx->out_len), "serObject(desObject(b)) differs (%zu vs %zu bytes)",
+              sdslen(s), fx->out_len);
+        if (fx->blob[0] == 0) {   /* String: desString keeps the caller's lru */
+            robj *o2 = desString((char *)fx->blob, fx->len, 77);
+            CHECK(o2->lru == 77 && o2->type == OBJ_STRING && o2->encoding == o->encoding, "desString");
+            decrRefCount(o2);
+        }
+        sdsfree(s);
+        decrRefCount(o);
+        bufs[nok] = (void *)fx->blob;
+        lens[nok] = fx->len;
+        okfx[nok++] = fx;
+        checked++;
+    }
+    /* the batch forms: every valid fixture in one decode call and one encode call */
+    mr_panic_jmp = NULL;
+    rr_compat_des_batch(bufs, lens, nok, objs);
+    sds outs[N_FIXTURES];
+    rr_compat_ser_batch(objs, nok, outs);
+    for (size_t i = 0; i < nok; i++) {
+        const fixture_t *fx = okfx[i];
+        CHECK(sdslen(outs[i]) == fx->out_len && !memcmp(outs[i], fx->out, fx->out_len), "batch round trip differs");
+        sdsfree(outs[i]);
+        decrRefCount(objs[i]);
+    }
+    printf("compat shim: %d fixtures round-tripped, %d rejected with a panic, batch of %zu; %d failures\n", checked,
+           panics, nok, fails);
+    return fails ? 1 : 0;
+}

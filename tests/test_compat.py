@@ -1,0 +1,74 @@
+"""The legacy-signature compat shim: redrock_old_amd/compat/
+rock_serdes_compat.c — desObject / desString / serObject (rock_serdes.h:47-49) plus batch
+forms over the engine's C-ABI — compiled as C with a minimal Redis model (tests/c/miniredis)
+into a C test program (tests/c/test_compat.c) that runs every golden fixture through the
+legacy signatures.  CPU: the program compiles and links against the engine library.  GPU:
+it runs (the shim's decode and encode are the GPU engine) and passes."""
+import json
+import os
+import struct
+import subprocess
+
+import pytest
+
+from helpers import golden
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _c_bytes(b):
+    return "{" + ",".join(str(x) for x in b) + "}" if b else "{0}"
+
+
+def write_fixtures(path):
+    G = golden()
+    fx = G["kats"] + G["edges"]
+    lines = ["typedef struct { const char *name; const unsigned char *blob; size_t len; int status;",
+             "                 const unsigned char *out; size_t out_len; } fixture_t;"]
+    for i, f in enumerate(fx):
+        blob = bytes.fromhex(f["blob"])
+        out = bytes.fromhex(f.get("reencoded", f["blob"]))
+        if len(out) >= 5:   # serObject writes robj.lru: 24 bits (server.h:592-599)
+            out = out[:1] + struct.pack("<I", struct.unpack_from("<I", out, 1)[0] & 0xFFFFFF) + out[5:]
+        lines.append(f"static const unsigned char B{i}[] = {_c_bytes(blob)};")
+        lines.append(f"static const unsigned char O{i}[] = {_c_bytes(out)};")
+    lines.append(f"#define N_FIXTURES {len(fx)}")
+    lines.append("static const fixture_t FIXTURES[N_FIXTURES] = {")
+    for i, f in enumerate(fx):
+        blob = bytes.fromhex(f["blob"])
+        out_len = len(bytes.fromhex(f.get("reencoded", f["blob"])))
+        lines.append(f'  {{"{f["name"]}", B{i}, {len(blob)}, {f["value"].get("status", 0)}, O{i}, {out_len}}},')
+    lines.append("};")
+    with open(path, "w") as fh:
+        fh.write("\n".join(lines) + "\n")
+
+
+def build(tmp):
+    write_fixtures(os.path.join(tmp, "fixtures.h"))
+    exe = os.path.join(tmp, "test_compat")
+    cmd = ["gcc", "-std=gnu11", "-O1", "-Wall", "-Werror", "-Wno-unused-function", "-DRR_REDIS_TREE",
+           "-I", os.path.join(ROOT, "tests", "c", "miniredis"), "-I", os.path.join(ROOT, "include"), "-I", tmp,
+           os.path.join(ROOT, "redrock_old_amd", "compat", "rock_serdes_compat.c"),
+           os.path.join(ROOT, "tests", "c", "miniredis", "miniredis.c"),
+           os.path.join(ROOT, "tests", "c", "test_compat.c"),
+           "-L", os.path.join(ROOT, "redrock_old_amd"), "-lrr_serdes",
+           "-Wl,-rpath," + os.path.join(ROOT, "redrock_old_amd"), "-o", exe]
+    subprocess.run(cmd, check=True)
+    return exe
+
+
+def test_compat_shim_builds_as_c(tmp_path):
+    exe = build(str(tmp_path))
+    assert os.path.exists(exe)
+    nm = subprocess.run(["nm", exe], capture_output=True, text=True, check=True).stdout
+    for sym in ("desObject", "desString", "serObject", "rr_compat_des_batch", "rr_compat_ser_batch"):
+        assert f" T {sym}" in nm, sym
+
+
+@pytest.mark.gpu
+def test_compat_shim_round_trips_fixtures_on_gpu(tmp_path):
+    exe = build(str(tmp_path))
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    print(r.stdout, r.stderr)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "0 failures" in r.stdout
