@@ -109,6 +109,49 @@ int rr_encode_batch_host(rr_ctx *ctx, const rr_value *values, const rr_elem *ele
                          uint64_t n, uint8_t *data, uint64_t data_cap, uint64_t *offsets,
                          rr_totals *totals);
 
+/* ---- multi-GPU sharding ---------------------------------------------- */
+/* Values are independent: a batch splits into G contiguous value ranges balanced by bytes,
+ * shard k starting at the first value whose first byte is at or after k * total / G; each GPU
+ * decodes / encodes its shard with the single-GPU calls, and RCCL over xGMI moves data only
+ * for a root split or gather (one process per GPU, one rr_comm per process). */
+typedef struct rr_shard {
+    uint64_t v0, v1;        /* values [v0, v1) of the whole batch */
+    uint64_t b0, b1;        /* their bytes [b0, b1) = offsets[v0], offsets[v1] */
+} rr_shard;
+
+/* Host: the byte-balanced plan of a batch (host offsets, n+1 entries) into g shards. */
+int rr_shard_plan(const uint64_t *offsets, uint64_t n, uint32_t g, rr_shard *plan);
+/* Device, in place: place a decoded shard in the whole batch — values' elem_base += elem_add,
+ * STR / ZLRAW arena offsets += byte_add (zero-filled slots of malformed values stay zero). */
+int rr_flat_rebase(rr_ctx *ctx, rr_value *values, uint64_t n, rr_elem *elems, uint64_t n_elems,
+                   uint64_t elem_add, uint64_t byte_add, void *stream);
+
+typedef struct rr_comm rr_comm;
+#define RR_COMM_ID_BYTES 128
+/* One rank creates the id and hands it to every rank by its own means (MPI, a file, a
+ * torch.distributed broadcast, ...); every rank then calls rr_comm_init (collective). */
+int rr_comm_get_id(uint8_t id[RR_COMM_ID_BYTES]);
+int rr_comm_init(rr_ctx *ctx, int nranks, int rank, const uint8_t id[RR_COMM_ID_BYTES], rr_comm **out);
+void rr_comm_destroy(rr_comm *comm);
+
+/* Collective.  The root holds the whole batch (device); every rank gets the plan (nranks
+ * entries, host memory) so it can size its shard buffers.  Blocks until the plan is known. */
+int rr_split_plan(rr_comm *comm, const rr_blob_batch *whole, int root, rr_shard *plan, void *stream);
+/* Collective.  Each rank receives its shard: mine->data (>= its b1 - b0 bytes, 16-byte
+ * aligned) and mine->offsets (v1 - v0 + 1 entries, rebased to 0); mine->n is set.  The root
+ * sends ncclSend slices over xGMI.  Asynchronous on `stream`.  The root may take its shard in
+ * place (mine->data == whole->data + b0, mine->offsets == whole->offsets + v0) only when its
+ * shard starts at byte 0 (root 0): the rebase rewrites those offsets. */
+int rr_split(rr_comm *comm, const rr_blob_batch *whole, const rr_shard *plan, int root, rr_blob_batch *mine,
+             void *stream);
+/* Collective.  Every rank passes its decoded shard (mine: n values, mine_elems descriptor
+ * slots = that decode's rr_totals.n_elems); the root receives all shards into whole->values /
+ * whole->elems at their places and rebases them, so whole equals a decode of the whole batch
+ * (whose arena is the whole blob buffer: the arena mirrors it, nothing moves).  Blocks until
+ * the shards' sizes are known (an all-gather of one word per rank). */
+int rr_gather(rr_comm *comm, const rr_flat_batch *mine, uint64_t mine_elems, const rr_shard *plan, int root,
+              rr_flat_batch *whole, void *stream);
+
 /* ---- synthetic batches (BASELINE.json configs) ------------------------ */
 /* config: 1 = 64-B RAW strings, 2 = Zipf 16B-4KiB strings, 3 = 16-pair hash ziplists,
  *         4 = mixed (config-4 proportions; also the 1M headline batch and config 5 shards),

@@ -31,7 +31,7 @@ T_SET_INTSET, T_ZSET_ZIPLIST, T_HASH_ZIPLIST, T_LIST_QUICKLIST = 11, 12, 13, 14
 K_STR, K_INT, K_SCORE, K_ZLRAW = 0, 1, 2, 3
 STATUS_NAMES = {0: "OK", 1: "SHORT", 2: "TYPE", 3: "STR_ENC", 4: "STR_INTLEN", 5: "EMBSTR_LEN",
                 6: "TRUNC", 7: "COUNT", 8: "INTSET", 9: "ZL_LEN", 10: "ZL_CORRUPT", 11: "CAPACITY",
-                12: "ENCODE"}
+                12: "ENCODE", 13: "DUP", 14: "NAN"}
 
 CONFIG_MIXED = 4
 
@@ -57,6 +57,10 @@ class FlatBatch(C.Structure):
                 ("elem_cap", C.c_uint64), ("arena_cap", C.c_uint64)]
 
 
+class Shard(C.Structure):
+    _fields_ = [("v0", C.c_uint64), ("v1", C.c_uint64), ("b0", C.c_uint64), ("b1", C.c_uint64)]
+
+
 class HostBatch(C.Structure):
     _fields_ = [("data", C.POINTER(C.c_uint8)), ("offsets", C.POINTER(C.c_uint64)), ("n", C.c_uint64),
                 ("bytes", C.c_uint64)]
@@ -65,7 +69,9 @@ class HostBatch(C.Structure):
 # Every symbol include/rr_serdes.h declares (the ABI test checks they are all exported).
 EXPORTS = ["rr_ctx_create", "rr_ctx_destroy", "rr_ctx_reserve", "rr_last_error", "rr_decode_batch",
            "rr_encode_batch", "rr_decode_elem_bound", "rr_decode_batch_host", "rr_encode_batch_host",
-           "rr_gen_batch", "rr_host_batch_free", "rr_gen_default_seed"]
+           "rr_gen_batch", "rr_host_batch_free", "rr_gen_default_seed", "rr_shard_plan", "rr_flat_rebase",
+           "rr_comm_get_id", "rr_comm_init", "rr_comm_destroy", "rr_split_plan", "rr_split", "rr_gather"]
+COMM_ID_BYTES = 128
 
 _lib = None
 
@@ -101,6 +107,15 @@ def lib():
     L.rr_host_batch_free.restype = None
     L.rr_gen_default_seed.argtypes = [C.c_int]
     L.rr_gen_default_seed.restype = u64
+    L.rr_shard_plan.argtypes = [vp, u64, C.c_uint32, C.POINTER(Shard)]
+    L.rr_flat_rebase.argtypes = [vp, vp, u64, vp, u64, u64, u64, vp]
+    L.rr_comm_get_id.argtypes = [vp]
+    L.rr_comm_init.argtypes = [vp, C.c_int, C.c_int, vp, C.POINTER(vp)]
+    L.rr_comm_destroy.argtypes = [vp]
+    L.rr_comm_destroy.restype = None
+    L.rr_split_plan.argtypes = [vp, C.POINTER(BlobBatch), C.c_int, C.POINTER(Shard), vp]
+    L.rr_split.argtypes = [vp, C.POINTER(BlobBatch), C.POINTER(Shard), C.c_int, C.POINTER(BlobBatch), vp]
+    L.rr_gather.argtypes = [vp, C.POINTER(FlatBatch), u64, C.POINTER(Shard), C.c_int, C.POINTER(FlatBatch), vp]
     _lib = L
     return L
 
@@ -130,6 +145,14 @@ def gen_batch(config: int, n: int, seed: int | None = None):
     finally:
         L.rr_host_batch_free(C.byref(hb))
     return data, offs
+
+
+def shard_plan(offsets: np.ndarray, g: int) -> np.ndarray:
+    """The C library's byte-balanced plan (rr_shard_plan): (g, 4) uint64 rows v0, v1, b0, b1."""
+    offsets = np.ascontiguousarray(offsets, np.uint64)
+    plan = (Shard * g)()
+    _check(lib().rr_shard_plan(_ptr(offsets), len(offsets) - 1, g, plan))
+    return np.array([[p.v0, p.v1, p.b0, p.b1] for p in plan], np.uint64).reshape(g, 4)
 
 
 def elem_bound(n: int, nbytes: int) -> int:
@@ -200,6 +223,12 @@ class Engine:
         _check(self._L.rr_decode_batch(self._ctx, C.byref(inb), C.byref(outb), C.c_void_p(totals.data_ptr()),
                                        C.c_void_p(s) if s else None))
 
+    def flat_rebase(self, values, elems, elem_add: int, byte_add: int, stream=None):
+        """In place on torch CUDA tensors (uint8 views of the flat records): rr_flat_rebase."""
+        _check(self._L.rr_flat_rebase(self._ctx, C.c_void_p(values.data_ptr()), values.numel() // 16,
+                                      C.c_void_p(elems.data_ptr()), elems.numel() // 16, elem_add, byte_add,
+                                      _sp(stream)))
+
     def encode_device(self, values, elems, arena, out_data, out_offsets, totals, stream=None):
         n = out_offsets.numel() - 1
         inb = FlatBatch(values.data_ptr(), elems.data_ptr(), arena.data_ptr(), n, elems.numel() // 16,
@@ -208,6 +237,60 @@ class Engine:
         s = stream.cuda_stream if stream is not None else None
         _check(self._L.rr_encode_batch(self._ctx, C.byref(inb), C.byref(outb), C.c_void_p(totals.data_ptr()),
                                        C.c_void_p(s) if s else None))
+
+
+class Comm:
+    """An RCCL communicator over one engine's device (include/rr_serdes.h multi-GPU calls).
+    Every rank builds one with the same 128-byte id (``Comm.new_id()`` on one rank, handed to
+    the others by any means).  Device arguments are torch CUDA tensors."""
+
+    def __init__(self, engine: Engine, nranks: int, rank: int, cid: bytes):
+        self._L = lib()
+        self.nranks, self.rank = nranks, rank
+        self._c = C.c_void_p()
+        buf = (C.c_uint8 * COMM_ID_BYTES).from_buffer_copy(cid)
+        _check(self._L.rr_comm_init(engine._ctx, nranks, rank, buf, C.byref(self._c)))
+
+    @staticmethod
+    def new_id() -> bytes:
+        buf = (C.c_uint8 * COMM_ID_BYTES)()
+        _check(lib().rr_comm_get_id(buf))
+        return bytes(buf)
+
+    def close(self):
+        if self._c:
+            self._L.rr_comm_destroy(self._c)
+            self._c = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def split_plan(self, data=None, offsets=None, root=0, stream=None):
+        whole = BlobBatch(data.data_ptr(), offsets.data_ptr(), offsets.numel() - 1, data.numel()) \
+            if offsets is not None else BlobBatch()
+        plan = (Shard * self.nranks)()
+        _check(self._L.rr_split_plan(self._c, C.byref(whole), root, plan, _sp(stream)))
+        return plan
+
+    def split(self, plan, data, offsets, mine_data, mine_offsets, root=0, stream=None):
+        whole = BlobBatch(data.data_ptr(), offsets.data_ptr(), offsets.numel() - 1, data.numel()) \
+            if offsets is not None else BlobBatch()
+        mine = BlobBatch(mine_data.data_ptr(), mine_offsets.data_ptr(), 0, mine_data.numel())
+        _check(self._L.rr_split(self._c, C.byref(whole), plan, root, C.byref(mine), _sp(stream)))
+        return int(mine.n)
+
+    def gather(self, plan, values, elems, mine_elems, whole_values=None, whole_elems=None, root=0, stream=None):
+        mine = FlatBatch(values.data_ptr(), elems.data_ptr(), None, values.numel() // 16, elems.numel() // 16, 0)
+        whole = FlatBatch(whole_values.data_ptr(), whole_elems.data_ptr(), None, whole_values.numel() // 16,
+                          whole_elems.numel() // 16, 0) if whole_values is not None else FlatBatch()
+        _check(self._L.rr_gather(self._c, C.byref(mine), mine_elems, plan, root, C.byref(whole), _sp(stream)))
+
+
+def _sp(stream):
+    return C.c_void_p(stream.cuda_stream) if stream is not None else None
 
 
 def encode_bound(values: np.ndarray, elems: np.ndarray) -> int:

@@ -10,32 +10,18 @@
 #include <stdlib.h>
 #include <string.h>
 
-#include "rr_kernels.h"
-
-struct rr_ctx {
-    int device;
-    hipStream_t stream;          /* used by the host entry points */
-    uint64_t *scratch;           /* look-back words + counters */
-    uint64_t scratch_words;
-    hipEvent_t scratch_done;     /* recorded after every call's last use of the scratch */
-    int scratch_used;
-    /* device staging for host entry points */
-    void *d_in, *d_off, *d_vals, *d_elems, *d_arena, *d_out, *d_ooff;
-    size_t c_in, c_off, c_vals, c_elems, c_arena, c_out, c_ooff;
-    rr_totals *d_totals;
-};
+#include "rr_internal.h"
 
 static __thread char g_err[256];
 const char *rr_last_error(void) { return g_err; }
-static int fail(int code, const char *fmt, ...) {
+int rr_fail(int code, const char *fmt, ...) {
     va_list ap;
     va_start(ap, fmt);
     vsnprintf(g_err, sizeof g_err, fmt, ap);
     va_end(ap);
     return code;
 }
-#define HIPCHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) \
-    return fail(RR_API_EHIP, "%s:%d %s: %s", __FILE__, __LINE__, #x, hipGetErrorString(e_)); } while (0)
+#define fail rr_fail
 
 int rr_ctx_create(int device, rr_ctx **out) {
     if (!out) return fail(RR_API_EINVAL, "out is NULL");

@@ -1,0 +1,25 @@
+/* rr_internal.h — what the C host files of the engine share (rr_api.c, rr_shard.c). */
+#ifndef RR_INTERNAL_H
+#define RR_INTERNAL_H
+
+#include "rr_kernels.h"
+
+struct rr_ctx {
+    int device;
+    hipStream_t stream;          /* used by the host entry points */
+    uint64_t *scratch;           /* look-back words + counters */
+    uint64_t scratch_words;
+    hipEvent_t scratch_done;     /* recorded after every call's last use of the scratch */
+    int scratch_used;
+    /* device staging for host entry points */
+    void *d_in, *d_off, *d_vals, *d_elems, *d_arena, *d_out, *d_ooff;
+    size_t c_in, c_off, c_vals, c_elems, c_arena, c_out, c_ooff;
+    rr_totals *d_totals;
+};
+
+/* sets rr_last_error() and returns code */
+int rr_fail(int code, const char *fmt, ...);
+#define HIPCHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) \
+    return rr_fail(RR_API_EHIP, "%s:%d %s: %s", __FILE__, __LINE__, #x, hipGetErrorString(e_)); } while (0)
+
+#endif

@@ -24,6 +24,10 @@ hipError_t rr_launch_encode(const rr_value *values, const rr_elem *elems, uint64
                             uint64_t arena_cap, uint64_t n, uint8_t *out, uint64_t cap, uint64_t *offsets,
                             uint64_t *scratch, rr_totals *totals, hipStream_t stream);
 uint64_t rr_decode_scratch_words(uint64_t data_cap, uint64_t n);
+hipError_t rr_launch_shard_plan(const uint64_t *offsets, uint64_t n, uint32_t g, uint64_t *plan, hipStream_t stream);
+hipError_t rr_launch_offsets_rebase(uint64_t *offs, uint64_t count, uint64_t sub, hipStream_t stream);
+hipError_t rr_launch_flat_rebase(rr_value *values, uint64_t n, rr_elem *elems, uint64_t ne, uint64_t elem_add,
+                                 uint64_t byte_add, hipStream_t stream);
 uint64_t rr_encode_scratch_words(uint64_t n, uint64_t data_cap);
 
 #ifdef __cplusplus

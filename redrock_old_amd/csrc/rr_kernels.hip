@@ -2013,3 +2013,91 @@ extern "C" hipError_t rr_launch_encode(const rr_value *values, const rr_elem *el
     if (e == hipSuccess && totals) e = launch_finalize(stats, lb, 2 * t, offsets, n, 0, totals, stream, err);
     return e;
 }
+
+// ---------------------------------------------------------------------------------------- shards
+// Multi-GPU sharding (rr_shard.c): values are independent, so a batch splits
+// into contiguous value ranges balanced by bytes, shard k starting at the first value whose
+// first byte is at or after k * total / g.  Three small kernels serve rr_shard.c:
+
+// plan[4k..4k+3] = {v0, v1, b0, b1} of shard k (thread k: two lower-bound searches)
+__global__ __launch_bounds__(64) void shard_plan_kernel(const uint64_t *__restrict__ offsets, uint64_t n, uint32_t g,
+                                                        uint64_t *__restrict__ plan) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= g) return;
+    const uint64_t total = offsets[n];
+    uint64_t cut[2];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+        const uint32_t kk = k + e;
+        if (kk == 0) { cut[e] = 0; continue; }
+        if (kk == g) { cut[e] = n; continue; }
+        const uint64_t target = (uint64_t)(((unsigned __int128)total * kk) / g);
+        uint64_t lo = 0, hi = n;   // first v in [0, n) with offsets[v] >= target, else n
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi) / 2;
+            if (offsets[mid] < target) lo = mid + 1;
+            else hi = mid;
+        }
+        cut[e] = lo;
+    }
+    plan[4 * (uint64_t)k + 0] = cut[0];
+    plan[4 * (uint64_t)k + 1] = cut[1];
+    plan[4 * (uint64_t)k + 2] = offsets[cut[0]];
+    plan[4 * (uint64_t)k + 3] = offsets[cut[1]];
+}
+
+// offsets[i] -= sub (a received shard's offsets, relative to its first byte)
+__global__ __launch_bounds__(256) void offsets_rebase_kernel(uint64_t *__restrict__ offs, uint64_t count, uint64_t sub) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < count) offs[i] -= sub;
+}
+
+// A decoded shard placed in the whole batch: elem_base += elem_add; the arena offsets of STR /
+// ZLRAW descriptors += byte_add (the arena mirrors the blob buffer, so a shard's arena is the
+// whole arena's slice at the shard's first byte).  The zero-filled slots of a malformed value
+// (kind STR, data 0, len 0 — no real string starts at byte 0 of a value) stay zero.
+__global__ __launch_bounds__(256) void flat_rebase_kernel(rr_value *__restrict__ values, uint64_t n,
+                                                          rr_elem *__restrict__ elems, uint64_t ne,
+                                                          uint64_t elem_add, uint64_t byte_add) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n || i < ne; i += stride) {
+        if (i < n) {
+            uint4 v = reinterpret_cast<uint4 *>(values)[i];
+            v.w += (uint32_t)elem_add;
+            reinterpret_cast<uint4 *>(values)[i] = v;
+        }
+        if (i < ne) {
+            uint4 e = reinterpret_cast<uint4 *>(elems)[i];
+            const uint32_t kind = e.w & 0xFF;
+            const uint64_t d = (uint64_t)e.x | ((uint64_t)e.y << 32);
+            if ((kind == RR_K_STR || kind == RR_K_ZLRAW) && (d | e.z) != 0) {
+                const uint64_t d2 = d + byte_add;
+                e.x = (uint32_t)d2;
+                e.y = (uint32_t)(d2 >> 32);
+                reinterpret_cast<uint4 *>(elems)[i] = e;
+            }
+        }
+    }
+}
+
+extern "C" hipError_t rr_launch_shard_plan(const uint64_t *offsets, uint64_t n, uint32_t g, uint64_t *plan,
+                                           hipStream_t stream) {
+    hipLaunchKernelGGL(shard_plan_kernel, dim3((g + 63) / 64), dim3(64), 0, stream, offsets, n, g, plan);
+    return hipGetLastError();
+}
+extern "C" hipError_t rr_launch_offsets_rebase(uint64_t *offs, uint64_t count, uint64_t sub, hipStream_t stream) {
+    if (count == 0 || sub == 0) return hipSuccess;
+    hipLaunchKernelGGL(offsets_rebase_kernel, dim3((uint32_t)((count + 255) / 256)), dim3(256), 0, stream, offs, count,
+                       sub);
+    return hipGetLastError();
+}
+extern "C" hipError_t rr_launch_flat_rebase(rr_value *values, uint64_t n, rr_elem *elems, uint64_t ne, uint64_t elem_add,
+                                            uint64_t byte_add, hipStream_t stream) {
+    const uint64_t m = n > ne ? n : ne;
+    if (m == 0 || (elem_add == 0 && byte_add == 0)) return hipSuccess;
+    uint64_t blocks = (m + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(flat_rebase_kernel, dim3((uint32_t)blocks), dim3(256), 0, stream, values, n, elems, ne, elem_add,
+                       byte_add);
+    return hipGetLastError();
+}

@@ -1,0 +1,212 @@
+/*
+ * rr_shard.c — multi-GPU sharding in the C host layer (include/rr_serdes.h "multi-GPU",
+ * SURVEY.md §8e): the byte-balanced plan, and the root split / gather of device-resident
+ * batches with RCCL point-to-point transfers over xGMI.  One process per GPU, one rr_comm per
+ * process.  Nothing here touches the decode: values are independent, so each rank decodes its
+ * shard with rr_decode_batch and only the split and the gather move data between GPUs.
+ */
+#include <stdlib.h>
+#include <string.h>
+
+#include <rccl/rccl.h>
+
+#include "rr_internal.h"
+
+struct rr_comm {
+    ncclComm_t nc;
+    int nranks, rank, device;
+    uint64_t *d_words;   /* 4 * nranks words: the plan / the all-gathered shard sizes */
+};
+
+#define NCCLCHK(x) do { ncclResult_t r_ = (x); if (r_ != ncclSuccess) \
+    return rr_fail(RR_API_EHIP, "%s:%d %s: %s", __FILE__, __LINE__, #x, ncclGetErrorString(r_)); } while (0)
+
+/* the same rule as shard_plan_kernel: shard k starts at the first value whose first byte is at
+ * or after floor(total * k / g) */
+int rr_shard_plan(const uint64_t *offsets, uint64_t n, uint32_t g, rr_shard *plan) {
+    if (!offsets || !plan || g == 0) return rr_fail(RR_API_EINVAL, "rr_shard_plan: bad argument");
+    const uint64_t total = offsets[n];
+    uint64_t prev = 0;
+    for (uint32_t k = 0; k < g; k++) {
+        uint64_t cut = n;
+        if (k + 1 < g) {
+            const uint64_t target = (uint64_t)(((unsigned __int128)total * (k + 1)) / g);
+            uint64_t lo = 0, hi = n;
+            while (lo < hi) {
+                const uint64_t mid = (lo + hi) / 2;
+                if (offsets[mid] < target) lo = mid + 1;
+                else hi = mid;
+            }
+            cut = lo;
+        }
+        plan[k].v0 = prev;
+        plan[k].v1 = cut;
+        plan[k].b0 = offsets[prev];
+        plan[k].b1 = offsets[cut];
+        prev = cut;
+    }
+    return RR_API_OK;
+}
+
+int rr_flat_rebase(rr_ctx *ctx, rr_value *values, uint64_t n, rr_elem *elems, uint64_t n_elems, uint64_t elem_add,
+                   uint64_t byte_add, void *stream) {
+    if (!ctx) return rr_fail(RR_API_EINVAL, "ctx is NULL");
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(rr_launch_flat_rebase(values, n, elems, n_elems, elem_add, byte_add, (hipStream_t)stream));
+    return RR_API_OK;
+}
+
+int rr_comm_get_id(uint8_t id[RR_COMM_ID_BYTES]) {
+    ncclUniqueId u;
+    NCCLCHK(ncclGetUniqueId(&u));
+    memcpy(id, &u, RR_COMM_ID_BYTES);
+    return RR_API_OK;
+}
+
+int rr_comm_init(rr_ctx *ctx, int nranks, int rank, const uint8_t id[RR_COMM_ID_BYTES], rr_comm **out) {
+    if (!ctx || !out || nranks < 1 || rank < 0 || rank >= nranks) return rr_fail(RR_API_EINVAL, "rr_comm_init: bad argument");
+    *out = NULL;
+    HIPCHK(hipSetDevice(ctx->device));
+    rr_comm *c = (rr_comm *)calloc(1, sizeof *c);
+    if (!c) return rr_fail(RR_API_ENOMEM, "calloc");
+    ncclUniqueId u;
+    memcpy(&u, id, RR_COMM_ID_BYTES);
+    ncclResult_t r = ncclCommInitRank(&c->nc, nranks, u, rank);
+    if (r != ncclSuccess) { free(c); return rr_fail(RR_API_EHIP, "ncclCommInitRank: %s", ncclGetErrorString(r)); }
+    if (hipMalloc((void **)&c->d_words, sizeof(uint64_t) * 4 * (size_t)nranks) != hipSuccess) {
+        ncclCommDestroy(c->nc);
+        free(c);
+        return rr_fail(RR_API_ENOMEM, "hipMalloc comm words");
+    }
+    c->nranks = nranks;
+    c->rank = rank;
+    c->device = ctx->device;
+    *out = c;
+    return RR_API_OK;
+}
+
+void rr_comm_destroy(rr_comm *c) {
+    if (!c) return;
+    hipSetDevice(c->device);
+    ncclCommDestroy(c->nc);
+    hipFree(c->d_words);
+    free(c);
+}
+
+int rr_split_plan(rr_comm *c, const rr_blob_batch *whole, int root, rr_shard *plan, void *stream) {
+    if (!c || !plan || root < 0 || root >= c->nranks) return rr_fail(RR_API_EINVAL, "rr_split_plan: bad argument");
+    hipStream_t s = (hipStream_t)stream;
+    HIPCHK(hipSetDevice(c->device));
+    if (c->rank == root) {
+        if (!whole || !whole->offsets) return rr_fail(RR_API_EINVAL, "rr_split_plan: root needs the whole batch");
+        HIPCHK(rr_launch_shard_plan(whole->offsets, whole->n, (uint32_t)c->nranks, c->d_words, s));
+    }
+    NCCLCHK(ncclBroadcast(c->d_words, c->d_words, 4 * (size_t)c->nranks, ncclUint64, root, c->nc, s));
+    HIPCHK(hipMemcpyAsync(plan, c->d_words, sizeof(rr_shard) * (size_t)c->nranks, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return RR_API_OK;
+}
+
+int rr_split(rr_comm *c, const rr_blob_batch *whole, const rr_shard *plan, int root, rr_blob_batch *mine,
+             void *stream) {
+    if (!c || !plan || !mine || root < 0 || root >= c->nranks) return rr_fail(RR_API_EINVAL, "rr_split: bad argument");
+    hipStream_t s = (hipStream_t)stream;
+    HIPCHK(hipSetDevice(c->device));
+    const rr_shard *me = &plan[c->rank];
+    const uint64_t nb = me->b1 - me->b0, nv = me->v1 - me->v0;
+    if (mine->data_cap < ((nb + 15) & ~15ull) || !mine->offsets || (nb && !mine->data))
+        return rr_fail(RR_API_EINVAL, "rr_split: shard buffers too small");
+    if (c->rank == root && (!whole || !whole->data || !whole->offsets))
+        return rr_fail(RR_API_EINVAL, "rr_split: root needs the whole batch");
+    if (c->rank == root && mine->offsets == whole->offsets + me->v0 && me->b0 != 0)
+        return rr_fail(RR_API_EINVAL, "rr_split: in-place offsets need the root's shard to start at byte 0");
+    NCCLCHK(ncclGroupStart());
+    if (c->rank == root) {
+        for (int k = 0; k < c->nranks; k++) {
+            if (k == root) continue;
+            const rr_shard *p = &plan[k];
+            if (p->b1 > p->b0) NCCLCHK(ncclSend(whole->data + p->b0, p->b1 - p->b0, ncclUint8, k, c->nc, s));
+            NCCLCHK(ncclSend(whole->offsets + p->v0, p->v1 - p->v0 + 1, ncclUint64, k, c->nc, s));
+        }
+    } else {
+        if (nb) NCCLCHK(ncclRecv(mine->data, nb, ncclUint8, root, c->nc, s));
+        NCCLCHK(ncclRecv(mine->offsets, nv + 1, ncclUint64, root, c->nc, s));
+    }
+    NCCLCHK(ncclGroupEnd());
+    if (c->rank == root) {   /* the root's own shard: a device copy (nothing if it decodes in place) */
+        if (mine->data != whole->data + me->b0 && nb)
+            HIPCHK(hipMemcpyAsync(mine->data, whole->data + me->b0, nb, hipMemcpyDeviceToDevice, s));
+        if (mine->offsets != whole->offsets + me->v0)
+            HIPCHK(hipMemcpyAsync(mine->offsets, whole->offsets + me->v0, (nv + 1) * sizeof(uint64_t),
+                                  hipMemcpyDeviceToDevice, s));
+    }
+    const int in_place = c->rank == root && mine->data == whole->data + me->b0;
+    if (nb < mine->data_cap && !in_place)   /* the shard's tail padding reads as zeros */
+        HIPCHK(hipMemsetAsync(mine->data + nb, 0, mine->data_cap - nb, s));
+    HIPCHK(rr_launch_offsets_rebase(mine->offsets, nv + 1, me->b0, s));
+    mine->n = nv;
+    return RR_API_OK;
+}
+
+int rr_gather(rr_comm *c, const rr_flat_batch *mine, uint64_t mine_elems, const rr_shard *plan, int root,
+              rr_flat_batch *whole, void *stream) {
+    if (!c || !mine || !plan || root < 0 || root >= c->nranks) return rr_fail(RR_API_EINVAL, "rr_gather: bad argument");
+    hipStream_t s = (hipStream_t)stream;
+    HIPCHK(hipSetDevice(c->device));
+    /* the shards' descriptor counts, everywhere (the root places the shards with them) */
+    HIPCHK(hipMemcpyAsync(c->d_words + c->rank, &mine_elems, sizeof(uint64_t), hipMemcpyHostToDevice, s));
+    NCCLCHK(ncclAllGather(c->d_words + c->rank, c->d_words, 1, ncclUint64, c->nc, s));
+    uint64_t *ne = (uint64_t *)malloc(sizeof(uint64_t) * (size_t)c->nranks);
+    if (!ne) return rr_fail(RR_API_ENOMEM, "malloc");
+    hipError_t he = hipMemcpyAsync(ne, c->d_words, sizeof(uint64_t) * (size_t)c->nranks, hipMemcpyDeviceToHost, s);
+    if (he == hipSuccess) he = hipStreamSynchronize(s);
+    if (he != hipSuccess) { free(ne); return rr_fail(RR_API_EHIP, "rr_gather sizes: %s", hipGetErrorString(he)); }
+    int rc = RR_API_OK;
+    uint64_t eb = 0;
+    if (c->rank == root) {
+        uint64_t tot = 0;
+        for (int k = 0; k < c->nranks; k++) tot += ne[k];
+        if (!whole || !whole->values || (tot && !whole->elems) || whole->elem_cap < tot)
+            rc = rr_fail(RR_API_EINVAL, "rr_gather: root's whole batch too small");
+    }
+    if (rc == RR_API_OK) {
+        ncclResult_t r = ncclGroupStart();
+        for (int k = 0; k < c->nranks && r == ncclSuccess; k++) {
+            const uint64_t nv = plan[k].v1 - plan[k].v0;
+            if (c->rank == root && k != root) {
+                if (nv) r = ncclRecv(whole->values + plan[k].v0, nv * sizeof(rr_value), ncclUint8, k, c->nc, s);
+                if (r == ncclSuccess && ne[k]) r = ncclRecv(whole->elems + eb, ne[k] * sizeof(rr_elem), ncclUint8, k, c->nc, s);
+            } else if (c->rank != root && k == c->rank) {
+                if (nv) r = ncclSend(mine->values, nv * sizeof(rr_value), ncclUint8, root, c->nc, s);
+                if (r == ncclSuccess && ne[k]) r = ncclSend(mine->elems, ne[k] * sizeof(rr_elem), ncclUint8, root, c->nc, s);
+            }
+            eb += ne[k];
+        }
+        ncclResult_t r2 = ncclGroupEnd();
+        if (r == ncclSuccess) r = r2;
+        if (r != ncclSuccess) rc = rr_fail(RR_API_EHIP, "rr_gather: %s", ncclGetErrorString(r));
+    }
+    if (rc == RR_API_OK && c->rank == root) {
+        eb = 0;
+        for (int k = 0; k < c->nranks && rc == RR_API_OK; k++) {
+            const uint64_t nv = plan[k].v1 - plan[k].v0;
+            rr_value *dv = whole->values + plan[k].v0;
+            rr_elem *de = whole->elems + eb;
+            if (k == root) {   /* the root's own shard: copy it in, unless it decoded in place */
+                hipError_t e2 = hipSuccess;
+                if (nv && (void *)mine->values != (void *)dv)
+                    e2 = hipMemcpyAsync(dv, mine->values, nv * sizeof(rr_value), hipMemcpyDeviceToDevice, s);
+                if (e2 == hipSuccess && ne[k] && (void *)mine->elems != (void *)de)
+                    e2 = hipMemcpyAsync(de, mine->elems, ne[k] * sizeof(rr_elem), hipMemcpyDeviceToDevice, s);
+                if (e2 != hipSuccess) rc = rr_fail(RR_API_EHIP, "rr_gather copy: %s", hipGetErrorString(e2));
+            }
+            if (rc == RR_API_OK) {
+                hipError_t e3 = rr_launch_flat_rebase(dv, nv, de, ne[k], eb, plan[k].b0, s);
+                if (e3 != hipSuccess) rc = rr_fail(RR_API_EHIP, "rr_gather rebase: %s", hipGetErrorString(e3));
+            }
+            eb += ne[k];
+        }
+    }
+    free(ne);
+    return rc;
+}

@@ -132,3 +132,106 @@ def test_rebase_with_malformed_values(g):
         sv, se, _, _ = cpu.decode(d, o)
         parts.append((sv, se, int(offs[cuts[k]])))
     assert_flat_equal(shard.rebase_flat(parts), expected_flat(fx), f"golden g {g}")
+
+
+@pytest.mark.parametrize("n,g", [(5000, 1), (5000, 3), (5000, 8), (3, 8), (0, 4), (1, 3)])
+def test_c_shard_plan_matches_partition(n, g):
+    """The C library's plan (rr_shard_plan, the rule shard_plan_kernel runs on the device for
+    rr_split_plan) is the host partition's."""
+    _, offs = rr.gen_batch(4, n) if n else (None, np.zeros(1, np.uint64))
+    plan = rr.shard_plan(offs, g)
+    cuts = shard.partition(offs, g)
+    assert (plan[:, 0] == cuts[:-1]).all() and (plan[:, 1] == cuts[1:]).all()
+    assert (plan[:, 2] == offs[cuts[:-1]]).all() and (plan[:, 3] == offs[cuts[1:]]).all()
+
+
+def _device_shards(engine, data, offs, g, torch_dev):
+    """Decode each shard on the device; returns whole-sized (values, elems) tensors with every
+    shard copied to its place and rebased by rr_flat_rebase, and the total descriptor count."""
+    n = len(offs) - 1
+    plan = rr.shard_plan(offs, g)
+    parts, ne_tot = [], 0
+    for k in range(g):
+        v0, v1, b0, b1 = (int(x) for x in plan[k])
+        d, o = shard.shard_of(data, offs, v0, v1)
+        nv, nb = v1 - v0, b1 - b0
+        cap = rr.elem_bound(nv, nb)
+        t_vals = torch.zeros(max(nv, 1) * 16, dtype=torch.uint8, device=torch_dev)[:nv * 16]
+        t_elems = torch.zeros(max(cap, 1) * 16, dtype=torch.uint8, device=torch_dev)
+        t_arena = torch.zeros(max(len(d), 16), dtype=torch.uint8, device=torch_dev)
+        t_tot = torch.zeros(4, dtype=torch.int64, device=torch_dev)
+        engine.decode_device(torch.from_numpy(d).to(torch_dev), torch.from_numpy(o.view(np.int64)).to(torch_dev),
+                             t_vals, t_elems, t_arena, t_tot)
+        ne = int(t_tot[0].item())
+        parts.append((t_vals, t_elems[:ne * 16], ne, b0))
+        ne_tot += ne
+    w_vals = torch.zeros(max(n, 1) * 16, dtype=torch.uint8, device=torch_dev)
+    w_elems = torch.zeros(max(ne_tot, 1) * 16, dtype=torch.uint8, device=torch_dev)
+    eb = 0
+    for k, (t_vals, t_elems, ne, b0) in enumerate(parts):
+        v0, v1 = int(plan[k][0]), int(plan[k][1])
+        dv, de = w_vals[v0 * 16:v1 * 16], w_elems[eb * 16:(eb + ne) * 16]
+        dv.copy_(t_vals)
+        de.copy_(t_elems)
+        engine.flat_rebase(dv, de, eb, b0)
+        eb += ne
+    torch.cuda.synchronize()
+    return w_vals[:n * 16], w_elems[:ne_tot * 16]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg,n,g", [(4, 20000, 4), (10, 500, 3), (4, 2000, 7)])
+def test_device_rebase_equals_whole(engine, cfg, n, g):
+    """Shards decoded on the device and placed by the device rebase (rr_flat_rebase, the step
+    rr_gather runs on the root) equal the whole batch's oracle decode."""
+    data, offs, v, e = _whole(cfg, n)
+    w_vals, w_elems = _device_shards(engine, data, offs, g, torch.device("cuda:0"))
+    got = (w_vals.cpu().numpy().view(rr.VALUE_DT), w_elems.cpu().numpy().view(rr.ELEM_DT))
+    assert_flat_equal(got, (v, e), f"device rebase cfg {cfg} g {g}")
+
+
+@pytest.mark.gpu
+def test_device_rebase_golden_malformed(engine):
+    from helpers import batch_from_blobs, expected_flat, golden
+    fx = (golden()["kats"] + golden()["edges"]) * 3
+    data, offs = batch_from_blobs([bytes.fromhex(f["blob"]) for f in fx])
+    w_vals, w_elems = _device_shards(engine, data, offs, 5, torch.device("cuda:0"))
+    got = (w_vals.cpu().numpy().view(rr.VALUE_DT), w_elems.cpu().numpy().view(rr.ELEM_DT))
+    assert_flat_equal(got, expected_flat(fx), "device rebase golden")
+
+
+@pytest.mark.gpu
+def test_rccl_split_gather_single_rank(engine):
+    """rr_comm over RCCL with one rank (the box has one GPU; the N>1 data movement is the same
+    ncclSend/Recv calls, rehearsed over gloo above): split_plan -> split -> decode -> gather
+    equals the whole decode."""
+    dev = torch.device("cuda:0")
+    data, offs, v, e = _whole(4, 30000)
+    n, nb = len(offs) - 1, int(offs[-1])
+    comm = rr.Comm(engine, 1, 0, rr.Comm.new_id())
+    try:
+        d_data = torch.from_numpy(data).to(dev)
+        d_offs = torch.from_numpy(offs.view(np.int64)).to(dev)
+        plan = comm.split_plan(d_data, d_offs, root=0)
+        assert (plan[0].v0, plan[0].v1, plan[0].b0, plan[0].b1) == (0, n, 0, nb)
+        m_data = torch.full(((nb + 15) & ~15,), 0xAB, dtype=torch.uint8, device=dev)
+        m_offs = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+        assert comm.split(plan, d_data, d_offs, m_data, m_offs, root=0) == n
+        torch.cuda.synchronize()
+        assert torch.equal(m_data[:nb].cpu(), d_data[:nb].cpu()) and torch.equal(m_offs.cpu(), d_offs.cpu())
+        assert int(m_data[nb:].sum().item()) == 0   # the tail padding is zeroed
+        cap = rr.elem_bound(n, nb)
+        t_vals = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
+        t_elems = torch.zeros(cap * 16, dtype=torch.uint8, device=dev)
+        t_arena = torch.zeros(len(data), dtype=torch.uint8, device=dev)
+        t_tot = torch.zeros(4, dtype=torch.int64, device=dev)
+        engine.decode_device(m_data, m_offs, t_vals, t_elems, t_arena, t_tot)
+        ne = int(t_tot[0].item())
+        w_vals = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
+        w_elems = torch.zeros(ne * 16, dtype=torch.uint8, device=dev)
+        comm.gather(plan, t_vals, t_elems, ne, w_vals, w_elems, root=0)
+        torch.cuda.synchronize()
+        got = (w_vals.cpu().numpy().view(rr.VALUE_DT), w_elems.cpu().numpy().view(rr.ELEM_DT))
+        assert_flat_equal(got, (v, e), "rccl single-rank split/gather")
+    finally:
+        comm.close()
