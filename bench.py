@@ -42,6 +42,7 @@ def parse():
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-check", action="store_true")
     p.add_argument("--no-host", action="store_true", help="skip the PCIe-inclusive host leg and the copy reference")
+    p.add_argument("--no-split", action="store_true", help="skip the RCCL root split/gather leg")
     p.add_argument("--profile-only", action="store_true", help="decode steps only (for rocprofv3)")
     p.add_argument("--profile-encode", action="store_true", help="one decode, then encode steps only (for rocprofv3)")
     return p.parse_args()
@@ -223,6 +224,27 @@ def main():
         "gen_s": round(t_gen, 2),
     }
 
+    if not args.no_split:
+        # a hang in a collective must not cost the headline line: after 120 s rank 0 prints
+        # what it has and every rank leaves
+        import threading
+
+        def _bail():
+            if rank == 0:
+                result["split_gather"] = {"error": "timeout after 120 s"}
+                print(json.dumps(result), flush=True)
+            os._exit(0)
+
+        dog = threading.Timer(120.0, _bail)
+        dog.daemon = True
+        dog.start()
+        try:
+            result["split_gather"] = split_gather_leg(rr, torch, dist, eng, world, rank, dev, stream, d_data, d_offs,
+                                                      d_vals, d_elems, n, nb, n_elems)
+        except Exception as ex:   # reported, never fatal to the headline
+            result["split_gather"] = {"error": repr(ex)[:300]}
+        dog.cancel()
+
     if rank == 0 and world == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(data, offs, nb, args.cpu_seconds)
 
@@ -230,6 +252,79 @@ def main():
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def split_gather_leg(rr, torch, dist, eng, world, rank, dev, stream, d_data, d_offs, d_vals, d_elems, n, nb,
+                     n_elems):
+    """Root split / gather through the C library's RCCL entry points (rr_split_plan, rr_split,
+    rr_gather), reported separately from the device-resident headline: rank 0's
+    batch is cut into `world` byte-balanced shards and scattered over xGMI, every rank decodes
+    its shard, and the decoded shards are gathered back to rank 0, where they must equal rank
+    0's whole-batch decode bit for bit."""
+    cid = torch.zeros(rr.COMM_ID_BYTES, dtype=torch.uint8, device=dev)
+    if rank == 0:
+        cid.copy_(torch.frombuffer(bytearray(rr.Comm.new_id()), dtype=torch.uint8))
+    if world > 1:
+        dist.broadcast(cid, 0)
+    comm = rr.Comm(eng, world, rank, bytes(cid.cpu().numpy().tobytes()))
+    try:
+        def sync():
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+
+        def tmax(x):
+            t = torch.tensor([x], dtype=torch.float64, device=dev)
+            if world > 1:
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            return float(t.item())
+
+        root = rank == 0
+        plan = comm.split_plan(d_data if root else None, d_offs if root else None, root=0, stream=stream)
+        me = plan[rank]
+        nv, mb = int(me.v1 - me.v0), int(me.b1 - me.b0)
+        m_data = torch.empty(max((mb + 15) & ~15, 16), dtype=torch.uint8, device=dev)
+        m_offs = torch.empty(nv + 1, dtype=torch.int64, device=dev)
+        cap = rr.elem_bound(nv, mb)
+        m_vals = torch.empty(max(nv, 1) * 16, dtype=torch.uint8, device=dev)
+        m_elems = torch.empty(max(cap, 1) * 16, dtype=torch.uint8, device=dev)
+        m_arena = torch.empty(m_data.numel(), dtype=torch.uint8, device=dev)
+        m_tot = torch.zeros(4, dtype=torch.int64, device=dev)
+        w_vals = torch.empty(n * 16, dtype=torch.uint8, device=dev) if root else None
+        w_elems = torch.empty(max(n_elems, 1) * 16, dtype=torch.uint8, device=dev) if root else None
+        t_split, t_dec, t_gather = [], [], []
+        for rep in range(4):   # rep 0 warms up
+            sync()
+            t0 = time.perf_counter()
+            plan = comm.split_plan(d_data if root else None, d_offs if root else None, root=0, stream=stream)
+            comm.split(plan, d_data if root else None, d_offs if root else None, m_data, m_offs, root=0,
+                       stream=stream)
+            sync()
+            t1 = time.perf_counter()
+            eng.decode_device(m_data, m_offs, m_vals[:nv * 16], m_elems, m_arena, m_tot, stream=stream)
+            sync()
+            t2 = time.perf_counter()
+            ne = int(m_tot[0].item())
+            comm.gather(plan, m_vals[:nv * 16], m_elems[:ne * 16], ne, w_vals, w_elems, root=0, stream=stream)
+            sync()
+            t3 = time.perf_counter()
+            if rep:
+                t_split.append(tmax(t1 - t0))
+                t_dec.append(tmax(t2 - t1))
+                t_gather.append(tmax(t3 - t2))
+        moved = sum(int(p.b1 - p.b0) + 8 * int(p.v1 - p.v0 + 1) for k, p in enumerate(plan) if k != 0)
+        out = {"what": f"rank 0's batch split into {world} shards over RCCL (rr_split), decoded per rank, "
+                       "gathered to rank 0 (rr_gather); wall ms, max over ranks, median of 3",
+               "split_ms": round(statistics.median(t_split) * 1e3, 3),
+               "shard_decode_ms": round(statistics.median(t_dec) * 1e3, 3),
+               "gather_ms": round(statistics.median(t_gather) * 1e3, 3),
+               "split_bytes_sent": moved}
+        if root:
+            out["gather_bit_exact"] = bool(torch.equal(w_vals, d_vals[:n * 16]) and
+                                           torch.equal(w_elems[:n_elems * 16], d_elems[:n_elems * 16]))
+        return out
+    finally:
+        comm.close()
 
 
 def measured_traffic(config, n, nb):
@@ -272,15 +367,21 @@ def cpu_baseline(data, offs, nb, budget_s):
     out.update({"value": round(sb / td / 2 ** 30, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
                 "sample": f"first {m} values ({sb} B) of the same batch, faithful desObject, median of {len(times_d)}",
                 "values_per_s": round(m / td, 1), "encode_gib_s": round(sb / te / 2 ** 30, 4)})
-    # flat restatement (same output as the GPU), 1 thread and all threads, same sample
-    nt = min(16, cpu.nprocs())
-    for k, thr in (("flat_1t_gib_s", 1), (f"flat_{nt}t_gib_s", nt)):
+    out["per_core_gib_s"] = out["value"]
+    # flat restatement (same output as the GPU) on 1 thread, 16 threads (the box's CPU share per
+    # GPU) and every core this process may run on (capped at 128 threads)
+    allc = min(len(os.sched_getaffinity(0)), 128)
+    flat = {}
+    for thr in sorted({1, min(16, allc), allc}):
         ts = []
-        for _ in range(3):
+        for _ in range(5):
             t0 = time.perf_counter()
             cpu.decode(sub, sub_off, nthreads=thr)
             ts.append(time.perf_counter() - t0)
-        out[k] = round(sb / statistics.median(ts) / 2 ** 30, 4)
+        flat[thr] = sb / statistics.median(ts) / 2 ** 30
+        out[f"flat_{thr}t_gib_s"] = round(flat[thr], 4)
+    out["flat_all_cores"] = {"cores": allc, "gib_s": round(flat[allc], 4),
+                             "per_core_gib_s": round(flat[allc] / allc, 4)}
     out["host_cpus"] = cpu.nprocs()
     return out
 

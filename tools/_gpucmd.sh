@@ -1,3 +1,8 @@
-timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -rf > gpurun_out/t15.log 2>&1; echo rc=$? >> gpurun_out/t15.log
-cd /tmp && export TMPDIR=/tmp && timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/prof15 -o run -- python3 $GRAFT_REPO_ROOT/tools/time_decode.py 4 1000000 10 > $GRAFT_REPO_ROOT/gpurun_out/prof15.log 2>&1
-cd $GRAFT_REPO_ROOT && for i in 1 2; do timeout -k 10 100 python tools/time_decode.py 4; done > gpurun_out/time15.log 2>&1
+set -e
+mkdir -p gpurun_out
+timeout -k 10 400 python -u bench.py > gpurun_out/r2_bench.log 2>&1
+tail -1 gpurun_out/r2_bench.log > gpurun_out/r2_bench.json
+timeout -k 10 400 bash tools/profile_bench.sh gpurun_out/r2prof
+RR_PROFILE=encode timeout -k 10 400 bash tools/profile_bench.sh gpurun_out/r2prof_enc
+timeout -k 10 600 bash tools/pmc_decode.sh gpurun_out/r2pmc 4
+echo done

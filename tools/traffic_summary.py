@@ -37,7 +37,7 @@ for c in ("FETCH_SIZE", "WRITE_SIZE"):
 if "enc_emit_kernel" in per:   # RR_PROFILE=encode run (one decode call precedes the encode steps)
     pipeline = ("enc_size_kernel", "scan_kernel", "enc_index_kernel", "enc_emit_kernel", "finalize_kernel")
 else:
-    pipeline = ("count_kernel", "scan_kernel", "decode_kernel", "finalize_kernel")
+    pipeline = ("count_kernel", "scan_kernel", "decode_kernel", "decode_post_kernel")
 res["pipeline"] = list(pipeline)
 tot = 0.0
 for k in pipeline:
