@@ -14,8 +14,8 @@
  *   - return value: RR_API_OK (0) or a negative RR_API_E* code for the whole call;
  *   - per-value status in rr_value.status (0 = OK), counted into rr_totals.n_bad;
  *   - caller-owned buffers; one rr_ctx per host thread; no hidden host synchronisation in the
- *     device entry points (graph-capturable after rr_ctx_reserve: decode = memset + 5 kernels,
- *     encode = memset + 5 kernels, all on the caller's stream).  The only wait is when the
+ *     device entry points (graph-capturable after rr_ctx_reserve: decode = 4 kernels, encode
+ *     = 5 kernels, all on the caller's stream; the per-call words are zeroed by the first).  The only wait is when the
  *     context's scratch must grow: it waits for the context's previous call to finish (an
  *     event, not a device sync) — and under graph capture it fails instead.
  * Plain C: no HIP or torch types in any signature.  Streams are passed as void* (hipStream_t).
