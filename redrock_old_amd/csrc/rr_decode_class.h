@@ -509,9 +509,16 @@ __device__ __forceinline__ bool do_list_g(const Src &R, const Lane &l, bool acti
     return fail || k != l.r;
 }
 
-// ---- Set / Hash hash tables, grouped.  A step reads the 8 bytes before p (they finish the
-// previous member's fingerprint) and the length field at p; the step at p == end only finishes
-// the last member.  Every lane of a group keeps the whole fingerprint register.
+// ---- Set / Hash hash tables, grouped.  The chain steps read only the u64 length fields (every
+// lane of the group, as in do_list_g); lane g takes elements g, g + G, ...: it stores the
+// descriptor and, for a key member, fingerprints it from the 8 bytes that end it (the bytes
+// do_ht reads at the next step's p - 8).  The duplicate test runs once per value after the
+// walk, not per step: key i is broadcast from its lane and compared with the lower-numbered
+// keys the other lanes hold.  A lane keeps the keys of its first HT_G_ROUNDS rounds, which
+// covers HT_FP_KEYS keys when G >= HT_FP_KEYS / HT_G_ROUNDS lanes hold keys (a hash's keys
+// are its even elements: G >= 8; a set: G >= 4 — the batch picks do_ht below that).
+constexpr uint32_t HT_G_ROUNDS = 4;
+__device__ __forceinline__ uint32_t ht_group_min(bool hash) { return hash ? 2 * HT_FP_KEYS / HT_G_ROUNDS : HT_FP_KEYS / HT_G_ROUNDS; }
 template <class Src>
 __device__ __forceinline__ bool do_ht_g(const Src &R, const Head &H, const Lane &l, bool active, uint32_t G,
                                         uint32_t g, uint32_t &n, uint64_t &pay, bool &fix, const bool hash) {
@@ -521,52 +528,59 @@ __device__ __forceinline__ bool do_ht_g(const Src &R, const Head &H, const Lane 
 #else   // timing-only builds (tools/): no fingerprints (duplicates go undetected)
     const bool chk = false;
 #endif
-    bool dupfp = active && cnt > HT_FP_KEYS;
-    uint32_t p = l.q + 13, k = 0, plen = 0, s = 0;   // s: steps taken (k of every walking lane)
+    uint32_t p = l.q + 13, k = 0;
     const uint32_t end = l.q + l.L;
     bool fail = false, walk = active;
-    uint32_t fpr[HT_FP_KEYS / 2];
+    uint32_t fps[HT_G_ROUNDS];
 #pragma unroll
-    for (uint32_t j = 0; j < HT_FP_KEYS / 2; ++j) fpr[j] = 0xFFFFFFFFu;
-    for (;;) {
+    for (uint32_t q = 0; q < HT_G_ROUNDS; ++q) fps[q] = 0xFFFFFFFFu;
+    for (uint32_t r = 0;; ++r) {
         uint32_t mp = 0, ml = 0, mk = 0;
         bool mine = false;
-        for (uint32_t j = 0; j < G; ++j, ++s) {
-            uint32_t b[4];
-            R.template get<4>(p - 8, b);
-            if (s > 0 && (!hash || (s & 1))) {   // member s-1 is a key (s is wave-uniform)
-                const uint32_t f = member_fp16(plen, b[0], b[1]);
-                const uint32_t pat = f | (f << 16);
-                u16x2 m = __builtin_bit_cast(u16x2, fpr[0] ^ pat);
-#pragma unroll
-                for (uint32_t i = 1; i < HT_FP_KEYS / 2; ++i)
-                    m = __builtin_elementwise_min(m, __builtin_bit_cast(u16x2, fpr[i] ^ pat));
-                dupfp |= chk & walk & ((m.x == 0) | (m.y == 0));
-#pragma unroll
-                for (uint32_t i = HT_FP_KEYS / 2 - 1; i > 0; --i) fpr[i] = __builtin_amdgcn_alignbit(fpr[i], fpr[i - 1], 16);
-                fpr[0] = (fpr[0] << 16) | f;
-            }
+        for (uint32_t j = 0; j < G; ++j) {
+            uint32_t x[2];
+            R.template get<2>(p, x);
             const uint32_t rem = end - p;
             const bool done = p == end;
-            const bool bad = (rem < 8) | (b[3] != 0) | (b[2] > rem - 8) | (k >= l.r);
+            const bool bad = (rem < 8) | (x[1] != 0) | (x[0] > rem - 8) | (k >= l.r);
             fail |= walk & !done & bad;
             const bool ok = walk & !done & !bad;
             mine = j == g ? ok : mine;
             mp = j == g ? p : mp;
-            ml = j == g ? b[2] : ml;
+            ml = j == g ? x[0] : ml;
             mk = j == g ? k : mk;
-            plen = b[2];
-            p = ok ? p + 8 + b[2] : p;
+            p = ok ? p + 8 + x[0] : p;
             k += ok;
             walk = ok;
         }
         put_desc(l.E, mine ? l.slot(mk) : NOSLOT, l.B + mp + 8, ml, RR_K_STR, 0);
         pay += mine ? ml : 0;
+        uint32_t t[2];
+        R.template get<2>(mp + ml, t);   // bytes [mp + 8 + ml - 8, mp + 8 + ml): the member's last 8
+        const bool key = mine & (!hash | ((mk & 1) == 0));
+        const uint32_t f = key ? member_fp16(ml, t[0], t[1]) : 0xFFFFFFFFu;
+#pragma unroll
+        for (uint32_t q = 0; q < HT_G_ROUNDS; ++q) fps[q] = r == q ? f : fps[q];
         if (__ballot(walk) == 0) break;
     }
+    // key i = element e (hash: 2i) sits on lane e % G of the group, round e / G
+    bool dup = false;
+    const uint32_t keys = hash ? k >> 1 : k;
+    const uint32_t base = lane_id() - g;
+    for (uint32_t i = 1; __ballot(chk & (i < keys)) != 0; ++i) {
+        const uint32_t e = hash ? 2 * i : i, q = e / G, owner = e - q * G;
+        if (q >= HT_G_ROUNDS) break;
+        const uint32_t src = q == 0 ? fps[0] : q == 1 ? fps[1] : q == 2 ? fps[2] : fps[3];
+        const uint32_t x = (uint32_t)__shfl((int)src, (int)(base + owner), RR_WAVE);
+#pragma unroll
+        for (uint32_t qq = 0; qq < HT_G_ROUNDS; ++qq)
+            dup |= (qq <= q) & (qq * G + g < e) & (fps[qq] == x) & (x != 0xFFFFFFFFu);
+    }
+    const uint64_t gm = (G >= 64 ? ~0ull : ((1ull << G) - 1)) << base;
+    const bool dupg = (__ballot(dup) & gm) != 0;
     n = k;
     const bool cnt_ok = !hash ? (uint64_t)k == cnt : ((k & 1) == 0 && (uint64_t)(k >> 1) == cnt);
-    fix = dupfp && k >= (hash ? 4u : 2u);
+    fix = active && (cnt > HT_FP_KEYS || (chk && dupg)) && k >= (hash ? 4u : 2u);
     return fail || !cnt_ok || k != l.r;
 }
 

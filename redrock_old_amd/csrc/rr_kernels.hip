@@ -765,8 +765,9 @@ __device__ __forceinline__ Acc run_batch(const Src &src, uint32_t c, bool active
             enc = H.f5();
         } else if (c == C_LIST) {
             fail = do_list_g(src, l, active, G, g, ne, vp);
-        } else if (c == C_HT || c == C_HH) {   // (lane per value: the fingerprints are chain work)
-            fail = do_ht(src, H, l, active, ne, vp, fixup, c == C_HH);
+        } else if (c == C_HT || c == C_HH) {   // lane per value (G == 1) unless RR_HT_GROUPED
+            if (G > 1) fail = do_ht_g(src, H, l, active, G, g, ne, vp, fixup, c == C_HH);
+            else fail = do_ht(src, H, l, active, ne, vp, fixup, c == C_HH);
         } else if (c == C_SL) {
             fail = do_skiplist_g(src, H, l, active, G, g, ne, vp);
         } else {   // C_ZL: G == 2, lane 1 of the pair walks backward
@@ -827,6 +828,9 @@ static_assert(DEC_BL >= 2 && DEC_BL <= RR_WAVE && DEC_BL % 2 == 0, "batch lanes"
 // during staging
 #ifndef RR_DEC_LATECOPY
 #define RR_DEC_LATECOPY 0
+#endif
+#ifndef RR_DEC_GLDS   // late-copy staging by global_load_lds (LDS-DMA) instead of register loads
+#define RR_DEC_GLDS 0
 #endif
 #ifndef RR_DEC_SU   // 16-byte staging loads in flight per thread (late-copy staging)
 #define RR_DEC_SU 4
@@ -892,6 +896,22 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
     // 1. value bytes -> LDS only; the window's arena copy is written in step 4 by waves that
     //    have run out of batches, overlapping the longest walks
     if (tid == 0) next_copy = 0;
+#if RR_DEC_GLDS
+    // every stage load in flight at once, straight to LDS (no VGPRs): wave w fills the 1 KiB
+    // blocks w, w + NW, ... (lane-linear: lane l's 16 bytes land at block + 16 l)
+    if (staged) {
+        const uint64_t cs0 = S0 >> 4, cs1 = S1 >> 4;
+        const uint32_t nblk = (uint32_t)((cs1 - cs0 + RR_WAVE - 1) / RR_WAVE);
+        for (uint32_t b = wave; b < nblk; b += NW) {
+            const uint64_t g = cs0 + (uint64_t)b * RR_WAVE + lane;
+            if (g < cs1)
+                __builtin_amdgcn_global_load_lds((const void *)(blob + g * 16),
+                                                 (__attribute__((address_space(3))) void *)(stage + b * 16 * RR_WAVE),
+                                                 16, 0, 0);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+#else
     if (staged) {
         const u32x4 *src = reinterpret_cast<const u32x4 *>(blob);
         u32x4 *lds = reinterpret_cast<u32x4 *>(stage);
@@ -906,6 +926,7 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
         }
         for (; c < cs1; c += NT) lds[c - cs0] = src[c];
     }
+#endif
 #else
     // 1. window -> arena, value bytes -> LDS (one load feeds both)
     {
@@ -1030,8 +1051,13 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
             PROBE(const uint64_t tb0 = __builtin_amdgcn_s_memtime();)
             // lanes per value: ziplists 2 (two-ended walk), chained classes 64 / cnt (grouped walks)
             const bool grouped = c == C_LIST || c == C_SL || c == C_IS;
-            const uint32_t G = __builtin_amdgcn_readfirstlane(
-                c == C_ZL ? 2u : grouped ? max(1u, min(GMAX, (uint32_t)RR_WAVE / cnt)) : 1u);
+            const uint32_t Gw = max(1u, min(GMAX, (uint32_t)RR_WAVE / cnt));
+#ifdef RR_HT_GROUPED   // timing builds (tools/): grouped hash-table walks (measured slower)
+            const bool htg = (c == C_HT || c == C_HH) && Gw >= ht_group_min(c == C_HH);
+#else
+            const bool htg = false;
+#endif
+            const uint32_t G = __builtin_amdgcn_readfirstlane(c == C_ZL ? 2u : (grouped || htg) ? Gw : 1u);
             const uint32_t li = lane / G, g = lane - li * G;   // the value's index in the batch
             const bool active = li < cnt;
             const uint64_t v = c0 + (active ? perm[first + li] : 0u);

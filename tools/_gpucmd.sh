@@ -1,8 +1,7 @@
 set -e
 mkdir -p gpurun_out
-timeout -k 10 400 python -u bench.py > gpurun_out/r2_bench.log 2>&1
-tail -1 gpurun_out/r2_bench.log > gpurun_out/r2_bench.json
-timeout -k 10 400 bash tools/profile_bench.sh gpurun_out/r2prof
-RR_PROFILE=encode timeout -k 10 400 bash tools/profile_bench.sh gpurun_out/r2prof_enc
-timeout -k 10 600 bash tools/pmc_decode.sh gpurun_out/r2pmc 4
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/t17.log 2>&1
+CONFIGS="4 3" timeout -k 10 300 bash tools/var_sweep.sh > gpurun_out/sweep2.log 2>&1
+CONFIGS="4 3" timeout -k 10 300 bash tools/var_sweep.sh >> gpurun_out/sweep2.log 2>&1
+RR_LIB=librr_serdes_probe.so timeout -k 10 100 python tools/probe_decode.py 4 > gpurun_out/probe2.log 2>&1
 echo done
