@@ -41,6 +41,16 @@ def lib():
         L.rro_store_free.argtypes = [vp]
         L.rro_store_free.restype = None
         L.rro_nprocs.restype = C.c_int
+        L.rrs_max_compressed.argtypes = [u64]
+        L.rrs_max_compressed.restype = u64
+        L.rrs_compress.argtypes = [vp, u64, vp]
+        L.rrs_compress.restype = u64
+        L.rrs_uncompressed_length.argtypes = [vp, u64, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
+        L.rrs_uncompress.argtypes = [vp, u64, vp, u64, C.POINTER(C.c_uint64)]
+        L.rrs_compress_batch.argtypes = [vp, vp, u64, vp, vp, vp, C.c_int]
+        L.rrs_compress_batch.restype = None
+        L.rrs_uncompress_batch.argtypes = [vp, vp, u64, vp, vp, vp, C.c_int]
+        L.rrs_uncompress_batch.restype = None
         _lib = L
     return _lib
 
@@ -129,3 +139,68 @@ def faithful_roundtrip(data, offsets):
     t3 = time.perf_counter()
     L.rro_store_free(st)
     return out[:int(ooff[-1])], ooff, int(bad.value), t1 - t0, t3 - t2
+
+
+# ---- snappy raw format (oracle/rr_snappy.c) ---------------------------
+def snappy_compress(data: bytes) -> bytes:
+    src = np.frombuffer(bytes(data), np.uint8)
+    out = np.zeros(int(lib().rrs_max_compressed(len(src))) + 8, np.uint8)
+    n = lib().rrs_compress(_p(src), len(src), _p(out))
+    return out[:n].tobytes()
+
+
+def snappy_uncompress(comp: bytes, cap: int | None = None):
+    """(status, bytes or None); cap defaults to the preamble's length."""
+    src = np.frombuffer(bytes(comp), np.uint8)
+    ln, hdr = C.c_uint32(), C.c_uint32()
+    st = lib().rrs_uncompressed_length(_p(src), len(src), C.byref(ln), C.byref(hdr))
+    if st:
+        return st, None
+    if cap is None:
+        cap = ln.value
+    out = np.zeros(max(cap, 1), np.uint8)
+    got = C.c_uint64()
+    st = lib().rrs_uncompress(_p(src), len(src), _p(out), cap, C.byref(got))
+    return st, (out[:got.value].tobytes() if st == 0 else None)
+
+
+def snappy_length(comp: bytes):
+    """(status, announced uncompressed length) of a snappy stream's preamble."""
+    src = np.frombuffer(bytes(comp), np.uint8)
+    ln, hdr = C.c_uint32(), C.c_uint32()
+    st = lib().rrs_uncompressed_length(_p(src), len(src), C.byref(ln), C.byref(hdr))
+    return st, (ln.value if st == 0 else 0)
+
+
+def snappy_compress_blocks(data, offs, nthreads=1):
+    """Every block [offs[i], offs[i+1]) compressed: (packed bytes, offsets, seconds)."""
+    L = lib()
+    offs = np.ascontiguousarray(offs, np.uint64)
+    n = len(offs) - 1
+    bounds = np.array([L.rrs_max_compressed(int(offs[i + 1] - offs[i])) for i in range(n)], np.uint64)
+    slot = np.zeros(n + 1, np.uint64)
+    np.cumsum(bounds, out=slot[1:])
+    out = np.zeros(int(slot[-1]) + 16, np.uint8)
+    sizes = np.zeros(max(n, 1), np.uint64)
+    data = np.ascontiguousarray(data, np.uint8)
+    t0 = time.perf_counter()
+    L.rrs_compress_batch(_p(data), _p(offs), n, _p(out), _p(slot), _p(sizes), nthreads)
+    dt = time.perf_counter() - t0
+    coffs = np.zeros(n + 1, np.uint64)
+    np.cumsum(sizes[:n], out=coffs[1:])
+    packed = np.concatenate([out[int(slot[i]):int(slot[i] + sizes[i])] for i in range(n)]) if n else np.zeros(0, np.uint8)
+    return packed, coffs, dt
+
+
+def snappy_uncompress_blocks(comp, coffs, out_offs, nthreads=1):
+    """Blocks of comp into slots [out_offs[i], out_offs[i+1]): (out, status, seconds)."""
+    L = lib()
+    coffs = np.ascontiguousarray(coffs, np.uint64)
+    out_offs = np.ascontiguousarray(out_offs, np.uint64)
+    n = len(coffs) - 1
+    out = np.zeros(int(out_offs[-1]) + 16, np.uint8)
+    st = np.zeros(max(n, 1), np.uint8)
+    comp = np.ascontiguousarray(comp, np.uint8)
+    t0 = time.perf_counter()
+    L.rrs_uncompress_batch(_p(comp), _p(coffs), n, _p(out), _p(out_offs), _p(st), nthreads)
+    return out[:int(out_offs[-1])], st[:n], time.perf_counter() - t0

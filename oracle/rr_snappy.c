@@ -1,0 +1,280 @@
+/*
+ * rr_snappy.c — TEST INFRASTRUCTURE (oracle).  Plain-C restatement of the snappy raw block
+ * format that RocksDB applies to its data blocks by default (the
+ * reference links the vendored deps/snappy, v1.1.8 per deps/snappy/NEWS:1, and leaves
+ * options.compression at RocksDB's default, src/rocksdbapi.cc:159-161).
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg load this file; the
+ * product (redrock_old_amd/csrc/rr_snappy.hip) never does.
+ *
+ *   rrs_compress    = snappy::RawCompress (snappy.cc:1398-1408 -> Compress): varint32 of the
+ *                     length, then every 64 KiB fragment by CompressFragment (snappy.cc:
+ *                     540-660) with a fresh hash table sized by CalculateTableSize (:442-455),
+ *                     literals by EmitLiteral (:357-377), copies by EmitCopy (:379-427).
+ *   rrs_uncompress  = snappy::RawUncompress + its validation (snappy.cc:779-800 length,
+ *                     :808-905 DecompressAllTags, SnappyArrayWriter Append / AppendFromSelf
+ *                     bounds, the eof + CheckLength test of InternalUncompressAllTags), with a
+ *                     status code per failure instead of `false`.
+ *
+ * Pinned against an independent build of the same published algorithm: pyarrow's bundled
+ * snappy (tests/test_snappy.py) — byte-identical compressed output and identical accept /
+ * reject decisions on the reference's own deps/snappy/testdata files (tests/golden/snappy/).
+ */
+#include "rr_snappy.h"
+
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define BLOCK_LOG 16
+#define BLOCK_SIZE (1u << BLOCK_LOG)               /* snappy.h:197-198 */
+#define MIN_TABLE (1u << 8)                        /* snappy.h:200-201 */
+#define MAX_TABLE (1u << 14)                       /* snappy.h:203-204 */
+#define INPUT_MARGIN 15                            /* snappy.cc:561 kInputMarginBytes */
+
+static uint32_t ld32(const uint8_t *p) { uint32_t v; memcpy(&v, p, 4); return v; }
+static uint64_t ld64(const uint8_t *p) { uint64_t v; memcpy(&v, p, 8); return v; }
+static uint32_t hash32(uint32_t bytes, int shift) { return (bytes * 0x1e35a7bdu) >> shift; }   /* snappy.cc:90-93 */
+static int log2floor(uint32_t n) { return 31 - __builtin_clz(n); }
+
+uint64_t rrs_max_compressed(uint64_t n) { return 32 + n + n / 6; }   /* snappy.cc:98-118 */
+
+/* snappy.cc:442-455 */
+static uint32_t table_size(uint32_t n) {
+    if (n > MAX_TABLE) return MAX_TABLE;
+    if (n < MIN_TABLE) return MIN_TABLE;
+    return 2u << log2floor(n - 1);
+}
+
+/* EmitLiteral, snappy.cc:357-377 (both fast-path forms write the same bytes) */
+static uint8_t *emit_literal(uint8_t *op, const uint8_t *lit, uint32_t len) {
+    const uint32_t n = len - 1;
+    if (n < 60) {
+        *op++ = (uint8_t)(n << 2);
+    } else {
+        const int count = (log2floor(n) >> 3) + 1;
+        *op++ = (uint8_t)((59 + count) << 2);
+        for (int i = 0; i < count; ++i) *op++ = (uint8_t)(n >> (8 * i));
+    }
+    memcpy(op, lit, len);
+    return op + len;
+}
+
+/* EmitCopyAtMost64, snappy.cc:379-397 */
+static uint8_t *emit_copy64(uint8_t *op, uint32_t offset, uint32_t len, int allow_short) {
+    if (allow_short && len < 12 && offset < 2048) {
+        *op++ = (uint8_t)(1 + ((len - 4) << 2) + ((offset >> 3) & 0xe0));
+        *op++ = (uint8_t)offset;
+    } else {
+        *op++ = (uint8_t)(2 + ((len - 1) << 2));
+        *op++ = (uint8_t)offset;
+        *op++ = (uint8_t)(offset >> 8);
+    }
+    return op;
+}
+
+/* EmitCopy, snappy.cc:399-427: 64-byte pieces (keeping >= 4 for the last), one 60 if the rest
+ * is above 64, then the remainder (the short copy-1 form only for the remainder) */
+static uint8_t *emit_copy(uint8_t *op, uint32_t offset, uint32_t len) {
+    if (len < 12) return emit_copy64(op, offset, len, 1);
+    while (len >= 68) { op = emit_copy64(op, offset, 64, 0); len -= 64; }
+    if (len > 64) { op = emit_copy64(op, offset, 60, 0); len -= 60; }
+    return emit_copy64(op, offset, len, 1);
+}
+
+/* FindMatchLength (snappy-internal.h:95-143): bytes of s1 equal to s2 up to s2_limit */
+static uint32_t match_len(const uint8_t *s1, const uint8_t *s2, const uint8_t *s2_limit) {
+    uint32_t m = 0;
+    while (s2 + m + 8 <= s2_limit) {
+        const uint64_t x = ld64(s2 + m) ^ ld64(s1 + m);
+        if (x) return m + (uint32_t)(__builtin_ctzll(x) >> 3);
+        m += 8;
+    }
+    while (s2 + m < s2_limit && s1[m] == s2[m]) ++m;
+    return m;
+}
+
+/* CompressFragment, snappy.cc:540-660 */
+static uint8_t *compress_fragment(const uint8_t *input, uint32_t n, uint8_t *op, uint16_t *table, uint32_t tsize) {
+    const uint8_t *ip = input, *ip_end = input + n, *base = input, *next_emit = input;
+    const int shift = 32 - log2floor(tsize);
+    if (n >= INPUT_MARGIN) {
+        const uint8_t *ip_limit = input + n - INPUT_MARGIN;
+        uint32_t next_hash = hash32(ld32(++ip), shift);
+        for (;;) {
+            /* step 1: scan for a 4-byte match, skipping faster the longer none is found */
+            uint32_t skip = 32;
+            const uint8_t *next_ip = ip, *cand;
+            do {
+                ip = next_ip;
+                const uint32_t h = next_hash;
+                const uint32_t between = skip >> 5;
+                skip += between;
+                next_ip = ip + between;
+                if (next_ip > ip_limit) goto remainder;
+                next_hash = hash32(ld32(next_ip), shift);
+                cand = base + table[h];
+                table[h] = (uint16_t)(ip - base);
+            } while (ld32(ip) != ld32(cand));
+            /* step 2: the bytes before the match as a literal */
+            op = emit_literal(op, next_emit, (uint32_t)(ip - next_emit));
+            /* step 3: copies while the bytes right after the last copy match again */
+            uint32_t cur;
+            uint32_t cand_bytes;
+            do {
+                const uint8_t *b = ip;
+                const uint32_t matched = 4 + match_len(cand + 4, ip + 4, ip_end);
+                ip += matched;
+                op = emit_copy(op, (uint32_t)(b - cand), matched);
+                next_emit = ip;
+                if (ip >= ip_limit) goto remainder;
+                const uint64_t in8 = ld64(ip - 1);
+                table[hash32((uint32_t)in8, shift)] = (uint16_t)(ip - base - 1);
+                cur = (uint32_t)(in8 >> 8);
+                const uint32_t ch = hash32(cur, shift);
+                cand = base + table[ch];
+                cand_bytes = ld32(cand);
+                table[ch] = (uint16_t)(ip - base);
+            } while (cur == cand_bytes);
+            next_hash = hash32((uint32_t)(ld64(ip - 1) >> 16), shift);
+            ++ip;
+        }
+    }
+remainder:
+    if (next_emit < ip_end) op = emit_literal(op, next_emit, (uint32_t)(ip_end - next_emit));
+    return op;
+}
+
+/* RawCompress -> Compress (snappy.cc:1000-1060): varint32 length, then 64 KiB fragments */
+uint64_t rrs_compress(const uint8_t *in, uint64_t n, uint8_t *out) {
+    uint8_t *op = out;
+    uint32_t v = (uint32_t)n;
+    while (v >= 128) { *op++ = (uint8_t)(v | 128); v >>= 7; }
+    *op++ = (uint8_t)v;
+    uint16_t *table = (uint16_t *)malloc(MAX_TABLE * sizeof(uint16_t));
+    for (uint64_t at = 0; at < n; at += BLOCK_SIZE) {
+        const uint32_t frag = (uint32_t)(n - at < BLOCK_SIZE ? n - at : BLOCK_SIZE);
+        const uint32_t ts = table_size(frag);
+        memset(table, 0, ts * sizeof(uint16_t));
+        op = compress_fragment(in + at, frag, op, table, ts);
+    }
+    free(table);
+    return (uint64_t)(op - out);
+}
+
+/* ReadUncompressedLength, snappy.cc:779-800 */
+int rrs_uncompressed_length(const uint8_t *in, uint64_t n, uint32_t *len, uint32_t *hdr) {
+    uint32_t r = 0, shift = 0, i = 0;
+    for (;;) {
+        if (shift >= 32 || i >= n) return RRS_E_HEADER;
+        const uint32_t c = in[i++], val = c & 0x7f;
+        if (shift == 28 && val >= 16) return RRS_E_HEADER;   /* LeftShiftOverflows */
+        r |= val << shift;
+        if (c < 128) break;
+        shift += 7;
+    }
+    *len = r;
+    if (hdr) *hdr = i;
+    return RRS_OK;
+}
+
+/* RawUncompress: DecompressAllTags (snappy.cc:808-905) into a SnappyArrayWriter of `expected`
+ * bytes; eof and CheckLength at the end */
+int rrs_uncompress(const uint8_t *in, uint64_t n, uint8_t *out, uint64_t out_cap, uint64_t *out_len) {
+    uint32_t expected, i;
+    if (rrs_uncompressed_length(in, n, &expected, &i) != RRS_OK) return RRS_E_HEADER;
+    if (expected > out_cap) return RRS_E_CAPACITY;
+    uint64_t o = 0;
+    while (i < n) {
+        const uint32_t c = in[i++];
+        if ((c & 3) == 0) {   /* literal */
+            uint64_t len = (c >> 2) + 1;
+            if (len >= 61) {
+                const uint32_t nb = (uint32_t)len - 60;
+                if (i + nb > n) return RRS_E_TRUNC;
+                uint32_t v = 0;
+                for (uint32_t k = 0; k < nb; ++k) v |= (uint32_t)in[i + k] << (8 * k);
+                len = (uint64_t)v + 1;
+                i += nb;
+            }
+            if (len > n - i) return RRS_E_TRUNC;
+            if (len > expected - o) return RRS_E_OVERFLOW;
+            memcpy(out + o, in + i, len);
+            o += len;
+            i += (uint32_t)len;
+        } else {              /* copy: 1, 2 or 4 offset bytes */
+            const uint32_t t = c & 3, nb = t == 1 ? 1 : t == 2 ? 2 : 4;
+            if (i + nb > n) return RRS_E_TRUNC;
+            uint32_t len, off;
+            if (t == 1) {
+                len = 4 + ((c >> 2) & 7);
+                off = ((c >> 5) << 8) | in[i];
+            } else {
+                len = (c >> 2) + 1;
+                off = t == 2 ? (uint32_t)in[i] | ((uint32_t)in[i + 1] << 8) : ld32(in + i);
+            }
+            i += nb;
+            if (o <= (uint64_t)off - 1u || off == 0) return RRS_E_OFFSET;   /* AppendFromSelf */
+            if (len > expected - o) return RRS_E_OVERFLOW;
+            for (uint32_t k = 0; k < len; ++k) out[o + k] = out[o - off + k];   /* overlapping: byte order */
+            o += len;
+        }
+    }
+    if (o != expected) return RRS_E_LENGTH;
+    if (out_len) *out_len = o;
+    return RRS_OK;
+}
+
+/* ---- batches on host threads (the CPU baseline) ---- */
+typedef struct {
+    const uint8_t *in;
+    const uint64_t *offs;
+    uint8_t *out;
+    const uint64_t *slot;      /* compress: output slot starts; uncompress: output offsets */
+    uint64_t *sizes;           /* compress: compressed size per block */
+    uint8_t *status;
+    uint64_t lo, hi;
+    int mode;
+} job_t;
+
+static void *worker(void *arg) {
+    job_t *j = (job_t *)arg;
+    for (uint64_t b = j->lo; b < j->hi; ++b) {
+        const uint8_t *src = j->in + j->offs[b];
+        const uint64_t len = j->offs[b + 1] - j->offs[b];
+        if (j->mode == 0) {
+            j->sizes[b] = rrs_compress(src, len, j->out + j->slot[b]);
+        } else {
+            uint64_t got = 0;
+            j->status[b] = (uint8_t)rrs_uncompress(src, len, j->out + j->slot[b], j->slot[b + 1] - j->slot[b], &got);
+        }
+    }
+    return NULL;
+}
+
+static void run(job_t base, uint64_t n, int nthreads) {
+    if (nthreads < 1) nthreads = 1;
+    if ((uint64_t)nthreads > n) nthreads = n ? (int)n : 1;
+    pthread_t th[256];
+    job_t jobs[256];
+    if (nthreads > 256) nthreads = 256;
+    for (int t = 0; t < nthreads; ++t) {
+        jobs[t] = base;
+        jobs[t].lo = n * t / nthreads;
+        jobs[t].hi = n * (t + 1) / nthreads;
+        pthread_create(&th[t], NULL, worker, &jobs[t]);
+    }
+    for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+}
+
+void rrs_compress_batch(const uint8_t *in, const uint64_t *offs, uint64_t n, uint8_t *out, const uint64_t *slot,
+                        uint64_t *sizes, int nthreads) {
+    job_t j = {in, offs, out, slot, sizes, NULL, 0, 0, 0};
+    run(j, n, nthreads);
+}
+
+void rrs_uncompress_batch(const uint8_t *in, const uint64_t *offs, uint64_t n, uint8_t *out, const uint64_t *out_offs,
+                          uint8_t *status, int nthreads) {
+    job_t j = {in, offs, out, out_offs, NULL, status, 0, 0, 1};
+    run(j, n, nthreads);
+}

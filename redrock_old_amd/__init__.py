@@ -72,6 +72,10 @@ EXPORTS = ["rr_ctx_create", "rr_ctx_destroy", "rr_ctx_reserve", "rr_last_error",
            "rr_gen_batch", "rr_host_batch_free", "rr_gen_default_seed", "rr_shard_plan", "rr_flat_rebase",
            "rr_comm_get_id", "rr_comm_init", "rr_comm_destroy", "rr_split_plan", "rr_split", "rr_gather"]
 COMM_ID_BYTES = 128
+# include/rr_snappy.h (GPU block compression)
+SNAPPY_EXPORTS = ["rr_snappy_max_compressed_length", "rr_snappy_compress_bound", "rr_snappy_compress_batch",
+                  "rr_snappy_decompress_batch", "rr_snappy_compress_batch_host", "rr_snappy_decompress_batch_host"]
+SNAPPY_STATUS = {0: "OK", 1: "HEADER", 2: "TRUNC", 3: "OFFSET", 4: "OVERFLOW", 5: "LENGTH", 6: "CAPACITY"}
 
 _lib = None
 
@@ -116,6 +120,14 @@ def lib():
     L.rr_split_plan.argtypes = [vp, C.POINTER(BlobBatch), C.c_int, C.POINTER(Shard), vp]
     L.rr_split.argtypes = [vp, C.POINTER(BlobBatch), C.POINTER(Shard), C.c_int, C.POINTER(BlobBatch), vp]
     L.rr_gather.argtypes = [vp, C.POINTER(FlatBatch), u64, C.POINTER(Shard), C.c_int, C.POINTER(FlatBatch), vp]
+    L.rr_snappy_max_compressed_length.argtypes = [u64]
+    L.rr_snappy_max_compressed_length.restype = u64
+    L.rr_snappy_compress_bound.argtypes = [u64, u64]
+    L.rr_snappy_compress_bound.restype = u64
+    L.rr_snappy_compress_batch.argtypes = [vp, C.POINTER(BlobBatch), C.POINTER(BlobBatch), vp]
+    L.rr_snappy_decompress_batch.argtypes = [vp, C.POINTER(BlobBatch), C.POINTER(BlobBatch), vp, vp]
+    L.rr_snappy_compress_batch_host.argtypes = [vp, vp, vp, u64, vp, u64, vp]
+    L.rr_snappy_decompress_batch_host.argtypes = [vp, vp, vp, u64, vp, u64, vp, vp]
     _lib = L
     return L
 
@@ -228,6 +240,43 @@ class Engine:
         _check(self._L.rr_flat_rebase(self._ctx, C.c_void_p(values.data_ptr()), values.numel() // 16,
                                       C.c_void_p(elems.data_ptr()), elems.numel() // 16, elem_add, byte_add,
                                       _sp(stream)))
+
+    # ---- snappy block compression (include/rr_snappy.h) -----------------------------------
+    def snappy_compress_host(self, data: np.ndarray, offsets: np.ndarray):
+        """Blocks [offsets[i], offsets[i+1]) of data -> (packed compressed bytes, offsets)."""
+        data = np.ascontiguousarray(data, np.uint8)
+        offsets = np.ascontiguousarray(offsets, np.uint64)
+        n = len(offsets) - 1
+        cap = int(self._L.rr_snappy_compress_bound(n, int(offsets[-1])))
+        out = np.zeros(max(cap, 1), np.uint8)
+        oo = np.zeros(n + 1, np.uint64)
+        _check(self._L.rr_snappy_compress_batch_host(self._ctx, _ptr(data), _ptr(offsets), n, _ptr(out), cap, _ptr(oo)))
+        return out[:int(oo[-1])], oo
+
+    def snappy_decompress_host(self, comp: np.ndarray, offsets: np.ndarray, out_cap: int):
+        """(out bytes, out offsets, per-block status) of snappy blocks."""
+        comp = np.ascontiguousarray(comp, np.uint8)
+        offsets = np.ascontiguousarray(offsets, np.uint64)
+        n = len(offsets) - 1
+        out = np.zeros(max(out_cap, 1), np.uint8)
+        oo = np.zeros(n + 1, np.uint64)
+        st = np.zeros(max(n, 1), np.uint8)
+        _check(self._L.rr_snappy_decompress_batch_host(self._ctx, _ptr(comp), _ptr(offsets), n, _ptr(out), out_cap,
+                                                       _ptr(oo), _ptr(st)))
+        return out[:int(oo[-1])], oo, st[:n]
+
+    def snappy_compress_device(self, data, offsets, out, out_offsets, stream=None):
+        n = offsets.numel() - 1
+        inb = BlobBatch(data.data_ptr(), offsets.data_ptr(), n, data.numel())
+        outb = BlobBatch(out.data_ptr(), out_offsets.data_ptr(), n, out.numel())
+        _check(self._L.rr_snappy_compress_batch(self._ctx, C.byref(inb), C.byref(outb), _sp(stream)))
+
+    def snappy_decompress_device(self, comp, offsets, out, out_offsets, status, stream=None):
+        n = offsets.numel() - 1
+        inb = BlobBatch(comp.data_ptr(), offsets.data_ptr(), n, comp.numel())
+        outb = BlobBatch(out.data_ptr(), out_offsets.data_ptr(), n, out.numel())
+        _check(self._L.rr_snappy_decompress_batch(self._ctx, C.byref(inb), C.byref(outb),
+                                                  C.c_void_p(status.data_ptr()), _sp(stream)))
 
     def encode_device(self, values, elems, arena, out_data, out_offsets, totals, stream=None):
         n = out_offsets.numel() - 1

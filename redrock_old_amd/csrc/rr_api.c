@@ -22,6 +22,9 @@ int rr_fail(int code, const char *fmt, ...) {
     return code;
 }
 #define fail rr_fail
+#define ensure_scratch rr_ensure_scratch
+#define mark_scratch rr_mark_scratch
+#define dgrow rr_dgrow
 
 int rr_ctx_create(int device, rr_ctx **out) {
     if (!out) return fail(RR_API_EINVAL, "out is NULL");
@@ -71,7 +74,7 @@ void rr_ctx_destroy(rr_ctx *c) {
  * scratch_done marks their end (whatever stream they ran on), so only that wait is needed — no
  * device-wide synchronisation.  Growing allocates, which a stream under graph capture cannot do:
  * size the scratch with rr_ctx_reserve before capturing. */
-static int ensure_scratch(rr_ctx *c, uint64_t words, hipStream_t stream) {
+int rr_ensure_scratch(rr_ctx *c, uint64_t words, hipStream_t stream) {
     if (c->scratch && words <= c->scratch_words) return RR_API_OK;
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     if (stream && hipStreamIsCapturing(stream, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
@@ -92,7 +95,7 @@ static int ensure_scratch(rr_ctx *c, uint64_t words, hipStream_t stream) {
 
 /* after a call's launches: remember where its use of the scratch ends (not under capture: the
  * captured graph replays later, and capture never grows the scratch) */
-static int mark_scratch(rr_ctx *c, hipStream_t stream) {
+int rr_mark_scratch(rr_ctx *c, hipStream_t stream) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     if (stream && hipStreamIsCapturing(stream, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
         return RR_API_OK;
@@ -147,7 +150,7 @@ int rr_encode_batch(rr_ctx *c, const rr_flat_batch *in, rr_blob_batch *out, rr_t
 }
 
 /* grow a device staging buffer (host entry points only) */
-static int dgrow(void **p, size_t *cap, size_t need) {
+int rr_dgrow(void **p, size_t *cap, size_t need) {
     if (need <= *cap && *p) return RR_API_OK;
     if (*p) hipFree(*p);
     *p = NULL;

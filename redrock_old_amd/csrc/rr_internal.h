@@ -1,4 +1,4 @@
-/* rr_internal.h — what the C host files of the engine share (rr_api.c, rr_shard.c). */
+/* rr_internal.h — what the C host files of the engine share (rr_api.c, rr_shard.c, rr_snappy_api.c). */
 #ifndef RR_INTERNAL_H
 #define RR_INTERNAL_H
 
@@ -16,6 +16,13 @@ struct rr_ctx {
     size_t c_in, c_off, c_vals, c_elems, c_arena, c_out, c_ooff;
     rr_totals *d_totals;
 };
+
+/* the context's scratch: grow to `words` (waits on the previous call through an event; fails
+ * under graph capture), and mark the end of a call's use of it */
+int rr_ensure_scratch(rr_ctx *c, uint64_t words, hipStream_t stream);
+int rr_mark_scratch(rr_ctx *c, hipStream_t stream);
+/* grow a device staging buffer of the host entry points */
+int rr_dgrow(void **p, size_t *cap, size_t need);
 
 /* sets rr_last_error() and returns code */
 int rr_fail(int code, const char *fmt, ...);

@@ -24,6 +24,14 @@ hipError_t rr_launch_encode(const rr_value *values, const rr_elem *elems, uint64
                             uint64_t arena_cap, uint64_t n, uint8_t *out, uint64_t cap, uint64_t *offsets,
                             uint64_t *scratch, rr_totals *totals, hipStream_t stream);
 uint64_t rr_decode_scratch_words(uint64_t data_cap, uint64_t n);
+uint64_t rr_scan_words(uint64_t n);
+hipError_t rr_launch_scan_u64(uint64_t *x, uint64_t n, uint64_t *lb, uint64_t *err, hipStream_t stream);
+uint64_t rr_snappy_scratch_words(uint64_t n, uint64_t slot_bytes);
+hipError_t rr_launch_snappy_decompress(const uint8_t *in, uint64_t in_cap, const uint64_t *in_offs, uint64_t n, uint8_t *out,
+                                       uint64_t out_cap, uint64_t *out_offs, uint8_t *status, uint64_t *scratch,
+                                       hipStream_t stream);
+hipError_t rr_launch_snappy_compress(const uint8_t *in, uint64_t in_cap, const uint64_t *in_offs, uint64_t n, uint8_t *out,
+                                     uint64_t *out_offs, uint64_t *scratch, uint64_t slot_bytes, hipStream_t stream);
 hipError_t rr_launch_shard_plan(const uint64_t *offsets, uint64_t n, uint32_t g, uint64_t *plan, hipStream_t stream);
 hipError_t rr_launch_offsets_rebase(uint64_t *offs, uint64_t count, uint64_t sub, hipStream_t stream);
 hipError_t rr_launch_flat_rebase(rr_value *values, uint64_t n, rr_elem *elems, uint64_t ne, uint64_t elem_add,

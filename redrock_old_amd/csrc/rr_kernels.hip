@@ -2127,3 +2127,16 @@ extern "C" hipError_t rr_launch_flat_rebase(rr_value *values, uint64_t n, rr_ele
                        byte_add);
     return hipGetLastError();
 }
+
+// ---- the look-back scan for other launchers (rr_snappy.hip) --------------------------------
+// x[0..n) -> exclusive prefix in place, x[n] = total; lb (rr_scan_words(n) words) must be zero
+// and x[n] must be 0 beforehand (the caller's first kernel does both, as count_kernel does).
+extern "C" uint64_t rr_scan_words(uint64_t n) {
+    const uint64_t st = scan_tiles(n);
+    return 1 + st + (st + LB_GROUP - 1) / LB_GROUP;
+}
+extern "C" hipError_t rr_launch_scan_u64(uint64_t *x, uint64_t n, uint64_t *lb, uint64_t *err, hipStream_t stream) {
+    const uint32_t st = (uint32_t)scan_tiles(n);
+    if (st) hipLaunchKernelGGL(scan_kernel, dim3(st), dim3(256), 0, stream, x, n, lb, st, err);
+    return hipGetLastError();
+}

@@ -1,0 +1,438 @@
+// rr_snappy.hip — snappy raw-format compression / decompression of RocksDB data blocks on
+// gfx950 (include/rr_snappy.h).
+//
+// One wave per block for both directions: snappy's format is a chain (every tag's size decides
+// where the next one starts; the compressor's hash table is updated probe by probe), so a block
+// is a serial walk, and the wave's 64 lanes work inside each step — the copy of a literal or a
+// back-reference, the extension of a match, the staging of the block into LDS.  Parallelism
+// comes from many blocks in flight.
+//
+//   snz_len_kernel    thread per block: the varint32 length preamble -> out_offs[i] (then the
+//                     engine's look-back scan turns the lengths into packed offsets)
+//   snz_dec_kernel    wave per block: the compressed bytes through a 1 KiB register window
+//                     (16 B per lane, uniform tag parsing by readlane), the output assembled
+//                     in LDS and written out once; a block longer than the LDS window is
+//                     decompressed straight into global memory (copies then read their
+//                     sources back through the L2 after the wave's stores drained)
+//   snz_comp_kernel   wave per block: snappy 1.1.8's CompressFragment (oracle/rr_snappy.c
+//                     cites the lines) on a uniform control path, with the fragment and its
+//                     16K-entry hash table in LDS; output to a per-block slot
+//   snz_pack_kernel   wave per block: slots -> packed output
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rr_kernels.h"
+#include "../../include/rr_snappy.h"
+
+namespace {
+
+constexpr uint32_t WAVE = 64;
+constexpr uint32_t FRAG = 1u << 16;        // snappy kBlockSize (snappy.h:197-198)
+constexpr uint32_t TAB_MIN = 1u << 8;      // kMinHashTableSize
+constexpr uint32_t TAB_MAX = 1u << 14;     // kMaxHashTableSize
+constexpr uint32_t MARGIN = 15;            // kInputMarginBytes
+
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+__device__ __forceinline__ rsrc_t mkr(const void *base, uint64_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc((void *)base, 0, (int)(bytes < 0x7FFFFFF0ull ? bytes : 0x7FFFFFF0ull),
+                                             0x00020000);
+}
+__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+__device__ __forceinline__ uint32_t rdl(uint32_t v, uint32_t l) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
+}
+
+// ---- decompression ------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void snz_len_kernel(const uint8_t *__restrict__ in,
+                                                      const uint64_t *__restrict__ in_offs, uint64_t n,
+                                                      uint64_t *__restrict__ out_offs, uint8_t *__restrict__ status,
+                                                      uint64_t *__restrict__ lb, uint32_t lbw) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < lbw) lb[i] = 0;
+    if (i < n) {
+        const uint64_t c0 = in_offs[i], c1 = in_offs[i + 1];
+        uint32_t v = 0, shift = 0;
+        bool ok = false;
+        for (uint64_t k = c0; k < c1 && shift < 32; ++k, shift += 7) {   // ReadUncompressedLength
+            const uint32_t c = in[k], val = c & 0x7F;
+            if (shift == 28 && val >= 16) break;
+            v |= val << shift;
+            if (c < 128) { ok = true; break; }
+        }
+        out_offs[i] = ok ? v : 0;
+        status[i] = ok ? RR_SNAPPY_OK : RR_SNAPPY_E_HEADER;
+    } else if (i == n) {
+        out_offs[n] = 0;
+    }
+}
+
+// The compressed block through a register window: lane l holds bytes [wb + 16 l, wb + 16 l + 16)
+// of the block's buffer resource (positions q relative to it), 1 KiB in all.
+struct Win {
+    rsrc_t R;
+    uint32_t wb;
+    uint32_t x[4];
+    __device__ __forceinline__ void load(uint32_t at) {
+        wb = at & ~15u;
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(R, (int)(wb + 16 * lane_id()), 0, 0);
+        x[0] = v[0]; x[1] = v[1]; x[2] = v[2]; x[3] = v[3];
+    }
+    // the aligned dword at q (q - wb < 1024, q % 4 == 0), uniform
+    __device__ __forceinline__ uint32_t dw(uint32_t q) const {
+        const uint32_t r = q - wb, k = (r >> 2) & 3;
+        const uint32_t v = k == 0 ? x[0] : k == 1 ? x[1] : k == 2 ? x[2] : x[3];
+        return rdl(v, r >> 4);
+    }
+    // 5+ bytes starting at q (uniform), low byte first
+    __device__ __forceinline__ uint64_t bytes(uint32_t q) const {
+        const uint32_t a = q & ~3u;
+        const uint64_t v = (uint64_t)dw(a) | ((uint64_t)dw(a + 4) << 32);
+        return v >> (8 * (q & 3));
+    }
+};
+
+__device__ __forceinline__ void wait_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+__global__ __launch_bounds__(WAVE) void snz_dec_kernel(const uint8_t *__restrict__ in, uint64_t in_cap,
+                                                       const uint64_t *__restrict__ in_offs, uint64_t n,
+                                                       uint8_t *__restrict__ out, uint64_t out_cap,
+                                                       const uint64_t *__restrict__ out_offs,
+                                                       uint8_t *__restrict__ status, uint32_t wcap) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t win[];
+    const uint32_t lane = lane_id();
+    for (uint64_t b = blockIdx.x; b < n; b += gridDim.x) {
+        if (status[b] != RR_SNAPPY_OK) continue;   // (the preamble did not parse)
+        const uint64_t o0 = out_offs[b], o1 = out_offs[b + 1];
+        if (o1 > out_cap) {
+            if (lane == 0) status[b] = RR_SNAPPY_E_CAPACITY;
+            continue;
+        }
+        const uint32_t expected = (uint32_t)(o1 - o0);
+        const uint64_t c0 = in_offs[b], clen = in_offs[b + 1] - c0;
+        const uint32_t s0 = (uint32_t)(c0 & 3), end = s0 + (uint32_t)clen;
+        Win W;
+        W.R = mkr(in + (c0 - s0), in_cap - (c0 - s0));   // (whole dwords: the buffer's padding, not past it)
+        W.load(s0);
+        uint32_t p = s0;
+        while (W.bytes(p) & 0x80) ++p;   // the preamble (already validated)
+        ++p;
+        const bool inl = expected <= wcap;
+        uint8_t *gout = out + o0;
+        const rsrc_t Ro = mkr(gout, expected);
+        uint32_t pos = 0, st = RR_SNAPPY_OK;
+        while (p < end) {
+            if (p + 8 > W.wb + 1024) W.load(p);
+            const uint64_t t = W.bytes(p);
+            const uint32_t c = (uint32_t)t & 0xFF;
+            if ((c & 3) == 0) {   // literal
+                uint32_t len = (c >> 2) + 1, hdr = 1;
+                if (len >= 61) {
+                    const uint32_t nb = len - 60;
+                    if (p + 1 + nb > end) { st = RR_SNAPPY_E_TRUNC; break; }
+                    const uint32_t v = (uint32_t)(t >> 8);
+                    len = (nb == 4 ? v : v & ((1u << (8 * nb)) - 1)) + 1;
+                    hdr += nb;
+                    if (len == 0) { st = RR_SNAPPY_E_TRUNC; break; }   // (2^32 wrapped: more than any block)
+                }
+                p += hdr;
+                if (len > end - p) { st = RR_SNAPPY_E_TRUNC; break; }
+                if (len > expected - pos) { st = RR_SNAPPY_E_OVERFLOW; break; }
+                for (uint32_t i = 0; i < len; i += WAVE) {
+                    const uint32_t k = i + lane;
+                    if (k < len) {
+                        const uint8_t v = __builtin_amdgcn_raw_buffer_load_b8(W.R, (int)(p + k), 0, 0);
+                        if (inl) win[pos + k] = v;
+                        else __builtin_amdgcn_raw_buffer_store_b8(v, Ro, (int)(pos + k), 0, 0);
+                    }
+                }
+                pos += len;
+                p += len;
+            } else {              // copy with a 1-, 2- or 4-byte offset
+                const uint32_t ty = c & 3, nb = ty == 1 ? 1u : ty == 2 ? 2u : 4u;
+                if (p + 1 + nb > end) { st = RR_SNAPPY_E_TRUNC; break; }
+                const uint32_t v = (uint32_t)(t >> 8);
+                const uint32_t len = ty == 1 ? 4 + ((c >> 2) & 7) : (c >> 2) + 1;
+                const uint32_t off = ty == 1 ? ((c >> 5) << 8) | (v & 0xFF) : ty == 2 ? v & 0xFFFF : v;
+                p += 1 + nb;
+                if (off == 0 || off > pos) { st = RR_SNAPPY_E_OFFSET; break; }
+                if (len > expected - pos) { st = RR_SNAPPY_E_OVERFLOW; break; }
+                // out[pos + j] = out[pos - off + j % off]: every source byte is already written
+                uint32_t j = lane;
+                if (off < len) {
+                    const uint32_t q = (uint32_t)(((float)lane + 0.5f) * (1.0f / (float)off));
+                    j = lane - q * off;
+                }
+                if (inl) {
+                    const uint8_t x = lane < len ? win[pos - off + j] : 0;
+                    if (lane < len) win[pos + lane] = x;
+                } else {
+                    wait_stores();   // the wave's earlier output has reached the L2
+                    const uint8_t x = lane < len ? __builtin_amdgcn_raw_buffer_load_b8(Ro, (int)(pos - off + j), 0, 17) : 0;
+                    if (lane < len) __builtin_amdgcn_raw_buffer_store_b8(x, Ro, (int)(pos + lane), 0, 0);
+                }
+                pos += len;
+            }
+        }
+        if (st == RR_SNAPPY_OK && pos != expected) st = RR_SNAPPY_E_LENGTH;
+        if (inl && st == RR_SNAPPY_OK)
+            for (uint32_t k = lane; k < expected; k += WAVE) __builtin_amdgcn_raw_buffer_store_b8(win[k], Ro, (int)k, 0, 0);
+        if (lane == 0) status[b] = (uint8_t)st;
+    }
+}
+
+// ---- compression (snappy 1.1.8 CompressFragment; oracle/rr_snappy.c) ------------------------
+__device__ __forceinline__ uint32_t log2floor(uint32_t v) { return 31u - (uint32_t)__builtin_clz(v); }
+__device__ __forceinline__ uint32_t table_size(uint32_t fn) {   // CalculateTableSize, snappy.cc:442-455
+    return fn > TAB_MAX ? TAB_MAX : fn < TAB_MIN ? TAB_MIN : 2u << log2floor(fn - 1);
+}
+__device__ __forceinline__ uint32_t hash32(uint32_t v, uint32_t shift) { return (v * 0x1e35a7bdu) >> shift; }
+
+// The fragment's bytes: staged in LDS (ib, at ib[sh + k]) or, when it does not fit, read from
+// global memory through the block's buffer resource (at R[g + k]).
+struct Frag {
+    const uint8_t *ib;   // LDS stage (generic pointer to __shared__)
+    rsrc_t R;
+    uint32_t sh, g;
+    bool lds;
+    __device__ __forceinline__ uint32_t ld32(uint32_t k) const {   // 4 bytes at k, uniform
+        if (lds) {
+            const uint32_t q = sh + k, a = q & ~3u;
+            const uint32_t lo = *reinterpret_cast<const uint32_t *>(ib + a);
+            const uint32_t hi = *reinterpret_cast<const uint32_t *>(ib + a + 4);
+            return __builtin_amdgcn_alignbyte(hi, lo, q & 3);
+        }
+        const uint32_t q = g + k, a = q & ~3u;
+        const uint32_t lo = __builtin_amdgcn_raw_buffer_load_b32(R, (int)a, 0, 0);
+        const uint32_t hi = __builtin_amdgcn_raw_buffer_load_b32(R, (int)a + 4, 0, 0);
+        return __builtin_amdgcn_alignbyte(hi, lo, q & 3);
+    }
+    __device__ __forceinline__ uint32_t byte(uint32_t k) const {   // per lane
+        if (lds) return ib[sh + k];
+        return __builtin_amdgcn_raw_buffer_load_b8(R, (int)(g + k), 0, 0);
+    }
+};
+
+// Output slot writer: uniform op, lanes store bytes.
+struct Out {
+    rsrc_t R;
+    uint32_t op;
+    __device__ __forceinline__ void put(uint32_t nbytes, uint64_t v) {   // up to 8 bytes, lanes < nbytes
+        const uint32_t l = lane_id();
+        if (l < nbytes) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(v >> (8 * l)), R, (int)(op + l), 0, 0);
+        op += nbytes;
+    }
+    __device__ __forceinline__ void literal(const Frag &F, uint32_t from, uint32_t len) {   // EmitLiteral
+        const uint32_t n1 = len - 1;
+        if (n1 < 60) {
+            put(1, n1 << 2);
+        } else {
+            const uint32_t count = (log2floor(n1) >> 3) + 1;
+            put(1 + count, (uint64_t)((59 + count) << 2) | ((uint64_t)n1 << 8));
+        }
+        const uint32_t l = lane_id();
+        for (uint32_t i = 0; i < len; i += WAVE)
+            if (i + l < len) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)F.byte(from + i + l), R, (int)(op + i + l), 0, 0);
+        op += len;
+    }
+    __device__ __forceinline__ void copy64(uint32_t offset, uint32_t len, bool allow_short) {   // EmitCopyAtMost64
+        if (allow_short && len < 12 && offset < 2048)
+            put(2, (uint64_t)(1 + ((len - 4) << 2) + ((offset >> 3) & 0xe0)) | ((uint64_t)(offset & 0xFF) << 8));
+        else
+            put(3, (uint64_t)(2 + ((len - 1) << 2)) | ((uint64_t)(offset & 0xFFFF) << 8));
+    }
+    __device__ __forceinline__ void copy(uint32_t offset, uint32_t len) {   // EmitCopy
+        if (len < 12) { copy64(offset, len, true); return; }
+        while (len >= 68) { copy64(offset, 64, false); len -= 64; }
+        if (len > 64) { copy64(offset, 60, false); len -= 60; }
+        copy64(offset, len, true);
+    }
+};
+
+// FindMatchLength: bytes equal at a + i and b + i, for b + i < lim; 64 lanes a step
+__device__ __forceinline__ uint32_t match_len(const Frag &F, uint32_t a, uint32_t b, uint32_t lim) {
+    const uint32_t l = lane_id();
+    for (uint32_t m = 0;; m += WAVE) {
+        const uint32_t k = m + l;
+        const bool stop = b + k >= lim || F.byte(a + k) != F.byte(b + k);
+        const uint64_t bal = __ballot(stop);
+        if (bal) return m + (uint32_t)__builtin_ctzll(bal);
+    }
+}
+
+__device__ void compress_fragment(const Frag &F, uint32_t fn, uint16_t *table, uint32_t ts, Out &O) {
+    const uint32_t shift = 32 - log2floor(ts);
+    uint32_t ip = 0, next_emit = 0;
+    if (fn >= MARGIN) {
+        const uint32_t ip_limit = fn - MARGIN;
+        uint32_t next_hash = hash32(F.ld32(++ip), shift);
+        for (;;) {
+            uint32_t skip = 32, next_ip = ip, cand;
+            for (;;) {   // step 1: probe for a 4-byte match
+                ip = next_ip;
+                const uint32_t h = next_hash;
+                const uint32_t between = skip >> 5;
+                skip += between;
+                next_ip = ip + between;
+                if (next_ip > ip_limit) goto remainder;
+                next_hash = hash32(F.ld32(next_ip), shift);
+                cand = table[h];
+                table[h] = (uint16_t)ip;
+                if (F.ld32(ip) == F.ld32(cand)) break;
+            }
+            O.literal(F, next_emit, ip - next_emit);   // step 2
+            uint32_t cur, cbytes;
+            do {   // step 3: copies while the next position matches again
+                const uint32_t b0 = ip;
+                const uint32_t matched = 4 + match_len(F, cand + 4, ip + 4, fn);
+                ip += matched;
+                O.copy(b0 - cand, matched);
+                next_emit = ip;
+                if (ip >= ip_limit) goto remainder;
+                const uint32_t prev = F.ld32(ip - 1);
+                table[hash32(prev, shift)] = (uint16_t)(ip - 1);
+                cur = F.ld32(ip);
+                const uint32_t ch = hash32(cur, shift);
+                cand = table[ch];
+                cbytes = F.ld32(cand);
+                table[ch] = (uint16_t)ip;
+            } while (cur == cbytes);
+            next_hash = hash32(F.ld32(ip + 1), shift);
+            ++ip;
+        }
+    }
+remainder:
+    if (next_emit < fn) O.literal(F, next_emit, fn - next_emit);
+}
+
+__global__ __launch_bounds__(WAVE) void snz_comp_kernel(const uint8_t *__restrict__ in, uint64_t in_cap,
+                                                        const uint64_t *__restrict__ in_offs, uint64_t n,
+                                                        uint8_t *__restrict__ slots,
+                                                        const uint64_t *__restrict__ slot_offs,
+                                                        uint64_t *__restrict__ sizes, uint32_t fcap) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
+    uint16_t *table = reinterpret_cast<uint16_t *>(sm);
+    uint8_t *ib = sm + 2 * TAB_MAX;
+    const uint32_t lane = lane_id();
+    for (uint64_t b = blockIdx.x; b < n; b += gridDim.x) {
+        const uint64_t c0 = in_offs[b], len = in_offs[b + 1] - c0;
+        const uint32_t s0 = (uint32_t)(c0 & 3);
+        Frag F;
+        F.R = mkr(in + (c0 - s0), in_cap - (c0 - s0));
+        F.ib = ib;
+        Out O;
+        O.R = mkr(slots + slot_offs[b], slot_offs[b + 1] - slot_offs[b]);
+        O.op = 0;
+        {   // varint32 length
+            uint32_t v = (uint32_t)len, nb = 1;
+            uint64_t enc = 0;
+            for (uint32_t k = 0; k < 5; ++k) {
+                const uint32_t more = v >= 128;
+                enc |= (uint64_t)((v & 0x7F) | (more << 7)) << (8 * k);
+                if (!more) { nb = k + 1; break; }
+                v >>= 7;
+            }
+            O.put(nb, enc);
+        }
+        for (uint64_t f = 0; f < len; f += FRAG) {
+            const uint32_t fn = (uint32_t)(len - f < FRAG ? len - f : FRAG);
+            const uint32_t ts = table_size(fn);
+            for (uint32_t k = lane; k < ts / 2; k += WAVE) reinterpret_cast<uint32_t *>(table)[k] = 0;
+            F.g = s0 + (uint32_t)f;
+            F.sh = F.g & 3;
+            F.lds = fn + 8 <= fcap;
+            if (F.lds) {   // aligned dwords covering the fragment (+ pad), source alignment kept
+                const uint32_t a0 = F.g & ~3u, nd = (F.sh + fn + 8 + 3) / 4;
+                for (uint32_t k = lane; k < nd; k += WAVE)
+                    reinterpret_cast<uint32_t *>(ib)[k] = __builtin_amdgcn_raw_buffer_load_b32(F.R, (int)(a0 + 4 * k), 0, 0);
+            }
+            compress_fragment(F, fn, table, ts, O);
+        }
+        if (lane == 0) sizes[b] = O.op;
+    }
+}
+
+__global__ __launch_bounds__(WAVE) void snz_pack_kernel(const uint8_t *__restrict__ slots,
+                                                        const uint64_t *__restrict__ slot_offs, uint64_t n,
+                                                        uint8_t *__restrict__ out,
+                                                        const uint64_t *__restrict__ out_offs) {
+    const uint32_t lane = lane_id();
+    for (uint64_t b = blockIdx.x; b < n; b += gridDim.x) {
+        const uint8_t *s = slots + slot_offs[b];
+        uint8_t *d = out + out_offs[b];
+        const uint64_t len = out_offs[b + 1] - out_offs[b];
+        for (uint64_t k = lane; k < len; k += WAVE) d[k] = s[k];
+    }
+}
+
+__global__ __launch_bounds__(256) void snz_bound_kernel(const uint64_t *__restrict__ in_offs, uint64_t n,
+                                                        uint64_t *__restrict__ slot_offs, uint64_t *__restrict__ lb,
+                                                        uint32_t lbw) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < lbw) lb[i] = 0;
+    if (i < n) {
+        const uint64_t len = in_offs[i + 1] - in_offs[i];
+        slot_offs[i] = 32 + len + len / 6;   // MaxCompressedLength
+    } else if (i == n) {
+        slot_offs[n] = 0;
+    }
+}
+
+__global__ __launch_bounds__(256) void snz_sizes_kernel(uint64_t *__restrict__ sizes, uint64_t n,
+                                                        uint64_t *__restrict__ lb, uint32_t lbw) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < lbw) lb[i] = 0;
+    if (i == n) sizes[n] = 0;
+}
+
+uint32_t grid_for(uint64_t n, uint32_t cap) { return (uint32_t)(n < cap ? (n ? n : 1) : cap); }
+
+}  // namespace
+
+constexpr uint32_t SNZ_DEC_WIN = 32768;   // LDS output window per wave (RocksDB blocks: 16 KiB)
+constexpr uint32_t SNZ_FRAG_LDS = 16384 + 64;   // staged fragment bytes per wave
+
+extern "C" uint64_t rr_snappy_scratch_words(uint64_t n, uint64_t slot_bytes) {
+    return rr_scan_words(n) + 1 + (n + 1) + (slot_bytes + 7) / 8 + 2;
+}
+
+// decompression: 3 launches (length preambles, scan, blocks)
+extern "C" hipError_t rr_launch_snappy_decompress(const uint8_t *in, uint64_t in_cap, const uint64_t *in_offs, uint64_t n, uint8_t *out,
+                                                  uint64_t out_cap, uint64_t *out_offs, uint8_t *status,
+                                                  uint64_t *scratch, hipStream_t stream) {
+    const uint64_t lbw = rr_scan_words(n);
+    uint64_t *lb = scratch, *err = scratch + lbw;
+    const uint64_t m = (n + 1 > lbw ? n + 1 : lbw);
+    hipLaunchKernelGGL(snz_len_kernel, dim3((uint32_t)((m + 255) / 256)), dim3(256), 0, stream, in, in_offs, n, out_offs,
+                       status, lb, (uint32_t)lbw);
+    hipError_t e = rr_launch_scan_u64(out_offs, n, lb, err, stream);
+    if (e != hipSuccess || n == 0) return e != hipSuccess ? e : hipGetLastError();
+    hipLaunchKernelGGL(snz_dec_kernel, dim3(grid_for(n, 1u << 20)), dim3(WAVE), SNZ_DEC_WIN, stream, in, in_cap, in_offs, n, out,
+                       out_cap, (const uint64_t *)out_offs, status, SNZ_DEC_WIN);
+    return hipGetLastError();
+}
+
+// compression: bounds + scan -> per-block slots in scratch, blocks, sizes + scan, pack
+extern "C" hipError_t rr_launch_snappy_compress(const uint8_t *in, uint64_t in_cap, const uint64_t *in_offs, uint64_t n, uint8_t *out,
+                                                uint64_t *out_offs, uint64_t *scratch, uint64_t slot_bytes,
+                                                hipStream_t stream) {
+    const uint64_t lbw = rr_scan_words(n);
+    uint64_t *lb = scratch, *err = scratch + lbw, *slot_offs = err + 1;
+    uint8_t *slots = reinterpret_cast<uint8_t *>(slot_offs + n + 1);
+    (void)slot_bytes;
+    const uint64_t m = (n + 1 > lbw ? n + 1 : lbw);
+    const dim3 g((uint32_t)((m + 255) / 256));
+    hipLaunchKernelGGL(snz_bound_kernel, g, dim3(256), 0, stream, in_offs, n, slot_offs, lb, (uint32_t)lbw);
+    hipError_t e = rr_launch_scan_u64(slot_offs, n, lb, err, stream);
+    if (e != hipSuccess) return e;
+    if (n) {
+        const uint32_t smem = 2 * TAB_MAX + SNZ_FRAG_LDS;
+        hipLaunchKernelGGL(snz_comp_kernel, dim3(grid_for(n, 1u << 20)), dim3(WAVE), smem, stream, in, in_cap, in_offs, n, slots,
+                           (const uint64_t *)slot_offs, out_offs, SNZ_FRAG_LDS);
+    }
+    hipLaunchKernelGGL(snz_sizes_kernel, g, dim3(256), 0, stream, out_offs, n, lb, (uint32_t)lbw);
+    e = rr_launch_scan_u64(out_offs, n, lb, err, stream);
+    if (e != hipSuccess || n == 0) return e != hipSuccess ? e : hipGetLastError();
+    hipLaunchKernelGGL(snz_pack_kernel, dim3(grid_for(n, 1u << 20)), dim3(WAVE), 0, stream, slots,
+                       (const uint64_t *)slot_offs, n, out, (const uint64_t *)out_offs);
+    return hipGetLastError();
+}

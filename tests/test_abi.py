@@ -25,6 +25,17 @@ def test_library_exports_every_declared_symbol():
     assert sorted(rr.EXPORTS) == syms
 
 
+def test_library_exports_every_snappy_symbol():
+    """include/rr_snappy.h (row f3): every declared function is exported and bound."""
+    lib = rr.lib()
+    syms = declared_symbols("rr_snappy.h")
+    assert len(syms) == 6
+    for s in syms:
+        assert hasattr(lib, s), f"{s} declared in include/rr_snappy.h but not exported"
+    assert sorted(rr.SNAPPY_EXPORTS) == syms
+    assert lib.rr_snappy_max_compressed_length(16384) == 32 + 16384 + 16384 // 6
+
+
 def test_compat_header_symbols_defined(tmp_path):
     """Every function include/rock_serdes_compat.h declares (the legacy desString / serObject /
     desObject of rock_serdes.h:47-49 and the rr_compat_* batch forms) is defined by the shim,
@@ -45,7 +56,7 @@ def test_compat_header_symbols_defined(tmp_path):
 
 def test_headers_compile_as_plain_c(tmp_path):
     src = tmp_path / "t.c"
-    src.write_text('#include "rr_serdes.h"\n#include "rock_serdes_compat.h"\n'
+    src.write_text('#include "rr_serdes.h"\n#include "rr_snappy.h"\n#include "rock_serdes_compat.h"\n'
                    'int main(void){ return (int)sizeof(rr_value) + (int)sizeof(rr_elem) - 32; }\n')
     subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), str(src),
                     "-o", str(tmp_path / "t")], check=True)
