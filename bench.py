@@ -43,6 +43,7 @@ def parse():
     p.add_argument("--no-check", action="store_true")
     p.add_argument("--no-host", action="store_true", help="skip the PCIe-inclusive host leg and the copy reference")
     p.add_argument("--no-split", action="store_true", help="skip the RCCL root split/gather leg")
+    p.add_argument("--no-snappy", action="store_true", help="skip the snappy block-compression leg (row f3)")
     p.add_argument("--profile-only", action="store_true", help="decode steps only (for rocprofv3)")
     p.add_argument("--profile-encode", action="store_true", help="one decode, then encode steps only (for rocprofv3)")
     return p.parse_args()
@@ -245,6 +246,13 @@ def main():
             result["split_gather"] = {"error": repr(ex)[:300]}
         dog.cancel()
 
+    if not args.no_snappy:
+        try:
+            result["snappy"] = snappy_leg(rr, torch, eng, stream, d_data, nb, timed, args,
+                                          cpu_too=(rank == 0 and world == 1 and not args.no_cpu))
+        except Exception as ex:   # reported, never fatal to the headline
+            result["snappy"] = {"error": repr(ex)[:300]}
+
     if rank == 0 and world == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(data, offs, nb, args.cpu_seconds)
 
@@ -325,6 +333,48 @@ def split_gather_leg(rr, torch, dist, eng, world, rank, dev, stream, d_data, d_o
         return out
     finally:
         comm.close()
+
+
+SNAPPY_BLOCK = 16384   # RocksDB data block size the reference configures (rocksdbapi.cc:77,142)
+
+
+def snappy_leg(rr, torch, eng, stream, d_data, nb, timed, args, cpu_too):
+    """Row f3: the same blob bytes cut into 16 KiB RocksDB data blocks, compressed and
+    decompressed on the GPU in snappy's raw format (include/rr_snappy.h), device-resident,
+    HIP events over the timed steps; round trip checked; the CPU oracle (snappy 1.1.8
+    restatement) on a bounded sample beside it."""
+    cuts = np.append(np.arange(0, nb, SNAPPY_BLOCK, dtype=np.uint64), np.uint64(nb))
+    n = len(cuts) - 1
+    d_offs = torch.from_numpy(cuts.view(np.int64)).to(d_data.device)
+    cap = int(rr.lib().rr_snappy_compress_bound(n, d_data.numel()))
+    d_comp = torch.empty(cap, dtype=torch.uint8, device=d_data.device)
+    d_coffs = torch.empty(n + 1, dtype=torch.int64, device=d_data.device)
+    d_back = torch.empty(d_data.numel(), dtype=torch.uint8, device=d_data.device)
+    d_boffs = torch.empty(n + 1, dtype=torch.int64, device=d_data.device)
+    d_st = torch.empty(n, dtype=torch.uint8, device=d_data.device)
+    steps, warm = max(1, args.steps // 4), 1
+    _, ev_c = timed(lambda: eng.snappy_compress_device(d_data, d_offs, d_comp, d_coffs, stream=stream), steps, warm)
+    zb = int(d_coffs[-1].item())
+    d_z = d_comp[:((zb + 15) & ~15) or 16]
+    _, ev_d = timed(lambda: eng.snappy_decompress_device(d_z, d_coffs, d_back, d_boffs, d_st, stream=stream), steps, warm)
+    ok = int(d_st.max().item()) == 0 and bool(torch.equal(d_back[:nb], d_data[:nb]))
+    out = {"what": f"{n} blocks of {SNAPPY_BLOCK} B (the decode batch's blobs), snappy raw format, device-resident",
+           "compressed_bytes": zb, "ratio": round(zb / nb, 4), "roundtrip_bit_exact": ok,
+           "compress": {"ms": round(ev_c, 3), "GBs_input": round(nb / ev_c / 1e6, 1)},
+           "decompress": {"ms": round(ev_d, 3), "GBs_output": round(nb / ev_d / 1e6, 1),
+                          "hbm_alg_GBs": round((nb + zb) / ev_d / 1e6, 1)}}
+    if cpu_too:
+        from oracle import cpu
+        data = d_data[:nb].cpu().numpy()
+        sub = cuts[: min(n, 2048) + 1]
+        sb = int(sub[-1])
+        for thr in (1, 16):
+            _, _, t1 = cpu.snappy_compress_blocks(data, sub, nthreads=thr)
+            z, zo, _ = cpu.snappy_compress_blocks(data, sub, nthreads=thr)
+            _, _, t2 = cpu.snappy_uncompress_blocks(z, zo, sub, nthreads=thr)
+            out[f"cpu_{thr}t"] = {"compress_GBs": round(sb / t1 / 1e9, 2), "decompress_GBs": round(sb / t2 / 1e9, 2)}
+        out["cpu_sample"] = f"first {len(sub) - 1} blocks ({sb} B), oracle/rr_snappy.c (snappy 1.1.8 restatement)"
+    return out
 
 
 def measured_traffic(config, n, nb):

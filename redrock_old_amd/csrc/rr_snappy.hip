@@ -33,6 +33,11 @@ constexpr uint32_t TAB_MAX = 1u << 14;     // kMaxHashTableSize
 constexpr uint32_t MARGIN = 15;            // kInputMarginBytes
 
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
+// LDS pointers kept in address space 3, so accesses compile to ds_* (a generic pointer gives flat_*
+// instructions, whose waits also drain every outstanding global store of the wave)
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+typedef __attribute__((address_space(3))) uint16_t lds_u16;
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
 __device__ __forceinline__ rsrc_t mkr(const void *base, uint64_t bytes) {
     return __builtin_amdgcn_make_buffer_rsrc((void *)base, 0, (int)(bytes < 0x7FFFFFF0ull ? bytes : 0x7FFFFFF0ull),
                                              0x00020000);
@@ -190,15 +195,15 @@ __device__ __forceinline__ uint32_t hash32(uint32_t v, uint32_t shift) { return 
 // The fragment's bytes: staged in LDS (ib, at ib[sh + k]) or, when it does not fit, read from
 // global memory through the block's buffer resource (at R[g + k]).
 struct Frag {
-    const uint8_t *ib;   // LDS stage (generic pointer to __shared__)
+    const lds_u8 *ib;    // LDS stage
     rsrc_t R;
     uint32_t sh, g;
     bool lds;
     __device__ __forceinline__ uint32_t ld32(uint32_t k) const {   // 4 bytes at k, uniform
         if (lds) {
             const uint32_t q = sh + k, a = q & ~3u;
-            const uint32_t lo = *reinterpret_cast<const uint32_t *>(ib + a);
-            const uint32_t hi = *reinterpret_cast<const uint32_t *>(ib + a + 4);
+            const uint32_t lo = *reinterpret_cast<const lds_u32 *>(ib + a);
+            const uint32_t hi = *reinterpret_cast<const lds_u32 *>(ib + a + 4);
             return __builtin_amdgcn_alignbyte(hi, lo, q & 3);
         }
         const uint32_t q = g + k, a = q & ~3u;
@@ -259,7 +264,7 @@ __device__ __forceinline__ uint32_t match_len(const Frag &F, uint32_t a, uint32_
     }
 }
 
-__device__ void compress_fragment(const Frag &F, uint32_t fn, uint16_t *table, uint32_t ts, Out &O) {
+__device__ void compress_fragment(const Frag &F, uint32_t fn, lds_u16 *table, uint32_t ts, Out &O) {
     const uint32_t shift = 32 - log2floor(ts);
     uint32_t ip = 0, next_emit = 0;
     if (fn >= MARGIN) {
@@ -310,8 +315,8 @@ __global__ __launch_bounds__(WAVE) void snz_comp_kernel(const uint8_t *__restric
                                                         const uint64_t *__restrict__ slot_offs,
                                                         uint64_t *__restrict__ sizes, uint32_t fcap) {
     extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
-    uint16_t *table = reinterpret_cast<uint16_t *>(sm);
-    uint8_t *ib = sm + 2 * TAB_MAX;
+    lds_u16 *table = (lds_u16 *)sm;
+    lds_u8 *ib = (lds_u8 *)sm + 2 * TAB_MAX;
     const uint32_t lane = lane_id();
     for (uint64_t b = blockIdx.x; b < n; b += gridDim.x) {
         const uint64_t c0 = in_offs[b], len = in_offs[b + 1] - c0;
@@ -336,14 +341,14 @@ __global__ __launch_bounds__(WAVE) void snz_comp_kernel(const uint8_t *__restric
         for (uint64_t f = 0; f < len; f += FRAG) {
             const uint32_t fn = (uint32_t)(len - f < FRAG ? len - f : FRAG);
             const uint32_t ts = table_size(fn);
-            for (uint32_t k = lane; k < ts / 2; k += WAVE) reinterpret_cast<uint32_t *>(table)[k] = 0;
+            for (uint32_t k = lane; k < ts / 2; k += WAVE) ((lds_u32 *)table)[k] = 0;
             F.g = s0 + (uint32_t)f;
             F.sh = F.g & 3;
             F.lds = fn + 8 <= fcap;
             if (F.lds) {   // aligned dwords covering the fragment (+ pad), source alignment kept
                 const uint32_t a0 = F.g & ~3u, nd = (F.sh + fn + 8 + 3) / 4;
                 for (uint32_t k = lane; k < nd; k += WAVE)
-                    reinterpret_cast<uint32_t *>(ib)[k] = __builtin_amdgcn_raw_buffer_load_b32(F.R, (int)(a0 + 4 * k), 0, 0);
+                    ((lds_u32 *)ib)[k] = __builtin_amdgcn_raw_buffer_load_b32(F.R, (int)(a0 + 4 * k), 0, 0);
             }
             compress_fragment(F, fn, table, ts, O);
         }
