@@ -31,6 +31,8 @@ constexpr uint32_t FRAG = 1u << 16;        // snappy kBlockSize (snappy.h:197-19
 constexpr uint32_t TAB_MIN = 1u << 8;      // kMinHashTableSize
 constexpr uint32_t TAB_MAX = 1u << 14;     // kMaxHashTableSize
 constexpr uint32_t MARGIN = 15;            // kInputMarginBytes
+constexpr uint32_t SNZ_DEC_WIN = 32768;     // LDS output window per wave (RocksDB blocks: 16 KiB)
+constexpr uint32_t SNZ_FRAG_LDS = 16384 + 64;   // staged fragment bytes per wave
 
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 // LDS pointers kept in address space 3, so accesses compile to ds_* (a generic pointer gives flat_*
@@ -264,14 +266,71 @@ __device__ __forceinline__ uint32_t match_len(const Frag &F, uint32_t a, uint32_
     }
 }
 
-__device__ void compress_fragment(const Frag &F, uint32_t fn, lds_u16 *table, uint32_t ts, Out &O) {
+#ifndef RR_SNZ_K   // most probes a compressor step-1 round evaluates at once (1: the serial loop)
+#define RR_SNZ_K 16
+#endif
+#ifndef RR_SNZ_K0  // the first round's width after a match
+#define RR_SNZ_K0 16
+#endif
+__device__ void compress_fragment(const Frag &F, uint32_t fn, lds_u16 *table, uint32_t ts, lds_u32 *mark, Out &O) {
     const uint32_t shift = 32 - log2floor(ts);
     uint32_t ip = 0, next_emit = 0;
     if (fn >= MARGIN) {
         const uint32_t ip_limit = fn - MARGIN;
         uint32_t next_hash = hash32(F.ld32(++ip), shift);
         for (;;) {
-            uint32_t skip = 32, next_ip = ip, cand;
+            uint32_t cand;
+#if RR_SNZ_K > 1
+            // step 1, RR_SNZ_K probes at once: lane j takes the j-th probe the scan would make
+            // from here if none before it matched (the skip schedule is known in advance); its
+            // candidate is the last earlier lane's position with the same hash, else the table.
+            // The first lane that matches (or whose next position passes ip_limit) is where the
+            // serial loop stops; the table gets exactly the updates the serial loop makes up to
+            // there, the last lane of each hash writing.
+            (void)next_hash;
+            {
+                const uint32_t lane = lane_id();
+                uint32_t P0 = ip, S0 = 32, K = RR_SNZ_K0;   // a round's width doubles while nothing matches
+                for (;;) {
+                    uint32_t P = P0, S = S0;
+                    for (uint32_t t = 0; t + 1 < K; ++t) {
+                        const uint32_t B = S >> 5;
+                        P = t < lane ? P + B : P;
+                        S = t < lane ? S + B : S;
+                    }
+                    const uint32_t B = S >> 5, Pn = P + B;
+                    const bool act = lane < K;
+                    const bool valid = act & (Pn <= ip_limit);
+                    const uint32_t x = F.ld32(act ? P : 0);
+                    const uint32_t H = hash32(x, shift);
+                    int prev = -1;
+                    for (uint32_t r = 1; r < K; ++r) {
+                        const uint32_t hk = (uint32_t)__shfl((int)H, (int)((lane - r) & (WAVE - 1)), WAVE);
+                        prev = (prev < 0 && lane >= r && hk == H) ? (int)(lane - r) : prev;
+                    }
+                    const uint32_t Pp = (uint32_t)__shfl((int)P, prev < 0 ? (int)lane : prev, WAVE);
+                    const uint32_t c = prev >= 0 ? Pp : (uint32_t)table[act ? H : 0];
+                    const bool m = valid && x == F.ld32(c);
+                    const uint64_t stop = __ballot(act && (!valid || m));
+                    const uint32_t sl = stop ? (uint32_t)__builtin_ctzll(stop) : K;
+                    const bool hit = sl < K && ((__ballot(m) >> sl) & 1);
+                    const bool commit = act && (lane < sl || (hit && lane == sl));
+                    mark[lane] = 0;
+                    if (commit && prev >= 0) mark[prev] = 1;
+                    if (commit && !mark[lane]) table[H] = (uint16_t)P;
+                    if (sl < K) {
+                        if (!hit) goto remainder;
+                        ip = rdl(P, sl);
+                        cand = rdl(c, sl);
+                        break;
+                    }
+                    P0 = rdl(Pn, K - 1);
+                    S0 = rdl(S + B, K - 1);
+                    K = K < RR_SNZ_K ? 2 * K : K;
+                }
+            }
+#else
+            uint32_t skip = 32, next_ip = ip;
             for (;;) {   // step 1: probe for a 4-byte match
                 ip = next_ip;
                 const uint32_t h = next_hash;
@@ -284,6 +343,7 @@ __device__ void compress_fragment(const Frag &F, uint32_t fn, lds_u16 *table, ui
                 table[h] = (uint16_t)ip;
                 if (F.ld32(ip) == F.ld32(cand)) break;
             }
+#endif
             O.literal(F, next_emit, ip - next_emit);   // step 2
             uint32_t cur, cbytes;
             do {   // step 3: copies while the next position matches again
@@ -317,6 +377,7 @@ __global__ __launch_bounds__(WAVE) void snz_comp_kernel(const uint8_t *__restric
     extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
     lds_u16 *table = (lds_u16 *)sm;
     lds_u8 *ib = (lds_u8 *)sm + 2 * TAB_MAX;
+    lds_u32 *mark = (lds_u32 *)(sm + 2 * TAB_MAX + SNZ_FRAG_LDS);   // WAVE words
     const uint32_t lane = lane_id();
     for (uint64_t b = blockIdx.x; b < n; b += gridDim.x) {
         const uint64_t c0 = in_offs[b], len = in_offs[b + 1] - c0;
@@ -350,7 +411,7 @@ __global__ __launch_bounds__(WAVE) void snz_comp_kernel(const uint8_t *__restric
                 for (uint32_t k = lane; k < nd; k += WAVE)
                     ((lds_u32 *)ib)[k] = __builtin_amdgcn_raw_buffer_load_b32(F.R, (int)(a0 + 4 * k), 0, 0);
             }
-            compress_fragment(F, fn, table, ts, O);
+            compress_fragment(F, fn, table, ts, mark, O);
         }
         if (lane == 0) sizes[b] = O.op;
     }
@@ -393,8 +454,6 @@ uint32_t grid_for(uint64_t n, uint32_t cap) { return (uint32_t)(n < cap ? (n ? n
 
 }  // namespace
 
-constexpr uint32_t SNZ_DEC_WIN = 32768;   // LDS output window per wave (RocksDB blocks: 16 KiB)
-constexpr uint32_t SNZ_FRAG_LDS = 16384 + 64;   // staged fragment bytes per wave
 
 extern "C" uint64_t rr_snappy_scratch_words(uint64_t n, uint64_t slot_bytes) {
     return rr_scan_words(n) + 1 + (n + 1) + (slot_bytes + 7) / 8 + 2;
@@ -430,7 +489,7 @@ extern "C" hipError_t rr_launch_snappy_compress(const uint8_t *in, uint64_t in_c
     hipError_t e = rr_launch_scan_u64(slot_offs, n, lb, err, stream);
     if (e != hipSuccess) return e;
     if (n) {
-        const uint32_t smem = 2 * TAB_MAX + SNZ_FRAG_LDS;
+        const uint32_t smem = 2 * TAB_MAX + SNZ_FRAG_LDS + 4 * WAVE;
         hipLaunchKernelGGL(snz_comp_kernel, dim3(grid_for(n, 1u << 20)), dim3(WAVE), smem, stream, in, in_cap, in_offs, n, slots,
                            (const uint64_t *)slot_offs, out_offs, SNZ_FRAG_LDS);
     }
