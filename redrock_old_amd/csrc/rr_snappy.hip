@@ -106,6 +106,7 @@ __global__ __launch_bounds__(WAVE) void snz_dec_kernel(const uint8_t *__restrict
                                                        const uint64_t *__restrict__ out_offs,
                                                        uint8_t *__restrict__ status, uint32_t wcap) {
     extern __shared__ __attribute__((aligned(16))) uint8_t win[];
+    lds_u32 *win32 = (lds_u32 *)win;
     const uint32_t lane = lane_id();
     for (uint64_t b = blockIdx.x; b < n; b += gridDim.x) {
         if (status[b] != RR_SNAPPY_OK) continue;   // (the preamble did not parse)
@@ -144,12 +145,38 @@ __global__ __launch_bounds__(WAVE) void snz_dec_kernel(const uint8_t *__restrict
                 p += hdr;
                 if (len > end - p) { st = RR_SNAPPY_E_TRUNC; break; }
                 if (len > expected - pos) { st = RR_SNAPPY_E_OVERFLOW; break; }
-                for (uint32_t i = 0; i < len; i += WAVE) {
-                    const uint32_t k = i + lane;
-                    if (k < len) {
-                        const uint8_t v = __builtin_amdgcn_raw_buffer_load_b8(W.R, (int)(p + k), 0, 0);
-                        if (inl) win[pos + k] = v;
-                        else __builtin_amdgcn_raw_buffer_store_b8(v, Ro, (int)(pos + k), 0, 0);
+                if (inl && len <= WAVE && p + len <= W.wb + 1024) {
+                    // a short literal inside the register window: lane k gathers byte p + k from
+                    // the lane holding it (ds_bpermute, no memory access)
+                    const uint32_t r = p + lane - W.wb, src = (r >> 4) & (WAVE - 1), k4 = (r >> 2) & 3;
+                    const uint32_t y0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src * 4), (int)W.x[0]);
+                    const uint32_t y1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src * 4), (int)W.x[1]);
+                    const uint32_t y2 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src * 4), (int)W.x[2]);
+                    const uint32_t y3 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src * 4), (int)W.x[3]);
+                    const uint32_t y = k4 == 0 ? y0 : k4 == 1 ? y1 : k4 == 2 ? y2 : y3;
+                    if (lane < len) win[pos + lane] = (uint8_t)(y >> (8 * (r & 3)));
+                } else if (inl) {
+                    // bytes up to a 4-aligned output position, then whole dwords (a lane's dword
+                    // from two aligned source dwords; the last may spill up to 3 bytes past the
+                    // literal, which the next element overwrites before anything reads them)
+                    const uint32_t h = min((4u - (pos & 3)) & 3, len);
+                    if (lane < h) win[pos + lane] = __builtin_amdgcn_raw_buffer_load_b8(W.R, (int)(p + lane), 0, 0);
+                    const uint32_t d0 = pos + h, q0 = p + h, body = len - h;
+                    for (uint32_t i = 0; i < body; i += 4 * WAVE) {
+                        const uint32_t k = i + 4 * lane;
+                        if (k < body) {
+                            const uint32_t q = q0 + k, a = q & ~3u;
+                            const uint32_t lo = __builtin_amdgcn_raw_buffer_load_b32(W.R, (int)a, 0, 0);
+                            const uint32_t hi = __builtin_amdgcn_raw_buffer_load_b32(W.R, (int)a + 4, 0, 0);
+                            win32[(d0 + k) >> 2] = __builtin_amdgcn_alignbyte(hi, lo, q & 3);
+                        }
+                    }
+                } else {
+                    for (uint32_t i = 0; i < len; i += WAVE) {
+                        const uint32_t k = i + lane;
+                        if (k < len)
+                            __builtin_amdgcn_raw_buffer_store_b8(__builtin_amdgcn_raw_buffer_load_b8(W.R, (int)(p + k), 0, 0),
+                                                                 Ro, (int)(pos + k), 0, 0);
                     }
                 }
                 pos += len;
@@ -181,8 +208,16 @@ __global__ __launch_bounds__(WAVE) void snz_dec_kernel(const uint8_t *__restrict
             }
         }
         if (st == RR_SNAPPY_OK && pos != expected) st = RR_SNAPPY_E_LENGTH;
-        if (inl && st == RR_SNAPPY_OK)
-            for (uint32_t k = lane; k < expected; k += WAVE) __builtin_amdgcn_raw_buffer_store_b8(win[k], Ro, (int)k, 0, 0);
+        if (inl && st == RR_SNAPPY_OK) {   // LDS -> output: bytes to a 4-aligned address, dwords, bytes
+            const uint32_t g0 = (uint32_t)((uintptr_t)gout & 3), hh = min((4u - g0) & 3, expected);
+            const uint32_t t0 = hh + ((expected - hh) & ~3u);
+            if (lane < hh) __builtin_amdgcn_raw_buffer_store_b8(win[lane], Ro, (int)lane, 0, 0);
+            for (uint32_t j = hh + 4 * lane; j < t0; j += 4 * WAVE) {
+                const uint32_t a = j >> 2;
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_amdgcn_alignbyte(win32[a + 1], win32[a], j & 3), Ro, (int)j, 0, 0);
+            }
+            if (t0 + lane < expected) __builtin_amdgcn_raw_buffer_store_b8(win[t0 + lane], Ro, (int)(t0 + lane), 0, 0);
+        }
         if (lane == 0) status[b] = (uint8_t)st;
     }
 }
@@ -470,7 +505,7 @@ extern "C" hipError_t rr_launch_snappy_decompress(const uint8_t *in, uint64_t in
                        status, lb, (uint32_t)lbw);
     hipError_t e = rr_launch_scan_u64(out_offs, n, lb, err, stream);
     if (e != hipSuccess || n == 0) return e != hipSuccess ? e : hipGetLastError();
-    hipLaunchKernelGGL(snz_dec_kernel, dim3(grid_for(n, 1u << 20)), dim3(WAVE), SNZ_DEC_WIN, stream, in, in_cap, in_offs, n, out,
+    hipLaunchKernelGGL(snz_dec_kernel, dim3(grid_for(n, 1u << 20)), dim3(WAVE), SNZ_DEC_WIN + 16, stream, in, in_cap, in_offs, n, out,
                        out_cap, (const uint64_t *)out_offs, status, SNZ_DEC_WIN);
     return hipGetLastError();
 }
