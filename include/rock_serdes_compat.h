@@ -24,6 +24,7 @@
 #define ROCK_SERDES_COMPAT_H
 
 #include "rr_serdes.h"
+#include "rr_rdb.h"
 
 #ifdef RR_REDIS_TREE
 /* rock_serdes.h:47 declares 2 args; the definition (rock_serdes.c:133) takes the lru too, and
@@ -36,6 +37,13 @@ robj *desObject(void *buf, size_t len); /* rock_serdes.h:49, rock_serdes.c:538 *
  * (out[i] == serObject(objs[i])), one engine call each. */
 void rr_compat_des_batch(void *const *bufs, const size_t *lens, size_t n, robj **out);
 void rr_compat_ser_batch(robj *const *objs, size_t n, sds *out);
+
+/* Row f4 (rr_rdb.h): the fork child's batch restore.  k keys of database dbid, held in the
+ * parent's RocksDB snapshot, requested over the child's pipes (rock_rdb.c:240-267) in one FLAT
+ * request: the parent's service (rr_rdb_serve) decodes them on its GPU and the robj are built
+ * here from the records — out[i] == loadValFromRockForRdb(dbid, keys[i]) (rock.c:527-550).
+ * The child never touches the GPU. */
+void rr_compat_rdb_load_batch(int fd_req, int fd_resp, int dbid, sds *keys, size_t k, robj **out);
 
 /* GPU the calling thread's engine context is created on (default 0; set before first use). */
 void rr_compat_set_device(int device);

@@ -75,6 +75,8 @@ COMM_ID_BYTES = 128
 # include/rr_snappy.h (GPU block compression)
 SNAPPY_EXPORTS = ["rr_snappy_max_compressed_length", "rr_snappy_compress_bound", "rr_snappy_compress_batch",
                   "rr_snappy_decompress_batch", "rr_snappy_compress_batch_host", "rr_snappy_decompress_batch_host"]
+# include/rr_rdb.h (batched snapshot restore over the fork-child pipes, row f4; used from C)
+RDB_EXPORTS = ["rr_rdb_request_batch", "rr_rdb_blobs_free", "rr_rdb_request_flat", "rr_rdb_flat_free", "rr_rdb_serve"]
 SNAPPY_STATUS = {0: "OK", 1: "HEADER", 2: "TRUNC", 3: "OFFSET", 4: "OVERFLOW", 5: "LENGTH", 6: "CAPACITY"}
 
 _lib = None

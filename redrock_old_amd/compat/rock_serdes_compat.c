@@ -164,6 +164,24 @@ void rr_compat_des_batch(void *const *bufs, const size_t *lens, size_t n, robj *
     zfree(offs); zfree(data); zfree(vals); zfree(els); zfree(arena);
 }
 
+void rr_compat_rdb_load_batch(int fd_req, int fd_resp, int dbid, sds *keys, size_t k, robj **out) {
+    if (k == 0) return;
+    int *dbis = zmalloc(sizeof(int) * k);
+    size_t *lens = zmalloc(sizeof(size_t) * k);
+    for (size_t i = 0; i < k; i++) { dbis[i] = dbid; lens[i] = sdslen(keys[i]); }
+    rr_rdb_flat f;
+    if (rr_rdb_request_flat(fd_req, fd_resp, dbis, (const char *const *)keys, lens, k, &f) != RR_API_OK || f.n != k)
+        serverPanic("rock rdb batch restore: %s", rr_last_error());
+    for (size_t i = 0; i < k; i++) {
+        if (f.values[i].status != RR_OK)   /* desObject's assert sites, as in rr_compat_des_batch */
+            serverPanic("desObject: bad blob (%s, status %u)", status_name(f.values[i].status), f.values[i].status);
+        out[i] = robj_from_flat(&f.values[i], f.elems + f.values[i].elem_base, f.arena);
+    }
+    rr_rdb_flat_free(&f);
+    zfree(dbis);
+    zfree(lens);
+}
+
 robj *desObject(void *buf, size_t len) {
     robj *o = NULL;
     rr_compat_des_batch(&buf, &len, 1, &o);

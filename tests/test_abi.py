@@ -36,13 +36,24 @@ def test_library_exports_every_snappy_symbol():
     assert lib.rr_snappy_max_compressed_length(16384) == 32 + 16384 + 16384 // 6
 
 
+def test_library_exports_every_rdb_symbol():
+    """include/rr_rdb.h (row f4): every declared function is exported."""
+    lib = rr.lib()
+    syms = declared_symbols("rr_rdb.h")
+    assert len(syms) == 5
+    for s in syms:
+        assert hasattr(lib, s), f"{s} declared in include/rr_rdb.h but not exported"
+    assert sorted(rr.RDB_EXPORTS) == syms
+
+
 def test_compat_header_symbols_defined(tmp_path):
     """Every function include/rock_serdes_compat.h declares (the legacy desString / serObject /
     desObject of rock_serdes.h:47-49 and the rr_compat_* batch forms) is defined by the shim,
     redrock_old_amd/compat/rock_serdes_compat.c, compiled as C inside a (model) Redis tree."""
     txt = re.sub(r"/\*.*?\*/", "", open(os.path.join(ROOT, "include", "rock_serdes_compat.h")).read(), flags=re.S)
     declared = sorted(set(re.findall(r"\b([A-Za-z_][A-Za-z_0-9]*)\s*\([^;{]*\)\s*;", txt)))
-    assert {"desString", "serObject", "desObject", "rr_compat_des_batch", "rr_compat_ser_batch"} <= set(declared)
+    assert {"desString", "serObject", "desObject", "rr_compat_des_batch", "rr_compat_ser_batch",
+            "rr_compat_rdb_load_batch"} <= set(declared)
     obj = tmp_path / "compat.o"
     subprocess.run(["gcc", "-std=gnu11", "-Wall", "-Werror", "-DRR_REDIS_TREE", "-c",
                     "-I", os.path.join(ROOT, "tests", "c", "miniredis"), "-I", os.path.join(ROOT, "include"),
@@ -56,7 +67,7 @@ def test_compat_header_symbols_defined(tmp_path):
 
 def test_headers_compile_as_plain_c(tmp_path):
     src = tmp_path / "t.c"
-    src.write_text('#include "rr_serdes.h"\n#include "rr_snappy.h"\n#include "rock_serdes_compat.h"\n'
+    src.write_text('#include "rr_serdes.h"\n#include "rr_snappy.h"\n#include "rr_rdb.h"\n#include "rock_serdes_compat.h"\n'
                    'int main(void){ return (int)sizeof(rr_value) + (int)sizeof(rr_elem) - 32; }\n')
     subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), str(src),
                     "-o", str(tmp_path / "t")], check=True)

@@ -72,3 +72,47 @@ def test_compat_shim_round_trips_fixtures_on_gpu(tmp_path):
     print(r.stdout, r.stderr)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "0 failures" in r.stdout
+
+
+# ---- row f4: batched snapshot restore over the fork-child pipes (include/rr_rdb.h) --------
+def build_rdb(tmp):
+    write_fixtures(os.path.join(tmp, "fixtures.h"))
+    exe = os.path.join(tmp, "test_rdb")
+    cmd = ["gcc", "-std=gnu11", "-O1", "-Wall", "-Werror", "-Wno-unused-function", "-DRR_REDIS_TREE", "-pthread",
+           "-I", os.path.join(ROOT, "tests", "c", "miniredis"), "-I", os.path.join(ROOT, "include"), "-I", tmp,
+           os.path.join(ROOT, "redrock_old_amd", "compat", "rock_serdes_compat.c"),
+           os.path.join(ROOT, "tests", "c", "miniredis", "miniredis.c"),
+           os.path.join(ROOT, "tests", "c", "test_rdb.c"),
+           "-L", os.path.join(ROOT, "redrock_old_amd"), "-lrr_serdes",
+           "-Wl,-rpath," + os.path.join(ROOT, "redrock_old_amd"), "-o", exe]
+    subprocess.run(cmd, check=True)
+    return exe
+
+
+def test_rdb_batch_protocol_cpu(tmp_path):
+    """RAW mode needs no GPU: pipelined batch requests (20000 keys, no deadlock), wire
+    compatibility with the reference's serial child and serial service, missing-key exit."""
+    exe = build_rdb(str(tmp_path))
+    r = subprocess.run([exe, "cpu"], capture_output=True, text=True, timeout=120)
+    print(r.stdout, r.stderr)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "0 failures" in r.stdout
+
+
+@pytest.mark.gpu
+def test_rdb_flat_restore_on_gpu(tmp_path):
+    """FLAT mode: the service decodes on the GPU, the child builds robj from the records;
+    every restored value equals desObject of its blob."""
+    exe = build_rdb(str(tmp_path))
+    r = subprocess.run([exe, "gpu"], capture_output=True, text=True, timeout=120)
+    print(r.stdout, r.stderr)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "0 failures" in r.stdout
+
+
+if __name__ == "__main__":   # python tests/test_compat.py bench  (GPU box): keys/s of the restore paths
+    import sys
+    import tempfile
+    if sys.argv[1:] == ["bench"]:
+        with tempfile.TemporaryDirectory() as d:
+            print(subprocess.run([build_rdb(d), "bench"], capture_output=True, text=True, timeout=300).stdout)
