@@ -829,6 +829,9 @@ static_assert(DEC_BL >= 2 && DEC_BL <= RR_WAVE && DEC_BL % 2 == 0, "batch lanes"
 #ifndef RR_DEC_LATECOPY
 #define RR_DEC_LATECOPY 0
 #endif
+#ifndef RR_DEC_PF   // persistent workgroups, next window's arena copy overlapped with the walks
+#define RR_DEC_PF 0
+#endif
 #ifndef RR_DEC_GLDS   // late-copy staging by global_load_lds (LDS-DMA) instead of register loads
 #define RR_DEC_GLDS 0
 #endif
@@ -859,19 +862,32 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
                                                               rr_value *__restrict__ values,
                                                               rr_elem *__restrict__ elems, uint64_t elem_cap,
                                                               uint8_t *__restrict__ arena, uint64_t *__restrict__ stats,
-                                                              uint64_t *fix) {
+                                                              uint64_t *fix, uint32_t nwin) {
     constexpr uint32_t NT = NW * RR_WAVE, STAGE = W + SLACK;
     static_assert(PMAX % NT == 0 && W % 16 == 0 && SLACK % 16 == 0, "tile shape");
     __shared__ __attribute__((aligned(16))) uint8_t stage[STAGE + 64];
     __shared__ uint16_t perm[PMAX];
     __shared__ uint32_t ccount[C_N], cbase[C_N], ccur[C_N], bpre[C_N + 1];
     __shared__ uint32_t next_batch;
-    PROBE_OR_LATE(__shared__ uint32_t next_copy;)
+    __shared__ uint32_t next_copy;
     __shared__ uint64_t red[2][NW];
     PROBE(__shared__ uint64_t prb[PROBE_WORDS]; uint64_t pt0 = __builtin_amdgcn_s_memtime(), pt1 = 0, pt2 = 0;
           if (threadIdx.x < PROBE_WORDS) prb[threadIdx.x] = 0;)
     const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid / RR_WAVE;
-    const uint32_t tile = blockIdx.x;
+#if RR_DEC_PF
+    // persistent: this workgroup's windows blockIdx.x, + gridDim.x, ...; while a window's longest
+    // walks run, the waves with no batch left copy the NEXT window to the arena (global ->
+    // global), which also leaves its bytes in the L2 for that window's LDS stage
+    for (uint32_t tile = blockIdx.x, it = 0; tile < nwin; tile += gridDim.x, ++it) {
+    if (it) __syncthreads();   // the previous window is done with the LDS
+    if (tid == 0) next_copy = 0;
+    PROBE(pt0 = __builtin_amdgcn_s_memtime(); if (threadIdx.x < PROBE_WORDS) prb[threadIdx.x] = 0;)
+#else
+    {
+    const uint32_t tile = blockIdx.x, it = 0;
+    (void)nwin;
+    (void)it;
+#endif
     const uint64_t v_lo = first_val[tile], v_hi = first_val[tile + 1];
     const uint64_t padded = (offsets[n] + 15) & ~15ull;
     const uint64_t W0 = (uint64_t)tile * W;
@@ -928,6 +944,24 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
     }
 #endif
 #else
+    if (RR_DEC_PF && it > 0) {
+        // 1'. the arena copy was made during the previous window: value bytes -> LDS only
+        //     (L2-hot: that copy just read them)
+        if (staged) {
+            const u32x4 *src = reinterpret_cast<const u32x4 *>(blob);
+            u32x4 *lds = reinterpret_cast<u32x4 *>(stage);
+            const uint64_t cs0 = S0 >> 4, cs1 = S1 >> 4;
+            uint64_t c = cs0 + tid;
+            for (; c + 3 * NT < cs1; c += 4 * NT) {
+                u32x4 x[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) x[k] = src[c + k * NT];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) lds[c + k * NT - cs0] = x[k];
+            }
+            for (; c < cs1; c += NT) lds[c - cs0] = src[c];
+        }
+    } else
     // 1. window -> arena, value bytes -> LDS (one load feeds both)
     {
         const u32x4 *src = reinterpret_cast<const u32x4 *>(blob);
@@ -1079,6 +1113,40 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
             })
         }
     }
+#if RR_DEC_PF
+    {   // 4'. the next window's mirror-arena copy, 4 KiB tasks taken by waves with no batch left
+        const uint32_t ntile = tile + gridDim.x;
+        const uint64_t nW0 = (uint64_t)ntile * W, nW1 = nW0 + W < padded ? nW0 + W : padded;
+        if (ntile < nwin && nW1 > nW0) {
+            if (v_end == v_lo) __syncthreads();   // (no chunk ran: order next_copy's reset)
+            const u32x4 *src = reinterpret_cast<const u32x4 *>(blob);
+            u32x4 *dst = reinterpret_cast<u32x4 *>(arena);
+            const uint64_t cw0 = nW0 >> 4, cw1 = nW1 >> 4;
+            constexpr uint32_t TASK = 4 * RR_WAVE;   // 16-byte granules per task
+            const uint32_t ntask = (uint32_t)((cw1 - cw0 + TASK - 1) / TASK);
+            for (;;) {
+                uint32_t ti = 0;
+                if (lane == 0) ti = atomicAdd(&next_copy, 1u);
+                ti = __builtin_amdgcn_readfirstlane(__shfl(ti, 0, RR_WAVE));
+                if (ti >= ntask) break;
+                const uint64_t g0 = cw0 + (uint64_t)ti * TASK + lane;
+                u32x4 x[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const uint64_t g = g0 + k * RR_WAVE;
+                    if (g < cw1) x[k] = src[g];
+                }
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const uint64_t g = g0 + k * RR_WAVE;
+#ifndef RR_ABLATE_NOCOPY
+                    if (g < cw1) __builtin_nontemporal_store(x[k], dst + g);
+#endif
+                }
+            }
+        }
+    }
+#endif
 #if RR_DEC_LATECOPY
     // 4. the window's mirror-arena copy in 4 KiB tasks, taken by each wave as soon as it has no
     //    batch left (from the LDS stage where the window's bytes are staged, else from global)
@@ -1123,6 +1191,7 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
         PROBE(prb[0] = pt1 - pt0; prb[1] = pt2 - pt1; prb[2] = __builtin_amdgcn_s_memtime() - pt2; prb[28] = v_hi - v_lo;
               prb[29] = staged; if (g_probe) for (uint32_t i = 0; i < PROBE_WORDS; ++i) g_probe[(uint64_t)tile * PROBE_WORDS + i] = prb[i];)
     }
+    }   // window
 }
 
 struct ElemV {
@@ -1989,8 +2058,15 @@ extern "C" hipError_t rr_launch_decode(const uint8_t *blob, const uint64_t *offs
     hipLaunchKernelGGL(count_kernel, dim3((uint32_t)((n + 1 + 255) / 256)), dim3(256), 0, stream, blob, offsets, n,
                        first_val, nw, DEC_W, counts, cls, lb, (uint32_t)(lb_words + FIX_HDR), totals);
     if (st) hipLaunchKernelGGL(scan_kernel, dim3(st), dim3(256), 0, stream, counts, n, lb, st, fix + 1);
-    hipLaunchKernelGGL((DECODE_KERNEL), dim3(nw), dim3(DEC_NW * RR_WAVE), 0, stream, blob, data_cap, offsets, n,
-                       first_val, cls, counts, values, elems, elem_cap, arena, stats, fix);
+#if RR_DEC_PF
+    static uint32_t dec_grid = 0;
+    if (!dec_grid) dec_grid = resident_grid(DECODE_KERNEL, DEC_NW * RR_WAVE, false);
+    const uint32_t grid = nw < dec_grid ? nw : dec_grid;
+#else
+    const uint32_t grid = nw;
+#endif
+    hipLaunchKernelGGL((DECODE_KERNEL), dim3(grid), dim3(DEC_NW * RR_WAVE), 0, stream, blob, data_cap, offsets, n,
+                       first_val, cls, counts, values, elems, elem_cap, arena, stats, fix, nw);
     static uint32_t post_grid = 0;
     if (!post_grid) post_grid = resident_grid(decode_post_kernel, FIX_NT, false);
     hipLaunchKernelGGL(decode_post_kernel, dim3(post_grid), dim3(FIX_NT), 0, stream, blob, fix, values, elems, stats,
