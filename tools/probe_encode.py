@@ -14,7 +14,7 @@ import redrock_old_amd as rr  # noqa: E402
 
 cfg = int(sys.argv[1]) if len(sys.argv) > 1 else 4
 n = int(sys.argv[2]) if len(sys.argv) > 2 else 1_000_000
-W = int(os.environ.get("RR_ENC_W", 32768))
+W = int(os.environ.get("RR_ENC_W", 16384))   # must match the build (rr_kernels.hip RR_ENC_W)
 data, offs = rr.gen_batch(cfg, n)
 nb = int(offs[-1])
 dev = torch.device("cuda:0")
@@ -32,7 +32,7 @@ d_ooffs = torch.empty(n + 1, dtype=torch.int64, device=dev)
 eng.decode_device(d_data, d_offs, d_vals, d_elems, d_arena, d_tot)
 torch.cuda.synchronize()
 PW = 13
-nwin = d_out.numel() // W + 1
+nwin = d_out.numel() // min(W, 4096) + 1   # (over-allocated: a smaller build window still fits)
 probe = torch.zeros(nwin * PW, dtype=torch.int64, device=dev)
 L = rr.lib()
 L.rr_eprobe_set.argtypes = [C.c_void_p]
