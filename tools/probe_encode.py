@@ -32,8 +32,9 @@ d_ooffs = torch.empty(n + 1, dtype=torch.int64, device=dev)
 eng.decode_device(d_data, d_offs, d_vals, d_elems, d_arena, d_tot)
 torch.cuda.synchronize()
 PW = 13
-nwin = d_out.numel() // min(W, 4096) + 1   # (over-allocated: a smaller build window still fits)
-probe = torch.zeros(nwin * PW, dtype=torch.int64, device=dev)
+nwin = d_out.numel() // W + 1
+# (allocated for 4 KiB windows: a build with smaller windows than W still stays inside it)
+probe = torch.zeros((d_out.numel() // 4096 + 1) * PW, dtype=torch.int64, device=dev)
 L = rr.lib()
 L.rr_eprobe_set.argtypes = [C.c_void_p]
 assert L.rr_eprobe_set(C.c_void_p(probe.data_ptr())) == 0
@@ -41,7 +42,7 @@ for _ in range(3):
     eng.encode_device(d_vals, d_elems, d_arena, d_out, d_ooffs, d_tot)
 torch.cuda.synchronize()
 assert torch.equal(d_out[:nb], d_data[:nb])
-p = probe.cpu().numpy().reshape(nwin, PW).astype(np.float64)
+p = probe.cpu().numpy()[:nwin * PW].reshape(nwin, PW).astype(np.float64)
 p = p[p[:, 5] > 0]
 print(f"cfg {cfg}: {len(p)} windows of {W} B, values/window {p[:, 6].mean():.1f}, "
       f"tasks/window {p[:, 7].mean():.0f}, pieces/window {p[:, 8].mean():.0f} (max {p[:, 8].max():.0f})")
