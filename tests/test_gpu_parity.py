@@ -361,3 +361,50 @@ def test_config4_at_baseline_size_10m(engine):
     assert int(tot[2]) == 0 and int(tot[1]) == nb
     assert torch.equal(d_out[:nb], d_data[:nb])
     assert np.array_equal(d_ooffs.cpu().numpy().view(np.uint64), offs)
+
+
+@pytest.mark.parametrize("cfg,n", [(4, 3000), (3, 1500), (10, 600), (11, 40), (1, 2000)])
+def test_fuzz_structured_decode_and_reencode(engine, cfg, n):
+    """~60K mutated blobs over five configs: bit flips, truncations, random bytes, header and
+    length fields overwritten with small / boundary / huge values (counts, lengths, zlbytes /
+    zltail / zllen, intset width and count, encoding bytes), inserted and swapped bytes.  The
+    GPU's records, descriptors and totals equal the oracle's value for value, and every value
+    that decoded re-encodes to the oracle's bytes."""
+    rng = np.random.default_rng(1000 + cfg)
+    data, offs = rr.gen_batch(cfg, n)
+    specials = [0, 1, 2, 3, 4, 7, 8, 15, 16, 0x7F, 0x80, 0xFE, 0xFF, 0xFFFF, 0x10000, 0x7FFFFFFF, 0xFFFFFFFF]
+    blobs = []
+    for i in range(len(offs) - 1):
+        b = bytes(data[offs[i]:offs[i + 1]])
+        for _ in range(5):
+            m = bytearray(b)
+            r = int(rng.integers(0, 7))
+            if r == 0 and m:
+                m[int(rng.integers(0, len(m)))] ^= 1 << int(rng.integers(0, 8))
+            elif r == 1 and m:
+                m = m[:int(rng.integers(0, len(m)))]
+            elif r == 2 and m:
+                m[int(rng.integers(0, len(m)))] = int(rng.integers(0, 256))
+            elif r == 3 and len(m) >= 9:   # a header field: bytes 5.. hold counts / lengths / ziplist words
+                at = int(rng.integers(5, min(len(m) - 3, 30)))
+                m[at:at + 4] = int(specials[int(rng.integers(len(specials)))]).to_bytes(4, "little")
+            elif r == 4 and len(m) >= 13:  # an element length field somewhere in the body
+                at = int(rng.integers(13, len(m) - 3)) if len(m) > 16 else 5
+                m[at:at + 4] = int(specials[int(rng.integers(len(specials)))]).to_bytes(4, "little")
+            elif r == 5 and m:
+                at = int(rng.integers(0, len(m)))
+                m[at:at] = bytes(rng.integers(0, 256, int(rng.integers(1, 9)), dtype=np.uint8))
+            elif r == 6 and len(m) > 2:
+                a, c = (int(x) for x in rng.integers(0, len(m), 2))
+                m[a], m[c] = m[c], m[a]
+            blobs.append(bytes(m))
+    fdata, foffs = batch_from_blobs(blobs)
+    v, e, a, t = engine.decode_host(fdata, foffs)
+    ov, oe, oa, ot = cpu.decode(fdata, foffs, nthreads=8)
+    assert_flat_equal((v, e), (ov, oe), f"structured fuzz cfg {cfg}")
+    assert t == ot
+    assert (v["status"] != 0).any() and (v["status"] == 0).any()
+    # every value that decoded re-encodes like the oracle's encode of the same flat batch
+    gd, go, gt = engine.encode_host(v, e, a)
+    od, oo, otot = cpu.encode(ov, oe, oa)
+    assert np.array_equal(go, oo) and np.array_equal(gd, od[:int(oo[-1])]) and gt == otot
