@@ -832,6 +832,9 @@ static_assert(DEC_BL >= 2 && DEC_BL <= RR_WAVE && DEC_BL % 2 == 0, "batch lanes"
 #ifndef RR_DEC_PF   // persistent workgroups, next window's arena copy overlapped with the walks
 #define RR_DEC_PF 0
 #endif
+#ifndef RR_DEC_EARLY  // late-copy builds: write the arena copy from the stage before the walks, not after
+#define RR_DEC_EARLY 0
+#endif
 #ifndef RR_DEC_GLDS   // late-copy staging by global_load_lds (LDS-DMA) instead of register loads
 #define RR_DEC_GLDS 0
 #endif
@@ -992,6 +995,23 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
         }
     }
 #endif
+#if RR_DEC_LATECOPY && RR_DEC_EARLY
+    // 1b. the window's arena copy straight from the LDS stage (bytes before S0, and windows
+    //     that are not staged, from global memory), before the walks start
+    __syncthreads();   // the stage is complete
+    {
+        const u32x4 *src = reinterpret_cast<const u32x4 *>(blob);
+        u32x4 *dst = reinterpret_cast<u32x4 *>(arena);
+        const u32x4 *lds = reinterpret_cast<const u32x4 *>(stage);
+        const uint64_t cw0 = W0 >> 4, cw1 = W1 >> 4, cs0 = S0 >> 4, cs1 = staged ? S1 >> 4 : cs0;
+        for (uint64_t g = cw0 + tid; g < cw1; g += NT) {
+            const u32x4 x = g >= cs0 && g < cs1 ? lds[g - cs0] : src[g];
+#ifndef RR_ABLATE_NOCOPY
+            __builtin_nontemporal_store(x, dst + g);
+#endif
+        }
+    }
+#endif
     // values that do not fit the stage are read from global memory; if even their 32-bit
     // window-relative byte or slot offsets could overflow, the exact parser takes them
     const uint64_t eb0 = ebase[v_lo], eb1 = ebase[v_hi];
@@ -1147,7 +1167,7 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
         }
     }
 #endif
-#if RR_DEC_LATECOPY
+#if RR_DEC_LATECOPY && !RR_DEC_EARLY
     // 4. the window's mirror-arena copy in 4 KiB tasks, taken by each wave as soon as it has no
     //    batch left (from the LDS stage where the window's bytes are staged, else from global)
     {
