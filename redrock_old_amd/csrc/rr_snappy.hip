@@ -328,10 +328,15 @@ __device__ void compress_fragment(const Frag &F, uint32_t fn, lds_u16 *table, ui
                 uint32_t P0 = ip, S0 = 32, K = RR_SNZ_K0;   // a round's width doubles while nothing matches
                 for (;;) {
                     uint32_t P = P0, S = S0;
-                    for (uint32_t t = 0; t + 1 < K; ++t) {
-                        const uint32_t B = S >> 5;
-                        P = t < lane ? P + B : P;
-                        S = t < lane ? S + B : S;
+                    if (S0 + K <= 64) {   // the stride is 1 for the whole round (the common case)
+                        P = P0 + lane;
+                        S = S0 + lane;
+                    } else {
+                        for (uint32_t t = 0; t + 1 < K; ++t) {
+                            const uint32_t B = S >> 5;
+                            P = t < lane ? P + B : P;
+                            S = t < lane ? S + B : S;
+                        }
                     }
                     const uint32_t B = S >> 5, Pn = P + B;
                     const bool act = lane < K;
@@ -339,10 +344,21 @@ __device__ void compress_fragment(const Frag &F, uint32_t fn, lds_u16 *table, ui
                     const uint32_t x = F.ld32(act ? P : 0);
                     const uint32_t H = hash32(x, shift);
                     int prev = -1;
+#if RR_SNZ_K == 16 && RR_SNZ_K0 == 16
+                    // (one 16-lane DPP row: lane j sees lane j - r by a row shift, no LDS round trip)
+#define SNZ_ROW_SHR(r) { \
+        const uint32_t hk = (uint32_t)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)H, 0x110 + (r), 0xF, 0xF, false); \
+        prev = (prev < 0 && hk == H) ? (int)lane - (r) : prev; }
+                    SNZ_ROW_SHR(1) SNZ_ROW_SHR(2) SNZ_ROW_SHR(3) SNZ_ROW_SHR(4) SNZ_ROW_SHR(5)
+                    SNZ_ROW_SHR(6) SNZ_ROW_SHR(7) SNZ_ROW_SHR(8) SNZ_ROW_SHR(9) SNZ_ROW_SHR(10)
+                    SNZ_ROW_SHR(11) SNZ_ROW_SHR(12) SNZ_ROW_SHR(13) SNZ_ROW_SHR(14) SNZ_ROW_SHR(15)
+#undef SNZ_ROW_SHR
+#else
                     for (uint32_t r = 1; r < K; ++r) {
                         const uint32_t hk = (uint32_t)__shfl((int)H, (int)((lane - r) & (WAVE - 1)), WAVE);
                         prev = (prev < 0 && lane >= r && hk == H) ? (int)(lane - r) : prev;
                     }
+#endif
                     const uint32_t Pp = (uint32_t)__shfl((int)P, prev < 0 ? (int)lane : prev, WAVE);
                     const uint32_t c = prev >= 0 ? Pp : (uint32_t)table[act ? H : 0];
                     const bool m = valid && x == F.ld32(c);
