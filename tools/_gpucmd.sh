@@ -1,5 +1,7 @@
 set -e
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_gpu_snappy.py -m gpu -q --timeout 200 --timeout-method thread > gpurun_out/snz7.log 2>&1
-for c in 4 3; do timeout -k 10 120 python -u tools/time_snappy.py $c 1000000 3 16384 | grep -v decompress > gpurun_out/tsnz7_$c.log 2>&1; done
+timeout -k 10 500 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -rf > gpurun_out/t19.log 2>&1
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/smoke19.log 2>&1
+timeout -k 10 400 python -u bench.py > gpurun_out/r2_bench3.log 2>&1
+timeout -k 10 400 bash tools/profile_bench.sh gpurun_out/r2prof3
 echo done
