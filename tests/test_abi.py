@@ -46,6 +46,16 @@ def test_library_exports_every_rdb_symbol():
     assert sorted(rr.RDB_EXPORTS) == syms
 
 
+def test_library_exports_every_kv_symbol():
+    """include/rr_kv.h (row f2): every declared function is exported."""
+    lib = rr.lib()
+    syms = declared_symbols("rr_kv.h")
+    assert len(syms) == 2
+    for s in syms:
+        assert hasattr(lib, s), f"{s} declared in include/rr_kv.h but not exported"
+    assert sorted(rr.KV_EXPORTS) == syms
+
+
 def test_compat_header_symbols_defined(tmp_path):
     """Every function include/rock_serdes_compat.h declares (the legacy desString / serObject /
     desObject of rock_serdes.h:47-49 and the rr_compat_* batch forms) is defined by the shim,
@@ -67,7 +77,7 @@ def test_compat_header_symbols_defined(tmp_path):
 
 def test_headers_compile_as_plain_c(tmp_path):
     src = tmp_path / "t.c"
-    src.write_text('#include "rr_serdes.h"\n#include "rr_snappy.h"\n#include "rr_rdb.h"\n#include "rock_serdes_compat.h"\n'
+    src.write_text('#include "rr_serdes.h"\n#include "rr_snappy.h"\n#include "rr_rdb.h"\n#include "rr_kv.h"\n#include "rock_serdes_compat.h"\n'
                    'int main(void){ return (int)sizeof(rr_value) + (int)sizeof(rr_elem) - 32; }\n')
     subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), str(src),
                     "-o", str(tmp_path / "t")], check=True)

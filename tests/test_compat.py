@@ -116,3 +116,31 @@ if __name__ == "__main__":   # python tests/test_compat.py bench  (GPU box): key
     if sys.argv[1:] == ["bench"]:
         with tempfile.TemporaryDirectory() as d:
             print(subprocess.run([build_rdb(d), "bench"], capture_output=True, text=True, timeout=300).stdout)
+
+
+# ---- row f2: batched store I/O around the GPU path (include/rr_kv.h) ----------------------
+def build_kv(tmp):
+    write_fixtures(os.path.join(tmp, "fixtures.h"))
+    exe = os.path.join(tmp, "test_kv")
+    cmd = ["gcc", "-std=gnu11", "-O1", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), "-I", tmp,
+           os.path.join(ROOT, "tests", "c", "test_kv.c"), "-L", os.path.join(ROOT, "redrock_old_amd"), "-lrr_serdes",
+           "-Wl,-rpath," + os.path.join(ROOT, "redrock_old_amd"), "-o", exe]
+    subprocess.run(cmd, check=True)
+    return exe
+
+
+def test_kv_batch_io_builds(tmp_path):
+    exe = build_kv(str(tmp_path))
+    nm = subprocess.run(["nm", exe], capture_output=True, text=True, check=True).stdout
+    assert " U rr_kv_dump_batch" in nm and " U rr_kv_restore_batch" in nm
+
+
+@pytest.mark.gpu
+def test_kv_batch_io_on_gpu(tmp_path):
+    """One WriteBatch-shaped dump and one MultiGet-shaped restore of 3000 values, plain and
+    snappy-compressed: stored bytes are serObject's, the restore equals the decode of them."""
+    exe = build_kv(str(tmp_path))
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    print(r.stdout, r.stderr)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "0 failures" in r.stdout
