@@ -832,6 +832,16 @@ static_assert(DEC_BL >= 2 && DEC_BL <= RR_WAVE && DEC_BL % 2 == 0, "batch lanes"
 #ifndef RR_DEC_PF   // persistent workgroups, next window's arena copy overlapped with the walks
 #define RR_DEC_PF 0
 #endif
+#ifndef RR_DEC_OVL   // the window's loads in flight under the class sort (fused copy builds)
+#define RR_DEC_OVL 1
+#endif
+#if RR_DEC_LATECOPY   // (the overlap applies to the fused copy)
+#undef RR_DEC_OVL
+#define RR_DEC_OVL 0
+#endif
+#ifndef RR_DEC_OVL_K  // granules (16 B) per thread loaded before the sort (the rest after it)
+#define RR_DEC_OVL_K 9
+#endif
 #ifndef RR_DEC_EARLY  // late-copy builds: write the arena copy from the stage before the walks, not after
 #define RR_DEC_EARLY 0
 #endif
@@ -947,6 +957,61 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
     }
 #endif
 #else
+#if RR_DEC_OVL
+    // 1''. the common case (the window and its values' tail fit RR_DEC_OVL_K granules per
+    //      thread): the loads are issued here and land while the class sort below runs; the
+    //      arena stores and the LDS stage writes follow the sort (plain loads survive its
+    //      barriers).  The sort reads no global memory, so none of its waits drain them.
+    const uint64_t eb0 = ebase[v_lo], eb1 = ebase[v_hi];
+    const uint64_t ov_w1 = W1 >> 4, ov_s0 = S0 >> 4, ov_e = (staged && S1 > W1 ? S1 : W1) >> 4;
+    const bool ovl = !(RR_DEC_PF && it > 0);
+    u32x4 ov_x[RR_DEC_OVL_K];
+    if (ovl) {
+        const u32x4 *src = reinterpret_cast<const u32x4 *>(blob);
+#pragma unroll
+        for (int k = 0; k < RR_DEC_OVL_K; ++k) {
+            const uint64_t g = (W0 >> 4) + tid + (uint64_t)k * NT;
+            ov_x[k] = g < ov_e ? src[g] : u32x4{0u, 0u, 0u, 0u};
+        }
+    }
+    auto ov_finish = [&]() __attribute__((always_inline)) {
+        const u32x4 *src = reinterpret_cast<const u32x4 *>(blob);
+        u32x4 *dst = reinterpret_cast<u32x4 *>(arena);
+        u32x4 *lds = reinterpret_cast<u32x4 *>(stage);
+#pragma unroll
+        for (int k = 0; k < RR_DEC_OVL_K; ++k) {
+            const uint64_t g = (W0 >> 4) + tid + (uint64_t)k * NT;
+#ifndef RR_ABLATE_NOCOPY
+            if (g < ov_w1) __builtin_nontemporal_store(ov_x[k], dst + g);
+#endif
+            if (staged && g >= ov_s0 && g < ov_e) lds[g - ov_s0] = ov_x[k];
+        }
+        // the rest of the window (beyond the prefetched granules), loaded now
+        uint64_t c = (W0 >> 4) + tid + (uint64_t)RR_DEC_OVL_K * NT;
+        for (; c + 3 * NT < ov_e; c += 4 * NT) {
+            u32x4 x[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) x[k] = src[c + k * NT];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint64_t cc = c + k * NT;
+#ifndef RR_ABLATE_NOCOPY
+                if (cc < ov_w1) __builtin_nontemporal_store(x[k], dst + cc);
+#endif
+                if (staged && cc >= ov_s0) lds[cc - ov_s0] = x[k];
+            }
+        }
+        for (; c < ov_e; c += NT) {
+            const u32x4 x = src[c];
+#ifndef RR_ABLATE_NOCOPY
+            if (c < ov_w1) __builtin_nontemporal_store(x, dst + c);
+#endif
+            if (staged && c >= ov_s0) lds[c - ov_s0] = x;
+        }
+    };
+    if (ovl) {
+    } else
+#endif
     if (RR_DEC_PF && it > 0) {
         // 1'. the arena copy was made during the previous window: value bytes -> LDS only
         //     (L2-hot: that copy just read them)
@@ -1014,7 +1079,9 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
 #endif
     // values that do not fit the stage are read from global memory; if even their 32-bit
     // window-relative byte or slot offsets could overflow, the exact parser takes them
+#if !RR_DEC_OVL
     const uint64_t eb0 = ebase[v_lo], eb1 = ebase[v_hi];
+#endif
     const bool far = (!staged && S1 - S0 > 0xFFFFFF00ull) || (eb1 - eb0) * 16 >= NOSLOT;
     const LdsSrc lsrc{(lds_cptr)stage};
     const GlbSrc gsrc{make_rsrc(blob + S0, (uint32_t)(data_cap - S0 < 0xFFFFFFFFull ? data_cap - S0 : 0xFFFFFFFFull))};
@@ -1029,13 +1096,13 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
 #else
     const uint64_t v_end = v_hi;
 #endif
-    for (uint64_t c0 = v_lo; c0 < v_end; c0 += PMAX) {
+    // 2. counting sort of a chunk of values by class (ballot per class, one LDS atomic per
+    //    class per wave-round) into perm, class bases and batch prefixes
+    auto sort_chunk = [&](uint64_t c0) __attribute__((always_inline)) {
         const uint32_t nv = (uint32_t)(v_hi - c0 < PMAX ? v_hi - c0 : PMAX);
-        // 2. counting sort by class (ballot per class, one LDS atomic per class per wave-round)
-        if (c0 != v_lo) __syncthreads();   // every wave is done with the previous chunk's batches
         if (tid < C_N) { ccount[tid] = 0; ccur[tid] = 0; }
         if (tid == 0) next_batch = 0;
-        __syncthreads();   // also: the stage is complete; the previous chunk's batches are done
+        __syncthreads();   // also: the previous chunk's batches are done
         PROBE(if (c0 == v_lo) pt1 = __builtin_amdgcn_s_memtime();)
         uint32_t myc[PMAX / NT];
 #pragma unroll
@@ -1079,7 +1146,17 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
                 }
             }
         }
-        __syncthreads();
+    };
+    if (v_end > v_lo) sort_chunk(v_lo);   // (with the window's loads still in flight)
+#if RR_DEC_OVL
+    if (ovl) ov_finish();   // they have landed under the sort
+#endif
+    for (uint64_t c0 = v_lo; c0 < v_end; c0 += PMAX) {
+        if (c0 != v_lo) {
+            __syncthreads();   // every wave is done with the previous chunk's batches
+            sort_chunk(c0);
+        }
+        __syncthreads();   // the stage and the chunk's sort are complete
 
         PROBE(if (c0 == v_lo) pt2 = __builtin_amdgcn_s_memtime();)
         // 3. single-class batches, taken dynamically by the waves
