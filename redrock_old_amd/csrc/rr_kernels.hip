@@ -1570,10 +1570,13 @@ __device__ __forceinline__ ElemCost elem_cost(uint32_t type, uint32_t enc, uint6
     }
 }
 
+#ifndef RR_ENC_SIZE_U   // descriptor loads in flight per lane in the size pass
+#define RR_ENC_SIZE_U 4
+#endif
 // serObject rock_serdes.c:512-535: blob size of one flat value, 0 + status if unencodable:
 // a value whose status is not RR_OK, whose descriptor range passes elem_cap or whose payloads
-// pass arena_cap is never read further (RR_E_ENCODE).  Descriptors are read four at a time
-// (independent 16-byte loads in flight per lane).
+// pass arena_cap is never read further (RR_E_ENCODE).  Descriptors are read RR_ENC_SIZE_U at a
+// time (independent 16-byte loads in flight per lane).
 __device__ uint64_t encode_size(uint32_t type, uint32_t enc, uint32_t vstatus, uint64_t eb, uint64_t n,
                                 const rr_elem *elems, uint64_t ecap, uint64_t acap, uint32_t &st, uint64_t &pay) {
     st = RR_OK;
@@ -1610,12 +1613,12 @@ __device__ uint64_t encode_size(uint32_t type, uint32_t enc, uint32_t vstatus, u
             if ((type == RR_TYPE_HASH_HT || type == RR_TYPE_ZSET_SKIPLIST) && (n & 1)) break;
             uint64_t sz = type == RR_TYPE_LIST_QUICKLIST ? 5 : 13, p = 0;
             bool bad = false;
-            for (uint64_t i = 0; i < n; i += 4) {
-                ElemV e[4];
+            for (uint64_t i = 0; i < n; i += RR_ENC_SIZE_U) {
+                ElemV e[RR_ENC_SIZE_U];
 #pragma unroll
-                for (uint32_t k = 0; k < 4; ++k) e[k] = i + k < n ? get_elem(el + i + k) : ElemV{0, 0, RR_K_INT};
+                for (uint32_t k = 0; k < RR_ENC_SIZE_U; ++k) e[k] = i + k < n ? get_elem(el + i + k) : ElemV{0, 0, RR_K_INT};
 #pragma unroll
-                for (uint32_t k = 0; k < 4; ++k) {
+                for (uint32_t k = 0; k < RR_ENC_SIZE_U; ++k) {
                     if (i + k < n) {
                         const ElemCost c = elem_cost(type, enc, i + k, e[k], acap);
                         sz += c.bytes;
@@ -1870,11 +1873,12 @@ struct Img {
         if (r_ & 1) i_[p_] = (uint8_t)P##t1;                                                     \
     }
 
-// Copy-queue entry: arena offset (40 bits) | image offset << 40 (16 bits) | (len - 1) << 56.
+// Copy-run queue: one entry per payload (arena offset (40 bits) | length << 40, image offset,
+// first piece); the copy phase splits the runs into 64-byte image-block pieces.
 constexpr uint64_t JQ_SRC = (1ull << 40) - 1;
 
 
-template <uint32_t W, uint32_t NT, uint32_t JCAP>
+template <uint32_t W, uint32_t NT, uint32_t RCAP>
 __global__ __launch_bounds__(NT) void enc_emit_kernel(const rr_value *__restrict__ values,
                                                       const rr_elem *__restrict__ elems,
                                                       const uint8_t *__restrict__ arena, uint64_t n,
@@ -1883,14 +1887,17 @@ __global__ __launch_bounds__(NT) void enc_emit_kernel(const rr_value *__restrict
                                                       const uint32_t *__restrict__ fv) {
     static_assert(W <= 65536 && W % 64 == 0, "image offsets are 16-bit, pieces 64-byte blocks");
     __shared__ uint4 img4[W / 16];
-    __shared__ uint64_t jq[JCAP];
+    __shared__ uint64_t rq_a[RCAP];        // run: arena offset | length << 40
+    __shared__ uint32_t rq_d[RCAP];        // run: image offset
+    __shared__ uint32_t rq_p[RCAP + 1];    // run: first piece (pieces of earlier runs)
     __shared__ uint32_t tb[NT + 1];        // task base of each value of the round
     __shared__ uint64_t sv_pos[NT];        // output position of the value's first task
     __shared__ uint64_t sv_eb[NT];         // element-byte scan at the value's first task
     __shared__ uint32_t sv_el[NT];         // elem_base
     __shared__ uint32_t sv_te[NT];         // type | enc << 8
     __shared__ uint64_t wsum[2][NT / RR_WAVE];
-    __shared__ uint32_t sh_nj;
+    __shared__ uint64_t sh_nrp;            // runs reserved | pieces reserved << 32
+    __shared__ uint32_t sh_pend;           // pieces of the queued runs, when the queue overflowed
     uint8_t *img = reinterpret_cast<uint8_t *>(img4);
     const uint32_t tid = threadIdx.x;
     const uint64_t total = offsets[n];
@@ -1902,16 +1909,16 @@ __global__ __launch_bounds__(NT) void enc_emit_kernel(const rr_value *__restrict
     const Img I{img, w0, span};
 #pragma unroll
     for (uint32_t k = tid; k < W / 16; k += NT) img4[k] = make_uint4(0, 0, 0, 0);
-    if (tid == 0) sh_nj = 0;
+    if (tid == 0) { sh_nrp = 0; sh_pend = 0xFFFFFFFFu; }
     const uint64_t v0 = fv[blockIdx.x];
     const uint64_t vend = w0 + W < total ? (uint64_t)fv[blockIdx.x + 1] + 1 : n;
     lds_barrier();
     EPROBE(const uint64_t et1 = rr_stamp();)
 
-    // Payload bytes [pos, pos+len) <- arena[src..]: clipped to the window, split into the
-    // 64-byte aligned image blocks it touches, queued for the copy phase.  Called by every
-    // lane of the wave (want = false for none): queue slots are reserved with one LDS atomic
-    // per wave over a wave prefix sum.
+    // Payload bytes [pos, pos+len) <- arena[src..]: clipped to the window and queued as one
+    // run for the copy phase.  Called by every lane of the wave (want = false for none): the
+    // run slot and its pieces are reserved together with one 64-bit LDS atomic per wave over
+    // two wave prefix sums, so run order and piece order agree.
     auto payload = [&](bool want, uint64_t pos, uint64_t src, uint64_t len) {
         uint64_t d0 = pos < w0 ? w0 : pos, d1 = pos + len;
         if (d1 > w0 + span) d1 = w0 + span;
@@ -1920,23 +1927,22 @@ __global__ __launch_bounds__(NT) void enc_emit_kernel(const rr_value *__restrict
         const uint32_t dst = want ? (uint32_t)(d0 - w0) : 0, l = want ? (uint32_t)(d1 - d0) : 0;
         const bool queued = want && src + l <= JQ_SRC;
         const uint32_t np = queued ? ((dst + l - 1) >> 6) - (dst >> 6) + 1 : 0;
-        const uint32_t incl = (uint32_t)wave_incl_scan(np);
-        const uint32_t wtot = __shfl(incl, RR_WAVE - 1, RR_WAVE);
-        uint32_t base = 0;
-        if (wtot && lane_id() == RR_WAVE - 1) base = atomicAdd(&sh_nj, wtot);
+        const uint64_t mine = queued ? (1ull | ((uint64_t)np << 32)) : 0;
+        const uint64_t incl = wave_incl_scan(mine);
+        const uint64_t wtot = __shfl(incl, RR_WAVE - 1, RR_WAVE);
+        uint64_t base = 0;
+        if (wtot && lane_id() == RR_WAVE - 1) base = atomicAdd((unsigned long long *)&sh_nrp, (unsigned long long)wtot);
         base = __shfl(base, RR_WAVE - 1, RR_WAVE);
         if (!want) return;
-        const uint32_t j = queued ? base + incl - np : JCAP;
-        const uint32_t npc = queued ? np : 1;
-        uint32_t pd = dst;
-        for (uint32_t k = 0; k < npc; ++k) {
-            const uint32_t pe = k + 1 < npc ? (pd | 63u) + 1 : dst + l;
-            const uint64_t ps = src + (pd - dst);
-            if (j + k < JCAP)
-                jq[j + k] = ps | ((uint64_t)pd << 40) | ((uint64_t)(pe - pd - 1) << 56);
-            else   // queue full: byte copy (rare; keeps the kernel small)
-                for (uint32_t i = pd; i < pe; ++i) img[i] = arena[ps + (i - pd)];
-            pd = pe;
+        const uint64_t at = base + incl - mine;
+        const uint32_t r = (uint32_t)at, p0 = (uint32_t)(at >> 32);
+        if (queued && r < RCAP) {
+            rq_a[r] = src | ((uint64_t)l << 40);
+            rq_d[r] = dst;
+            rq_p[r] = p0;
+        } else {   // queue full (rare; keeps the kernel small): byte copy
+            if (queued && r == RCAP) sh_pend = p0;
+            for (uint32_t i = 0; i < l; ++i) img[dst + i] = arena[src + i];
         }
     };
 
@@ -2063,15 +2069,31 @@ __global__ __launch_bounds__(NT) void enc_emit_kernel(const rr_value *__restrict
     }
     EPROBE(const uint64_t et2 = rr_stamp();)
 
-    // payload pieces
-    const uint32_t nj = sh_nj < JCAP ? sh_nj : JCAP;
-    for (uint32_t j = tid; j < nj; j += 2 * NT) {
-        const bool two = j + NT < nj;
-        const uint64_t q0 = jq[j], q1 = two ? jq[j + NT] : 0;
-        const uint32_t d0 = (uint32_t)(q0 >> 40) & 0xFFFF, l0 = (uint32_t)(q0 >> 56) + 1;
-        const uint32_t d1 = (uint32_t)(q1 >> 40) & 0xFFFF, l1 = two ? (uint32_t)(q1 >> 56) + 1 : 0;
-        RR_PIECE_LOAD(a_, arena + (q0 & JQ_SRC), d0, l0)
-        RR_PIECE_LOAD(b_, arena + (q1 & JQ_SRC), d1, l1)
+    // payload pieces: piece b of the window -> its run (last run whose first piece <= b) ->
+    // the run's k-th 64-byte image block
+    const uint32_t nr = (uint32_t)sh_nrp < RCAP ? (uint32_t)sh_nrp : RCAP;
+    const uint32_t npc = sh_pend != 0xFFFFFFFFu ? sh_pend : (uint32_t)(sh_nrp >> 32);
+    auto piece = [&](uint32_t b, uint64_t &ps, uint32_t &pd, uint32_t &pl) {
+        uint32_t lo = 0;
+#pragma unroll
+        for (uint32_t s = RCAP / 2; s > 0; s >>= 1)
+            if (lo + s < nr && rq_p[lo + s] <= b) lo += s;
+        const uint64_t a = rq_a[lo];
+        const uint32_t dst = rq_d[lo], l = (uint32_t)(a >> 40), k = b - rq_p[lo];
+        const uint32_t d0 = k == 0 ? dst : ((dst >> 6) + k) << 6;
+        const uint32_t e1 = (((dst >> 6) + k + 1) << 6), e = e1 < dst + l ? e1 : dst + l;
+        ps = (a & JQ_SRC) + (d0 - dst);
+        pd = d0;
+        pl = e - d0;
+    };
+    for (uint32_t j = tid; j < npc; j += 2 * NT) {
+        const bool two = j + NT < npc;
+        uint64_t s0, s1 = 0;
+        uint32_t d0, l0, d1 = 0, l1 = 0;
+        piece(j, s0, d0, l0);
+        if (two) piece(j + NT, s1, d1, l1);
+        RR_PIECE_LOAD(a_, arena + s0, d0, l0)
+        RR_PIECE_LOAD(b_, arena + s1, d1, l1)
         RR_PIECE_STORE(a_, img, d0, l0)
         RR_PIECE_STORE(b_, img, d1, l1)
     }
@@ -2089,7 +2111,7 @@ __global__ __launch_bounds__(NT) void enc_emit_kernel(const rr_value *__restrict
            if (tid == 0 && g_eprobe) {
                uint64_t *o = g_eprobe + (uint64_t)blockIdx.x * EPROBE_WORDS;
                o[0] = et1 - et0; o[1] = (et2 - et1) - etk; o[2] = etk; o[3] = et3 - et2; o[4] = et4 - et3;
-               o[5] = et4 - et0; o[6] = vend - v0; o[7] = ent; o[8] = sh_nj;
+               o[5] = et4 - et0; o[6] = vend - v0; o[7] = ent; o[8] = npc;
                o[9] = tw1; o[10] = tsc; o[11] = twr; o[12] = tw2;
            })
 }
@@ -2176,7 +2198,7 @@ extern "C" hipError_t rr_launch_decode(const uint8_t *blob, const uint64_t *offs
 #ifndef RR_ENC_W
 #define RR_ENC_W 16384
 #endif
-constexpr uint32_t ENC_W = RR_ENC_W, ENC_NT = 256, ENC_JCAP = 1024;
+constexpr uint32_t ENC_W = RR_ENC_W, ENC_NT = 256, ENC_RCAP = 512;
 static uint64_t enc_windows(uint64_t data_cap) { return data_cap / ENC_W + 1; }
 
 extern "C" uint64_t rr_encode_scratch_words(uint64_t n, uint64_t data_cap) {
@@ -2206,7 +2228,7 @@ extern "C" hipError_t rr_launch_encode(const rr_value *values, const rr_elem *el
     hipLaunchKernelGGL(scan_kernel, dim3(st), dim3(256), 0, stream, offsets, n, lb, st, err);
     hipLaunchKernelGGL(enc_index_kernel<ENC_W>, dim3(t), dim3(256), 0, stream, values, elems, n, elem_cap, arena_cap,
                        offsets, cap, fv, nw, stats + 3 * (uint64_t)t);
-    hipLaunchKernelGGL((enc_emit_kernel<ENC_W, ENC_NT, ENC_JCAP>), dim3((uint32_t)nw), dim3(ENC_NT), 0, stream,
+    hipLaunchKernelGGL((enc_emit_kernel<ENC_W, ENC_NT, ENC_RCAP>), dim3((uint32_t)nw), dim3(ENC_NT), 0, stream,
                        values, elems, arena, n, out, cap, offsets, fv);
     e = hipGetLastError();
     if (e == hipSuccess && totals) e = launch_finalize(stats, lb, 2 * t, offsets, n, 0, totals, stream, err);
