@@ -1570,13 +1570,11 @@ __device__ __forceinline__ ElemCost elem_cost(uint32_t type, uint32_t enc, uint6
     }
 }
 
-#ifndef RR_ENC_SIZE_U   // descriptor loads in flight per lane in the size pass
-#define RR_ENC_SIZE_U 4
-#endif
 // serObject rock_serdes.c:512-535: blob size of one flat value, 0 + status if unencodable:
 // a value whose status is not RR_OK, whose descriptor range passes elem_cap or whose payloads
-// pass arena_cap is never read further (RR_E_ENCODE).  Descriptors are read RR_ENC_SIZE_U at a
-// time (independent 16-byte loads in flight per lane).
+// pass arena_cap is never read further (RR_E_ENCODE).  Descriptors are read four at a time
+// (independent 16-byte loads in flight per lane).  Used by E3 for the values past data_cap;
+// E1 computes the same sizes element-parallel.
 __device__ uint64_t encode_size(uint32_t type, uint32_t enc, uint32_t vstatus, uint64_t eb, uint64_t n,
                                 const rr_elem *elems, uint64_t ecap, uint64_t acap, uint32_t &st, uint64_t &pay) {
     st = RR_OK;
@@ -1613,12 +1611,12 @@ __device__ uint64_t encode_size(uint32_t type, uint32_t enc, uint32_t vstatus, u
             if ((type == RR_TYPE_HASH_HT || type == RR_TYPE_ZSET_SKIPLIST) && (n & 1)) break;
             uint64_t sz = type == RR_TYPE_LIST_QUICKLIST ? 5 : 13, p = 0;
             bool bad = false;
-            for (uint64_t i = 0; i < n; i += RR_ENC_SIZE_U) {
-                ElemV e[RR_ENC_SIZE_U];
+            for (uint64_t i = 0; i < n; i += 4) {
+                ElemV e[4];
 #pragma unroll
-                for (uint32_t k = 0; k < RR_ENC_SIZE_U; ++k) e[k] = i + k < n ? get_elem(el + i + k) : ElemV{0, 0, RR_K_INT};
+                for (uint32_t k = 0; k < 4; ++k) e[k] = i + k < n ? get_elem(el + i + k) : ElemV{0, 0, RR_K_INT};
 #pragma unroll
-                for (uint32_t k = 0; k < RR_ENC_SIZE_U; ++k) {
+                for (uint32_t k = 0; k < 4; ++k) {
                     if (i + k < n) {
                         const ElemCost c = elem_cost(type, enc, i + k, e[k], acap);
                         sz += c.bytes;
@@ -1641,8 +1639,8 @@ __device__ uint64_t encode_size(uint32_t type, uint32_t enc, uint32_t vstatus, u
 
 // Encode runs as five launches (one memset, no inter-workgroup waits beyond the scan's
 // look-back):
-//   E1 enc_size_kernel  thread per value: blob size (0 for an unencodable value) into
-//                       offsets[v], per-tile {bad, payload, descriptors};
+//   E1 enc_size_kernel  workgroup per 256 values, element-parallel: blob size (0 for an
+//                       unencodable value) into offsets[v], per-tile {bad, payload, descriptors};
 //   E2 scan_kernel      in-place exclusive scan -> offsets[0..n];
 //   E3 enc_index_kernel thread per value: first value of every W-byte output window, and the
 //                       values that would cross data_cap (RR_E_CAPACITY, payload taken back);
@@ -1654,33 +1652,189 @@ __device__ uint64_t encode_size(uint32_t type, uint32_t enc, uint32_t vstatus, u
 // Output bytes past the last value that fits (and of a value that does not fit) are zero.
 
 // ---- E1: blob size per value -----------------------------------------------------------
-__global__ __launch_bounds__(256) void enc_size_kernel(const rr_value *__restrict__ values,
-                                                       const rr_elem *__restrict__ elems, uint64_t n,
-                                                       uint64_t ecap, uint64_t acap,
-                                                       uint64_t *__restrict__ sizes, uint64_t *__restrict__ stats,
-                                                       uint64_t *zero_words, uint32_t nzero, rr_totals *tot) {
+// Workgroup per NT values, element-parallel: a value's descriptors are "tasks" (one for a
+// STRING or a ziplist: the payload / ZLRAW descriptor; n for the others); a block scan of the
+// task counts maps task t to its value (binary search of the task bases in LDS), the tasks are
+// costed NT per round (U rounds' descriptors loaded at once), and a value's size is the
+// difference of the running task-byte scan between its first and its last task.  The cost
+// of a value is then additive in its descriptors, not the longest value of the wave.  Values
+// of at most ENC_SHORT tasks (strings, ziplists, small collections) skip the rounds: their own
+// lane costs them, as a thread-per-value pass would.
+// Sizes are serObject's (encode_size, same statuses).
+__device__ __forceinline__ ElemCost task_cost(uint32_t type, uint32_t enc, uint64_t k, const ElemV &e, uint64_t acap) {
+    switch (type) {
+        case RR_TYPE_STRING:
+            if (enc == RR_ENC_INT) return {8, 0, e.kind != RR_K_INT};
+            return {e.len, e.len, e.kind != RR_K_STR || !in_arena(e, acap)};
+        case RR_TYPE_HASH_ZIPLIST:
+        case RR_TYPE_ZSET_ZIPLIST:
+            return {e.len, e.len, e.kind != RR_K_ZLRAW || !in_arena(e, acap)};
+        default:
+            return elem_cost(type, enc, k, e, acap);
+    }
+}
+// two block-wide exclusive scans sharing one barrier (ws: [2][NT / RR_WAVE])
+template <uint32_t NT>
+__device__ __forceinline__ void block_excl_scan2(uint64_t x, uint64_t y, uint64_t (*ws)[NT / RR_WAVE], uint64_t &ex,
+                                                 uint64_t &ey, uint64_t &tx, uint64_t &ty) {
+    const uint64_t ix = wave_incl_scan(x), iy = wave_incl_scan(y);
+    const uint32_t wv = threadIdx.x / RR_WAVE;
+    if (lane_id() == RR_WAVE - 1) { ws[0][wv] = ix; ws[1][wv] = iy; }
+    lds_barrier();
+    uint64_t px = 0, py = 0, sx = 0, sy = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < NT / RR_WAVE; ++k) {
+        const uint64_t a = ws[0][k], b = ws[1][k];
+        px += k < wv ? a : 0;
+        py += k < wv ? b : 0;
+        sx += a;
+        sy += b;
+    }
+    ex = px + ix - x;
+    ey = py + iy - y;
+    tx = sx;
+    ty = sy;
+}
+
+#ifndef RR_ENC_SIZE_U   // task rounds whose descriptors are loaded together
+#define RR_ENC_SIZE_U 2
+#endif
+#ifndef RR_ENC_SHORT   // values with at most this many tasks are costed by their own lane
+#define RR_ENC_SHORT 4
+#endif
+constexpr uint32_t ENC_SHORT = RR_ENC_SHORT;
+template <uint32_t NT, uint32_t U>
+__global__ __launch_bounds__(NT) void enc_size_kernel(const rr_value *__restrict__ values,
+                                                      const rr_elem *__restrict__ elems, uint64_t n,
+                                                      uint64_t ecap, uint64_t acap,
+                                                      uint64_t *__restrict__ sizes, uint64_t *__restrict__ stats,
+                                                      uint64_t *zero_words, uint32_t nzero, rr_totals *tot) {
     zero_call_words(zero_words, nzero, tot);
-    __shared__ uint64_t red[3][4];
-    const uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    uint64_t size = 0, pay = 0, ne = 0, bad = 0;
+    __shared__ uint32_t tb[NT + 1];                  // first task of each value
+    __shared__ uint32_t s_el[NT], s_te[NT], s_bad[NT];
+    __shared__ uint64_t s_b0[NT], s_b1[NT], s_p0[NT], s_p1[NT];   // byte / payload scans at the first task, after the last
+    __shared__ uint64_t ws0[NT / RR_WAVE], ws[2][2][NT / RR_WAVE];
+    __shared__ uint64_t red[3][NT / RR_WAVE];
+    const uint32_t tid = threadIdx.x;
+    const uint64_t v = (uint64_t)blockIdx.x * NT + tid;
+    uint32_t type = 0, enc = 0, ntask = 0, hdr = 0, bad = 0;
+    uint64_t ne = 0, eb = 0;
     if (v < n) {
         const uint4 w = reinterpret_cast<const uint4 *>(values)[v];
-        uint32_t st;
+        type = w.x & 0xFF;
+        enc = (w.x >> 8) & 0xFF;
         ne = w.z;
-        size = encode_size(w.x & 0xFF, (w.x >> 8) & 0xFF, w.x >> 16, w.w, ne, elems, ecap, acap, st, pay);
-        bad = st != RR_OK;
+        eb = w.w;
+        bad = 1;
+        if ((w.x >> 16) == RR_OK && eb + ne <= ecap) {
+            switch (type) {
+                case RR_TYPE_STRING:
+                    if (ne == 1 && (enc == RR_ENC_INT || enc == RR_ENC_RAW || enc == RR_ENC_EMBSTR)) { bad = 0; hdr = 6; ntask = 1; }
+                    break;
+                case RR_TYPE_HASH_ZIPLIST:
+                case RR_TYPE_ZSET_ZIPLIST:
+                    if (ne >= 1) { bad = 0; hdr = 13; ntask = 1; }
+                    break;
+                case RR_TYPE_SET_INTSET:
+                    if (enc == 2 || enc == 4 || enc == 8) { bad = 0; hdr = 13; ntask = (uint32_t)ne; }
+                    break;
+                case RR_TYPE_LIST_QUICKLIST: bad = 0; hdr = 5; ntask = (uint32_t)ne; break;
+                case RR_TYPE_SET_HT: bad = 0; hdr = 13; ntask = (uint32_t)ne; break;
+                case RR_TYPE_HASH_HT:
+                case RR_TYPE_ZSET_SKIPLIST:
+                    if (!(ne & 1)) { bad = 0; hdr = 13; ntask = (uint32_t)ne; }
+                    break;
+                default: break;
+            }
+        }
+    }
+    // a short value is costed here, by its own lane (its loads in flight under the scan)
+    uint64_t sh_b = 0, sh_p = 0;
+    if (ntask <= ENC_SHORT) {
+        ElemV e[ENC_SHORT];
+#pragma unroll
+        for (uint32_t k = 0; k < ENC_SHORT; ++k) e[k] = k < ntask ? get_elem(elems + eb + k) : ElemV{0, 0, 0};
+#pragma unroll
+        for (uint32_t k = 0; k < ENC_SHORT; ++k) {
+            if (k < ntask) {
+                const ElemCost c = task_cost(type, enc, k, e[k], acap);
+                sh_b += c.bytes;
+                sh_p += c.pay;
+                bad |= c.bad ? 1u : 0u;
+            }
+        }
+        ntask = 0;
+    }
+    s_el[tid] = (uint32_t)eb;
+    s_te[tid] = type | (enc << 8);
+    s_bad[tid] = bad;
+    s_b0[tid] = s_p0[tid] = 0;
+    s_b1[tid] = sh_b;
+    s_p1[tid] = sh_p;
+    uint64_t TT;
+    const uint32_t base = (uint32_t)block_excl_scan<NT>(ntask, ws0, TT);
+    tb[tid] = base;
+    if (tid == NT - 1) tb[NT] = base + ntask;
+    lds_barrier();
+    auto fetch = [&](uint64_t t, uint32_t &pj, ElemV &pe) {
+        pj = 0;
+        pe = ElemV{0, 0, 0};
+        if (t < TT) {
+            uint32_t lo = 0;
+#pragma unroll
+            for (uint32_t s = NT / 2; s > 0; s >>= 1)
+                if (tb[lo + s] <= t) lo += s;
+            pj = lo;
+            pe = get_elem(elems + s_el[lo] + (uint32_t)(t - tb[lo]));
+        }
+    };
+    uint64_t runb = 0, runp = 0;
+    uint32_t par = 0;
+    for (uint64_t g0 = 0; g0 < TT; g0 += U * NT) {
+        uint32_t j[U];
+        ElemV e[U];
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) fetch(g0 + u * NT + tid, j[u], e[u]);
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) {
+            if (g0 + u * NT >= TT) break;
+            const uint64_t t = g0 + u * NT + tid;
+            const bool act = t < TT;
+            ElemCost c{0, 0, false};
+            uint32_t k = 0;
+            if (act) {
+                k = (uint32_t)(t - tb[j[u]]);
+                const uint32_t te = s_te[j[u]];
+                c = task_cost(te & 0xFF, te >> 8, k, e[u], acap);
+            }
+            uint64_t exb, exp, tb_, tp_;
+            block_excl_scan2<NT>(c.bytes, c.pay, ws[par], exb, exp, tb_, tp_);
+            par ^= 1;
+            if (act) {
+                if (k == 0) { s_b0[j[u]] = runb + exb; s_p0[j[u]] = runp + exp; }
+                if (t + 1 == tb[j[u] + 1]) { s_b1[j[u]] = runb + exb + c.bytes; s_p1[j[u]] = runp + exp + c.pay; }
+                if (c.bad) s_bad[j[u]] = 1;
+            }
+            runb += tb_;
+            runp += tp_;
+        }
+    }
+    lds_barrier();
+    uint64_t size = 0, pay = 0;
+    if (v < n) {
+        bad = s_bad[tid];
+        size = bad ? 0 : hdr + (s_b1[tid] - s_b0[tid]);
+        pay = bad ? 0 : s_p1[tid] - s_p0[tid];
         sizes[v] = size;
     }
-    bad = wave_sum(bad);
-    pay = wave_sum(pay);
-    ne = wave_sum(ne);
-    const uint32_t wv = threadIdx.x / RR_WAVE;
-    if (lane_id() == 0) { red[0][wv] = bad; red[1][wv] = pay; red[2][wv] = ne; }
+    uint64_t sb = wave_sum(bad), sp = wave_sum(pay), sn = wave_sum(ne);
+    const uint32_t wv = tid / RR_WAVE;
+    if (lane_id() == 0) { red[0][wv] = sb; red[1][wv] = sp; red[2][wv] = sn; }
     __syncthreads();
-    if (threadIdx.x < 3) {
-        uint64_t s = 0;
-        for (uint32_t k = 0; k < blockDim.x / RR_WAVE; ++k) s += red[threadIdx.x][k];
-        stats[3 * (uint64_t)blockIdx.x + threadIdx.x] = s;
+    if (tid < 3) {
+        uint64_t sum = 0;
+        for (uint32_t k = 0; k < NT / RR_WAVE; ++k) sum += red[tid][k];
+        stats[3 * (uint64_t)blockIdx.x + tid] = sum;
     }
 }
 
@@ -2223,7 +2377,7 @@ extern "C" hipError_t rr_launch_encode(const rr_value *values, const rr_elem *el
     uint64_t *err = lb + lb_words;   // device error word (look-back timeout)
     uint64_t *stats = err + 1;
     uint32_t *fv = reinterpret_cast<uint32_t *>(stats + 6 * (uint64_t)t);
-    hipLaunchKernelGGL(enc_size_kernel, dim3(t), dim3(256), 0, stream, values, elems, n, elem_cap, arena_cap, offsets,
+    hipLaunchKernelGGL((enc_size_kernel<256, RR_ENC_SIZE_U>), dim3(t), dim3(256), 0, stream, values, elems, n, elem_cap, arena_cap, offsets,
                        stats, lb, (uint32_t)(lb_words + 1), totals);
     hipLaunchKernelGGL(scan_kernel, dim3(st), dim3(256), 0, stream, offsets, n, lb, st, err);
     hipLaunchKernelGGL(enc_index_kernel<ENC_W>, dim3(t), dim3(256), 0, stream, values, elems, n, elem_cap, arena_cap,
