@@ -1933,6 +1933,21 @@ __device__ __forceinline__ void lds_put(uint8_t *img, uint32_t d, uint64_t v, ui
     if (r & 1) img[d] = (uint8_t)v;
 }
 
+// x < 10^8 as 8 ASCII digits, the most significant in byte 0: 4-digit halves, 2-digit pairs,
+// digits (exact reciprocal multiplies for these ranges)
+__device__ __forceinline__ uint64_t swar8(uint32_t x) {
+    const uint32_t hi = x / 10000u, lo = x - hi * 10000u;
+    auto two = [](uint32_t p) {   // p < 100 -> tens | units << 8
+        const uint32_t t = (p * 103u) >> 10;
+        return t | ((p - t * 10u) << 8);
+    };
+    auto four = [&](uint32_t h) {   // h < 10^4 -> 4 digits
+        const uint32_t a = (h * 5243u) >> 19;
+        return two(a) | (two(h - a * 100u) << 16);
+    };
+    return ((uint64_t)four(hi) | ((uint64_t)four(lo) << 32)) + 0x3030303030303030ull;
+}
+
 // The window image: writes at absolute output positions, clipped to [w0, w0 + span).
 struct Img {
     uint8_t *img;
@@ -1949,31 +1964,29 @@ struct Img {
         else
             for (uint32_t i = 0; i < nb; ++i) put(pos + i, (uint32_t)(v >> (8 * i)) & 0xFF);
     }
-    // sdsll2str(x) (sds.c:450-479), l characters at pos: the characters are shifted into a
-    // 24-byte register string (last digit first, so the first character ends in byte 0),
-    // then stored as up to three fields
+    // sdsll2str(x) (sds.c:450-479), l characters at pos: |x| as three 8-digit chunks, each
+    // turned into 8 ASCII digits at once (SWAR), the 24-character string shifted right past
+    // its leading zeros (first character in byte 0), the sign prepended, then stored as up to
+    // three fields
     __device__ __forceinline__ void decimal(uint64_t pos, int64_t x, uint32_t l) const {
-        uint64_t u = x < 0 ? 0ull - (uint64_t)x : (uint64_t)x;
-        uint64_t a0 = 0, a1 = 0, a2 = 0;
-        auto push = [&](uint32_t c) {
+        const uint64_t u = x < 0 ? 0ull - (uint64_t)x : (uint64_t)x;
+        const uint64_t q = u / 100000000ull, q2 = q / 100000000ull;
+        uint64_t w[3] = {swar8((uint32_t)q2), swar8((uint32_t)(q - q2 * 100000000ull)),
+                         swar8((uint32_t)(u - q * 100000000ull))};
+        const uint32_t neg = x < 0 ? 1u : 0u, zb = 8u * (24u - (l - neg)), ws = zb >> 6, bs = zb & 63;
+        auto word = [&](uint32_t i) { return i == 0 ? w[0] : i == 1 ? w[1] : i == 2 ? w[2] : 0ull; };
+        auto shr = [&](uint32_t i) {
+            const uint64_t lo = word(ws + i), hi = word(ws + i + 1);
+            return bs ? (lo >> bs) | (hi << (64 - bs)) : lo;
+        };
+        uint64_t a0 = shr(0), a1 = shr(1), a2 = shr(2);
+        if (neg) {
             a2 = (a2 << 8) | (a1 >> 56);
             a1 = (a1 << 8) | (a0 >> 56);
-            a0 = (a0 << 8) | c;
-        };
-        // base-1e9 chunks, then 32-bit digit steps
-        const uint64_t t = u / 1000000000ull;
-        uint32_t c[3] = {(uint32_t)(u - t * 1000000000ull), (uint32_t)(t % 1000000000ull), (uint32_t)(t / 1000000000ull)};
-        const uint32_t nd = l - (x < 0 ? 1u : 0u);
-        uint32_t cur = c[0];
-        for (uint32_t k = 0; k < nd; ++k) {
-            if (k == 9) cur = c[1];
-            if (k == 18) cur = c[2];
-            push('0' + cur % 10);
-            cur /= 10;
+            a0 = (a0 << 8) | '-';
         }
-        if (x < 0) push('-');
-        for (uint32_t w = 0; 8 * w < l; ++w)
-            field(pos + 8 * w, w == 0 ? a0 : w == 1 ? a1 : a2, l - 8 * w < 8 ? l - 8 * w : 8);
+        for (uint32_t k = 0; 8 * k < l; ++k)
+            field(pos + 8 * k, k == 0 ? a0 : k == 1 ? a1 : a2, l - 8 * k < 8 ? l - 8 * k : 8);
     }
 };
 
