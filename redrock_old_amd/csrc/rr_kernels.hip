@@ -613,7 +613,10 @@ __global__ __launch_bounds__(256) void count_kernel(const uint8_t *__restrict__ 
 // ---- K2: exclusive scan of the reservations -> elem_base -------------------------------
 // 4096 values per 256-thread workgroup, tile ids from an atomic ticket (so a tile only waits
 // on tiles already running), decoupled look-back between tiles (two-level, rr_device.h).
-constexpr uint32_t SCAN_PER_THREAD = 16;
+#ifndef RR_SCAN_PT
+#define RR_SCAN_PT 16
+#endif
+constexpr uint32_t SCAN_PER_THREAD = RR_SCAN_PT;
 constexpr uint32_t SCAN_TILE = 256 * SCAN_PER_THREAD;
 
 __global__ __launch_bounds__(256) void scan_kernel(uint64_t *__restrict__ counts, uint64_t n, uint64_t *lb,
