@@ -65,6 +65,13 @@ void rr_ctx_destroy(rr_ctx *c) {
     dfree(&c->d_elems, &c->c_elems); dfree(&c->d_arena, &c->c_arena); dfree(&c->d_out, &c->c_out);
     dfree(&c->d_ooff, &c->c_ooff);
     if (c->d_totals) hipFree(c->d_totals);
+    if (c->pipe_ready) {
+        for (int k = 0; k < RR_HOST_MAXCHUNK; k++) { hipEventDestroy(c->ev_up[k]); hipEventDestroy(c->ev_dec[k]); }
+        hipStreamDestroy(c->up);
+        hipStreamDestroy(c->down);
+        hipFree(c->d_ktot);
+        hipHostFree(c->h_ktot);
+    }
     hipEventDestroy(c->scratch_done);
     hipStreamDestroy(c->stream);
     free(c);
@@ -162,6 +169,102 @@ int rr_dgrow(void **p, size_t *cap, size_t need) {
 }
 #define GROW(P, C, N) do { int r_ = dgrow((void **)&(P), &(C), (N)); if (r_) return r_; } while (0)
 
+/* ---- pipelined host decode -------------------------------------------------------------
+ * A batch of more than one RR_HOST_CHUNK goes in chunks of whole values (at most
+ * RR_HOST_MAXCHUNK): every chunk's blob bytes and offsets are queued up at once on the `up`
+ * stream; chunk k decodes on the context stream once its bytes are in (its descriptors placed
+ * after the earlier chunks', its elem_base rebased on the device), and its records, descriptors
+ * and arena slice go down on the `down` stream while later chunks are still going up.  With
+ * pinned host buffers (hipHostMalloc / hipHostRegister) the two PCIe directions overlap;
+ * pageable buffers still work, staged by the runtime.  The device layout is the whole batch's
+ * (offsets, arena mirror and data_cap are global), so a chunk's decode is the whole-batch decode
+ * restricted to its values: results are identical to the one-call path. */
+static int pipe_init(rr_ctx *c) {
+    if (c->pipe_ready) return RR_API_OK;
+    HIPCHK(hipStreamCreateWithFlags(&c->up, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&c->down, hipStreamNonBlocking));
+    for (int k = 0; k < RR_HOST_MAXCHUNK; k++) {
+        HIPCHK(hipEventCreateWithFlags(&c->ev_up[k], hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&c->ev_dec[k], hipEventDisableTiming));
+    }
+    HIPCHK(hipMalloc((void **)&c->d_ktot, RR_HOST_MAXCHUNK * sizeof(rr_totals)));
+    HIPCHK(hipHostMalloc((void **)&c->h_ktot, RR_HOST_MAXCHUNK * sizeof(rr_totals), hipHostMallocDefault));
+    c->pipe_ready = 1;
+    return RR_API_OK;
+}
+
+/* chunk cuts: cut[k] = first value whose first byte is at or after k * bytes / K */
+static int plan_chunks(const uint64_t *offsets, uint64_t n, uint64_t bytes, uint64_t *cut) {
+    uint64_t K = (bytes + RR_HOST_CHUNK - 1) / RR_HOST_CHUNK;
+    if (K > RR_HOST_MAXCHUNK) K = RR_HOST_MAXCHUNK;
+    int m = 0;
+    cut[m++] = 0;
+    for (uint64_t k = 1; k < K; k++) {
+        const uint64_t target = bytes / K * k;
+        uint64_t lo = cut[m - 1], hi = n;   /* first v in [lo, n] with offsets[v] >= target */
+        while (lo < hi) {
+            const uint64_t mid = lo + (hi - lo) / 2;
+            if (offsets[mid] >= target) hi = mid; else lo = mid + 1;
+        }
+        if (lo > cut[m - 1] && lo < n) cut[m++] = lo;
+    }
+    cut[m] = n;
+    return m;   /* chunks */
+}
+
+static int decode_host_pipelined(rr_ctx *c, const uint8_t *data, const uint64_t *offsets, uint64_t n,
+                                 rr_value *values, rr_elem *elems, uint64_t elem_cap, uint8_t *arena,
+                                 rr_totals *totals, uint64_t bytes, size_t pbytes, const uint64_t *cut, int K) {
+    int rc = pipe_init(c);
+    if (rc) return rc;
+    uint8_t *d_in = (uint8_t *)c->d_in, *d_arena = (uint8_t *)c->d_arena;
+    uint64_t *d_off = (uint64_t *)c->d_off;
+    rr_value *d_vals = (rr_value *)c->d_vals;
+    rr_elem *d_elems = (rr_elem *)c->d_elems;
+    /* the stream of the previous host call is done with the staging buffers: wait for it */
+    HIPCHK(hipEventRecord(c->ev_dec[0], c->stream));
+    HIPCHK(hipStreamWaitEvent(c->up, c->ev_dec[0], 0));
+    HIPCHK(hipMemsetAsync(d_in + bytes, 0, pbytes + 16 - bytes, c->up));
+    HIPCHK(hipMemsetAsync(d_arena + bytes, 0, pbytes + 16 - bytes, c->up));
+    for (int k = 0; k < K; k++) {
+        const uint64_t v0 = cut[k], v1 = cut[k + 1], b0 = offsets[v0], b1 = offsets[v1];
+        if (b1 > b0) HIPCHK(hipMemcpyAsync(d_in + b0, data + b0, b1 - b0, hipMemcpyHostToDevice, c->up));
+        HIPCHK(hipMemcpyAsync(d_off + v0, offsets + v0, (v1 - v0 + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, c->up));
+        HIPCHK(hipEventRecord(c->ev_up[k], c->up));
+    }
+    rr_totals sum = {0, 0, 0, 0};
+    uint64_t E = 0;   /* descriptor slots of the earlier chunks */
+    for (int k = 0; k < K; k++) {
+        const uint64_t v0 = cut[k], v1 = cut[k + 1], nk = v1 - v0, b0 = offsets[v0], b1 = offsets[v1];
+        HIPCHK(hipStreamWaitEvent(c->stream, c->ev_up[k], 0));
+        rr_blob_batch in = {d_in, d_off + v0, nk, pbytes};
+        const uint64_t ek = E < elem_cap ? E : elem_cap;   /* (past elem_cap: nothing is written) */
+        rr_flat_batch out = {d_vals + v0, d_elems + ek, d_arena, nk, elem_cap - ek, pbytes};
+        rc = rr_decode_batch(c, &in, &out, c->d_ktot + k, c->stream);
+        if (rc) return rc;
+        HIPCHK(rr_launch_flat_rebase(d_vals + v0, nk, NULL, 0, E, 0, c->stream));
+        HIPCHK(hipMemcpyAsync(&c->h_ktot[k], c->d_ktot + k, sizeof(rr_totals), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipEventRecord(c->ev_dec[k], c->stream));
+        HIPCHK(hipEventSynchronize(c->ev_dec[k]));   /* (later chunks keep going up meanwhile) */
+        const rr_totals t = c->h_ktot[k];
+        if (t.bytes == ~0ull) return fail(RR_API_EDEVICE, "decode: device-side failure (look-back timeout)");
+        HIPCHK(hipStreamWaitEvent(c->down, c->ev_dec[k], 0));
+        HIPCHK(hipMemcpyAsync(values + v0, d_vals + v0, nk * sizeof(rr_value), hipMemcpyDeviceToHost, c->down));
+        const uint64_t ne = E >= elem_cap ? 0 : t.n_elems < elem_cap - E ? t.n_elems : elem_cap - E;
+        if (ne && elems) HIPCHK(hipMemcpyAsync(elems + E, d_elems + E, ne * sizeof(rr_elem), hipMemcpyDeviceToHost, c->down));
+        if (b1 > b0 && arena) HIPCHK(hipMemcpyAsync(arena + b0, d_arena + b0, b1 - b0, hipMemcpyDeviceToHost, c->down));
+        E += t.n_elems;
+        sum.n_elems += t.n_elems;
+        sum.bytes = t.bytes;   /* (the offsets are the whole batch's: a chunk reports its end) */
+        sum.n_bad += t.n_bad;
+        sum.payload += t.payload;
+    }
+    HIPCHK(hipStreamSynchronize(c->down));
+    if (E > elem_cap) return 1;   /* the batch overflows elem_cap: the caller redoes it in one call */
+    if (totals) *totals = sum;
+    return RR_API_OK;
+}
+
 int rr_decode_batch_host(rr_ctx *c, const uint8_t *data, const uint64_t *offsets, uint64_t n, rr_value *values,
                          rr_elem *elems, uint64_t elem_cap, uint8_t *arena, rr_totals *totals) {
     if (!c || !offsets || (n && (!data || !values))) return fail(RR_API_EINVAL, "NULL argument");
@@ -174,6 +277,18 @@ int rr_decode_batch_host(rr_ctx *c, const uint8_t *data, const uint64_t *offsets
     GROW(c->d_vals, c->c_vals, (n ? n : 1) * sizeof(rr_value));
     GROW(c->d_elems, c->c_elems, (elem_cap ? elem_cap : 1) * sizeof(rr_elem));
     GROW(c->d_arena, c->c_arena, pbytes + 16);
+    /* chunked when the batch is big enough.  While the descriptors fit elem_cap a chunk's
+     * capacity check is the whole batch's; a batch that overflows it (the pipelined pass
+     * returns 1) is decoded again in one call, so capacity statuses match it exactly. */
+    if (bytes > RR_HOST_CHUNK) {
+        uint64_t cut[RR_HOST_MAXCHUNK + 1];
+        const int K = plan_chunks(offsets, n, bytes, cut);
+        if (K > 1) {
+            const int rc = decode_host_pipelined(c, data, offsets, n, values, elems, elem_cap, arena, totals, bytes,
+                                                 pbytes, cut, K);
+            if (rc != 1) return rc;
+        }
+    }
     HIPCHK(hipMemsetAsync(c->d_in, 0, pbytes + 16, c->stream));
     if (bytes) HIPCHK(hipMemcpyAsync(c->d_in, data, bytes, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(c->d_off, offsets, (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));

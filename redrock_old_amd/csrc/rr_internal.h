@@ -4,6 +4,9 @@
 
 #include "rr_kernels.h"
 
+#define RR_HOST_CHUNK (16ull << 20)   /* pipelined host decode: bytes per chunk (at least) */
+#define RR_HOST_MAXCHUNK 64
+
 struct rr_ctx {
     int device;
     hipStream_t stream;          /* used by the host entry points */
@@ -15,6 +18,11 @@ struct rr_ctx {
     void *d_in, *d_off, *d_vals, *d_elems, *d_arena, *d_out, *d_ooff;
     size_t c_in, c_off, c_vals, c_elems, c_arena, c_out, c_ooff;
     rr_totals *d_totals;
+    /* pipelined host decode (rr_api.c): transfer streams, per-chunk events and totals */
+    int pipe_ready;
+    hipStream_t up, down;
+    hipEvent_t ev_up[RR_HOST_MAXCHUNK], ev_dec[RR_HOST_MAXCHUNK];
+    rr_totals *d_ktot, *h_ktot;   /* device / pinned host, RR_HOST_MAXCHUNK each */
 };
 
 /* the context's scratch: grow to `words` (waits on the previous call through an event; fails

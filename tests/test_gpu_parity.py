@@ -408,3 +408,93 @@ def test_fuzz_structured_decode_and_reencode(engine, cfg, n):
     gd, go, gt = engine.encode_host(v, e, a)
     od, oo, otot = cpu.encode(ov, oe, oa)
     assert np.array_equal(go, oo) and np.array_equal(gd, od[:int(oo[-1])]) and gt == otot
+
+
+def _device_decode(data, offs, cap=None):
+    import torch
+    n, nb = len(offs) - 1, int(offs[-1])
+    dev = torch.device("cuda:0")
+    d_data = torch.zeros((nb + 15) & ~15 or 16, dtype=torch.uint8, device=dev)
+    d_data[:nb] = torch.from_numpy(data[:nb]).to(dev)
+    d_offs = torch.from_numpy(offs.view(np.int64)).to(dev)
+    cap = rr.elem_bound(n, nb) if cap is None else cap
+    d_vals = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
+    d_elems = torch.zeros(max(cap, 1) * 16, dtype=torch.uint8, device=dev)
+    d_arena = torch.zeros(d_data.numel(), dtype=torch.uint8, device=dev)
+    d_tot = torch.zeros(4, dtype=torch.int64, device=dev)
+    eng = rr.Engine(0)
+    eng.decode_device(d_data, d_offs, d_vals, d_elems, d_arena, d_tot)
+    torch.cuda.synchronize()
+    tot = d_tot.cpu().numpy().view(np.uint64).copy()
+    eng.close()
+    return (d_vals.cpu().numpy().view(rr.VALUE_DT), d_elems.cpu().numpy().view(rr.ELEM_DT)[:min(int(tot[0]), cap)],
+            d_arena.cpu().numpy()[:nb], tot)
+
+
+def _payload_equal(e, a, b):
+    """the arena bytes every STR / ZLRAW descriptor points at"""
+    k = (e["kind"] == 1) | (e["kind"] == 3)
+    for d, ln in zip(e["data"][k].astype(np.int64), e["len"][k].astype(np.int64)):
+        if not np.array_equal(a[d:d + ln], b[d:d + ln]):
+            return False
+    return True
+
+
+@pytest.mark.parametrize("cfg,n", [(4, 1_000_000), (3, 200_000), (10, 8_000)])
+def test_host_decode_pipelined_matches_device(engine, cfg, n):
+    """rr_decode_batch_host on a batch of more than RR_HOST_CHUNK bytes runs chunked (uploads,
+    per-chunk decodes with descriptor placement and elem_base rebase, downloads on a second
+    stream): records, descriptors, totals and every payload equal one whole-batch device
+    decode.  Config 10 carries malformed values (statuses and zero-filled slots)."""
+    data, offs = rr.gen_batch(cfg, n)
+    nb = int(offs[-1])
+    assert nb > 16 << 20, "the batch must take the chunked path"
+    v, e, a, tot = _device_decode(data, offs)
+    hv, he, ha, ht = engine.decode_host(data, offs)
+    assert_flat_equal((v, e), (hv, he), f"cfg {cfg} pipelined host decode")
+    assert (int(tot[0]), int(tot[1]), int(tot[2]), int(tot[3])) == (ht["n_elems"], ht["bytes"], ht["n_bad"], ht["payload"])
+    assert _payload_equal(e, a, ha)
+
+
+def test_host_decode_pipelined_pinned_buffers(engine):
+    """The same path with pinned host buffers (the overlap case) and a reused context: two
+    calls of different batches through one engine give each batch's device decode."""
+    import ctypes as C
+    import torch
+    L = rr.lib()
+    for cfg, n in [(2, 150_000), (4, 300_000)]:
+        data, offs = rr.gen_batch(cfg, n)
+        nb = int(offs[-1])
+        cap = rr.elem_bound(n, nb)
+        h_data = torch.from_numpy(data).pin_memory()
+        h_offs = torch.from_numpy(offs.view(np.int64)).pin_memory()
+        h_vals = torch.zeros(n * 16, dtype=torch.uint8).pin_memory()
+        h_elems = torch.zeros(cap * 16, dtype=torch.uint8).pin_memory()
+        h_arena = torch.zeros(nb, dtype=torch.uint8).pin_memory()
+        t = rr.Totals()
+        rc = L.rr_decode_batch_host(engine._ctx, h_data.data_ptr(), h_offs.data_ptr(), n, h_vals.data_ptr(),
+                                    h_elems.data_ptr(), cap, h_arena.data_ptr(), C.byref(t))
+        assert rc == 0, rr.lib().rr_last_error()
+        v, e, a, tot = _device_decode(data, offs)
+        hv = h_vals.numpy().view(rr.VALUE_DT)
+        he = h_elems.numpy().view(rr.ELEM_DT)[:int(t.n_elems)]
+        assert_flat_equal((v, e), (hv, he), f"cfg {cfg} pinned")
+        assert int(t.n_elems) == int(tot[0]) and int(t.payload) == int(tot[3])
+        assert _payload_equal(e, a, h_arena.numpy())
+
+
+def test_host_decode_pipelined_capacity(engine):
+    """A chunked host decode whose descriptors overflow elem_cap is redone in one call: the
+    capacity statuses, records and descriptors equal a whole-batch device decode with the same
+    elem_cap."""
+    data, offs = rr.gen_batch(4, 200_000)
+    _, _, _, full = _device_decode(data, offs)
+    cap = int(full[0]) * 3 // 5
+    v, e, a, tot = _device_decode(data, offs, cap)
+    hv, he, ha, ht = engine.decode_host(data, offs, elem_cap=cap)
+    # descriptors of the values that fit (the slots below elem_cap of the value that crosses it
+    # belong to no value and are not written)
+    ok = v["status"] == 0
+    end = int((v["elem_base"][ok].astype(np.int64) + v["n_elems"][ok]).max())
+    assert_flat_equal((v, e[:end]), (hv, he[:end]), "pipelined capacity")
+    assert ht["n_bad"] == int(tot[2]) > 0
