@@ -103,7 +103,9 @@ uint64_t rr_decode_elem_bound(uint64_t n, uint64_t bytes);
 /* A batch of more than 16 MiB of blobs is decoded in chunks of whole values whose uploads,
  * decodes and downloads overlap on separate streams (results identical to one call); with
  * pinned host buffers (hipHostMalloc / hipHostRegister) the two PCIe directions then run at
- * once.  A batch whose descriptors overflow elem_cap is decoded again in one call. */
+ * once.  A batch whose descriptors overflow elem_cap is decoded again in one call.
+ * arena may be NULL: the arena is a byte-for-byte mirror of `data` (rr_format.h), so a caller
+ * that keeps `data` can index it with the descriptors and skip the arena's download. */
 int rr_decode_batch_host(rr_ctx *ctx, const uint8_t *data, const uint64_t *offsets, uint64_t n,
                          rr_value *values, rr_elem *elems, uint64_t elem_cap,
                          uint8_t *arena, rr_totals *totals);

@@ -915,6 +915,10 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
     }
     const bool staged = S1 - S0 <= STAGE;
     const uint64_t cap = elem_cap < 0xFFFFFFFFull ? elem_cap : 0xFFFFFFFFull;   // elem_base is 32-bit
+    // the arena copy starts at the call's first value (a call over a slice of a larger buffer —
+    // the chunks of rr_decode_batch_host — copies only its own bytes); the stage always lies
+    // past it (S0 >= offsets[v_lo] >= offsets[0])
+    const uint64_t A0 = W0 > (offsets[0] & ~15ull) ? W0 : (offsets[0] & ~15ull);
 
     // the first chunk's class bytes, loaded before the copy so their latency hides under it
     uint32_t cls0[PMAX / NT];
@@ -973,7 +977,7 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
         const u32x4 *src = reinterpret_cast<const u32x4 *>(blob);
 #pragma unroll
         for (int k = 0; k < RR_DEC_OVL_K; ++k) {
-            const uint64_t g = (W0 >> 4) + tid + (uint64_t)k * NT;
+            const uint64_t g = (A0 >> 4) + tid + (uint64_t)k * NT;
             ov_x[k] = g < ov_e ? src[g] : u32x4{0u, 0u, 0u, 0u};
         }
     }
@@ -983,14 +987,14 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
         u32x4 *lds = reinterpret_cast<u32x4 *>(stage);
 #pragma unroll
         for (int k = 0; k < RR_DEC_OVL_K; ++k) {
-            const uint64_t g = (W0 >> 4) + tid + (uint64_t)k * NT;
+            const uint64_t g = (A0 >> 4) + tid + (uint64_t)k * NT;
 #ifndef RR_ABLATE_NOCOPY
             if (g < ov_w1) __builtin_nontemporal_store(ov_x[k], dst + g);
 #endif
             if (staged && g >= ov_s0 && g < ov_e) lds[g - ov_s0] = ov_x[k];
         }
         // the rest of the window (beyond the prefetched granules), loaded now
-        uint64_t c = (W0 >> 4) + tid + (uint64_t)RR_DEC_OVL_K * NT;
+        uint64_t c = (A0 >> 4) + tid + (uint64_t)RR_DEC_OVL_K * NT;
         for (; c + 3 * NT < ov_e; c += 4 * NT) {
             u32x4 x[4];
 #pragma unroll
@@ -1040,7 +1044,7 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
         u32x4 *lds = reinterpret_cast<u32x4 *>(stage);
         const uint64_t cw1 = W1 >> 4, cs0 = S0 >> 4;
         const uint64_t ce = (staged && S1 > W1 ? S1 : W1) >> 4;
-        uint64_t c = (W0 >> 4) + tid;
+        uint64_t c = (A0 >> 4) + tid;
         for (; c + 3 * NT < ce; c += 4 * NT) {
             u32x4 x[4];
 #pragma unroll

@@ -498,3 +498,23 @@ def test_host_decode_pipelined_capacity(engine):
     end = int((v["elem_base"][ok].astype(np.int64) + v["n_elems"][ok]).max())
     assert_flat_equal((v, e[:end]), (hv, he[:end]), "pipelined capacity")
     assert ht["n_bad"] == int(tot[2]) > 0
+
+
+def test_host_decode_without_arena(engine):
+    """arena = NULL skips the arena's download (the caller's blob buffer is the mirror): the
+    records and descriptors are those of the full call, and every STR / ZLRAW descriptor
+    indexes the caller's own blob bytes."""
+    import ctypes as C
+    L = rr.lib()
+    data, offs = rr.gen_batch(4, 120_000)   # > 16 MiB: the chunked path
+    n, nb = len(offs) - 1, int(offs[-1])
+    cap = rr.elem_bound(n, nb)
+    hv, he, ha, ht = engine.decode_host(data, offs)
+    vals = np.zeros(n, rr.VALUE_DT)
+    els = np.zeros(cap, rr.ELEM_DT)
+    t = rr.Totals()
+    rc = L.rr_decode_batch_host(engine._ctx, data.ctypes.data, offs.ctypes.data, n, vals.ctypes.data,
+                                els.ctypes.data, cap, None, C.byref(t))
+    assert rc == 0
+    assert_flat_equal((vals, els[:int(t.n_elems)]), (hv, he), "arena = NULL")
+    assert _payload_equal(he, ha, data)
