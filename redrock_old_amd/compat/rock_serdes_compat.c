@@ -152,16 +152,16 @@ void rr_compat_des_batch(void *const *bufs, const size_t *lens, size_t n, robj *
     const uint64_t cap = rr_decode_elem_bound(n, bytes);
     rr_value *vals = zmalloc(sizeof(rr_value) * n);
     rr_elem *els = zmalloc(sizeof(rr_elem) * (cap ? cap : 1));
-    uint8_t *arena = zmalloc(padded ? padded : 16);
     rr_totals t;
-    if (rr_decode_batch_host(engine(), data, offs, n, vals, els, cap, arena, &t) != RR_API_OK)
+    /* no arena download: it would mirror `data` byte for byte, so the descriptors index it */
+    if (rr_decode_batch_host(engine(), data, offs, n, vals, els, cap, NULL, &t) != RR_API_OK)
         serverPanic("desObject: %s", rr_last_error());
     for (size_t i = 0; i < n; i++) {
         if (vals[i].status != RR_OK)   /* the reference's serverAssert / serverPanic site */
             serverPanic("desObject: bad blob (%s, status %u)", status_name(vals[i].status), vals[i].status);
-        out[i] = robj_from_flat(&vals[i], els + vals[i].elem_base, arena);
+        out[i] = robj_from_flat(&vals[i], els + vals[i].elem_base, data);
     }
-    zfree(offs); zfree(data); zfree(vals); zfree(els); zfree(arena);
+    zfree(offs); zfree(data); zfree(vals); zfree(els);
 }
 
 void rr_compat_rdb_load_batch(int fd_req, int fd_resp, int dbid, sds *keys, size_t k, robj **out) {
