@@ -450,6 +450,15 @@ def cpu_baseline(data, offs, nb, budget_s):
     # flat restatement (same output as the GPU) on 1 thread, 16 threads (the box's CPU share per
     # GPU) and every core this process may run on (capped at 128 threads)
     allc = min(len(os.sched_getaffinity(0)), 128)
+    quota = None   # the job's CPU quota (cgroup v2 cpu.max), which bounds any thread count
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            quota = round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    out["cpu_quota_cores"] = quota
     flat = {}
     for thr in sorted({1, min(16, allc), allc}):
         ts = []

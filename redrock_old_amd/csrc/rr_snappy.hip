@@ -31,8 +31,19 @@ constexpr uint32_t FRAG = 1u << 16;        // snappy kBlockSize (snappy.h:197-19
 constexpr uint32_t TAB_MIN = 1u << 8;      // kMinHashTableSize
 constexpr uint32_t TAB_MAX = 1u << 14;     // kMaxHashTableSize
 constexpr uint32_t MARGIN = 15;            // kInputMarginBytes
-constexpr uint32_t SNZ_DEC_WIN = 32768;     // LDS output window per wave (RocksDB blocks: 16 KiB)
-constexpr uint32_t SNZ_FRAG_LDS = 16384 + 64;   // staged fragment bytes per wave
+// LDS output window per wave: RocksDB blocks are cut at ~16 KiB (block_size, rocksdbapi.cc:77)
+// plus at most one entry; 20 KiB holds those with 7 waves per CU (32 KiB: 4 waves, half the
+// throughput), and a longer block decompresses straight into global memory
+#ifndef RR_SNZ_DEC_WIN
+#define RR_SNZ_DEC_WIN 20480
+#endif
+constexpr uint32_t SNZ_DEC_WIN = RR_SNZ_DEC_WIN;
+// staged fragment bytes per wave; 0 (default): the compressor reads its input in place through
+// the buffer resource, so a wave holds only the 32 KiB hash table (4 waves per CU instead of 3)
+#ifndef RR_SNZ_FRAG
+#define RR_SNZ_FRAG 0
+#endif
+constexpr uint32_t SNZ_FRAG_LDS = RR_SNZ_FRAG;
 
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 // LDS pointers kept in address space 3, so accesses compile to ds_* (a generic pointer gives flat_*
