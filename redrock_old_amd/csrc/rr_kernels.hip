@@ -2053,20 +2053,24 @@ constexpr uint64_t JQ_SRC = (1ull << 40) - 1;
 
 
 template <uint32_t W, uint32_t NT, uint32_t RCAP>
-__global__ __launch_bounds__(NT) void enc_emit_kernel(const rr_value *__restrict__ values,
+#ifndef RR_ENC_WPE   // waves per SIMD the emit kernel is built for
+#define RR_ENC_WPE 5
+#endif
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(RR_ENC_WPE))) void enc_emit_kernel(const rr_value *__restrict__ values,
                                                       const rr_elem *__restrict__ elems,
                                                       const uint8_t *__restrict__ arena, uint64_t n,
                                                       uint8_t *__restrict__ out, uint64_t cap,
                                                       const uint64_t *__restrict__ offsets,
                                                       const uint32_t *__restrict__ fv) {
     static_assert(W <= 65536 && W % 64 == 0, "image offsets are 16-bit, pieces 64-byte blocks");
+    static_assert(RCAP >= 2 && W / 64 + RCAP < 65536, "run piece bases are 16-bit");
+    constexpr uint32_t RTOP = 1u << (31 - __builtin_clz(RCAP - 1));   // largest power of two < RCAP
     __shared__ uint4 img4[W / 16];
     __shared__ uint64_t rq_a[RCAP];        // run: arena offset | length << 40
-    __shared__ uint32_t rq_d[RCAP];        // run: image offset
-    __shared__ uint32_t rq_p[RCAP + 1];    // run: first piece (pieces of earlier runs)
+    __shared__ uint32_t rq_dp[RCAP];       // run: image offset | first piece (pieces of earlier runs) << 16
     __shared__ uint32_t tb[NT + 1];        // task base of each value of the round
-    __shared__ uint64_t sv_pos[NT];        // output position of the value's first task
-    __shared__ uint64_t sv_eb[NT];         // element-byte scan at the value's first task
+    __shared__ uint64_t sv_pos[NT];        // output position of the value's first task, less the
+                                           // element-byte scan there once its first task is costed
     __shared__ uint32_t sv_el[NT];         // elem_base
     __shared__ uint32_t sv_te[NT];         // type | enc << 8
     __shared__ uint64_t wsum[2][NT / RR_WAVE];
@@ -2112,8 +2116,7 @@ __global__ __launch_bounds__(NT) void enc_emit_kernel(const rr_value *__restrict
         const uint32_t r = (uint32_t)at, p0 = (uint32_t)(at >> 32);
         if (queued && r < RCAP) {
             rq_a[r] = src | ((uint64_t)l << 40);
-            rq_d[r] = dst;
-            rq_p[r] = p0;
+            rq_dp[r] = dst | (p0 << 16);
         } else {   // queue full (rare; keeps the kernel small): byte copy
             if (queued && r == RCAP) sh_pend = p0;
             for (uint32_t i = 0; i < l; ++i) img[dst + i] = arena[src + i];
@@ -2188,13 +2191,13 @@ __global__ __launch_bounds__(NT) void enc_emit_kernel(const rr_value *__restrict
             }
             uint64_t rt;
             const uint64_t ex = run + block_excl_scan<NT>(es, wsum[1], rt);
-            if (act && k == 0) sv_eb[j] = ex;
+            if (act && k == 0) sv_pos[j] -= ex;
             lds_barrier();
             EPROBE(const uint64_t rs1 = rr_stamp(); tsc += rs1 - rs0;)
             bool pay = false;
             uint64_t ppos = 0;
             if (act) {
-                const uint64_t p = sv_pos[j] + ex - sv_eb[j];
+                const uint64_t p = sv_pos[j] + ex;
                 // one fixed field, then a decimal or a payload (single call sites keep the
                 // kernel small enough for the instruction cache)
                 uint64_t fval = e.len;
@@ -2248,17 +2251,17 @@ __global__ __launch_bounds__(NT) void enc_emit_kernel(const rr_value *__restrict
     const uint32_t nr = (uint32_t)sh_nrp < RCAP ? (uint32_t)sh_nrp : RCAP;
     const uint32_t npc = sh_pend != 0xFFFFFFFFu ? sh_pend : (uint32_t)(sh_nrp >> 32);
     auto piece = [&](uint32_t b, uint64_t &ps, uint32_t &pd, uint32_t &pl) {
-        uint32_t lo = 0;
+        uint32_t lo = 0;   // (steps from the largest power of two below RCAP: every index reachable)
 #pragma unroll
-        for (uint32_t s = RCAP / 2; s > 0; s >>= 1)
-            if (lo + s < nr && rq_p[lo + s] <= b) lo += s;
+        for (uint32_t s = RTOP; s > 0; s >>= 1)
+            if (lo + s < nr && (rq_dp[lo + s] >> 16) <= b) lo += s;
         const uint64_t a = rq_a[lo];
-        const uint32_t dst = rq_d[lo], l = (uint32_t)(a >> 40), k = b - rq_p[lo];
+        const uint32_t dp = rq_dp[lo], dst = dp & 0xFFFF, l = (uint32_t)(a >> 40), k = b - (dp >> 16);
         const uint32_t d0 = k == 0 ? dst : ((dst >> 6) + k) << 6;
         const uint32_t e1 = (((dst >> 6) + k + 1) << 6), e = e1 < dst + l ? e1 : dst + l;
         ps = (a & JQ_SRC) + (d0 - dst);
         pd = d0;
-        pl = e - d0;
+        pl = e > d0 ? e - d0 : 0;   // (inside one 64-byte block by construction)
     };
     for (uint32_t j = tid; j < npc; j += 2 * NT) {
         const bool two = j + NT < npc;
@@ -2372,7 +2375,10 @@ extern "C" hipError_t rr_launch_decode(const uint8_t *blob, const uint64_t *offs
 #ifndef RR_ENC_W
 #define RR_ENC_W 16384
 #endif
-constexpr uint32_t ENC_W = RR_ENC_W, ENC_NT = 256, ENC_RCAP = 512;
+#ifndef RR_ENC_RCAP   // payload runs queued per window (LDS: 12 bytes each)
+#define RR_ENC_RCAP 512
+#endif
+constexpr uint32_t ENC_W = RR_ENC_W, ENC_NT = 256, ENC_RCAP = RR_ENC_RCAP;
 static uint64_t enc_windows(uint64_t data_cap) { return data_cap / ENC_W + 1; }
 
 extern "C" uint64_t rr_encode_scratch_words(uint64_t n, uint64_t data_cap) {
