@@ -176,8 +176,22 @@ def main():
             assert rc == 0, "rr_decode_batch_host failed"
 
         wall_rec, _ = timed(e2e_records, 5, 1)
+        e2e_api()   # (the arena back on the host for the encode leg)
         api_ok = (int(h_tot.n_elems) == n_elems and int(h_tot.payload) == payload
                   and torch.equal(h_vals, d_vals.cpu()) and torch.equal(h_elems, d_elems[: n_elems * 16].cpu()))
+        # dump direction from host memory: rr_encode_batch_host on the decoded flat batch
+        h_out = torch.empty((nb + 15) & ~15, dtype=torch.uint8).pin_memory()
+        h_ooffs = torch.empty(n + 1, dtype=torch.int64).pin_memory()
+        h_tot2 = rr.Totals()
+
+        def e2e_encode():
+            rc = L.rr_encode_batch_host(eng._ctx, h_vals.data_ptr(), h_elems.data_ptr(), n_elems,
+                                        h_arena.data_ptr(), nb, n, h_out.data_ptr(), h_out.numel(),
+                                        h_ooffs.data_ptr(), ctypes.byref(h_tot2))
+            assert rc == 0, "rr_encode_batch_host failed"
+
+        wall_enc_host, _ = timed(e2e_encode, 5, 1)
+        enc_ok = bool(torch.equal(h_out[:nb], h_data[:nb])) and int(h_tot2.bytes) == nb
         host = {"copy_ref": {"GBs": round(copy_gbs, 1), "frac_of_peak": round(copy_gbs / HBM_PEAK_GBS, 4),
                              "what": "torch device-to-device copy of the blob buffer (read + write bytes)"},
                 "host_e2e": {"gib_s": round(nb * 5 / wall_api / 2 ** 30, 2),
@@ -188,10 +202,14 @@ def main():
                                            "ms_per_step": round(wall_rec / 5 * 1e3, 3),
                                            "what": "the same call with arena = NULL: records and descriptors "
                                                    "come down, the caller's blob buffer serves as the arena"},
+                "host_e2e_encode": {"gib_s": round(nb * 5 / wall_enc_host / 2 ** 30, 2),
+                                    "ms_per_step": round(wall_enc_host / 5 * 1e3, 3), "roundtrip_bit_exact": enc_ok,
+                                    "what": "rr_encode_batch_host on pinned host buffers: records+descriptors+arena "
+                                            "up, encode, blobs+offsets down (one stream)"},
                 "host_e2e_serial": {"gib_s": round(nb * 5 / wall_ser / 2 ** 30, 2),
                                     "ms_per_step": round(wall_ser / 5 * 1e3, 3),
                                     "what": "the same transfers in one stream, back to back (no overlap)"}}
-        del h_data, h_offs, h_vals, h_elems, h_arena
+        del h_data, h_offs, h_vals, h_elems, h_arena, h_out, h_ooffs
 
     # ---- correctness of what was timed ----
     parity = None
@@ -448,7 +466,7 @@ def cpu_baseline(data, offs, nb, budget_s):
                 "values_per_s": round(m / td, 1), "encode_gib_s": round(sb / te / 2 ** 30, 4)})
     out["per_core_gib_s"] = out["value"]
     # flat restatement (same output as the GPU) on 1 thread, 16 threads (the box's CPU share per
-    # GPU) and every core this process may run on (capped at 128 threads)
+    # GPU) and every core this process may run on (its affinity and cgroup quota; at most 128)
     allc = min(len(os.sched_getaffinity(0)), 128)
     quota = None   # the job's CPU quota (cgroup v2 cpu.max), which bounds any thread count
     try:
@@ -459,6 +477,8 @@ def cpu_baseline(data, offs, nb, budget_s):
     except (OSError, ValueError):
         pass
     out["cpu_quota_cores"] = quota
+    if quota:   # threads past the quota only time-share the same cores
+        allc = min(allc, max(1, int(quota)))
     flat = {}
     for thr in sorted({1, min(16, allc), allc}):
         ts = []
