@@ -1,4 +1,5 @@
 set -e
 mkdir -p gpurun_out
-timeout -k 10 600 python bench.py --n 10000000 --steps 10 --warmup 2 --no-cpu --no-split --no-snappy > gpurun_out/bench10m.json 2> gpurun_out/bench10m.err
+rm -f gpurun_out/nsweep.log
+for n in 250000 500000 1000000 2000000 4000000 8000000; do timeout -k 10 200 python tools/time_decode.py 4 $n | grep cfg >> gpurun_out/nsweep.log; done
 echo done
