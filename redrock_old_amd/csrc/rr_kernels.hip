@@ -845,6 +845,20 @@ static_assert(DEC_BL >= 2 && DEC_BL <= RR_WAVE && DEC_BL % 2 == 0, "batch lanes"
 #ifndef RR_DEC_OVL_K  // granules (16 B) per thread loaded before the sort (the rest after it)
 #define RR_DEC_OVL_K 9
 #endif
+// 1: the window's loads, arena stores and stage writes go through buffer resources with no
+// exec-mask branches (out-of-range loads read zeros, out-of-range stores are dropped, unstaged
+// granules are written to a dummy LDS slot), and the workgroup's barriers order LDS only.
+// With __syncthreads() (a workgroup-scope fence for all memory) every barrier waited for the
+// window's loads and for the acknowledgement of every arena store, and the branch joins of
+// the guarded copy made the compiler wait for each store's acknowledgement before the next.
+#ifndef RR_DEC_BFREE
+#define RR_DEC_BFREE 1
+#endif
+#if RR_DEC_BFREE
+#define DEC_SYNC() lds_barrier()
+#else
+#define DEC_SYNC() __syncthreads()
+#endif
 #ifndef RR_DEC_EARLY  // late-copy builds: write the arena copy from the stage before the walks, not after
 #define RR_DEC_EARLY 0
 #endif
@@ -973,6 +987,53 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
     const uint64_t ov_w1 = W1 >> 4, ov_s0 = S0 >> 4, ov_e = (staged && S1 > W1 ? S1 : W1) >> 4;
     const bool ovl = !(RR_DEC_PF && it > 0);
     u32x4 ov_x[RR_DEC_OVL_K];
+#if RR_DEC_BFREE
+    // the window's granules [A0, ov_e) (loads past it read zeros), the arena's [A0, ov_w1)
+    // (stores past it are dropped); g = A0 / 16 + tid + k * NT is at byte offset 16 (tid + k NT)
+    const uint64_t ov_a = A0 >> 4;
+    const rsrc_t ov_RL = make_rsrc(blob + A0, ov_e > ov_a ? (uint32_t)((ov_e - ov_a) * 16) : 0u);
+    const rsrc_t ov_RA = make_rsrc(arena + A0, ov_w1 > ov_a ? (uint32_t)((ov_w1 - ov_a) * 16) : 0u);
+    typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
+    lds_u32x4 *ov_lds = (lds_u32x4 *)(__attribute__((address_space(3))) uint8_t *)stage;
+    // granule g's stage slot, or the dummy slot just past the stage (reads past the stage see
+    // garbage there, which the walks never use: every read is checked against its value's end)
+    auto ov_slot = [&](uint64_t g) __attribute__((always_inline)) -> uint32_t {
+        return (staged & (g >= ov_s0) & (g < ov_e)) ? (uint32_t)(g - ov_s0) : STAGE / 16;
+    };
+#pragma unroll
+    for (int k = 0; k < RR_DEC_OVL_K; ++k)
+        ov_x[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ov_RL, (int)((tid + k * NT) * 16), 0, 0));
+    auto ov_finish = [&]() __attribute__((always_inline)) {
+#pragma unroll
+        for (int k = 0; k < RR_DEC_OVL_K; ++k) {
+            const uint32_t o = (tid + k * NT) * 16;
+#ifndef RR_ABLATE_NOCOPY
+            __builtin_amdgcn_raw_buffer_store_b128(ov_x[k], ov_RA, (int)o, 0, 2 /* nt */);
+#endif
+            ov_lds[ov_slot(ov_a + tid + (uint64_t)k * NT)] = ov_x[k];
+        }
+        // the rest of the window (beyond the prefetched granules): wave-uniform rounds
+        const uint64_t tot = ov_e > ov_a ? ov_e - ov_a : 0;
+        const uint32_t rounds = tot > (uint64_t)RR_DEC_OVL_K * NT ? (uint32_t)((tot - (uint64_t)RR_DEC_OVL_K * NT + NT - 1) / NT) : 0u;
+        for (uint32_t r = 0; r < rounds; r += 4) {
+            u32x4 x[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                x[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                     ov_RL, (int)((tid + (RR_DEC_OVL_K + r + k) * NT) * 16), 0, 0));
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t o = (tid + (RR_DEC_OVL_K + r + k) * NT) * 16;
+#ifndef RR_ABLATE_NOCOPY
+                __builtin_amdgcn_raw_buffer_store_b128(x[k], ov_RA, (int)o, 0, 2 /* nt */);
+#endif
+                ov_lds[ov_slot(ov_a + tid + (uint64_t)(RR_DEC_OVL_K + r + k) * NT)] = x[k];
+            }
+        }
+    };
+    if (ovl) {
+    } else
+#else
     if (ovl) {
         const u32x4 *src = reinterpret_cast<const u32x4 *>(blob);
 #pragma unroll
@@ -1018,6 +1079,7 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
     };
     if (ovl) {
     } else
+#endif   // RR_DEC_BFREE
 #endif
     if (RR_DEC_PF && it > 0) {
         // 1'. the arena copy was made during the previous window: value bytes -> LDS only
@@ -1109,7 +1171,7 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
         const uint32_t nv = (uint32_t)(v_hi - c0 < PMAX ? v_hi - c0 : PMAX);
         if (tid < C_N) { ccount[tid] = 0; ccur[tid] = 0; }
         if (tid == 0) next_batch = 0;
-        __syncthreads();   // also: the previous chunk's batches are done
+        DEC_SYNC();   // also: the previous chunk's batches are done
         PROBE(if (c0 == v_lo) pt1 = __builtin_amdgcn_s_memtime();)
         uint32_t myc[PMAX / NT];
 #pragma unroll
@@ -1124,7 +1186,7 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
                 if (m && lane == 0) atomicAdd(&ccount[c], (uint32_t)__popcll(m));
             }
         }
-        __syncthreads();
+        DEC_SYNC();
         if (tid == 0) {
             uint32_t s = 0, bs = 0;
             for (uint32_t k = 0; k < C_N; ++k) {
@@ -1137,7 +1199,7 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
             }
             bpre[C_N] = bs;
         }
-        __syncthreads();
+        DEC_SYNC();
 #pragma unroll
         for (uint32_t j = 0; j < PMAX / NT; ++j) {
             const uint32_t i = j * NT + tid;
@@ -1160,10 +1222,10 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
 #endif
     for (uint64_t c0 = v_lo; c0 < v_end; c0 += PMAX) {
         if (c0 != v_lo) {
-            __syncthreads();   // every wave is done with the previous chunk's batches
+            DEC_SYNC();   // every wave is done with the previous chunk's batches
             sort_chunk(c0);
         }
-        __syncthreads();   // the stage and the chunk's sort are complete
+        DEC_SYNC();   // the stage and the chunk's sort are complete
 
         PROBE(if (c0 == v_lo) pt2 = __builtin_amdgcn_s_memtime();)
         // 3. single-class batches, taken dynamically by the waves
@@ -1285,7 +1347,7 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
     bad = wave_sum(bad);
     pay = wave_sum(pay);
     if (lane == 0) { red[0][wave] = bad; red[1][wave] = pay; }
-    __syncthreads();
+    DEC_SYNC();
     if (tid == 0) {
         uint64_t tb = 0, tp = 0;
         for (uint32_t w = 0; w < NW; ++w) { tb += red[0][w]; tp += red[1][w]; }
