@@ -718,7 +718,10 @@ __device__ RR_COLD Acc exact_value(const uint8_t *__restrict__ blob, uint64_t v,
 }
 
 // class batch order: heaviest walks first (longest-job-first over the window's waves)
-__constant__ uint32_t CLASS_ORDER[C_N] = {C_ZL, C_SL, C_HH, C_HT, C_LIST, C_EXACT, C_IS, C_STR};
+#ifndef RR_DEC_ORDER
+#define RR_DEC_ORDER C_ZL, C_SL, C_HH, C_HT, C_LIST, C_EXACT, C_IS, C_STR
+#endif
+__constant__ uint32_t CLASS_ORDER[C_N] = {RR_DEC_ORDER};
 
 // One single-class batch: lane < cnt decodes value v (byte offsets relative to the source,
 // whose byte 0 is batch offset B).
