@@ -744,4 +744,94 @@ __device__ __forceinline__ bool do_ziplist(const Src &R, const Lane &l, bool act
     return !ok || n != l.r;
 }
 
+// ---- Hash / ZSet ziplists, grouped, on ONE backward chain.  A backward step needs only the
+// prevlen field (ziplist.c:300-330: 1 byte, or 0xFE + u32; an entry's prevlen is the size of
+// the entry before it), so the chain costs a few instructions per entry; all the per-entry
+// work — the encoding, the length / integer fields, the checks, the descriptor store — is done
+// off the chain, lane g of the value's G-lane group taking entries N-1-g, N-1-g-G, ...  The
+// checks are those of one forward walk (ziplist.c:300-447): the entries tile [10, zlbytes-1)
+// exactly (each entry, decoded from its own header, ends where the next one starts; the last
+// ends at the 0xFF byte, entry 0 starts right after the header with prevlen 0), zltail is the
+// last entry, zllen entries, an even count of them.  A ziplist whose zllen saturated (0xFFFF)
+// goes to the exact parser.
+template <class Src>
+__device__ __forceinline__ bool do_ziplist_bg(const Src &R, const Lane &l, bool active, uint32_t G, uint32_t g,
+                                              uint32_t &n, uint64_t &pay) {
+    const uint32_t zl0 = l.q + 13, zend = l.q + l.L, zlast = zend - 1;   // zlast: the 0xFF byte
+    const uint32_t first = zl0 + 10;                                     // entry 0
+    uint32_t z[3];
+    R.template get<3>(zl0, z);   // zlbytes, zltail, zllen
+    const uint32_t N = z[2] & 0xFFFF;
+    const uint32_t endbyte = R.template fetch<1>(zlast).w[0];   // (aligned dword holding zlast)
+    put_desc(l.E, active && g == 0 ? l.slot(0) : NOSLOT, l.B + zl0, l.L - 13, RR_K_ZLRAW, 0);
+    pay += active && g == 0 ? l.L - 13 : 0;
+    bool fail = active && N == 0xFFFF;
+    uint32_t p = zl0 + z[1];   // entry N-1 (zltail)
+    uint32_t expect = zlast;   // where the entry at p must end
+    uint32_t k = 0;            // entries walked
+    bool walk = active && N != 0xFFFF && N > 0;
+    for (;;) {
+        uint32_t mp = zl0, me = 0, mi = 0;
+        bool mine = false;
+        for (uint32_t j = 0; j < G; ++j) {
+            uint32_t x[2];
+            R.template get<2>(walk ? p : zl0, x);
+            const uint32_t b0 = x[0] & 0xFF;
+            const uint32_t pl = b0 >= 254 ? ab(x[1], x[0], 1) : b0;
+            const uint32_t idx = N - 1 - k;
+            // the chain's own checks: p among the entries, not the end marker; entry 0 right
+            // after the header with prevlen 0, every other prevlen reaching back inside
+            const bool bad = (p < first) | (p >= zlast) | (b0 == 0xFF) |
+                             (idx == 0 ? ((p != first) | (pl != 0)) : (pl > p - first));
+            fail |= walk & bad;
+            const bool ok = walk & !bad;
+            mine = j == g ? ok : mine;
+            mp = ((j == g) & ok) ? p : mp;
+            me = j == g ? expect : me;
+            mi = j == g ? idx : mi;
+            expect = ok ? p : expect;
+            p = ok ? p - pl : p;
+            k += ok;
+            walk = ok & (k < N);
+        }
+        // my entry: every field of its header from registers, as selects (no per-encoding
+        // branches), then the checks of one forward step and the descriptor
+        uint32_t b[4];
+        R.template get<4>(mp, b);
+        const uint32_t b0 = b[0] & 0xFF;
+        const bool big = b0 >= 254;
+        const uint32_t qp = mp + (big ? 5u : 1u);
+        const uint32_t e = big ? (b[1] >> 8) & 0xFF : (b[0] >> 8) & 0xFF;
+        const uint32_t x1 = big ? (b[1] >> 16) & 0xFF : (b[0] >> 16) & 0xFF;
+        const uint32_t lo = big ? ab(b[2], b[1], 2) : ab(b[1], b[0], 2);   // bytes after the encoding byte
+        const uint32_t hi = big ? ab(b[3], b[2], 2) : ab(b[2], b[1], 2);
+        const bool zstr = e < 0xC0;
+        const uint32_t scls = e >> 6;                        // string length class 0 / 1 / 2
+        const uint32_t ls = 1 + scls + 2 * (scls >> 1);      // 1 / 2 / 5 length bytes
+        const uint32_t sl1 = scls == 0 ? (e & 0x3F) : (((e & 0x3F) << 8) | x1);
+        const uint32_t sl = scls >= 2 ? __builtin_bswap32(lo) : sl1;
+        const bool imm = e - 0xF1u <= 0xFDu - 0xF1u;
+        const uint32_t isz = (uint32_t)(e == 0xFE) + 2 * (uint32_t)(e == 0xC0) + 3 * (uint32_t)(e == 0xF0) +
+                             4 * (uint32_t)(e == 0xD0) + 8 * (uint32_t)(e == 0xE0);
+        const uint64_t endp = (uint64_t)qp + (zstr ? ls + sl : 1 + isz);
+        const bool bad = (big & (mp + 5 > zlast)) | (qp >= zlast) | (mi + 1 >= l.r) | (!zstr & !imm & (isz == 0)) |
+                         (zstr & (qp + ls > zlast)) | (endp != (uint64_t)me);
+        fail |= mine & bad;
+        const uint32_t sh = (32 - 8 * isz) & 31;
+        const int64_t v32 = (int32_t)(lo << sh) >> sh;
+        const int64_t iv = isz == 8 ? (int64_t)((uint64_t)lo | ((uint64_t)hi << 32)) : imm ? (int64_t)(e & 0x0F) - 1 : v32;
+        put_desc(l.E, (mine & !bad) ? l.slot(mi + 1) : NOSLOT, zstr ? l.B + qp + ls : (uint64_t)iv, zstr ? sl : 0,
+                 zstr ? RR_K_STR : RR_K_INT, zstr ? (e & 0xC0) : e);
+        if (__ballot(walk) == 0) break;
+    }
+    // one verdict for the whole group
+    const uint32_t base = lane_id() - g;
+    const uint64_t gm = (G >= 64 ? ~0ull : ((1ull << G) - 1)) << base;
+    const bool gfail = (__ballot(fail) & gm) != 0;
+    const bool ok = !gfail && k == N && (N & 1) == 0 && (endbyte >> (8 * (zlast & 3)) & 0xFF) == 0xFF &&
+                    (N > 0 || (z[1] == 10 && first == zlast));
+    n = 1 + N;
+    return !ok || n != l.r;
+}
+
 }  // namespace rr

@@ -717,6 +717,17 @@ __device__ RR_COLD Acc exact_value(const uint8_t *__restrict__ blob, uint64_t v,
     return Acc{status != RR_OK ? 1u : 0u, pay};
 }
 
+// ziplists: 1 = grouped walks on one backward prevlen chain (do_ziplist_bg, RR_ZL_VPB values
+// per batch), 0 = two lanes per value walking from both ends (do_ziplist, DEC_BL / 2 values)
+#ifndef RR_ZL_BACK
+#define RR_ZL_BACK 1
+#endif
+#ifndef RR_ZL_VPB
+#define RR_ZL_VPB 16
+#endif
+#if RR_ZL_BACK
+constexpr uint32_t ZL_VPB = RR_ZL_VPB;
+#endif
 // class batch order: heaviest walks first (longest-job-first over the window's waves)
 #ifndef RR_DEC_ORDER
 #define RR_DEC_ORDER C_ZL, C_SL, C_HH, C_HT, C_LIST, C_EXACT, C_IS, C_STR
@@ -776,8 +787,12 @@ __device__ __forceinline__ Acc run_batch(const Src &src, uint32_t c, bool active
             else fail = do_ht(src, H, l, active, ne, vp, fixup, c == C_HH);
         } else if (c == C_SL) {
             fail = do_skiplist_g(src, H, l, active, G, g, ne, vp);
-        } else {   // C_ZL: G == 2, lane 1 of the pair walks backward
+        } else {
+#if RR_ZL_BACK   // C_ZL: grouped, one backward prevlen chain per value
+            fail = do_ziplist_bg(src, l, active, G, g, ne, vp);
+#else            // C_ZL: G == 2, lane 1 of the pair walks backward
             fail = do_ziplist(src, l, active, g != 0, ne, vp);
+#endif
         }
         exact = fail;
         if (active && !fail) {
@@ -898,7 +913,10 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
                                                               uint64_t *fix, uint32_t nwin) {
     constexpr uint32_t NT = NW * RR_WAVE, STAGE = W + SLACK;
     static_assert(PMAX % NT == 0 && W % 16 == 0 && SLACK % 16 == 0, "tile shape");
-    __shared__ __attribute__((aligned(16))) uint8_t stage[STAGE + 64];
+#ifndef RR_DEC_LDSPAD   // diagnostics: extra LDS per workgroup (e.g. to hold one workgroup per CU)
+#define RR_DEC_LDSPAD 0
+#endif
+    __shared__ __attribute__((aligned(16))) uint8_t stage[STAGE + 64 + RR_DEC_LDSPAD];
     __shared__ uint16_t perm[PMAX];
     __shared__ uint32_t ccount[C_N], cbase[C_N], ccur[C_N], bpre[C_N + 1];
     __shared__ uint32_t next_batch;
@@ -912,7 +930,7 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
     // walks run, the waves with no batch left copy the NEXT window to the arena (global ->
     // global), which also leaves its bytes in the L2 for that window's LDS stage
     for (uint32_t tile = blockIdx.x, it = 0; tile < nwin; tile += gridDim.x, ++it) {
-    if (it) __syncthreads();   // the previous window is done with the LDS
+    if (it) DEC_SYNC();   // the previous window is done with the LDS
     if (tid == 0) next_copy = 0;
     PROBE(pt0 = __builtin_amdgcn_s_memtime(); if (threadIdx.x < PROBE_WORDS) prb[threadIdx.x] = 0;)
 #else
@@ -1194,7 +1212,11 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
             uint32_t s = 0, bs = 0;
             for (uint32_t k = 0; k < C_N; ++k) {
                 const uint32_t c = CLASS_ORDER[k];
+#if RR_ZL_BACK
+                const uint32_t vpb = c == C_ZL ? ZL_VPB : DEC_BL;
+#else
                 const uint32_t vpb = c == C_ZL ? DEC_BL / 2 : DEC_BL;   // ziplists: two lanes each
+#endif
                 cbase[c] = s;
                 bpre[k] = bs;
                 s += ccount[c];
@@ -1245,7 +1267,11 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
             uint32_t k = 0;
             while (bi >= bpre[k + 1]) ++k;
             const uint32_t c = CLASS_ORDER[k];
+#if RR_ZL_BACK
+            const uint32_t vpb = c == C_ZL ? ZL_VPB : DEC_BL;
+#else
             const uint32_t vpb = c == C_ZL ? DEC_BL / 2 : DEC_BL;
+#endif
             const uint32_t first = cbase[c] + (bi - bpre[k]) * vpb;
             const uint32_t cnt = min(ccount[c] - (bi - bpre[k]) * vpb, vpb);
 #ifdef RR_SKIP_CLASSES   // timing-only builds (tools/): skip the batches of these classes
@@ -1253,14 +1279,14 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
 #endif
             PROBE(const uint64_t tb0 = __builtin_amdgcn_s_memtime();)
             // lanes per value: ziplists 2 (two-ended walk), chained classes 64 / cnt (grouped walks)
-            const bool grouped = c == C_LIST || c == C_SL || c == C_IS;
+            const bool grouped = c == C_LIST || c == C_SL || c == C_IS || (RR_ZL_BACK && c == C_ZL);
             const uint32_t Gw = max(1u, min(GMAX, (uint32_t)RR_WAVE / cnt));
 #ifdef RR_HT_GROUPED   // timing builds (tools/): grouped hash-table walks (measured slower)
             const bool htg = (c == C_HT || c == C_HH) && Gw >= ht_group_min(c == C_HH);
 #else
             const bool htg = false;
 #endif
-            const uint32_t G = __builtin_amdgcn_readfirstlane(c == C_ZL ? 2u : (grouped || htg) ? Gw : 1u);
+            const uint32_t G = __builtin_amdgcn_readfirstlane((c == C_ZL && !RR_ZL_BACK) ? 2u : (grouped || htg) ? Gw : 1u);
             const uint32_t li = lane / G, g = lane - li * G;   // the value's index in the batch
             const bool active = li < cnt;
             const uint64_t v = c0 + (active ? perm[first + li] : 0u);
@@ -1287,29 +1313,27 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
         const uint32_t ntile = tile + gridDim.x;
         const uint64_t nW0 = (uint64_t)ntile * W, nW1 = nW0 + W < padded ? nW0 + W : padded;
         if (ntile < nwin && nW1 > nW0) {
-            if (v_end == v_lo) __syncthreads();   // (no chunk ran: order next_copy's reset)
-            const u32x4 *src = reinterpret_cast<const u32x4 *>(blob);
-            u32x4 *dst = reinterpret_cast<u32x4 *>(arena);
+            if (v_end == v_lo) DEC_SYNC();   // (no chunk ran: order next_copy's reset)
             const uint64_t cw0 = nW0 >> 4, cw1 = nW1 >> 4;
             constexpr uint32_t TASK = 4 * RR_WAVE;   // 16-byte granules per task
             const uint32_t ntask = (uint32_t)((cw1 - cw0 + TASK - 1) / TASK);
+            // buffer resources over the next window: no exec-mask branches around the stores
+            const rsrc_t RL = make_rsrc(blob + nW0, (uint32_t)(nW1 - nW0));
+            const rsrc_t RA = make_rsrc(arena + nW0, (uint32_t)(nW1 - nW0));
             for (;;) {
                 uint32_t ti = 0;
                 if (lane == 0) ti = atomicAdd(&next_copy, 1u);
                 ti = __builtin_amdgcn_readfirstlane(__shfl(ti, 0, RR_WAVE));
                 if (ti >= ntask) break;
-                const uint64_t g0 = cw0 + (uint64_t)ti * TASK + lane;
                 u32x4 x[4];
 #pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const uint64_t g = g0 + k * RR_WAVE;
-                    if (g < cw1) x[k] = src[g];
-                }
+                for (int k = 0; k < 4; ++k)
+                    x[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                         RL, (int)((ti * TASK + lane + k * RR_WAVE) * 16), 0, 0));
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
-                    const uint64_t g = g0 + k * RR_WAVE;
 #ifndef RR_ABLATE_NOCOPY
-                    if (g < cw1) __builtin_nontemporal_store(x[k], dst + g);
+                    __builtin_amdgcn_raw_buffer_store_b128(x[k], RA, (int)((ti * TASK + lane + k * RR_WAVE) * 16), 0, 2);
 #endif
                 }
             }
