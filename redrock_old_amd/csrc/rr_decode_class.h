@@ -510,13 +510,16 @@ __device__ __forceinline__ bool do_list_g(const Src &R, const Lane &l, bool acti
 }
 
 // ---- Set / Hash hash tables, grouped.  The chain steps read only the u64 length fields (every
-// lane of the group, as in do_list_g); lane g takes elements g, g + G, ...: it stores the
-// descriptor and, for a key member, fingerprints it from the 8 bytes that end it (the bytes
-// do_ht reads at the next step's p - 8).  The duplicate test runs once per value after the
-// walk, not per step: key i is broadcast from its lane and compared with the lower-numbered
-// keys the other lanes hold.  A lane keeps the keys of its first HT_G_ROUNDS rounds, which
-// covers HT_FP_KEYS keys when G >= HT_FP_KEYS / HT_G_ROUNDS lanes hold keys (a hash's keys
-// are its even elements: G >= 8; a set: G >= 4 — the batch picks do_ht below that).
+// lane of the group walks the same chain: a read, three checks and an add per member); lane g
+// takes members g, g + G, ...: once per G chain steps it stores its member's descriptor and,
+// for a key member, fingerprints it from the 8 bytes that end it (as do_ht).  The walk takes
+// exactly the value's reservation of members and then must stand at the value's end (the
+// verdicts of do_ht's walk to the end).  The duplicate test runs once per value after the
+// walk: each lane compares the keys it holds with those of every other lane of its group
+// (rotations by d = 1 .. G-1, one shuffle per round of keys) and its own.  A lane keeps the
+// keys of its first HT_G_ROUNDS rounds, which covers HT_FP_KEYS keys when G >= HT_FP_KEYS /
+// HT_G_ROUNDS lanes hold keys (a hash's keys are its even members: G >= 8; a set: G >= 4 —
+// below that the batch runs do_ht).
 constexpr uint32_t HT_G_ROUNDS = 4;
 __device__ __forceinline__ uint32_t ht_group_min(bool hash) { return hash ? 2 * HT_FP_KEYS / HT_G_ROUNDS : HT_FP_KEYS / HT_G_ROUNDS; }
 template <class Src>
@@ -528,60 +531,68 @@ __device__ __forceinline__ bool do_ht_g(const Src &R, const Head &H, const Lane 
 #else   // timing-only builds (tools/): no fingerprints (duplicates go undetected)
     const bool chk = false;
 #endif
-    uint32_t p = l.q + 13, k = 0;
-    const uint32_t end = l.q + l.L;
-    bool fail = false, walk = active;
+    const uint32_t end = l.q + l.L, r = active ? l.r : 0u;
+    uint32_t p = l.q + 13;
+    bool fail = active && r == 0 && p != end;   // an empty table is its 13-byte header
     uint32_t fps[HT_G_ROUNDS];
 #pragma unroll
     for (uint32_t q = 0; q < HT_G_ROUNDS; ++q) fps[q] = 0xFFFFFFFFu;
-    for (uint32_t r = 0;; ++r) {
-        uint32_t mp = 0, ml = 0, mk = 0;
-        bool mine = false;
+    uint32_t rounds = 0;   // (wave-uniform)
+    for (;; ++rounds) {
+        // G chain steps with no checks: p only moves forward and stays <= end, a member whose
+        // length does not fit is caught by its own lane below (and fails the whole value)
+        uint32_t mp = l.q;
         for (uint32_t j = 0; j < G; ++j) {
-            uint32_t x[2];
-            R.template get<2>(p, x);
+            uint32_t x[1];
+            R.template get<1>(p, x);
             const uint32_t rem = end - p;
-            const bool done = p == end;
-            const bool bad = (rem < 8) | (x[1] != 0) | (x[0] > rem - 8) | (k >= l.r);
-            fail |= walk & !done & bad;
-            const bool ok = walk & !done & !bad;
-            mine = j == g ? ok : mine;
             mp = j == g ? p : mp;
-            ml = j == g ? x[0] : ml;
-            mk = j == g ? k : mk;
-            p = ok ? p + 8 + x[0] : p;
-            k += ok;
-            walk = ok;
+            p = min(p + 8 + min(x[0], rem), end);
         }
-        put_desc(l.E, mine ? l.slot(mk) : NOSLOT, l.B + mp + 8, ml, RR_K_STR, 0);
-        pay += mine ? ml : 0;
+        // my member (index mk): its length field's checks, the descriptor, the fingerprint
+        const uint32_t mk = rounds * G + g;
+        const bool mine = mk < r;
+        uint32_t x[2];
+        R.template get<2>(mp, x);
+        const uint32_t ml = x[0], rem = end - mp;
+        const bool bad = (rem < 8) | (x[1] != 0) | (ml > rem - 8) | ((mk + 1 == r) & (mp + 8 + ml != end));
+        fail |= mine & bad;
+        put_desc(l.E, (mine & !bad) ? l.slot(mk) : NOSLOT, l.B + mp + 8, ml, RR_K_STR, 0);
+        pay += (mine & !bad) ? ml : 0;
         uint32_t t[2];
-        R.template get<2>(mp + ml, t);   // bytes [mp + 8 + ml - 8, mp + 8 + ml): the member's last 8
+        R.template get<2>((mine & !bad) ? mp + ml : l.q, t);   // bytes [mp + 8 + ml - 8, mp + 8 + ml): the member's last 8
         const bool key = mine & (!hash | ((mk & 1) == 0));
         const uint32_t f = key ? member_fp16(ml, t[0], t[1]) : 0xFFFFFFFFu;
 #pragma unroll
-        for (uint32_t q = 0; q < HT_G_ROUNDS; ++q) fps[q] = r == q ? f : fps[q];
-        if (__ballot(walk) == 0) break;
+        for (uint32_t q = 0; q < HT_G_ROUNDS; ++q) fps[q] = rounds == q ? f : fps[q];
+        if (__ballot((rounds + 1) * G < r) == 0) break;
     }
-    // key i = element e (hash: 2i) sits on lane e % G of the group, round e / G
+    // duplicate keys: my keys against every other lane's (rotation d) and against each other
     bool dup = false;
-    const uint32_t keys = hash ? k >> 1 : k;
+    const uint32_t RU = rounds + 1 < HT_G_ROUNDS ? rounds + 1 : HT_G_ROUNDS;   // rounds holding keys
     const uint32_t base = lane_id() - g;
-    for (uint32_t i = 1; __ballot(chk & (i < keys)) != 0; ++i) {
-        const uint32_t e = hash ? 2 * i : i, q = e / G, owner = e - q * G;
-        if (q >= HT_G_ROUNDS) break;
-        const uint32_t src = q == 0 ? fps[0] : q == 1 ? fps[1] : q == 2 ? fps[2] : fps[3];
-        const uint32_t x = (uint32_t)__shfl((int)src, (int)(base + owner), RR_WAVE);
 #pragma unroll
-        for (uint32_t qq = 0; qq < HT_G_ROUNDS; ++qq)
-            dup |= (qq <= q) & (qq * G + g < e) & (fps[qq] == x) & (x != 0xFFFFFFFFu);
+    for (uint32_t a = 0; a < HT_G_ROUNDS; ++a)
+#pragma unroll
+        for (uint32_t b = a + 1; b < HT_G_ROUNDS; ++b) dup |= (fps[a] == fps[b]) & (fps[a] != 0xFFFFFFFFu);
+    for (uint32_t d = 1; d < G; ++d) {
+        uint32_t src = g + d;
+        src = base + (src >= G ? src - G : src);
+#pragma unroll
+        for (uint32_t q = 0; q < HT_G_ROUNDS; ++q) {
+            if (q >= RU) break;
+            const uint32_t x = (uint32_t)__shfl((int)fps[q], (int)src, RR_WAVE);
+#pragma unroll
+            for (uint32_t qq = 0; qq < HT_G_ROUNDS; ++qq) dup |= (fps[qq] == x) & (x != 0xFFFFFFFFu);
+        }
     }
     const uint64_t gm = (G >= 64 ? ~0ull : ((1ull << G) - 1)) << base;
-    const bool dupg = (__ballot(dup) & gm) != 0;
-    n = k;
-    const bool cnt_ok = !hash ? (uint64_t)k == cnt : ((k & 1) == 0 && (uint64_t)(k >> 1) == cnt);
-    fix = active && (cnt > HT_FP_KEYS || (chk && dupg)) && k >= (hash ? 4u : 2u);
-    return fail || !cnt_ok || k != l.r;
+    const bool gfail = (__ballot(fail) & gm) != 0;
+    const bool dupg = (__ballot(dup & chk) & gm) != 0;
+    n = r;
+    const bool cnt_ok = !hash ? (uint64_t)r == cnt : ((r & 1) == 0 && (uint64_t)(r >> 1) == cnt);
+    fix = active && (cnt > HT_FP_KEYS || (chk && dupg)) && r >= (hash ? 4u : 2u);
+    return gfail || !cnt_ok;
 }
 
 // ---- ZSet skiplist, grouped: a step takes one (member, score) pair — the member's length
@@ -761,45 +772,42 @@ __device__ __forceinline__ bool do_ziplist_bg(const Src &R, const Lane &l, bool 
     const uint32_t first = zl0 + 10;                                     // entry 0
     uint32_t z[3];
     R.template get<3>(zl0, z);   // zlbytes, zltail, zllen
-    const uint32_t N = z[2] & 0xFFFF;
+    const uint32_t N = active && (z[2] & 0xFFFF) != 0xFFFF ? z[2] & 0xFFFF : 0u;
     const uint32_t endbyte = R.template fetch<1>(zlast).w[0];   // (aligned dword holding zlast)
     put_desc(l.E, active && g == 0 ? l.slot(0) : NOSLOT, l.B + zl0, l.L - 13, RR_K_ZLRAW, 0);
     pay += active && g == 0 ? l.L - 13 : 0;
-    bool fail = active && N == 0xFFFF;
-    uint32_t p = zl0 + z[1];   // entry N-1 (zltail)
+    bool fail = active && (z[2] & 0xFFFF) == 0xFFFF;   // saturated count: the exact parser walks it
+    // the chain: p = start of entry N-1-s after s steps; each step goes back by the entry's
+    // prevlen, clamped to stay at or after entry 0's position (a prevlen that does not fit is
+    // caught below by the lane that holds that entry)
+    uint32_t p = zl0 + z[1];
+    p = p < first ? first : p > zlast ? zlast : p;
     uint32_t expect = zlast;   // where the entry at p must end
-    uint32_t k = 0;            // entries walked
-    bool walk = active && N != 0xFFFF && N > 0;
-    for (;;) {
-        uint32_t mp = zl0, me = 0, mi = 0;
-        bool mine = false;
+    for (uint32_t rounds = 0;; ++rounds) {
+        uint32_t mp = first, me = zlast;
         for (uint32_t j = 0; j < G; ++j) {
             uint32_t x[2];
-            R.template get<2>(walk ? p : zl0, x);
+            R.template get<2>(p, x);
             const uint32_t b0 = x[0] & 0xFF;
             const uint32_t pl = b0 >= 254 ? ab(x[1], x[0], 1) : b0;
-            const uint32_t idx = N - 1 - k;
-            // the chain's own checks: p among the entries, not the end marker; entry 0 right
-            // after the header with prevlen 0, every other prevlen reaching back inside
-            const bool bad = (p < first) | (p >= zlast) | (b0 == 0xFF) |
-                             (idx == 0 ? ((p != first) | (pl != 0)) : (pl > p - first));
-            fail |= walk & bad;
-            const bool ok = walk & !bad;
-            mine = j == g ? ok : mine;
-            mp = ((j == g) & ok) ? p : mp;
+            const uint32_t pn = p - min(pl, p - first);
+            mp = j == g ? p : mp;
             me = j == g ? expect : me;
-            mi = j == g ? idx : mi;
-            expect = ok ? p : expect;
-            p = ok ? p - pl : p;
-            k += ok;
-            walk = ok & (k < N);
+            expect = p;
+            p = pn;
         }
-        // my entry: every field of its header from registers, as selects (no per-encoding
-        // branches), then the checks of one forward step and the descriptor
+        // my entry (index idx = N-1-mk): every field of its header from registers, as selects
+        // (no per-encoding branches); it must end where the entry after it starts (me) — which
+        // makes every prevlen the size of the entry before it — and its prevlen must stay inside
+        // the entries; entry 0 sits right after the header with prevlen 0
+        const uint32_t mk = rounds * G + g;
+        const bool mine = mk < N;
+        const uint32_t idx = N - 1 - mk;
         uint32_t b[4];
         R.template get<4>(mp, b);
         const uint32_t b0 = b[0] & 0xFF;
         const bool big = b0 >= 254;
+        const uint32_t pl = big ? ab(b[1], b[0], 1) : b0;
         const uint32_t qp = mp + (big ? 5u : 1u);
         const uint32_t e = big ? (b[1] >> 8) & 0xFF : (b[0] >> 8) & 0xFF;
         const uint32_t x1 = big ? (b[1] >> 16) & 0xFF : (b[0] >> 16) & 0xFF;
@@ -814,23 +822,26 @@ __device__ __forceinline__ bool do_ziplist_bg(const Src &R, const Lane &l, bool 
         const uint32_t isz = (uint32_t)(e == 0xFE) + 2 * (uint32_t)(e == 0xC0) + 3 * (uint32_t)(e == 0xF0) +
                              4 * (uint32_t)(e == 0xD0) + 8 * (uint32_t)(e == 0xE0);
         const uint64_t endp = (uint64_t)qp + (zstr ? ls + sl : 1 + isz);
-        const bool bad = (big & (mp + 5 > zlast)) | (qp >= zlast) | (mi + 1 >= l.r) | (!zstr & !imm & (isz == 0)) |
-                         (zstr & (qp + ls > zlast)) | (endp != (uint64_t)me);
+        const bool bad = (mp < first) | (mp >= zlast) | (b0 == 0xFF) | (big & (mp + 5 > zlast)) | (qp >= zlast) |
+                         (idx + 1 >= l.r) | (!zstr & !imm & (isz == 0)) | (zstr & (qp + ls > zlast)) |
+                         (endp != (uint64_t)me) |
+                         (idx == 0 ? ((mp != first) | (pl != 0)) : (pl > mp - first));
         fail |= mine & bad;
         const uint32_t sh = (32 - 8 * isz) & 31;
         const int64_t v32 = (int32_t)(lo << sh) >> sh;
         const int64_t iv = isz == 8 ? (int64_t)((uint64_t)lo | ((uint64_t)hi << 32)) : imm ? (int64_t)(e & 0x0F) - 1 : v32;
-        put_desc(l.E, (mine & !bad) ? l.slot(mi + 1) : NOSLOT, zstr ? l.B + qp + ls : (uint64_t)iv, zstr ? sl : 0,
+        put_desc(l.E, (mine & !bad) ? l.slot(idx + 1) : NOSLOT, zstr ? l.B + qp + ls : (uint64_t)iv, zstr ? sl : 0,
                  zstr ? RR_K_STR : RR_K_INT, zstr ? (e & 0xC0) : e);
-        if (__ballot(walk) == 0) break;
+        if (__ballot((rounds + 1) * G < N) == 0) break;
     }
     // one verdict for the whole group
     const uint32_t base = lane_id() - g;
     const uint64_t gm = (G >= 64 ? ~0ull : ((1ull << G) - 1)) << base;
     const bool gfail = (__ballot(fail) & gm) != 0;
-    const bool ok = !gfail && k == N && (N & 1) == 0 && (endbyte >> (8 * (zlast & 3)) & 0xFF) == 0xFF &&
-                    (N > 0 || (z[1] == 10 && first == zlast));
-    n = 1 + N;
+    const uint32_t zllen = z[2] & 0xFFFF;
+    const bool ok = !gfail && (zllen & 1) == 0 && (endbyte >> (8 * (zlast & 3)) & 0xFF) == 0xFF &&
+                    (zllen > 0 || (z[1] == 10 && first == zlast));
+    n = 1 + zllen;
     return !ok || n != l.r;
 }
 

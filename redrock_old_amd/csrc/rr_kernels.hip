@@ -728,6 +728,17 @@ __device__ RR_COLD Acc exact_value(const uint8_t *__restrict__ blob, uint64_t v,
 #if RR_ZL_BACK
 constexpr uint32_t ZL_VPB = RR_ZL_VPB;
 #endif
+// hash tables: 1 = grouped walks (do_ht_g) whenever the batch gives a value enough lanes to
+// hold its keys, with RR_HH_VPB hashes / RR_HT_VPB sets per batch; 0 = lane per value (do_ht)
+#ifndef RR_HT_GROUPED
+#define RR_HT_GROUPED 1
+#endif
+#ifndef RR_HH_VPB
+#define RR_HH_VPB 8
+#endif
+#ifndef RR_HT_VPB
+#define RR_HT_VPB 16
+#endif
 // class batch order: heaviest walks first (longest-job-first over the window's waves)
 #ifndef RR_DEC_ORDER
 #define RR_DEC_ORDER C_ZL, C_SL, C_HH, C_HT, C_LIST, C_EXACT, C_IS, C_STR
@@ -782,7 +793,7 @@ __device__ __forceinline__ Acc run_batch(const Src &src, uint32_t c, bool active
             enc = H.f5();
         } else if (c == C_LIST) {
             fail = do_list_g(src, l, active, G, g, ne, vp);
-        } else if (c == C_HT || c == C_HH) {   // lane per value (G == 1) unless RR_HT_GROUPED
+        } else if (c == C_HT || c == C_HH) {   // grouped (G > 1) or lane per value (do_ht)
             if (G > 1) fail = do_ht_g(src, H, l, active, G, g, ne, vp, fixup, c == C_HH);
             else fail = do_ht(src, H, l, active, ne, vp, fixup, c == C_HH);
         } else if (c == C_SL) {
@@ -845,6 +856,19 @@ extern "C" int rr_probe_set(void *p) { return hipMemcpyToSymbol(HIP_SYMBOL(g_pro
 #endif
 constexpr uint32_t DEC_BL = RR_DEC_BL;
 static_assert(DEC_BL >= 2 && DEC_BL <= RR_WAVE && DEC_BL % 2 == 0, "batch lanes");
+// values per batch of a class (a class with more values in the chunk gets several batches)
+__device__ __forceinline__ uint32_t class_vpb(uint32_t c) {
+#if RR_ZL_BACK
+    if (c == C_ZL) return ZL_VPB;
+#else
+    if (c == C_ZL) return DEC_BL / 2;   // two lanes each
+#endif
+#if RR_HT_GROUPED
+    if (c == C_HH) return RR_HH_VPB;
+    if (c == C_HT) return RR_HT_VPB;
+#endif
+    return DEC_BL;
+}
 // 1: the mirror-arena copy is written by waves that ran out of walk batches (step 4), not
 // during staging
 #ifndef RR_DEC_LATECOPY
@@ -920,7 +944,8 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
     __shared__ uint16_t perm[PMAX];
     __shared__ uint32_t ccount[C_N], cbase[C_N], ccur[C_N], bpre[C_N + 1];
     __shared__ uint32_t next_batch;
-    __shared__ uint32_t next_copy;
+    __shared__ uint32_t next_copy;   // (late-copy and persistent builds)
+    (void)next_copy;
     __shared__ uint64_t red[2][NW];
     PROBE(__shared__ uint64_t prb[PROBE_WORDS]; uint64_t pt0 = __builtin_amdgcn_s_memtime(), pt1 = 0, pt2 = 0;
           if (threadIdx.x < PROBE_WORDS) prb[threadIdx.x] = 0;)
@@ -1212,11 +1237,7 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
             uint32_t s = 0, bs = 0;
             for (uint32_t k = 0; k < C_N; ++k) {
                 const uint32_t c = CLASS_ORDER[k];
-#if RR_ZL_BACK
-                const uint32_t vpb = c == C_ZL ? ZL_VPB : DEC_BL;
-#else
-                const uint32_t vpb = c == C_ZL ? DEC_BL / 2 : DEC_BL;   // ziplists: two lanes each
-#endif
+                const uint32_t vpb = class_vpb(c);
                 cbase[c] = s;
                 bpre[k] = bs;
                 s += ccount[c];
@@ -1267,11 +1288,7 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
             uint32_t k = 0;
             while (bi >= bpre[k + 1]) ++k;
             const uint32_t c = CLASS_ORDER[k];
-#if RR_ZL_BACK
-            const uint32_t vpb = c == C_ZL ? ZL_VPB : DEC_BL;
-#else
-            const uint32_t vpb = c == C_ZL ? DEC_BL / 2 : DEC_BL;
-#endif
+            const uint32_t vpb = class_vpb(c);
             const uint32_t first = cbase[c] + (bi - bpre[k]) * vpb;
             const uint32_t cnt = min(ccount[c] - (bi - bpre[k]) * vpb, vpb);
 #ifdef RR_SKIP_CLASSES   // timing-only builds (tools/): skip the batches of these classes
@@ -1281,7 +1298,7 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
             // lanes per value: ziplists 2 (two-ended walk), chained classes 64 / cnt (grouped walks)
             const bool grouped = c == C_LIST || c == C_SL || c == C_IS || (RR_ZL_BACK && c == C_ZL);
             const uint32_t Gw = max(1u, min(GMAX, (uint32_t)RR_WAVE / cnt));
-#ifdef RR_HT_GROUPED   // timing builds (tools/): grouped hash-table walks (measured slower)
+#if RR_HT_GROUPED   // grouped hash-table walks when a value gets lanes enough for its keys
             const bool htg = (c == C_HT || c == C_HH) && Gw >= ht_group_min(c == C_HH);
 #else
             const bool htg = false;
