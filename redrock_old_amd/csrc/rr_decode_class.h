@@ -469,44 +469,52 @@ __device__ __forceinline__ bool do_skiplist(const Src &R, const Head &H, const L
 // the group's lane 0 records the value.
 constexpr uint32_t GMAX = 16;
 
-// ---- List (rock_serdes.c:162-214), grouped: {u32 len, bytes}* to the end
+// One verdict for a grouped value: any lane's failure fails the whole group
+__device__ __forceinline__ bool group_any(bool x, uint32_t G, uint32_t g) {
+    const uint32_t base = lane_id() - g;
+    const uint64_t gm = (G >= 64 ? ~0ull : ((1ull << G) - 1)) << base;
+    return (__ballot(x) & gm) != 0;
+}
+
+// ---- List (rock_serdes.c:162-214), grouped: {u32 len, bytes}* to the end.  The chain takes
+// exactly the value's reservation of elements (count_kernel counted the ones that parse) with
+// no checks — a read and an add per element, the position clamped to the value; each lane then
+// checks its own elements' length fields (and that the last one ends the value) and stores
+// them.  The verdicts are those of one walk to the end.
 template <class Src>
 __device__ __forceinline__ bool do_list_g(const Src &R, const Lane &l, bool active, uint32_t G, uint32_t g,
                                           uint32_t &n, uint64_t &pay) {
-    uint32_t p = l.q + 5, k = 0;   // k: index of the element that starts at p
-    const uint32_t end = l.q + l.L;
-    bool fail = false, walk = active && p != end;
-    for (;;) {
-        uint32_t mp = 0, ml = 0, mk = 0;
-        bool mine = false;
+    const uint32_t end = l.q + l.L, r = active ? l.r : 0u;
+    uint32_t p = l.q + 5;
+    bool fail = active && r == 0 && p != end;
+    for (uint32_t rounds = 0;; ++rounds) {
+        uint32_t mp = l.q;
         for (uint32_t j = 0; j < G; ++j) {
             uint32_t x[1];
             R.template get<1>(p, x);
-            const uint32_t len = x[0], rem = end - p;
-            const bool bad = (rem < 4) | (len > rem - 4) | (k >= l.r);
-            fail |= walk & bad;
-            const bool ok = walk & !bad;
-            mine = j == g ? ok : mine;
+            const uint32_t rem = end - p;
             mp = j == g ? p : mp;
-            ml = j == g ? len : ml;
-            mk = j == g ? k : mk;
-            p = ok ? p + 4 + len : p;
-            k += ok;
-            walk = ok & (p != end);
+            p = min(p + 4 + min(x[0], rem), end);
         }
         // my element: integer or string (zipTryEncoding, as quicklistPushTail stores it)
+        const uint32_t mk = rounds * G + g;
+        const bool mine = mk < r;
         uint32_t b[6];
         R.template get<6>(mp, b);
+        const uint32_t ml = b[0], rem = end - mp;
+        const bool bad = (rem < 4) | (ml > rem - 4) | ((mk + 1 == r) & (mp + 4 + ml != end));
+        fail |= mine & bad;
         const uint32_t d[5] = {b[1], b[2], b[3], b[4], b[5]};
         int64_t iv;
         const bool isint = regs_try_int(d, ml, iv);
-        put_desc(l.E, mine ? l.slot(mk) : NOSLOT, isint ? (uint64_t)iv : l.B + mp + 4, isint ? 0 : ml,
+        const bool st = mine & !bad;
+        put_desc(l.E, st ? l.slot(mk) : NOSLOT, isint ? (uint64_t)iv : l.B + mp + 4, isint ? 0 : ml,
                  isint ? RR_K_INT : RR_K_STR, 0);
-        pay += mine && !isint ? ml : 0;
-        if (__ballot(walk) == 0) break;
+        pay += st && !isint ? ml : 0;
+        if (__ballot((rounds + 1) * G < r) == 0) break;
     }
-    n = k;
-    return fail || k != l.r;
+    n = r;
+    return group_any(fail, G, g);
 }
 
 // ---- Set / Hash hash tables, grouped.  The chain steps read only the u64 length fields (every
@@ -595,50 +603,54 @@ __device__ __forceinline__ bool do_ht_g(const Src &R, const Head &H, const Lane 
     return gfail || !cnt_ok;
 }
 
-// ---- ZSet skiplist, grouped: a step takes one (member, score) pair — the member's length
-// field, then the score after it (a second, dependent read); the order and NaN checks run on
-// every lane (see do_skiplist)
+// ---- ZSet skiplist, grouped: the chain takes the reservation's pairs with no checks (a read
+// and an add per pair: {u64 l, member, f64 score}); each lane then checks its pairs' length
+// fields and scores — the order / NaN check (see do_skiplist) against the previous pair's
+// score, from the lane before it or, for a round's first pair, from the previous round's last
 template <class Src>
 __device__ __forceinline__ bool do_skiplist_g(const Src &R, const Head &H, const Lane &l, bool active, uint32_t G,
                                               uint32_t g, uint32_t &n, uint64_t &pay) {
     const uint64_t cnt = H.u5();
-    uint32_t p = l.q + 13, k = 0;   // k: pairs
-    const uint32_t end = l.q + l.L;
-    bool fail = false, walk = active && p != end;
-    double prev = 0.0;
-    for (;;) {
-        uint32_t mp = 0, ml = 0, mk = 0, s0 = 0, s1 = 0;
-        bool mine = false;
+    const uint32_t end = l.q + l.L, r = active ? l.r : 0u, np = r >> 1;   // np: pairs
+    uint32_t p = l.q + 13;
+    bool fail = active && ((r & 1) || (uint64_t)np != cnt || (np == 0 && p != end));
+    const uint32_t base = lane_id() - g;
+    uint32_t clo = 0, chi = 0;   // the previous round's last score
+    for (uint32_t rounds = 0;; ++rounds) {
+        uint32_t mp = l.q;
         for (uint32_t j = 0; j < G; ++j) {
-            uint32_t a[2], c[2];
-            R.template get<2>(p, a);
+            uint32_t x[1];
+            R.template get<1>(p, x);
             const uint32_t rem = end - p;
-            const bool bad1 = (rem < 16) | (a[1] != 0) | (a[0] > rem - 16) | (2 * k + 1 >= l.r);
-            const uint32_t sp = p + 8 + a[0];
-            R.template get<2>(bad1 ? p : sp, c);
-            const double sc = __longlong_as_double((long long)((uint64_t)c[0] | ((uint64_t)c[1] << 32)));
-            const bool order = k == 0 ? !(sc != sc) : sc < prev;
-            const bool bad = bad1 | !order;
-            fail |= walk & bad;
-            const bool ok = walk & !bad;
-            mine = j == g ? ok : mine;
             mp = j == g ? p : mp;
-            ml = j == g ? a[0] : ml;
-            mk = j == g ? k : mk;
-            s0 = j == g ? c[0] : s0;
-            s1 = j == g ? c[1] : s1;
-            prev = ok ? sc : prev;
-            p = ok ? sp + 8 : p;
-            k += ok;
-            walk = ok & (p != end);
+            p = min(p + 16 + min(x[0], rem), end);
         }
-        put_desc(l.E, mine ? l.slot(2 * mk) : NOSLOT, l.B + mp + 8, ml, RR_K_STR, 0);
-        put_desc(l.E, mine ? l.slot(2 * mk + 1) : NOSLOT, (uint64_t)s0 | ((uint64_t)s1 << 32), 0, RR_K_SCORE, 0);
-        pay += mine ? ml : 0;
-        if (__ballot(walk) == 0) break;
+        const uint32_t mk = rounds * G + g;
+        const bool mine = mk < np;
+        uint32_t a[2], c[2];
+        R.template get<2>(mp, a);
+        const uint32_t ml = a[0], rem = end - mp;
+        const bool bad1 = (rem < 16) | (a[1] != 0) | (ml > rem - 16) | ((mk + 1 == np) & (mp + 16 + ml != end));
+        R.template get<2>((mine & !bad1) ? mp + 8 + ml : l.q, c);
+        const double sc = __longlong_as_double((long long)((uint64_t)c[0] | ((uint64_t)c[1] << 32)));
+        const uint32_t plo = (uint32_t)__shfl((int)c[0], (int)(base + (g ? g - 1 : 0)), RR_WAVE);
+        const uint32_t phi = (uint32_t)__shfl((int)c[1], (int)(base + (g ? g - 1 : 0)), RR_WAVE);
+        const double prev = __longlong_as_double((long long)(g ? ((uint64_t)plo | ((uint64_t)phi << 32))
+                                                               : ((uint64_t)clo | ((uint64_t)chi << 32))));
+        clo = (uint32_t)__shfl((int)c[0], (int)(base + G - 1), RR_WAVE);
+        chi = (uint32_t)__shfl((int)c[1], (int)(base + G - 1), RR_WAVE);
+        // strictly below the previous score (pair 0: not NaN)
+        const bool order = mk == 0 ? !(sc != sc) : sc < prev;
+        const bool bad = bad1 | !order;
+        fail |= mine & bad;
+        const bool st = mine & !bad;
+        put_desc(l.E, st ? l.slot(2 * mk) : NOSLOT, l.B + mp + 8, ml, RR_K_STR, 0);
+        put_desc(l.E, st ? l.slot(2 * mk + 1) : NOSLOT, (uint64_t)c[0] | ((uint64_t)c[1] << 32), 0, RR_K_SCORE, 0);
+        pay += st ? ml : 0;
+        if (__ballot((rounds + 1) * G < np) == 0) break;
     }
-    n = 2 * k;
-    return fail || (uint64_t)k != cnt || 2 * k != l.r;
+    n = r;
+    return group_any(fail, G, g);
 }
 
 // ---- intset, grouped: members at fixed positions, lane g takes members g, g + G, ...; the

@@ -739,6 +739,9 @@ constexpr uint32_t ZL_VPB = RR_ZL_VPB;
 #ifndef RR_HT_VPB
 #define RR_HT_VPB 16
 #endif
+#ifndef RR_LIST_VPB   // Lists per batch (grouped: fewer Lists per batch, more lanes per List)
+#define RR_LIST_VPB 64
+#endif
 // class batch order: heaviest walks first (longest-job-first over the window's waves)
 #ifndef RR_DEC_ORDER
 #define RR_DEC_ORDER C_ZL, C_SL, C_HH, C_HT, C_LIST, C_EXACT, C_IS, C_STR
@@ -867,6 +870,7 @@ __device__ __forceinline__ uint32_t class_vpb(uint32_t c) {
     if (c == C_HH) return RR_HH_VPB;
     if (c == C_HT) return RR_HT_VPB;
 #endif
+    if (c == C_LIST) return RR_LIST_VPB;
     return DEC_BL;
 }
 // 1: the mirror-arena copy is written by waves that ran out of walk batches (step 4), not
@@ -895,6 +899,9 @@ __device__ __forceinline__ uint32_t class_vpb(uint32_t c) {
 // the guarded copy made the compiler wait for each store's acknowledgement before the next.
 #ifndef RR_DEC_BFREE
 #define RR_DEC_BFREE 1
+#endif
+#ifndef RR_DEC_KE   // window granules per thread loaded before the class bytes (the rest after)
+#define RR_DEC_KE 2
 #endif
 #if RR_DEC_BFREE
 #define DEC_SYNC() lds_barrier()
@@ -964,10 +971,35 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
     (void)nwin;
     (void)it;
 #endif
-    const uint64_t v_lo = first_val[tile], v_hi = first_val[tile + 1];
     const uint64_t padded = (offsets[n] + 15) & ~15ull;
     const uint64_t W0 = (uint64_t)tile * W;
     const uint64_t W1 = W0 + W < padded ? W0 + W : padded;
+    // the arena copy starts at the call's first value (a call over a slice of a larger buffer —
+    // the chunks of rr_decode_batch_host — copies only its own bytes); the stage always lies
+    // past it (S0 >= offsets[v_lo] >= offsets[0])
+    const uint64_t A0 = W0 > (offsets[0] & ~15ull) ? W0 : (offsets[0] & ~15ull);
+#if RR_DEC_OVL && RR_DEC_BFREE
+    // the window's own granules [A0, W1) first: their range needs only offsets[0] and
+    // offsets[n], not first_val -> offsets, so the loads go out at the window's start; the
+    // stage's tail [W1, ov_e) (the last values' bytes past the window) follows the sort.  The
+    // arena gets [A0, W1) (stores past it are dropped); g = A0 / 16 + tid + k * NT is at byte
+    // offset 16 (tid + k NT)
+    constexpr uint32_t KM = W / 16 / NT;   // granules per thread of a whole window
+    static_assert(W % (16 * NT) == 0, "window granules per thread");
+    const uint64_t ov_a = A0 >> 4, ov_w1 = W1 >> 4;
+    const uint32_t ov_mb = ov_w1 > ov_a ? (uint32_t)((ov_w1 - ov_a) * 16) : 0u;
+    const rsrc_t ov_RM = make_rsrc(blob + A0, ov_mb);
+    const rsrc_t ov_RA = make_rsrc(arena + A0, ov_mb);
+    // KE granules per thread go out before the first_val -> offsets / class-byte loads, the rest
+    // after the class bytes: the sort waits (vmcnt, in issue order) for the class bytes and
+    // therefore for the early granules only
+    constexpr uint32_t KE = RR_DEC_KE < KM ? RR_DEC_KE : KM;
+    u32x4 ov_m[KM];
+#pragma unroll
+    for (uint32_t k = 0; k < KE; ++k)
+        ov_m[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ov_RM, (int)((tid + k * NT) * 16), 0, 0));
+#endif
+    const uint64_t v_lo = first_val[tile], v_hi = first_val[tile + 1];
     uint64_t S0 = W0, S1 = W0;
     if (v_hi > v_lo) {
         S0 = offsets[v_lo] & ~15ull;
@@ -975,10 +1007,6 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
     }
     const bool staged = S1 - S0 <= STAGE;
     const uint64_t cap = elem_cap < 0xFFFFFFFFull ? elem_cap : 0xFFFFFFFFull;   // elem_base is 32-bit
-    // the arena copy starts at the call's first value (a call over a slice of a larger buffer —
-    // the chunks of rr_decode_batch_host — copies only its own bytes); the stage always lies
-    // past it (S0 >= offsets[v_lo] >= offsets[0])
-    const uint64_t A0 = W0 > (offsets[0] & ~15ull) ? W0 : (offsets[0] & ~15ull);
 
     // the first chunk's class bytes, loaded before the copy so their latency hides under it
     uint32_t cls0[PMAX / NT];
@@ -987,6 +1015,11 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
         const uint64_t v = v_lo + j * NT + tid;
         cls0[j] = v < v_hi ? (uint32_t)cls[v] : C_N;
     }
+#if RR_DEC_OVL && RR_DEC_BFREE
+#pragma unroll
+    for (uint32_t k = KE; k < KM; ++k)
+        ov_m[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ov_RM, (int)((tid + k * NT) * 16), 0, 0));
+#endif
 
 #if RR_DEC_LATECOPY
     // 1. value bytes -> LDS only; the window's arena copy is written in step 4 by waves that
@@ -1030,15 +1063,9 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
     //      arena stores and the LDS stage writes follow the sort (plain loads survive its
     //      barriers).  The sort reads no global memory, so none of its waits drain them.
     const uint64_t eb0 = ebase[v_lo], eb1 = ebase[v_hi];
-    const uint64_t ov_w1 = W1 >> 4, ov_s0 = S0 >> 4, ov_e = (staged && S1 > W1 ? S1 : W1) >> 4;
+    const uint64_t ov_s0 = S0 >> 4, ov_e = (staged && S1 > W1 ? S1 : W1) >> 4;
     const bool ovl = !(RR_DEC_PF && it > 0);
-    u32x4 ov_x[RR_DEC_OVL_K];
 #if RR_DEC_BFREE
-    // the window's granules [A0, ov_e) (loads past it read zeros), the arena's [A0, ov_w1)
-    // (stores past it are dropped); g = A0 / 16 + tid + k * NT is at byte offset 16 (tid + k NT)
-    const uint64_t ov_a = A0 >> 4;
-    const rsrc_t ov_RL = make_rsrc(blob + A0, ov_e > ov_a ? (uint32_t)((ov_e - ov_a) * 16) : 0u);
-    const rsrc_t ov_RA = make_rsrc(arena + A0, ov_w1 > ov_a ? (uint32_t)((ov_w1 - ov_a) * 16) : 0u);
     typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
     lds_u32x4 *ov_lds = (lds_u32x4 *)(__attribute__((address_space(3))) uint8_t *)stage;
     // granule g's stage slot, or the dummy slot just past the stage (reads past the stage see
@@ -1046,40 +1073,33 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
     auto ov_slot = [&](uint64_t g) __attribute__((always_inline)) -> uint32_t {
         return (staged & (g >= ov_s0) & (g < ov_e)) ? (uint32_t)(g - ov_s0) : STAGE / 16;
     };
-#pragma unroll
-    for (int k = 0; k < RR_DEC_OVL_K; ++k)
-        ov_x[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ov_RL, (int)((tid + k * NT) * 16), 0, 0));
     auto ov_finish = [&]() __attribute__((always_inline)) {
 #pragma unroll
-        for (int k = 0; k < RR_DEC_OVL_K; ++k) {
-            const uint32_t o = (tid + k * NT) * 16;
+        for (uint32_t k = 0; k < KM; ++k) {
 #ifndef RR_ABLATE_NOCOPY
-            __builtin_amdgcn_raw_buffer_store_b128(ov_x[k], ov_RA, (int)o, 0, 2 /* nt */);
+            __builtin_amdgcn_raw_buffer_store_b128(ov_m[k], ov_RA, (int)((tid + k * NT) * 16), 0, 2 /* nt */);
 #endif
-            ov_lds[ov_slot(ov_a + tid + (uint64_t)k * NT)] = ov_x[k];
+            ov_lds[ov_slot(ov_a + tid + (uint64_t)k * NT)] = ov_m[k];
         }
-        // the rest of the window (beyond the prefetched granules): wave-uniform rounds
-        const uint64_t tot = ov_e > ov_a ? ov_e - ov_a : 0;
-        const uint32_t rounds = tot > (uint64_t)RR_DEC_OVL_K * NT ? (uint32_t)((tot - (uint64_t)RR_DEC_OVL_K * NT + NT - 1) / NT) : 0u;
+        // the stage's tail [W1, ov_e): LDS only, wave-uniform rounds
+        const uint64_t t0 = ov_w1 > ov_a ? ov_w1 : ov_a;
+        const rsrc_t RT = make_rsrc(blob + t0 * 16, ov_e > t0 ? (uint32_t)((ov_e - t0) * 16) : 0u);
+        const uint32_t rounds = ov_e > t0 ? (uint32_t)((ov_e - t0 + NT - 1) / NT) : 0u;
         for (uint32_t r = 0; r < rounds; r += 4) {
             u32x4 x[4];
 #pragma unroll
-            for (int k = 0; k < 4; ++k)
-                x[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                     ov_RL, (int)((tid + (RR_DEC_OVL_K + r + k) * NT) * 16), 0, 0));
+            for (uint32_t k = 0; k < 4; ++k)
+                x[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(RT, (int)((tid + (r + k) * NT) * 16), 0, 0));
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const uint32_t o = (tid + (RR_DEC_OVL_K + r + k) * NT) * 16;
-#ifndef RR_ABLATE_NOCOPY
-                __builtin_amdgcn_raw_buffer_store_b128(x[k], ov_RA, (int)o, 0, 2 /* nt */);
-#endif
-                ov_lds[ov_slot(ov_a + tid + (uint64_t)(RR_DEC_OVL_K + r + k) * NT)] = x[k];
-            }
+            for (uint32_t k = 0; k < 4; ++k)
+                if (r + k < rounds) ov_lds[ov_slot(t0 + tid + (uint64_t)(r + k) * NT)] = x[k];
         }
     };
     if (ovl) {
     } else
 #else
+    const uint64_t ov_w1 = W1 >> 4;
+    u32x4 ov_x[RR_DEC_OVL_K];
     if (ovl) {
         const u32x4 *src = reinterpret_cast<const u32x4 *>(blob);
 #pragma unroll
