@@ -900,6 +900,9 @@ __device__ __forceinline__ uint32_t class_vpb(uint32_t c) {
 #ifndef RR_DEC_BFREE
 #define RR_DEC_BFREE 1
 #endif
+#ifndef RR_DEC_PRIO   // wave priority during the walks (0: none; see the batch loop)
+#define RR_DEC_PRIO 0
+#endif
 #ifndef RR_DEC_KE   // window granules per thread loaded before the class bytes (the rest after)
 #define RR_DEC_KE 2
 #endif
@@ -1019,6 +1022,13 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
 #pragma unroll
     for (uint32_t k = KE; k < KM; ++k)
         ov_m[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ov_RM, (int)((tid + k * NT) * 16), 0, 0));
+    // the stage's tail [W1, S1): at most SLACK bytes, one granule per thread, also in flight
+    // under the sort
+    static_assert(SLACK / 16 <= NT, "stage tail granules per thread");
+    const uint64_t ov_t0 = ov_w1 > ov_a ? ov_w1 : ov_a;
+    const uint64_t ov_te = (staged && S1 > W1 ? S1 : W1) >> 4;
+    const u32x4 ov_t = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+        make_rsrc(blob + ov_t0 * 16, ov_te > ov_t0 ? (uint32_t)((ov_te - ov_t0) * 16) : 0u), (int)(tid * 16), 0, 0));
 #endif
 
 #if RR_DEC_LATECOPY
@@ -1081,19 +1091,8 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
 #endif
             ov_lds[ov_slot(ov_a + tid + (uint64_t)k * NT)] = ov_m[k];
         }
-        // the stage's tail [W1, ov_e): LDS only, wave-uniform rounds
-        const uint64_t t0 = ov_w1 > ov_a ? ov_w1 : ov_a;
-        const rsrc_t RT = make_rsrc(blob + t0 * 16, ov_e > t0 ? (uint32_t)((ov_e - t0) * 16) : 0u);
-        const uint32_t rounds = ov_e > t0 ? (uint32_t)((ov_e - t0 + NT - 1) / NT) : 0u;
-        for (uint32_t r = 0; r < rounds; r += 4) {
-            u32x4 x[4];
-#pragma unroll
-            for (uint32_t k = 0; k < 4; ++k)
-                x[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(RT, (int)((tid + (r + k) * NT) * 16), 0, 0));
-#pragma unroll
-            for (uint32_t k = 0; k < 4; ++k)
-                if (r + k < rounds) ov_lds[ov_slot(t0 + tid + (uint64_t)(r + k) * NT)] = x[k];
-        }
+        // the stage's tail [W1, ov_e): LDS only
+        ov_lds[ov_slot(ov_t0 + tid)] = ov_t;
     };
     if (ovl) {
     } else
@@ -1315,6 +1314,11 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
             if ((RR_SKIP_CLASSES >> c) & 1) continue;
 #endif
             PROBE(const uint64_t tb0 = __builtin_amdgcn_s_memtime();)
+#if RR_DEC_PRIO == 1   // the long chained classes issue ahead of the other waves of their SIMD
+            if (c == C_HH || c == C_ZL || c == C_LIST || c == C_HT) __builtin_amdgcn_s_setprio(2);
+#elif RR_DEC_PRIO == 2   // every walk ahead of the copy / sort phases of the other workgroup
+            __builtin_amdgcn_s_setprio(1);
+#endif
             // lanes per value: ziplists 2 (two-ended walk), chained classes 64 / cnt (grouped walks)
             const bool grouped = c == C_LIST || c == C_SL || c == C_IS || (RR_ZL_BACK && c == C_ZL);
             const uint32_t Gw = max(1u, min(GMAX, (uint32_t)RR_WAVE / cnt));
@@ -1335,6 +1339,9 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
 #else   // timing-only builds (tools/): no unstaged walks (wrong for windows that overflow the stage)
             const Acc a = run_batch(lsrc, c, active, v, G, g, S0, E, eb0, blob, offsets, ebase, values, elems, cap, fix);
             (void)gsrc;
+#endif
+#if RR_DEC_PRIO
+            __builtin_amdgcn_s_setprio(0);
 #endif
             bad += a.bad;
             pay += a.pay;
