@@ -575,25 +575,35 @@ __device__ __forceinline__ bool do_ht_g(const Src &R, const Head &H, const Lane 
         for (uint32_t q = 0; q < HT_G_ROUNDS; ++q) fps[q] = rounds == q ? f : fps[q];
         if (__ballot((rounds + 1) * G < r) == 0) break;
     }
-    // duplicate keys: my keys against every other lane's (rotation d) and against each other
-    bool dup = false;
+    // duplicate keys: each key packed with its group's id (lane / G; G is a power of two <= 16
+    // here, so a group never straddles a 16-lane DPP row), non-keys get values no key can have
+    // and no other slot shares; then my keys against each other and against those of the lanes
+    // d = 1 .. G-1 away in my row (DPP row rotations: no LDS round trips), so an equal pair is
+    // a repeated fingerprint within one value
     const uint32_t RU = rounds + 1 < HT_G_ROUNDS ? rounds + 1 : HT_G_ROUNDS;   // rounds holding keys
     const uint32_t base = lane_id() - g;
+    const uint32_t gid = lane_id() / G;
+    uint32_t fpp[HT_G_ROUNDS];
+#pragma unroll
+    for (uint32_t q = 0; q < HT_G_ROUNDS; ++q)
+        fpp[q] = fps[q] != 0xFFFFFFFFu ? (gid << 16) | fps[q] : 0xFFFF0000u | (lane_id() << 2) | q;
+    bool dup = false;
 #pragma unroll
     for (uint32_t a = 0; a < HT_G_ROUNDS; ++a)
 #pragma unroll
-        for (uint32_t b = a + 1; b < HT_G_ROUNDS; ++b) dup |= (fps[a] == fps[b]) & (fps[a] != 0xFFFFFFFFu);
-    for (uint32_t d = 1; d < G; ++d) {
-        uint32_t src = g + d;
-        src = base + (src >= G ? src - G : src);
-#pragma unroll
-        for (uint32_t q = 0; q < HT_G_ROUNDS; ++q) {
-            if (q >= RU) break;
-            const uint32_t x = (uint32_t)__shfl((int)fps[q], (int)src, RR_WAVE);
-#pragma unroll
-            for (uint32_t qq = 0; qq < HT_G_ROUNDS; ++qq) dup |= (fps[qq] == x) & (x != 0xFFFFFFFFu);
-        }
+        for (uint32_t b = a + 1; b < HT_G_ROUNDS; ++b) dup |= fpp[a] == fpp[b];
+#define RR_HT_ROT(D)                                                                                   \
+    if ((D) < G) {                                                                                     \
+        _Pragma("unroll") for (uint32_t q = 0; q < HT_G_ROUNDS; ++q) {                                 \
+            if (q < RU) {                                                                              \
+                const uint32_t x = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)fpp[q], 0x120 + (D), 0xF, 0xF, false); \
+                _Pragma("unroll") for (uint32_t qq = 0; qq < HT_G_ROUNDS; ++qq) dup |= (qq < RU) & (fpp[qq] == x); \
+            }                                                                                          \
+        }                                                                                              \
     }
+    RR_HT_ROT(1) RR_HT_ROT(2) RR_HT_ROT(3) RR_HT_ROT(4) RR_HT_ROT(5) RR_HT_ROT(6) RR_HT_ROT(7)
+    RR_HT_ROT(8) RR_HT_ROT(9) RR_HT_ROT(10) RR_HT_ROT(11) RR_HT_ROT(12) RR_HT_ROT(13) RR_HT_ROT(14) RR_HT_ROT(15)
+#undef RR_HT_ROT
     const uint64_t gm = (G >= 64 ? ~0ull : ((1ull << G) - 1)) << base;
     const bool gfail = (__ballot(fail) & gm) != 0;
     const bool dupg = (__ballot(dup & chk) & gm) != 0;

@@ -1327,7 +1327,9 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
 #else
             const bool htg = false;
 #endif
-            const uint32_t G = __builtin_amdgcn_readfirstlane((c == C_ZL && !RR_ZL_BACK) ? 2u : (grouped || htg) ? Gw : 1u);
+            // (hash tables: a power of two, so a value's lanes lie in one DPP row, do_ht_g)
+            const uint32_t Gh = 1u << (31 - __builtin_clz(Gw));
+            const uint32_t G = __builtin_amdgcn_readfirstlane((c == C_ZL && !RR_ZL_BACK) ? 2u : grouped ? Gw : htg ? Gh : 1u);
             const uint32_t li = lane / G, g = lane - li * G;   // the value's index in the batch
             const bool active = li < cnt;
             const uint64_t v = c0 + (active ? perm[first + li] : 0u);
