@@ -518,3 +518,79 @@ def test_host_decode_without_arena(engine):
     assert rc == 0
     assert_flat_equal((vals, els[:int(t.n_elems)]), (hv, he), "arena = NULL")
     assert _payload_equal(he, ha, data)
+
+
+def _dense_class_batches(rng):
+    """Homogeneous batches of small values: a 64 KiB window then holds hundreds of one class,
+    so its batches carry 64 values (one or two lanes each: the grouped walks at G = 1, 2, 4)
+    as well as the partly filled last batch; sizes vary so windows see every G."""
+    def word(lo, hi):
+        return rng.integers(97, 123, int(rng.integers(lo, hi + 1)), dtype=np.uint8).tobytes()
+
+    def lst(k):
+        items = [str(int(rng.integers(-10**6, 10**6))).encode() if rng.random() < 0.5 else word(0, 12) for _ in range(k)]
+        return bytes([rr.T_LIST_QUICKLIST]) + struct.pack("<I", 5) + b"".join(struct.pack("<I", len(x)) + x for x in items)
+
+    def iset(k):
+        w = int(rng.choice([2, 4, 8]))
+        vals = sorted(set(int(x) for x in rng.integers(-(1 << (8 * w - 1)), (1 << (8 * w - 1)) - 1, k)))
+        return bytes([rr.T_SET_INTSET]) + struct.pack("<III", 3, w, len(vals)) + b"".join(
+            v.to_bytes(w, "little", signed=True) for v in vals)
+
+    def zl(t, k):
+        items = []
+        for i in range(k):
+            items += [word(1, 10) + str(i).encode(),
+                      (str(int(rng.integers(-10**9, 10**9))).encode() if rng.random() < 0.5 else word(0, 70))]
+        z = po.build_ziplist(items)
+        return bytes([t]) + struct.pack("<I", 11) + struct.pack("<Q", len(z)) + z
+
+    def sl(k):
+        pairs = sorted(((word(0, 9) + str(i).encode(), float(rng.integers(-10**6, 10**6)) + i / 7) for i in range(k)),
+                       key=lambda x: (x[1], x[0]), reverse=True)
+        return _sl_blob(pairs)
+
+    makers = {
+        "list": lambda k: lst(k),
+        "intset": lambda k: iset(max(k, 1)),
+        "set_ht": lambda k: _ht_blob(rr.T_SET_HT, [word(0, 8) + str(i).encode() for i in range(k)]),
+        "hash_ht": lambda k: _ht_blob(rr.T_HASH_HT, sum(([b"f%d" % i, word(0, 12)] for i in range(k)), [])),
+        "zset_sl": lambda k: sl(k),
+        "hash_zl": lambda k: zl(rr.T_HASH_ZIPLIST, k),
+        "zset_zl": lambda k: zl(rr.T_ZSET_ZIPLIST, k),
+    }
+    for name, mk in makers.items():
+        for kmax in (1, 3, 9):
+            yield f"{name} k<={kmax}", [mk(int(rng.integers(0, kmax + 1))) for _ in range(6000)]
+        # and with every 37th value cut short, grown by a byte or with a body byte flipped (the
+        # walks' failure paths; the oracle decides which values stay valid)
+        blobs = [mk(int(rng.integers(0, 4))) for _ in range(6000)]
+        for i in range(0, len(blobs), 37):
+            b, how = blobs[i], (i // 37) % 3
+            if how == 0:
+                b = b[:-1]
+            elif how == 1:
+                b = b + b"\x00"
+            elif len(b) > 14:
+                j = int(rng.integers(13, len(b)))
+                b = b[:j] + bytes([b[j] ^ (1 << int(rng.integers(0, 8)))]) + b[j + 1:]
+            blobs[i] = b
+        yield f"{name} damaged", blobs
+
+
+def test_dense_single_class_windows(engine):
+    """Windows holding hundreds of values of one class: every grouped walk at G = 1 / 2 / 4 and
+    with partly filled batches, against the C oracle, plus the byte-exact round trip."""
+    rng = np.random.default_rng(2024)
+    for what, blobs in _dense_class_batches(rng):
+        data, offs = batch_from_blobs(blobs)
+        v, e, a, t = engine.decode_host(data, offs)
+        ov, oe, oa, ot = cpu.decode(data, offs, nthreads=8)
+        assert_flat_equal((v, e), (ov, oe), what)
+        assert t == ot, what
+        if "damaged" in what:
+            assert t["n_bad"] > 0, what
+            continue
+        assert t["n_bad"] == 0, what
+        out, ooffs, t2 = engine.encode_host(v, e, a)
+        assert np.array_equal(out, data[:int(offs[-1])]), what
