@@ -894,9 +894,9 @@ __device__ __forceinline__ uint32_t class_vpb(uint32_t c) {
 // 1: the window's loads, arena stores and stage writes go through buffer resources with no
 // exec-mask branches (out-of-range loads read zeros, out-of-range stores are dropped, unstaged
 // granules are written to a dummy LDS slot), and the workgroup's barriers order LDS only.
-// With __syncthreads() (a workgroup-scope fence for all memory) every barrier waited for the
-// window's loads and for the acknowledgement of every arena store, and the branch joins of
-// the guarded copy made the compiler wait for each store's acknowledgement before the next.
+// The branch joins of the guarded copy made the compiler's wait-count pass wait for each
+// store's acknowledgement before the next store, and the conditional loads made the sort's
+// first barrier wait for all of them (vmcnt(0)).
 #ifndef RR_DEC_BFREE
 #define RR_DEC_BFREE 1
 #endif
