@@ -1022,13 +1022,16 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
 #pragma unroll
     for (uint32_t k = KE; k < KM; ++k)
         ov_m[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ov_RM, (int)((tid + k * NT) * 16), 0, 0));
-    // the stage's tail [W1, S1): at most SLACK bytes, one granule per thread, also in flight
+    // the stage's tail [W1, S1): at most SLACK bytes, KT granules per thread, also in flight
     // under the sort
-    static_assert(SLACK / 16 <= NT, "stage tail granules per thread");
+    constexpr uint32_t KT = (SLACK / 16 + NT - 1) / NT;
     const uint64_t ov_t0 = ov_w1 > ov_a ? ov_w1 : ov_a;
     const uint64_t ov_te = (staged && S1 > W1 ? S1 : W1) >> 4;
-    const u32x4 ov_t = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
-        make_rsrc(blob + ov_t0 * 16, ov_te > ov_t0 ? (uint32_t)((ov_te - ov_t0) * 16) : 0u), (int)(tid * 16), 0, 0));
+    const rsrc_t ov_RT = make_rsrc(blob + ov_t0 * 16, ov_te > ov_t0 ? (uint32_t)((ov_te - ov_t0) * 16) : 0u);
+    u32x4 ov_t[KT];
+#pragma unroll
+    for (uint32_t k = 0; k < KT; ++k)
+        ov_t[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ov_RT, (int)((tid + k * NT) * 16), 0, 0));
 #endif
 
 #if RR_DEC_LATECOPY
@@ -1092,7 +1095,8 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
             ov_lds[ov_slot(ov_a + tid + (uint64_t)k * NT)] = ov_m[k];
         }
         // the stage's tail [W1, ov_e): LDS only
-        ov_lds[ov_slot(ov_t0 + tid)] = ov_t;
+#pragma unroll
+        for (uint32_t k = 0; k < KT; ++k) ov_lds[ov_slot(ov_t0 + tid + (uint64_t)k * NT)] = ov_t[k];
     };
     if (ovl) {
     } else
