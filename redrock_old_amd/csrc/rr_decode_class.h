@@ -787,6 +787,10 @@ __device__ __forceinline__ bool do_ziplist(const Src &R, const Lane &l, bool act
 // ends at the 0xFF byte, entry 0 starts right after the header with prevlen 0), zltail is the
 // last entry, zllen entries, an even count of them.  A ziplist whose zllen saturated (0xFFFF)
 // goes to the exact parser.
+#ifndef RR_ZL_U   // entries per lane per round of do_ziplist_bg
+#define RR_ZL_U 1
+#endif
+constexpr uint32_t ZL_U = RR_ZL_U;
 template <class Src>
 __device__ __forceinline__ bool do_ziplist_bg(const Src &R, const Lane &l, bool active, uint32_t G, uint32_t g,
                                               uint32_t &n, uint64_t &pay) {
@@ -805,56 +809,68 @@ __device__ __forceinline__ bool do_ziplist_bg(const Src &R, const Lane &l, bool 
     uint32_t p = zl0 + z[1];
     p = p < first ? first : p > zlast ? zlast : p;
     uint32_t expect = zlast;   // where the entry at p must end
+    // ZL_U entries per lane per round (U G chain steps): the U entry decodes are independent,
+    // so their instruction streams interleave
+    constexpr uint32_t U = ZL_U;
     for (uint32_t rounds = 0;; ++rounds) {
-        uint32_t mp = first, me = zlast;
-        for (uint32_t j = 0; j < G; ++j) {
-            uint32_t x[2];
-            R.template get<2>(p, x);
-            const uint32_t b0 = x[0] & 0xFF;
-            const uint32_t pl = b0 >= 254 ? ab(x[1], x[0], 1) : b0;
-            const uint32_t pn = p - min(pl, p - first);
-            mp = j == g ? p : mp;
-            me = j == g ? expect : me;
-            expect = p;
-            p = pn;
+        uint32_t mp[U], me[U];
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) {
+            mp[u] = first;
+            me[u] = zlast;
+            for (uint32_t j = 0; j < G; ++j) {
+                uint32_t x[2];
+                R.template get<2>(p, x);
+                const uint32_t b0 = x[0] & 0xFF;
+                const uint32_t pl = b0 >= 254 ? ab(x[1], x[0], 1) : b0;
+                const uint32_t pn = p - min(pl, p - first);
+                mp[u] = j == g ? p : mp[u];
+                me[u] = j == g ? expect : me[u];
+                expect = p;
+                p = pn;
+            }
         }
-        // my entry (index idx = N-1-mk): every field of its header from registers, as selects
-        // (no per-encoding branches); it must end where the entry after it starts (me) — which
-        // makes every prevlen the size of the entry before it — and its prevlen must stay inside
-        // the entries; entry 0 sits right after the header with prevlen 0
-        const uint32_t mk = rounds * G + g;
-        const bool mine = mk < N;
-        const uint32_t idx = N - 1 - mk;
-        uint32_t b[4];
-        R.template get<4>(mp, b);
-        const uint32_t b0 = b[0] & 0xFF;
-        const bool big = b0 >= 254;
-        const uint32_t pl = big ? ab(b[1], b[0], 1) : b0;
-        const uint32_t qp = mp + (big ? 5u : 1u);
-        const uint32_t e = big ? (b[1] >> 8) & 0xFF : (b[0] >> 8) & 0xFF;
-        const uint32_t x1 = big ? (b[1] >> 16) & 0xFF : (b[0] >> 16) & 0xFF;
-        const uint32_t lo = big ? ab(b[2], b[1], 2) : ab(b[1], b[0], 2);   // bytes after the encoding byte
-        const uint32_t hi = big ? ab(b[3], b[2], 2) : ab(b[2], b[1], 2);
-        const bool zstr = e < 0xC0;
-        const uint32_t scls = e >> 6;                        // string length class 0 / 1 / 2
-        const uint32_t ls = 1 + scls + 2 * (scls >> 1);      // 1 / 2 / 5 length bytes
-        const uint32_t sl1 = scls == 0 ? (e & 0x3F) : (((e & 0x3F) << 8) | x1);
-        const uint32_t sl = scls >= 2 ? __builtin_bswap32(lo) : sl1;
-        const bool imm = e - 0xF1u <= 0xFDu - 0xF1u;
-        const uint32_t isz = (uint32_t)(e == 0xFE) + 2 * (uint32_t)(e == 0xC0) + 3 * (uint32_t)(e == 0xF0) +
-                             4 * (uint32_t)(e == 0xD0) + 8 * (uint32_t)(e == 0xE0);
-        const uint64_t endp = (uint64_t)qp + (zstr ? ls + sl : 1 + isz);
-        const bool bad = (mp < first) | (mp >= zlast) | (b0 == 0xFF) | (big & (mp + 5 > zlast)) | (qp >= zlast) |
-                         (idx + 1 >= l.r) | (!zstr & !imm & (isz == 0)) | (zstr & (qp + ls > zlast)) |
-                         (endp != (uint64_t)me) |
-                         (idx == 0 ? ((mp != first) | (pl != 0)) : (pl > mp - first));
-        fail |= mine & bad;
-        const uint32_t sh = (32 - 8 * isz) & 31;
-        const int64_t v32 = (int32_t)(lo << sh) >> sh;
-        const int64_t iv = isz == 8 ? (int64_t)((uint64_t)lo | ((uint64_t)hi << 32)) : imm ? (int64_t)(e & 0x0F) - 1 : v32;
-        put_desc(l.E, (mine & !bad) ? l.slot(idx + 1) : NOSLOT, zstr ? l.B + qp + ls : (uint64_t)iv, zstr ? sl : 0,
-                 zstr ? RR_K_STR : RR_K_INT, zstr ? (e & 0xC0) : e);
-        if (__ballot((rounds + 1) * G < N) == 0) break;
+        // my entries (index idx = N-1-mk): every field of the header from registers, as selects
+        // (no per-encoding branches); an entry must end where the entry after it starts (me) —
+        // which makes every prevlen the size of the entry before it — and its prevlen must stay
+        // inside the entries; entry 0 sits right after the header with prevlen 0
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) {
+            const uint32_t mk = (rounds * U + u) * G + g;
+            const bool mine = mk < N;
+            const uint32_t idx = N - 1 - mk;
+            uint32_t b[4];
+            R.template get<4>(mp[u], b);
+            const uint32_t b0 = b[0] & 0xFF;
+            const bool big = b0 >= 254;
+            const uint32_t pl = big ? ab(b[1], b[0], 1) : b0;
+            const uint32_t qp = mp[u] + (big ? 5u : 1u);
+            const uint32_t e = big ? (b[1] >> 8) & 0xFF : (b[0] >> 8) & 0xFF;
+            const uint32_t x1 = big ? (b[1] >> 16) & 0xFF : (b[0] >> 16) & 0xFF;
+            const uint32_t lo = big ? ab(b[2], b[1], 2) : ab(b[1], b[0], 2);   // bytes after the encoding byte
+            const uint32_t hi = big ? ab(b[3], b[2], 2) : ab(b[2], b[1], 2);
+            const bool zstr = e < 0xC0;
+            const uint32_t scls = e >> 6;                        // string length class 0 / 1 / 2
+            const uint32_t ls = 1 + scls + 2 * (scls >> 1);      // 1 / 2 / 5 length bytes
+            const uint32_t sl1 = scls == 0 ? (e & 0x3F) : (((e & 0x3F) << 8) | x1);
+            const uint32_t sl = scls >= 2 ? __builtin_bswap32(lo) : sl1;
+            const bool imm = e - 0xF1u <= 0xFDu - 0xF1u;
+            // integer bytes: C0 2, D0 4, E0 8, F0 3 (a nibble table on bits 4-5), FE 1, else 0
+            const uint32_t isz = (e & 0x0F) == 0 && e >= 0xC0 ? (0x3842u >> (4 * ((e >> 4) & 3))) & 0xF
+                                                               : (uint32_t)(e == 0xFE);
+            const uint64_t endp = (uint64_t)qp + (zstr ? ls + sl : 1 + isz);
+            const bool bad = (mp[u] < first) | (mp[u] >= zlast) | (b0 == 0xFF) | (big & (mp[u] + 5 > zlast)) |
+                             (qp >= zlast) | (idx + 1 >= l.r) | (!zstr & !imm & (isz == 0)) |
+                             (zstr & (qp + ls > zlast)) | (endp != (uint64_t)me[u]) |
+                             (idx == 0 ? ((mp[u] != first) | (pl != 0)) : (pl > mp[u] - first));
+            fail |= mine & bad;
+            const uint32_t sh = (32 - 8 * isz) & 31;
+            const int64_t v32 = (int32_t)(lo << sh) >> sh;
+            const int64_t iv = isz == 8 ? (int64_t)((uint64_t)lo | ((uint64_t)hi << 32)) : imm ? (int64_t)(e & 0x0F) - 1 : v32;
+            put_desc(l.E, (mine & !bad) ? l.slot(idx + 1) : NOSLOT, zstr ? l.B + qp + ls : (uint64_t)iv, zstr ? sl : 0,
+                     zstr ? RR_K_STR : RR_K_INT, zstr ? (e & 0xC0) : e);
+        }
+        if (__ballot((rounds + 1) * U * G < N) == 0) break;
     }
     // one verdict for the whole group
     const uint32_t base = lane_id() - g;
