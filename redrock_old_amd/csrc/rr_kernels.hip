@@ -2436,16 +2436,16 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(RR_ENC_WPE))
 
 // ---------------------------------------------------------------------------------------- launch
 #ifndef RR_DEC_W
-#define RR_DEC_W 65536
+#define RR_DEC_W 73728
 #endif
 #ifndef RR_DEC_SLACK
-#define RR_DEC_SLACK 8192
+#define RR_DEC_SLACK 4096
 #endif
 #ifndef RR_DEC_NW
 #define RR_DEC_NW 8
 #endif
 #ifndef RR_DEC_PMAX
-#define RR_DEC_PMAX 2048
+#define RR_DEC_PMAX 1024
 #endif
 constexpr uint32_t DEC_W = RR_DEC_W, DEC_NW = RR_DEC_NW;
 #define DECODE_KERNEL decode_kernel<RR_DEC_W, RR_DEC_SLACK, RR_DEC_NW, RR_DEC_PMAX>

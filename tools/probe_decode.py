@@ -26,7 +26,7 @@ d_vals = torch.empty(n * 16, dtype=torch.uint8, device=dev)
 d_elems = torch.empty(cap * 16, dtype=torch.uint8, device=dev)
 d_arena = torch.empty((nb + 15) & ~15, dtype=torch.uint8, device=dev)
 d_tot = torch.zeros(4, dtype=torch.int64, device=dev)
-W = int(os.environ.get("RR_DEC_W", 65536))
+W = int(os.environ.get("RR_DEC_W", 73728))
 nwin = len(data) // W + 1
 probe = torch.zeros(nwin * 32, dtype=torch.int64, device=dev)
 L = rr.lib()
