@@ -900,6 +900,9 @@ __device__ __forceinline__ uint32_t class_vpb(uint32_t c) {
 #ifndef RR_DEC_BFREE
 #define RR_DEC_BFREE 1
 #endif
+#ifndef RR_DEC_BALANCE   // 1: a class's values split evenly over its batches
+#define RR_DEC_BALANCE 0
+#endif
 #ifndef RR_DEC_PRIO   // wave priority during the walks (0: none; see the batch loop)
 #define RR_DEC_PRIO 0
 #endif
@@ -1311,7 +1314,12 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
             uint32_t k = 0;
             while (bi >= bpre[k + 1]) ++k;
             const uint32_t c = CLASS_ORDER[k];
+#if RR_DEC_BALANCE   // the class's values split evenly over its batches (same batch count)
+            const uint32_t vpb0 = class_vpb(c), nbc = (ccount[c] + vpb0 - 1) / vpb0;
+            const uint32_t vpb = (ccount[c] + nbc - 1) / nbc;
+#else
             const uint32_t vpb = class_vpb(c);
+#endif
             const uint32_t first = cbase[c] + (bi - bpre[k]) * vpb;
             const uint32_t cnt = min(ccount[c] - (bi - bpre[k]) * vpb, vpb);
 #ifdef RR_SKIP_CLASSES   // timing-only builds (tools/): skip the batches of these classes
