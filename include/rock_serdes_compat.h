@@ -47,6 +47,22 @@ void rr_compat_rdb_load_batch(int fd_req, int fd_resp, int dbid, sds *keys, size
 
 /* GPU the calling thread's engine context is created on (default 0; set before first use). */
 void rr_compat_set_device(int device);
+
+/* rock_serdes.h:51-55: the debug round trips of `ROCK testserdes*` (rock.c:170-184), over the
+ * engine, logging through serverLog as the reference's do (rock_serdes.c:626-901). */
+void _test_ser_des_string(void);
+void _test_ser_des_list(void);
+void _test_ser_des_set(void);
+void _test_ser_des_hash(void);
+void _test_ser_des_zset(void);
+
+/* Fork children (rock.c:527-550).  A process that has used the engine starts, right before it
+ * forks (pthread_atfork), a decode service thread; desObject in the child sends its blobs
+ * there over a socket and builds the robj from the flat records that come back, never touching
+ * the HIP runtime.  rr_compat_service_start starts it explicitly (0 or -1);
+ * rr_compat_test_as_child(1) makes this process route desObject as a child would (tests). */
+int rr_compat_service_start(void);
+void rr_compat_test_as_child(int on);
 #endif
 
 #endif

@@ -131,6 +131,14 @@ int rr_shard_plan(const uint64_t *offsets, uint64_t n, uint32_t g, rr_shard *pla
  * STR / ZLRAW arena offsets += byte_add (zero-filled slots of malformed values stay zero). */
 int rr_flat_rebase(rr_ctx *ctx, rr_value *values, uint64_t n, rr_elem *elems, uint64_t n_elems,
                    uint64_t elem_add, uint64_t byte_add, void *stream);
+/* The same placement in host memory (a caller gathering decoded shards on the host).  Both
+ * refuse (RR_API_EINVAL) a placement past 2^32 - 1 descriptors: elem_base is 32-bit. */
+int rr_flat_rebase_host(rr_value *values, uint64_t n, rr_elem *elems, uint64_t n_elems, uint64_t elem_add,
+                        uint64_t byte_add);
+/* Where a gather places shard k's descriptors (elem_at[k] = the descriptors of the shards before
+ * it, also its rebase's elem_add; its records go at the plan's value range).  Returns the total
+ * descriptor count, UINT64_MAX past 2^32 - 1.  rr_gather uses it; elem_at may be NULL. */
+uint64_t rr_gather_layout(const uint64_t *shard_elems, int nranks, uint64_t *elem_at);
 
 typedef struct rr_comm rr_comm;
 #define RR_COMM_ID_BYTES 128
@@ -143,6 +151,9 @@ void rr_comm_destroy(rr_comm *comm);
 /* Collective.  The root holds the whole batch (device); every rank gets the plan (nranks
  * entries, host memory) so it can size its shard buffers.  Blocks until the plan is known. */
 int rr_split_plan(rr_comm *comm, const rr_blob_batch *whole, int root, rr_shard *plan, void *stream);
+/* rr_split and rr_gather agree on every rank's arguments (a one-word all-reduce) before any
+ * point-to-point call, so a bad argument on one rank returns RR_API_EINVAL on every rank
+ * instead of leaving the others' sends and receives waiting. */
 /* Collective.  Each rank receives its shard: mine->data (>= its b1 - b0 bytes, 16-byte
  * aligned) and mine->offsets (v1 - v0 + 1 entries, rebased to 0); mine->n is set.  The root
  * sends ncclSend slices over xGMI.  Asynchronous on `stream`.  The root may take its shard in
@@ -152,11 +163,18 @@ int rr_split(rr_comm *comm, const rr_blob_batch *whole, const rr_shard *plan, in
              void *stream);
 /* Collective.  Every rank passes its decoded shard (mine: n values, mine_elems descriptor
  * slots = that decode's rr_totals.n_elems); the root receives all shards into whole->values /
- * whole->elems at their places and rebases them, so whole equals a decode of the whole batch
+ * whole->elems (whole->n >= the batch's values, whole->elem_cap >= all shards' descriptors) at
+ * their places (rr_gather_layout) and rebases them, so whole equals a decode of the whole batch
  * (whose arena is the whole blob buffer: the arena mirrors it, nothing moves).  Blocks until
  * the shards' sizes are known (an all-gather of one word per rank). */
 int rr_gather(rr_comm *comm, const rr_flat_batch *mine, uint64_t mine_elems, const rr_shard *plan, int root,
               rr_flat_batch *whole, void *stream);
+
+/* ---- diagnostics ------------------------------------------------------------------------ */
+/* The engine's streaming device copy (16-byte buffer loads, 8 in flight per lane, nontemporal
+ * stores): the measured copy bandwidth bench.py prices the decode's roofline against
+ * (SURVEY.md §8d).  16-byte aligned device pointers, any byte count; asynchronous on `stream`. */
+int rr_copy_device(rr_ctx *ctx, void *dst, const void *src, uint64_t bytes, void *stream);
 
 /* ---- synthetic batches (BASELINE.json configs) ------------------------ */
 /* config: 1 = 64-B RAW strings, 2 = Zipf 16B-4KiB strings, 3 = 16-pair hash ziplists,

@@ -70,7 +70,8 @@ class HostBatch(C.Structure):
 EXPORTS = ["rr_ctx_create", "rr_ctx_destroy", "rr_ctx_reserve", "rr_last_error", "rr_decode_batch",
            "rr_encode_batch", "rr_decode_elem_bound", "rr_decode_batch_host", "rr_encode_batch_host",
            "rr_gen_batch", "rr_host_batch_free", "rr_gen_default_seed", "rr_shard_plan", "rr_flat_rebase",
-           "rr_comm_get_id", "rr_comm_init", "rr_comm_destroy", "rr_split_plan", "rr_split", "rr_gather"]
+           "rr_comm_get_id", "rr_comm_init", "rr_comm_destroy", "rr_split_plan", "rr_split", "rr_gather",
+           "rr_flat_rebase_host", "rr_gather_layout", "rr_copy_device"]
 COMM_ID_BYTES = 128
 # include/rr_snappy.h (GPU block compression)
 SNAPPY_EXPORTS = ["rr_snappy_max_compressed_length", "rr_snappy_compress_bound", "rr_snappy_compress_batch",
@@ -117,6 +118,10 @@ def lib():
     L.rr_gen_default_seed.restype = u64
     L.rr_shard_plan.argtypes = [vp, u64, C.c_uint32, C.POINTER(Shard)]
     L.rr_flat_rebase.argtypes = [vp, vp, u64, vp, u64, u64, u64, vp]
+    L.rr_flat_rebase_host.argtypes = [vp, u64, vp, u64, u64, u64]
+    L.rr_gather_layout.argtypes = [vp, C.c_int, vp]
+    L.rr_gather_layout.restype = u64
+    L.rr_copy_device.argtypes = [vp, vp, vp, u64, vp]
     L.rr_comm_get_id.argtypes = [vp]
     L.rr_comm_init.argtypes = [vp, C.c_int, C.c_int, vp, C.POINTER(vp)]
     L.rr_comm_destroy.argtypes = [vp]
@@ -169,6 +174,22 @@ def shard_plan(offsets: np.ndarray, g: int) -> np.ndarray:
     plan = (Shard * g)()
     _check(lib().rr_shard_plan(_ptr(offsets), len(offsets) - 1, g, plan))
     return np.array([[p.v0, p.v1, p.b0, p.b1] for p in plan], np.uint64).reshape(g, 4)
+
+
+def flat_rebase_host(values: np.ndarray, elems: np.ndarray, elem_add: int, byte_add: int):
+    """In place on host records (rr_flat_rebase_host): the placement rr_gather makes on the device."""
+    assert values.dtype == VALUE_DT and elems.dtype == ELEM_DT and values.flags.c_contiguous and elems.flags.c_contiguous
+    _check(lib().rr_flat_rebase_host(_ptr(values), len(values), _ptr(elems), len(elems), elem_add, byte_add))
+
+
+def gather_layout(shard_elems) -> tuple[np.ndarray, int]:
+    """(elem_at per shard, total) of the C library's gather placement (rr_gather_layout)."""
+    ne = np.ascontiguousarray(shard_elems, np.uint64)
+    at = np.zeros(max(len(ne), 1), np.uint64)
+    tot = int(lib().rr_gather_layout(_ptr(ne), len(ne), _ptr(at)))
+    if tot == 2 ** 64 - 1:
+        raise RRError("gather layout past 2^32 - 1 descriptors")
+    return at[:len(ne)], tot
 
 
 def elem_bound(n: int, nbytes: int) -> int:
@@ -243,6 +264,12 @@ class Engine:
         """In place on torch CUDA tensors (uint8 views of the flat records): rr_flat_rebase."""
         _check(self._L.rr_flat_rebase(self._ctx, C.c_void_p(values.data_ptr()), values.numel() // 16,
                                       C.c_void_p(elems.data_ptr()), elems.numel() // 16, elem_add, byte_add,
+                                      _sp(stream)))
+
+    def copy_device(self, dst, src, nbytes: int | None = None, stream=None):
+        """The engine's streaming copy (rr_copy_device) between torch CUDA tensors."""
+        nb = src.numel() * src.element_size() if nbytes is None else nbytes
+        _check(self._L.rr_copy_device(self._ctx, C.c_void_p(dst.data_ptr()), C.c_void_p(src.data_ptr()), nb,
                                       _sp(stream)))
 
     # ---- snappy block compression (include/rr_snappy.h) -----------------------------------

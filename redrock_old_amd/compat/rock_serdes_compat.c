@@ -15,9 +15,12 @@
 #ifndef RR_REDIS_TREE
 #define RR_REDIS_TREE 1
 #endif
+#include <pthread.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/socket.h>
+#include <unistd.h>
 
 #include "server.h"
 
@@ -28,11 +31,77 @@ static __thread rr_ctx *g_ctx;   /* one engine context per host thread (rr_serde
 
 void rr_compat_set_device(int device) { g_device = device; }
 
+/* ---- fork children (rock.c:527-550: BGSAVE / AOF rewrite call desObject in a fork()ed child).
+ * A child must not touch the HIP runtime its parent initialised, so in a child desObject does
+ * not decode itself: it sends the blob over a socket to a decode service thread in the parent
+ * (rr_rdb_serve's FLAT request, the blob standing in for the key) and builds the robj from the
+ * flat records that come back.  The service is started in the parent right before a fork
+ * (pthread_atfork prepare), once the parent has used the engine; Redis runs one child at a time
+ * (hasActiveChildProcess), so one socket serves them in turn.  rock.c needs no change. */
+static pid_t g_owner;                     /* the process whose threads own GPU contexts */
+static pthread_mutex_t g_svc_mu = PTHREAD_MUTEX_INITIALIZER;
+static int g_svc_fd = -1, g_child_fd = -1;   /* socketpair: service end / child end */
+static volatile int g_svc_alive;
+static int g_as_child;                    /* test hook: route this process as a child would */
+
+static int in_child(void) { return g_as_child || (g_owner && getpid() != g_owner); }
+
 static rr_ctx *engine(void) {
-    if (!g_ctx && rr_ctx_create(g_device, &g_ctx) != RR_API_OK)
-        serverPanic("rock serdes engine: %s", rr_last_error());
+    if (in_child()) serverPanic("rock serdes: the GPU engine cannot be used in a fork child (HIP is the parent's)");
+    if (!g_ctx) {
+        if (rr_ctx_create(g_device, &g_ctx) != RR_API_OK) serverPanic("rock serdes engine: %s", rr_last_error());
+        if (!g_owner) g_owner = getpid();
+    }
     return g_ctx;
 }
+
+static int echo_blob(void *user, size_t k, const int *dbis, const char *const *keys, const size_t *key_lens,
+                     void **vals, size_t *val_lens) {
+    (void)user; (void)dbis;
+    for (size_t i = 0; i < k; i++) { vals[i] = (void *)keys[i]; val_lens[i] = key_lens[i]; }
+    return 0;
+}
+
+static void *decode_service(void *arg) {
+    (void)arg;
+    rr_ctx *ctx = NULL;
+    if (rr_ctx_create(g_device, &ctx) == RR_API_OK) {
+        rr_rdb_serve(g_svc_fd, g_svc_fd, echo_blob, NULL, NULL, ctx, 64);
+        rr_ctx_destroy(ctx);
+    }
+    g_svc_alive = 0;   /* a broken request ended it: the next fork starts a new one */
+    return NULL;
+}
+
+int rr_compat_service_start(void) {
+    int rc = 0;
+    pthread_mutex_lock(&g_svc_mu);
+    if (!g_svc_alive) {
+        int sv[2];
+        pthread_t th;
+        if (g_svc_fd >= 0) { close(g_svc_fd); close(g_child_fd); g_svc_fd = g_child_fd = -1; }
+        if (socketpair(AF_UNIX, SOCK_STREAM, 0, sv) != 0) rc = -1;
+        else {
+            g_svc_fd = sv[0];
+            g_child_fd = sv[1];
+            g_svc_alive = 1;
+            if (pthread_create(&th, NULL, decode_service, NULL) != 0) { g_svc_alive = 0; rc = -1; }
+            else pthread_detach(th);
+        }
+    }
+    pthread_mutex_unlock(&g_svc_mu);
+    return rc;
+}
+
+static void atfork_prepare(void) {
+    if (g_owner && getpid() == g_owner && !g_as_child) (void)rr_compat_service_start();
+}
+static void atfork_child(void) { g_ctx = NULL; }   /* (the parent's context is not ours) */
+__attribute__((constructor)) static void compat_atfork_register(void) {
+    pthread_atfork(atfork_prepare, NULL, atfork_child);
+}
+
+void rr_compat_test_as_child(int on) { g_as_child = on; }
 
 static const char *status_name(unsigned st) {
     static const char *names[RR_N_STATUS] = {"ok", "short blob", "unknown type", "string encoding",
@@ -140,8 +209,28 @@ static robj *robj_from_flat(const rr_value *v, const rr_elem *el, const uint8_t 
     return o;
 }
 
+/* a child's batch: the parent's decode service decodes it, the robj are built here */
+static void des_batch_in_child(void *const *bufs, const size_t *lens, size_t n, robj **out) {
+    if (!g_svc_alive || g_child_fd < 0)
+        serverPanic("desObject in a fork child: the parent's decode service is not running "
+                    "(the parent must use the engine before it forks)");
+    int *dbis = zmalloc(sizeof(int) * n);
+    for (size_t i = 0; i < n; i++) dbis[i] = 0;
+    rr_rdb_flat f;
+    if (rr_rdb_request_flat(g_child_fd, g_child_fd, dbis, (const char *const *)bufs, lens, n, &f) != RR_API_OK || f.n != n)
+        serverPanic("desObject in a fork child: %s", rr_last_error());
+    for (size_t i = 0; i < n; i++) {
+        if (f.values[i].status != RR_OK)   /* the reference's serverAssert / serverPanic site */
+            serverPanic("desObject: bad blob (%s, status %u)", status_name(f.values[i].status), f.values[i].status);
+        out[i] = robj_from_flat(&f.values[i], f.elems + f.values[i].elem_base, f.arena);
+    }
+    rr_rdb_flat_free(&f);
+    zfree(dbis);
+}
+
 void rr_compat_des_batch(void *const *bufs, const size_t *lens, size_t n, robj **out) {
     if (n == 0) return;
+    if (in_child()) { des_batch_in_child(bufs, lens, n, out); return; }
     uint64_t *offs = zmalloc(sizeof(uint64_t) * (n + 1));
     offs[0] = 0;
     for (size_t i = 0; i < n; i++) offs[i + 1] = offs[i] + lens[i];
@@ -344,4 +433,133 @@ sds serObject(robj *o) {
     sds s = NULL;
     rr_compat_ser_batch(&o, 1, &s);
     return s;
+}
+
+/* ---------------------------------------------------------------- rock_serdes.h:51-55
+ * The debug round trips `ROCK testserdes{str,list,set,hash,zset}` runs (rock.c:170-184), with
+ * the reference's inputs (rock_serdes.c:626-901): a live key of db 0 ("abc"; "def" for the set)
+ * of the encoding the reference's hook exercises goes through serObject + desObject (here: the
+ * GPU engine) and the result is logged; the string hook round-trips its three literal strings
+ * through desString.  Like the reference they only log, they assert nothing. */
+
+/* the value of `name` in db 0 when it has the given type and encoding, else a logged NULL */
+static robj *test_value(const char *name, unsigned type, unsigned enc) {
+    sds key = sdsnewlen(name, strlen(name));
+    dictEntry *de = dictFind(server.db[0].dict, key);
+    sdsfree(key);
+    if (!de) {
+        serverLog(LL_NOTICE, "de is null for key = %s", name);
+        return NULL;
+    }
+    robj *o = dictGetVal(de);
+    if (o->type != type || o->encoding != enc) {
+        serverLog(LL_NOTICE, "val type or encoding not correct! type = %u, encoding = %u", o->type, o->encoding);
+        return NULL;
+    }
+    return o;
+}
+
+static robj *test_round_trip(robj *o) {
+    sds blob = serObject(o);
+    robj *back = desObject(blob, sdslen(blob));
+    sdsfree(blob);
+    return back;
+}
+
+static void test_log_quicklist(quicklist *ql) {
+    quicklistIter *it = quicklistGetIterator(ql, AL_START_HEAD);
+    quicklistEntry e;
+    for (int i = 0; quicklistNext(it, &e); i++) {
+        if (e.value) serverLog(LL_NOTICE, "index = %d, entry sz = %u, entry val = %.*s", i, e.sz, (int)e.sz, e.value);
+        else serverLog(LL_NOTICE, "index = %d, entry long value = %lld", i, e.longval);
+    }
+    quicklistReleaseIterator(it);
+}
+
+void _test_ser_des_string(void) {                                             /* :829-901 */
+    serverLog(LL_NOTICE, "_test_ser_des_string");
+    static const char raw60[] = "aadfcrghsdgggggggggggadbAFWEdsar4dadsrd423FASFASXASDFASR3ADFASDFASFASR34RFADSFSADFSAFXEEdsdec";
+    robj *src[3] = {createStringObjectFromLongLongForValue(134123), createEmbeddedStringObject("abc", 3),
+                    createRawStringObject(raw60, 60)};
+    for (int k = 0; k < 3; k++) {
+        sds blob = serObject(src[k]);
+        const size_t len = sdslen(blob);
+        char *copy = zmalloc(len);   /* desString borrows a caller buffer, as rock.c's zmalloc'd read */
+        memcpy(copy, blob, len);
+        robj *d = desString(copy, len, src[k]->lru);
+        serverAssert(d->refcount == 1);
+        const char *what = NULL;
+        if (src[k]->type != d->type) what = "type";
+        else if (src[k]->encoding != d->encoding) what = "encoding";
+        else if (src[k]->encoding == OBJ_ENCODING_INT) { if (src[k]->ptr != d->ptr) what = "long val"; }
+        else if (sdslen(src[k]->ptr) != sdslen(d->ptr)) what = "sds len";
+        else if (memcmp(src[k]->ptr, d->ptr, sdslen(d->ptr))) what = "memcmp";
+        if (what) serverLog(LL_NOTICE, "%d %s!", k + 1, what);
+        else serverLog(LL_NOTICE, "%d round trip ok, blob len = %zu", k + 1, len);
+        decrRefCount(d);
+        zfree(copy);
+        sdsfree(blob);
+        decrRefCount(src[k]);
+    }
+}
+
+void _test_ser_des_list(void) {                                               /* :792-827 */
+    serverLog(LL_NOTICE, "_test_ser_des_list");
+    robj *o = test_value("abc", OBJ_LIST, OBJ_ENCODING_QUICKLIST);
+    if (!o) return;
+    test_log_quicklist(o->ptr);
+    robj *list = createQuicklistObject();
+    quicklistSetOptions(list->ptr, server.list_max_ziplist_size, server.list_compress_depth);
+    sds xxx = sdsnewlen("xxx", 3), num = sdsfromlonglong(-1234567);
+    quicklistPushTail(list->ptr, xxx, sdslen(xxx));
+    quicklistPushTail(list->ptr, num, sdslen(num));
+    sdsfree(xxx);
+    sdsfree(num);
+    test_log_quicklist(list->ptr);
+    robj *back = test_round_trip(list);
+    test_log_quicklist(back->ptr);
+    decrRefCount(back);
+    decrRefCount(list);
+}
+
+void _test_ser_des_set(void) {                                                /* :741-773 (HT) */
+    robj *o = test_value("def", OBJ_SET, OBJ_ENCODING_HT);
+    if (!o) return;
+    robj *back = test_round_trip(o);
+    dictIterator *di = dictGetIterator(back->ptr);
+    dictEntry *de;
+    while ((de = dictNext(di)))
+        serverLog(LL_NOTICE, "set ht, key = %s, val is %s", (char *)dictGetKey(de), dictGetVal(de) ? "not null" : "null");
+    dictReleaseIterator(di);
+    decrRefCount(back);
+}
+
+void _test_ser_des_hash(void) {                                               /* :694-718 (HT) */
+    robj *o = test_value("abc", OBJ_HASH, OBJ_ENCODING_HT);
+    if (!o) return;
+    robj *back = test_round_trip(o);
+    serverLog(LL_NOTICE, "des encoding = %s", back->encoding == OBJ_ENCODING_HT ? "ht" : "not ht!!!");
+    if (back->encoding == OBJ_ENCODING_HT) {
+        dictIterator *di = dictGetIterator(back->ptr);
+        dictEntry *de;
+        for (int no = 0; (de = dictNext(di)); no++)
+            serverLog(LL_NOTICE, "no = %d, field = %s, val = %s", no, (char *)dictGetKey(de), (char *)dictGetVal(de));
+        dictReleaseIterator(di);
+    }
+    decrRefCount(back);
+}
+
+void _test_ser_des_zset(void) {                                               /* :647-671 (skiplist) */
+    robj *o = test_value("abc", OBJ_ZSET, OBJ_ENCODING_SKIPLIST);
+    if (!o) return;
+    robj *back = test_round_trip(o);
+    serverLog(LL_NOTICE, "des encoding = %s", back->encoding == OBJ_ENCODING_SKIPLIST ? "skiplist" : "not skiplist!!!");
+    if (back->encoding == OBJ_ENCODING_SKIPLIST) {
+        zset *zs = back->ptr;
+        serverAssert(zs->zsl->length == dictSize(zs->dict));
+        int i = 0;
+        for (zskiplistNode *zn = zs->zsl->tail; zn; zn = zn->backward, i++)   /* tail -> head */
+            serverLog(LL_NOTICE, "zset skiplist i = %d, key = %s, score = %lf", i, zn->ele, zn->score);
+    }
+    decrRefCount(back);
 }

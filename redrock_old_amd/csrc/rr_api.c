@@ -156,6 +156,14 @@ int rr_encode_batch(rr_ctx *c, const rr_flat_batch *in, rr_blob_batch *out, rr_t
     return mark_scratch(c, (hipStream_t)stream);
 }
 
+int rr_copy_device(rr_ctx *c, void *dst, const void *src, uint64_t bytes, void *stream) {
+    if (!c || (bytes && (!dst || !src))) return fail(RR_API_EINVAL, "NULL argument");
+    if (((uintptr_t)dst | (uintptr_t)src) & 15) return fail(RR_API_EINVAL, "rr_copy_device: pointers must be 16-byte aligned");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(rr_launch_copy((uint8_t *)dst, (const uint8_t *)src, bytes, (hipStream_t)stream));
+    return RR_API_OK;
+}
+
 /* grow a device staging buffer (host entry points only) */
 int rr_dgrow(void **p, size_t *cap, size_t need) {
     if (need <= *cap && *p) return RR_API_OK;
@@ -212,11 +220,10 @@ static int plan_chunks(const uint64_t *offsets, uint64_t n, uint64_t bytes, uint
     return m;   /* chunks */
 }
 
-static int decode_host_pipelined(rr_ctx *c, const uint8_t *data, const uint64_t *offsets, uint64_t n,
-                                 rr_value *values, rr_elem *elems, uint64_t elem_cap, uint8_t *arena,
-                                 rr_totals *totals, uint64_t bytes, size_t pbytes, const uint64_t *cut, int K) {
-    int rc = pipe_init(c);
-    if (rc) return rc;
+static int decode_host_pipelined_run(rr_ctx *c, const uint8_t *data, const uint64_t *offsets, uint64_t n,
+                                     rr_value *values, rr_elem *elems, uint64_t elem_cap, uint8_t *arena,
+                                     rr_totals *totals, uint64_t bytes, size_t pbytes, const uint64_t *cut, int K) {
+    int rc;
     uint8_t *d_in = (uint8_t *)c->d_in, *d_arena = (uint8_t *)c->d_arena;
     uint64_t *d_off = (uint64_t *)c->d_off;
     rr_value *d_vals = (rr_value *)c->d_vals;
@@ -265,10 +272,30 @@ static int decode_host_pipelined(rr_ctx *c, const uint8_t *data, const uint64_t 
     return RR_API_OK;
 }
 
+/* On an error after the uploads are queued, the transfers still in flight would keep writing
+ * the caller's host buffers (downloads) and the staging buffers the next call reuses (uploads):
+ * wait for both transfer streams before reporting it. */
+static int decode_host_pipelined(rr_ctx *c, const uint8_t *data, const uint64_t *offsets, uint64_t n,
+                                 rr_value *values, rr_elem *elems, uint64_t elem_cap, uint8_t *arena,
+                                 rr_totals *totals, uint64_t bytes, size_t pbytes, const uint64_t *cut, int K) {
+    int rc = pipe_init(c);
+    if (rc) return rc;
+    rc = decode_host_pipelined_run(c, data, offsets, n, values, elems, elem_cap, arena, totals, bytes, pbytes, cut, K);
+    if (rc != RR_API_OK && rc != 1) {
+        (void)hipStreamSynchronize(c->up);
+        (void)hipStreamSynchronize(c->down);
+        (void)hipStreamSynchronize(c->stream);
+    }
+    return rc;
+}
+
 int rr_decode_batch_host(rr_ctx *c, const uint8_t *data, const uint64_t *offsets, uint64_t n, rr_value *values,
                          rr_elem *elems, uint64_t elem_cap, uint8_t *arena, rr_totals *totals) {
     if (!c || !offsets || (n && (!data || !values))) return fail(RR_API_EINVAL, "NULL argument");
     if (n >= RR_MAX_VALUES) return fail(RR_API_EINVAL, "batch too large (value indices are 32-bit)");
+    /* elem_base is 32-bit (rr_format.h): past 2^32 - 1 descriptors a value gets RR_E_CAPACITY,
+     * as in the one-call path, and the chunks' running descriptor base never wraps */
+    if (elem_cap > 0xFFFFFFFFull) elem_cap = 0xFFFFFFFFull;
     HIPCHK(hipSetDevice(c->device));
     uint64_t bytes = offsets[n];
     size_t pbytes = (size_t)((bytes + 15) & ~15ull);

@@ -37,6 +37,7 @@ hipError_t rr_launch_offsets_rebase(uint64_t *offs, uint64_t count, uint64_t sub
 hipError_t rr_launch_flat_rebase(rr_value *values, uint64_t n, rr_elem *elems, uint64_t ne, uint64_t elem_add,
                                  uint64_t byte_add, hipStream_t stream);
 uint64_t rr_encode_scratch_words(uint64_t n, uint64_t data_cap);
+hipError_t rr_launch_copy(uint8_t *dst, const uint8_t *src, uint64_t bytes, hipStream_t stream);
 
 #ifdef __cplusplus
 }

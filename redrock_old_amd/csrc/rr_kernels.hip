@@ -2650,6 +2650,36 @@ extern "C" hipError_t rr_launch_flat_rebase(rr_value *values, uint64_t n, rr_ele
     return hipGetLastError();
 }
 
+// ---- streaming device copy: the roofline anchor (SURVEY.md §8d "a measured device copy-kernel
+// bandwidth on the box") -----------------------------------------------------------------------
+// The same bytes-per-lane shape the decode's window copy uses: 16-byte buffer loads, COPY_U of
+// them in flight per lane before any store, nontemporal 16-byte stores; a workgroup per
+// COPY_U * 256 * 16 bytes (≫ 256 CUs' worth of workgroups), blocks dealt over the XCDs in
+// order.  Bytes past the end read as zeros and their stores are dropped (buffer range), so
+// there is no tail branch.  Used by bench.py as `copy_ref`; no part of the serdes path.
+constexpr uint32_t COPY_U = 8, COPY_NT = 256;
+__global__ __launch_bounds__(COPY_NT) void copy_kernel(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst,
+                                                       uint64_t bytes) {
+    const uint64_t base = (uint64_t)blockIdx.x * (COPY_U * COPY_NT * 16);
+    const uint64_t left = bytes - base;
+    const uint32_t span = left < COPY_U * COPY_NT * 16 ? (uint32_t)left : COPY_U * COPY_NT * 16;
+    const rsrc_t RS = make_rsrc(src + base, span), RD = make_rsrc(dst + base, span);
+    u32x4 x[COPY_U];
+#pragma unroll
+    for (uint32_t k = 0; k < COPY_U; ++k)
+        x[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(RS, (int)((threadIdx.x + k * COPY_NT) * 16), 0, 0));
+#pragma unroll
+    for (uint32_t k = 0; k < COPY_U; ++k)
+        __builtin_amdgcn_raw_buffer_store_b128(x[k], RD, (int)((threadIdx.x + k * COPY_NT) * 16), 0, 2 /* nt */);
+}
+
+extern "C" hipError_t rr_launch_copy(uint8_t *dst, const uint8_t *src, uint64_t bytes, hipStream_t stream) {
+    if (bytes == 0) return hipSuccess;
+    const uint64_t blocks = (bytes + COPY_U * COPY_NT * 16 - 1) / (COPY_U * COPY_NT * 16);
+    hipLaunchKernelGGL(copy_kernel, dim3((uint32_t)blocks), dim3(COPY_NT), 0, stream, src, dst, bytes);
+    return hipGetLastError();
+}
+
 // ---- the look-back scan for other launchers (rr_snappy.hip) --------------------------------
 // x[0..n) -> exclusive prefix in place, x[n] = total; lb (rr_scan_words(n) words) must be zero
 // and x[n] must be 0 beforehand (the caller's first kernel does both, as count_kernel does).

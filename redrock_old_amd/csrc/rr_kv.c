@@ -38,7 +38,9 @@ static uint64_t encode_bound(size_t k, const rr_elem *elems, uint64_t n_elems) {
 int rr_kv_dump_batch(rr_ctx *c, const rr_kv_ops *kv, int dbi, size_t k, const char *const *keys,
                      const size_t *key_lens, const rr_value *values, const rr_elem *elems, uint64_t n_elems,
                      const uint8_t *arena, uint64_t arena_bytes, int flags) {
-    if (!c || !kv || !kv->write_batch || (k && (!keys || !key_lens || !values))) return fail(RR_API_EINVAL, "rr_kv_dump_batch: NULL argument");
+    if (!c || !kv || !kv->write_batch || (k && (!keys || !key_lens || !values)) || (n_elems && !elems) ||
+        (arena_bytes && !arena))
+        return fail(RR_API_EINVAL, "rr_kv_dump_batch: NULL argument");
     if (k == 0) return RR_API_OK;
     dbufs d = {{0}, 0};
     int rc = RR_API_OK;

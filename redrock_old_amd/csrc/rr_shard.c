@@ -48,12 +48,45 @@ int rr_shard_plan(const uint64_t *offsets, uint64_t n, uint32_t g, rr_shard *pla
     return RR_API_OK;
 }
 
+/* elem_base is 32-bit (rr_format.h): a shard placed past 2^32 - 1 descriptors cannot be
+ * represented, so an elem_add that large is refused instead of wrapping in the kernel */
 int rr_flat_rebase(rr_ctx *ctx, rr_value *values, uint64_t n, rr_elem *elems, uint64_t n_elems, uint64_t elem_add,
                    uint64_t byte_add, void *stream) {
     if (!ctx) return rr_fail(RR_API_EINVAL, "ctx is NULL");
+    if (elem_add > 0xFFFFFFFFull || n_elems > 0xFFFFFFFFull - elem_add)
+        return rr_fail(RR_API_EINVAL, "rr_flat_rebase: descriptors past 2^32 - 1 (elem_base is 32-bit)");
     HIPCHK(hipSetDevice(ctx->device));
     HIPCHK(rr_launch_flat_rebase(values, n, elems, n_elems, elem_add, byte_add, (hipStream_t)stream));
     return RR_API_OK;
+}
+
+/* Host forms of the placement rr_gather makes on the device (flat_rebase_kernel's rule), for a
+ * caller that gathers decoded shards in host memory: values' elem_base += elem_add, STR /
+ * ZLRAW arena offsets += byte_add, zero-filled slots of malformed values left zero. */
+int rr_flat_rebase_host(rr_value *values, uint64_t n, rr_elem *elems, uint64_t n_elems, uint64_t elem_add,
+                        uint64_t byte_add) {
+    if ((n && !values) || (n_elems && !elems)) return rr_fail(RR_API_EINVAL, "rr_flat_rebase_host: NULL buffer");
+    if (elem_add > 0xFFFFFFFFull || n_elems > 0xFFFFFFFFull - elem_add)
+        return rr_fail(RR_API_EINVAL, "rr_flat_rebase_host: descriptors past 2^32 - 1 (elem_base is 32-bit)");
+    for (uint64_t i = 0; i < n; i++) values[i].elem_base += (uint32_t)elem_add;
+    for (uint64_t i = 0; i < n_elems; i++) {
+        rr_elem *e = &elems[i];
+        if ((e->kind == RR_K_STR || e->kind == RR_K_ZLRAW) && (e->data | e->len) != 0) e->data += byte_add;
+    }
+    return RR_API_OK;
+}
+
+/* Where the gather puts shard k: its records at values + plan[k].v0 (the plan's value range),
+ * its descriptors at elems + elem_at[k] = the descriptors of the shards before it, which is
+ * also the elem_add its rebase applies.  Returns the total, or UINT64_MAX past 2^32 - 1. */
+uint64_t rr_gather_layout(const uint64_t *shard_elems, int nranks, uint64_t *elem_at) {
+    uint64_t e = 0;
+    for (int k = 0; k < nranks; k++) {
+        if (elem_at) elem_at[k] = e;
+        e += shard_elems[k];
+        if (e > 0xFFFFFFFFull) return UINT64_MAX;
+    }
+    return e;
 }
 
 int rr_comm_get_id(uint8_t id[RR_COMM_ID_BYTES]) {
@@ -107,32 +140,58 @@ int rr_split_plan(rr_comm *c, const rr_blob_batch *whole, int root, rr_shard *pl
     return RR_API_OK;
 }
 
+/* Every rank's verdict on its own arguments, agreed before any point-to-point call: a rank
+ * that returned early would leave its peers' sends / receives waiting forever on their
+ * streams.  bad = this rank's local verdict; returns whether ANY rank is bad (or a transport
+ * error: RR_API_EHIP).  An all-reduce (max) of one word, then a host sync. */
+static int agree(rr_comm *c, int bad, hipStream_t s, int *any_bad) {
+    uint64_t w = bad ? 1 : 0;
+    HIPCHK(hipMemcpyAsync(c->d_words, &w, sizeof w, hipMemcpyHostToDevice, s));
+    NCCLCHK(ncclAllReduce(c->d_words, c->d_words, 1, ncclUint64, ncclMax, c->nc, s));
+    HIPCHK(hipMemcpyAsync(&w, c->d_words, sizeof w, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    *any_bad = w != 0;
+    return RR_API_OK;
+}
+
 int rr_split(rr_comm *c, const rr_blob_batch *whole, const rr_shard *plan, int root, rr_blob_batch *mine,
              void *stream) {
-    if (!c || !plan || !mine || root < 0 || root >= c->nranks) return rr_fail(RR_API_EINVAL, "rr_split: bad argument");
+    /* (arguments every rank shares: a bad one fails on every rank alike, before any collective) */
+    if (!c || !plan || root < 0 || root >= c->nranks) return rr_fail(RR_API_EINVAL, "rr_split: bad argument");
     hipStream_t s = (hipStream_t)stream;
     HIPCHK(hipSetDevice(c->device));
     const rr_shard *me = &plan[c->rank];
     const uint64_t nb = me->b1 - me->b0, nv = me->v1 - me->v0;
-    if (mine->data_cap < ((nb + 15) & ~15ull) || !mine->offsets || (nb && !mine->data))
-        return rr_fail(RR_API_EINVAL, "rr_split: shard buffers too small");
-    if (c->rank == root && (!whole || !whole->data || !whole->offsets))
-        return rr_fail(RR_API_EINVAL, "rr_split: root needs the whole batch");
-    if (c->rank == root && mine->offsets == whole->offsets + me->v0 && me->b0 != 0)
-        return rr_fail(RR_API_EINVAL, "rr_split: in-place offsets need the root's shard to start at byte 0");
-    NCCLCHK(ncclGroupStart());
-    if (c->rank == root) {
-        for (int k = 0; k < c->nranks; k++) {
-            if (k == root) continue;
-            const rr_shard *p = &plan[k];
-            if (p->b1 > p->b0) NCCLCHK(ncclSend(whole->data + p->b0, p->b1 - p->b0, ncclUint8, k, c->nc, s));
-            NCCLCHK(ncclSend(whole->offsets + p->v0, p->v1 - p->v0 + 1, ncclUint64, k, c->nc, s));
+    int bad = 0;
+    if (!mine || mine->data_cap < ((nb + 15) & ~15ull) || !mine->offsets || (nb && !mine->data))
+        bad = rr_fail(RR_API_EINVAL, "rr_split: shard buffers too small");
+    else if (c->rank == root && (!whole || !whole->data || !whole->offsets))
+        bad = rr_fail(RR_API_EINVAL, "rr_split: root needs the whole batch");
+    else if (c->rank == root && mine->offsets == whole->offsets + me->v0 && me->b0 != 0)
+        bad = rr_fail(RR_API_EINVAL, "rr_split: in-place offsets need the root's shard to start at byte 0");
+    int any_bad = 0;
+    int rc = agree(c, bad, s, &any_bad);
+    if (rc) return rc;
+    if (bad) return bad;
+    if (any_bad) return rr_fail(RR_API_EINVAL, "rr_split: another rank's arguments are invalid");
+    /* the group is always closed, whatever a call inside it returns */
+    ncclResult_t r = ncclGroupStart();
+    if (r == ncclSuccess) {
+        if (c->rank == root) {
+            for (int k = 0; k < c->nranks && r == ncclSuccess; k++) {
+                if (k == root) continue;
+                const rr_shard *p = &plan[k];
+                if (p->b1 > p->b0) r = ncclSend(whole->data + p->b0, p->b1 - p->b0, ncclUint8, k, c->nc, s);
+                if (r == ncclSuccess) r = ncclSend(whole->offsets + p->v0, p->v1 - p->v0 + 1, ncclUint64, k, c->nc, s);
+            }
+        } else {
+            if (nb) r = ncclRecv(mine->data, nb, ncclUint8, root, c->nc, s);
+            if (r == ncclSuccess) r = ncclRecv(mine->offsets, nv + 1, ncclUint64, root, c->nc, s);
         }
-    } else {
-        if (nb) NCCLCHK(ncclRecv(mine->data, nb, ncclUint8, root, c->nc, s));
-        NCCLCHK(ncclRecv(mine->offsets, nv + 1, ncclUint64, root, c->nc, s));
+        const ncclResult_t r2 = ncclGroupEnd();
+        if (r == ncclSuccess) r = r2;
     }
-    NCCLCHK(ncclGroupEnd());
+    if (r != ncclSuccess) return rr_fail(RR_API_EHIP, "rr_split: %s", ncclGetErrorString(r));
     if (c->rank == root) {   /* the root's own shard: a device copy (nothing if it decodes in place) */
         if (mine->data != whole->data + me->b0 && nb)
             HIPCHK(hipMemcpyAsync(mine->data, whole->data + me->b0, nb, hipMemcpyDeviceToDevice, s));
@@ -150,63 +209,75 @@ int rr_split(rr_comm *c, const rr_blob_batch *whole, const rr_shard *plan, int r
 
 int rr_gather(rr_comm *c, const rr_flat_batch *mine, uint64_t mine_elems, const rr_shard *plan, int root,
               rr_flat_batch *whole, void *stream) {
-    if (!c || !mine || !plan || root < 0 || root >= c->nranks) return rr_fail(RR_API_EINVAL, "rr_gather: bad argument");
+    if (!c || !plan || root < 0 || root >= c->nranks) return rr_fail(RR_API_EINVAL, "rr_gather: bad argument");
     hipStream_t s = (hipStream_t)stream;
     HIPCHK(hipSetDevice(c->device));
-    /* the shards' descriptor counts, everywhere (the root places the shards with them) */
-    HIPCHK(hipMemcpyAsync(c->d_words + c->rank, &mine_elems, sizeof(uint64_t), hipMemcpyHostToDevice, s));
-    NCCLCHK(ncclAllGather(c->d_words + c->rank, c->d_words, 1, ncclUint64, c->nc, s));
-    uint64_t *ne = (uint64_t *)malloc(sizeof(uint64_t) * (size_t)c->nranks);
-    if (!ne) return rr_fail(RR_API_ENOMEM, "malloc");
-    hipError_t he = hipMemcpyAsync(ne, c->d_words, sizeof(uint64_t) * (size_t)c->nranks, hipMemcpyDeviceToHost, s);
+    const int R = c->nranks;
+    const uint64_t my_nv = plan[c->rank].v1 - plan[c->rank].v0;
+    int bad = 0;
+    if (!mine || (my_nv && !mine->values) || (mine_elems && !mine->elems))
+        bad = rr_fail(RR_API_EINVAL, "rr_gather: NULL shard buffer");
+    /* every rank's {descriptor count, verdict} (the root places the shards with the counts) */
+    uint64_t w2[2] = {mine_elems, bad ? 1u : 0u};
+    HIPCHK(hipMemcpyAsync(c->d_words + 2 * c->rank, w2, sizeof w2, hipMemcpyHostToDevice, s));
+    NCCLCHK(ncclAllGather(c->d_words + 2 * c->rank, c->d_words, 2, ncclUint64, c->nc, s));
+    uint64_t *got = (uint64_t *)malloc(sizeof(uint64_t) * 4 * (size_t)R);
+    if (!got) return rr_fail(RR_API_ENOMEM, "malloc");
+    uint64_t *cnt = got + 2 * R, *at = got + 3 * R;   /* descriptor counts, shard placements */
+    hipError_t he = hipMemcpyAsync(got, c->d_words, sizeof(uint64_t) * 2 * (size_t)R, hipMemcpyDeviceToHost, s);
     if (he == hipSuccess) he = hipStreamSynchronize(s);
-    if (he != hipSuccess) { free(ne); return rr_fail(RR_API_EHIP, "rr_gather sizes: %s", hipGetErrorString(he)); }
-    int rc = RR_API_OK;
-    uint64_t eb = 0;
-    if (c->rank == root) {
-        uint64_t tot = 0;
-        for (int k = 0; k < c->nranks; k++) tot += ne[k];
-        if (!whole || !whole->values || (tot && !whole->elems) || whole->elem_cap < tot)
-            rc = rr_fail(RR_API_EINVAL, "rr_gather: root's whole batch too small");
+    if (he != hipSuccess) { free(got); return rr_fail(RR_API_EHIP, "rr_gather sizes: %s", hipGetErrorString(he)); }
+    int any_bad = 0;
+    for (int k = 0; k < R; k++) { cnt[k] = got[2 * k]; any_bad |= got[2 * k + 1] != 0; }
+    /* the root's verdict on the whole batch needs the counts: one more agreement round */
+    int rbad = 0;
+    if (c->rank == root && !any_bad) {
+        const uint64_t tot = rr_gather_layout(cnt, R, NULL);
+        if (tot == UINT64_MAX) rbad = rr_fail(RR_API_EINVAL, "rr_gather: descriptors past 2^32 - 1 (elem_base is 32-bit)");
+        else if (!whole || (plan[R - 1].v1 && !whole->values) || (tot && !whole->elems) || whole->elem_cap < tot ||
+                 whole->n < plan[R - 1].v1)
+            rbad = rr_fail(RR_API_EINVAL, "rr_gather: root's whole batch too small");
     }
-    if (rc == RR_API_OK) {
+    int root_bad = 0;
+    int rc = any_bad ? RR_API_OK : agree(c, rbad, s, &root_bad);
+    if (rc == RR_API_OK && (any_bad || root_bad))
+        rc = bad ? bad : rbad ? rbad : rr_fail(RR_API_EINVAL, "rr_gather: another rank's arguments are invalid");
+    if (rc == RR_API_OK) rr_gather_layout(cnt, R, at);
+    if (rc == RR_API_OK) {   /* the group is always closed, whatever a call inside it returns */
         ncclResult_t r = ncclGroupStart();
-        for (int k = 0; k < c->nranks && r == ncclSuccess; k++) {
+        for (int k = 0; k < R && r == ncclSuccess; k++) {
             const uint64_t nv = plan[k].v1 - plan[k].v0;
             if (c->rank == root && k != root) {
                 if (nv) r = ncclRecv(whole->values + plan[k].v0, nv * sizeof(rr_value), ncclUint8, k, c->nc, s);
-                if (r == ncclSuccess && ne[k]) r = ncclRecv(whole->elems + eb, ne[k] * sizeof(rr_elem), ncclUint8, k, c->nc, s);
+                if (r == ncclSuccess && cnt[k]) r = ncclRecv(whole->elems + at[k], cnt[k] * sizeof(rr_elem), ncclUint8, k, c->nc, s);
             } else if (c->rank != root && k == c->rank) {
                 if (nv) r = ncclSend(mine->values, nv * sizeof(rr_value), ncclUint8, root, c->nc, s);
-                if (r == ncclSuccess && ne[k]) r = ncclSend(mine->elems, ne[k] * sizeof(rr_elem), ncclUint8, root, c->nc, s);
+                if (r == ncclSuccess && cnt[k]) r = ncclSend(mine->elems, cnt[k] * sizeof(rr_elem), ncclUint8, root, c->nc, s);
             }
-            eb += ne[k];
         }
-        ncclResult_t r2 = ncclGroupEnd();
+        const ncclResult_t r2 = ncclGroupEnd();
         if (r == ncclSuccess) r = r2;
         if (r != ncclSuccess) rc = rr_fail(RR_API_EHIP, "rr_gather: %s", ncclGetErrorString(r));
     }
     if (rc == RR_API_OK && c->rank == root) {
-        eb = 0;
-        for (int k = 0; k < c->nranks && rc == RR_API_OK; k++) {
+        for (int k = 0; k < R && rc == RR_API_OK; k++) {
             const uint64_t nv = plan[k].v1 - plan[k].v0;
             rr_value *dv = whole->values + plan[k].v0;
-            rr_elem *de = whole->elems + eb;
+            rr_elem *de = whole->elems + at[k];
             if (k == root) {   /* the root's own shard: copy it in, unless it decoded in place */
                 hipError_t e2 = hipSuccess;
                 if (nv && (void *)mine->values != (void *)dv)
                     e2 = hipMemcpyAsync(dv, mine->values, nv * sizeof(rr_value), hipMemcpyDeviceToDevice, s);
-                if (e2 == hipSuccess && ne[k] && (void *)mine->elems != (void *)de)
-                    e2 = hipMemcpyAsync(de, mine->elems, ne[k] * sizeof(rr_elem), hipMemcpyDeviceToDevice, s);
+                if (e2 == hipSuccess && cnt[k] && (void *)mine->elems != (void *)de)
+                    e2 = hipMemcpyAsync(de, mine->elems, cnt[k] * sizeof(rr_elem), hipMemcpyDeviceToDevice, s);
                 if (e2 != hipSuccess) rc = rr_fail(RR_API_EHIP, "rr_gather copy: %s", hipGetErrorString(e2));
             }
             if (rc == RR_API_OK) {
-                hipError_t e3 = rr_launch_flat_rebase(dv, nv, de, ne[k], eb, plan[k].b0, s);
+                hipError_t e3 = rr_launch_flat_rebase(dv, nv, de, cnt[k], at[k], plan[k].b0, s);
                 if (e3 != hipSuccess) rc = rr_fail(RR_API_EHIP, "rr_gather rebase: %s", hipGetErrorString(e3));
             }
-            eb += ne[k];
         }
     }
-    free(ne);
+    free(got);
     return rc;
 }

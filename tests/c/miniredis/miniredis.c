@@ -77,6 +77,12 @@ int dictAdd(dict *d, void *key, void *val) {
     d->used++;
     return DICT_OK;
 }
+dictEntry *dictFind(dict *d, const void *key) {
+    for (unsigned long i = 0; i < d->used; i++)
+        if (sdslen(d->ents[i].key) == sdslen((const sds)key) && !memcmp(d->ents[i].key, key, sdslen((const sds)key)))
+            return &d->ents[i];
+    return NULL;
+}
 dictIterator *dictGetIterator(dict *d) { dictIterator *it = zmalloc(sizeof *it); it->d = d; it->i = 0; return it; }
 dictEntry *dictNext(dictIterator *it) { return it->i < it->d->used ? &it->d->ents[it->i++] : NULL; }
 void dictReleaseIterator(dictIterator *it) { zfree(it); }
@@ -202,7 +208,41 @@ void decrRefCount(robj *o) {
     zfree(o);
 }
 
-struct redisServer server = {-2, 0};   /* list-max-ziplist-size -2, list-compress-depth 0 */
+struct redisServer server = {-2, 0, NULL};   /* list-max-ziplist-size -2, list-compress-depth 0 */
+static redisDb mr_db0;
+void mr_init_db(void) {
+    if (!mr_db0.dict) mr_db0.dict = dictCreate(NULL, NULL);
+    server.db = &mr_db0;
+}
+
+sds sdsfromlonglong(long long value) {
+    char buf[32];
+    int l = ll2string(buf, sizeof buf, value);
+    return sdsnewlen(buf, (size_t)l);
+}
+
+char *mr_log;
+size_t mr_log_len;
+static size_t mr_log_cap;
+void mr_log_reset(void) { mr_log_len = 0; if (mr_log) mr_log[0] = 0; }
+void serverLog(int level, const char *fmt, ...) {
+    char line[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    int l = vsnprintf(line, sizeof line, fmt, ap);
+    va_end(ap);
+    if (l < 0) return;
+    if ((size_t)l >= sizeof line) l = (int)sizeof line - 1;
+    if (mr_log_len + (size_t)l + 2 > mr_log_cap) {
+        mr_log_cap = (mr_log_len + (size_t)l + 2) * 2;
+        mr_log = zrealloc(mr_log, mr_log_cap);
+    }
+    memcpy(mr_log + mr_log_len, line, (size_t)l);
+    mr_log_len += (size_t)l;
+    mr_log[mr_log_len++] = '\n';
+    mr_log[mr_log_len] = 0;
+    printf("[log %d] %s\n", level, line);
+}
 
 jmp_buf *mr_panic_jmp;
 char mr_panic_msg[256];

@@ -64,6 +64,7 @@ extern dictType setDictType, hashDictType, zsetDictType;
 dict *dictCreate(dictType *type, void *privDataPtr);
 int dictExpand(dict *d, unsigned long size);
 int dictAdd(dict *d, void *key, void *val);
+dictEntry *dictFind(dict *d, const void *key);
 dictIterator *dictGetIterator(dict *d);
 dictEntry *dictNext(dictIterator *iter);
 void dictReleaseIterator(dictIterator *iter);
@@ -113,8 +114,23 @@ robj *createIntsetObject(void);
 robj *createZsetObject(void);
 void decrRefCount(robj *o);
 
-struct redisServer { int list_max_ziplist_size; int list_compress_depth; };
+sds sdsfromlonglong(long long value);
+
+/* server.h:1059 keyspace of one database (the model keeps only its main dict) */
+typedef struct redisDb { dict *dict; } redisDb;
+struct redisServer { int list_max_ziplist_size; int list_compress_depth; redisDb *db; };
 extern struct redisServer server;
+void mr_init_db(void);   /* server.db[0] with an empty keyspace dict */
+
+/* serverLog levels, server.h:344-347; the model appends every line to mr_log (and stdout) */
+#define LL_DEBUG 0
+#define LL_VERBOSE 1
+#define LL_NOTICE 2
+#define LL_WARNING 3
+extern char *mr_log;       /* all lines logged so far, '\n'-separated */
+extern size_t mr_log_len;
+void mr_log_reset(void);
+void serverLog(int level, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
 
 extern jmp_buf *mr_panic_jmp;
 extern char mr_panic_msg[256];

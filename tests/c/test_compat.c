@@ -67,7 +67,41 @@ int main(void) {
         sdsfree(outs[i]);
         decrRefCount(objs[i]);
     }
-    printf("compat shim: %d fixtures round-tripped, %d rejected with a panic, batch of %zu; %d failures\n", checked,
-           panics, nok, fails);
+    /* a fork child's route (rock.c:538): desObject through the parent's decode service thread
+     * (the process routes as a child; the service decodes on the GPU), then the objects compared
+     * through serObject back in parent mode; the engine itself must refuse child use */
+    const fixture_t *fx = NULL;
+    CHECK(rr_compat_service_start() == 0, "decode service start");
+    rr_compat_test_as_child(1);
+    rr_compat_des_batch(bufs, lens, nok, objs);
+    int child_panics = 0;
+    for (int i = 0; i < N_FIXTURES; i++) {
+        if (!FIXTURES[i].status) continue;
+        jmp_buf jb;
+        mr_panic_jmp = &jb;
+        if (setjmp(jb) == 0) (void)desObject((void *)FIXTURES[i].blob, FIXTURES[i].len);
+        else child_panics++;
+    }
+    {
+        jmp_buf jb;
+        mr_panic_jmp = &jb;
+        volatile int refused = 0;
+        if (setjmp(jb) == 0) (void)serObject(objs[0]);
+        else refused = strstr(mr_panic_msg, "fork child") != NULL;
+        CHECK(refused, "serObject in a child must refuse the GPU: %s", mr_panic_msg);
+        mr_panic_jmp = NULL;
+    }
+    rr_compat_test_as_child(0);
+    rr_compat_ser_batch(objs, nok, outs);
+    for (size_t i = 0; i < nok; i++) {
+        fx = okfx[i];
+        CHECK(sdslen(outs[i]) == fx->out_len && !memcmp(outs[i], fx->out, fx->out_len), "child-route round trip differs");
+        sdsfree(outs[i]);
+        decrRefCount(objs[i]);
+    }
+    fx = &FIXTURES[0];
+    CHECK(child_panics == panics, "child route rejected %d malformed blobs, parent %d", child_panics, panics);
+    printf("compat shim: %d fixtures round-tripped, %d rejected with a panic, batch of %zu, child route %zu + %d; "
+           "%d failures\n", checked, panics, nok, nok, child_panics, fails);
     return fails ? 1 : 0;
 }

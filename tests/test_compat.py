@@ -51,7 +51,7 @@ def build(tmp):
            os.path.join(ROOT, "redrock_old_amd", "compat", "rock_serdes_compat.c"),
            os.path.join(ROOT, "tests", "c", "miniredis", "miniredis.c"),
            os.path.join(ROOT, "tests", "c", "test_compat.c"),
-           "-L", os.path.join(ROOT, "redrock_old_amd"), "-lrr_serdes",
+           "-L", os.path.join(ROOT, "redrock_old_amd"), "-lrr_serdes", "-lpthread",
            "-Wl,-rpath," + os.path.join(ROOT, "redrock_old_amd"), "-o", exe]
     subprocess.run(cmd, check=True)
     return exe
@@ -63,6 +63,40 @@ def test_compat_shim_builds_as_c(tmp_path):
     nm = subprocess.run(["nm", exe], capture_output=True, text=True, check=True).stdout
     for sym in ("desObject", "desString", "serObject", "rr_compat_des_batch", "rr_compat_ser_batch"):
         assert f" T {sym}" in nm, sym
+
+
+def build_link(tmp):
+    """tests/c/test_rock_link.c: rock_serdes.h:47-55 exactly as rock.c sees them, linked against
+    the shim + the Redis model + librr_serdes.so."""
+    exe = os.path.join(tmp, "test_rock_link")
+    cmd = ["gcc", "-std=gnu11", "-O1", "-Wall", "-Werror", "-Wno-unused-function", "-DRR_REDIS_TREE",
+           "-I", os.path.join(ROOT, "tests", "c", "miniredis"), "-I", os.path.join(ROOT, "include"),
+           os.path.join(ROOT, "redrock_old_amd", "compat", "rock_serdes_compat.c"),
+           os.path.join(ROOT, "tests", "c", "miniredis", "miniredis.c"),
+           os.path.join(ROOT, "tests", "c", "test_rock_link.c"),
+           "-L", os.path.join(ROOT, "redrock_old_amd"), "-lrr_serdes", "-lpthread",
+           "-Wl,-rpath," + os.path.join(ROOT, "redrock_old_amd"), "-o", exe]
+    subprocess.run(cmd, check=True)
+    return exe
+
+
+def test_rock_c_call_set_links(tmp_path):
+    """Every function rock_serdes.h:47-55 declares is defined by the shim, so rock.c's call set
+    (desObject :468/:538, serObject :691, the ROCK testserdes* hooks :175-183) links unchanged."""
+    exe = build_link(str(tmp_path))
+    nm = subprocess.run(["nm", exe], capture_output=True, text=True, check=True).stdout
+    for sym in ("desString", "serObject", "desObject", "_test_ser_des_string", "_test_ser_des_list",
+                "_test_ser_des_set", "_test_ser_des_hash", "_test_ser_des_zset"):
+        assert f" T {sym}" in nm, sym
+
+
+@pytest.mark.gpu
+def test_rock_c_call_set_runs_on_gpu(tmp_path):
+    exe = build_link(str(tmp_path))
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    print(r.stdout[-4000:], r.stderr[-2000:])
+    assert r.returncode == 0, r.stdout[-4000:] + r.stderr
+    assert "0 failures" in r.stdout
 
 
 @pytest.mark.gpu

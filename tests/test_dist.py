@@ -1,7 +1,12 @@
-"""Sharding across ranks: byte-balanced partition, offset/elem_base rebase,
-root split/gather over torch.distributed.  CPU tests use gloo with world_size 2 and the C
-oracle as the per-shard decoder (the checker stands in for the device here; the GPU test at
-the bottom decodes every shard through the HIP C-ABI)."""
+"""Sharding across ranks through the C library's own plan, placement and
+rebase: rr_shard_plan (the rule shard_plan_kernel runs for rr_split_plan), rr_gather_layout
+(where rr_gather puts each shard's descriptors) and rr_flat_rebase_host / rr_flat_rebase (the
+placement flat_rebase_kernel applies on the root).  CPU tests: gloo with world size 2, the
+transfers in rr_split's / rr_gather's pairing (the root sends each peer its bytes + offsets;
+every peer sends the root its records + descriptors after an all-gather of the descriptor
+counts), the C oracle as the per-shard decoder (the checker stands in for the device on CPU).
+GPU tests: every shard decoded through the HIP C-ABI, placed by the device rebase, and the RCCL
+entry points with one rank."""
 import os
 import socket
 
@@ -12,7 +17,6 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 import redrock_old_amd as rr
-from redrock_old_amd import shard
 from oracle import cpu
 
 from helpers import assert_flat_equal
@@ -24,40 +28,82 @@ def _whole(cfg, n, seed=None):
     return data, offs, v, e
 
 
+def shard_of(data, offsets, lo, hi):
+    """What rr_split hands rank k: values [lo, hi)'s bytes in a zero-padded 16-aligned buffer
+    and their offsets rebased to 0 (offsets_rebase_kernel)."""
+    offsets = np.asarray(offsets, np.uint64)
+    b0, b1 = int(offsets[lo]), int(offsets[hi])
+    buf = np.zeros((b1 - b0 + 15) & ~15, np.uint8)
+    buf[: b1 - b0] = data[b0:b1]
+    return buf, (offsets[lo: hi + 1] - offsets[lo]).astype(np.uint64)
+
+
+def place(plan, parts, n):
+    """The root's placement of decoded shards (values, elems) — rr_gather's layout and rebase,
+    through the C library's host forms."""
+    at, tot = rr.gather_layout([len(e) for _, e in parts])
+    vals = np.zeros(n, rr.VALUE_DT)
+    els = np.zeros(tot, rr.ELEM_DT)
+    for k, (sv, se) in enumerate(parts):
+        v0, v1, b0 = int(plan[k][0]), int(plan[k][1]), int(plan[k][2])
+        dv = np.array(sv, rr.VALUE_DT, copy=True)
+        de = np.array(se, rr.ELEM_DT, copy=True)
+        rr.flat_rebase_host(dv, de, int(at[k]), b0)
+        vals[v0:v1] = dv
+        els[int(at[k]):int(at[k]) + len(de)] = de
+    return vals, els
+
+
 @pytest.mark.parametrize("g", [1, 2, 3, 8])
-def test_partition_balanced(g):
+def test_plan_balanced(g):
     data, offs = rr.gen_batch(4, 5000)
-    cuts = shard.partition(offs, g)
-    assert cuts[0] == 0 and cuts[-1] == 5000 and np.all(np.diff(cuts) >= 0)
+    plan = rr.shard_plan(offs, g)
+    assert plan[0, 0] == 0 and plan[-1, 1] == 5000 and (plan[1:, 0] == plan[:-1, 1]).all()
     total = int(offs[-1])
-    sizes = [int(offs[cuts[k + 1]] - offs[cuts[k]]) for k in range(g)]
-    assert sum(sizes) == total
+    sizes = (plan[:, 3] - plan[:, 2]).astype(np.int64)
+    assert int(sizes.sum()) == total
     big = int(np.max(np.diff(offs.astype(np.int64))))
     for s in sizes:   # each shard within one value of the even split
-        assert abs(s - total / g) <= big + 1
+        assert abs(int(s) - total / g) <= big + 1
+    for k in range(g):   # shard k starts at the first value at or after k * total / g
+        t = (total * k) // g
+        v0 = int(plan[k, 0])
+        assert k == 0 or (int(offs[v0]) >= t and (v0 == 0 or int(offs[v0 - 1]) < t))
 
 
-def test_partition_edges():
-    assert list(shard.partition(np.zeros(1, np.uint64), 4)) == [0, 0, 0, 0, 0]
+def test_plan_edges():
+    plan = rr.shard_plan(np.zeros(1, np.uint64), 4)
+    assert (plan == 0).all()
     offs = np.array([0, 100], np.uint64)   # one value: it lands in one shard
-    cuts = shard.partition(offs, 3)
-    assert cuts[0] == 0 and cuts[-1] == 1
+    plan = rr.shard_plan(offs, 3)
+    assert plan[0, 0] == 0 and plan[-1, 1] == 1 and int((plan[:, 1] - plan[:, 0]).sum()) == 1
+
+
+def test_gather_layout_and_32bit_guard():
+    at, tot = rr.gather_layout([5, 0, 7, 1])
+    assert list(at) == [0, 5, 5, 12] and tot == 13
+    with pytest.raises(rr.RRError):
+        rr.gather_layout([2 ** 31, 2 ** 31])   # past 2^32 - 1: elem_base is 32-bit
+    v = np.zeros(1, rr.VALUE_DT)
+    e = np.zeros(1, rr.ELEM_DT)
+    with pytest.raises(rr.RRError):
+        rr.flat_rebase_host(v, e, 2 ** 32 - 1, 0)
+    rr.flat_rebase_host(v, e, 2 ** 32 - 2, 16)
+    assert int(v[0]["elem_base"]) == 2 ** 32 - 2 and int(e[0]["data"]) == 0   # zero slots stay zero
 
 
 @pytest.mark.parametrize("cfg,g", [(4, 2), (4, 5), (10, 3), (3, 4)])
 def test_rebase_equals_whole_decode(cfg, g):
     data, offs, v, e = _whole(cfg, 3000 if cfg != 10 else 600)
     n = len(offs) - 1
-    cuts = shard.partition(offs, g)
+    plan = rr.shard_plan(offs, g)
     parts = []
     for k in range(g):
-        d, o = shard.shard_of(data, offs, int(cuts[k]), int(cuts[k + 1]))
+        d, o = shard_of(data, offs, int(plan[k, 0]), int(plan[k, 1]))
         assert len(d) % 16 == 0
         sv, se, _, _ = cpu.decode(d, o)
-        parts.append((sv, se, int(offs[cuts[k]])))
-    got = shard.rebase_flat(parts)
-    assert len(got[0]) == n
-    assert_flat_equal(got, (v, e), f"cfg {cfg} g {g}")
+        parts.append((sv, se))
+    assert_flat_equal(place(plan, parts, n), (v, e), f"cfg {cfg} g {g}")
 
 
 def _free_port():
@@ -66,22 +112,72 @@ def _free_port():
         return s.getsockname()[1]
 
 
+def _t(a):
+    return torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).copy())
+
+
 def _worker(rank, world, port, cfg, n, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        dev = torch.device("cpu")
+        root = 0
         data = offs = None
-        if rank == 0:
+        # rr_split_plan: the root plans (rr_shard_plan), every rank gets the plan
+        plan_t = torch.zeros(world * 4, dtype=torch.int64)
+        if rank == root:
             data, offs = rr.gen_batch(cfg, n)
-        d, o, lo, b0 = shard.split(dist, torch, dev, data, offs)
+            plan_t.copy_(torch.from_numpy(rr.shard_plan(offs, world).view(np.int64).reshape(-1)))
+        dist.broadcast(plan_t, root)
+        plan = plan_t.numpy().view(np.uint64).reshape(world, 4)
+        v0, v1, b0, b1 = (int(x) for x in plan[rank])
+        # rr_split: the root sends each peer its bytes and offsets; the peer rebases them to 0
+        if rank == root:
+            for k in range(world):
+                if k == root:
+                    continue
+                kb0, kb1, kv0, kv1 = int(plan[k, 2]), int(plan[k, 3]), int(plan[k, 0]), int(plan[k, 1])
+                if kb1 > kb0:
+                    dist.send(_t(data[kb0:kb1]), k)
+                dist.send(_t(offs[kv0:kv1 + 1]), k)
+            d, o = shard_of(data, offs, v0, v1)
+        else:
+            buf = torch.zeros(b1 - b0, dtype=torch.uint8)
+            if b1 > b0:
+                dist.recv(buf, root)
+            ob = torch.zeros((v1 - v0 + 1) * 8, dtype=torch.uint8)
+            dist.recv(ob, root)
+            d = np.zeros((b1 - b0 + 15) & ~15, np.uint8)
+            d[: b1 - b0] = buf.numpy()
+            o = ob.numpy().view(np.uint64) - np.uint64(b0)
         sv, se, _, _ = cpu.decode(d, o)
-        out = shard.gather(dist, torch, dev, sv, se, b0)
-        if rank == 0:
+        # rr_gather: all-gather of the descriptor counts, peers send records + descriptors,
+        # the root places them (rr_gather_layout) and rebases them (rr_flat_rebase_host)
+        ne = torch.zeros(world, dtype=torch.int64)
+        dist.all_gather_into_tensor(ne, torch.tensor([len(se)], dtype=torch.int64))
+        ne = [int(x) for x in ne]
+        if rank == root:
+            parts = []
+            for k in range(world):
+                if k == root:
+                    parts.append((sv, se))
+                    continue
+                kv = int(plan[k, 1] - plan[k, 0])
+                vb = torch.zeros(kv * 16, dtype=torch.uint8)
+                eb = torch.zeros(ne[k] * 16, dtype=torch.uint8)
+                if kv:
+                    dist.recv(vb, k)
+                if ne[k]:
+                    dist.recv(eb, k)
+                parts.append((vb.numpy().view(rr.VALUE_DT), eb.numpy().view(rr.ELEM_DT)))
             wv, we, _, _ = cpu.decode(data, offs)
-            assert_flat_equal(out, (wv, we), f"split/gather cfg {cfg}")
-        q.put((rank, "ok", lo, len(o) - 1))
+            assert_flat_equal(place(plan, parts, n), (wv, we), f"split/gather cfg {cfg}")
+        else:
+            if v1 > v0:
+                dist.send(_t(sv), root)
+            if ne[rank]:
+                dist.send(_t(se), root)
+        q.put((rank, "ok", v0, v1 - v0))
     except Exception as ex:   # report to the parent
         q.put((rank, repr(ex), -1, -1))
     finally:
@@ -108,13 +204,13 @@ def test_sharded_device_decode_equals_whole(engine):
     """Every shard decoded by the HIP engine, rebased, equals the engine's whole-batch decode
     and the oracle's."""
     data, offs, v, e = _whole(4, 20000)
-    cuts = shard.partition(offs, 4)
+    plan = rr.shard_plan(offs, 4)
     parts = []
     for k in range(4):
-        d, o = shard.shard_of(data, offs, int(cuts[k]), int(cuts[k + 1]))
+        d, o = shard_of(data, offs, int(plan[k, 0]), int(plan[k, 1]))
         sv, se, _, _ = engine.decode_host(d, o)
-        parts.append((sv, se, int(offs[cuts[k]])))
-    assert_flat_equal(shard.rebase_flat(parts), (v, e), "sharded HIP decode")
+        parts.append((sv, se))
+    assert_flat_equal(place(plan, parts, len(offs) - 1), (v, e), "sharded HIP decode")
 
 
 @pytest.mark.parametrize("g", [2, 7])
@@ -125,22 +221,26 @@ def test_rebase_with_malformed_values(g):
     fx = (golden()["kats"] + golden()["edges"]) * 3
     data, offs = batch_from_blobs([bytes.fromhex(f["blob"]) for f in fx])
     assert any(f["value"].get("status", 0) for f in fx)
-    cuts = shard.partition(offs, g)
+    plan = rr.shard_plan(offs, g)
     parts = []
     for k in range(g):
-        d, o = shard.shard_of(data, offs, int(cuts[k]), int(cuts[k + 1]))
+        d, o = shard_of(data, offs, int(plan[k, 0]), int(plan[k, 1]))
         sv, se, _, _ = cpu.decode(d, o)
-        parts.append((sv, se, int(offs[cuts[k]])))
-    assert_flat_equal(shard.rebase_flat(parts), expected_flat(fx), f"golden g {g}")
+        parts.append((sv, se))
+    assert_flat_equal(place(plan, parts, len(offs) - 1), expected_flat(fx), f"golden g {g}")
 
 
 @pytest.mark.parametrize("n,g", [(5000, 1), (5000, 3), (5000, 8), (3, 8), (0, 4), (1, 3)])
-def test_c_shard_plan_matches_partition(n, g):
-    """The C library's plan (rr_shard_plan, the rule shard_plan_kernel runs on the device for
-    rr_split_plan) is the host partition's."""
+def test_c_shard_plan_rule(n, g):
+    """rr_shard_plan (the rule shard_plan_kernel runs on the device for rr_split_plan): shard k
+    starts at the first value whose first byte is at or after floor(total * k / g)."""
     _, offs = rr.gen_batch(4, n) if n else (None, np.zeros(1, np.uint64))
     plan = rr.shard_plan(offs, g)
-    cuts = shard.partition(offs, g)
+    total = int(offs[-1])
+    targets = np.array([(total * k) // g for k in range(g + 1)], np.uint64)
+    cuts = np.searchsorted(offs[:n], targets, side="left").astype(np.int64)
+    cuts[0], cuts[-1] = 0, n
+    cuts = np.maximum.accumulate(cuts)
     assert (plan[:, 0] == cuts[:-1]).all() and (plan[:, 1] == cuts[1:]).all()
     assert (plan[:, 2] == offs[cuts[:-1]]).all() and (plan[:, 3] == offs[cuts[1:]]).all()
 
@@ -153,7 +253,7 @@ def _device_shards(engine, data, offs, g, torch_dev):
     parts, ne_tot = [], 0
     for k in range(g):
         v0, v1, b0, b1 = (int(x) for x in plan[k])
-        d, o = shard.shard_of(data, offs, v0, v1)
+        d, o = shard_of(data, offs, v0, v1)
         nv, nb = v1 - v0, b1 - b0
         cap = rr.elem_bound(nv, nb)
         t_vals = torch.zeros(max(nv, 1) * 16, dtype=torch.uint8, device=torch_dev)[:nv * 16]
@@ -167,14 +267,14 @@ def _device_shards(engine, data, offs, g, torch_dev):
         ne_tot += ne
     w_vals = torch.zeros(max(n, 1) * 16, dtype=torch.uint8, device=torch_dev)
     w_elems = torch.zeros(max(ne_tot, 1) * 16, dtype=torch.uint8, device=torch_dev)
-    eb = 0
+    at, tot = rr.gather_layout([p[2] for p in parts])   # rr_gather's placement
+    assert tot == ne_tot
     for k, (t_vals, t_elems, ne, b0) in enumerate(parts):
-        v0, v1 = int(plan[k][0]), int(plan[k][1])
+        v0, v1, eb = int(plan[k][0]), int(plan[k][1]), int(at[k])
         dv, de = w_vals[v0 * 16:v1 * 16], w_elems[eb * 16:(eb + ne) * 16]
         dv.copy_(t_vals)
         de.copy_(t_elems)
         engine.flat_rebase(dv, de, eb, b0)
-        eb += ne
     torch.cuda.synchronize()
     return w_vals[:n * 16], w_elems[:ne_tot * 16]
 
