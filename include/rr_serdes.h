@@ -178,7 +178,9 @@ int rr_copy_device(rr_ctx *ctx, void *dst, const void *src, uint64_t bytes, void
 
 /* ---- synthetic batches (BASELINE.json configs) ------------------------ */
 /* config: 1 = 64-B RAW strings, 2 = Zipf 16B-4KiB strings, 3 = 16-pair hash ziplists,
- *         4 = mixed (config-4 proportions; also the 1M headline batch and config 5 shards),
+ *         4 = mixed (config-4 proportions; also the 1M headline batch),
+ *         5 = config-4 proportions, seekable: value i drawn from its own seed (the 100M batch
+ *             of BASELINE config 5, any shard of it generated alone — rr_gen_range),
  *         10 = edge cases, 11 = mixed with large values.  Host memory, malloc'd. */
 typedef struct rr_host_batch {
     uint8_t  *data;
@@ -189,6 +191,13 @@ typedef struct rr_host_batch {
 int  rr_gen_batch(int config, uint64_t n, uint64_t seed, rr_host_batch *out);
 void rr_host_batch_free(rr_host_batch *b);
 uint64_t rr_gen_default_seed(int config);   /* 0x5EED0000 + config */
+/* Config 5 only, nthreads host threads: blob bytes and descriptor counts (either may be NULL) of
+ * values [v0, v1) of the seeded batch, without keeping their bytes; and the blobs of values
+ * [v0, v1) (out->offsets relative to the range's first byte) — equal to the same range of
+ * rr_gen_batch(5, n, seed) for any n >= v1. */
+int rr_gen_sizes(int config, uint64_t v0, uint64_t v1, uint64_t seed, uint64_t *bytes, uint32_t *descs,
+                 int nthreads);
+int rr_gen_range(int config, uint64_t v0, uint64_t v1, uint64_t seed, rr_host_batch *out, int nthreads);
 
 #ifdef __cplusplus
 }

@@ -16,9 +16,18 @@
  *                     bounds, the eof + CheckLength test of InternalUncompressAllTags), with a
  *                     status code per failure instead of `false`.
  *
- * Pinned against an independent build of the same published algorithm: pyarrow's bundled
- * snappy (tests/test_snappy.py) — byte-identical compressed output and identical accept /
- * reject decisions on the reference's own deps/snappy/testdata files (tests/golden/snappy/).
+ * What pins it (tests/test_snappy.py):
+ *   - the reference's own test inputs (tests/snappy_reference.py): baddata{1,2,3}.snappy are
+ *     rejected with a sane length (snappy_unittest.cc:583-597), the corruption cases of
+ *     :531-580 and :888-965 get the verdicts that test requires, and the corpus files of its
+ *     `files[]` table (tests/golden/snappy/, copied from deps/snappy/testdata) round-trip;
+ *   - an independent build of the format, pyarrow's bundled snappy (a later release): every
+ *     stream either side writes decompresses on the other to the input, and both accept and
+ *     reject the same hand-built and mutated streams.
+ * Not pinned: the compressor's exact bytes.  They follow 1.1.8's CompressFragment as restated
+ * from its source; later snappy releases changed the match finder, so pyarrow's compressed
+ * bytes differ from 1.1.8's, and the reference ships no 1.1.8 compressed output — compression
+ * bit-exactness against 1.1.8 itself is parity unpinned.
  */
 #include "rr_snappy.h"
 

@@ -71,7 +71,7 @@ EXPORTS = ["rr_ctx_create", "rr_ctx_destroy", "rr_ctx_reserve", "rr_last_error",
            "rr_encode_batch", "rr_decode_elem_bound", "rr_decode_batch_host", "rr_encode_batch_host",
            "rr_gen_batch", "rr_host_batch_free", "rr_gen_default_seed", "rr_shard_plan", "rr_flat_rebase",
            "rr_comm_get_id", "rr_comm_init", "rr_comm_destroy", "rr_split_plan", "rr_split", "rr_gather",
-           "rr_flat_rebase_host", "rr_gather_layout", "rr_copy_device"]
+           "rr_flat_rebase_host", "rr_gather_layout", "rr_copy_device", "rr_gen_sizes", "rr_gen_range"]
 COMM_ID_BYTES = 128
 # include/rr_snappy.h (GPU block compression)
 SNAPPY_EXPORTS = ["rr_snappy_max_compressed_length", "rr_snappy_compress_bound", "rr_snappy_compress_batch",
@@ -114,6 +114,8 @@ def lib():
     L.rr_gen_batch.argtypes = [C.c_int, u64, u64, C.POINTER(HostBatch)]
     L.rr_host_batch_free.argtypes = [C.POINTER(HostBatch)]
     L.rr_host_batch_free.restype = None
+    L.rr_gen_sizes.argtypes = [C.c_int, u64, u64, u64, vp, vp, C.c_int]
+    L.rr_gen_range.argtypes = [C.c_int, u64, u64, u64, C.POINTER(HostBatch), C.c_int]
     L.rr_gen_default_seed.argtypes = [C.c_int]
     L.rr_gen_default_seed.restype = u64
     L.rr_shard_plan.argtypes = [vp, u64, C.c_uint32, C.POINTER(Shard)]
@@ -159,6 +161,35 @@ def gen_batch(config: int, n: int, seed: int | None = None):
     _check(L.rr_gen_batch(config, n, seed, C.byref(hb)))
     try:
         nbytes = int(hb.bytes)
+        padded = (nbytes + 15) & ~15
+        data = np.ctypeslib.as_array(hb.data, shape=(max(padded, 1),))[:padded].copy() if padded else \
+            np.zeros(0, np.uint8)
+        offs = np.ctypeslib.as_array(hb.offsets, shape=(n + 1,)).copy()
+    finally:
+        L.rr_host_batch_free(C.byref(hb))
+    return data, offs
+
+
+def gen_sizes(config: int, v0: int, v1: int, seed: int | None = None, nthreads: int = 8):
+    """Config 5 (seekable): (blob bytes uint64, descriptor counts uint32) of values [v0, v1)."""
+    L = lib()
+    if seed is None:
+        seed = L.rr_gen_default_seed(config)
+    nb = np.zeros(max(v1 - v0, 1), np.uint64)
+    nd = np.zeros(max(v1 - v0, 1), np.uint32)
+    _check(L.rr_gen_sizes(config, v0, v1, seed, _ptr(nb), _ptr(nd), nthreads))
+    return nb[:v1 - v0], nd[:v1 - v0]
+
+
+def gen_range(config: int, v0: int, v1: int, seed: int | None = None, nthreads: int = 8):
+    """Config 5 (seekable): (data uint8 padded to 16, offsets relative to v0) of values [v0, v1)."""
+    L = lib()
+    if seed is None:
+        seed = L.rr_gen_default_seed(config)
+    hb = HostBatch()
+    _check(L.rr_gen_range(config, v0, v1, seed, C.byref(hb), nthreads))
+    try:
+        n, nbytes = v1 - v0, int(hb.bytes)
         padded = (nbytes + 15) & ~15
         data = np.ctypeslib.as_array(hb.data, shape=(max(padded, 1),))[:padded].copy() if padded else \
             np.zeros(0, np.uint8)

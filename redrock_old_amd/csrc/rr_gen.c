@@ -11,6 +11,7 @@
  */
 #define _GNU_SOURCE
 #include <math.h>
+#include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -333,23 +334,29 @@ static uint64_t zipf_draw(zipf_t *z, rng_t *r) {
 /* config-4 proportions: 40% String (INT 10 / EMBSTR 45 / RAW 45),
  * 15% List (16, 50% ints), 15% Set (intset 16 w=2/4/8 | HT 16, 50/50),
  * 15% Hash (ziplist 16 pairs 80% | HT 16 pairs 20%), 15% ZSet (ziplist 80% | skiplist 20%). */
-static void gen_mixed(buf_t *o, rng_t *r, zipf_t *zraw, uint64_t scale) {
+/* returns the descriptors the value decodes to (rr_format.h element layout), from what it
+ * generated: String 1, List / intset / HT set n, hash / zset ziplist 1 + 2n, HT hash / skiplist 2n */
+static uint64_t gen_mixed(buf_t *o, rng_t *r, zipf_t *zraw, uint64_t scale) {
     uint64_t t = rnd_below(r, 100), u = rnd_below(r, 100);
     uint64_t ne = 16 * scale;
     if (t < 40) {
         if (u < 10) gen_string(o, r, RR_ENC_INT, 0, rand_logint(r), 0);
         else if (u < 55) gen_string(o, r, RR_ENC_EMBSTR, rnd_range(r, 1, 44), 0, 1);
         else gen_string(o, r, RR_ENC_RAW, zipf_draw(zraw, r) * scale, 0, 1);
-    } else if (t < 55) gen_list(o, r, ne, 50, 1, 64);
+        return 1;
+    } else if (t < 55) { gen_list(o, r, ne, 50, 1, 64); return ne; }
     else if (t < 70) {
         if (u < 50) gen_intset(o, r, ne, (unsigned[]){2, 4, 8}[rnd_below(r, 3)]);
         else gen_set_ht(o, r, ne, 1, 64);
+        return ne;
     } else if (t < 85) {
-        if (u < 80) gen_hash_zl(o, r, ne, 1, 64, 25);
-        else gen_hash_ht(o, r, ne, 65, 128);
+        if (u < 80) { gen_hash_zl(o, r, ne, 1, 64, 25); return 1 + 2 * ne; }
+        gen_hash_ht(o, r, ne, 65, 128);
+        return 2 * ne;
     } else {
-        if (u < 80) gen_zset_zl(o, r, ne, 1, 64);
-        else gen_zset_sl(o, r, ne, 65, 128);
+        if (u < 80) { gen_zset_zl(o, r, ne, 1, 64); return 1 + 2 * ne; }
+        gen_zset_sl(o, r, ne, 65, 128);
+        return 2 * ne;
     }
 }
 
@@ -441,6 +448,131 @@ static void gen_edge(buf_t *o, rng_t *r, uint64_t k) {
     }
 }
 
+/* ------------------------------------------------------------------ config 5: seekable */
+/* BASELINE config 5 (100M values in config-4 proportions over 8 GPUs): value i is drawn from
+ * its own seed, so any value range of the batch — one GPU's shard — can be generated alone,
+ * and the sizes of all 100M values without keeping their bytes. */
+static uint64_t value_seed(uint64_t seed, uint64_t i) {
+    uint64_t x = seed ^ (i * 0xD1B54A32D192ED03ull);
+    return splitmix(&x);
+}
+
+typedef struct {
+    uint64_t v0, v1, seed;
+    const zipf_t *z;
+    uint64_t *bytes;    /* sizes pass: per-value blob bytes (or NULL) */
+    uint32_t *descs;    /* per-value descriptor counts (or NULL) */
+    buf_t out;          /* range pass: the chunk's blobs */
+    uint64_t *offs;     /* range pass: v1 - v0 + 1 chunk-relative offsets */
+    int keep;           /* range pass: keep the bytes */
+} genjob_t;
+
+static void *gen_worker(void *arg) {
+    genjob_t *j = (genjob_t *)arg;
+    buf_t tmp = {0};
+    buf_t *o = j->keep ? &j->out : &tmp;
+    if (j->offs) j->offs[0] = 0;
+    for (uint64_t i = j->v0; i < j->v1; i++) {
+        rng_t r; rng_seed(&r, value_seed(j->seed, i));
+        const uint64_t start = o->n;
+        const uint64_t nd = gen_mixed(o, &r, (zipf_t *)j->z, 1);
+        if (j->bytes) j->bytes[i - j->v0] = o->n - start;
+        if (j->descs) j->descs[i - j->v0] = (uint32_t)nd;
+        if (j->offs) j->offs[i - j->v0 + 1] = o->n;
+        if (!j->keep) o->n = 0;
+    }
+    free(tmp.p);
+    return NULL;
+}
+
+static int run_jobs(genjob_t *jobs, int nt) {
+    pthread_t th[64];
+    int started = 0, rc = RR_API_OK;
+    for (int k = 1; k < nt; k++) {
+        if (pthread_create(&th[k], NULL, gen_worker, &jobs[k]) != 0) { rc = RR_API_ENOMEM; break; }
+        started = k;
+    }
+    gen_worker(&jobs[0]);
+    for (int k = 1; k <= started; k++) pthread_join(th[k], NULL);
+    if (rc != RR_API_OK)   /* the jobs that never started: run them here */
+        for (int k = started + 1; k < nt; k++) gen_worker(&jobs[k]);
+    return RR_API_OK;
+}
+
+static int clamp_threads(int nt, uint64_t n) {
+    if (nt < 1) nt = 1;
+    if (nt > 64) nt = 64;
+    if ((uint64_t)nt > n / 4096 + 1) nt = (int)(n / 4096 + 1);
+    return nt;
+}
+
+int rr_gen_sizes(int config, uint64_t v0, uint64_t v1, uint64_t seed, uint64_t *bytes, uint32_t *descs, int nthreads) {
+    if (config != 5 || v1 < v0 || (!bytes && !descs)) return RR_API_EINVAL;
+    zipf_t z = {0};
+    zipf_init(&z, 45, 4096);
+    const uint64_t n = v1 - v0;
+    const int nt = clamp_threads(nthreads, n);
+    genjob_t jobs[64];
+    memset(jobs, 0, sizeof jobs);
+    for (int k = 0; k < nt; k++) {
+        jobs[k].v0 = v0 + n * (uint64_t)k / (uint64_t)nt;
+        jobs[k].v1 = v0 + n * (uint64_t)(k + 1) / (uint64_t)nt;
+        jobs[k].seed = seed;
+        jobs[k].z = &z;
+        jobs[k].bytes = bytes ? bytes + (jobs[k].v0 - v0) : NULL;
+        jobs[k].descs = descs ? descs + (jobs[k].v0 - v0) : NULL;
+    }
+    const int rc = run_jobs(jobs, nt);
+    free(z.cdf);
+    return rc;
+}
+
+int rr_gen_range(int config, uint64_t v0, uint64_t v1, uint64_t seed, rr_host_batch *out, int nthreads) {
+    if (!out || config != 5 || v1 < v0) return RR_API_EINVAL;
+    memset(out, 0, sizeof *out);
+    zipf_t z = {0};
+    zipf_init(&z, 45, 4096);
+    const uint64_t n = v1 - v0;
+    const int nt = clamp_threads(nthreads, n);
+    genjob_t jobs[64];
+    memset(jobs, 0, sizeof jobs);
+    int rc = RR_API_OK;
+    for (int k = 0; k < nt; k++) {
+        jobs[k].v0 = v0 + n * (uint64_t)k / (uint64_t)nt;
+        jobs[k].v1 = v0 + n * (uint64_t)(k + 1) / (uint64_t)nt;
+        jobs[k].seed = seed;
+        jobs[k].z = &z;
+        jobs[k].keep = 1;
+        jobs[k].offs = (uint64_t *)malloc(sizeof(uint64_t) * (jobs[k].v1 - jobs[k].v0 + 1));
+        if (!jobs[k].offs) rc = RR_API_ENOMEM;
+    }
+    uint64_t *off = (uint64_t *)malloc(sizeof(uint64_t) * (n + 1));
+    if (!off) rc = RR_API_ENOMEM;
+    if (rc == RR_API_OK) rc = run_jobs(jobs, nt);
+    uint64_t total = 0;
+    for (int k = 0; k < nt; k++) total += jobs[k].out.n;
+    const uint64_t padded = (total + 15) & ~15ull;
+    uint8_t *data = NULL;
+    if (rc == RR_API_OK && posix_memalign((void **)&data, 64, padded ? padded : 16)) rc = RR_API_ENOMEM;
+    if (rc == RR_API_OK) {
+        uint64_t base = 0;
+        off[0] = 0;
+        for (int k = 0; k < nt; k++) {
+            const uint64_t m = jobs[k].v1 - jobs[k].v0;
+            if (jobs[k].out.n) memcpy(data + base, jobs[k].out.p, jobs[k].out.n);
+            for (uint64_t i = 1; i <= m; i++) off[jobs[k].v0 - v0 + i] = base + jobs[k].offs[i];
+            base += jobs[k].out.n;
+        }
+        memset(data + total, 0, padded - total);
+        out->data = data; out->offsets = off; out->n = n; out->bytes = total;
+    } else {
+        free(off);
+    }
+    for (int k = 0; k < nt; k++) { free(jobs[k].out.p); free(jobs[k].offs); }
+    free(z.cdf);
+    return rc;
+}
+
 /* ------------------------------------------------------------------ API */
 uint64_t rr_gen_default_seed(int config) { return 0x5EED0000ull + (uint64_t)config; }
 
@@ -453,7 +585,7 @@ int rr_gen_batch(int config, uint64_t n, uint64_t seed, rr_host_batch *out) {
     if (!off) return RR_API_ENOMEM;
     zipf_t zs = {0}, zr = {0};
     if (config == 2) zipf_init(&zs, 16, 4096);
-    if (config == 4 || config == 11) zipf_init(&zr, 45, 4096);
+    if (config == 4 || config == 5 || config == 11) zipf_init(&zr, 45, 4096);
     off[0] = 0;
     for (uint64_t i = 0; i < n; i++) {
         switch (config) {
@@ -462,6 +594,10 @@ int rr_gen_batch(int config, uint64_t n, uint64_t seed, rr_host_batch *out) {
                   gen_string(&o, &r, s <= RR_EMBSTR_SIZE_LIMIT ? RR_ENC_EMBSTR : RR_ENC_RAW, s, 0, 1); break; }
         case 3: gen_hash_zl(&o, &r, 16, 1, 64, 25); break;
         case 4: gen_mixed(&o, &r, &zr, 1); break;
+        case 5: {   /* seekable: value i from its own seed (rr_gen_range) */
+            rng_t ri; rng_seed(&ri, value_seed(seed, i));
+            gen_mixed(&o, &ri, &zr, 1);
+            break; }
         case 10: gen_edge(&o, &r, i); break;
         case 11: {
             uint64_t u = rnd_below(&r, 100);

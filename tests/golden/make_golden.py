@@ -343,6 +343,63 @@ def edges():
     return E
 
 
+def shapes():
+    """Values built the way the reference's own tests build them, expected flat forms written
+    by the recording writers from the construction (every zipTryEncoding decision a literal):
+
+      ziplist.c:1255-1281  createList / createIntList — the ziplists ziplist.c's self-test
+                           builds by ziplistPush (HEAD pushes included), each as a hash ziplist;
+      testredrock/test_redrock.py:76-111 (_warm_up_with_all_data_types) — the value of every
+                           data type the E2E checker warms up, in the encoding Redis gives it
+                           under the reference's config defaults (SURVEY.md §5 Config)."""
+    E = []
+    # createList: push "foo" T, "quux" T, "hello" H, "1024" T -> hello, foo, quux, 1024; "1024"
+    # passes zipTryEncoding as a 16-bit integer (ziplist.c:486-498: > INT8_MAX, <= INT16_MAX)
+    E.append(w_ziplist("ziplist_c_createList", "ziplist.c:1255-1262", 13,
+                       [S(b"hello"), S(b"foo"), S(b"quux"), I(1024, 0xC0)]))
+    # createIntList: "100" T, "128000" T, "-100" H, "4294967296" H, "non integer" T,
+    # "much much longer non integer" T -> 4294967296, -100, 100, 128000, then the two strings;
+    # widths: 2^32 > INT32_MAX -> 64-bit, -100 / 100 -> 8-bit, 128000 -> 24-bit
+    E.append(w_ziplist("ziplist_c_createIntList", "ziplist.c:1264-1281", 13,
+                       [I(4294967296, 0xE0), I(-100, 0xFE), I(100, 0xFE), I(128000, 0xF0), S(b"non integer"),
+                        S(b"much much longer non integer")]))
+    # String: "0123...1999" (6,890 bytes), RAW (longer than the 44-byte EMBSTR limit)
+    s = "".join(str(i) for i in range(2000)).encode()
+    assert len(s) == 6890
+    E.append(w_string("redrock_py_string_0_1999", "test_redrock.py:82-84,96 r.set(i, string_val)", 0, s, lru=0x00ABCD))
+    # List: lpush 0..99 -> 99, 98, ..., 0; every element an integer entry (serList renders it
+    # by sdsll2str, desList's quicklistPushTail re-encodes it as that integer)
+    E.append(w_list("redrock_py_list_lpush_100", "test_redrock.py:97-99 r.lpush(i, j)",
+                    [(str(j).encode(), j) for j in range(99, -1, -1)], lru=0x00ABCD))
+    # Set: sadd 0..999 -> past set-max-intset-entries (512, config.c:2262) the intset becomes a
+    # hash table of decimal members (any dict order; this one ascending)
+    E.append(w_ht("redrock_py_set_1000", "test_redrock.py:100-103 r.sadd(i, j), 1000 > 512 -> HT", 2,
+                  [str(j).encode() for j in range(1000)], lru=0x00ABCD))
+    # Hash: hset j -> "0123...99" (190 bytes) for 1000 fields -> HT (1000 > 512 entries, 190 > 64 bytes)
+    hv = "".join(str(i) for i in range(100)).encode()
+    assert len(hv) == 190
+    E.append(w_ht("redrock_py_hash_1000x190", "test_redrock.py:104-107 r.hset(i, j, hash_field_val)", 4,
+                  [x for j in range(1000) for x in (str(j).encode(), hv)], lru=0x00ABCD))
+    # ZSet: zadd {j: j} for 100 members -> ziplist (100 <= 128 entries): member j and score
+    # d2string(j) = "j" are both integer entries (0..12 immediate 0xF1+j, 13..99 8-bit), ascending
+    zent = []
+    for j in range(100):
+        e = I(j, 0xF1 + j) if j <= 12 else I(j, 0xFE)
+        zent += [e, e]
+    E.append(w_ziplist("redrock_py_zset_ziplist_100", "test_redrock.py:108-111 r.zadd(i, {j: j}), t_zset.c:1029-1050",
+                       12, zent))
+    # Geo: a zset ziplist of members with integral 52-bit geohash scores (d2string -> ll2string ->
+    # a 64-bit integer entry); scores in ascending order
+    E.append(w_ziplist("redrock_py_geo_zset", "test_redrock.py:112-114 r.geoadd(...): zset of geohash scores", 12,
+                       [S(b"Palermo"), I(3479099956230698, 0xE0), S(b"Catania"), I(3479447370796909, 0xE0)]))
+    # HyperLogLog: a RAW binary string (sparse encoding header "HYLL", encoding 1, cached
+    # cardinality, opcodes): NUL and high bytes in the payload
+    hll = b"HYLL" + bytes([1, 0, 0, 0]) + bytes([7, 0, 0, 0, 0, 0, 0, 0]) + bytes(
+        [0x7F, 0xFF, 0x80, 0x51, 0x7F, 0x3A, 0x84, 0x4C, 0x90, 0x7F, 0xFF, 0x7F, 0xFF, 0x5E, 0x10])
+    E.append(w_string("redrock_py_hll_raw_binary", "test_redrock.py:115-117 r.pfadd(...): RAW binary", 0, hll))
+    return E
+
+
 def check_against_pyoracle(kats, edges_):
     """Consistency report: the Python restatement must agree with every literal."""
     from oracle import pyoracle as po
@@ -363,16 +420,18 @@ def main():
     ed = edges()
     names = [e["name"] for e in ed]
     assert len(names) == len(set(names))
-    mism = check_against_pyoracle(kats, ed)
+    sh = shapes()
+    assert not set(e["name"] for e in sh) & set(names)
+    mism = check_against_pyoracle(kats, ed + sh)
     if mism:
         for m in mism:
             print("MISMATCH", *m, sep="\n  ")
         raise SystemExit(1)
-    doc = dict(generator="tests/golden/make_golden.py", kats=kats, edges=ed, string2ll=STRING2LL,
+    doc = dict(generator="tests/golden/make_golden.py", kats=kats, edges=ed, shapes=sh, string2ll=STRING2LL,
                ll2string=LL2STRING, ziplist_example=ZIPLIST_EXAMPLE, intset_encoding=INTSET_ENC)
     with open(OUT, "w") as f:
         json.dump(doc, f, indent=1)
-    print(f"wrote {OUT}: {len(kats)} KATs, {len(ed)} edge fixtures")
+    print(f"wrote {OUT}: {len(kats)} KATs, {len(ed)} edge fixtures, {len(sh)} reference-shaped values")
 
 
 if __name__ == "__main__":

@@ -36,6 +36,22 @@ def test_golden_batch(engine):
     assert bytes(out) == exp
 
 
+def test_reference_shaped_values(engine):
+    """ziplist.c:1255-1281's test lists and testredrock/test_redrock.py's value of every type
+    (a 6,890-B string, a 100-int List, a 1000-member HT Set, a 1000 x 190-B HT Hash, a 100-member
+    ziplist ZSet, a geo zset, an HLL string), each repeated so they share windows with each other
+    and with the golden fixtures: the GPU decode equals the literal flat forms (the 1000-key
+    tables go through the exact duplicate test of the fixup pass), and the encode rewrites them."""
+    fx = (G["shapes"] + G["kats"]) * 7
+    blobs = [bytes.fromhex(f["blob"]) for f in fx]
+    data, offs = batch_from_blobs(blobs)
+    v, e, a, t = engine.decode_host(data, offs)
+    assert_flat_equal((v, e), expected_flat(fx), "reference shapes")
+    assert t["n_bad"] == 0
+    out, ooffs, t2 = engine.encode_host(v, e, a)
+    assert t2["n_bad"] == 0 and bytes(out) == b"".join(blobs)
+
+
 @pytest.mark.parametrize("cfg,n", [(1, 100000), (2, 100000), (3, 50000), (4, 100000), (10, 2400), (11, 400)])
 def test_config_parity(engine, cfg, n):
     data, offs = rr.gen_batch(cfg, n)
@@ -594,3 +610,66 @@ def test_dense_single_class_windows(engine):
         assert t["n_bad"] == 0, what
         out, ooffs, t2 = engine.encode_host(v, e, a)
         assert np.array_equal(out, data[:int(offs[-1])]), what
+
+
+def test_config5_per_gpu_shard_at_full_size(engine):
+    """BASELINE config 5 — 100M values in config-4 proportions over 8 GPUs — one GPU's share
+    at its real size: the byte-balanced 8-way plan of the whole 100M batch (rr_shard_plan over
+    the sizes of all 100M values), then the LAST shard (~12.5M values, ~6.2 GB) generated on
+    its own, decoded on the device and checked bit-exact against the C oracle, encoded back on
+    the device bit-exact, and placed at its whole-batch position with rr_flat_rebase
+    (elem_base += the descriptors of the 87.5M values before it, arena offsets += its first
+    byte, ~43 GB) — equal to the oracle's decode rebased the same way."""
+    import torch
+    N, G, nt = 100_000_000, 8, min(16, cpu.nprocs())
+    nb, nd = rr.gen_sizes(5, 0, N, nthreads=nt)
+    offs = np.zeros(N + 1, np.uint64)
+    np.cumsum(nb, out=offs[1:])
+    del nb
+    plan = rr.shard_plan(offs, G)
+    v0, v1, b0, b1 = (int(x) for x in plan[G - 1])
+    elem_add = int(nd[:v0].sum(dtype=np.uint64))
+    shard_descs = int(nd[v0:v1].sum(dtype=np.uint64))
+    assert v1 == N and b1 == int(offs[N]) and 12_000_000 < v1 - v0 < 13_000_000
+    assert 40e9 < b0 < 46e9 and 1.2e9 < elem_add < 2 ** 32 - shard_descs
+    data, soffs = rr.gen_range(5, v0, v1, nthreads=nt)
+    assert np.array_equal(soffs, offs[v0:v1 + 1] - np.uint64(b0))
+    del offs
+    n, nbytes = v1 - v0, b1 - b0
+    ov, oe, _, ot = cpu.decode(data, soffs, elem_cap=shard_descs, nthreads=nt)
+    assert ot["n_bad"] == 0 and ot["n_elems"] == shard_descs and np.array_equal(ov["n_elems"], nd[v0:v1])
+    del nd
+    dev = torch.device("cuda:0")
+    d_data = torch.from_numpy(data).to(dev)
+    d_offs = torch.from_numpy(soffs.view(np.int64)).to(dev)
+    d_vals = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
+    d_elems = torch.zeros(shard_descs * 16, dtype=torch.uint8, device=dev)
+    d_arena = torch.zeros(d_data.numel(), dtype=torch.uint8, device=dev)
+    d_tot = torch.zeros(4, dtype=torch.int64, device=dev)
+    engine.reserve(n, nbytes)
+    engine.decode_device(d_data, d_offs, d_vals, d_elems, d_arena, d_tot)
+    torch.cuda.synchronize()
+    tot = d_tot.cpu().numpy().view(np.uint64)
+    assert int(tot[0]) == shard_descs and int(tot[1]) == nbytes and int(tot[2]) == 0
+    assert torch.equal(d_arena[:nbytes], d_data[:nbytes])
+    assert_flat_equal((d_vals.cpu().numpy().view(rr.VALUE_DT), d_elems.cpu().numpy().view(rr.ELEM_DT)), (ov, oe),
+                      "config 5 last shard")
+    # encode back on the device
+    d_out = torch.zeros(d_data.numel(), dtype=torch.uint8, device=dev)
+    d_ooffs = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    d_tot2 = torch.zeros(4, dtype=torch.int64, device=dev)
+    engine.encode_device(d_vals, d_elems, d_arena, d_out, d_ooffs, d_tot2)
+    torch.cuda.synchronize()
+    assert int(d_tot2[2].item()) == 0 and torch.equal(d_out[:nbytes], d_data[:nbytes])
+    assert torch.equal(d_ooffs, d_offs)
+    del d_out, d_ooffs
+    # the shard at its place in the whole 100M batch
+    engine.flat_rebase(d_vals, d_elems, elem_add, b0)
+    torch.cuda.synchronize()
+    ov["elem_base"] += np.uint32(elem_add)
+    ref = ((oe["kind"] == rr.K_STR) | (oe["kind"] == rr.K_ZLRAW)) & ((oe["data"] | oe["len"]) != 0)
+    oe["data"][ref] += np.uint64(b0)
+    gv, ge = d_vals.cpu().numpy().view(rr.VALUE_DT), d_elems.cpu().numpy().view(rr.ELEM_DT)
+    assert int(gv["elem_base"].max()) + int(gv["n_elems"][gv["elem_base"].argmax()]) == elem_add + shard_descs
+    assert int(ge["data"][ref].max()) > 40_000_000_000
+    assert_flat_equal((gv, ge), (ov, oe), "config 5 last shard rebased to its whole-batch position")

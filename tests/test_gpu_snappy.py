@@ -164,3 +164,43 @@ def test_device_entry_full_batch_roundtrip(engine):
     assert int(d_st.max().item()) == 0
     assert np.array_equal(d_boffs.cpu().numpy().view(np.uint64), cuts)
     assert torch.equal(d_back[:nb], d_data[:nb])
+
+
+# ---- the reference's own snappy test inputs (tests/snappy_reference.py) ---------------------
+import snappy_reference as sref  # noqa: E402
+
+
+def test_reference_corpus_files(engine):
+    """The files of snappy_unittest.cc's corpus table (:1239-1252), whole and as RocksDB 16 KiB
+    blocks: GPU compression bit-exact with the 1.1.8 restatement, GPU decompression of those
+    streams and of pyarrow's restores the files."""
+    import pyarrow as pa
+    c = sref.corpus()
+    whole = [c[k] for k in sref.CORPUS]
+    check_compress(engine, whole, "reference corpus")
+    parts = []
+    for x in whole:
+        cuts = blocks(x, 16384)
+        parts += [x[a:b] for a, b in zip(cuts[:-1], cuts[1:])]
+    check_compress(engine, parts, "reference corpus blocks")
+    streams = [cpu.snappy_compress(x) for x in whole + parts]
+    streams += [pa.compress(x, codec="snappy", asbytes=True) for x in whole]
+    check_decompress(engine, streams, "reference corpus streams")
+
+
+def test_reference_baddata_and_corruption(engine):
+    """baddata{1,2,3}.snappy (snappy_unittest.cc:583-597) and the corruption cases
+    (:531-580, :888-965): the GPU decompressor gives the oracle's status for every stream (a
+    rejection wherever the reference's test requires one) and the literal case's bytes."""
+    bad = list(sref.baddata().values())
+    cases = sref.corruption_cases(cpu.snappy_compress)
+    streams = bad + [s for _, s, _, _ in cases]
+    for z in bad:
+        st, ln = cpu.snappy_length(z)
+        assert st != 0 or ln < (1 << 20)
+    # (output slots as every preamble announces: the largest lie here is ~2 MB)
+    assert sum(cpu.snappy_length(s)[1] for s in streams) < (8 << 20)
+    _, _, st = check_decompress(engine, streams, "reference bad streams")
+    verdicts = [int(x) == 0 for x in st]
+    assert verdicts[:3] == [False, False, False]
+    assert verdicts[3:] == [v for _, _, v, _ in cases]

@@ -223,3 +223,54 @@ def test_decode_capacity_and_empty():
     assert t["n_bad"] > 0 and (v["status"] == 11).any()
     v, e, a, t = cpu.decode(np.zeros(16, np.uint8), np.zeros(1, np.uint64))
     assert len(v) == 0 and t["n_elems"] == 0
+
+
+@pytest.mark.parametrize("fx", G["shapes"], ids=[f["name"] for f in G["shapes"]])
+def test_reference_shaped_values(fx):
+    """ziplist.c:1255-1281's createList / createIntList and the value of every type
+    testredrock/test_redrock.py:76-117 warms up: the C oracle's decode equals the literal flat
+    form, its encode rewrites the blob, and the reference-faithful restatement (robj rebuilt,
+    serObject) accepts it and writes the same bytes (HT types: the same members)."""
+    blob = bytes.fromhex(fx["blob"])
+    data, offs = batch_from_blobs([blob])
+    v, e, a, t = cpu.decode(data, offs)
+    assert_flat_equal((v, e), expected_flat([fx]), fx["name"])
+    assert t["n_bad"] == 0
+    out, _, _ = cpu.encode(v, e, a)
+    assert bytes(out) == blob
+    fout, _, fbad, _, _ = cpu.faithful_roundtrip(data, offs)
+    assert fbad == 0
+    if blob[0] in (rr.T_SET_HT, rr.T_HASH_HT):
+        assert _members(bytes(fout)) == _members(blob)
+    else:
+        assert bytes(fout) == blob
+
+
+def test_reference_shaped_batch():
+    """All of them in one multi-threaded batch (arena offsets across values)."""
+    blobs = [bytes.fromhex(f["blob"]) for f in G["shapes"]]
+    data, offs = batch_from_blobs(blobs)
+    v, e, a, t = cpu.decode(data, offs, nthreads=4)
+    assert_flat_equal((v, e), expected_flat(G["shapes"]), "shapes batch")
+    out, _, _ = cpu.encode(v, e, a)
+    assert bytes(out) == b"".join(blobs)
+
+
+def test_config5_generator_is_seekable():
+    """Config 5 (the 100M batch of BASELINE config 5): any value range generated alone equals
+    the same range of the whole batch, sizes and descriptor counts come without the bytes and
+    agree with the C oracle's decode."""
+    d, o = rr.gen_batch(5, 12000)
+    d2, o2 = rr.gen_range(5, 0, 12000, nthreads=4)
+    assert np.array_equal(d, d2) and np.array_equal(o, o2)
+    d3, o3 = rr.gen_range(5, 5000, 9001, nthreads=3)
+    assert np.array_equal(o3, o[5000:9002] - o[5000])
+    assert np.array_equal(d3[:int(o3[-1])], d[int(o[5000]):int(o[9001])])
+    nb, nd = rr.gen_sizes(5, 0, 12000, nthreads=5)
+    assert np.array_equal(np.cumsum(nb.astype(np.int64)), o[1:].astype(np.int64))
+    v, e, a, t = cpu.decode(d, o, nthreads=4)
+    assert t["n_bad"] == 0 and np.array_equal(v["n_elems"], nd) and t["n_elems"] == int(nd.sum())
+    # config-4 proportions: 40 % strings, 15 % each collection type
+    types, counts = np.unique(d[o[:-1].astype(np.int64)], return_counts=True)
+    frac = dict(zip(types.tolist(), (counts / 12000).tolist()))
+    assert abs(frac[0] - 0.40) < 0.03 and abs(frac[14] - 0.15) < 0.02

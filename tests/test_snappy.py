@@ -1,13 +1,17 @@
 """CPU tests of the snappy block-compression oracle (oracle/rr_snappy.c).
 
 Pinning: the reference vendors snappy 1.1.8 (deps/snappy) but cannot be built or run here
-(SURVEY.md §8c).  pyarrow bundles an independent build of snappy (a later release), which
-pins the FORMAT: every stream either side writes, the other decompresses to the input, and both
-accept / reject the same hand-built and mutated streams.  The compressor's exact bytes follow
-snappy 1.1.8's CompressFragment as restated from its source (rr_snappy.c cites the lines); later
-snappy releases changed the match finder, so pyarrow's compressed bytes differ from 1.1.8's on
-some inputs and are not used as the expected bytes: compression bit-exactness against a run of
-1.1.8 itself is unpinned, and the GPU compressor is held bit-exact to the restatement.
+(SURVEY.md §8c).  Two things pin the oracle:
+  - the reference's own snappy test inputs (tests/snappy_reference.py): baddata{1,2,3}.snappy,
+    the corruption cases of snappy_unittest.cc and the corpus files of its benchmark table;
+  - pyarrow's bundled snappy (an independent, later release), which pins the FORMAT: every
+    stream either side writes, the other decompresses to the input, and both accept / reject
+    the same hand-built and mutated streams.
+The compressor's exact bytes follow snappy 1.1.8's CompressFragment as restated from its source
+(rr_snappy.c cites the lines); later snappy releases changed the match finder, so pyarrow's
+compressed bytes differ from 1.1.8's on some inputs and are not used as the expected bytes:
+compression bit-exactness against a run of 1.1.8 itself is unpinned, and the GPU compressor is
+held bit-exact to the restatement.
 """
 import numpy as np
 import pytest
@@ -129,3 +133,56 @@ def test_compressor_properties():
                 assert (pos - off) // 65536 == pos // 65536, "copy crosses a fragment"
                 pos += ln
         assert pos == len(x)
+
+
+# ---- the reference's own snappy test inputs (tests/snappy_reference.py) ---------------------
+import snappy_reference as sref  # noqa: E402
+
+
+def test_reference_fixture_checksums():
+    sref.check_sums()
+
+
+@pytest.mark.parametrize("name", sref.BADDATA)
+def test_reference_baddata_rejected_with_sane_length(name):
+    """snappy_unittest.cc:583-597: the length preamble either fails or stays under 1 MiB, and
+    the stream is rejected (by the oracle and by pyarrow's independent snappy)."""
+    z = sref.baddata()[name]
+    st, ln = cpu.snappy_length(z)
+    assert st != 0 or ln < (1 << 20)
+    st, _ = cpu.snappy_uncompress(z)
+    assert st != 0
+    with pytest.raises(Exception):
+        pa_decompress(z, ln if st == 0 or ln else 1 << 20)
+
+
+def test_reference_corruption_cases():
+    """snappy_unittest.cc:531-580 (VerifyCorrupted) and :888-965 (truncated, unterminated and
+    overflowing varints, a literal ending the buffer, zero-offset copies): the verdict each
+    test requires, from the oracle and from pyarrow."""
+    for name, stream, valid, expected in sref.corruption_cases(cpu.snappy_compress):
+        st, y = cpu.snappy_uncompress(stream)
+        assert (st == 0) == valid, (name, st)
+        if valid:
+            assert y == expected, name
+            assert pa_decompress(stream, len(expected)) == expected
+        else:
+            lst, ln = cpu.snappy_length(stream)
+            with pytest.raises(Exception):
+                pa_decompress(stream, ln if lst == 0 and ln < (1 << 24) else 1 << 20)
+
+
+@pytest.mark.parametrize("name", sref.CORPUS)
+def test_reference_corpus_roundtrip(name):
+    """The files of snappy_unittest.cc's corpus table (:1239-1252): whole-file and RocksDB
+    16 KiB block streams decompress to the input here and under pyarrow, and pyarrow's
+    streams decompress here."""
+    x = sref.corpus()[name]
+    cuts = blocks(x, 16384)
+    for part in [x] + [x[a:b] for a, b in zip(cuts[:-1], cuts[1:])]:
+        z = cpu.snappy_compress(part)
+        st, y = cpu.snappy_uncompress(z)
+        assert st == 0 and y == part
+        assert pa_decompress(z, len(part)) == part
+        st, y = cpu.snappy_uncompress(pa_compress(part))
+        assert st == 0 and y == part
