@@ -28,7 +28,8 @@ sys.path.insert(0, ROOT)
 METRIC = "GiB/s + values/s device-resident serdes, 1M mixed batch @1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 CONFIG_NAMES = {1: "100K 64-byte RAW strings", 2: "1M Zipf 16B-4KiB strings", 3: "1M hash ziplists x16 pairs",
-                4: "1M mixed String/List/Set/Hash/ZSet (config-4 proportions)"}
+                4: "1M mixed String/List/Set/Hash/ZSet (config-4 proportions)",
+                5: "config 5: shards of a 100M mixed batch (config-4 proportions), byte-balanced 8-way plan"}
 
 
 def parse():
@@ -38,6 +39,10 @@ def parse():
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--n", type=int, default=1_000_000, help="values per GPU")
     p.add_argument("--config", type=int, default=4)
+    p.add_argument("--total", type=int, default=100_000_000, help="config 5: values in the whole batch")
+    p.add_argument("--shards", type=int, default=8, help="config 5: shards of the byte-balanced plan")
+    p.add_argument("--shard-index", type=int, default=None,
+                   help="config 5: the shard this rank decodes (default: its rank; the last shard at N=1)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="budget for the CPU baseline leg")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-check", action="store_true")
@@ -66,9 +71,27 @@ def main():
     torch.cuda.set_device(dev)
 
     # ---- this rank's shard (pre-sharded: distinct seed per rank) ----
-    seed = int(rr.lib().rr_gen_default_seed(args.config)) + 7919 * rank
     t0 = time.perf_counter()
-    data, offs = rr.gen_batch(args.config, args.n, seed)
+    shard_info = None
+    if args.config == 5:
+        # BASELINE config 5: one shard of the byte-balanced plan of the whole 100M batch, generated
+        # on its own (seekable generator: sizes of all values, then the shard's bytes)
+        nt = min(16, len(os.sched_getaffinity(0)))
+        k = args.shard_index if args.shard_index is not None else (rank if world > 1 else args.shards - 1)
+        nb_all, nd_all = rr.gen_sizes(5, 0, args.total, nthreads=nt)
+        offs_all = np.zeros(args.total + 1, np.uint64)
+        np.cumsum(nb_all, out=offs_all[1:])
+        del nb_all
+        v0, v1, b0, b1 = (int(x) for x in rr.shard_plan(offs_all, args.shards)[k])
+        shard_info = {"total_values": args.total, "shards": args.shards, "shard": k, "values": [v0, v1],
+                      "bytes": [b0, b1], "whole_batch_bytes": int(offs_all[-1]),
+                      "descriptors_before": int(nd_all[:v0].sum(dtype=np.uint64)),
+                      "descriptors": int(nd_all[v0:v1].sum(dtype=np.uint64))}
+        del offs_all, nd_all
+        data, offs = rr.gen_range(5, v0, v1, nthreads=nt)
+    else:
+        seed = int(rr.lib().rr_gen_default_seed(args.config)) + 7919 * rank
+        data, offs = rr.gen_batch(args.config, args.n, seed)
     t_gen = time.perf_counter() - t0
     n = len(offs) - 1
     nb = int(offs[-1])
@@ -78,7 +101,7 @@ def main():
     eng.reserve(n, nb)
     d_data = torch.from_numpy(data).to(dev)
     d_offs = torch.from_numpy(offs.view(np.int64)).to(dev)
-    cap = rr.elem_bound(n, nb)
+    cap = rr.elem_bound(n, nb) if shard_info is None else shard_info["descriptors"]   # (config 5: the exact count)
     d_vals = torch.empty(n * 16, dtype=torch.uint8, device=dev)
     d_elems = torch.empty(cap * 16, dtype=torch.uint8, device=dev)
     d_arena = torch.empty((nb + 15) & ~15, dtype=torch.uint8, device=dev)
@@ -263,7 +286,8 @@ def main():
         "config": {"workload": f"device-resident decode, {CONFIG_NAMES.get(args.config, args.config)}",
                    "values_per_gpu": n, "blob_bytes_per_gpu": nb, "descriptors_per_gpu": n_elems,
                    "parallelism": f"shard{world} (pre-sharded, no data-path collective)",
-                   "type_histogram": {int(t): int(c) for t, c in zip(types, counts)}},
+                   "type_histogram": {int(t): int(c) for t, c in zip(types, counts)},
+                   **({"config5_shard": shard_info} if shard_info else {})},
         "values_per_s": round(vals_s, 1),
         "decode": {"gib_s": round(gib_s, 2), "values_per_s": round(vals_s, 1), "ms_per_step": round(ms_step, 4),
                    "event_ms_per_launch": round(ev_dec, 4)},

@@ -99,6 +99,9 @@ struct GlbSrc {   // global memory through a buffer descriptor: reads past its r
     }
     template <int N>
     __device__ __forceinline__ void get(uint32_t p, uint32_t (&o)[N]) const { fetch<N>(p).align(o); }
+    // the chain steps' reads: the dword / the byte at p (an aligned pair + alignbyte here)
+    __device__ __forceinline__ uint32_t u32(uint32_t p) const { uint32_t x[1]; get<1>(p, x); return x[0]; }
+    __device__ __forceinline__ uint32_t u8(uint32_t p) const { return u32(p) & 0xFF; }
 };
 struct LdsSrc {   // the workgroup's staged window; reads may run up to 64 bytes past it
     lds_cptr S;
@@ -114,6 +117,11 @@ struct LdsSrc {   // the workgroup's staged window; reads may run up to 64 bytes
     }
     template <int N>
     __device__ __forceinline__ void get(uint32_t p, uint32_t (&o)[N]) const { fetch<N>(p).align(o); }
+    // the chain steps' reads: the dword at p from the aligned pair + alignbyte.  (An unaligned
+    // ds_read_b32 — gfx950 serves it — measured slower on every walk: ZL batches 16.7K -> 22.4K
+    // cycles, cfg 4 0.353 -> 0.392 ms; the LDS splits it.)
+    __device__ __forceinline__ uint32_t u32(uint32_t p) const { uint32_t x[1]; get<1>(p, x); return x[0]; }
+    __device__ __forceinline__ uint32_t u8(uint32_t p) const { return u32(p) & 0xFF; }
 };
 
 __device__ __forceinline__ uint32_t ab(uint32_t hi, uint32_t lo, uint32_t s) { return __builtin_amdgcn_alignbyte(hi, lo, s); }
@@ -490,11 +498,10 @@ __device__ __forceinline__ bool do_list_g(const Src &R, const Lane &l, bool acti
     for (uint32_t rounds = 0;; ++rounds) {
         uint32_t mp = l.q;
         for (uint32_t j = 0; j < G; ++j) {
-            uint32_t x[1];
-            R.template get<1>(p, x);
+            const uint32_t x = R.u32(p);
             const uint32_t rem = end - p;
             mp = j == g ? p : mp;
-            p = min(p + 4 + min(x[0], rem), end);
+            p = min(p + 4 + min(x, rem), end);
         }
         // my element: integer or string (zipTryEncoding, as quicklistPushTail stores it)
         const uint32_t mk = rounds * G + g;
@@ -551,11 +558,10 @@ __device__ __forceinline__ bool do_ht_g(const Src &R, const Head &H, const Lane 
         // length does not fit is caught by its own lane below (and fails the whole value)
         uint32_t mp = l.q;
         for (uint32_t j = 0; j < G; ++j) {
-            uint32_t x[1];
-            R.template get<1>(p, x);
+            const uint32_t x = R.u32(p);
             const uint32_t rem = end - p;
             mp = j == g ? p : mp;
-            p = min(p + 8 + min(x[0], rem), end);
+            p = min(p + 8 + min(x, rem), end);
         }
         // my member (index mk): its length field's checks, the descriptor, the fingerprint
         const uint32_t mk = rounds * G + g;
@@ -629,11 +635,10 @@ __device__ __forceinline__ bool do_skiplist_g(const Src &R, const Head &H, const
     for (uint32_t rounds = 0;; ++rounds) {
         uint32_t mp = l.q;
         for (uint32_t j = 0; j < G; ++j) {
-            uint32_t x[1];
-            R.template get<1>(p, x);
+            const uint32_t x = R.u32(p);
             const uint32_t rem = end - p;
             mp = j == g ? p : mp;
-            p = min(p + 16 + min(x[0], rem), end);
+            p = min(p + 16 + min(x, rem), end);
         }
         const uint32_t mk = rounds * G + g;
         const bool mine = mk < np;
@@ -873,6 +878,103 @@ __device__ __forceinline__ bool do_ziplist_bg(const Src &R, const Lane &l, bool 
         if (__ballot((rounds + 1) * U * G < N) == 0) break;
     }
     // one verdict for the whole group
+    const uint32_t base = lane_id() - g;
+    const uint64_t gm = (G >= 64 ? ~0ull : ((1ull << G) - 1)) << base;
+    const bool gfail = (__ballot(fail) & gm) != 0;
+    const uint32_t zllen = z[2] & 0xFFFF;
+    const bool ok = !gfail && (zllen & 1) == 0 && (endbyte >> (8 * (zlast & 3)) & 0xFF) == 0xFF &&
+                    (zllen > 0 || (z[1] == 10 && first == zlast));
+    n = 1 + zllen;
+    return !ok || n != l.r;
+}
+
+// ---- Hash / ZSet ziplists, grouped and SOFTWARE-PIPELINED: do_ziplist_bg with the group
+// size a compile-time constant, so a round's G backward chain steps are straight-line code, and
+// the chain of round r + 1 (which needs only the positions) is issued in the same basic block as
+// the entry decode of round r (which needs nothing of the next chain): the decode's instructions
+// fill the chain's LDS-latency gaps instead of following them.  The last round walks one wasted
+// chain (clamped at entry 0).  Checks, stores and verdicts are do_ziplist_bg's.
+template <uint32_t G, class Src>
+__device__ __forceinline__ bool do_ziplist_bp(const Src &R, const Lane &l, bool active, uint32_t g, uint32_t &n,
+                                              uint64_t &pay) {
+    const uint32_t zl0 = l.q + 13, zend = l.q + l.L, zlast = zend - 1;   // zlast: the 0xFF byte
+    const uint32_t first = zl0 + 10;                                     // entry 0
+    uint32_t z[3];
+    R.template get<3>(zl0, z);   // zlbytes, zltail, zllen
+    const uint32_t N = active && (z[2] & 0xFFFF) != 0xFFFF ? z[2] & 0xFFFF : 0u;
+    const uint32_t endbyte = R.template fetch<1>(zlast).w[0];   // (aligned dword holding zlast)
+    put_desc(l.E, active && g == 0 ? l.slot(0) : NOSLOT, l.B + zl0, l.L - 13, RR_K_ZLRAW, 0);
+    pay += active && g == 0 ? l.L - 13 : 0;
+    bool fail = active && (z[2] & 0xFFFF) == 0xFFFF;   // saturated count: the exact parser walks it
+    uint32_t p = zl0 + z[1];
+    p = p < first ? first : p > zlast ? zlast : p;
+    uint32_t expect = zlast;   // where the entry at p must end
+    // one round's chain: G backward steps; this lane keeps step g's entry (mp) and its end (me)
+    auto chain = [&](uint32_t &mp, uint32_t &me) __attribute__((always_inline)) {
+#ifdef RR_ASM_MARK
+        asm volatile("; ZLCHAIN_BEGIN" ::: "memory");
+#endif
+        mp = first;
+        me = zlast;
+#pragma unroll
+        for (uint32_t j = 0; j < G; ++j) {
+            uint32_t x[2];
+            R.template get<2>(p, x);   // prevlen: 1 byte, or 0xFE + u32
+            const uint32_t b0 = x[0] & 0xFF;
+            const uint32_t pl = b0 >= 254 ? ab(x[1], x[0], 1) : b0;
+            const uint32_t pn = p - min(pl, p - first);
+            mp = j == g ? p : mp;
+            me = j == g ? expect : me;
+            expect = p;
+            p = pn;
+        }
+#ifdef RR_ASM_MARK
+        asm volatile("; ZLCHAIN_END" ::: "memory");
+#endif
+    };
+    // the entry decode and checks of do_ziplist_bg (index idx = N-1-mk)
+    auto decode = [&](uint32_t mk, uint32_t mp, uint32_t me) __attribute__((always_inline)) {
+        const bool mine = mk < N;
+        const uint32_t idx = N - 1 - mk;
+        uint32_t b[4];
+        R.template get<4>(mp, b);
+        const uint32_t b0 = b[0] & 0xFF;
+        const bool big = b0 >= 254;
+        const uint32_t pl = big ? ab(b[1], b[0], 1) : b0;
+        const uint32_t qp = mp + (big ? 5u : 1u);
+        const uint32_t e = big ? (b[1] >> 8) & 0xFF : (b[0] >> 8) & 0xFF;
+        const uint32_t x1 = big ? (b[1] >> 16) & 0xFF : (b[0] >> 16) & 0xFF;
+        const uint32_t lo = big ? ab(b[2], b[1], 2) : ab(b[1], b[0], 2);
+        const uint32_t hi = big ? ab(b[3], b[2], 2) : ab(b[2], b[1], 2);
+        const bool zstr = e < 0xC0;
+        const uint32_t scls = e >> 6;
+        const uint32_t ls = 1 + scls + 2 * (scls >> 1);
+        const uint32_t sl1 = scls == 0 ? (e & 0x3F) : (((e & 0x3F) << 8) | x1);
+        const uint32_t sl = scls >= 2 ? __builtin_bswap32(lo) : sl1;
+        const bool imm = e - 0xF1u <= 0xFDu - 0xF1u;
+        const uint32_t isz = (e & 0x0F) == 0 && e >= 0xC0 ? (0x3842u >> (4 * ((e >> 4) & 3))) & 0xF
+                                                           : (uint32_t)(e == 0xFE);
+        const uint64_t endp = (uint64_t)qp + (zstr ? ls + sl : 1 + isz);
+        const bool bad = (mp < first) | (mp >= zlast) | (b0 == 0xFF) | (big & (mp + 5 > zlast)) | (qp >= zlast) |
+                         (idx + 1 >= l.r) | (!zstr & !imm & (isz == 0)) | (zstr & (qp + ls > zlast)) |
+                         (endp != (uint64_t)me) | (idx == 0 ? ((mp != first) | (pl != 0)) : (pl > mp - first));
+        fail |= mine & bad;
+        const uint32_t sh = (32 - 8 * isz) & 31;
+        const int64_t v32 = (int32_t)(lo << sh) >> sh;
+        const int64_t iv = isz == 8 ? (int64_t)((uint64_t)lo | ((uint64_t)hi << 32)) : imm ? (int64_t)(e & 0x0F) - 1 : v32;
+        put_desc(l.E, (mine & !bad) ? l.slot(idx + 1) : NOSLOT, zstr ? l.B + qp + ls : (uint64_t)iv, zstr ? sl : 0,
+                 zstr ? RR_K_STR : RR_K_INT, zstr ? (e & 0xC0) : e);
+    };
+    uint32_t mpA, meA;
+    chain(mpA, meA);
+    for (uint32_t rounds = 0;; ++rounds) {
+        uint32_t mpB, meB;
+        chain(mpB, meB);   // round + 1's chain ...
+        decode(rounds * G + g, mpA, meA);   // ... beside round's decode
+        if (__ballot((rounds + 1) * G < N) == 0) break;
+        mpA = mpB;
+        meA = meB;
+    }
     const uint32_t base = lane_id() - g;
     const uint64_t gm = (G >= 64 ? ~0ull : ((1ull << G) - 1)) << base;
     const bool gfail = (__ballot(fail) & gm) != 0;

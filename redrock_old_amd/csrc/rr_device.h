@@ -142,14 +142,26 @@ constexpr uint64_t GRP_VAL = GRP_ONE - 1;
 // A wait that never ends (a tile that never publishes: a hardware or scheduling fault) is cut
 // after 2^24 sleeps: the call's error word *err is set and the prefix returned is 0 — the host
 // sees rr_totals.bytes == UINT64_MAX (rr_serdes.h) instead of silently wrong offsets.
+// The look-back in two halves, so a tile can publish its aggregate as soon as it knows it and
+// resolve its prefix later (other work in between): lb_publish by one wave, lb_resolve by one
+// whole wave (it also publishes the inclusive prefix).
+__device__ __forceinline__ void lb_publish(uint64_t *state, uint64_t *groups, uint32_t tile, uint64_t agg) {
+    if (lane_id() == 0) {
+        lb_store(&state[tile], (tile == 0 ? LB_INC : LB_AGG) | agg);
+        atomicAdd((unsigned long long *)&groups[tile / LB_GROUP], (unsigned long long)(GRP_ONE | agg));
+    }
+}
+__device__ __forceinline__ uint64_t lb_resolve(uint64_t *state, uint64_t *groups, uint32_t tile, uint32_t ntiles,
+                                               uint64_t agg, uint64_t *err);
 __device__ __forceinline__ uint64_t lookback(uint64_t *state, uint64_t *groups, uint32_t tile, uint32_t ntiles,
                                              uint64_t agg, uint64_t *err) {
+    lb_publish(state, groups, tile, agg);
+    return lb_resolve(state, groups, tile, ntiles, agg, err);
+}
+__device__ __forceinline__ uint64_t lb_resolve(uint64_t *state, uint64_t *groups, uint32_t tile, uint32_t ntiles,
+                                               uint64_t agg, uint64_t *err) {
     const uint32_t lane = lane_id();
     const uint32_t g = tile / LB_GROUP, p = tile % LB_GROUP;
-    if (lane == 0) {
-        lb_store(&state[tile], (tile == 0 ? LB_INC : LB_AGG) | agg);
-        atomicAdd((unsigned long long *)&groups[g], (unsigned long long)(GRP_ONE | agg));
-    }
     if (tile == 0) return 0;
     uint64_t excl = 0;
     uint32_t spins = 0;

@@ -685,13 +685,13 @@ __device__ __forceinline__ void queue_fixup(uint64_t *fix, uint64_t v) {
     reinterpret_cast<uint32_t *>(fix + FIX_HDR)[i] = (uint32_t)v;
 }
 
+// (eb, r: the value's first descriptor slot and its reservation)
 __device__ RR_COLD Acc exact_value(const uint8_t *__restrict__ blob, uint64_t v,
-                                           const uint64_t *__restrict__ offsets, const uint64_t *__restrict__ ebase,
+                                           const uint64_t *__restrict__ offsets, uint64_t eb, uint64_t r,
                                            rr_value *__restrict__ values, rr_elem *__restrict__ elems, uint64_t cap,
                                            uint64_t *fix) {
     uint64_t pay = 0;
     const uint64_t o_lo = offsets[v], o_hi = offsets[v + 1];
-    const uint64_t eb = ebase[v], r = ebase[v + 1] - eb;
     const uint8_t *b = blob + o_lo;
     Parsed pr = parse_value<false, const uint8_t *>(b, o_lo, o_hi - o_lo, nullptr);
     uint32_t status = pr.status;
@@ -725,6 +725,9 @@ __device__ RR_COLD Acc exact_value(const uint8_t *__restrict__ blob, uint64_t v,
 #ifndef RR_ZL_VPB
 #define RR_ZL_VPB 16
 #endif
+#ifndef RR_ZL_PIPE   // 1: ziplist batches run do_ziplist_bp (compile-time group size, pipelined rounds)
+#define RR_ZL_PIPE 1
+#endif
 #if RR_ZL_BACK
 constexpr uint32_t ZL_VPB = RR_ZL_VPB;
 #endif
@@ -757,11 +760,12 @@ __constant__ uint32_t CLASS_ORDER[C_N] = {RR_DEC_ORDER};
 // G lanes per value (grouped walks, rr_decode_class.h), this lane being lane g of its group;
 // the group's lane 0 records the value (or runs the exact parser), every lane returns the
 // payload of the elements it stored.
+// (eb_v, r_v: value v's first descriptor slot and its reservation, for active lanes)
 template <class Src>
 __device__ __forceinline__ Acc run_batch(const Src &src, uint32_t c, bool active, uint64_t v, uint32_t G, uint32_t g,
                                          uint64_t B, rsrc_t E,
                                          uint64_t eb0, const uint8_t *__restrict__ blob,
-                                         const uint64_t *__restrict__ offsets, const uint64_t *__restrict__ ebase,
+                                         const uint64_t *__restrict__ offsets, uint64_t eb_v, uint64_t r_v,
                                          rr_value *__restrict__ values, rr_elem *__restrict__ elems, uint64_t cap,
                                          uint64_t *fix) {
     // (one exact_value call site: the parser is large and every inlined copy costs I-cache)
@@ -774,8 +778,8 @@ __device__ __forceinline__ Acc run_batch(const Src &src, uint32_t c, bool active
         l.E = E;
         if (active) {
             const uint64_t o = offsets[v], o1 = offsets[v + 1];
-            eb = ebase[v];
-            r = ebase[v + 1] - eb;
+            eb = eb_v;
+            r = r_v;
             l.q = (uint32_t)(o - B);
             l.L = (uint32_t)(o1 - o);
             l.so = (uint32_t)(eb - eb0) * 16;
@@ -802,7 +806,11 @@ __device__ __forceinline__ Acc run_batch(const Src &src, uint32_t c, bool active
         } else if (c == C_SL) {
             fail = do_skiplist_g(src, H, l, active, G, g, ne, vp);
         } else {
-#if RR_ZL_BACK   // C_ZL: grouped, one backward prevlen chain per value
+#if RR_ZL_BACK && RR_ZL_PIPE   // C_ZL: grouped, software-pipelined (G a power of two >= 4)
+            if (G >= 16) fail = do_ziplist_bp<16>(src, l, active, g, ne, vp);
+            else if (G >= 8) fail = do_ziplist_bp<8>(src, l, active, g, ne, vp);
+            else fail = do_ziplist_bp<4>(src, l, active, g, ne, vp);
+#elif RR_ZL_BACK   // C_ZL: grouped, one backward prevlen chain per value
             fail = do_ziplist_bg(src, l, active, G, g, ne, vp);
 #else            // C_ZL: G == 2, lane 1 of the pair walks backward
             fail = do_ziplist(src, l, active, g != 0, ne, vp);
@@ -819,7 +827,7 @@ __device__ __forceinline__ Acc run_batch(const Src &src, uint32_t c, bool active
         }
         active &= g == 0;   // the exact parser runs once per value, on the group's lane 0
     }
-    if (active && exact) acc = exact_value(blob, v, offsets, ebase, values, elems, cap, fix);
+    if (active && exact) acc = exact_value(blob, v, offsets, eb_v, r_v, values, elems, cap, fix);
     return acc;
 }
 
@@ -827,10 +835,10 @@ __device__ __forceinline__ Acc run_batch(const Src &src, uint32_t c, bool active
 // builds so the hot staged code stays small
 __device__ RR_COLD Acc run_batch_g(const GlbSrc &src, uint32_t c, bool active, uint64_t v, uint32_t G, uint32_t g,
                                    uint64_t B, rsrc_t E, uint64_t eb0, const uint8_t *__restrict__ blob,
-                                   const uint64_t *__restrict__ offsets, const uint64_t *__restrict__ ebase,
+                                   const uint64_t *__restrict__ offsets, uint64_t eb_v, uint64_t r_v,
                                    rr_value *__restrict__ values, rr_elem *__restrict__ elems, uint64_t cap,
                                    uint64_t *fix) {
-    return run_batch(src, c, active, v, G, g, B, E, eb0, blob, offsets, ebase, values, elems, cap, fix);
+    return run_batch(src, c, active, v, G, g, B, E, eb0, blob, offsets, eb_v, r_v, values, elems, cap, fix);
 }
 
 // Workgroup per byte WINDOW of W bytes: window t owns the values whose first byte lies in
@@ -1341,17 +1349,20 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
 #endif
             // (hash tables: a power of two, so a value's lanes lie in one DPP row, do_ht_g)
             const uint32_t Gh = 1u << (31 - __builtin_clz(Gw));
-            const uint32_t G = __builtin_amdgcn_readfirstlane((c == C_ZL && !RR_ZL_BACK) ? 2u : grouped ? Gw : htg ? Gh : 1u);
+            const bool pow2 = htg || (RR_ZL_PIPE && c == C_ZL);   // (a ziplist batch's G: 4, 8 or 16)
+            const uint32_t G = __builtin_amdgcn_readfirstlane((c == C_ZL && !RR_ZL_BACK) ? 2u : pow2 ? Gh : grouped ? Gw : 1u);
             const uint32_t li = lane / G, g = lane - li * G;   // the value's index in the batch
             const bool active = li < cnt;
             const uint64_t v = c0 + (active ? perm[first + li] : 0u);
+            uint64_t eb_v = eb0, r_v = 0;
+            if (active) { eb_v = ebase[v]; r_v = ebase[v + 1] - eb_v; }
 #ifndef RR_DEC_NOGLOBAL
-            const Acc a = staged ? run_batch(lsrc, c, active, v, G, g, S0, E, eb0, blob, offsets, ebase, values, elems,
+            const Acc a = staged ? run_batch(lsrc, c, active, v, G, g, S0, E, eb0, blob, offsets, eb_v, r_v, values, elems,
                                              cap, fix)
-                                 : run_batch_g(gsrc, c, active, v, G, g, S0, E, eb0, blob, offsets, ebase, values,
+                                 : run_batch_g(gsrc, c, active, v, G, g, S0, E, eb0, blob, offsets, eb_v, r_v, values,
                                                elems, cap, fix);
 #else   // timing-only builds (tools/): no unstaged walks (wrong for windows that overflow the stage)
-            const Acc a = run_batch(lsrc, c, active, v, G, g, S0, E, eb0, blob, offsets, ebase, values, elems, cap, fix);
+            const Acc a = run_batch(lsrc, c, active, v, G, g, S0, E, eb0, blob, offsets, eb_v, r_v, values, elems, cap, fix);
             (void)gsrc;
 #endif
 #if RR_DEC_PRIO
@@ -1443,6 +1454,381 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
               prb[29] = staged; if (g_probe) for (uint32_t i = 0; i < PROBE_WORDS; ++i) g_probe[(uint64_t)tile * PROBE_WORDS + i] = prb[i];)
     }
     }   // window
+}
+
+// ---- fused decode: one pass over the windows -------------------------------------------
+// decode_fused_kernel replaces count_kernel + scan_kernel + decode_kernel: a window classifies
+// and reserves its own values from its LDS stage (pass A, thread per value; a List walks its
+// length chain in LDS), publishes the window's descriptor total right away, sorts its values by
+// class and lays out their window-relative slot offsets while the earlier windows' totals come
+// in, then resolves its first slot by a decoupled look-back over the windows (rr_device.h) and
+// walks + emits the single-class batches as decode_kernel does.  No value header is read from
+// global memory twice.  dec_index_kernel before it only reads the offsets (the first value of
+// every window) and zeroes the call's words.
+
+// reserve_classify over a byte source (the LDS stage, or global memory through a buffer
+// resource for a window whose values overflow the stage): same results, byte for byte
+__device__ __forceinline__ uint64_t rfl64(uint64_t x) {   // a wave-uniform 64-bit value into SGPRs
+    return (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)x) |
+           ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)) << 32);
+}
+
+template <class Src>
+__device__ __forceinline__ void classify_reserve_src(const Src &S, uint32_t q, uint64_t L, const uint8_t *b_glb,
+                                                     uint32_t &c, uint64_t &r) {
+    r = 0;
+    c = C_EXACT;
+    if (L < 5) return;
+    uint32_t d[6];
+    S.template get<6>(q, d);
+    const uint32_t t = d[0] & 0xFF;
+    const uint32_t f5 = __builtin_amdgcn_alignbyte(d[2], d[1], 1), f9 = __builtin_amdgcn_alignbyte(d[3], d[2], 1);
+    const uint32_t f13 = __builtin_amdgcn_alignbyte(d[4], d[3], 1);
+    const uint64_t u5 = (uint64_t)f5 | ((uint64_t)f9 << 32);
+    switch (t) {
+        case RR_TYPE_STRING: {
+            if (L < 6) return;
+            r = 1;
+            const uint32_t enc = (d[1] >> 8) & 0xFF;
+            const uint64_t rest = L - 6;
+            if (enc == RR_ENC_INT) c = rest == 8 ? C_STR : C_EXACT;
+            else if (enc == RR_ENC_EMBSTR) c = rest <= RR_EMBSTR_SIZE_LIMIT ? C_STR : C_EXACT;
+            else if (enc == RR_ENC_RAW) c = rest <= 0xFFFFFFFFull ? C_STR : C_EXACT;
+            return;
+        }
+        case RR_TYPE_LIST_QUICKLIST: {   // the length chain (the count the walk will take)
+            c = C_LIST;
+            uint64_t p = 5, n = 0;
+            while (p < L) {
+                if (L - p < 4) break;
+                uint32_t x[1];
+                S.template get<1>(q + (uint32_t)p, x);
+                const uint64_t l = x[0];
+                if (l > L - p - 4) break;
+                ++n;
+                p += 4 + l;
+            }
+            r = n;
+            return;
+        }
+        default:
+            break;
+    }
+    if (L < 13) return;
+    switch (t) {
+        case RR_TYPE_SET_INTSET: {
+            const uint64_t w = f5, cnt = f9;
+            const bool ok = (w == 2 || w == 4 || w == 8) && L - 13 == w * cnt;
+            r = ok ? cnt : 0;
+            c = ok ? C_IS : C_EXACT;
+            return;
+        }
+        case RR_TYPE_SET_HT: { const uint64_t m = (L - 13) / 8; r = u5 < m ? u5 : m; c = C_HT; return; }
+        case RR_TYPE_HASH_HT: { const uint64_t m = (L - 13) / 8; r = u5 > m / 2 ? m : 2 * u5; c = C_HH; return; }
+        case RR_TYPE_ZSET_SKIPLIST: { const uint64_t m = (L - 13) / 16; r = 2 * (u5 < m ? u5 : m); c = C_SL; return; }
+        case RR_TYPE_HASH_ZIPLIST:
+        case RR_TYPE_ZSET_ZIPLIST: {
+            const uint64_t Lz = u5;
+            c = (L >= 24 && Lz == L - 13 && f13 == Lz) ? C_ZL : C_EXACT;
+            if (Lz != L - 13 || Lz < 11) return;
+            const uint64_t zllen = (d[5] >> 8) & 0xFFFF;
+            if (zllen != 0xFFFF) { const uint64_t m = (Lz - 11) / 2; r = 1 + (zllen < m ? zllen : m); return; }
+            r = 1 + zl_walk_count_g(b_glb + 13, Lz);   // (a saturated count: rare, from global memory)
+            return;
+        }
+        default:
+            return;
+    }
+}
+
+// zeroes the call's words (window look-back state, fixup header, totals) and finds the first
+// value of every window from the offsets alone
+__global__ __launch_bounds__(256) void dec_index_kernel(const uint64_t *__restrict__ offsets, uint64_t n,
+                                                        uint32_t *__restrict__ first_val, uint32_t nwin, uint32_t win,
+                                                        uint64_t *zero_words, uint32_t nzero, rr_totals *tot) {
+    zero_call_words(zero_words, nzero, tot);
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i > n) return;
+    const uint64_t o_hi = offsets[i];
+    const uint64_t w_lo = i == 0 ? 0 : offsets[i - 1] / win + 1;
+    const uint64_t w_hi = i == n ? nwin : o_hi / win;
+    for (uint64_t w = w_lo; w <= w_hi && w <= nwin; ++w) first_val[w] = (uint32_t)i;
+}
+
+template <uint32_t W, uint32_t SLACK, uint32_t NW, uint32_t PMAX>
+__global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_fused_kernel(
+    const uint8_t *__restrict__ blob, uint64_t data_cap, const uint64_t *__restrict__ offsets, uint64_t n,
+    const uint32_t *__restrict__ first_val, uint8_t *__restrict__ cls, uint32_t *__restrict__ cnt,
+    rr_value *__restrict__ values, rr_elem *__restrict__ elems, uint64_t elem_cap, uint8_t *__restrict__ arena,
+    uint64_t *__restrict__ stats, uint64_t *fix, uint32_t nwin, uint64_t *lb_state, uint64_t *lb_groups,
+    uint64_t *total) {
+    constexpr uint32_t NT = NW * RR_WAVE, STAGE = W + SLACK;
+    // a chunk of values is one pass-A round: thread i holds value i of every chunk, so the class
+    // and reservation it wrote for a later chunk are its own writes when it reads them back
+    static_assert(PMAX == NT && W % 16 == 0 && SLACK % 16 == 0, "tile shape");
+    __shared__ __attribute__((aligned(16))) uint8_t stage[STAGE + 64];
+    __shared__ uint16_t perm[PMAX];
+    __shared__ uint32_t eloc[PMAX + 1];   // window-relative first slot of the chunk's values
+    __shared__ uint32_t ccount[C_N], cbase[C_N], ccur[C_N], bpre[C_N + 1];
+    __shared__ uint32_t next_batch;
+    __shared__ uint64_t red[2][NW];
+    __shared__ uint64_t sh_eb0;
+    PROBE(__shared__ uint64_t prb[PROBE_WORDS]; uint64_t pt0 = __builtin_amdgcn_s_memtime(), pt1 = 0, pt2 = 0;
+          if (threadIdx.x < PROBE_WORDS) prb[threadIdx.x] = 0;)
+    const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid / RR_WAVE;
+    const uint32_t tile = blockIdx.x;
+    const uint64_t padded = (offsets[n] + 15) & ~15ull;
+    const uint64_t W0 = (uint64_t)tile * W;
+    const uint64_t W1 = W0 + W < padded ? W0 + W : padded;
+    const uint64_t A0 = W0 > (offsets[0] & ~15ull) ? W0 : (offsets[0] & ~15ull);
+    // 1. the window's loads (as decode_kernel: buffer resources, no exec-mask branches)
+    constexpr uint32_t KM = W / 16 / NT;
+    static_assert(W % (16 * NT) == 0, "window granules per thread");
+    const uint64_t ov_a = A0 >> 4, ov_w1 = W1 >> 4;
+    const uint32_t ov_mb = ov_w1 > ov_a ? (uint32_t)((ov_w1 - ov_a) * 16) : 0u;
+    const rsrc_t ov_RM = make_rsrc(blob + A0, ov_mb);
+    const rsrc_t ov_RA = make_rsrc(arena + A0, ov_mb);
+    u32x4 ov_m[KM];
+#pragma unroll
+    for (uint32_t k = 0; k < KM; ++k)
+        ov_m[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ov_RM, (int)((tid + k * NT) * 16), 0, 0));
+    const uint64_t v_lo = first_val[tile], v_hi = first_val[tile + 1];
+    uint64_t S0 = W0, S1 = W0;
+    if (v_hi > v_lo) {
+        S0 = offsets[v_lo] & ~15ull;
+        S1 = (offsets[v_hi] + 15) & ~15ull;
+    }
+    const bool staged = S1 - S0 <= STAGE;
+    const uint64_t cap = elem_cap < 0xFFFFFFFFull ? elem_cap : 0xFFFFFFFFull;   // elem_base is 32-bit
+    constexpr uint32_t KT = (SLACK / 16 + NT - 1) / NT;
+    const uint64_t ov_t0 = ov_w1 > ov_a ? ov_w1 : ov_a;
+    const uint64_t ov_te = (staged && S1 > W1 ? S1 : W1) >> 4;
+    const rsrc_t ov_RT = make_rsrc(blob + ov_t0 * 16, ov_te > ov_t0 ? (uint32_t)((ov_te - ov_t0) * 16) : 0u);
+    u32x4 ov_t[KT];
+#pragma unroll
+    for (uint32_t k = 0; k < KT; ++k)
+        ov_t[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ov_RT, (int)((tid + k * NT) * 16), 0, 0));
+    // the window's first values' offsets, loaded while the window lands
+    const uint64_t v0 = v_lo + tid;
+    uint64_t o0 = 0, o1 = 0;
+    if (v0 < v_hi) { o0 = offsets[v0]; o1 = offsets[v0 + 1]; }
+    // 2. window -> arena (nontemporal), value bytes -> the LDS stage
+    {
+        const uint64_t ov_s0 = S0 >> 4;
+        typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
+        lds_u32x4 *ov_lds = (lds_u32x4 *)(__attribute__((address_space(3))) uint8_t *)stage;
+        auto ov_slot = [&](uint64_t g) __attribute__((always_inline)) -> uint32_t {
+            return (staged & (g >= ov_s0) & (g < ov_te)) ? (uint32_t)(g - ov_s0) : STAGE / 16;
+        };
+#pragma unroll
+        for (uint32_t k = 0; k < KM; ++k) {
+            __builtin_amdgcn_raw_buffer_store_b128(ov_m[k], ov_RA, (int)((tid + k * NT) * 16), 0, 2 /* nt */);
+            ov_lds[ov_slot(ov_a + tid + (uint64_t)k * NT)] = ov_m[k];
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < KT; ++k) ov_lds[ov_slot(ov_t0 + tid + (uint64_t)k * NT)] = ov_t[k];
+    }
+    const bool far = !staged && S1 - S0 > 0xFFFFFF00ull;
+    const LdsSrc lsrc{(lds_cptr)stage};
+    const GlbSrc gsrc{make_rsrc(blob + S0, (uint32_t)(data_cap - S0 < 0xFFFFFFFFull ? data_cap - S0 : 0xFFFFFFFFull))};
+    DEC_SYNC();   // the stage is complete
+    PROBE(pt1 = __builtin_amdgcn_s_memtime();)
+
+    // 3. pass A: class and reservation of every value of the window (thread per value); the
+    //    first chunk's stay in registers, later chunks' go to cls / cnt for the same thread
+    uint32_t c_first = C_N;
+    uint64_t r_first = 0, agg = 0;
+    for (uint64_t r0 = v_lo; r0 < v_hi; r0 += NT) {
+        const uint64_t v = r0 + tid;
+        uint32_t c = C_N;
+        uint64_t r = 0;
+        if (v < v_hi) {
+            const uint64_t o = r0 == v_lo ? o0 : offsets[v], o_end = r0 == v_lo ? o1 : offsets[v + 1];
+            const uint64_t L = o_end - o;
+            if (far) {
+                c = C_EXACT;
+                r = reserve_g(blob + o, L);
+            } else if (staged) {
+                classify_reserve_src(lsrc, (uint32_t)(o - S0), L, blob + o, c, r);
+            } else {
+                classify_reserve_src(gsrc, (uint32_t)(o - S0), L, blob + o, c, r);
+            }
+            r = r < 0xFFFFFFFFull ? r : 0xFFFFFFFFull;
+            if (r0 == v_lo) { c_first = c; r_first = r; }
+        }
+        agg += r;
+    }
+    // (a later chunk classifies its values again in step 4: a class written to global memory
+    // here and read back there could come from a stale line of the CU's L1, which the other
+    // workgroup on the CU may have filled; only multi-chunk windows pay this)
+    (void)cls; (void)cnt;
+    agg = wave_sum(agg);
+    if (lane == 0) red[0][wave] = agg;
+    DEC_SYNC();
+    agg = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < NW; ++w) agg += red[0][w];
+    agg = rfl64(agg);
+#ifdef RR_FUSED_NOLB   // timing-only builds (tools/): no look-back (every window's first slot is 0: wrong)
+    const bool nolb = true;
+#else
+    const bool nolb = false;
+#endif
+    if (wave == 0 && !nolb) lb_publish(lb_state, lb_groups, tile, agg);   // the window's total, as early as possible
+    // a window whose descriptor byte offsets overflow the 32-bit slot resource: exact parser
+    const bool far2 = far || agg * 16 >= NOSLOT;
+    PROBE(pt2 = __builtin_amdgcn_s_memtime();)
+
+    uint64_t bad = 0, pay = 0;
+    bool have_eb0 = false;
+    uint64_t eb0 = 0;
+    uint32_t run = 0;   // window-relative slots of the earlier chunks
+    for (uint64_t c0 = v_lo; c0 < v_hi; c0 += PMAX) {
+        const uint32_t nv = (uint32_t)(v_hi - c0 < PMAX ? v_hi - c0 : PMAX);
+        if (tid < C_N) { ccount[tid] = 0; ccur[tid] = 0; }
+        if (tid == 0) next_batch = 0;
+        DEC_SYNC();   // (also: every wave is done with the previous chunk's batches)
+        // 4. counting sort of the chunk by class + its window-relative slot offsets
+        const uint64_t v = c0 + tid;
+        const bool in = tid < nv;
+        uint32_t myc = C_N, myr = 0;
+        if (in) {
+            if (c0 == v_lo) { myc = c_first; myr = (uint32_t)r_first; }
+            else {
+                const uint64_t o = offsets[v], L = offsets[v + 1] - o;
+                uint64_t r = 0;
+                if (far) { myc = C_EXACT; r = reserve_g(blob + o, L); }
+                else if (staged) classify_reserve_src(lsrc, (uint32_t)(o - S0), L, blob + o, myc, r);
+                else classify_reserve_src(gsrc, (uint32_t)(o - S0), L, blob + o, myc, r);
+                myr = (uint32_t)(r < 0xFFFFFFFFull ? r : 0xFFFFFFFFull);
+            }
+            myc = far2 ? C_EXACT : myc;
+        }
+        if (wave * RR_WAVE < nv) {
+#pragma unroll
+            for (uint32_t c = 0; c < C_N; ++c) {
+                const uint64_t m = __ballot(myc == c);
+                if (m && lane == 0) atomicAdd(&ccount[c], (uint32_t)__popcll(m));
+            }
+        }
+        const uint64_t incl = wave_incl_scan((uint64_t)myr);
+        if (lane == RR_WAVE - 1) red[1][wave] = incl;
+        DEC_SYNC();
+        uint64_t wpre = 0, ctot = 0;
+#pragma unroll
+        for (uint32_t w = 0; w < NW; ++w) {
+            const uint64_t x = red[1][w];
+            wpre += w < wave ? x : 0;
+            ctot += x;
+        }
+        ctot = rfl64(ctot);
+        if (in) eloc[tid] = run + (uint32_t)(wpre + incl - myr);
+        if (tid == 0) {
+            eloc[nv] = run + (uint32_t)ctot;
+            uint32_t s = 0, bs = 0;
+            for (uint32_t k = 0; k < C_N; ++k) {
+                const uint32_t c = CLASS_ORDER[k];
+                const uint32_t vpb = class_vpb(c);
+                cbase[c] = s;
+                bpre[k] = bs;
+                s += ccount[c];
+                bs += (ccount[c] + vpb - 1) / vpb;
+            }
+            bpre[C_N] = bs;
+        }
+        run += (uint32_t)ctot;
+        DEC_SYNC();
+        if (wave * RR_WAVE < nv) {
+#pragma unroll
+            for (uint32_t c = 0; c < C_N; ++c) {
+                const uint64_t m = __ballot(myc == c);
+                if (m) {
+                    uint32_t at = 0;
+                    if (lane == 0) at = atomicAdd(&ccur[c], (uint32_t)__popcll(m));
+                    at = __shfl(at, 0, RR_WAVE);
+                    if (myc == c) perm[cbase[c] + at + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = (uint16_t)tid;
+                }
+            }
+        }
+        // 5. the window's first slot: the look-back over the earlier windows' totals (resolved
+        //    once, by wave 0, after the first chunk's sort — their totals had time to arrive)
+        if (!have_eb0) {
+            if (nolb) { if (tid == 0) sh_eb0 = 0; }
+            else if (wave == 0) {
+                const uint64_t pre = lb_resolve(lb_state, lb_groups, tile, nwin, agg, fix + 1);
+                if (lane == 0) {
+                    sh_eb0 = pre;
+                    if (tile == nwin - 1) *total = pre + agg;
+                }
+            }
+            have_eb0 = true;
+        }
+        DEC_SYNC();   // the chunk's sort, its slot offsets and the window's first slot are complete
+        eb0 = rfl64(sh_eb0);
+        // the window's descriptor slots [eb0, eb0 + agg), cut at the capacity
+        const uint64_t eb1 = eb0 + agg;
+        const uint64_t ecut = eb1 < cap ? eb1 : cap;
+        const rsrc_t E = make_rsrc(reinterpret_cast<const uint8_t *>(elems + eb0),
+                                   far2 || ecut <= eb0 ? 0u : (uint32_t)((ecut - eb0) * 16));
+        // 6. single-class batches, taken dynamically by the waves
+        const uint32_t nb = __builtin_amdgcn_readfirstlane(bpre[C_N]);
+        for (;;) {
+            uint32_t bi = 0;
+            if (lane == 0) bi = atomicAdd(&next_batch, 1u);
+            bi = __builtin_amdgcn_readfirstlane(__shfl(bi, 0, RR_WAVE));
+            if (bi >= nb) break;
+            uint32_t k = 0;
+            while (bi >= bpre[k + 1]) ++k;
+            const uint32_t c = CLASS_ORDER[k];
+            const uint32_t vpb = class_vpb(c);
+            const uint32_t first = cbase[c] + (bi - bpre[k]) * vpb;
+            const uint32_t bcnt = min(ccount[c] - (bi - bpre[k]) * vpb, vpb);
+            PROBE(const uint64_t tb0 = __builtin_amdgcn_s_memtime();)
+            const bool grouped = c == C_LIST || c == C_SL || c == C_IS || (RR_ZL_BACK && c == C_ZL);
+            const uint32_t Gw = max(1u, min(GMAX, (uint32_t)RR_WAVE / bcnt));
+#if RR_HT_GROUPED
+            const bool htg = (c == C_HT || c == C_HH) && Gw >= ht_group_min(c == C_HH);
+#else
+            const bool htg = false;
+#endif
+            const uint32_t Gh = 1u << (31 - __builtin_clz(Gw));
+            const bool pow2 = htg || (RR_ZL_PIPE && c == C_ZL);   // (a ziplist batch's G: 4, 8 or 16)
+            const uint32_t G = __builtin_amdgcn_readfirstlane((c == C_ZL && !RR_ZL_BACK) ? 2u : pow2 ? Gh : grouped ? Gw : 1u);
+            const uint32_t li = lane / G, g = lane - li * G;
+            const bool active = li < bcnt;
+            const uint32_t pi = active ? perm[first + li] : 0u;
+            const uint64_t vv = c0 + pi;
+            const uint64_t eb_v = eb0 + eloc[pi], r_v = active ? eloc[pi + 1] - eloc[pi] : 0;
+            const Acc a = staged ? run_batch(lsrc, c, active, vv, G, g, S0, E, eb0, blob, offsets, eb_v, r_v, values,
+                                             elems, cap, fix)
+                                 : run_batch_g(gsrc, c, active, vv, G, g, S0, E, eb0, blob, offsets, eb_v, r_v, values,
+                                               elems, cap, fix);
+            bad += a.bad;
+            pay += a.pay;
+            PROBE(if (lane == 0) {
+                atomicAdd((unsigned long long *)&prb[3 + c], (unsigned long long)(__builtin_amdgcn_s_memtime() - tb0));
+                atomicAdd((unsigned long long *)&prb[3 + C_N + c], 1ull);
+                atomicAdd((unsigned long long *)&prb[3 + 2 * C_N + c], (unsigned long long)bcnt);
+            })
+        }
+    }
+    if (v_hi == v_lo && wave == 0 && !nolb) {   // a window with no values still takes part in the look-back
+        const uint64_t pre = lb_resolve(lb_state, lb_groups, tile, nwin, agg, fix + 1);
+        if (lane == 0 && tile == nwin - 1) *total = pre + agg;
+    }
+    bad = wave_sum(bad);
+    pay = wave_sum(pay);
+    if (lane == 0) { red[0][wave] = bad; red[1][wave] = pay; }
+    DEC_SYNC();
+    if (tid == 0) {
+        uint64_t tb = 0, tp = 0;
+        for (uint32_t w = 0; w < NW; ++w) { tb += red[0][w]; tp += red[1][w]; }
+        stats[3 * (uint64_t)tile + 0] = tb;
+        stats[3 * (uint64_t)tile + 1] = tp;
+        stats[3 * (uint64_t)tile + 2] = 0;
+        PROBE(prb[0] = pt1 - pt0; prb[1] = pt2 - pt1; prb[2] = __builtin_amdgcn_s_memtime() - pt2; prb[28] = v_hi - v_lo;
+              prb[29] = staged; if (g_probe) for (uint32_t i = 0; i < PROBE_WORDS; ++i) g_probe[(uint64_t)tile * PROBE_WORDS + i] = prb[i];)
+    }
 }
 
 struct ElemV {
@@ -2477,6 +2863,48 @@ static uint64_t scan_tiles(uint64_t n) { return (n + SCAN_TILE - 1) / SCAN_TILE;
 // offsets[n] own no values and copy nothing
 static uint64_t dec_windows(uint64_t data_cap) { return data_cap / DEC_W + 1; }
 
+#ifndef RR_DEC_FUSED   // 1: dec_index_kernel + decode_fused_kernel; 0: count + scan + decode_kernel
+#define RR_DEC_FUSED 0
+#endif
+#if RR_DEC_FUSED
+// the fused kernel's chunk is one pass-A round of the workgroup's threads
+#undef RR_DEC_PMAX
+#define RR_DEC_PMAX (RR_DEC_NW * RR_WAVE)
+#define DECODE_FUSED_KERNEL decode_fused_kernel<RR_DEC_W, RR_DEC_SLACK, RR_DEC_NW, RR_DEC_PMAX>
+// Decode scratch (uint64 words): [HDR] [window look-back: state nwin, groups] [descriptor total,
+// 1] [fixup header, then its u32 list of up to n values] [window stats, 3 per window] [first_val
+// u32, nwin+1] [reservations u32, n] [class bytes, n].  dec_index_kernel zeroes the look-back
+// words, the total and the fixup header.
+extern "C" uint64_t rr_decode_scratch_words(uint64_t data_cap, uint64_t n) {
+    const uint64_t nw = dec_windows(data_cap);
+    return RR_SCRATCH_HDR + nw + (nw + LB_GROUP - 1) / LB_GROUP + FIX_HDR + (n + 2) / 2 + 1 + 3 * nw + (nw + 2) / 2 +
+           (n + 2) / 2 + (n + 7) / 8 + 2;
+}
+
+extern "C" hipError_t rr_launch_decode(const uint8_t *blob, const uint64_t *offsets, uint64_t n, rr_value *values,
+                                       rr_elem *elems, uint64_t elem_cap, uint8_t *arena, uint64_t *scratch,
+                                       uint64_t data_cap, rr_totals *totals, hipStream_t stream) {
+    const uint32_t nw = (uint32_t)dec_windows(data_cap);
+    uint64_t *lb_state = scratch + RR_SCRATCH_HDR;
+    uint64_t *lb_groups = lb_state + nw;
+    const uint64_t lb_words = nw + (nw + LB_GROUP - 1) / LB_GROUP;
+    uint64_t *total = lb_state + lb_words;
+    uint64_t *fix = total + 1;                           // header words, then the u32 list
+    uint64_t *stats = fix + FIX_HDR + (n + 2) / 2;
+    uint32_t *first_val = reinterpret_cast<uint32_t *>(stats + 3 * (uint64_t)nw);
+    uint32_t *cnt = first_val + ((nw + 2) & ~1u);
+    uint8_t *cls = reinterpret_cast<uint8_t *>(cnt + ((n + 2) & ~1ull));
+    hipLaunchKernelGGL(dec_index_kernel, dim3((uint32_t)((n + 1 + 255) / 256)), dim3(256), 0, stream, offsets, n,
+                       first_val, nw, DEC_W, lb_state, (uint32_t)(lb_words + 1 + FIX_HDR), totals);
+    hipLaunchKernelGGL((DECODE_FUSED_KERNEL), dim3(nw), dim3(DEC_NW * RR_WAVE), 0, stream, blob, data_cap, offsets, n,
+                       first_val, cls, cnt, values, elems, elem_cap, arena, stats, fix, nw, lb_state, lb_groups, total);
+    static uint32_t post_grid = 0;
+    if (!post_grid) post_grid = resident_grid(decode_post_kernel, FIX_NT, false);
+    hipLaunchKernelGGL(decode_post_kernel, dim3(post_grid), dim3(FIX_NT), 0, stream, blob, fix, values, elems, stats,
+                       total, nw, offsets, n, totals);
+    return hipGetLastError();
+}
+#else
 // Decode scratch (uint64 words): [HDR] [scan: ticket, look-back state + groups] [fixup header,
 // then its u32 list of up to n values] [counts -> elem_base, n+1] [window stats, 3 per window]
 // [first_val u32, nwin+1] [class bytes, n].  The look-back words and the fixup header are
@@ -2516,6 +2944,8 @@ extern "C" hipError_t rr_launch_decode(const uint8_t *blob, const uint64_t *offs
                        counts + n, nw, offsets, n, totals);
     return hipGetLastError();
 }
+
+#endif   // RR_DEC_FUSED
 
 // Encode scratch (uint64 words): [HDR] [scan: ticket, look-back state + groups]
 // [tile stats, 3 per 256 values, twice] [first value per output window u32, nwin+1].
