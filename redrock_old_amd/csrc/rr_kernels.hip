@@ -302,12 +302,17 @@ __device__ __forceinline__ void tile_stats(uint64_t *stats, uint32_t tile, uint6
 // mode 0 (decode): bytes = offsets[n]; mode 1 (encode): bytes = inclusive prefix of the last
 // tile.  Many blocks (one CU reads ~60 GB/s: a single-block fold of 121K tiles took 56 us),
 // each folding a slice and adding into *out, which the launcher zeroes first.
+// (nblocks: how many of the grid's blocks fold — the decode's post kernel folds in block 0 alone:
+// ~500 blocks each adding into the same three words serialised at the memory side)
 __device__ __forceinline__ void fold_totals(const uint64_t *__restrict__ stats, uint64_t *state, uint32_t ntiles,
                                             const uint64_t *__restrict__ offsets, uint64_t n, int mode, rr_totals *out,
-                                            const uint64_t *__restrict__ extra, uint64_t *err) {
+                                            const uint64_t *__restrict__ extra, uint64_t *err,
+                                            uint32_t nblocks = 0xFFFFFFFFu) {
     __shared__ uint64_t red[3][4];
     uint64_t b = 0, p = 0, c = 0;
-    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < ntiles; t += gridDim.x * blockDim.x) {
+    const uint32_t nbk = gridDim.x < nblocks ? gridDim.x : nblocks;
+    if (blockIdx.x >= nbk) return;
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < ntiles; t += nbk * blockDim.x) {
         b += stats[3 * (uint64_t)t + 0];
         p += stats[3 * (uint64_t)t + 1];
         c += stats[3 * (uint64_t)t + 2];
@@ -608,6 +613,60 @@ __global__ __launch_bounds__(256) void count_kernel(const uint8_t *__restrict__ 
         cls[i] = (uint8_t)c;
 #endif
     }
+}
+
+// ---- K1+K2 in one launch: count_scan_kernel -----------------------------------------------
+// count_kernel's per-value work, then the block's exclusive scan, then a decoupled look-back
+// between the 256-value blocks (blockIdx order, two-level groups, rr_device.h): the block writes
+// elem_base straight away.  The look-back's round trips (a few us under load) sit at the end of
+// each block and are hidden by the other resident blocks of the CU, so the separate scan launch
+// (its own look-back, the counts written and read again) goes away.  (A look-back that never
+// resolves — a block dispatched out of order behind a full machine — sets the call's error word
+// after the bounded wait: the host sees RR_API_EDEVICE, never a hang.)
+constexpr uint32_t CS_NT = 256;
+__global__ __launch_bounds__(CS_NT) void count_scan_kernel(const uint8_t *__restrict__ blob,
+                                                          const uint64_t *__restrict__ offsets, uint64_t n,
+                                                          uint32_t *__restrict__ first_val, uint32_t nwin, uint32_t win,
+                                                          uint64_t *__restrict__ ebase, uint8_t *__restrict__ cls,
+                                                          uint64_t *lb_state, uint64_t *lb_groups, uint32_t ntiles,
+                                                          uint64_t *err, rr_totals *tot) {
+    zero_call_words(nullptr, 0, tot);
+    __shared__ uint64_t wsum[CS_NT / RR_WAVE];
+    __shared__ uint64_t sh_pre;
+    const uint32_t tile = blockIdx.x, tid = threadIdx.x, lane = lane_id(), wave = tid / RR_WAVE;
+    const uint64_t i = (uint64_t)tile * CS_NT + tid;
+    uint64_t r = 0;
+    if (i <= n) {
+        const uint64_t o_hi = offsets[i];
+        const uint64_t w_lo = i == 0 ? 0 : offsets[i - 1] / win + 1;
+        const uint64_t w_hi = i == n ? nwin : o_hi / win;
+        for (uint64_t w = w_lo; w <= w_hi && w <= nwin; ++w) first_val[w] = (uint32_t)i;
+        if (i < n) {
+            const uint64_t b1 = offsets[i + 1];
+            uint32_t d[6];
+            head24(blob, o_hi, b1, d);
+            uint32_t c;
+            reserve_classify(blob + o_hi, b1 - o_hi, d, r, c);
+            cls[i] = (uint8_t)c;
+        }
+    }
+    const uint64_t incl = wave_incl_scan(r);
+    if (lane == RR_WAVE - 1) wsum[wave] = incl;
+    __syncthreads();
+    uint64_t wpre = 0, agg = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < CS_NT / RR_WAVE; ++k) {
+        wpre += k < wave ? wsum[k] : 0;
+        agg += wsum[k];
+    }
+    if (wave == 0) {
+        const uint64_t pre = lookback(lb_state, lb_groups, tile, ntiles, agg, err);
+        if (lane == 0) sh_pre = pre;
+    }
+    __syncthreads();
+    const uint64_t pre = sh_pre;
+    if (i < n) ebase[i] = pre + wpre + incl - r;
+    if (tile == ntiles - 1 && tid == CS_NT - 1) ebase[n] = pre + agg;   // the call's descriptor total
 }
 
 // ---- K2: exclusive scan of the reservations -> elem_base -------------------------------
@@ -1875,6 +1934,9 @@ __device__ __forceinline__ uint64_t block_excl_scan(uint64_t x, uint64_t *wsum, 
 // serObject output whose hash tables hold at most HT_FP_KEYS keys, barring 16-bit fingerprint
 // collisions.
 constexpr uint32_t FIX_NT = 256, FIX_TAB = 8192, FIX_TAB_BITS = 13, FIX_PASS_KEYS = 2048;
+#ifndef RR_POST_FOLD_BLOCKS   // blocks of the decode's post kernel that fold the window totals
+#define RR_POST_FOLD_BLOCKS 32
+#endif
 
 // 32-bit fingerprint of a member: length, first and last 8 bytes (bytes of the member only)
 __device__ __forceinline__ uint32_t member_fp(const uint8_t *__restrict__ blob, uint64_t off, uint32_t len) {
@@ -2059,7 +2121,7 @@ __global__ __launch_bounds__(FIX_NT) void decode_post_kernel(const uint8_t *__re
                                                              uint32_t ntiles, const uint64_t *__restrict__ offsets,
                                                              uint64_t n, rr_totals *out) {
     fixup_values(blob, fix, values, elems, out);
-    if (out) fold_totals(stats, state, ntiles, offsets, n, 2, out, nullptr, fix + 1);
+    if (out) fold_totals(stats, state, ntiles, offsets, n, 2, out, nullptr, fix + 1, RR_POST_FOLD_BLOCKS);
 }
 
 // ---------------------------------------------------------------------------------------- encode
@@ -2909,26 +2971,51 @@ extern "C" hipError_t rr_launch_decode(const uint8_t *blob, const uint64_t *offs
 // then its u32 list of up to n values] [counts -> elem_base, n+1] [window stats, 3 per window]
 // [first_val u32, nwin+1] [class bytes, n].  The look-back words and the fixup header are
 // zeroed by one memset per call.
+#ifndef RR_COUNT_SCAN   // 1: count_scan_kernel (one launch); 0: count_kernel + scan_kernel
+#define RR_COUNT_SCAN 0     // (measured: the 3.9K in-kernel look-backs cost +40 us on cfg 4, +50 on cfg 2)
+#endif
+static uint32_t cs_tiles(uint64_t n) { return (uint32_t)((n + 1 + CS_NT - 1) / CS_NT); }
+// look-back words of the reservation scan: count_scan_kernel's 256-value blocks, or scan_kernel's
+// ticket + 4096-value tiles
+static uint64_t dec_lb_words(uint64_t n) {
+#if RR_COUNT_SCAN
+    const uint64_t t = cs_tiles(n);
+    return t + (t + LB_GROUP - 1) / LB_GROUP;
+#else
+    const uint64_t st = scan_tiles(n);
+    return 1 + st + (st + LB_GROUP - 1) / LB_GROUP;
+#endif
+}
 extern "C" uint64_t rr_decode_scratch_words(uint64_t data_cap, uint64_t n) {
-    const uint64_t st = scan_tiles(n), nw = dec_windows(data_cap);
-    return RR_SCRATCH_HDR + 1 + st + (st + LB_GROUP - 1) / LB_GROUP + FIX_HDR + (n + 2) / 2 + (n + 1) + 3 * nw +
-           (nw + 2) / 2 + (n + 7) / 8 + 2;
+    const uint64_t nw = dec_windows(data_cap);
+    return RR_SCRATCH_HDR + dec_lb_words(n) + FIX_HDR + (n + 2) / 2 + (n + 1) + 3 * nw + (nw + 2) / 2 + (n + 7) / 8 + 2;
 }
 
 extern "C" hipError_t rr_launch_decode(const uint8_t *blob, const uint64_t *offsets, uint64_t n, rr_value *values,
                                        rr_elem *elems, uint64_t elem_cap, uint8_t *arena, uint64_t *scratch,
                                        uint64_t data_cap, rr_totals *totals, hipStream_t stream) {
     const uint32_t st = (uint32_t)scan_tiles(n), nw = (uint32_t)dec_windows(data_cap);
+    (void)st;
     uint64_t *lb = scratch + RR_SCRATCH_HDR;
-    const uint64_t lb_words = 1 + st + (st + LB_GROUP - 1) / LB_GROUP;
+    const uint64_t lb_words = dec_lb_words(n);
     uint64_t *fix = lb + lb_words;                      // header words, then the u32 list
     uint64_t *counts = fix + FIX_HDR + (n + 2) / 2;
     uint64_t *stats = counts + n + 1;
     uint32_t *first_val = reinterpret_cast<uint32_t *>(stats + 3 * (uint64_t)nw);
     uint8_t *cls = reinterpret_cast<uint8_t *>(first_val + ((nw + 2) & ~1u));
+#if RR_COUNT_SCAN   // reservations, classes and elem_base in one launch (count_scan_kernel), after one
+                    // memset of its look-back words and the fixup header (contiguous: scratch layout)
+    {
+        const uint32_t nb = cs_tiles(n);
+        if (hipMemsetAsync(lb, 0, (lb_words + FIX_HDR) * sizeof(uint64_t), stream) != hipSuccess) return hipGetLastError();
+        hipLaunchKernelGGL(count_scan_kernel, dim3(nb), dim3(CS_NT), 0, stream, blob, offsets, n, first_val, nw, DEC_W,
+                           counts, cls, lb, lb + nb, nb, fix + 1, totals);
+    }
+#else
     hipLaunchKernelGGL(count_kernel, dim3((uint32_t)((n + 1 + 255) / 256)), dim3(256), 0, stream, blob, offsets, n,
                        first_val, nw, DEC_W, counts, cls, lb, (uint32_t)(lb_words + FIX_HDR), totals);
     if (st) hipLaunchKernelGGL(scan_kernel, dim3(st), dim3(256), 0, stream, counts, n, lb, st, fix + 1);
+#endif
 #if RR_DEC_PF
     static uint32_t dec_grid = 0;
     if (!dec_grid) dec_grid = resident_grid(DECODE_KERNEL, DEC_NW * RR_WAVE, false);

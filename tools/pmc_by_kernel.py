@@ -1,0 +1,27 @@
+"""Sum rocprofv3 PMC counter_collection.csv values per kernel (diagnostics).
+usage: python3 tools/pmc_by_kernel.py DIR [DIR ...]"""
+import collections
+import csv
+import glob
+import re
+import sys
+
+for d in sys.argv[1:]:
+    tot = collections.defaultdict(lambda: collections.defaultdict(float))
+    for p in glob.glob(d + "/**/*counter_collection.csv", recursive=True):
+        for r in csv.DictReader(open(p)):
+            name = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "")
+            name = re.sub(r"[<(].*", "", name)
+            tot[name][r["Counter_Name"]] += float(r["Counter_Value"])
+    for k, c in tot.items():
+        if not any(x in k for x in ("decode", "count", "scan", "enc_", "post")):
+            continue
+        bc, ia = c.get("SQ_LDS_BANK_CONFLICT", 0), c.get("SQ_LDS_IDX_ACTIVE", 0)
+        line = f"{d.rstrip('/').split('/')[-1]:26s} {k:20s}"
+        if ia:
+            line += f" conflict/active {bc / ia:.3f} (conflict {bc:.3e}, active {ia:.3e})"
+        if "SQ_INSTS_LDS" in c:
+            line += f"  LDS insts {c['SQ_INSTS_LDS']:.3e}"
+        if "SQ_WAIT_INST_LDS" in c and c.get("SQ_WAVE_CYCLES"):
+            line += f"  wait_inst_lds/wave_cycles {c['SQ_WAIT_INST_LDS'] / c['SQ_WAVE_CYCLES']:.3f}"
+        print(line)
