@@ -894,9 +894,6 @@ __device__ __forceinline__ bool do_ziplist_bg(const Src &R, const Lane &l, bool 
 // the entry decode of round r (which needs nothing of the next chain): the decode's instructions
 // fill the chain's LDS-latency gaps instead of following them.  The last round walks one wasted
 // chain (clamped at entry 0).  Checks, stores and verdicts are do_ziplist_bg's.
-#ifndef RR_ZL_BLOCK   // rounds per block of the blocked ziplist walk (0: pipelined rounds)
-#define RR_ZL_BLOCK 0
-#endif
 template <uint32_t G, class Src>
 __device__ __forceinline__ bool do_ziplist_bp(const Src &R, const Lane &l, bool active, uint32_t g, uint32_t &n,
                                               uint64_t &pay) {
@@ -968,19 +965,6 @@ __device__ __forceinline__ bool do_ziplist_bp(const Src &R, const Lane &l, bool 
         put_desc(l.E, (mine & !bad) ? l.slot(idx + 1) : NOSLOT, zstr ? l.B + qp + ls : (uint64_t)iv, zstr ? sl : 0,
                  zstr ? RR_K_STR : RR_K_INT, zstr ? (e & 0xC0) : e);
     };
-#if RR_ZL_BLOCK > 0
-    // blocked: RR_ZL_BLOCK rounds of the lean chain (positions in registers), then their entry
-    // decodes, which are independent of each other (the compiler overlaps them)
-    constexpr uint32_t RB = RR_ZL_BLOCK;
-    for (uint32_t r0 = 0;; r0 += RB) {
-        uint32_t mp[RB], me[RB];
-#pragma unroll
-        for (uint32_t k = 0; k < RB; ++k) chain(mp[k], me[k]);
-#pragma unroll
-        for (uint32_t k = 0; k < RB; ++k) decode((r0 + k) * G + g, mp[k], me[k]);
-        if (__ballot((r0 + RB) * G < N) == 0) break;
-    }
-#else
     uint32_t mpA, meA;
     chain(mpA, meA);
     for (uint32_t rounds = 0;; ++rounds) {
@@ -991,7 +975,6 @@ __device__ __forceinline__ bool do_ziplist_bp(const Src &R, const Lane &l, bool 
         mpA = mpB;
         meA = meB;
     }
-#endif
     const uint32_t base = lane_id() - g;
     const uint64_t gm = (G >= 64 ? ~0ull : ((1ull << G) - 1)) << base;
     const bool gfail = (__ballot(fail) & gm) != 0;
