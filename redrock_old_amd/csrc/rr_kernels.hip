@@ -2550,6 +2550,24 @@ __device__ __forceinline__ uint64_t swar8(uint32_t x) {
     return ((uint64_t)four(hi) | ((uint64_t)four(lo) << 32)) + 0x3030303030303030ull;
 }
 
+#ifndef RR_ENC_OR   // 1: fields OR-ed into the zeroed image (one or two aligned 64-bit LDS atomics)
+#define RR_ENC_OR 1
+#endif
+#ifndef RR_ENC_ALIGNED   // 1: granule copies for pieces aligned with their image offset mod 16
+#define RR_ENC_ALIGNED 0
+#endif
+// lds_or writes the low nb (<= 8) bytes of v at image offset d into an image whose bytes there
+// are still zero (the image is zeroed first and no two fields overlap): the field OR-ed into the
+// one or two naturally aligned 8-byte words it touches, no-return LDS atomics, no branches on
+// the alignment (lds_put takes up to seven conditional stores).
+__device__ __forceinline__ void lds_or(uint8_t *img, uint32_t d, uint64_t v, uint32_t nb) {
+    v = nb >= 8 ? v : v & ((1ull << (8 * nb)) - 1);
+    const uint32_t s = (d & 7u) * 8u;
+    uint64_t *w = reinterpret_cast<uint64_t *>(img + (d & ~7u));
+    __hip_atomic_fetch_or(w, v << s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (s && s + 8 * nb > 64) __hip_atomic_fetch_or(w + 1, v >> (64 - s), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 // The window image: writes at absolute output positions, clipped to [w0, w0 + span).
 struct Img {
     uint8_t *img;
@@ -2562,7 +2580,11 @@ struct Img {
     // little-endian field of nb (<= 8) bytes
     __device__ __forceinline__ void field(uint64_t pos, uint64_t v, uint32_t nb) const {
         const uint64_t d = pos - w0;
+#if RR_ENC_OR
+        if (d < span && d + nb <= span) lds_or(img, (uint32_t)d, v, nb);
+#else
         if (d < span && d + nb <= span) lds_put(img, (uint32_t)d, v, nb);
+#endif
         else
             for (uint32_t i = 0; i < nb; ++i) put(pos + i, (uint32_t)(v >> (8 * i)) & 0xFF);
     }
@@ -2642,6 +2664,44 @@ struct Img {
         if (r_ & 1) i_[p_] = (uint8_t)P##t1;                                                     \
     }
 
+// Granule copy of a piece aligned with its image offset mod 16 (RR_ENC_ALIGNED): up to four
+// aligned 16-byte loads, each clamped to the piece's last granule; full granules stored as
+// they are, partial ones masked and OR-ed into the zeroed image (no-return 64-bit LDS atomics).
+#define RR_AL_LOAD(X, S, D, L)                                                                   \
+    u32x4 X##0 = {0u, 0u, 0u, 0u}, X##1 = X##0, X##2 = X##0, X##3 = X##0;                      \
+    if ((L) > 0) {                                                                               \
+        const uint32_t c0_ = (D) & ~15u, cl_ = ((D) + (L) - 1) & ~15u;                           \
+        const u32x4 *g_ = reinterpret_cast<const u32x4 *>(arena + (S) - ((D) - c0_));            \
+        X##0 = g_[0];                                                                            \
+        X##1 = g_[c0_ + 16 <= cl_ ? 1 : 0];                                                      \
+        X##2 = g_[c0_ + 32 <= cl_ ? 2 : 0];                                                      \
+        X##3 = g_[c0_ + 48 <= cl_ ? 3 : 0];                                                      \
+    }
+#define RR_AL_CHUNK(XK, K, D, L)                                                                 \
+    {                                                                                            \
+        const uint32_t dc_ = ((D) & ~15u) + 16u * (K), e_ = (D) + (L);                           \
+        if ((L) > 0 && dc_ < e_) {                                                               \
+            const uint32_t lo_ = (D) > dc_ ? (D) - dc_ : 0u, hi_ = e_ < dc_ + 16u ? e_ - dc_ : 16u; \
+            if (lo_ == 0 && hi_ == 16) {                                                         \
+                img4[dc_ >> 4] = make_uint4(XK[0], XK[1], XK[2], XK[3]);                         \
+            } else {                                                                             \
+                _Pragma("unroll") for (uint32_t h_ = 0; h_ < 2; ++h_) {                          \
+                    const uint32_t a_ = lo_ > 8 * h_ ? lo_ - 8 * h_ : 0u;                         \
+                    const uint32_t b0_ = hi_ > 8 * h_ ? hi_ - 8 * h_ : 0u, b_ = b0_ < 8 ? b0_ : 8u; \
+                    if (b_ > a_) {                                                               \
+                        const uint64_t m_ = (~0ull >> (64 - 8 * (b_ - a_))) << (8 * a_);         \
+                        const uint64_t v_ = (h_ ? ((uint64_t)XK[3] << 32 | XK[2])                \
+                                                : ((uint64_t)XK[1] << 32 | XK[0])) & m_;         \
+                        __hip_atomic_fetch_or(reinterpret_cast<uint64_t *>(img + dc_ + 8 * h_), v_, \
+                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);   \
+                    }                                                                            \
+                }                                                                                \
+            }                                                                                    \
+        }                                                                                        \
+    }
+#define RR_AL_STORE(X, D, L)                                                                     \
+    RR_AL_CHUNK(X##0, 0, D, L) RR_AL_CHUNK(X##1, 1, D, L) RR_AL_CHUNK(X##2, 2, D, L) RR_AL_CHUNK(X##3, 3, D, L)
+
 // Copy-run queue: one entry per payload (arena offset (40 bits) | length << 40, image offset,
 // first piece); the copy phase splits the runs into 64-byte image-block pieces.
 constexpr uint64_t JQ_SRC = (1ull << 40) - 1;
@@ -2671,6 +2731,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(RR_ENC_WPE))
     __shared__ uint64_t wsum[2][NT / RR_WAVE];
     __shared__ uint64_t sh_nrp;            // runs reserved | pieces reserved << 32
     __shared__ uint32_t sh_pend;           // pieces of the queued runs, when the queue overflowed
+    __shared__ uint32_t sh_unal;           // some queued run is not aligned with its image offset mod 16
     uint8_t *img = reinterpret_cast<uint8_t *>(img4);
     const uint32_t tid = threadIdx.x;
     const uint64_t total = offsets[n];
@@ -2682,7 +2743,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(RR_ENC_WPE))
     const Img I{img, w0, span};
 #pragma unroll
     for (uint32_t k = tid; k < W / 16; k += NT) img4[k] = make_uint4(0, 0, 0, 0);
-    if (tid == 0) { sh_nrp = 0; sh_pend = 0xFFFFFFFFu; }
+    if (tid == 0) { sh_nrp = 0; sh_pend = 0xFFFFFFFFu; sh_unal = 0; }
     const uint64_t v0 = fv[blockIdx.x];
     const uint64_t vend = w0 + W < total ? (uint64_t)fv[blockIdx.x + 1] + 1 : n;
     lds_barrier();
@@ -2712,6 +2773,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(RR_ENC_WPE))
         if (queued && r < RCAP) {
             rq_a[r] = src | ((uint64_t)l << 40);
             rq_dp[r] = dst | (p0 << 16);
+#if RR_ENC_ALIGNED
+            if ((reinterpret_cast<uintptr_t>(arena) + src - dst) & 15) sh_unal = 1;
+#endif
         } else {   // queue full (rare; keeps the kernel small): byte copy
             if (queued && r == RCAP) sh_pend = p0;
             for (uint32_t i = 0; i < l; ++i) img[dst + i] = arena[src + i];
@@ -2858,6 +2922,24 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(RR_ENC_WPE))
         pd = d0;
         pl = e > d0 ? e - d0 : 0;   // (inside one 64-byte block by construction)
     };
+#if RR_ENC_ALIGNED
+    // Every run aligned with its image offset mod 16 (any arena that keeps the blob layout, the
+    // decode's mirror arena included): pieces move whole granules (RR_AL_LOAD / RR_AL_STORE).
+    // A window with any other run takes the byte plan below for all its pieces.
+    if (sh_unal == 0) {
+        for (uint32_t j = tid; j < npc; j += 2 * NT) {
+            const bool two = j + NT < npc;
+            uint64_t s0, s1 = 0;
+            uint32_t d0, l0, d1 = 0, l1 = 0;
+            piece(j, s0, d0, l0);
+            if (two) piece(j + NT, s1, d1, l1);
+            RR_AL_LOAD(xa, s0, d0, l0)
+            RR_AL_LOAD(xb, s1, d1, l1)
+            RR_AL_STORE(xa, d0, l0)
+            RR_AL_STORE(xb, d1, l1)
+        }
+    } else
+#endif
     for (uint32_t j = tid; j < npc; j += 2 * NT) {
         const bool two = j + NT < npc;
         uint64_t s0, s1 = 0;
