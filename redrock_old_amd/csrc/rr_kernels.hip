@@ -2554,7 +2554,7 @@ __device__ __forceinline__ uint64_t swar8(uint32_t x) {
 #define RR_ENC_OR 1
 #endif
 #ifndef RR_ENC_ALIGNED   // 1: granule copies for pieces aligned with their image offset mod 16
-#define RR_ENC_ALIGNED 0
+#define RR_ENC_ALIGNED 1
 #endif
 // lds_or writes the low nb (<= 8) bytes of v at image offset d into an image whose bytes there
 // are still zero (the image is zeroed first and no two fields overlap): the field OR-ed into the
