@@ -27,27 +27,39 @@
 static int fails;
 #define CHECK(c, ...) do { if (!(c)) { fails++; printf("FAIL: "); printf(__VA_ARGS__); printf("\n"); } } while (0)
 
-/* ---- the snapshot store: key "k:<i>" -> valid fixture i % nvalid ---- */
+/* ---- the snapshot store: key "k:<i>" -> valid fixture i % nvalid, or (bench with a config)
+ * value i of a generated batch ---- */
 static const fixture_t *valid[N_FIXTURES];
 static int nvalid;
-static const fixture_t *blob_of(const char *key, size_t len) {
+static rr_host_batch gen;   /* gen.n > 0: the store serves this batch */
+typedef struct { const uint8_t *blob; size_t len; } val_t;
+static int blob_of(const char *key, size_t len, val_t *v) {
     char buf[32];
-    if (len < 3 || len >= sizeof buf) return NULL;
+    if (len < 3 || len >= sizeof buf) return 0;
     memcpy(buf, key, len);
     buf[len] = 0;
     long i = strtol(buf + 2, NULL, 10);
-    return i >= 0 ? valid[i % nvalid] : NULL;
+    if (i < 0) return 0;
+    if (gen.n) {
+        const uint64_t j = (uint64_t)i % gen.n;
+        v->blob = gen.data + gen.offsets[j];
+        v->len = gen.offsets[j + 1] - gen.offsets[j];
+    } else {
+        v->blob = valid[i % nvalid]->blob;
+        v->len = valid[i % nvalid]->len;
+    }
+    return 1;
 }
 static int store_get(void *user, size_t k, const int *dbis, const char *const *keys, const size_t *lens, void **vals,
                      size_t *vlens) {
     (void)user;
     for (size_t i = 0; i < k; i++) {
-        const fixture_t *f = dbis[i] == 3 ? blob_of(keys[i], lens[i]) : NULL;
+        val_t f;
         vals[i] = NULL;
-        if (!f) continue;
-        vals[i] = malloc(f->len ? f->len : 1);
-        memcpy(vals[i], f->blob, f->len);
-        vlens[i] = f->len;
+        if (dbis[i] != 3 || !blob_of(keys[i], lens[i], &f)) continue;
+        vals[i] = malloc(f.len ? f.len : 1);
+        memcpy(vals[i], f.blob, f.len);
+        vlens[i] = f.len;
     }
     return 0;
 }
@@ -72,10 +84,10 @@ static void *serial_server(void *a) {
         if (rd(s->rfd, &klen, sizeof klen) != 1) { s->rc = -1; break; }
         char key[64];
         if (klen >= sizeof key || rd(s->rfd, key, klen) != 1) { s->rc = -1; break; }
-        const fixture_t *f = dbi == 3 ? blob_of(key, klen) : NULL;
-        if (!f) { s->rc = -1; break; }
-        size_t vlen = f->len;
-        if (wr(s->wfd, &vlen, sizeof vlen) != 1 || wr(s->wfd, f->blob, vlen) != 1) { s->rc = -1; break; }
+        val_t f;
+        if (dbi != 3 || !blob_of(key, klen, &f)) { s->rc = -1; break; }
+        size_t vlen = f.len;
+        if (wr(s->wfd, &vlen, sizeof vlen) != 1 || wr(s->wfd, f.blob, vlen) != 1) { s->rc = -1; break; }
     }
     close(s->wfd);
     return NULL;
@@ -107,9 +119,10 @@ static void stop(server_t *s, int cfd_req, int cfd_resp, pthread_t th) {
 static void check_blobs(const rr_rdb_blobs *b, size_t k, char **keys, size_t *lens, const char *what) {
     CHECK(b->n == k, "%s: %llu values for %zu keys", what, (unsigned long long)b->n, k);
     for (size_t i = 0; i < k && i < b->n; i++) {
-        const fixture_t *f = blob_of(keys[i], lens[i]);
+        val_t f;
+        blob_of(keys[i], lens[i], &f);
         const uint64_t len = b->offsets[i + 1] - b->offsets[i];
-        if (len != f->len || memcmp(b->data + b->offsets[i], f->blob, f->len)) {
+        if (len != f.len || memcmp(b->data + b->offsets[i], f.blob, f.len)) {
             CHECK(0, "%s: value %zu differs", what, i);
             break;
         }
@@ -120,7 +133,13 @@ static void check_blobs(const rr_rdb_blobs *b, size_t k, char **keys, size_t *le
 static double now(void) { struct timespec t; clock_gettime(CLOCK_MONOTONIC, &t); return t.tv_sec + t.tv_nsec * 1e-9; }
 
 /* bench: keys/s of the reference's serial fetch, the pipelined RAW batch and the FLAT restore
- * (fetch + GPU decode in the service + robj in the child) over the same pipes */
+ * (fetch + GPU decode in the service + robj in the child) over the same pipes.  With the oracle
+ * linked (RR_RDB_BENCH_ORACLE, test infrastructure), the RAW legs also run the child's CPU
+ * desObject on every fetched value (oracle/rro_faithful.c: the reference's allocation pattern),
+ * so the child's whole restore is timed on both sides. */
+#ifdef RR_RDB_BENCH_ORACLE
+#include "rr_oracle.h"
+#endif
 static int bench(size_t k, char **keys, size_t *lens, int *dbis) {
     server_t s;
     pthread_t th;
@@ -137,11 +156,40 @@ static int bench(size_t k, char **keys, size_t *lens, int *dbis) {
     }
     const double t_serial = now() - t0;
     stop(&s, fq, fr, th);
+    double t_serial_des = 0, t_batch_des = 0;
+#ifdef RR_RDB_BENCH_ORACLE
+    /* the reference child: one round trip, then desObject, per key (rock.c:527-550) */
+    start(&s, &fq, &fr, 0, NULL, &th);
+    t0 = now();
+    for (size_t i = 0; i < k; i++) {
+        size_t vlen = 0;
+        wr(fq, &dbis[i], sizeof(int)); wr(fq, &lens[i], sizeof(size_t)); wr(fq, keys[i], lens[i]);
+        rd(fr, &vlen, sizeof vlen);
+        uint8_t *v = malloc(vlen ? vlen : 1);
+        rd(fr, v, vlen);
+        const uint64_t o[2] = {0, vlen};
+        uint64_t nbad = 0;
+        rro_store *st = rro_faithful_decode(v, o, 1, &nbad);
+        rro_store_free(st);
+        free(v);
+    }
+    t_serial_des = now() - t0;
+    stop(&s, fq, fr, th);
+#endif
     start(&s, &fq, &fr, 0, NULL, &th);
     rr_rdb_blobs b;
     t0 = now();
     rr_rdb_request_batch(fq, fr, dbis, (const char *const *)keys, lens, k, &b);
     const double t_batch = now() - t0;
+#ifdef RR_RDB_BENCH_ORACLE
+    {   /* the pipelined RAW batch + the child's CPU desObject on every value */
+        uint64_t nbad = 0;
+        const double t1 = now();
+        rro_store *st = rro_faithful_decode(b.data, b.offsets, b.n, &nbad);
+        t_batch_des = t_batch + (now() - t1);
+        rro_store_free(st);
+    }
+#endif
     rr_rdb_blobs_free(&b);
     stop(&s, fq, fr, th);
     rr_ctx *ctx = NULL;
@@ -159,8 +207,20 @@ static int bench(size_t k, char **keys, size_t *lens, int *dbis) {
     for (size_t i = 0; i < k; i++) { decrRefCount(objs[i]); sdsfree(sk[i]); }
     free(objs); free(sk);
     rr_ctx_destroy(ctx);
-    printf("{\"keys\": %zu, \"serial_fetch_keys_per_s\": %.0f, \"batch_fetch_keys_per_s\": %.0f, "
-           "\"flat_restore_keys_per_s\": %.0f}\n", k, k / t_serial, k / t_batch, k / t_flat);
+    uint64_t bytes = 0;
+    for (size_t i = 0; i < k; i++) {
+        val_t f;
+        blob_of(keys[i], lens[i], &f);
+        bytes += f.len;
+    }
+    printf("{\"keys\": %zu, \"bytes\": %llu, \"store\": \"%s\", \"serial_fetch_keys_per_s\": %.0f, "
+           "\"batch_fetch_keys_per_s\": %.0f, \"flat_restore_keys_per_s\": %.0f",
+           k, (unsigned long long)bytes, gen.n ? "generated batch" : "golden fixtures", k / t_serial, k / t_batch,
+           k / t_flat);
+    if (t_serial_des > 0)
+        printf(", \"serial_fetch_cpu_desobject_keys_per_s\": %.0f, \"batch_fetch_cpu_desobject_keys_per_s\": %.0f",
+               k / t_serial_des, k / t_batch_des);
+    printf("}\n");
     return 0;
 }
 
@@ -168,12 +228,19 @@ int main(int argc, char **argv) {
     const int gpu = argc > 1 && !strcmp(argv[1], "gpu");
     for (int i = 0; i < N_FIXTURES; i++)
         if (FIXTURES[i].status == 0) valid[nvalid++] = &FIXTURES[i];
-    enum { K = 20000 };
-    static char *keys[K];
-    static size_t lens[K];
-    static int dbis[K];
-    make_keys(K, keys, lens, dbis);
-    if (argc > 1 && !strcmp(argv[1], "bench")) return bench(K, keys, lens, dbis);
+    enum { K = 20000, KB = 200000 };
+    static char *keys[KB];
+    static size_t lens[KB];
+    static int dbis[KB];
+    make_keys(KB, keys, lens, dbis);
+    if (argc > 1 && !strcmp(argv[1], "bench")) {   /* bench [config k]: a generated store of k values */
+        size_t k = K;
+        if (argc > 3) {
+            k = (size_t)strtoull(argv[3], NULL, 10);
+            if (k == 0 || k > KB || rr_gen_batch(atoi(argv[2]), k, rr_gen_default_seed(atoi(argv[2])), &gen) != 0) return 2;
+        }
+        return bench(k, keys, lens, dbis);
+    }
     server_t s;
     pthread_t th;
     int fq, fr;
@@ -199,8 +266,9 @@ int main(int argc, char **argv) {
         if (rd(fr, &vlen, sizeof vlen) != 1) { CHECK(0, "serial child: no response"); break; }
         char *v = malloc(vlen ? vlen : 1);
         rd(fr, v, vlen);
-        const fixture_t *f = blob_of(keys[i], lens[i]);
-        CHECK(vlen == f->len && !memcmp(v, f->blob, vlen), "serial child: value %zu differs", i);
+        val_t f;
+        blob_of(keys[i], lens[i], &f);
+        CHECK(vlen == f.len && !memcmp(v, f.blob, vlen), "serial child: value %zu differs", i);
         free(v);
     }
     stop(&s, fq, fr, th);
@@ -234,8 +302,9 @@ int main(int argc, char **argv) {
         stop(&s, fq, fr, th);
         CHECK(s.rc == 0, "flat service error");
         for (size_t i = 0; i < KF; i++) {
-            const fixture_t *f = blob_of(keys[i], lens[i]);
-            robj *o = desObject((void *)f->blob, f->len);
+            val_t f;
+            blob_of(keys[i], lens[i], &f);
+            robj *o = desObject((void *)f.blob, f.len);
             sds a = serObject(objs[i]), c = serObject(o);
             if (sdslen(a) != sdslen(c) || memcmp(a, c, sdslen(a))) { CHECK(0, "flat restore: value %zu differs", i); }
             CHECK(objs[i]->lru == o->lru && objs[i]->type == o->type && objs[i]->encoding == o->encoding,
@@ -247,7 +316,7 @@ int main(int argc, char **argv) {
         }
         rr_ctx_destroy(ctx);
     }
-    for (size_t i = 0; i < K; i++) free(keys[i]);
+    for (size_t i = 0; i < KB; i++) free(keys[i]);
     printf("%d failures (%d valid fixtures, %s)\n", fails, nvalid, gpu ? "cpu+gpu" : "cpu");
     return fails ? 1 : 0;
 }

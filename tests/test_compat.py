@@ -109,16 +109,20 @@ def test_compat_shim_round_trips_fixtures_on_gpu(tmp_path):
 
 
 # ---- row f4: batched snapshot restore over the fork-child pipes (include/rr_rdb.h) --------
-def build_rdb(tmp):
+def build_rdb(tmp, bench=False):
+    """bench=True links the oracle (test infrastructure) for the CPU desObject legs of the bench."""
     write_fixtures(os.path.join(tmp, "fixtures.h"))
     exe = os.path.join(tmp, "test_rdb")
-    cmd = ["gcc", "-std=gnu11", "-O1", "-Wall", "-Werror", "-Wno-unused-function", "-DRR_REDIS_TREE", "-pthread",
+    oracle = os.path.join(ROOT, "oracle")
+    extra = (["-DRR_RDB_BENCH_ORACLE", "-I", oracle, "-L", oracle, "-lrr_oracle", "-Wl,-rpath," + oracle]
+             if bench else [])
+    cmd = ["gcc", "-std=gnu11", "-O2", "-Wall", "-Werror", "-Wno-unused-function", "-DRR_REDIS_TREE", "-pthread",
            "-I", os.path.join(ROOT, "tests", "c", "miniredis"), "-I", os.path.join(ROOT, "include"), "-I", tmp,
            os.path.join(ROOT, "redrock_old_amd", "compat", "rock_serdes_compat.c"),
            os.path.join(ROOT, "tests", "c", "miniredis", "miniredis.c"),
            os.path.join(ROOT, "tests", "c", "test_rdb.c"),
            "-L", os.path.join(ROOT, "redrock_old_amd"), "-lrr_serdes",
-           "-Wl,-rpath," + os.path.join(ROOT, "redrock_old_amd"), "-o", exe]
+           "-Wl,-rpath," + os.path.join(ROOT, "redrock_old_amd")] + extra + ["-o", exe]
     subprocess.run(cmd, check=True)
     return exe
 
@@ -144,12 +148,14 @@ def test_rdb_flat_restore_on_gpu(tmp_path):
     assert "0 failures" in r.stdout
 
 
-if __name__ == "__main__":   # python tests/test_compat.py bench  (GPU box): keys/s of the restore paths
+if __name__ == "__main__":   # python tests/test_compat.py bench [config k]  (GPU box): keys/s of the restore paths
     import sys
     import tempfile
-    if sys.argv[1:] == ["bench"]:
+    if sys.argv[1:2] == ["bench"]:
         with tempfile.TemporaryDirectory() as d:
-            print(subprocess.run([build_rdb(d), "bench"], capture_output=True, text=True, timeout=300).stdout)
+            r = subprocess.run([build_rdb(d, bench=True), "bench"] + sys.argv[2:4], capture_output=True, text=True,
+                               timeout=600)
+            print(r.stdout, r.stderr)
 
 
 # ---- row f2: batched store I/O around the GPU path (include/rr_kv.h) ----------------------
