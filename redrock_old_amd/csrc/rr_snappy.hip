@@ -38,6 +38,9 @@ constexpr uint32_t MARGIN = 15;            // kInputMarginBytes
 #define RR_SNZ_DEC_WIN 20480
 #endif
 constexpr uint32_t SNZ_DEC_WIN = RR_SNZ_DEC_WIN;
+#ifndef RR_SNZ_LIT16   // 1: long literals copied 16 bytes per lane, two 1 KiB chunks per round trip
+#define RR_SNZ_LIT16 1
+#endif
 // staged fragment bytes per wave; 0 (default): the compressor reads its input in place through
 // the buffer resource, so a wave holds only the 32 KiB hash table (4 waves per CU instead of 3)
 #ifndef RR_SNZ_FRAG
@@ -46,6 +49,7 @@ constexpr uint32_t SNZ_DEC_WIN = RR_SNZ_DEC_WIN;
 constexpr uint32_t SNZ_FRAG_LDS = RR_SNZ_FRAG;
 
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 // LDS pointers kept in address space 3, so accesses compile to ds_* (a generic pointer gives flat_*
 // instructions, whose waits also drain every outstanding global store of the wave)
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
@@ -85,17 +89,23 @@ __global__ __launch_bounds__(256) void snz_len_kernel(const uint8_t *__restrict_
 }
 
 // The compressed block through a register window: lane l holds bytes [wb + 16 l, wb + 16 l + 16)
-// of the block's buffer resource (positions q relative to it), 1 KiB in all.
+// of the block's buffer resource (positions q relative to it), 1 KiB in all.  (A second KiB
+// loaded ahead, the window sliding by 1 KiB as the parse passes it, measured 17 % slower.)
 struct Win {
     rsrc_t R;
     uint32_t wb;
     uint32_t x[4];
+    static constexpr uint32_t SPAN = 1024;
     __device__ __forceinline__ void load(uint32_t at) {
         wb = at & ~15u;
         const auto v = __builtin_amdgcn_raw_buffer_load_b128(R, (int)(wb + 16 * lane_id()), 0, 0);
         x[0] = v[0]; x[1] = v[1]; x[2] = v[2]; x[3] = v[3];
     }
-    // the aligned dword at q (q - wb < 1024, q % 4 == 0), uniform
+    // keep p (+ 8 bytes) inside the window
+    __device__ __forceinline__ void track(uint32_t p) {
+        if (p + 8 > wb + SPAN) load(p);
+    }
+    // the aligned dword at q (q - wb < SPAN, q % 4 == 0), uniform
     __device__ __forceinline__ uint32_t dw(uint32_t q) const {
         const uint32_t r = q - wb, k = (r >> 2) & 3;
         const uint32_t v = k == 0 ? x[0] : k == 1 ? x[1] : k == 2 ? x[2] : x[3];
@@ -140,7 +150,7 @@ __global__ __launch_bounds__(WAVE) void snz_dec_kernel(const uint8_t *__restrict
         const rsrc_t Ro = mkr(gout, expected);
         uint32_t pos = 0, st = RR_SNAPPY_OK;
         while (p < end) {
-            if (p + 8 > W.wb + 1024) W.load(p);
+            W.track(p);
             const uint64_t t = W.bytes(p);
             const uint32_t c = (uint32_t)t & 0xFF;
             if ((c & 3) == 0) {   // literal
@@ -156,7 +166,7 @@ __global__ __launch_bounds__(WAVE) void snz_dec_kernel(const uint8_t *__restrict
                 p += hdr;
                 if (len > end - p) { st = RR_SNAPPY_E_TRUNC; break; }
                 if (len > expected - pos) { st = RR_SNAPPY_E_OVERFLOW; break; }
-                if (inl && len <= WAVE && p + len <= W.wb + 1024) {
+                if (inl && len <= WAVE && p + len <= W.wb + Win::SPAN) {
                     // a short literal inside the register window: lane k gathers byte p + k from
                     // the lane holding it (ds_bpermute, no memory access)
                     const uint32_t r = p + lane - W.wb, src = (r >> 4) & (WAVE - 1), k4 = (r >> 2) & 3;
@@ -164,7 +174,7 @@ __global__ __launch_bounds__(WAVE) void snz_dec_kernel(const uint8_t *__restrict
                     const uint32_t y1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src * 4), (int)W.x[1]);
                     const uint32_t y2 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src * 4), (int)W.x[2]);
                     const uint32_t y3 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src * 4), (int)W.x[3]);
-                    const uint32_t y = k4 == 0 ? y0 : k4 == 1 ? y1 : k4 == 2 ? y2 : y3;
+                    uint32_t y = k4 == 0 ? y0 : k4 == 1 ? y1 : k4 == 2 ? y2 : y3;
                     if (lane < len) win[pos + lane] = (uint8_t)(y >> (8 * (r & 3)));
                 } else if (inl) {
                     // bytes up to a 4-aligned output position, then whole dwords (a lane's dword
@@ -173,6 +183,37 @@ __global__ __launch_bounds__(WAVE) void snz_dec_kernel(const uint8_t *__restrict
                     const uint32_t h = min((4u - (pos & 3)) & 3, len);
                     if (lane < h) win[pos + lane] = __builtin_amdgcn_raw_buffer_load_b8(W.R, (int)(p + lane), 0, 0);
                     const uint32_t d0 = pos + h, q0 = p + h, body = len - h;
+#if RR_SNZ_LIT16
+                    // 16 bytes per lane (one dwordx4 + one dword load from the dword-aligned source,
+                    // four alignbyte dwords), two 1 KiB chunks in flight per round trip
+                    const uint32_t a0 = q0 & ~3u, sh = q0 & 3;
+                    // the window the next tag needs, loaded beside the literal's bytes (one round
+                    // trip for both instead of a reload after the copy)
+                    const uint32_t pn = p + len, nwb = pn & ~15u;
+                    const bool slide = pn + 8 > W.wb + Win::SPAN;
+                    u32x4_t nx = {W.x[0], W.x[1], W.x[2], W.x[3]};
+                    if (slide) nx = __builtin_amdgcn_raw_buffer_load_b128(W.R, (int)(nwb + 16 * lane), 0, 0);
+                    for (uint32_t i = 0; i < body; i += 32 * WAVE) {
+                        const uint32_t kA = i + 16 * lane, kB = kA + 16 * WAVE;
+                        const auto xA = __builtin_amdgcn_raw_buffer_load_b128(W.R, (int)(a0 + kA), 0, 0);
+                        const uint32_t eA = __builtin_amdgcn_raw_buffer_load_b32(W.R, (int)(a0 + kA + 16), 0, 0);
+                        const auto xB = __builtin_amdgcn_raw_buffer_load_b128(W.R, (int)(a0 + kB), 0, 0);
+                        const uint32_t eB = __builtin_amdgcn_raw_buffer_load_b32(W.R, (int)(a0 + kB + 16), 0, 0);
+                        lds_u32 *wA = win32 + ((d0 + kA) >> 2), *wB = win32 + ((d0 + kB) >> 2);
+                        if (kA < body) wA[0] = __builtin_amdgcn_alignbyte(xA[1], xA[0], sh);
+                        if (kA + 4 < body) wA[1] = __builtin_amdgcn_alignbyte(xA[2], xA[1], sh);
+                        if (kA + 8 < body) wA[2] = __builtin_amdgcn_alignbyte(xA[3], xA[2], sh);
+                        if (kA + 12 < body) wA[3] = __builtin_amdgcn_alignbyte(eA, xA[3], sh);
+                        if (kB < body) wB[0] = __builtin_amdgcn_alignbyte(xB[1], xB[0], sh);
+                        if (kB + 4 < body) wB[1] = __builtin_amdgcn_alignbyte(xB[2], xB[1], sh);
+                        if (kB + 8 < body) wB[2] = __builtin_amdgcn_alignbyte(xB[3], xB[2], sh);
+                        if (kB + 12 < body) wB[3] = __builtin_amdgcn_alignbyte(eB, xB[3], sh);
+                    }
+                    if (slide) {
+                        W.wb = nwb;
+                        W.x[0] = nx[0]; W.x[1] = nx[1]; W.x[2] = nx[2]; W.x[3] = nx[3];
+                    }
+#else
                     for (uint32_t i = 0; i < body; i += 4 * WAVE) {
                         const uint32_t k = i + 4 * lane;
                         if (k < body) {
@@ -182,6 +223,7 @@ __global__ __launch_bounds__(WAVE) void snz_dec_kernel(const uint8_t *__restrict
                             win32[(d0 + k) >> 2] = __builtin_amdgcn_alignbyte(hi, lo, q & 3);
                         }
                     }
+#endif
                 } else {
                     for (uint32_t i = 0; i < len; i += WAVE) {
                         const uint32_t k = i + lane;
@@ -223,10 +265,27 @@ __global__ __launch_bounds__(WAVE) void snz_dec_kernel(const uint8_t *__restrict
             const uint32_t g0 = (uint32_t)((uintptr_t)gout & 3), hh = min((4u - g0) & 3, expected);
             const uint32_t t0 = hh + ((expected - hh) & ~3u);
             if (lane < hh) __builtin_amdgcn_raw_buffer_store_b8(win[lane], Ro, (int)lane, 0, 0);
+#if RR_SNZ_LIT16
+            // 16 bytes per lane: five LDS dwords -> four output dwords, one dwordx4 store (output
+            // dword-aligned); the last partial group of dwords one at a time
+            const uint32_t sh = hh & 3, t16 = hh + ((t0 - hh) & ~15u);
+            for (uint32_t j = hh + 16 * lane; j < t16; j += 16 * WAVE) {
+                const uint32_t a = j >> 2;
+                const uint32_t w0 = win32[a], w1 = win32[a + 1], w2 = win32[a + 2], w3 = win32[a + 3], w4 = win32[a + 4];
+                const u32x4_t v = {__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
+                                   __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh)};
+                __builtin_amdgcn_raw_buffer_store_b128(v, Ro, (int)j, 0, 0);
+            }
+            for (uint32_t j = t16 + 4 * lane; j < t0; j += 4 * WAVE) {
+                const uint32_t a = j >> 2;
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_amdgcn_alignbyte(win32[a + 1], win32[a], j & 3), Ro, (int)j, 0, 0);
+            }
+#else
             for (uint32_t j = hh + 4 * lane; j < t0; j += 4 * WAVE) {
                 const uint32_t a = j >> 2;
                 __builtin_amdgcn_raw_buffer_store_b32(__builtin_amdgcn_alignbyte(win32[a + 1], win32[a], j & 3), Ro, (int)j, 0, 0);
             }
+#endif
             if (t0 + lane < expected) __builtin_amdgcn_raw_buffer_store_b8(win[t0 + lane], Ro, (int)(t0 + lane), 0, 0);
         }
         if (lane == 0) status[b] = (uint8_t)st;

@@ -9,10 +9,14 @@
  *                 status == 0  -> serObject(desObject(b)) must be the blob serObject writes for
  *                                 the object desObject built (the fixture's "reencoded", lru
  *                                 masked to 24 bits), and desString must keep the caller's lru.
+ * Then the fork-child route: in-process (rr_compat_test_as_child) and through a real fork whose
+ * child decodes every valid fixture through the parent's decode service.
  * Exit status 0 when every check passes.
  */
 #include <stdio.h>
 #include <string.h>
+#include <sys/wait.h>
+#include <unistd.h>
 
 #include "server.h"
 #include "rock_serdes_compat.h"
@@ -20,6 +24,60 @@
 
 static int fails;
 #define CHECK(c, ...) do { if (!(c)) { fails++; printf("FAIL %s: ", fx->name); printf(__VA_ARGS__); printf("\n"); } } while (0)
+
+/* Structural equality of two objects of the minimal Redis model (no serObject: a fork child
+ * must not touch the GPU the parent's encode would use). */
+static int sds_eq(sds a, sds b) { return sdslen(a) == sdslen(b) && !memcmp(a, b, sdslen(a)); }
+static int dict_eq(dict *a, dict *b, int vals) {
+    if (dictSize(a) != dictSize(b)) return 0;
+    dictIterator *it = dictGetIterator(a);
+    dictEntry *e;
+    int ok = 1;
+    while (ok && (e = dictNext(it))) {
+        dictEntry *f = dictFind(b, dictGetKey(e));
+        ok = f && (!vals || sds_eq(dictGetVal(e), dictGetVal(f)));
+    }
+    dictReleaseIterator(it);
+    return ok;
+}
+static int obj_eq(robj *a, robj *b) {
+    if (a->type != b->type || a->encoding != b->encoding || a->lru != b->lru) return 0;
+    switch (a->encoding) {
+        case OBJ_ENCODING_INT: return a->ptr == b->ptr;
+        case OBJ_ENCODING_RAW:
+        case OBJ_ENCODING_EMBSTR: return sds_eq(a->ptr, b->ptr);
+        case OBJ_ENCODING_ZIPLIST: {
+            const size_t l = ziplistBlobLen(a->ptr);
+            return l == ziplistBlobLen(b->ptr) && !memcmp(a->ptr, b->ptr, l);
+        }
+        case OBJ_ENCODING_INTSET: {
+            const intset *x = a->ptr, *y = b->ptr;
+            return x->encoding == y->encoding && x->length == y->length &&
+                   !memcmp(x->contents, y->contents, (size_t)x->encoding * x->length);
+        }
+        case OBJ_ENCODING_QUICKLIST: {
+            quicklistIter *i = quicklistGetIterator(a->ptr, AL_START_HEAD), *j = quicklistGetIterator(b->ptr, AL_START_HEAD);
+            quicklistEntry x, y;
+            int ok = 1, nx, ny;
+            while (ok && (nx = quicklistNext(i, &x)) & (ny = quicklistNext(j, &y)))
+                ok = (x.value == NULL) == (y.value == NULL) &&
+                     (x.value ? x.sz == y.sz && !memcmp(x.value, y.value, x.sz) : x.longval == y.longval);
+            ok = ok && !nx && !ny;
+            quicklistReleaseIterator(i);
+            quicklistReleaseIterator(j);
+            return ok;
+        }
+        case OBJ_ENCODING_HT: return dict_eq(a->ptr, b->ptr, a->type == OBJ_HASH);
+        case OBJ_ENCODING_SKIPLIST: {
+            const zset *x = a->ptr, *y = b->ptr;
+            if (x->zsl->length != y->zsl->length || !dict_eq(x->dict, y->dict, 0)) return 0;
+            for (zskiplistNode *n = x->zsl->header, *m = y->zsl->header; n || m; n = n->forward, m = m->forward)
+                if (!n || !m || n->score != m->score || !sds_eq(n->ele, m->ele)) return 0;
+            return 1;
+        }
+        default: return 0;
+    }
+}
 
 int main(void) {
     int checked = 0, panics = 0;
@@ -101,7 +159,29 @@ int main(void) {
     }
     fx = &FIXTURES[0];
     CHECK(child_panics == panics, "child route rejected %d malformed blobs, parent %d", child_panics, panics);
-    printf("compat shim: %d fixtures round-tripped, %d rejected with a panic, batch of %zu, child route %zu + %d; "
-           "%d failures\n", checked, panics, nok, nok, child_panics, fails);
+
+    /* a real fork (rock.c:536-538): the parent decodes every valid fixture on its GPU (its engine
+     * context exists), then forks; the child's desObject goes through the parent's decode
+     * service and must build the same objects.  The child leaves with _exit: it never touches
+     * the HIP runtime, not even through exit handlers. */
+    robj *pobj[N_FIXTURES];
+    for (size_t i = 0; i < nok; i++) pobj[i] = desObject(bufs[i], lens[i]);
+    fflush(stdout);
+    const pid_t pid = fork();
+    if (pid == 0) {
+        int bad = 0;
+        for (size_t i = 0; i < nok; i++) {
+            robj *o = desObject(bufs[i], lens[i]);
+            if (!obj_eq(o, pobj[i])) bad++;
+            decrRefCount(o);
+        }
+        _exit(bad ? 1 : 0);
+    }
+    int wst = -1;
+    CHECK(pid > 0 && waitpid(pid, &wst, 0) == pid, "fork / waitpid");
+    CHECK(WIFEXITED(wst) && WEXITSTATUS(wst) == 0, "forked child: decode differs or failed (wait status %d)", wst);
+    for (size_t i = 0; i < nok; i++) decrRefCount(pobj[i]);
+    printf("compat shim: %d fixtures round-tripped, %d rejected with a panic, batch of %zu, child route %zu + %d, "
+           "forked child %zu; %d failures\n", checked, panics, nok, nok, child_panics, nok, fails);
     return fails ? 1 : 0;
 }

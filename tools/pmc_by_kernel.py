@@ -17,7 +17,7 @@ for d in [a for a in sys.argv[1:] if a != "-a"]:
             tot[name][r["Counter_Name"]] += float(r["Counter_Value"])
             calls[(name, r["Counter_Name"])].add(r.get("Dispatch_Id", ""))
     for k, c in tot.items():
-        if not any(x in k for x in ("decode", "count", "scan", "enc_", "post")):
+        if not any(x in k for x in ("decode", "count", "scan", "enc_", "post", "snz")):
             continue
         bc, ia = c.get("SQ_LDS_BANK_CONFLICT", 0), c.get("SQ_LDS_IDX_ACTIVE", 0)
         line = f"{d.rstrip('/').split('/')[-1]:26s} {k:20s}"
