@@ -536,6 +536,9 @@ __device__ __forceinline__ bool do_list_g(const Src &R, const Lane &l, bool acti
 // HT_G_ROUNDS lanes hold keys (a hash's keys are its even members: G >= 8; a set: G >= 4 —
 // below that the batch runs do_ht).
 constexpr uint32_t HT_G_ROUNDS = 4;
+#ifndef RR_HT_ROT_LEAN   // 1: the duplicate test skips a hash's odd rotations and the RU masks
+#define RR_HT_ROT_LEAN 1
+#endif
 __device__ __forceinline__ uint32_t ht_group_min(bool hash) { return hash ? 2 * HT_FP_KEYS / HT_G_ROUNDS : HT_FP_KEYS / HT_G_ROUNDS; }
 template <class Src>
 __device__ __forceinline__ bool do_ht_g(const Src &R, const Head &H, const Lane &l, bool active, uint32_t G,
@@ -598,6 +601,20 @@ __device__ __forceinline__ bool do_ht_g(const Src &R, const Head &H, const Lane 
     for (uint32_t a = 0; a < HT_G_ROUNDS; ++a)
 #pragma unroll
         for (uint32_t b = a + 1; b < HT_G_ROUNDS; ++b) dup |= fpp[a] == fpp[b];
+#if RR_HT_ROT_LEAN
+    // A hash's keys are its even members and G is even, so only even lanes hold keys: an odd
+    // rotation pairs keys with non-keys and is skipped.  The fillers (top half 0xFFFF, unique per
+    // lane and round) match nothing, so the rounds past RU need no mask in the compares.
+#define RR_HT_ROT(D)                                                                                   \
+    if ((D) < G && (!hash || ((D) & 1) == 0)) {                                                        \
+        _Pragma("unroll") for (uint32_t q = 0; q < HT_G_ROUNDS; ++q) {                                 \
+            if (q < RU) {                                                                              \
+                const uint32_t x = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)fpp[q], 0x120 + (D), 0xF, 0xF, false); \
+                _Pragma("unroll") for (uint32_t qq = 0; qq < HT_G_ROUNDS; ++qq) dup |= fpp[qq] == x;   \
+            }                                                                                          \
+        }                                                                                              \
+    }
+#else
 #define RR_HT_ROT(D)                                                                                   \
     if ((D) < G) {                                                                                     \
         _Pragma("unroll") for (uint32_t q = 0; q < HT_G_ROUNDS; ++q) {                                 \
@@ -607,6 +624,7 @@ __device__ __forceinline__ bool do_ht_g(const Src &R, const Head &H, const Lane 
             }                                                                                          \
         }                                                                                              \
     }
+#endif
     RR_HT_ROT(1) RR_HT_ROT(2) RR_HT_ROT(3) RR_HT_ROT(4) RR_HT_ROT(5) RR_HT_ROT(6) RR_HT_ROT(7)
     RR_HT_ROT(8) RR_HT_ROT(9) RR_HT_ROT(10) RR_HT_ROT(11) RR_HT_ROT(12) RR_HT_ROT(13) RR_HT_ROT(14) RR_HT_ROT(15)
 #undef RR_HT_ROT
