@@ -102,6 +102,7 @@ struct GlbSrc {   // global memory through a buffer descriptor: reads past its r
     // the chain steps' reads: the dword / the byte at p (an aligned pair + alignbyte here)
     __device__ __forceinline__ uint32_t u32(uint32_t p) const { uint32_t x[1]; get<1>(p, x); return x[0]; }
     __device__ __forceinline__ uint32_t u8(uint32_t p) const { return u32(p) & 0xFF; }
+    __device__ __forceinline__ uint32_t u8b(uint32_t p) const { return u8(p); }
 };
 struct LdsSrc {   // the workgroup's staged window; reads may run up to 64 bytes past it
     lds_cptr S;
@@ -122,6 +123,8 @@ struct LdsSrc {   // the workgroup's staged window; reads may run up to 64 bytes
     // cycles, cfg 4 0.353 -> 0.392 ms; the LDS splits it.)
     __device__ __forceinline__ uint32_t u32(uint32_t p) const { uint32_t x[1]; get<1>(p, x); return x[0]; }
     __device__ __forceinline__ uint32_t u8(uint32_t p) const { return u32(p) & 0xFF; }
+    // the byte at p by a byte read (ds_read_u8: any address, no align step)
+    __device__ __forceinline__ uint32_t u8b(uint32_t p) const { return S[p]; }
 };
 
 __device__ __forceinline__ uint32_t ab(uint32_t hi, uint32_t lo, uint32_t s) { return __builtin_amdgcn_alignbyte(hi, lo, s); }
@@ -814,6 +817,9 @@ __device__ __forceinline__ bool do_ziplist(const Src &R, const Lane &l, bool act
 #define RR_ZL_U 1
 #endif
 constexpr uint32_t ZL_U = RR_ZL_U;
+#ifndef RR_ZL_U8   // 1: the pipelined ziplist chain reads a prevlen's first byte with a byte read (ZL batch 16.9K -> 16.3K cycles)
+#define RR_ZL_U8 1
+#endif
 template <class Src>
 __device__ __forceinline__ bool do_ziplist_bg(const Src &R, const Lane &l, bool active, uint32_t G, uint32_t g,
                                               uint32_t &n, uint64_t &pay) {
@@ -936,10 +942,18 @@ __device__ __forceinline__ bool do_ziplist_bp(const Src &R, const Lane &l, bool 
         me = zlast;
 #pragma unroll
         for (uint32_t j = 0; j < G; ++j) {
+#if RR_ZL_U8
+            // prevlen: its first byte by a byte read, the u32 of a 5-byte prevlen by a dword
+            // read issued beside it (off the common path's dependency chain)
+            const uint32_t b0 = R.u8b(p);
+            const uint32_t pb = R.u32(p + 1);
+            const uint32_t pl = b0 >= 254 ? pb : b0;
+#else
             uint32_t x[2];
             R.template get<2>(p, x);   // prevlen: 1 byte, or 0xFE + u32
             const uint32_t b0 = x[0] & 0xFF;
             const uint32_t pl = b0 >= 254 ? ab(x[1], x[0], 1) : b0;
+#endif
             const uint32_t pn = p - min(pl, p - first);
             mp = j == g ? p : mp;
             me = j == g ? expect : me;

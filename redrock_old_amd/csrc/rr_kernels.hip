@@ -508,6 +508,9 @@ __device__ __forceinline__ uint32_t ld_u32_al(const uint8_t *b, uint64_t p) {
     return __builtin_amdgcn_alignbyte(hi, lo, s);
 }
 
+#ifndef RR_COUNT_HOIST   // 1: count_kernel issues its offsets loads together, the header loads next
+#define RR_COUNT_HOIST 1
+#endif
 // reserve_g + classify_g from the header dwords (same results, byte for byte)
 __device__ __forceinline__ void reserve_classify(const uint8_t *b, uint64_t L, const uint32_t (&d)[6],
                                                  uint64_t &r, uint32_t &c) {
@@ -592,20 +595,36 @@ __global__ __launch_bounds__(256) void count_kernel(const uint8_t *__restrict__ 
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i > n) return;
     if (i == n) counts[n] = 0;   // (the scan writes the total here when there are values)
-    // first_val[w] = first value whose first byte is at or after w*win (windows past the
-    // last value start, and the sentinel nwin, get n)
+#if RR_COUNT_HOIST
+    // the three offsets in one round trip (loads at clamped indices, no guard branch whose join
+    // made the compiler wait for the first two before issuing the third), the header granules
+    // in the next, issued before the first_val stores
+    const uint64_t o_hi = offsets[i];
+    const uint64_t o_lo = offsets[i ? i - 1 : 0];
+    const uint64_t b1 = offsets[i < n ? i + 1 : n];
+    uint32_t d[6];
+    if (i < n) head24(blob, o_hi, b1, d);
+    const uint64_t w_lo = i == 0 ? 0 : o_lo / win + 1;
+#else
     const uint64_t o_hi = offsets[i];
     const uint64_t w_lo = i == 0 ? 0 : offsets[i - 1] / win + 1;
+#endif
+    // first_val[w] = first value whose first byte is at or after w*win (windows past the
+    // last value start, and the sentinel nwin, get n)
     const uint64_t w_hi = i == n ? nwin : o_hi / win;
     for (uint64_t w = w_lo; w <= w_hi && w <= nwin; ++w) first_val[w] = (uint32_t)i;
     if (i < n) {
+#if !RR_COUNT_HOIST
         const uint64_t b1 = offsets[i + 1];
+#endif
 #ifdef RR_COUNT_BYTES   // the byte-load formulation (diagnostics)
         counts[i] = reserve_g(blob + o_hi, b1 - o_hi);
         cls[i] = (uint8_t)classify_g(blob + o_hi, b1 - o_hi);
 #else
+#if !RR_COUNT_HOIST
         uint32_t d[6];
         head24(blob, o_hi, b1, d);
+#endif
         uint64_t r;
         uint32_t c;
         reserve_classify(blob + o_hi, b1 - o_hi, d, r, c);
@@ -1000,6 +1019,9 @@ __device__ __forceinline__ uint32_t class_vpb(uint32_t c) {
 #ifndef RR_DEC_WPE
 #define RR_DEC_WPE 4
 #endif
+#ifndef RR_DEC_ATOT   // 1: decode_kernel adds its windows' totals atomically (no fold in decode_post)
+#define RR_DEC_ATOT 1
+#endif
 #if RR_DEC_WPE > 0
 #define DEC_WPE_ATTR __attribute__((amdgpu_waves_per_eu(RR_DEC_WPE)))
 #else
@@ -1014,7 +1036,7 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
                                                               rr_value *__restrict__ values,
                                                               rr_elem *__restrict__ elems, uint64_t elem_cap,
                                                               uint8_t *__restrict__ arena, uint64_t *__restrict__ stats,
-                                                              uint64_t *fix, uint32_t nwin) {
+                                                              uint64_t *fix, uint32_t nwin, rr_totals *tot) {
     constexpr uint32_t NT = NW * RR_WAVE, STAGE = W + SLACK;
     static_assert(PMAX % NT == 0 && W % 16 == 0 && SLACK % 16 == 0, "tile shape");
 #ifndef RR_DEC_LDSPAD   // diagnostics: extra LDS per workgroup (e.g. to hold one workgroup per CU)
@@ -1506,9 +1528,19 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
     if (tid == 0) {
         uint64_t tb = 0, tp = 0;
         for (uint32_t w = 0; w < NW; ++w) { tb += red[0][w]; tp += red[1][w]; }
+#if RR_DEC_ATOT
+        // the window's {bad, payload} straight into the call's totals (zeroed by count_kernel):
+        // two non-returning atomics per window, ~7K per call spread over the kernel, so
+        // decode_post has no fold to do (7.3 -> 5.6 us)
+        (void)stats;
+        if (tot && tb) atomicAdd((unsigned long long *)&tot->n_bad, (unsigned long long)tb);
+        if (tot && tp) atomicAdd((unsigned long long *)&tot->payload, (unsigned long long)tp);
+#else
+        (void)tot;
         stats[3 * (uint64_t)tile + 0] = tb;
         stats[3 * (uint64_t)tile + 1] = tp;
         stats[3 * (uint64_t)tile + 2] = 0;
+#endif
         PROBE(prb[0] = pt1 - pt0; prb[1] = pt2 - pt1; prb[2] = __builtin_amdgcn_s_memtime() - pt2; prb[28] = v_hi - v_lo;
               prb[29] = staged; if (g_probe) for (uint32_t i = 0; i < PROBE_WORDS; ++i) g_probe[(uint64_t)tile * PROBE_WORDS + i] = prb[i];)
     }
@@ -2121,7 +2153,11 @@ __global__ __launch_bounds__(FIX_NT) void decode_post_kernel(const uint8_t *__re
                                                              uint32_t ntiles, const uint64_t *__restrict__ offsets,
                                                              uint64_t n, rr_totals *out) {
     fixup_values(blob, fix, values, elems, out);
+#if RR_DEC_ATOT   // (block 0 only: the bytes, the descriptor total and the error word)
+    if (out) fold_totals(stats, state, 0, offsets, n, 2, out, nullptr, fix + 1, 1);
+#else
     if (out) fold_totals(stats, state, ntiles, offsets, n, 2, out, nullptr, fix + 1, RR_POST_FOLD_BLOCKS);
+#endif
 }
 
 // ---------------------------------------------------------------------------------------- encode
@@ -3106,7 +3142,7 @@ extern "C" hipError_t rr_launch_decode(const uint8_t *blob, const uint64_t *offs
     const uint32_t grid = nw;
 #endif
     hipLaunchKernelGGL((DECODE_KERNEL), dim3(grid), dim3(DEC_NW * RR_WAVE), 0, stream, blob, data_cap, offsets, n,
-                       first_val, cls, counts, values, elems, elem_cap, arena, stats, fix, nw);
+                       first_val, cls, counts, values, elems, elem_cap, arena, stats, fix, nw, totals);
     static uint32_t post_grid = 0;
     if (!post_grid) post_grid = resident_grid(decode_post_kernel, FIX_NT, false);
     hipLaunchKernelGGL(decode_post_kernel, dim3(post_grid), dim3(FIX_NT), 0, stream, blob, fix, values, elems, stats,
