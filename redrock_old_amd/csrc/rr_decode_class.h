@@ -527,6 +527,55 @@ __device__ __forceinline__ bool do_list_g(const Src &R, const Lane &l, bool acti
     return group_any(fail, G, g);
 }
 
+// ---- List, grouped and SOFTWARE-PIPELINED: do_list_g with the group size a compile-time
+// constant, round r + 1's G chain steps issued in the same basic block as round r's element
+// decode (string2ll, checks, descriptor store), so the decode fills the chain's LDS-latency gaps
+// (as do_ziplist_bp).  The last round walks one wasted chain (clamped at the value's end).
+// Checks, stores and verdicts are do_list_g's.
+template <uint32_t G, class Src>
+__device__ __forceinline__ bool do_list_bp(const Src &R, const Lane &l, bool active, uint32_t g, uint32_t &n,
+                                           uint64_t &pay) {
+    const uint32_t end = l.q + l.L, r = active ? l.r : 0u;
+    uint32_t p = l.q + 5;
+    bool fail = active && r == 0 && p != end;
+    auto chain = [&](uint32_t &mp) __attribute__((always_inline)) {
+        mp = l.q;
+#pragma unroll
+        for (uint32_t j = 0; j < G; ++j) {
+            const uint32_t x = R.u32(p);
+            const uint32_t rem = end - p;
+            mp = j == g ? p : mp;
+            p = min(p + 4 + min(x, rem), end);
+        }
+    };
+    auto decode = [&](uint32_t mk, uint32_t mp) __attribute__((always_inline)) {
+        const bool mine = mk < r;
+        uint32_t b[6];
+        R.template get<6>(mp, b);
+        const uint32_t ml = b[0], rem = end - mp;
+        const bool bad = (rem < 4) | (ml > rem - 4) | ((mk + 1 == r) & (mp + 4 + ml != end));
+        fail |= mine & bad;
+        const uint32_t d[5] = {b[1], b[2], b[3], b[4], b[5]};
+        int64_t iv;
+        const bool isint = regs_try_int(d, ml, iv);
+        const bool st = mine & !bad;
+        put_desc(l.E, st ? l.slot(mk) : NOSLOT, isint ? (uint64_t)iv : l.B + mp + 4, isint ? 0 : ml,
+                 isint ? RR_K_INT : RR_K_STR, 0);
+        pay += st && !isint ? ml : 0;
+    };
+    uint32_t mpA;
+    chain(mpA);
+    for (uint32_t rounds = 0;; ++rounds) {
+        uint32_t mpB;
+        chain(mpB);                     // round + 1's chain ...
+        decode(rounds * G + g, mpA);    // ... beside round's element decode
+        if (__ballot((rounds + 1) * G < r) == 0) break;
+        mpA = mpB;
+    }
+    n = r;
+    return group_any(fail, G, g);
+}
+
 // ---- Set / Hash hash tables, grouped.  The chain steps read only the u64 length fields (every
 // lane of the group walks the same chain: a read, three checks and an add per member); lane g
 // takes members g, g + G, ...: once per G chain steps it stores its member's descriptor and,

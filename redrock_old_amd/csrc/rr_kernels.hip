@@ -508,6 +508,10 @@ __device__ __forceinline__ uint32_t ld_u32_al(const uint8_t *b, uint64_t p) {
     return __builtin_amdgcn_alignbyte(hi, lo, s);
 }
 
+typedef uint32_t u32_ua __attribute__((aligned(1)));   // unaligned dword (one global_load_dword)
+#ifndef RR_COUNT_UA   // 1: count_kernel's List chain reads each length field with one unaligned load
+#define RR_COUNT_UA 1     // (count 54.6 -> 52.5 us)
+#endif
 #ifndef RR_COUNT_HOIST   // 1: count_kernel issues its offsets loads together, the header loads next
 #define RR_COUNT_HOIST 1
 #endif
@@ -540,7 +544,11 @@ __device__ __forceinline__ void reserve_classify(const uint8_t *b, uint64_t L, c
 #endif
             while (p < L) {
                 if (L - p < 4) break;
+#if RR_COUNT_UA   // one unaligned dword load (gfx950 serves it from one line) instead of an aligned pair
+                const uint64_t l = *reinterpret_cast<const u32_ua *>(b + p);
+#else
                 const uint64_t l = ld_u32_al(b, p);
+#endif
                 if (l > L - p - 4) break;
                 ++n;
                 p += 4 + l;
@@ -820,8 +828,15 @@ constexpr uint32_t ZL_VPB = RR_ZL_VPB;
 #ifndef RR_HT_VPB
 #define RR_HT_VPB 16
 #endif
+#ifndef RR_LIST_PIPE   // 1: List batches run do_list_bp (compile-time group size, pipelined rounds)
+#define RR_LIST_PIPE 1     // (LIST batch 17.3K -> 12.1K cycles with 16 Lists per batch)
+#endif
 #ifndef RR_LIST_VPB   // Lists per batch (grouped: fewer Lists per batch, more lanes per List)
+#if RR_LIST_PIPE
+#define RR_LIST_VPB 16
+#else
 #define RR_LIST_VPB 64
+#endif
 #endif
 // class batch order: heaviest walks first (longest-job-first over the window's waves)
 #ifndef RR_DEC_ORDER
@@ -877,7 +892,15 @@ __device__ __forceinline__ Acc run_batch(const Src &src, uint32_t c, bool active
             ne = H.f9();
             enc = H.f5();
         } else if (c == C_LIST) {
+#if RR_LIST_PIPE   // grouped, software-pipelined (G a power of two)
+            if (G >= 16) fail = do_list_bp<16>(src, l, active, g, ne, vp);
+            else if (G >= 8) fail = do_list_bp<8>(src, l, active, g, ne, vp);
+            else if (G >= 4) fail = do_list_bp<4>(src, l, active, g, ne, vp);
+            else if (G >= 2) fail = do_list_bp<2>(src, l, active, g, ne, vp);
+            else fail = do_list_bp<1>(src, l, active, g, ne, vp);
+#else
             fail = do_list_g(src, l, active, G, g, ne, vp);
+#endif
         } else if (c == C_HT || c == C_HH) {   // grouped (G > 1) or lane per value (do_ht)
             if (G > 1) fail = do_ht_g(src, H, l, active, G, g, ne, vp, fixup, c == C_HH);
             else fail = do_ht(src, H, l, active, ne, vp, fixup, c == C_HH);
@@ -1430,7 +1453,7 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
 #endif
             // (hash tables: a power of two, so a value's lanes lie in one DPP row, do_ht_g)
             const uint32_t Gh = 1u << (31 - __builtin_clz(Gw));
-            const bool pow2 = htg || (RR_ZL_PIPE && c == C_ZL);   // (a ziplist batch's G: 4, 8 or 16)
+            const bool pow2 = htg || (RR_ZL_PIPE && c == C_ZL) || (RR_LIST_PIPE && c == C_LIST);   // (ziplists: G 4, 8 or 16)
             const uint32_t G = __builtin_amdgcn_readfirstlane((c == C_ZL && !RR_ZL_BACK) ? 2u : pow2 ? Gh : grouped ? Gw : 1u);
             const uint32_t li = lane / G, g = lane - li * G;   // the value's index in the batch
             const bool active = li < cnt;
@@ -1883,7 +1906,7 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_fused_kernel
             const bool htg = false;
 #endif
             const uint32_t Gh = 1u << (31 - __builtin_clz(Gw));
-            const bool pow2 = htg || (RR_ZL_PIPE && c == C_ZL);   // (a ziplist batch's G: 4, 8 or 16)
+            const bool pow2 = htg || (RR_ZL_PIPE && c == C_ZL) || (RR_LIST_PIPE && c == C_LIST);   // (ziplists: G 4, 8 or 16)
             const uint32_t G = __builtin_amdgcn_readfirstlane((c == C_ZL && !RR_ZL_BACK) ? 2u : pow2 ? Gh : grouped ? Gw : 1u);
             const uint32_t li = lane / G, g = lane - li * G;
             const bool active = li < bcnt;
