@@ -465,7 +465,7 @@ def measured_traffic(config, n, nb):
         try:
             with open(p) as f:
                 d = json.load(f)
-            w = d.get("workload", {})
+            w = d.get("workload") or {}
             if (w.get("config"), w.get("n"), w.get("blob_bytes")) == (config, n, nb) and d.get("traffic_bytes_per_call"):
                 return int(d["traffic_bytes_per_call"])
         except (OSError, ValueError):

@@ -18,8 +18,4 @@ python3 tools/traffic_summary.py $E/enc $E/${R}_encode_summary.json > /dev/null
 cp $E/${R}_decode_summary.json profiles/${R}_decode_summary.json
 bash tools/pmc_decode.sh $E/pmc 4 && echo "pmc done"
 python3 tools/pmc_summary.py $E/pmc > $E/${R}_decode_pmc.txt 2>&1 || true
-timeout -k 10 600 python3 -u bench.py > $E/bench.log 2>&1 && echo "bench done"
-grep '^{' $E/bench.log | tail -1 > $E/${R}_bench.json
-timeout -k 10 600 python3 -u bench.py --n 10000000 --steps 10 --warmup 2 --no-cpu --no-split --no-snappy > $E/bench10m.log 2>&1 && echo "bench 10m done"
-grep '^{' $E/bench10m.log | tail -1 > $E/${R}_bench_10m.json
-cat $E/${R}_bench.json
+bash tools/bench_lines.sh $R

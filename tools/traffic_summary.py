@@ -46,10 +46,16 @@ for k in pipeline:
         res["kernels"].setdefault(k, {}).update({"fetch_bytes": f, "write_bytes": w, "hbm_bytes": 2 * f + w})
         tot += 2 * f + w
 res["traffic_bytes_per_call"] = tot if per else None
-if os.path.exists(out):   # keep the workload tag bench.py matches the summary by
+# the workload tag bench.py matches the summary by (profile_bench.sh's default workload: the
+# bench line's 1M-value config-4 batch); an existing tag in OUT is kept
+wl = {"config": 4, "n": 1000000, "blob_bytes": 497270349,
+      "command": ("bench.py --profile-encode" if "enc_emit_kernel" in per else "bench.py --profile-only") +
+                 " (rocprofv3 --kernel-trace --stats; --pmc FETCH_SIZE; --pmc WRITE_SIZE)"}
+if os.path.exists(out):
     try:
-        res.setdefault("workload", json.load(open(out)).get("workload"))
+        wl = json.load(open(out)).get("workload") or wl
     except ValueError:
         pass
+res["workload"] = wl
 json.dump(res, open(out, "w"), indent=1)
 print(json.dumps(res, indent=1))
