@@ -2335,10 +2335,19 @@ __device__ __forceinline__ ElemCost task_cost(uint32_t type, uint32_t enc, uint6
     }
 }
 // two block-wide exclusive scans sharing one barrier (ws: [2][NT / RR_WAVE])
+#ifndef RR_ENC_SIZE_DPP   // 1: E1's per-round wave scans in DPP (u32) when no lane's cost reaches 2^26
+#define RR_ENC_SIZE_DPP 1
+#endif
 template <uint32_t NT>
 __device__ __forceinline__ void block_excl_scan2(uint64_t x, uint64_t y, uint64_t (*ws)[NT / RR_WAVE], uint64_t &ex,
                                                  uint64_t &ey, uint64_t &tx, uint64_t &ty) {
+#if RR_ENC_SIZE_DPP   // (64 lanes below 2^26 each: the wave's sums fit 32 bits; else the u64 shuffles)
+    const bool small = __ballot((x | y) >= (1ull << 26)) == 0;
+    const uint64_t ix = small ? (uint64_t)wave_incl_scan_u32((uint32_t)x) : wave_incl_scan(x);
+    const uint64_t iy = small ? (uint64_t)wave_incl_scan_u32((uint32_t)y) : wave_incl_scan(y);
+#else
     const uint64_t ix = wave_incl_scan(x), iy = wave_incl_scan(y);
+#endif
     const uint32_t wv = threadIdx.x / RR_WAVE;
     if (lane_id() == RR_WAVE - 1) { ws[0][wv] = ix; ws[1][wv] = iy; }
     lds_barrier();
@@ -2364,8 +2373,23 @@ __device__ __forceinline__ void block_excl_scan2(uint64_t x, uint64_t y, uint64_
 #define RR_ENC_SHORT 4
 #endif
 constexpr uint32_t ENC_SHORT = RR_ENC_SHORT;
+#ifndef RR_ENC_SIZE_SEG   // 1: E1 sums a value's task costs by wave-segmented LDS atomics (no per-round barrier)
+#define RR_ENC_SIZE_SEG 1
+#endif
+#ifndef RR_ENC_SIZE_MAP   // 1: E1 maps tasks to values through an LDS map (blocks of <= ENC_MAPCAP tasks)
+#define RR_ENC_SIZE_MAP 1
+#endif
+constexpr uint32_t ENC_MAPCAP = 4096;
+#ifndef RR_ENC_SIZE_WPE   // waves per SIMD E1 is built for (0: the compiler's choice)
+#define RR_ENC_SIZE_WPE 0
+#endif
+#if RR_ENC_SIZE_WPE > 0
+#define ENC_SIZE_WPE_ATTR __attribute__((amdgpu_waves_per_eu(RR_ENC_SIZE_WPE)))
+#else
+#define ENC_SIZE_WPE_ATTR
+#endif
 template <uint32_t NT, uint32_t U>
-__global__ __launch_bounds__(NT) void enc_size_kernel(const rr_value *__restrict__ values,
+__global__ __launch_bounds__(NT) ENC_SIZE_WPE_ATTR void enc_size_kernel(const rr_value *__restrict__ values,
                                                       const rr_elem *__restrict__ elems, uint64_t n,
                                                       uint64_t ecap, uint64_t acap,
                                                       uint64_t *__restrict__ sizes, uint64_t *__restrict__ stats,
@@ -2376,6 +2400,17 @@ __global__ __launch_bounds__(NT) void enc_size_kernel(const rr_value *__restrict
     __shared__ uint64_t s_b0[NT], s_b1[NT], s_p0[NT], s_p1[NT];   // byte / payload scans at the first task, after the last
     __shared__ uint64_t ws0[NT / RR_WAVE], ws[2][2][NT / RR_WAVE];
     __shared__ uint64_t red[3][NT / RR_WAVE];
+#if RR_ENC_SIZE_MAP
+    // task -> value map of the block (the value's index at each of its tasks), when the block
+    // has at most ENC_MAPCAP tasks: one LDS read per task instead of a binary search of the task
+    // bases.  Built as heads (value j at its first task) and a running max: heads increase along
+    // the map, so the zeros between them never win.
+    static_assert(NT <= 256 && ENC_MAPCAP == 16 * NT, "u8 map, 16 bytes per thread");
+    __shared__ __attribute__((aligned(16))) uint8_t tmap[ENC_MAPCAP];
+    __shared__ uint32_t wmax[NT / RR_WAVE];
+    reinterpret_cast<uint4 *>(tmap)[threadIdx.x] = make_uint4(0, 0, 0, 0);   // (ordered before the
+                                                                             // heads by the scan's barrier)
+#endif
     const uint32_t tid = threadIdx.x;
     const uint64_t v = (uint64_t)blockIdx.x * NT + tid;
     uint32_t type = 0, enc = 0, ntask = 0, hdr = 0, bad = 0;
@@ -2436,12 +2471,46 @@ __global__ __launch_bounds__(NT) void enc_size_kernel(const rr_value *__restrict
     const uint32_t base = (uint32_t)block_excl_scan<NT>(ntask, ws0, TT);
     tb[tid] = base;
     if (tid == NT - 1) tb[NT] = base + ntask;
+#if RR_ENC_SIZE_MAP
+    const bool usemap = TT <= ENC_MAPCAP;   // (block-uniform)
+    if (usemap && ntask) tmap[base] = (uint8_t)tid;   // the head of the value's task run
     lds_barrier();
+    if (usemap && TT) {
+        // fill the runs: a running max over the map (heads increase along it), 16 positions a
+        // thread, the carry across threads by a DPP max scan and the waves' maxima in LDS
+        uint4 q = reinterpret_cast<uint4 *>(tmap)[tid];
+        uint32_t w[4] = {q.x, q.y, q.z, q.w}, m = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < 16; ++k) m = max(m, (w[k >> 2] >> (8 * (k & 3))) & 0xFF);
+        const uint32_t im = wave_incl_max_u32(m);
+        if (lane_id() == RR_WAVE - 1) wmax[tid / RR_WAVE] = im;
+        lds_barrier();
+        uint32_t carry = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < NT / RR_WAVE; ++k) carry = k < tid / RR_WAVE ? max(carry, wmax[k]) : carry;
+        const uint32_t prev = __shfl_up(im, 1, RR_WAVE);
+        carry = max(carry, lane_id() ? prev : 0u);
+#pragma unroll
+        for (uint32_t k = 0; k < 16; ++k) {
+            const uint32_t b = (w[k >> 2] >> (8 * (k & 3))) & 0xFF;
+            carry = max(carry, b);
+            w[k >> 2] = (w[k >> 2] & ~(0xFFu << (8 * (k & 3)))) | (carry << (8 * (k & 3)));
+        }
+        reinterpret_cast<uint4 *>(tmap)[tid] = make_uint4(w[0], w[1], w[2], w[3]);
+        lds_barrier();
+    }
+#else
+    lds_barrier();
+#endif
     auto fetch = [&](uint64_t t, uint32_t &pj, ElemV &pe) {
         pj = 0;
         pe = ElemV{0, 0, 0};
         if (t < TT) {
             uint32_t lo = 0;
+#if RR_ENC_SIZE_MAP
+            if (usemap) lo = tmap[t];
+            else
+#endif
 #pragma unroll
             for (uint32_t s = NT / 2; s > 0; s >>= 1)
                 if (tb[lo + s] <= t) lo += s;
@@ -2468,6 +2537,29 @@ __global__ __launch_bounds__(NT) void enc_size_kernel(const rr_value *__restrict
                 const uint32_t te = s_te[j[u]];
                 c = task_cost(te & 0xFF, te >> 8, k, e[u], acap);
             }
+#if RR_ENC_SIZE_SEG
+            // wave-segmented sums, no block barrier per round: a wave's tasks run over a few
+            // values in order; each value's run in the wave adds (inclusive scan at its last
+            // task) - (exclusive scan at its first task) to the value's sums with two LDS atomics
+            (void)k;
+            const bool small = __ballot((c.bytes | c.pay) >= (1ull << 26)) == 0;
+            const uint64_t ib = small ? (uint64_t)wave_incl_scan_u32((uint32_t)c.bytes) : wave_incl_scan(c.bytes);
+            const uint64_t ip = small ? (uint64_t)wave_incl_scan_u32((uint32_t)c.pay) : wave_incl_scan(c.pay);
+            const uint32_t jp = __shfl_up(j[u], 1, RR_WAVE), jn = __shfl_down(j[u], 1, RR_WAVE);
+            const uint32_t ln = lane_id();
+            const bool first = act && (ln == 0 || jp != j[u]);
+            const bool last = act && (ln == RR_WAVE - 1 || t + 1 >= TT || jn != j[u]);
+            if (first) {
+                atomicAdd((unsigned long long *)&s_b1[j[u]], (unsigned long long)(0ull - (ib - c.bytes)));
+                atomicAdd((unsigned long long *)&s_p1[j[u]], (unsigned long long)(0ull - (ip - c.pay)));
+            }
+            if (last) {
+                atomicAdd((unsigned long long *)&s_b1[j[u]], (unsigned long long)ib);
+                atomicAdd((unsigned long long *)&s_p1[j[u]], (unsigned long long)ip);
+            }
+            if (act && c.bad) s_bad[j[u]] = 1;
+            (void)par; (void)runb; (void)runp; (void)ws;
+#else
             uint64_t exb, exp, tb_, tp_;
             block_excl_scan2<NT>(c.bytes, c.pay, ws[par], exb, exp, tb_, tp_);
             par ^= 1;
@@ -2478,6 +2570,7 @@ __global__ __launch_bounds__(NT) void enc_size_kernel(const rr_value *__restrict
             }
             runb += tb_;
             runp += tp_;
+#endif
         }
     }
     lds_barrier();
