@@ -2373,6 +2373,9 @@ __device__ __forceinline__ void block_excl_scan2(uint64_t x, uint64_t y, uint64_
 #define RR_ENC_SHORT 4
 #endif
 constexpr uint32_t ENC_SHORT = RR_ENC_SHORT;
+#ifndef RR_ENC_SIZE_PF   // descriptor lines of a long value prefetched by E1 before its task rounds
+#define RR_ENC_SIZE_PF 0
+#endif
 #ifndef RR_ENC_SIZE_SEG   // 1: E1 sums a value's task costs by wave-segmented LDS atomics (no per-round barrier)
 #define RR_ENC_SIZE_SEG 1
 #endif
@@ -2461,6 +2464,18 @@ __global__ __launch_bounds__(NT) ENC_SIZE_WPE_ATTR void enc_size_kernel(const rr
         }
         ntask = 0;
     }
+#if RR_ENC_SIZE_PF
+    // a long value's lane requests the first RR_ENC_SIZE_PF 64-byte lines of its descriptors
+    // while the short values' lanes load theirs, so the task rounds' loads later hit the L2
+    // (the OR keeps the loads; it is consumed once, after the rounds)
+    uint32_t pfacc = 0;
+    if (ntask > ENC_SHORT) {
+        const uint32_t *d = reinterpret_cast<const uint32_t *>(elems + eb);
+        const uint32_t lines = (uint32_t)((ne + 3) / 4);   // 4 descriptors per 64-byte line
+#pragma unroll
+        for (uint32_t k = 0; k < RR_ENC_SIZE_PF; ++k) pfacc |= d[16 * (k < lines ? k : lines - 1)];
+    }
+#endif
     s_el[tid] = (uint32_t)eb;
     s_te[tid] = type | (enc << 8);
     s_bad[tid] = bad;
@@ -2574,6 +2589,9 @@ __global__ __launch_bounds__(NT) ENC_SIZE_WPE_ATTR void enc_size_kernel(const rr
         }
     }
     lds_barrier();
+#if RR_ENC_SIZE_PF
+    asm volatile("" ::"v"(pfacc));
+#endif
     uint64_t size = 0, pay = 0;
     if (v < n) {
         bad = s_bad[tid];
