@@ -1955,9 +1955,16 @@ __device__ __forceinline__ ElemV get_elem(const rr_elem *e) {
     return ElemV{(uint64_t)w.x | ((uint64_t)w.y << 32), w.z, w.w & 0xFF};
 }
 
+#ifndef RR_SCAN_DPP   // 1: block_excl_scan's wave scan in DPP (u32) when no lane's value reaches 2^26
+#define RR_SCAN_DPP 1
+#endif
 template <uint32_t NT>
 __device__ __forceinline__ uint64_t block_excl_scan(uint64_t x, uint64_t *wsum, uint64_t &total) {
+#if RR_SCAN_DPP   // (64 lanes below 2^26 each: the wave's sum fits 32 bits; else the u64 shuffles)
+    const uint64_t incl = __ballot(x >= (1ull << 26)) == 0 ? (uint64_t)wave_incl_scan_u32((uint32_t)x) : wave_incl_scan(x);
+#else
     const uint64_t incl = wave_incl_scan(x);
+#endif
     const uint32_t wv = threadIdx.x / RR_WAVE;
     if (lane_id() == RR_WAVE - 1) wsum[wv] = incl;
     lds_barrier();
@@ -2383,6 +2390,43 @@ constexpr uint32_t ENC_SHORT = RR_ENC_SHORT;
 #define RR_ENC_SIZE_MAP 1
 #endif
 constexpr uint32_t ENC_MAPCAP = 4096;
+// Task -> value map of a round of NT values (the value's index at each of its tasks, u8), from
+// the task bases: the value with tasks writes its index at its first task (the head), then a
+// running max fills the runs — heads increase along the map, so the zeros between them (the map
+// was zeroed beforehand, ordered by a barrier) never win: 16 positions a thread, the carry across
+// threads by a DPP max scan and the waves' maxima in LDS.  Returns whether the round's tt tasks
+// fit the map (block-uniform); ends with an LDS barrier either way.
+template <uint32_t NT>
+__device__ __forceinline__ bool build_task_map(uint8_t *tmap, uint32_t *wmax, uint32_t base, uint32_t ntask,
+                                               uint64_t tt) {
+    static_assert(NT <= 256 && ENC_MAPCAP == 16 * NT, "u8 map, 16 bytes per thread");
+    const uint32_t tid = threadIdx.x;
+    const bool usemap = tt <= ENC_MAPCAP;
+    if (usemap && ntask) tmap[base] = (uint8_t)tid;
+    lds_barrier();
+    if (usemap && tt) {
+        const uint4 q = reinterpret_cast<uint4 *>(tmap)[tid];
+        uint32_t w[4] = {q.x, q.y, q.z, q.w}, m = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < 16; ++k) m = max(m, (w[k >> 2] >> (8 * (k & 3))) & 0xFF);
+        const uint32_t im = wave_incl_max_u32(m);
+        if (lane_id() == RR_WAVE - 1) wmax[tid / RR_WAVE] = im;
+        lds_barrier();
+        uint32_t carry = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < NT / RR_WAVE; ++k) carry = k < tid / RR_WAVE ? max(carry, wmax[k]) : carry;
+        const uint32_t prev = __shfl_up(im, 1, RR_WAVE);
+        carry = max(carry, lane_id() ? prev : 0u);
+#pragma unroll
+        for (uint32_t k = 0; k < 16; ++k) {
+            carry = max(carry, (w[k >> 2] >> (8 * (k & 3))) & 0xFF);
+            w[k >> 2] = (w[k >> 2] & ~(0xFFu << (8 * (k & 3)))) | (carry << (8 * (k & 3)));
+        }
+        reinterpret_cast<uint4 *>(tmap)[tid] = make_uint4(w[0], w[1], w[2], w[3]);
+        lds_barrier();
+    }
+    return usemap;
+}
 #ifndef RR_ENC_SIZE_WPE   // waves per SIMD E1 is built for (0: the compiler's choice)
 #define RR_ENC_SIZE_WPE 0
 #endif
@@ -2404,11 +2448,8 @@ __global__ __launch_bounds__(NT) ENC_SIZE_WPE_ATTR void enc_size_kernel(const rr
     __shared__ uint64_t ws0[NT / RR_WAVE], ws[2][2][NT / RR_WAVE];
     __shared__ uint64_t red[3][NT / RR_WAVE];
 #if RR_ENC_SIZE_MAP
-    // task -> value map of the block (the value's index at each of its tasks), when the block
-    // has at most ENC_MAPCAP tasks: one LDS read per task instead of a binary search of the task
-    // bases.  Built as heads (value j at its first task) and a running max: heads increase along
-    // the map, so the zeros between them never win.
-    static_assert(NT <= 256 && ENC_MAPCAP == 16 * NT, "u8 map, 16 bytes per thread");
+    // task -> value map of the block when it has at most ENC_MAPCAP tasks (build_task_map): one
+    // LDS read per task instead of a binary search of the task bases
     __shared__ __attribute__((aligned(16))) uint8_t tmap[ENC_MAPCAP];
     __shared__ uint32_t wmax[NT / RR_WAVE];
     reinterpret_cast<uint4 *>(tmap)[threadIdx.x] = make_uint4(0, 0, 0, 0);   // (ordered before the
@@ -2487,33 +2528,7 @@ __global__ __launch_bounds__(NT) ENC_SIZE_WPE_ATTR void enc_size_kernel(const rr
     tb[tid] = base;
     if (tid == NT - 1) tb[NT] = base + ntask;
 #if RR_ENC_SIZE_MAP
-    const bool usemap = TT <= ENC_MAPCAP;   // (block-uniform)
-    if (usemap && ntask) tmap[base] = (uint8_t)tid;   // the head of the value's task run
-    lds_barrier();
-    if (usemap && TT) {
-        // fill the runs: a running max over the map (heads increase along it), 16 positions a
-        // thread, the carry across threads by a DPP max scan and the waves' maxima in LDS
-        uint4 q = reinterpret_cast<uint4 *>(tmap)[tid];
-        uint32_t w[4] = {q.x, q.y, q.z, q.w}, m = 0;
-#pragma unroll
-        for (uint32_t k = 0; k < 16; ++k) m = max(m, (w[k >> 2] >> (8 * (k & 3))) & 0xFF);
-        const uint32_t im = wave_incl_max_u32(m);
-        if (lane_id() == RR_WAVE - 1) wmax[tid / RR_WAVE] = im;
-        lds_barrier();
-        uint32_t carry = 0;
-#pragma unroll
-        for (uint32_t k = 0; k < NT / RR_WAVE; ++k) carry = k < tid / RR_WAVE ? max(carry, wmax[k]) : carry;
-        const uint32_t prev = __shfl_up(im, 1, RR_WAVE);
-        carry = max(carry, lane_id() ? prev : 0u);
-#pragma unroll
-        for (uint32_t k = 0; k < 16; ++k) {
-            const uint32_t b = (w[k >> 2] >> (8 * (k & 3))) & 0xFF;
-            carry = max(carry, b);
-            w[k >> 2] = (w[k >> 2] & ~(0xFFu << (8 * (k & 3)))) | (carry << (8 * (k & 3)));
-        }
-        reinterpret_cast<uint4 *>(tmap)[tid] = make_uint4(w[0], w[1], w[2], w[3]);
-        lds_barrier();
-    }
+    const bool usemap = build_task_map<NT>(tmap, wmax, base, ntask, TT);
 #else
     lds_barrier();
 #endif
@@ -2673,6 +2688,9 @@ __device__ __forceinline__ uint64_t rr_stamp() {
 
 #ifndef RR_ENC_TPF
 #define RR_ENC_TPF 1
+#endif
+#ifndef RR_ENC_EMIT_MAP   // 1: E4 maps tasks to values through an LDS map (build_task_map)
+#define RR_ENC_EMIT_MAP 0   // (measured: E4 +2 %, its 4 KiB more LDS per workgroup)
 #endif
 
 // ---- E4: window emission -------------------------------------------------------------------
@@ -2902,6 +2920,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(RR_ENC_WPE))
     __shared__ uint64_t sh_nrp;            // runs reserved | pieces reserved << 32
     __shared__ uint32_t sh_pend;           // pieces of the queued runs, when the queue overflowed
     __shared__ uint32_t sh_unal;           // some queued run is not aligned with its image offset mod 16
+#if RR_ENC_EMIT_MAP   // task -> value map of a value round (build_task_map)
+    __shared__ __attribute__((aligned(16))) uint8_t tmap[ENC_MAPCAP];
+    __shared__ uint32_t wmax[NT / RR_WAVE];
+#endif
     uint8_t *img = reinterpret_cast<uint8_t *>(img4);
     const uint32_t tid = threadIdx.x;
     const uint64_t total = offsets[n];
@@ -2955,6 +2977,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(RR_ENC_WPE))
     for (uint64_t vb = v0; vb < vend; vb += NT) {
         const uint64_t v = vb + tid;
         uint32_t tasks = 0;
+#if RR_ENC_EMIT_MAP   // (the previous round's last reads of the map are behind its closing barrier)
+        reinterpret_cast<uint4 *>(tmap)[tid] = make_uint4(0, 0, 0, 0);
+#endif
         if (v < vend) {
             const uint64_t a = offsets[v], b = offsets[v + 1];
             const uint4 x = reinterpret_cast<const uint4 *>(values)[v];
@@ -2980,7 +3005,11 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(RR_ENC_WPE))
         const uint32_t base = (uint32_t)block_excl_scan<NT>(tasks, wsum[0], tt);
         tb[tid] = base;
         if (tid == NT - 1) tb[NT] = base + tasks;
+#if RR_ENC_EMIT_MAP
+        const bool usemap = build_task_map<NT>(tmap, wmax, base, tasks, tt);
+#else
         lds_barrier();
+#endif
         EPROBE(const uint64_t eth = rr_stamp(); ent += tt;)
         uint64_t run = 0;   // element bytes of the earlier task rounds
         // task rounds in groups of TPF: every round's descriptor is loaded up front, so a
@@ -2991,6 +3020,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(RR_ENC_WPE))
             if (t < tt) {
                 // last value j with tb[j] <= t
                 uint32_t lo = 0;
+#if RR_ENC_EMIT_MAP
+                if (usemap) lo = tmap[t];
+                else
+#endif
 #pragma unroll
                 for (uint32_t s = NT / 2; s > 0; s >>= 1)
                     if (tb[lo + s] <= t) lo += s;
