@@ -129,6 +129,17 @@ __device__ __forceinline__ uint64_t wave_sum(uint64_t x) {
     for (int d = RR_WAVE / 2; d > 0; d >>= 1) x += __shfl_xor(x, d, RR_WAVE);
     return x;
 }
+// wave_sum (every lane active) by the DPP scan and one readlane when no lane reaches 2^26 (the
+// sum then fits 32 bits): six VALU ops instead of twelve ds_bpermute round trips
+__device__ __forceinline__ uint64_t wave_sum_fast(uint64_t x) {
+    if (__ballot(x >= (1ull << 26)) == 0)
+        return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan_u32((uint32_t)x), RR_WAVE - 1);
+    return wave_sum(x);
+}
+// inclusive scan (every lane active): DPP u32 when no lane reaches 2^26, else the shuffles
+__device__ __forceinline__ uint64_t wave_incl_scan_fast(uint64_t x) {
+    return __ballot(x >= (1ull << 26)) == 0 ? (uint64_t)wave_incl_scan_u32((uint32_t)x) : wave_incl_scan(x);
+}
 
 // ---- decoupled look-back (single-pass scan across wave tiles) ---------------------------
 // One 8-byte word per tile: bits 62-63 flag (0 empty, 1 aggregate, 2 inclusive prefix),

@@ -724,7 +724,7 @@ __global__ __launch_bounds__(256) void scan_kernel(uint64_t *__restrict__ counts
         x[k] = base + k < n ? counts[base + k] : 0;
         sum += x[k];
     }
-    const uint64_t incl = wave_incl_scan(sum);
+    const uint64_t incl = wave_incl_scan_fast(sum);
     const uint32_t w = threadIdx.x / RR_WAVE;
     if (lane_id() == RR_WAVE - 1) wsum[w] = incl;
     __syncthreads();
@@ -1394,7 +1394,7 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
                 if (m) {
                     uint32_t at = 0;
                     if (lane == 0) at = atomicAdd(&ccur[c], (uint32_t)__popcll(m));
-                    at = __shfl(at, 0, RR_WAVE);
+                    at = __builtin_amdgcn_readfirstlane(at);   // (lane 0 took the atomic)
                     if (myc[j] == c) perm[cbase[c] + at + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = (uint16_t)i;
                 }
             }
@@ -1421,7 +1421,7 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
         for (;;) {
             uint32_t bi = 0;
             if (lane == 0) bi = atomicAdd(&next_batch, 1u);
-            bi = __builtin_amdgcn_readfirstlane(__shfl(bi, 0, RR_WAVE));
+            bi = __builtin_amdgcn_readfirstlane(bi);
             if (bi >= nb) break;
             uint32_t k = 0;
             while (bi >= bpre[k + 1]) ++k;
@@ -1496,7 +1496,7 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
             for (;;) {
                 uint32_t ti = 0;
                 if (lane == 0) ti = atomicAdd(&next_copy, 1u);
-                ti = __builtin_amdgcn_readfirstlane(__shfl(ti, 0, RR_WAVE));
+                ti = __builtin_amdgcn_readfirstlane(ti);
                 if (ti >= ntask) break;
                 u32x4 x[4];
 #pragma unroll
@@ -1527,7 +1527,7 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
         for (;;) {
             uint32_t ti = 0;
             if (lane == 0) ti = atomicAdd(&next_copy, 1u);
-            ti = __builtin_amdgcn_readfirstlane(__shfl(ti, 0, RR_WAVE));
+            ti = __builtin_amdgcn_readfirstlane(ti);
             if (ti >= ntask) break;
             const uint64_t g0 = cw0 + (uint64_t)ti * TASK + lane;
             u32x4 x[4];
@@ -1544,8 +1544,8 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
         }
     }
 #endif
-    bad = wave_sum(bad);
-    pay = wave_sum(pay);
+    bad = wave_sum_fast(bad);
+    pay = wave_sum_fast(pay);
     if (lane == 0) { red[0][wave] = bad; red[1][wave] = pay; }
     DEC_SYNC();
     if (tid == 0) {
@@ -1859,7 +1859,7 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_fused_kernel
                 if (m) {
                     uint32_t at = 0;
                     if (lane == 0) at = atomicAdd(&ccur[c], (uint32_t)__popcll(m));
-                    at = __shfl(at, 0, RR_WAVE);
+                    at = __builtin_amdgcn_readfirstlane(at);   // (lane 0 took the atomic)
                     if (myc == c) perm[cbase[c] + at + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = (uint16_t)tid;
                 }
             }
@@ -1889,7 +1889,7 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_fused_kernel
         for (;;) {
             uint32_t bi = 0;
             if (lane == 0) bi = atomicAdd(&next_batch, 1u);
-            bi = __builtin_amdgcn_readfirstlane(__shfl(bi, 0, RR_WAVE));
+            bi = __builtin_amdgcn_readfirstlane(bi);
             if (bi >= nb) break;
             uint32_t k = 0;
             while (bi >= bpre[k + 1]) ++k;
@@ -1930,8 +1930,8 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_fused_kernel
         const uint64_t pre = lb_resolve(lb_state, lb_groups, tile, nwin, agg, fix + 1);
         if (lane == 0 && tile == nwin - 1) *total = pre + agg;
     }
-    bad = wave_sum(bad);
-    pay = wave_sum(pay);
+    bad = wave_sum_fast(bad);
+    pay = wave_sum_fast(pay);
     if (lane == 0) { red[0][wave] = bad; red[1][wave] = pay; }
     DEC_SYNC();
     if (tid == 0) {
@@ -2614,7 +2614,7 @@ __global__ __launch_bounds__(NT) ENC_SIZE_WPE_ATTR void enc_size_kernel(const rr
         pay = bad ? 0 : s_p1[tid] - s_p0[tid];
         sizes[v] = size;
     }
-    uint64_t sb = wave_sum(bad), sp = wave_sum(pay), sn = wave_sum(ne);
+    uint64_t sb = wave_sum_fast(bad), sp = wave_sum_fast(pay), sn = wave_sum_fast(ne);
     const uint32_t wv = tid / RR_WAVE;
     if (lane_id() == 0) { red[0][wv] = sb; red[1][wv] = sp; red[2][wv] = sn; }
     __syncthreads();
@@ -2655,8 +2655,8 @@ __global__ __launch_bounds__(256) void enc_index_kernel(const rr_value *__restri
             }
         }
     }
-    bad = wave_sum(bad);
-    pay = wave_sum(pay);
+    bad = wave_sum_fast(bad);
+    pay = wave_sum_fast(pay);
     const uint32_t wv = threadIdx.x / RR_WAVE;
     if (lane_id() == 0) { red[0][wv] = bad; red[1][wv] = pay; }
     __syncthreads();
@@ -2954,8 +2954,11 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(RR_ENC_WPE))
         const bool queued = want && src + l <= JQ_SRC;
         const uint32_t np = queued ? ((dst + l - 1) >> 6) - (dst >> 6) + 1 : 0;
         const uint64_t mine = queued ? (1ull | ((uint64_t)np << 32)) : 0;
-        const uint64_t incl = wave_incl_scan(mine);
-        const uint64_t wtot = __shfl(incl, RR_WAVE - 1, RR_WAVE);
+        // (the two 32-bit fields scanned apart in DPP: a wave's runs and pieces stay far below 2^32)
+        const uint64_t incl = (uint64_t)wave_incl_scan_u32(queued ? 1u : 0u) |
+                              ((uint64_t)wave_incl_scan_u32(queued ? np : 0u) << 32);
+        const uint64_t wtot = ((uint64_t)__builtin_amdgcn_readlane((int)(uint32_t)(incl >> 32), RR_WAVE - 1) << 32) |
+                              (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)incl, RR_WAVE - 1);
         uint64_t base = 0;
         if (wtot && lane_id() == RR_WAVE - 1) base = atomicAdd((unsigned long long *)&sh_nrp, (unsigned long long)wtot);
         base = __shfl(base, RR_WAVE - 1, RR_WAVE);
