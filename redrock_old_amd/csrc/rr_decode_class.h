@@ -718,8 +718,7 @@ __device__ __forceinline__ bool do_skiplist_g(const Src &R, const Head &H, const
         const bool bad1 = (rem < 16) | (a[1] != 0) | (ml > rem - 16) | ((mk + 1 == np) & (mp + 16 + ml != end));
         R.template get<2>((mine & !bad1) ? mp + 8 + ml : l.q, c);
         const double sc = __longlong_as_double((long long)((uint64_t)c[0] | ((uint64_t)c[1] << 32)));
-        const uint32_t plo = (uint32_t)__shfl((int)c[0], (int)(base + (g ? g - 1 : 0)), RR_WAVE);
-        const uint32_t phi = (uint32_t)__shfl((int)c[1], (int)(base + (g ? g - 1 : 0)), RR_WAVE);
+        const uint32_t plo = wave_from_prev(c[0]), phi = wave_from_prev(c[1]);   // (lane g - 1; g = 0 uses clo / chi)
         const double prev = __longlong_as_double((long long)(g ? ((uint64_t)plo | ((uint64_t)phi << 32))
                                                                : ((uint64_t)clo | ((uint64_t)chi << 32))));
         clo = (uint32_t)__shfl((int)c[0], (int)(base + G - 1), RR_WAVE);

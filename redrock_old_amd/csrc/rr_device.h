@@ -124,6 +124,13 @@ __device__ __forceinline__ uint32_t wave_incl_max_u32(uint32_t x) {   // (same s
     x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false));
     return x;
 }
+// the value of lane - 1 (lane 0: 0) / lane + 1 (lane 63: 0) by a whole-wave DPP shift
+__device__ __forceinline__ uint32_t wave_from_prev(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x138, 0xF, 0xF, false);   // wave_shr:1
+}
+__device__ __forceinline__ uint32_t wave_from_next(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x130, 0xF, 0xF, false);   // wave_shl:1
+}
 __device__ __forceinline__ uint64_t wave_sum(uint64_t x) {
 #pragma unroll
     for (int d = RR_WAVE / 2; d > 0; d >>= 1) x += __shfl_xor(x, d, RR_WAVE);
@@ -211,7 +218,7 @@ __device__ __forceinline__ uint64_t lb_resolve(uint64_t *state, uint64_t *groups
                 __builtin_amdgcn_s_sleep(1);
                 continue;
             }
-            excl = wave_sum(lane < p && lane <= first ? (s & LB_VAL) : 0);
+            excl = wave_sum_fast(lane < p && lane <= first ? (s & LB_VAL) : 0);
             if (first < 64) goto done;
             break;
         }
@@ -241,7 +248,7 @@ __device__ __forceinline__ uint64_t lb_resolve(uint64_t *state, uint64_t *groups
         uint64_t v = 0;
         if (lane < first) v = grp & GRP_VAL;
         else if (lane == first) v = last & LB_VAL;
-        excl += wave_sum(v);
+        excl += wave_sum_fast(v);
         if (first < 64) break;
         gg -= RR_WAVE;
     }

@@ -1042,6 +1042,9 @@ __device__ __forceinline__ uint32_t class_vpb(uint32_t c) {
 #ifndef RR_DEC_WPE
 #define RR_DEC_WPE 4
 #endif
+#ifndef RR_DEC_EBPF   // 1: the window's elem_base words touched under the sort (cache-warm batch loads)
+#define RR_DEC_EBPF 0
+#endif
 #ifndef RR_DEC_ATOT   // 1: decode_kernel adds its windows' totals atomically (no fold in decode_post)
 #define RR_DEC_ATOT 1
 #endif
@@ -1133,6 +1136,16 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
         const uint64_t v = v_lo + j * NT + tid;
         cls0[j] = v < v_hi ? (uint32_t)cls[v] : C_N;
     }
+#if RR_DEC_EBPF
+    // the first chunk's elem_base words touched now, in flight under the sort (into this CU's
+    // L1 and the L2), so each batch's per-value elem_base loads hit the cache instead of memory
+    uint32_t ebpf = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < PMAX / NT; ++j) {
+        const uint64_t v = v_lo + j * NT + tid;
+        ebpf |= (uint32_t)ebase[v < v_hi ? v : v_lo];
+    }
+#endif
 #if RR_DEC_OVL && RR_DEC_BFREE
 #pragma unroll
     for (uint32_t k = KE; k < KM; ++k)
@@ -1403,6 +1416,9 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
     if (v_end > v_lo) sort_chunk(v_lo);   // (with the window's loads still in flight)
 #if RR_DEC_OVL
     if (ovl) ov_finish();   // they have landed under the sort
+#if RR_DEC_EBPF
+    asm volatile("" ::"v"(ebpf));   // (landed with the window's loads: keeps the touch alive)
+#endif
 #endif
     for (uint64_t c0 = v_lo; c0 < v_end; c0 += PMAX) {
         if (c0 != v_lo) {
@@ -2415,7 +2431,7 @@ __device__ __forceinline__ bool build_task_map(uint8_t *tmap, uint32_t *wmax, ui
         uint32_t carry = 0;
 #pragma unroll
         for (uint32_t k = 0; k < NT / RR_WAVE; ++k) carry = k < tid / RR_WAVE ? max(carry, wmax[k]) : carry;
-        const uint32_t prev = __shfl_up(im, 1, RR_WAVE);
+        const uint32_t prev = wave_from_prev(im);
         carry = max(carry, lane_id() ? prev : 0u);
 #pragma unroll
         for (uint32_t k = 0; k < 16; ++k) {
@@ -2575,7 +2591,7 @@ __global__ __launch_bounds__(NT) ENC_SIZE_WPE_ATTR void enc_size_kernel(const rr
             const bool small = __ballot((c.bytes | c.pay) >= (1ull << 26)) == 0;
             const uint64_t ib = small ? (uint64_t)wave_incl_scan_u32((uint32_t)c.bytes) : wave_incl_scan(c.bytes);
             const uint64_t ip = small ? (uint64_t)wave_incl_scan_u32((uint32_t)c.pay) : wave_incl_scan(c.pay);
-            const uint32_t jp = __shfl_up(j[u], 1, RR_WAVE), jn = __shfl_down(j[u], 1, RR_WAVE);
+            const uint32_t jp = wave_from_prev(j[u]), jn = wave_from_next(j[u]);
             const uint32_t ln = lane_id();
             const bool first = act && (ln == 0 || jp != j[u]);
             const bool last = act && (ln == RR_WAVE - 1 || t + 1 >= TT || jn != j[u]);
@@ -2961,7 +2977,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(RR_ENC_WPE))
                               (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)incl, RR_WAVE - 1);
         uint64_t base = 0;
         if (wtot && lane_id() == RR_WAVE - 1) base = atomicAdd((unsigned long long *)&sh_nrp, (unsigned long long)wtot);
-        base = __shfl(base, RR_WAVE - 1, RR_WAVE);
+        base = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(base >> 32), RR_WAVE - 1) << 32) |
+               (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)base, RR_WAVE - 1);   // (lane 63 took the atomic)
         if (!want) return;
         const uint64_t at = base + incl - mine;
         const uint32_t r = (uint32_t)at, p0 = (uint32_t)(at >> 32);
