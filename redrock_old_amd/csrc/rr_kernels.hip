@@ -843,6 +843,18 @@ constexpr uint32_t ZL_VPB = RR_ZL_VPB;
 #define RR_DEC_ORDER C_ZL, C_SL, C_HH, C_HT, C_LIST, C_EXACT, C_IS, C_STR
 #endif
 __constant__ uint32_t CLASS_ORDER[C_N] = {RR_DEC_ORDER};
+// the class of batch-order slot k from registers (a select chain over the compile-time order:
+// no constant-memory load on each batch's path)
+__device__ __forceinline__ uint32_t class_at(uint32_t k) {
+    constexpr uint32_t ord[C_N] = {RR_DEC_ORDER};
+    uint32_t c = ord[0];
+#pragma unroll
+    for (uint32_t i = 1; i < C_N; ++i) c = k == i ? ord[i] : c;
+    return c;
+}
+#ifndef RR_DEC_BREG   // 1: the batch loop keeps the chunk's batch prefixes in registers
+#define RR_DEC_BREG 0   // (measured: decode_kernel -2.6 % in one trace, calls mixed, cfg 3 +1.5 %)
+#endif
 
 // One single-class batch: lane < cnt decodes value v (byte offsets relative to the source,
 // whose byte 0 is batch offset B).
@@ -1434,22 +1446,41 @@ __global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const
 #else
         const uint32_t nb = bpre[C_N];
 #endif
+#if RR_DEC_BREG   // the chunk's batch prefixes, read once (wave-uniform)
+        uint32_t bp[C_N + 1];
+#pragma unroll
+        for (uint32_t k = 0; k <= C_N; ++k) bp[k] = __builtin_amdgcn_readfirstlane(bpre[k]);
+#endif
         for (;;) {
             uint32_t bi = 0;
             if (lane == 0) bi = atomicAdd(&next_batch, 1u);
             bi = __builtin_amdgcn_readfirstlane(bi);
             if (bi >= nb) break;
+#if RR_DEC_BREG
+            uint32_t k = 0, bk = bp[0];
+#pragma unroll
+            for (uint32_t i = 1; i < C_N; ++i) {
+                const bool ge = bi >= bp[i];
+                k = ge ? i : k;
+                bk = ge ? bp[i] : bk;
+            }
+            const uint32_t c = class_at(k);
+#define BPRE_K bk
+#else
             uint32_t k = 0;
             while (bi >= bpre[k + 1]) ++k;
             const uint32_t c = CLASS_ORDER[k];
+#define BPRE_K bpre[k]
+#endif
 #if RR_DEC_BALANCE   // the class's values split evenly over its batches (same batch count)
             const uint32_t vpb0 = class_vpb(c), nbc = (ccount[c] + vpb0 - 1) / vpb0;
             const uint32_t vpb = (ccount[c] + nbc - 1) / nbc;
 #else
             const uint32_t vpb = class_vpb(c);
 #endif
-            const uint32_t first = cbase[c] + (bi - bpre[k]) * vpb;
-            const uint32_t cnt = min(ccount[c] - (bi - bpre[k]) * vpb, vpb);
+            const uint32_t first = cbase[c] + (bi - BPRE_K) * vpb;
+            const uint32_t cnt = min(ccount[c] - (bi - BPRE_K) * vpb, vpb);
+#undef BPRE_K
 #ifdef RR_SKIP_CLASSES   // timing-only builds (tools/): skip the batches of these classes
             if ((RR_SKIP_CLASSES >> c) & 1) continue;
 #endif
@@ -2412,6 +2443,24 @@ constexpr uint32_t ENC_MAPCAP = 4096;
 // was zeroed beforehand, ordered by a barrier) never win: 16 positions a thread, the carry across
 // threads by a DPP max scan and the waves' maxima in LDS.  Returns whether the round's tt tasks
 // fit the map (block-uniform); ends with an LDS barrier either way.
+// The last j in [0, NT) with tb[j] <= t, for a non-decreasing tb[0..NT] with tb[0] <= t: two
+// rounds of independent LDS reads instead of log2(NT) dependent ones — the 16 bucket heads
+// tb[16k] (compared all at once), then the 16 entries of the chosen bucket (four 16-byte reads).
+template <uint32_t NT>
+__device__ __forceinline__ uint32_t search_last_le(const uint32_t *tb, uint32_t t) {
+    static_assert(NT == 256, "16 buckets of 16");
+    uint32_t b = 0;
+#pragma unroll
+    for (uint32_t k = 1; k < 16; ++k) b += tb[16 * k] <= t ? 1u : 0u;
+    const uint4 *q = reinterpret_cast<const uint4 *>(tb + 16 * b);
+    uint32_t c = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+        const uint4 x = q[k];
+        c += (x.x <= t ? 1u : 0u) + (x.y <= t ? 1u : 0u) + (x.z <= t ? 1u : 0u) + (x.w <= t ? 1u : 0u);
+    }
+    return 16 * b + c - 1;
+}
 template <uint32_t NT>
 __device__ __forceinline__ bool build_task_map(uint8_t *tmap, uint32_t *wmax, uint32_t base, uint32_t ntask,
                                                uint64_t tt) {
@@ -2705,6 +2754,9 @@ __device__ __forceinline__ uint64_t rr_stamp() {
 #ifndef RR_ENC_TPF
 #define RR_ENC_TPF 1
 #endif
+#ifndef RR_ENC_SEARCH2   // 1: E4's task -> value search in two rounds of independent LDS reads
+#define RR_ENC_SEARCH2 0   // (measured: E4 343.6 -> 365 us: more LDS instructions in an issue-bound kernel)
+#endif
 #ifndef RR_ENC_EMIT_MAP   // 1: E4 maps tasks to values through an LDS map (build_task_map)
 #define RR_ENC_EMIT_MAP 0   // (measured: E4 +2 %, its 4 KiB more LDS per workgroup)
 #endif
@@ -2927,7 +2979,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(RR_ENC_WPE))
     __shared__ uint4 img4[W / 16];
     __shared__ uint64_t rq_a[RCAP];        // run: arena offset | length << 40
     __shared__ uint32_t rq_dp[RCAP];       // run: image offset | first piece (pieces of earlier runs) << 16
-    __shared__ uint32_t tb[NT + 1];        // task base of each value of the round
+    __shared__ __attribute__((aligned(16))) uint32_t tb[NT + 1];   // task base of each value of the round
     __shared__ uint64_t sv_pos[NT];        // output position of the value's first task, less the
                                            // element-byte scan there once its first task is costed
     __shared__ uint32_t sv_el[NT];         // elem_base
@@ -3044,9 +3096,13 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(RR_ENC_WPE))
                 if (usemap) lo = tmap[t];
                 else
 #endif
+#if RR_ENC_SEARCH2
+                lo = search_last_le<NT>(tb, (uint32_t)t);
+#else
 #pragma unroll
                 for (uint32_t s = NT / 2; s > 0; s >>= 1)
                     if (tb[lo + s] <= t) lo += s;
+#endif
                 pj = lo;
                 pe = get_elem(elems + sv_el[lo] + (uint32_t)(t - tb[lo]));
             }
@@ -3134,9 +3190,28 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(RR_ENC_WPE))
     const uint32_t npc = sh_pend != 0xFFFFFFFFu ? sh_pend : (uint32_t)(sh_nrp >> 32);
     auto piece = [&](uint32_t b, uint64_t &ps, uint32_t &pd, uint32_t &pl) {
         uint32_t lo = 0;   // (steps from the largest power of two below RCAP: every index reachable)
+#if RR_ENC_SEARCH2
+        // the last queued run whose first piece <= b, in three rounds of seven independent LDS
+        // reads (stride 64, 8, 1) instead of nine dependent ones: rq_dp[i] < (b + 1) << 16 is a
+        // prefix-true predicate over the runs [0, nr)
+        static_assert(RCAP == 512, "three levels of 8");
+        (void)RTOP;
+        const uint32_t key = (b + 1) << 16;
+#pragma unroll
+        for (uint32_t st = 64; st > 0; st >>= 3) {
+            uint32_t c = 0;
+#pragma unroll
+            for (uint32_t k = 1; k < 8; ++k) {
+                const uint32_t i = lo + k * st;
+                c += (i < nr && rq_dp[i < RCAP ? i : RCAP - 1] < key) ? 1u : 0u;
+            }
+            lo += c * st;
+        }
+#else
 #pragma unroll
         for (uint32_t s = RTOP; s > 0; s >>= 1)
             if (lo + s < nr && (rq_dp[lo + s] >> 16) <= b) lo += s;
+#endif
         const uint64_t a = rq_a[lo];
         const uint32_t dp = rq_dp[lo], dst = dp & 0xFFFF, l = (uint32_t)(a >> 40), k = b - (dp >> 16);
         const uint32_t d0 = k == 0 ? dst : ((dst >> 6) + k) << 6;
