@@ -2754,6 +2754,9 @@ __device__ __forceinline__ uint64_t rr_stamp() {
 #ifndef RR_ENC_TPF
 #define RR_ENC_TPF 1
 #endif
+#ifndef RR_ENC_ROT   // 1: the granule copies' store order rotated per lane group (LDS bank spread)
+#define RR_ENC_ROT 0   // (measured: within noise, cfg 2 / 3 +1-2 %)
+#endif
 #ifndef RR_ENC_SEARCH2   // 1: E4's task -> value search in two rounds of independent LDS reads
 #define RR_ENC_SEARCH2 0   // (measured: E4 343.6 -> 365 us: more LDS instructions in an issue-bound kernel)
 #endif
@@ -2923,15 +2926,19 @@ struct Img {
 // Granule copy of a piece aligned with its image offset mod 16 (RR_ENC_ALIGNED): up to four
 // aligned 16-byte loads, each clamped to the piece's last granule; full granules stored as
 // they are, partial ones masked and OR-ed into the zeroed image (no-return 64-bit LDS atomics).
-#define RR_AL_LOAD(X, S, D, L)                                                                   \
+// The piece's granules are visited in an order rotated by R (0-3): X##k holds granule (k + R) & 3
+// of the piece.  With R = (lane / 4) mod 4, the 16 lanes a ds_write_b128 serves together — which
+// hold consecutive 64-byte image blocks, i.e. four block phases mod 256 bytes — write 16
+// distinct bank groups at every step instead of four lanes per 16-byte bank group.
+#define RR_AL_LOAD(X, S, D, L, R)                                                                \
     u32x4 X##0 = {0u, 0u, 0u, 0u}, X##1 = X##0, X##2 = X##0, X##3 = X##0;                      \
     if ((L) > 0) {                                                                               \
         const uint32_t c0_ = (D) & ~15u, cl_ = ((D) + (L) - 1) & ~15u;                           \
         const u32x4 *g_ = reinterpret_cast<const u32x4 *>(arena + (S) - ((D) - c0_));            \
-        X##0 = g_[0];                                                                            \
-        X##1 = g_[c0_ + 16 <= cl_ ? 1 : 0];                                                      \
-        X##2 = g_[c0_ + 32 <= cl_ ? 2 : 0];                                                      \
-        X##3 = g_[c0_ + 48 <= cl_ ? 3 : 0];                                                      \
+        X##0 = g_[c0_ + 16 * (((R) + 0) & 3) <= cl_ ? (((R) + 0) & 3) : 0];                      \
+        X##1 = g_[c0_ + 16 * (((R) + 1) & 3) <= cl_ ? (((R) + 1) & 3) : 0];                      \
+        X##2 = g_[c0_ + 16 * (((R) + 2) & 3) <= cl_ ? (((R) + 2) & 3) : 0];                      \
+        X##3 = g_[c0_ + 16 * (((R) + 3) & 3) <= cl_ ? (((R) + 3) & 3) : 0];                      \
     }
 #define RR_AL_CHUNK(XK, K, D, L)                                                                 \
     {                                                                                            \
@@ -2955,8 +2962,9 @@ struct Img {
             }                                                                                    \
         }                                                                                        \
     }
-#define RR_AL_STORE(X, D, L)                                                                     \
-    RR_AL_CHUNK(X##0, 0, D, L) RR_AL_CHUNK(X##1, 1, D, L) RR_AL_CHUNK(X##2, 2, D, L) RR_AL_CHUNK(X##3, 3, D, L)
+#define RR_AL_STORE(X, D, L, R)                                                                  \
+    RR_AL_CHUNK(X##0, ((R) + 0) & 3, D, L) RR_AL_CHUNK(X##1, ((R) + 1) & 3, D, L)                \
+    RR_AL_CHUNK(X##2, ((R) + 2) & 3, D, L) RR_AL_CHUNK(X##3, ((R) + 3) & 3, D, L)
 
 // Copy-run queue: one entry per payload (arena offset (40 bits) | length << 40, image offset,
 // first piece); the copy phase splits the runs into 64-byte image-block pieces.
@@ -3231,10 +3239,15 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(RR_ENC_WPE))
             uint32_t d0, l0, d1 = 0, l1 = 0;
             piece(j, s0, d0, l0);
             if (two) piece(j + NT, s1, d1, l1);
-            RR_AL_LOAD(xa, s0, d0, l0)
-            RR_AL_LOAD(xb, s1, d1, l1)
-            RR_AL_STORE(xa, d0, l0)
-            RR_AL_STORE(xb, d1, l1)
+#if RR_ENC_ROT
+            const uint32_t rot = (lane_id() >> 2) & 3;
+#else
+            const uint32_t rot = 0;
+#endif
+            RR_AL_LOAD(xa, s0, d0, l0, rot)
+            RR_AL_LOAD(xb, s1, d1, l1, rot)
+            RR_AL_STORE(xa, d0, l0, rot)
+            RR_AL_STORE(xb, d1, l1, rot)
         }
     } else
 #endif
