@@ -2973,7 +2973,7 @@ constexpr uint64_t JQ_SRC = (1ull << 40) - 1;
 
 template <uint32_t W, uint32_t NT, uint32_t RCAP>
 #ifndef RR_ENC_WPE   // waves per SIMD the emit kernel is built for
-#define RR_ENC_WPE 5
+#define RR_ENC_WPE 6      // (74 VGPRs, no spills; 5: E4 345 us, 6: 307 us)
 #endif
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(RR_ENC_WPE))) void enc_emit_kernel(const rr_value *__restrict__ values,
                                                       const rr_elem *__restrict__ elems,
@@ -3433,7 +3433,7 @@ extern "C" hipError_t rr_launch_decode(const uint8_t *blob, const uint64_t *offs
 #define RR_ENC_W 16384
 #endif
 #ifndef RR_ENC_RCAP   // payload runs queued per window (LDS: 12 bytes each)
-#define RR_ENC_RCAP 512
+#define RR_ENC_RCAP 416   // (6 emit workgroups per CU: 26.6 KB of LDS each)
 #endif
 constexpr uint32_t ENC_W = RR_ENC_W, ENC_NT = 256, ENC_RCAP = RR_ENC_RCAP;
 static uint64_t enc_windows(uint64_t data_cap) { return data_cap / ENC_W + 1; }
