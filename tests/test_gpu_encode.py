@@ -161,3 +161,36 @@ def test_encode_rejects_bad_status_and_out_of_range(engine):
     v2["elem_base"][ok[50]] = len(e2) - 1
     out, ooffs, t2 = _check_against_oracle(engine, v2, e2, a)
     assert t2["n_bad"] > t["n_bad"]
+
+
+def test_windows_with_more_runs_than_the_run_queue(engine):
+    """E4 queues one copy run per payload, RR_ENC_RCAP (416) per 16 KiB output window; a window
+    of tiny payloads (1-3 byte strings, Lists of 1-byte elements: 2-3K runs per window) takes
+    the queue-overflow path for the rest.  Bytes, offsets and totals must equal the oracle's,
+    with the decoder's mirror arena (aligned granule copies) and with a relocated one (byte plan),
+    and encode(decode(b)) == b."""
+    rng = np.random.default_rng(23)
+    blobs = []
+    for i in range(9000):
+        k = i % 3
+        if k == 0:
+            blobs.append(s_raw(i, bytes(rng.integers(97, 123, int(rng.integers(1, 4)), dtype=np.uint8))))
+        elif k == 1:
+            items = [bytes([int(rng.integers(97, 123))]) for _ in range(int(rng.integers(1, 40)))]
+            blobs.append(l_list(i, items))
+        else:
+            blobs.append(s_ht(i, [bytes([97 + j]) * int(rng.integers(1, 3))   # (distinct members)
+                                  for j in range(int(rng.integers(1, 12)))]))
+    data, offs = batch_from_blobs(blobs)
+    v, e, a, t = engine.decode_host(data, offs)
+    assert t["n_bad"] == 0
+    out, ooffs, t2 = _check_against_oracle(engine, v, e, a)
+    assert np.array_equal(out, data[:int(offs[-1])])
+    # the same payloads one byte further on in a new arena: no run is aligned with its image
+    # offset mod 16, so every window takes the byte plan
+    e2 = e.copy()
+    strs = np.isin(e2["kind"], [rr.K_STR, rr.K_ZLRAW])
+    e2["data"][strs] += 1
+    a2 = np.concatenate([np.zeros(1, np.uint8), a, np.zeros(16, np.uint8)])
+    out2, ooffs2, t3 = _check_against_oracle(engine, v, e2, a2)
+    assert np.array_equal(out2, data[:int(offs[-1])])
