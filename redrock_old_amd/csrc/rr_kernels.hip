@@ -2695,6 +2695,9 @@ __global__ __launch_bounds__(NT) ENC_SIZE_WPE_ATTR void enc_size_kernel(const rr
 // passes data_cap is not written (rock_serdes has no such case: sds grows; the batch API
 // bounds the output): it counts as bad and its payload is taken back out of the totals
 // (stored as a two's-complement negative, folded by the same modular sum).
+#ifndef RR_ENC_FOLD4   // 1: E4's block 0 folds the tile totals (no finalize launch)
+#define RR_ENC_FOLD4 0
+#endif
 #ifndef RR_ENC_ATOT   // 1: E3 adds the totals atomically and sets the bytes (no finalize launch)
 #define RR_ENC_ATOT 0   // (measured: encode +7 %: 11.7K same-address atomics inside a 5 us kernel serialize)
 #endif
@@ -3004,8 +3007,17 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(RR_ENC_WPE))
                                                       const uint8_t *__restrict__ arena, uint64_t n,
                                                       uint8_t *__restrict__ out, uint64_t cap,
                                                       const uint64_t *__restrict__ offsets,
-                                                      const uint32_t *__restrict__ fv) {
+                                                      const uint32_t *__restrict__ fv,
+                                                      const uint64_t *__restrict__ stats, uint32_t ntiles,
+                                                      rr_totals *tot, uint64_t *err) {
     static_assert(W <= 65536 && W % 64 == 0, "image offsets are 16-bit, pieces 64-byte blocks");
+#if RR_ENC_FOLD4
+    // block 0 folds E1's and E3's tile totals into the call's totals before its window (the
+    // finalize launch's work, hidden under the other windows)
+    if (tot) fold_totals(stats, nullptr, ntiles, offsets, n, 0, tot, nullptr, err, 1);
+#else
+    (void)stats; (void)ntiles; (void)tot; (void)err;
+#endif
     static_assert(RCAP >= 2 && W / 64 + RCAP < 65536, "run piece bases are 16-bit");
     constexpr uint32_t RTOP = 1u << (31 - __builtin_clz(RCAP - 1));   // largest power of two < RCAP
     __shared__ uint4 img4[W / 16];
@@ -3443,7 +3455,11 @@ extern "C" hipError_t rr_launch_decode(const uint8_t *blob, const uint64_t *offs
     hipLaunchKernelGGL((DECODE_KERNEL), dim3(grid), dim3(DEC_NW * RR_WAVE), 0, stream, blob, data_cap, offsets, n,
                        first_val, cls, counts, values, elems, elem_cap, arena, stats, fix, nw, totals);
     static uint32_t post_grid = 0;
+#ifdef RR_POST_GRID   // (tuning: a fixed post grid instead of the resident one)
+    if (!post_grid) post_grid = RR_POST_GRID;
+#else
     if (!post_grid) post_grid = resident_grid(decode_post_kernel, FIX_NT, false);
+#endif
     hipLaunchKernelGGL(decode_post_kernel, dim3(post_grid), dim3(FIX_NT), 0, stream, blob, fix, values, elems, stats,
                        counts + n, nw, offsets, n, totals);
     return hipGetLastError();
@@ -3490,9 +3506,10 @@ extern "C" hipError_t rr_launch_encode(const rr_value *values, const rr_elem *el
     hipLaunchKernelGGL(enc_index_kernel<ENC_W>, dim3(t), dim3(256), 0, stream, values, elems, n, elem_cap, arena_cap,
                        offsets, cap, fv, nw, stats + 3 * (uint64_t)t, totals, err);
     hipLaunchKernelGGL((enc_emit_kernel<ENC_W, ENC_NT, ENC_RCAP>), dim3((uint32_t)nw), dim3(ENC_NT), 0, stream,
-                       values, elems, arena, n, out, cap, offsets, fv);
+                       values, elems, arena, n, out, cap, offsets, fv, stats, 2 * t, RR_ENC_FOLD4 ? totals : nullptr,
+                       err);
     e = hipGetLastError();
-#if !RR_ENC_ATOT
+#if !RR_ENC_ATOT && !RR_ENC_FOLD4
     if (e == hipSuccess && totals) e = launch_finalize(stats, lb, 2 * t, offsets, n, 0, totals, stream, err);
 #endif
     return e;
