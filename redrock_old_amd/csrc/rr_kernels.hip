@@ -2696,7 +2696,7 @@ __global__ __launch_bounds__(NT) ENC_SIZE_WPE_ATTR void enc_size_kernel(const rr
 // bounds the output): it counts as bad and its payload is taken back out of the totals
 // (stored as a two's-complement negative, folded by the same modular sum).
 #ifndef RR_ENC_FOLD4   // 1: E4's block 0 folds the tile totals (no finalize launch)
-#define RR_ENC_FOLD4 0
+#define RR_ENC_FOLD4 1   // (encode cfg 4 -1 %, cfg 2 / 3 within noise)
 #endif
 #ifndef RR_ENC_ATOT   // 1: E3 adds the totals atomically and sets the bytes (no finalize launch)
 #define RR_ENC_ATOT 0   // (measured: encode +7 %: 11.7K same-address atomics inside a 5 us kernel serialize)
