@@ -56,13 +56,20 @@ void _test_ser_des_set(void);
 void _test_ser_des_hash(void);
 void _test_ser_des_zset(void);
 
-/* Fork children (rock.c:527-550).  A process that has used the engine starts, right before it
- * forks (pthread_atfork), a decode service thread; desObject in the child sends its blobs
- * there over a socket and builds the robj from the flat records that come back, never touching
- * the HIP runtime.  rr_compat_service_start starts it explicitly (0 or -1);
- * rr_compat_test_as_child(1) makes this process route desObject as a child would (tests). */
+/* Fork children (rock.c:527-550).  A process that has used the engine opens, right before each
+ * fork (pthread_atfork), a connection of the child's own with a decode service thread behind
+ * it; desObject in the child sends its blobs there over a socket and builds the robj from the
+ * flat records that come back, never touching the HIP runtime.  The service ends when the
+ * child closes its end (exit, kill) and closes its own end when a request fails, so a child
+ * never reads another child's reply and never waits on a dead service.
+ * rr_compat_service_start opens this process's own connection (0 or -1);
+ * rr_compat_test_as_child(1) makes this process route desObject as a child would;
+ * rr_compat_test_send_only writes one FLAT request and returns without its reply (a child
+ * killed mid-call); rr_compat_test_drop_services shuts every live service end down (tests). */
 int rr_compat_service_start(void);
 void rr_compat_test_as_child(int on);
+int rr_compat_test_send_only(const void *blob, size_t len);
+void rr_compat_test_drop_services(void);
 #endif
 
 #endif

@@ -151,14 +151,41 @@ void rr_comm_destroy(rr_comm *comm);
 /* Collective.  The root holds the whole batch (device); every rank gets the plan (nranks
  * entries, host memory) so it can size its shard buffers.  Blocks until the plan is known. */
 int rr_split_plan(rr_comm *comm, const rr_blob_batch *whole, int root, rr_shard *plan, void *stream);
+
+/* The point-to-point transfers rr_split / rr_gather post, as data: each entry is one transfer
+ * this rank makes — send (RR_XFER_SEND) or receive (RR_XFER_RECV) `bytes` bytes at byte
+ * `offset` of the buffer `buf` names, to / from rank `peer`.  rr_split and rr_gather post
+ * exactly these lists, in this order, inside one ncclGroup; a caller with another transport
+ * (the CPU tests' gloo ranks) runs the same lists.  Zero-byte transfers are left out on both
+ * sides.  At most 2 * nranks entries; the count is returned, -1 for a bad argument (and for a
+ * gather placed past 2^32 - 1 descriptors). */
+enum { RR_XFER_SEND = 0, RR_XFER_RECV = 1 };
+enum {
+    RR_BUF_WHOLE_DATA = 0, RR_BUF_WHOLE_OFFSETS = 1, RR_BUF_MINE_DATA = 2, RR_BUF_MINE_OFFSETS = 3,   /* split */
+    RR_BUF_MINE_VALUES = 4, RR_BUF_MINE_ELEMS = 5, RR_BUF_WHOLE_VALUES = 6, RR_BUF_WHOLE_ELEMS = 7   /* gather */
+};
+typedef struct {
+    int32_t peer, dir, buf, rsv;
+    uint64_t offset, bytes;
+} rr_xfer;
+/* split: the root sends rank k (k != root) its bytes [b0, b1) and offsets [v0, v1]; rank k
+ * receives them at offset 0 of its shard buffers (the root's own shard is a local copy) */
+int rr_split_schedule(const rr_shard *plan, int nranks, int rank, int root, rr_xfer *out);
+/* gather: rank k (k != root) sends the root its records and its shard_elems[k] descriptors;
+ * the root receives them at the plan's value range and at rr_gather_layout's position */
+int rr_gather_schedule(const rr_shard *plan, const uint64_t *shard_elems, int nranks, int rank, int root,
+                       rr_xfer *out);
+
 /* rr_split and rr_gather agree on every rank's arguments (a one-word all-reduce) before any
  * point-to-point call, so a bad argument on one rank returns RR_API_EINVAL on every rank
- * instead of leaving the others' sends and receives waiting. */
+ * instead of leaving the others' sends and receives waiting.  That agreement reads one word
+ * back to the host, so both calls BLOCK the host until the work queued on `stream` before them
+ * has run; the transfers themselves are queued on `stream` and not waited for. */
 /* Collective.  Each rank receives its shard: mine->data (>= its b1 - b0 bytes, 16-byte
  * aligned) and mine->offsets (v1 - v0 + 1 entries, rebased to 0); mine->n is set.  The root
- * sends ncclSend slices over xGMI.  Asynchronous on `stream`.  The root may take its shard in
- * place (mine->data == whole->data + b0, mine->offsets == whole->offsets + v0) only when its
- * shard starts at byte 0 (root 0): the rebase rewrites those offsets. */
+ * sends ncclSend slices over xGMI (rr_split_schedule).  The root may take its shard in place
+ * (mine->data == whole->data + b0, mine->offsets == whole->offsets + v0) only when its shard
+ * starts at byte 0 (root 0): the rebase rewrites those offsets. */
 int rr_split(rr_comm *comm, const rr_blob_batch *whole, const rr_shard *plan, int root, rr_blob_batch *mine,
              void *stream);
 /* Collective.  Every rank passes its decoded shard (mine: n values, mine_elems descriptor

@@ -61,6 +61,17 @@ class Shard(C.Structure):
     _fields_ = [("v0", C.c_uint64), ("v1", C.c_uint64), ("b0", C.c_uint64), ("b1", C.c_uint64)]
 
 
+class Xfer(C.Structure):
+    _fields_ = [("peer", C.c_int32), ("dir", C.c_int32), ("buf", C.c_int32), ("rsv", C.c_int32),
+                ("offset", C.c_uint64), ("bytes", C.c_uint64)]
+
+
+# rr_xfer directions and buffers (include/rr_serdes.h)
+XFER_SEND, XFER_RECV = 0, 1
+BUF_WHOLE_DATA, BUF_WHOLE_OFFSETS, BUF_MINE_DATA, BUF_MINE_OFFSETS = 0, 1, 2, 3
+BUF_MINE_VALUES, BUF_MINE_ELEMS, BUF_WHOLE_VALUES, BUF_WHOLE_ELEMS = 4, 5, 6, 7
+
+
 class HostBatch(C.Structure):
     _fields_ = [("data", C.POINTER(C.c_uint8)), ("offsets", C.POINTER(C.c_uint64)), ("n", C.c_uint64),
                 ("bytes", C.c_uint64)]
@@ -71,7 +82,8 @@ EXPORTS = ["rr_ctx_create", "rr_ctx_destroy", "rr_ctx_reserve", "rr_last_error",
            "rr_encode_batch", "rr_decode_elem_bound", "rr_decode_batch_host", "rr_encode_batch_host",
            "rr_gen_batch", "rr_host_batch_free", "rr_gen_default_seed", "rr_shard_plan", "rr_flat_rebase",
            "rr_comm_get_id", "rr_comm_init", "rr_comm_destroy", "rr_split_plan", "rr_split", "rr_gather",
-           "rr_flat_rebase_host", "rr_gather_layout", "rr_copy_device", "rr_gen_sizes", "rr_gen_range"]
+           "rr_flat_rebase_host", "rr_gather_layout", "rr_copy_device", "rr_gen_sizes", "rr_gen_range",
+           "rr_split_schedule", "rr_gather_schedule"]
 COMM_ID_BYTES = 128
 # include/rr_snappy.h (GPU block compression)
 SNAPPY_EXPORTS = ["rr_snappy_max_compressed_length", "rr_snappy_compress_bound", "rr_snappy_compress_batch",
@@ -122,6 +134,9 @@ def lib():
     L.rr_flat_rebase.argtypes = [vp, vp, u64, vp, u64, u64, u64, vp]
     L.rr_flat_rebase_host.argtypes = [vp, u64, vp, u64, u64, u64]
     L.rr_gather_layout.argtypes = [vp, C.c_int, vp]
+    if hasattr(L, "rr_split_schedule"):   # (RR_LIB: an older build for A/B timing may predate them)
+        L.rr_split_schedule.argtypes = [C.POINTER(Shard), C.c_int, C.c_int, C.c_int, C.POINTER(Xfer)]
+        L.rr_gather_schedule.argtypes = [C.POINTER(Shard), vp, C.c_int, C.c_int, C.c_int, C.POINTER(Xfer)]
     L.rr_gather_layout.restype = u64
     L.rr_copy_device.argtypes = [vp, vp, vp, u64, vp]
     L.rr_comm_get_id.argtypes = [vp]
@@ -221,6 +236,35 @@ def gather_layout(shard_elems) -> tuple[np.ndarray, int]:
     if tot == 2 ** 64 - 1:
         raise RRError("gather layout past 2^32 - 1 descriptors")
     return at[:len(ne)], tot
+
+
+def _plan_arg(plan):
+    plan = np.ascontiguousarray(plan, np.uint64).reshape(-1, 4)
+    arr = (Shard * len(plan))()
+    for k, (v0, v1, b0, b1) in enumerate(plan):
+        arr[k] = Shard(int(v0), int(v1), int(b0), int(b1))
+    return arr, len(plan)
+
+
+def _xfers(out, m):
+    if m < 0:
+        raise RRError("bad schedule arguments")
+    return [(int(x.peer), int(x.dir), int(x.buf), int(x.offset), int(x.bytes)) for x in out[:m]]
+
+
+def split_schedule(plan, rank: int, root: int = 0):
+    """The transfers rr_split posts on `rank` (rr_split_schedule): [(peer, dir, buf, offset, bytes)]."""
+    arr, g = _plan_arg(plan)
+    out = (Xfer * (2 * g))()
+    return _xfers(out, lib().rr_split_schedule(arr, g, rank, root, out))
+
+
+def gather_schedule(plan, shard_elems, rank: int, root: int = 0):
+    """The transfers rr_gather posts on `rank` (rr_gather_schedule)."""
+    arr, g = _plan_arg(plan)
+    ne = np.ascontiguousarray(shard_elems, np.uint64)
+    out = (Xfer * (2 * g))()
+    return _xfers(out, lib().rr_gather_schedule(arr, _ptr(ne), g, rank, root, out))
 
 
 def elem_bound(n: int, nbytes: int) -> int:

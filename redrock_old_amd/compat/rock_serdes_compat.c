@@ -16,6 +16,7 @@
 #define RR_REDIS_TREE 1
 #endif
 #include <pthread.h>
+#include <signal.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -35,13 +36,23 @@ void rr_compat_set_device(int device) { g_device = device; }
  * A child must not touch the HIP runtime its parent initialised, so in a child desObject does
  * not decode itself: it sends the blob over a socket to a decode service thread in the parent
  * (rr_rdb_serve's FLAT request, the blob standing in for the key) and builds the robj from the
- * flat records that come back.  The service is started in the parent right before a fork
- * (pthread_atfork prepare), once the parent has used the engine; Redis runs one child at a time
- * (hasActiveChildProcess), so one socket serves them in turn.  rock.c needs no change. */
+ * flat records that come back.  rock.c needs no change.
+ *
+ * Every fork gets a connection of its own: right before the fork (pthread_atfork prepare) the
+ * parent opens a socketpair and starts a service thread on one end; after the fork the parent
+ * closes the child's end and the child closes every service end it inherited.  So the service
+ * sees EOF when its child exits (killRDBChild on FLUSHALL, SHUTDOWN, replication changes) and
+ * drops any response it still owed, and a later child can never read an earlier child's reply
+ * or send into the middle of its request.  A service that fails (a decode error, a device
+ * failure, a write error) closes its end: the child's request then fails and it panics instead
+ * of waiting forever. */
 static pid_t g_owner;                     /* the process whose threads own GPU contexts */
 static pthread_mutex_t g_svc_mu = PTHREAD_MUTEX_INITIALIZER;
-static int g_svc_fd = -1, g_child_fd = -1;   /* socketpair: service end / child end */
-static volatile int g_svc_alive;
+#define RR_COMPAT_MAX_SVC 64
+static int g_svc_fds[RR_COMPAT_MAX_SVC];  /* service ends of the live connections (parent) */
+static int g_nsvc;
+static int g_child_fd = -1;               /* this process's own connection (child end) */
+static int g_fork_fd = -1;                /* the connection opened for the fork in progress */
 static int g_as_child;                    /* test hook: route this process as a child would */
 
 static int in_child(void) { return g_as_child || (g_owner && getpid() != g_owner); }
@@ -62,46 +73,91 @@ static int echo_blob(void *user, size_t k, const int *dbis, const char *const *k
     return 0;
 }
 
+/* one connection's service: until its child closes the other end, or a request fails */
 static void *decode_service(void *arg) {
-    (void)arg;
+    const int fd = (int)(intptr_t)arg;
+    sigset_t pipe_set;   /* a reply to a child that is gone: EPIPE on this thread, not SIGPIPE */
+    sigemptyset(&pipe_set);
+    sigaddset(&pipe_set, SIGPIPE);
+    pthread_sigmask(SIG_BLOCK, &pipe_set, NULL);
     rr_ctx *ctx = NULL;
     if (rr_ctx_create(g_device, &ctx) == RR_API_OK) {
-        rr_rdb_serve(g_svc_fd, g_svc_fd, echo_blob, NULL, NULL, ctx, 64);
+        rr_rdb_serve(fd, fd, echo_blob, NULL, NULL, ctx, 64);
         rr_ctx_destroy(ctx);
     }
-    g_svc_alive = 0;   /* a broken request ended it: the next fork starts a new one */
+    pthread_mutex_lock(&g_svc_mu);
+    for (int i = 0; i < g_nsvc; i++)
+        if (g_svc_fds[i] == fd) { g_svc_fds[i] = g_svc_fds[--g_nsvc]; break; }
+    close(fd);   /* the child's read sees EOF */
+    pthread_mutex_unlock(&g_svc_mu);
     return NULL;
 }
 
-int rr_compat_service_start(void) {
-    int rc = 0;
-    pthread_mutex_lock(&g_svc_mu);
-    if (!g_svc_alive) {
-        int sv[2];
-        pthread_t th;
-        if (g_svc_fd >= 0) { close(g_svc_fd); close(g_child_fd); g_svc_fd = g_child_fd = -1; }
-        if (socketpair(AF_UNIX, SOCK_STREAM, 0, sv) != 0) rc = -1;
-        else {
-            g_svc_fd = sv[0];
-            g_child_fd = sv[1];
-            g_svc_alive = 1;
-            if (pthread_create(&th, NULL, decode_service, NULL) != 0) { g_svc_alive = 0; rc = -1; }
-            else pthread_detach(th);
-        }
+/* a new connection with its own service thread (g_svc_mu held): the child end, or -1 */
+static int open_connection(void) {
+    int sv[2];
+    pthread_t th;
+    if (g_nsvc == RR_COMPAT_MAX_SVC || socketpair(AF_UNIX, SOCK_STREAM, 0, sv) != 0) return -1;
+    g_svc_fds[g_nsvc++] = sv[0];
+    if (pthread_create(&th, NULL, decode_service, (void *)(intptr_t)sv[0]) != 0) {
+        g_nsvc--;
+        close(sv[0]);
+        close(sv[1]);
+        return -1;
     }
+    pthread_detach(th);
+    return sv[1];
+}
+
+/* this process's own connection (the in-process child route of the tests) */
+int rr_compat_service_start(void) {
+    pthread_mutex_lock(&g_svc_mu);
+    if (g_child_fd < 0) g_child_fd = open_connection();
+    const int rc = g_child_fd >= 0 ? 0 : -1;
     pthread_mutex_unlock(&g_svc_mu);
     return rc;
 }
 
+/* the lock is held across the fork, so the child's copy of the registry is consistent */
 static void atfork_prepare(void) {
-    if (g_owner && getpid() == g_owner && !g_as_child) (void)rr_compat_service_start();
+    pthread_mutex_lock(&g_svc_mu);
+    if (g_owner && getpid() == g_owner && !g_as_child) g_fork_fd = open_connection();
 }
-static void atfork_child(void) { g_ctx = NULL; }   /* (the parent's context is not ours) */
+static void atfork_parent(void) {
+    if (g_fork_fd >= 0) close(g_fork_fd);   /* the child's end is the child's alone */
+    g_fork_fd = -1;
+    pthread_mutex_unlock(&g_svc_mu);
+}
+static void atfork_child(void) {
+    g_ctx = NULL;   /* (the parent's context is not ours) */
+    for (int i = 0; i < g_nsvc; i++) close(g_svc_fds[i]);   /* the parent's service ends */
+    g_nsvc = 0;
+    if (g_child_fd >= 0) close(g_child_fd);   /* the parent's own connection */
+    g_child_fd = g_fork_fd;
+    g_fork_fd = -1;
+    pthread_mutex_unlock(&g_svc_mu);
+}
 __attribute__((constructor)) static void compat_atfork_register(void) {
-    pthread_atfork(atfork_prepare, NULL, atfork_child);
+    pthread_atfork(atfork_prepare, atfork_parent, atfork_child);
 }
 
 void rr_compat_test_as_child(int on) { g_as_child = on; }
+
+/* test hooks: a child that dies after sending a request (its reply must never reach another
+ * child), and the parent's services ending (a waiting child must fail, not hang) */
+int rr_compat_test_send_only(const void *blob, size_t len) {
+    const int dbi = RR_RDB_FLAT_TAG, zero = 0;
+    const size_t one = 1;
+    return g_child_fd >= 0 && write(g_child_fd, &dbi, sizeof dbi) == sizeof dbi &&
+                   write(g_child_fd, &one, sizeof one) == sizeof one && write(g_child_fd, &zero, sizeof zero) == sizeof zero &&
+                   write(g_child_fd, &len, sizeof len) == sizeof len && write(g_child_fd, blob, len) == (ssize_t)len
+               ? 0 : -1;
+}
+void rr_compat_test_drop_services(void) {
+    pthread_mutex_lock(&g_svc_mu);
+    for (int i = 0; i < g_nsvc; i++) shutdown(g_svc_fds[i], SHUT_RDWR);
+    pthread_mutex_unlock(&g_svc_mu);
+}
 
 static const char *status_name(unsigned st) {
     static const char *names[RR_N_STATUS] = {"ok", "short blob", "unknown type", "string encoding",
@@ -211,7 +267,7 @@ static robj *robj_from_flat(const rr_value *v, const rr_elem *el, const uint8_t 
 
 /* a child's batch: the parent's decode service decodes it, the robj are built here */
 static void des_batch_in_child(void *const *bufs, const size_t *lens, size_t n, robj **out) {
-    if (!g_svc_alive || g_child_fd < 0)
+    if (g_child_fd < 0)
         serverPanic("desObject in a fork child: the parent's decode service is not running "
                     "(the parent must use the engine before it forks)");
     int *dbis = zmalloc(sizeof(int) * n);

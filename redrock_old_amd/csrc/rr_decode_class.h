@@ -205,10 +205,10 @@ __device__ __forceinline__ void put_desc(rsrc_t E, uint32_t off, uint64_t data, 
     w.y = (uint32_t)(data >> 32);
     w.z = len;
     w.w = kind | (zenc << 8);
-#ifndef RR_ABLATE_NOSTORE   // timing-only builds (tools/)
-    __builtin_amdgcn_raw_buffer_store_b128(w, E, (int)off, 0, 0);
-#else
+#if defined(RR_ABLATE) && RR_ABLATE == 4   // timing-only builds (tools/): no descriptor stores
     asm volatile("" ::"v"(w.x), "v"(w.y), "v"(w.z), "v"(w.w), "v"(off));
+#else
+    __builtin_amdgcn_raw_buffer_store_b128(w, E, (int)off, 0, 0);
 #endif
 }
 
@@ -273,76 +273,6 @@ __device__ __forceinline__ void do_string(const Head &H, const Lane &l, uint64_t
         if (STEP(RB, RA)) break;   \
     }
 
-// ---- intset (rock_serdes.c:217-245, intset.c:45-52): fixed-width members, no walk
-template <class Src>
-__device__ __forceinline__ void do_intset(const Src &R, const Head &H, const Lane &l, bool active) {
-    const uint32_t w = H.f5(), cnt = active && l.ok ? H.f9() : 0;
-    uint32_t p = l.q + 13, k = 0;
-    Raw<2> ra = R.template fetch<2>(p), rb;
-    auto step = [&](const Raw<2> &cur, Raw<2> &nxt) __attribute__((always_inline)) {
-        const bool live = k < cnt;
-        uint32_t x[2];
-        cur.align(x);
-        nxt = R.template fetch<2>(p + w);   // (reads may run past the value: in range of the source)
-        __builtin_amdgcn_sched_barrier(0);   // keep the read ahead of the checks and the store
-        const int64_t v = w == 2 ? (int64_t)(int16_t)(x[0] & 0xFFFF)
-                        : w == 4 ? (int64_t)(int32_t)x[0] : (int64_t)((uint64_t)x[0] | ((uint64_t)x[1] << 32));
-        put_desc(l.E, live ? l.so + 16 * k : NOSLOT, (uint64_t)v, 0, RR_K_INT, 0);
-        k += live;
-        p += w;
-        return __ballot(k < cnt) == 0;
-    };
-    RR_PINGPONG(ra, rb, step)
-}
-
-// ---- List (rock_serdes.c:162-214): {u32 len, bytes}* to the end; integer-looking entries
-// become INT (quicklistPushTail re-encodes them, ziplist.c:480)
-template <class Src>
-__device__ __forceinline__ bool do_list(const Src &R, const Lane &l, bool active, uint32_t &n, uint64_t &pay) {
-    uint32_t p = l.q + 5, k = 0;
-    const uint32_t end = l.q + l.L;
-    bool fail = false, live = active;
-#ifndef RR_LIST_RAW   // timing-only builds (tools/) narrow the step's read (wrong int decisions)
-#define RR_LIST_RAW 6
-#endif
-    Raw<RR_LIST_RAW> ra = R.template fetch<RR_LIST_RAW>(p), rb;   // len + 20 bytes
-    auto step = [&](const Raw<RR_LIST_RAW> &cur, Raw<RR_LIST_RAW> &nxt) __attribute__((always_inline)) {
-        uint32_t b[6] = {0u, 0u, 0u, 0u, 0u, 0u};
-        {
-            uint32_t t[RR_LIST_RAW];
-            cur.align(t);
-#pragma unroll
-            for (int i = 0; i < RR_LIST_RAW; ++i) b[i] = t[i];
-        }
-        const uint32_t rem = end - p, len = b[0];
-        const uint64_t nx = (uint64_t)p + 4 + len;
-        const uint32_t pn = nx < end ? (uint32_t)nx : end;
-        nxt = R.template fetch<RR_LIST_RAW>(live ? pn : p);
-        __builtin_amdgcn_sched_barrier(0);   // keep the read ahead of the checks and the store
-        const bool done = p == end;
-        const bool bad = (rem < 4) | (len > rem - 4) | (k >= l.r);
-        const bool emit = live & !done & !bad;
-        fail |= live & !done & bad;
-        const uint32_t d[5] = {b[1], b[2], b[3], b[4], b[5]};
-        int64_t iv;
-#ifdef RR_LIST_NOINT   // timing-only builds (tools/): no integer check (wrong int decisions)
-        const bool isint = false; iv = 0; (void)d;
-#else
-        const bool isint = regs_try_int(d, len, iv);
-#endif
-        put_desc(l.E, emit ? l.slot(k) : NOSLOT, isint ? (uint64_t)iv : l.B + p + 4, isint ? 0 : len,
-                 isint ? RR_K_INT : RR_K_STR, 0);
-        pay += emit && !isint ? len : 0;
-        k += emit;
-        p = emit ? pn : p;
-        live = emit;
-        return __ballot(live) == 0;
-    };
-    RR_PINGPONG(ra, rb, step)
-    n = k;
-    return fail || k != l.r;
-}
-
 // ---- duplicate keys of hash tables (desSet's dictAdd keeps the first copy, rock_serdes.c:297;
 // desHash asserts there is none, :399-400).  The walk fingerprints every key member (set members,
 // hash fields) of a value with at most HT_FP_KEYS keys into 16 bits and keeps them in a packed
@@ -368,11 +298,7 @@ template <class Src>
 __device__ __forceinline__ bool do_ht(const Src &R, const Head &H, const Lane &l, bool active, uint32_t &n,
                                       uint64_t &pay, bool &fix, const bool hash) {
     const uint64_t cnt = H.u5();
-#ifndef RR_HT_NOFP
     const bool chk = active && cnt <= HT_FP_KEYS;
-#else   // timing-only builds (tools/): no fingerprints (duplicates go undetected)
-    const bool chk = false;
-#endif
     bool dupfp = active && cnt > HT_FP_KEYS;
     uint32_t p = l.q + 13, k = 0, it = 0, plen = 0;
     const uint32_t end = l.q + l.L;
@@ -423,51 +349,6 @@ __device__ __forceinline__ bool do_ht(const Src &R, const Head &H, const Lane &l
     return fail || !cnt_ok || k != l.r;
 }
 
-// ---- ZSet skiplist (rock_serdes.c:448-508): u64 count, {u64 len, member, f64 score}*
-// desZset rebuilds a skiplist and serZset writes it tail->head, so the flat form lists the pairs
-// descending by (score, member).  The walk accepts a blob already in that order with all scores
-// distinct (what serZset writes); a NaN score (t_zset.c:137), a tie or an ascent sends the value
-// to the exact parser, which assigns the status or checks ties by member and queues a re-sort.
-template <class Src>
-__device__ __forceinline__ bool do_skiplist(const Src &R, const Head &H, const Lane &l, bool active, uint32_t &n,
-                                            uint64_t &pay) {
-    const uint64_t cnt = H.u5();
-    uint32_t p = l.q + 13, k = 0;
-    const uint32_t end = l.q + l.L;
-    bool fail = false, live = active;
-    double prev = __builtin_inf();
-    Raw<2> ra = R.template fetch<2>(p), rb;
-    auto step = [&](const Raw<2> &cur, Raw<2> &nxt) __attribute__((always_inline)) {
-        uint32_t b[2];
-        cur.align(b);
-        const uint32_t rem = end - p;
-        const bool score = (k & 1) != 0;
-        const uint64_t nx = (uint64_t)p + 8 + (score ? 0u : b[0]);
-        const uint32_t pn = ((nx < end) & (score | (b[1] == 0))) ? (uint32_t)nx : end;
-        nxt = R.template fetch<2>(live ? pn : p);
-        __builtin_amdgcn_sched_barrier(0);   // keep the read ahead of the checks and the store
-        const bool done = p == end;
-        const uint64_t bits = (uint64_t)b[0] | ((uint64_t)b[1] << 32);
-        const double sc = __longlong_as_double((long long)bits);
-        // strictly below the previous score (k == 1: below +inf, i.e. not NaN / +inf after none)
-        const bool order = (k == 1) ? !(sc != sc) : (sc < prev);
-        const bool bad = (rem < 8) | (k >= l.r) | (!score & ((b[1] != 0) | (b[0] > rem - 8))) | (score & !order);
-        const bool emit = live & !done & !bad;
-        fail |= live & !done & bad;
-        put_desc(l.E, emit ? l.slot(k) : NOSLOT, score ? bits : l.B + p + 8, score ? 0 : b[0],
-                 score ? RR_K_SCORE : RR_K_STR, 0);
-        pay += emit && !score ? b[0] : 0;
-        prev = (emit & score) ? sc : prev;
-        k += emit;
-        p = emit ? pn : p;
-        live = emit;
-        return __ballot(live) == 0;
-    };
-    RR_PINGPONG(ra, rb, step)
-    n = k;
-    return fail || (k & 1) || (uint64_t)(k >> 1) != cnt || k != l.r;
-}
-
 // ---- grouped walks ---------------------------------------------------------------------
 // A batch of cnt values gives each value G = 64 / cnt lanes (G <= GMAX, uniform per batch;
 // lane g of its group).  Every lane of a group walks the value's chain — the length fields, a
@@ -492,46 +373,10 @@ __device__ __forceinline__ bool group_any(bool x, uint32_t G, uint32_t g) {
 // no checks — a read and an add per element, the position clamped to the value; each lane then
 // checks its own elements' length fields (and that the last one ends the value) and stores
 // them.  The verdicts are those of one walk to the end.
-template <class Src>
-__device__ __forceinline__ bool do_list_g(const Src &R, const Lane &l, bool active, uint32_t G, uint32_t g,
-                                          uint32_t &n, uint64_t &pay) {
-    const uint32_t end = l.q + l.L, r = active ? l.r : 0u;
-    uint32_t p = l.q + 5;
-    bool fail = active && r == 0 && p != end;
-    for (uint32_t rounds = 0;; ++rounds) {
-        uint32_t mp = l.q;
-        for (uint32_t j = 0; j < G; ++j) {
-            const uint32_t x = R.u32(p);
-            const uint32_t rem = end - p;
-            mp = j == g ? p : mp;
-            p = min(p + 4 + min(x, rem), end);
-        }
-        // my element: integer or string (zipTryEncoding, as quicklistPushTail stores it)
-        const uint32_t mk = rounds * G + g;
-        const bool mine = mk < r;
-        uint32_t b[6];
-        R.template get<6>(mp, b);
-        const uint32_t ml = b[0], rem = end - mp;
-        const bool bad = (rem < 4) | (ml > rem - 4) | ((mk + 1 == r) & (mp + 4 + ml != end));
-        fail |= mine & bad;
-        const uint32_t d[5] = {b[1], b[2], b[3], b[4], b[5]};
-        int64_t iv;
-        const bool isint = regs_try_int(d, ml, iv);
-        const bool st = mine & !bad;
-        put_desc(l.E, st ? l.slot(mk) : NOSLOT, isint ? (uint64_t)iv : l.B + mp + 4, isint ? 0 : ml,
-                 isint ? RR_K_INT : RR_K_STR, 0);
-        pay += st && !isint ? ml : 0;
-        if (__ballot((rounds + 1) * G < r) == 0) break;
-    }
-    n = r;
-    return group_any(fail, G, g);
-}
-
-// ---- List, grouped and SOFTWARE-PIPELINED: do_list_g with the group size a compile-time
-// constant, round r + 1's G chain steps issued in the same basic block as round r's element
-// decode (string2ll, checks, descriptor store), so the decode fills the chain's LDS-latency gaps
-// (as do_ziplist_bp).  The last round walks one wasted chain (clamped at the value's end).
-// Checks, stores and verdicts are do_list_g's.
+// Software-pipelined with the group size a compile-time constant: round r + 1's G chain steps are
+// issued in the same basic block as round r's element decode (string2ll, checks, descriptor
+// store), so the decode fills the chain's LDS-latency gaps (as do_ziplist_bp; LIST batch 17.3K
+// -> 12.1K cycles).  The last round walks one wasted chain (clamped at the value's end).
 template <uint32_t G, class Src>
 __device__ __forceinline__ bool do_list_bp(const Src &R, const Lane &l, bool active, uint32_t g, uint32_t &n,
                                            uint64_t &pay) {
@@ -588,19 +433,12 @@ __device__ __forceinline__ bool do_list_bp(const Src &R, const Lane &l, bool act
 // HT_G_ROUNDS lanes hold keys (a hash's keys are its even members: G >= 8; a set: G >= 4 —
 // below that the batch runs do_ht).
 constexpr uint32_t HT_G_ROUNDS = 4;
-#ifndef RR_HT_ROT_LEAN   // 1: the duplicate test skips a hash's odd rotations and the RU masks
-#define RR_HT_ROT_LEAN 1
-#endif
 __device__ __forceinline__ uint32_t ht_group_min(bool hash) { return hash ? 2 * HT_FP_KEYS / HT_G_ROUNDS : HT_FP_KEYS / HT_G_ROUNDS; }
 template <class Src>
 __device__ __forceinline__ bool do_ht_g(const Src &R, const Head &H, const Lane &l, bool active, uint32_t G,
                                         uint32_t g, uint32_t &n, uint64_t &pay, bool &fix, const bool hash) {
     const uint64_t cnt = H.u5();
-#ifndef RR_HT_NOFP
     const bool chk = active && cnt <= HT_FP_KEYS;
-#else   // timing-only builds (tools/): no fingerprints (duplicates go undetected)
-    const bool chk = false;
-#endif
     const uint32_t end = l.q + l.L, r = active ? l.r : 0u;
     uint32_t p = l.q + 13;
     bool fail = active && r == 0 && p != end;   // an empty table is its 13-byte header
@@ -653,7 +491,6 @@ __device__ __forceinline__ bool do_ht_g(const Src &R, const Head &H, const Lane 
     for (uint32_t a = 0; a < HT_G_ROUNDS; ++a)
 #pragma unroll
         for (uint32_t b = a + 1; b < HT_G_ROUNDS; ++b) dup |= fpp[a] == fpp[b];
-#if RR_HT_ROT_LEAN
     // A hash's keys are its even members and G is even, so only even lanes hold keys: an odd
     // rotation pairs keys with non-keys and is skipped.  The fillers (top half 0xFFFF, unique per
     // lane and round) match nothing, so the rounds past RU need no mask in the compares.
@@ -666,17 +503,6 @@ __device__ __forceinline__ bool do_ht_g(const Src &R, const Head &H, const Lane 
             }                                                                                          \
         }                                                                                              \
     }
-#else
-#define RR_HT_ROT(D)                                                                                   \
-    if ((D) < G) {                                                                                     \
-        _Pragma("unroll") for (uint32_t q = 0; q < HT_G_ROUNDS; ++q) {                                 \
-            if (q < RU) {                                                                              \
-                const uint32_t x = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)fpp[q], 0x120 + (D), 0xF, 0xF, false); \
-                _Pragma("unroll") for (uint32_t qq = 0; qq < HT_G_ROUNDS; ++qq) dup |= (qq < RU) & (fpp[qq] == x); \
-            }                                                                                          \
-        }                                                                                              \
-    }
-#endif
     RR_HT_ROT(1) RR_HT_ROT(2) RR_HT_ROT(3) RR_HT_ROT(4) RR_HT_ROT(5) RR_HT_ROT(6) RR_HT_ROT(7)
     RR_HT_ROT(8) RR_HT_ROT(9) RR_HT_ROT(10) RR_HT_ROT(11) RR_HT_ROT(12) RR_HT_ROT(13) RR_HT_ROT(14) RR_HT_ROT(15)
 #undef RR_HT_ROT
@@ -755,217 +581,23 @@ __device__ __forceinline__ void do_intset_g(const Src &R, const Head &H, const L
 }
 
 // ---- Hash / ZSet ziplists (rock_serdes.c:314-346, :417-446; ziplist.c:300-447): element 0
-// is the raw ziplist, then one descriptor per entry.
-// Two lanes per value walk it from both ends (ziplist.c:300-330: an entry's prevlen field gives
-// the start of the entry before it): the even lane forward from the first entry through entries
-// [0, m), the odd lane backward from zltail through entries [m, N) (N = zllen, m = ceil(N/2)),
-// each descriptor stored at its own slot.  The walks meet: the forward lane's end position and
-// last entry size must be the backward lane's last entry start and its prevlen.  Together the
-// checks are those of one forward walk (every prevlen == the size of the entry before it, the
-// entries tile [10, zlbytes-1) exactly, the last one starts at zltail, the byte after it is
-// 0xFF, N entries) with half the chained steps.  A ziplist whose zllen saturated (0xFFFF) is
-// walked forward to its end marker by the even lane alone.
-template <class Src>
-__device__ __forceinline__ bool do_ziplist(const Src &R, const Lane &l, bool active, const bool back, uint32_t &n,
-                                           uint64_t &pay) {
-    const uint32_t zl0 = l.q + 13, zend = l.q + l.L, zlast = zend - 1;   // zlast: the 0xFF byte
-    uint32_t z[3];
-    R.template get<3>(zl0, z);   // zlbytes, zltail, zllen
-    const uint32_t zllen = z[2] & 0xFFFF;
-    const bool two = zllen != 0xFFFF;
-    const uint32_t mf = two ? (zllen + 1) / 2 : 0xFFFFFFFFu, nb = two ? zllen - (zllen + 1) / 2 : 0;
-    const uint32_t endbyte = R.template fetch<1>(zlast).w[0];   // (aligned dword holding zlast)
-    put_desc(l.E, active && !back ? l.slot(0) : NOSLOT, l.B + zl0, l.L - 13, RR_K_ZLRAW, 0);
-    pay += active && !back ? l.L - 13 : 0;
-    const uint32_t lim = back ? nb : mf;
-    uint32_t p = back ? zl0 + z[1] : zl0 + 10;
-    uint32_t prev_raw = 0, last = zl0 + 10, k = 0, expect = zlast, plm = 0;
-    bool fail = false, live = active && lim > 0;
-    Raw<4> ra = R.template fetch<4>(p < zend ? p : zl0), rb;   // prevlen (1 or 5) + encoding + up to 9 more bytes
-    auto step = [&](const Raw<4> &cur, Raw<4> &nxt) __attribute__((always_inline)) {
-        uint32_t b[4];
-        cur.align(b);
-        const uint32_t b0 = b[0] & 0xFF;
-        // every field of the entry header from registers, as selects (no per-encoding branches)
-        const bool big = b0 >= 254;
-        const uint32_t pl = big ? ab(b[1], b[0], 1) : b0;
-        const uint32_t qp = p + (big ? 5u : 1u);
-        const uint32_t e = big ? (b[1] >> 8) & 0xFF : (b[0] >> 8) & 0xFF;
-        const uint32_t x1 = big ? (b[1] >> 16) & 0xFF : (b[0] >> 16) & 0xFF;
-        const uint32_t lo = big ? ab(b[2], b[1], 2) : ab(b[1], b[0], 2);   // bytes after the encoding byte
-        const uint32_t hi = big ? ab(b[3], b[2], 2) : ab(b[2], b[1], 2);
-        // (bitwise | and arithmetic selects, not || / ?: chains: the compiler turns those into
-        // exec-mask branches)
-        const bool zstr = e < 0xC0;
-        const uint32_t scls = e >> 6;                        // string length class 0 / 1 / 2
-        const uint32_t ls = 1 + scls + 2 * (scls >> 1);      // 1 / 2 / 5 length bytes
-        const uint32_t sl1 = scls == 0 ? (e & 0x3F) : (((e & 0x3F) << 8) | x1);
-        const uint32_t sl = scls >= 2 ? __builtin_bswap32(lo) : sl1;
-        const bool imm = e - 0xF1u <= 0xFDu - 0xF1u;
-        const uint32_t isz = (uint32_t)(e == 0xFE) + 2 * (uint32_t)(e == 0xC0) + 3 * (uint32_t)(e == 0xF0) +
-                             4 * (uint32_t)(e == 0xD0) + 8 * (uint32_t)(e == 0xE0);
-        const uint64_t endp = (uint64_t)qp + (zstr ? ls + sl : 1 + isz);
-        // next entry: forward past this one; backward to the one this prevlen describes
-        const uint32_t pn = back ? p - pl : (endp < zlast ? (uint32_t)endp : zlast);
-        nxt = R.template fetch<4>((live & (pn < zend)) ? pn : zl0);
-        __builtin_amdgcn_sched_barrier(0);   // keep the read ahead of the checks and the store
-        const uint32_t idx = back ? zllen - 1 - k : k;       // entry index
-        const bool done = !two & (b0 == 0xFF) & (p < zend);   // forward to the end marker
-        const bool bad = (p >= zend) | (p < zl0 + 10) | (b0 == 0xFF) | (big & (p + 5 > zlast)) | (qp >= zlast) |
-                         (idx + 1 >= l.r) | (!zstr & !imm & (isz == 0)) | (zstr & (qp + ls > zlast)) |
-                         (endp > zlast) | (back ? endp != expect : pl != prev_raw);
-        const bool emit = live & !done & !bad;
-        fail |= live & !done & bad;
-        // little-endian integer of isz (1..4) bytes, sign-extended by a shift pair; 8 bytes; or
-        // the 4-bit immediate
-        const uint32_t sh = (32 - 8 * isz) & 31;
-        const int64_t v32 = (int32_t)(lo << sh) >> sh;
-        const int64_t iv = isz == 8 ? (int64_t)((uint64_t)lo | ((uint64_t)hi << 32)) : imm ? (int64_t)(e & 0x0F) - 1 : v32;
-        put_desc(l.E, emit ? l.slot(idx + 1) : NOSLOT, zstr ? l.B + qp + ls : (uint64_t)iv, zstr ? sl : 0,
-                 zstr ? RR_K_STR : RR_K_INT, zstr ? (e & 0xC0) : e);
-        prev_raw = emit ? (uint32_t)endp - p : prev_raw;
-        last = emit ? p : last;
-        plm = emit ? pl : plm;
-        expect = emit ? p : expect;
-        p = emit ? pn : p;
-        k += emit;
-        live = emit & (k < lim);
-        return __ballot(live) == 0;
-    };
-    RR_PINGPONG(ra, rb, step)
-    // the meeting: the backward lane's last entry must start where the forward lane stopped,
-    // and its prevlen must be the size of the forward lane's last entry
-    const uint32_t o_k = __shfl_xor(k, 1, RR_WAVE), o_last = __shfl_xor(last, 1, RR_WAVE);
-    const uint32_t o_plm = __shfl_xor(plm, 1, RR_WAVE);
-    const bool o_fail = __shfl_xor((uint32_t)fail, 1, RR_WAVE) != 0;
-    bool ok;
-    if (two) {
-        ok = !fail && k == mf && (zllen & 1) == 0 && (endbyte >> (8 * (zlast & 3)) & 0xFF) == 0xFF &&
-             (nb > 0 ? (!o_fail && o_k == nb && p == o_last && prev_raw == o_plm)
-                     : (p == zlast && z[1] == last - zl0));
-        n = 1 + zllen;
-    } else {   // one forward walk to the end marker (ziplist.c:300-447)
-        ok = !fail && p == zlast && z[1] == last - zl0 && (k & 1) == 0;
-        n = 1 + k;
-    }
-    return !ok || n != l.r;
-}
-
-// ---- Hash / ZSet ziplists, grouped, on ONE backward chain.  A backward step needs only the
-// prevlen field (ziplist.c:300-330: 1 byte, or 0xFE + u32; an entry's prevlen is the size of
-// the entry before it), so the chain costs a few instructions per entry; all the per-entry
-// work — the encoding, the length / integer fields, the checks, the descriptor store — is done
-// off the chain, lane g of the value's G-lane group taking entries N-1-g, N-1-g-G, ...  The
-// checks are those of one forward walk (ziplist.c:300-447): the entries tile [10, zlbytes-1)
-// exactly (each entry, decoded from its own header, ends where the next one starts; the last
-// ends at the 0xFF byte, entry 0 starts right after the header with prevlen 0), zltail is the
-// last entry, zllen entries, an even count of them.  A ziplist whose zllen saturated (0xFFFF)
-// goes to the exact parser.
-#ifndef RR_ZL_U   // entries per lane per round of do_ziplist_bg
-#define RR_ZL_U 1
-#endif
-constexpr uint32_t ZL_U = RR_ZL_U;
-#ifndef RR_ZL_U8   // 1: the pipelined ziplist chain reads a prevlen's first byte with a byte read (ZL batch 16.9K -> 16.3K cycles)
-#define RR_ZL_U8 1
-#endif
-template <class Src>
-__device__ __forceinline__ bool do_ziplist_bg(const Src &R, const Lane &l, bool active, uint32_t G, uint32_t g,
-                                              uint32_t &n, uint64_t &pay) {
-    const uint32_t zl0 = l.q + 13, zend = l.q + l.L, zlast = zend - 1;   // zlast: the 0xFF byte
-    const uint32_t first = zl0 + 10;                                     // entry 0
-    uint32_t z[3];
-    R.template get<3>(zl0, z);   // zlbytes, zltail, zllen
-    const uint32_t N = active && (z[2] & 0xFFFF) != 0xFFFF ? z[2] & 0xFFFF : 0u;
-    const uint32_t endbyte = R.template fetch<1>(zlast).w[0];   // (aligned dword holding zlast)
-    put_desc(l.E, active && g == 0 ? l.slot(0) : NOSLOT, l.B + zl0, l.L - 13, RR_K_ZLRAW, 0);
-    pay += active && g == 0 ? l.L - 13 : 0;
-    bool fail = active && (z[2] & 0xFFFF) == 0xFFFF;   // saturated count: the exact parser walks it
-    // the chain: p = start of entry N-1-s after s steps; each step goes back by the entry's
-    // prevlen, clamped to stay at or after entry 0's position (a prevlen that does not fit is
-    // caught below by the lane that holds that entry)
-    uint32_t p = zl0 + z[1];
-    p = p < first ? first : p > zlast ? zlast : p;
-    uint32_t expect = zlast;   // where the entry at p must end
-    // ZL_U entries per lane per round (U G chain steps): the U entry decodes are independent,
-    // so their instruction streams interleave
-    constexpr uint32_t U = ZL_U;
-    for (uint32_t rounds = 0;; ++rounds) {
-        uint32_t mp[U], me[U];
-#pragma unroll
-        for (uint32_t u = 0; u < U; ++u) {
-            mp[u] = first;
-            me[u] = zlast;
-            for (uint32_t j = 0; j < G; ++j) {
-                uint32_t x[2];
-                R.template get<2>(p, x);
-                const uint32_t b0 = x[0] & 0xFF;
-                const uint32_t pl = b0 >= 254 ? ab(x[1], x[0], 1) : b0;
-                const uint32_t pn = p - min(pl, p - first);
-                mp[u] = j == g ? p : mp[u];
-                me[u] = j == g ? expect : me[u];
-                expect = p;
-                p = pn;
-            }
-        }
-        // my entries (index idx = N-1-mk): every field of the header from registers, as selects
-        // (no per-encoding branches); an entry must end where the entry after it starts (me) —
-        // which makes every prevlen the size of the entry before it — and its prevlen must stay
-        // inside the entries; entry 0 sits right after the header with prevlen 0
-#pragma unroll
-        for (uint32_t u = 0; u < U; ++u) {
-            const uint32_t mk = (rounds * U + u) * G + g;
-            const bool mine = mk < N;
-            const uint32_t idx = N - 1 - mk;
-            uint32_t b[4];
-            R.template get<4>(mp[u], b);
-            const uint32_t b0 = b[0] & 0xFF;
-            const bool big = b0 >= 254;
-            const uint32_t pl = big ? ab(b[1], b[0], 1) : b0;
-            const uint32_t qp = mp[u] + (big ? 5u : 1u);
-            const uint32_t e = big ? (b[1] >> 8) & 0xFF : (b[0] >> 8) & 0xFF;
-            const uint32_t x1 = big ? (b[1] >> 16) & 0xFF : (b[0] >> 16) & 0xFF;
-            const uint32_t lo = big ? ab(b[2], b[1], 2) : ab(b[1], b[0], 2);   // bytes after the encoding byte
-            const uint32_t hi = big ? ab(b[3], b[2], 2) : ab(b[2], b[1], 2);
-            const bool zstr = e < 0xC0;
-            const uint32_t scls = e >> 6;                        // string length class 0 / 1 / 2
-            const uint32_t ls = 1 + scls + 2 * (scls >> 1);      // 1 / 2 / 5 length bytes
-            const uint32_t sl1 = scls == 0 ? (e & 0x3F) : (((e & 0x3F) << 8) | x1);
-            const uint32_t sl = scls >= 2 ? __builtin_bswap32(lo) : sl1;
-            const bool imm = e - 0xF1u <= 0xFDu - 0xF1u;
-            // integer bytes: C0 2, D0 4, E0 8, F0 3 (a nibble table on bits 4-5), FE 1, else 0
-            const uint32_t isz = (e & 0x0F) == 0 && e >= 0xC0 ? (0x3842u >> (4 * ((e >> 4) & 3))) & 0xF
-                                                               : (uint32_t)(e == 0xFE);
-            const uint64_t endp = (uint64_t)qp + (zstr ? ls + sl : 1 + isz);
-            const bool bad = (mp[u] < first) | (mp[u] >= zlast) | (b0 == 0xFF) | (big & (mp[u] + 5 > zlast)) |
-                             (qp >= zlast) | (idx + 1 >= l.r) | (!zstr & !imm & (isz == 0)) |
-                             (zstr & (qp + ls > zlast)) | (endp != (uint64_t)me[u]) |
-                             (idx == 0 ? ((mp[u] != first) | (pl != 0)) : (pl > mp[u] - first));
-            fail |= mine & bad;
-            const uint32_t sh = (32 - 8 * isz) & 31;
-            const int64_t v32 = (int32_t)(lo << sh) >> sh;
-            const int64_t iv = isz == 8 ? (int64_t)((uint64_t)lo | ((uint64_t)hi << 32)) : imm ? (int64_t)(e & 0x0F) - 1 : v32;
-            put_desc(l.E, (mine & !bad) ? l.slot(idx + 1) : NOSLOT, zstr ? l.B + qp + ls : (uint64_t)iv, zstr ? sl : 0,
-                     zstr ? RR_K_STR : RR_K_INT, zstr ? (e & 0xC0) : e);
-        }
-        if (__ballot((rounds + 1) * U * G < N) == 0) break;
-    }
-    // one verdict for the whole group
-    const uint32_t base = lane_id() - g;
-    const uint64_t gm = (G >= 64 ? ~0ull : ((1ull << G) - 1)) << base;
-    const bool gfail = (__ballot(fail) & gm) != 0;
-    const uint32_t zllen = z[2] & 0xFFFF;
-    const bool ok = !gfail && (zllen & 1) == 0 && (endbyte >> (8 * (zlast & 3)) & 0xFF) == 0xFF &&
-                    (zllen > 0 || (z[1] == 10 && first == zlast));
-    n = 1 + zllen;
-    return !ok || n != l.r;
-}
-
-// ---- Hash / ZSet ziplists, grouped and SOFTWARE-PIPELINED: do_ziplist_bg with the group
-// size a compile-time constant, so a round's G backward chain steps are straight-line code, and
-// the chain of round r + 1 (which needs only the positions) is issued in the same basic block as
-// the entry decode of round r (which needs nothing of the next chain): the decode's instructions
-// fill the chain's LDS-latency gaps instead of following them.  The last round walks one wasted
-// chain (clamped at entry 0).  Checks, stores and verdicts are do_ziplist_bg's.
+// is the raw ziplist, then one descriptor per entry.  Grouped on ONE backward chain: a backward
+// step needs only the prevlen field (ziplist.c:300-330: 1 byte, or 0xFE + u32; an entry's
+// prevlen is the size of the entry before it), so the chain costs a few instructions per entry;
+// all the per-entry work — the encoding, the length / integer fields, the checks, the descriptor
+// store — is done off the chain, lane g of the value's G-lane group taking entries N-1-g,
+// N-1-g-G, ...  The checks are those of one forward walk (ziplist.c:300-447): the entries tile
+// [10, zlbytes-1) exactly (each entry, decoded from its own header, ends where the next one
+// starts; the last ends at the 0xFF byte, entry 0 starts right after the header with prevlen 0),
+// zltail is the last entry, zllen entries, an even count of them.  A ziplist whose zllen
+// saturated (0xFFFF) goes to the exact parser.
+// Software-pipelined with the group size a compile-time constant: a round's G backward chain
+// steps are straight-line code, and the chain of round r + 1 (which needs only the positions) is
+// issued in the same basic block as the entry decode of round r (which needs nothing of the next
+// chain), so the decode's instructions fill the chain's LDS-latency gaps instead of following
+// them (ZL batch 18.5K -> 16.7K cycles).  The last round walks one wasted chain (clamped at entry
+// 0).  (Measured dead ends: two lanes per value walking from both ends, 2 or 4 entries per lane
+// per round, R rounds of the chain blocked into registers before R decodes.)
 template <uint32_t G, class Src>
 __device__ __forceinline__ bool do_ziplist_bp(const Src &R, const Lane &l, bool active, uint32_t g, uint32_t &n,
                                               uint64_t &pay) {
@@ -983,36 +615,24 @@ __device__ __forceinline__ bool do_ziplist_bp(const Src &R, const Lane &l, bool 
     uint32_t expect = zlast;   // where the entry at p must end
     // one round's chain: G backward steps; this lane keeps step g's entry (mp) and its end (me)
     auto chain = [&](uint32_t &mp, uint32_t &me) __attribute__((always_inline)) {
-#ifdef RR_ASM_MARK
-        asm volatile("; ZLCHAIN_BEGIN" ::: "memory");
-#endif
         mp = first;
         me = zlast;
 #pragma unroll
         for (uint32_t j = 0; j < G; ++j) {
-#if RR_ZL_U8
             // prevlen: its first byte by a byte read, the u32 of a 5-byte prevlen by a dword
-            // read issued beside it (off the common path's dependency chain)
+            // read issued beside it (off the common path's dependency chain; an aligned pair +
+            // alignbyte measured ZL batch 16.9K vs 16.3K cycles)
             const uint32_t b0 = R.u8b(p);
             const uint32_t pb = R.u32(p + 1);
             const uint32_t pl = b0 >= 254 ? pb : b0;
-#else
-            uint32_t x[2];
-            R.template get<2>(p, x);   // prevlen: 1 byte, or 0xFE + u32
-            const uint32_t b0 = x[0] & 0xFF;
-            const uint32_t pl = b0 >= 254 ? ab(x[1], x[0], 1) : b0;
-#endif
             const uint32_t pn = p - min(pl, p - first);
             mp = j == g ? p : mp;
             me = j == g ? expect : me;
             expect = p;
             p = pn;
         }
-#ifdef RR_ASM_MARK
-        asm volatile("; ZLCHAIN_END" ::: "memory");
-#endif
     };
-    // the entry decode and checks of do_ziplist_bg (index idx = N-1-mk)
+    // the entry decode and its checks (index idx = N-1-mk)
     auto decode = [&](uint32_t mk, uint32_t mp, uint32_t me) __attribute__((always_inline)) {
         const bool mine = mk < N;
         const uint32_t idx = N - 1 - mk;

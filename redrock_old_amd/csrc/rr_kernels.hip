@@ -288,31 +288,15 @@ __device__ __forceinline__ Parsed parse_value(P b, uint64_t off, uint64_t len, r
     return r;
 }
 
-// Batch totals: every tile stores its partials {bad, payload, count} with plain stores into
-// its own slot; a one-workgroup finalize kernel folds them after the main launch.  (A single
-// returning atomic per tile on one word serialises at ~88/us — measured 2.8 ms at 121K tiles.)
-__device__ __forceinline__ void tile_stats(uint64_t *stats, uint32_t tile, uint64_t bad, uint64_t pay, uint64_t cnt) {
-    if (lane_id() == 0) {
-        stats[3 * (uint64_t)tile + 0] = bad;
-        stats[3 * (uint64_t)tile + 1] = pay;
-        stats[3 * (uint64_t)tile + 2] = cnt;
-    }
-}
-
-// mode 0 (decode): bytes = offsets[n]; mode 1 (encode): bytes = inclusive prefix of the last
-// tile.  Many blocks (one CU reads ~60 GB/s: a single-block fold of 121K tiles took 56 us),
-// each folding a slice and adding into *out, which the launcher zeroes first.
-// (nblocks: how many of the grid's blocks fold — the decode's post kernel folds in block 0 alone:
-// ~500 blocks each adding into the same three words serialised at the memory side)
-__device__ __forceinline__ void fold_totals(const uint64_t *__restrict__ stats, uint64_t *state, uint32_t ntiles,
-                                            const uint64_t *__restrict__ offsets, uint64_t n, int mode, rr_totals *out,
-                                            const uint64_t *__restrict__ extra, uint64_t *err,
-                                            uint32_t nblocks = 0xFFFFFFFFu) {
+// The encode's totals: E1's and E3's per-tile partials {bad, payload, descriptors} (3 words a
+// tile), folded by E4's block 0 into the call's totals (zeroed by E1's block 0); bytes =
+// offsets[n], or UINT64_MAX when the call's error word is set (device-side failure).
+__device__ __forceinline__ void fold_totals(const uint64_t *__restrict__ stats, uint32_t ntiles,
+                                            const uint64_t *__restrict__ offsets, uint64_t n, rr_totals *out,
+                                            uint64_t *err) {
     __shared__ uint64_t red[3][4];
     uint64_t b = 0, p = 0, c = 0;
-    const uint32_t nbk = gridDim.x < nblocks ? gridDim.x : nblocks;
-    if (blockIdx.x >= nbk) return;
-    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < ntiles; t += nbk * blockDim.x) {
+    for (uint32_t t = threadIdx.x; t < ntiles; t += blockDim.x) {
         b += stats[3 * (uint64_t)t + 0];
         p += stats[3 * (uint64_t)t + 1];
         c += stats[3 * (uint64_t)t + 2];
@@ -329,38 +313,8 @@ __device__ __forceinline__ void fold_totals(const uint64_t *__restrict__ stats, 
         if (tb) atomicAdd((unsigned long long *)&out->n_bad, (unsigned long long)tb);
         if (tp) atomicAdd((unsigned long long *)&out->payload, (unsigned long long)tp);
         if (tc) atomicAdd((unsigned long long *)&out->n_elems, (unsigned long long)tc);
-        if (blockIdx.x == 0) {
-            if (extra) {   // decode: {bad, payload} changes of the fixup pass
-                atomicAdd((unsigned long long *)&out->n_bad, (unsigned long long)extra[0]);
-                atomicAdd((unsigned long long *)&out->payload, (unsigned long long)extra[1]);
-            }
-            if (mode == 2) {   // decode: descriptor slots = scanned total, bytes = offsets[n]
-                out->bytes = offsets[n];
-                atomicAdd((unsigned long long *)&out->n_elems, (unsigned long long)state[0]);
-            } else
-                out->bytes = mode == 0 ? offsets[n] : (ntiles ? (lb_load(&state[ntiles - 1]) & LB_VAL) : 0);
-            if (err && lb_load(err)) out->bytes = ~0ull;   // device-side failure: outputs invalid
-        }
+        out->bytes = lb_load(err) ? ~0ull : offsets[n];
     }
-}
-
-__global__ __launch_bounds__(256) void finalize_kernel(const uint64_t *__restrict__ stats, uint64_t *state,
-                                                       uint32_t ntiles, const uint64_t *__restrict__ offsets,
-                                                       uint64_t n, int mode, rr_totals *out,
-                                                       const uint64_t *__restrict__ extra, uint64_t *err) {
-    fold_totals(stats, state, ntiles, offsets, n, mode, out, extra, err);
-}
-
-// (the totals were zeroed by the pipeline's first kernel)
-static hipError_t launch_finalize(const uint64_t *stats, uint64_t *state, uint32_t ntiles, const uint64_t *offsets,
-                                  uint64_t n, int mode, rr_totals *out, hipStream_t stream, uint64_t *err,
-                                  const uint64_t *extra = nullptr) {
-    uint32_t blocks = (ntiles + 255) / 256;
-    if (blocks > 512) blocks = 512;
-    if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL(finalize_kernel, dim3(blocks), dim3(256), 0, stream, stats, state, ntiles, offsets, n, mode, out,
-                       extra, err);
-    return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------------------- decode
@@ -403,81 +357,6 @@ __device__ __forceinline__ uint64_t zl_walk_count_g(const uint8_t *zl, uint64_t 
     return n;
 }
 
-__device__ __forceinline__ uint64_t reserve_g(const uint8_t *b, uint64_t L) {
-    if (L < 5) return 0;
-    const uint32_t t = b[0];
-    if (t == RR_TYPE_STRING) return L >= 6 ? 1 : 0;
-    if (t == RR_TYPE_LIST_QUICKLIST) {
-        uint64_t p = 5, n = 0;
-        while (p < L) {
-            if (L - p < 4) break;
-            const uint64_t l = ld_u32(b + p);
-            if (l > L - p - 4) break;
-            ++n;
-            p += 4 + l;
-        }
-        return n;
-    }
-    if (L < 13) return 0;
-    switch (t) {
-        case RR_TYPE_SET_INTSET: {
-            const uint64_t w = ld_u32(b + 5), c = ld_u32(b + 9);
-            return ((w == 2 || w == 4 || w == 8) && L - 13 == w * c) ? c : 0;
-        }
-        case RR_TYPE_SET_HT: { const uint64_t c = ld_u64(b + 5), m = (L - 13) / 8; return c < m ? c : m; }
-        case RR_TYPE_HASH_HT: { const uint64_t c = ld_u64(b + 5), m = (L - 13) / 8; return c > m / 2 ? m : 2 * c; }
-        case RR_TYPE_ZSET_SKIPLIST: { const uint64_t c = ld_u64(b + 5), m = (L - 13) / 16; return 2 * (c < m ? c : m); }
-        case RR_TYPE_HASH_ZIPLIST:
-        case RR_TYPE_ZSET_ZIPLIST: {
-            const uint64_t Lz = ld_u64(b + 5);
-            if (Lz != L - 13 || Lz < 11) return 0;
-            const uint64_t zllen = ld_u16(b + 21);
-            if (zllen != 0xFFFF) { const uint64_t m = (Lz - 11) / 2; return 1 + (zllen < m ? zllen : m); }
-            return 1 + zl_walk_count_g(b + 13, Lz);
-        }
-        default:
-            return 0;
-    }
-}
-
-// The class of a value: which single-class walk decodes it.  Every check that needs only the
-// header is made here; values failing one (and unknown types) go to the exact parser.
-__device__ __forceinline__ uint32_t classify_g(const uint8_t *b, uint64_t L) {
-    if (L < 5) return C_EXACT;
-    switch (b[0]) {
-        case RR_TYPE_STRING: {
-            if (L < 6) return C_EXACT;
-            const uint32_t enc = b[5];
-            const uint64_t rest = L - 6;
-            if (enc == RR_ENC_INT) return rest == 8 ? C_STR : C_EXACT;
-            if (enc == RR_ENC_EMBSTR) return rest <= RR_EMBSTR_SIZE_LIMIT ? C_STR : C_EXACT;
-            if (enc == RR_ENC_RAW) return rest <= 0xFFFFFFFFull ? C_STR : C_EXACT;
-            return C_EXACT;
-        }
-        case RR_TYPE_LIST_QUICKLIST:
-            return C_LIST;
-        case RR_TYPE_SET_INTSET: {
-            if (L < 13) return C_EXACT;
-            const uint64_t w = ld_u32(b + 5), c = ld_u32(b + 9);
-            return ((w == 2 || w == 4 || w == 8) && L - 13 == w * c) ? C_IS : C_EXACT;
-        }
-        case RR_TYPE_SET_HT:
-            return L < 13 ? C_EXACT : C_HT;
-        case RR_TYPE_HASH_HT:
-            return L < 13 ? C_EXACT : C_HH;
-        case RR_TYPE_ZSET_SKIPLIST:
-            return L < 13 ? C_EXACT : C_SL;
-        case RR_TYPE_HASH_ZIPLIST:
-        case RR_TYPE_ZSET_ZIPLIST: {
-            if (L < 24) return C_EXACT;   // 13-byte header + the 11-byte empty ziplist
-            const uint64_t Lz = ld_u64(b + 5);
-            return (Lz == L - 13 && ld_u32(b + 13) == Lz) ? C_ZL : C_EXACT;
-        }
-        default:
-            return C_EXACT;
-    }
-}
-
 // The first 24 bytes of a value as six dwords, from at most three aligned 16-byte loads
 // (granules past the value's end are not read: they may lie past the padded batch), instead
 // of one scattered byte load per header byte.  Bytes past the value's end are don't-cares:
@@ -499,23 +378,8 @@ __device__ __forceinline__ void head24(const uint8_t *blob, uint64_t o, uint64_t
         d[j] = __builtin_amdgcn_alignbyte(hi, lo, sh);
     }
 }
-// dword at byte p of the value b (p + 4 <= its length): aligned loads only
-__device__ __forceinline__ uint32_t ld_u32_al(const uint8_t *b, uint64_t p) {
-    const uintptr_t x = reinterpret_cast<uintptr_t>(b) + p;
-    const uint32_t *w = reinterpret_cast<const uint32_t *>(x & ~(uintptr_t)3);
-    const uint32_t s = (uint32_t)x & 3;
-    const uint32_t lo = w[0], hi = s ? w[1] : 0u;
-    return __builtin_amdgcn_alignbyte(hi, lo, s);
-}
-
 typedef uint32_t u32_ua __attribute__((aligned(1)));   // unaligned dword (one global_load_dword)
-#ifndef RR_COUNT_UA   // 1: count_kernel's List chain reads each length field with one unaligned load
-#define RR_COUNT_UA 1     // (count 54.6 -> 52.5 us)
-#endif
-#ifndef RR_COUNT_HOIST   // 1: count_kernel issues its offsets loads together, the header loads next
-#define RR_COUNT_HOIST 1
-#endif
-// reserve_g + classify_g from the header dwords (same results, byte for byte)
+// The descriptor reservation (rr_format.h) and the walk class of a value from its header dwords.
 __device__ __forceinline__ void reserve_classify(const uint8_t *b, uint64_t L, const uint32_t (&d)[6],
                                                  uint64_t &r, uint32_t &c) {
     r = 0;
@@ -539,16 +403,11 @@ __device__ __forceinline__ void reserve_classify(const uint8_t *b, uint64_t L, c
         case RR_TYPE_LIST_QUICKLIST: {
             c = C_LIST;
             uint64_t p = 5, n = 0;
-#ifdef RR_COUNT_NOLIST   // timing-only builds (tools/): no list walk (wrong reservations)
-            p = L;
-#endif
             while (p < L) {
                 if (L - p < 4) break;
-#if RR_COUNT_UA   // one unaligned dword load (gfx950 serves it from one line) instead of an aligned pair
+                // one unaligned dword load (gfx950 serves it from one line; an aligned pair +
+                // alignbyte measured count 52.5 -> 54.6 us)
                 const uint64_t l = *reinterpret_cast<const u32_ua *>(b + p);
-#else
-                const uint64_t l = ld_u32_al(b, p);
-#endif
                 if (l > L - p - 4) break;
                 ++n;
                 p += 4 + l;
@@ -594,106 +453,61 @@ __device__ __forceinline__ void zero_call_words(uint64_t *words, uint32_t nwords
     if (tot && threadIdx.x < 4) reinterpret_cast<uint64_t *>(tot)[threadIdx.x] = 0;
 }
 
+// Per value: its reservation (u32; a value that would need 2^32 slots fails capacity anyway),
+// its class and first_val.  Per window: the reservations of its values summed into wtot[w], and
+// per group of WGROUP windows into gtot[w / WGROUP] (both zeroed by a memset before the launch):
+// a window's values are consecutive, so each run of one window (group) in a wave adds its sum
+// with two non-returning atomics — the inclusive wave scan at its last lane, minus the
+// exclusive scan at its first.  decode_kernel then finds its first descriptor slot from at most
+// two loads per lane (the groups before it, the windows before it in its group): no scan launch.
+constexpr uint32_t WGROUP = 64;
 __global__ __launch_bounds__(256) void count_kernel(const uint8_t *__restrict__ blob,
                                                     const uint64_t *__restrict__ offsets, uint64_t n,
                                                     uint32_t *__restrict__ first_val, uint32_t nwin, uint32_t win,
-                                                    uint64_t *__restrict__ counts, uint8_t *__restrict__ cls,
+                                                    uint32_t *__restrict__ counts, uint8_t *__restrict__ cls,
+                                                    uint64_t *wtot, uint64_t *gtot,
                                                     uint64_t *zero_words, uint32_t nzero, rr_totals *tot) {
     zero_call_words(zero_words, nzero, tot);
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i > n) return;
-    if (i == n) counts[n] = 0;   // (the scan writes the total here when there are values)
-#if RR_COUNT_HOIST
+    const uint64_t ic = i < n ? i : n;   // (every lane stays for the wave scans; i == n: first_val's sentinel)
     // the three offsets in one round trip (loads at clamped indices, no guard branch whose join
     // made the compiler wait for the first two before issuing the third), the header granules
     // in the next, issued before the first_val stores
-    const uint64_t o_hi = offsets[i];
-    const uint64_t o_lo = offsets[i ? i - 1 : 0];
-    const uint64_t b1 = offsets[i < n ? i + 1 : n];
+    const uint64_t o_hi = offsets[ic];
+    const uint64_t o_lo = offsets[ic ? ic - 1 : 0];
+    const uint64_t b1 = offsets[ic < n ? ic + 1 : n];
     uint32_t d[6];
     if (i < n) head24(blob, o_hi, b1, d);
-    const uint64_t w_lo = i == 0 ? 0 : o_lo / win + 1;
-#else
-    const uint64_t o_hi = offsets[i];
-    const uint64_t w_lo = i == 0 ? 0 : offsets[i - 1] / win + 1;
-#endif
-    // first_val[w] = first value whose first byte is at or after w*win (windows past the
-    // last value start, and the sentinel nwin, get n)
-    const uint64_t w_hi = i == n ? nwin : o_hi / win;
-    for (uint64_t w = w_lo; w <= w_hi && w <= nwin; ++w) first_val[w] = (uint32_t)i;
-    if (i < n) {
-#if !RR_COUNT_HOIST
-        const uint64_t b1 = offsets[i + 1];
-#endif
-#ifdef RR_COUNT_BYTES   // the byte-load formulation (diagnostics)
-        counts[i] = reserve_g(blob + o_hi, b1 - o_hi);
-        cls[i] = (uint8_t)classify_g(blob + o_hi, b1 - o_hi);
-#else
-#if !RR_COUNT_HOIST
-        uint32_t d[6];
-        head24(blob, o_hi, b1, d);
-#endif
-        uint64_t r;
-        uint32_t c;
-        reserve_classify(blob + o_hi, b1 - o_hi, d, r, c);
-        counts[i] = r;
-        cls[i] = (uint8_t)c;
-#endif
-    }
-}
-
-// ---- K1+K2 in one launch: count_scan_kernel -----------------------------------------------
-// count_kernel's per-value work, then the block's exclusive scan, then a decoupled look-back
-// between the 256-value blocks (blockIdx order, two-level groups, rr_device.h): the block writes
-// elem_base straight away.  The look-back's round trips (a few us under load) sit at the end of
-// each block and are hidden by the other resident blocks of the CU, so the separate scan launch
-// (its own look-back, the counts written and read again) goes away.  (A look-back that never
-// resolves — a block dispatched out of order behind a full machine — sets the call's error word
-// after the bounded wait: the host sees RR_API_EDEVICE, never a hang.)
-constexpr uint32_t CS_NT = 256;
-__global__ __launch_bounds__(CS_NT) void count_scan_kernel(const uint8_t *__restrict__ blob,
-                                                          const uint64_t *__restrict__ offsets, uint64_t n,
-                                                          uint32_t *__restrict__ first_val, uint32_t nwin, uint32_t win,
-                                                          uint64_t *__restrict__ ebase, uint8_t *__restrict__ cls,
-                                                          uint64_t *lb_state, uint64_t *lb_groups, uint32_t ntiles,
-                                                          uint64_t *err, rr_totals *tot) {
-    zero_call_words(nullptr, 0, tot);
-    __shared__ uint64_t wsum[CS_NT / RR_WAVE];
-    __shared__ uint64_t sh_pre;
-    const uint32_t tile = blockIdx.x, tid = threadIdx.x, lane = lane_id(), wave = tid / RR_WAVE;
-    const uint64_t i = (uint64_t)tile * CS_NT + tid;
-    uint64_t r = 0;
     if (i <= n) {
-        const uint64_t o_hi = offsets[i];
-        const uint64_t w_lo = i == 0 ? 0 : offsets[i - 1] / win + 1;
+        // first_val[w] = first value whose first byte is at or after w*win (windows past the
+        // last value start, and the sentinel nwin, get n)
+        const uint64_t w_lo = i == 0 ? 0 : o_lo / win + 1;
         const uint64_t w_hi = i == n ? nwin : o_hi / win;
         for (uint64_t w = w_lo; w <= w_hi && w <= nwin; ++w) first_val[w] = (uint32_t)i;
-        if (i < n) {
-            const uint64_t b1 = offsets[i + 1];
-            uint32_t d[6];
-            head24(blob, o_hi, b1, d);
-            uint32_t c;
-            reserve_classify(blob + o_hi, b1 - o_hi, d, r, c);
-            cls[i] = (uint8_t)c;
+    }
+    uint64_t r = 0;
+    uint32_t w = 0xFFFFFFFFu;   // (lanes past n: a window no value has)
+    if (i < n) {
+        uint32_t c;
+        reserve_classify(blob + o_hi, b1 - o_hi, d, r, c);
+        counts[i] = (uint32_t)(r < 0xFFFFFFFFull ? r : 0xFFFFFFFFull);
+        cls[i] = (uint8_t)c;
+        w = (uint32_t)(o_hi / win);
+    }
+    const uint64_t incl = wave_incl_scan_fast(r);
+    const uint32_t lane = lane_id(), wp = wave_from_prev(w), wn = wave_from_next(w);
+    const bool in = i < n;
+    auto run_sum = [&](uint64_t *t, uint32_t k, bool head, bool tail) __attribute__((always_inline)) {
+        if (head && tail) {
+            if (r) atomicAdd((unsigned long long *)&t[k], (unsigned long long)r);
+        } else {
+            if (head && incl != r) atomicAdd((unsigned long long *)&t[k], (unsigned long long)(0ull - (incl - r)));
+            if (tail && incl) atomicAdd((unsigned long long *)&t[k], (unsigned long long)incl);
         }
-    }
-    const uint64_t incl = wave_incl_scan(r);
-    if (lane == RR_WAVE - 1) wsum[wave] = incl;
-    __syncthreads();
-    uint64_t wpre = 0, agg = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < CS_NT / RR_WAVE; ++k) {
-        wpre += k < wave ? wsum[k] : 0;
-        agg += wsum[k];
-    }
-    if (wave == 0) {
-        const uint64_t pre = lookback(lb_state, lb_groups, tile, ntiles, agg, err);
-        if (lane == 0) sh_pre = pre;
-    }
-    __syncthreads();
-    const uint64_t pre = sh_pre;
-    if (i < n) ebase[i] = pre + wpre + incl - r;
-    if (tile == ntiles - 1 && tid == CS_NT - 1) ebase[n] = pre + agg;   // the call's descriptor total
+    };
+    run_sum(wtot, w, in & (lane == 0 || wp != w), in & (lane == RR_WAVE - 1 || wn != w));
+    const uint32_t g = w / WGROUP;
+    run_sum(gtot, g, in & (lane == 0 || wp / WGROUP != g), in & (lane == RR_WAVE - 1 || wn / WGROUP != g));
 }
 
 // ---- K2: exclusive scan of the reservations -> elem_base -------------------------------
@@ -747,9 +561,7 @@ __global__ __launch_bounds__(256) void scan_kernel(uint64_t *__restrict__ counts
     if (tile == ntiles - 1 && threadIdx.x == 255) counts[n] = sh_prefix + agg;
 }
 
-// ---- K3: tiles: mirror copy + class sort + single-class batches ------------------------
-// The exact parser, lane = value v (from global memory): the reference's status codes for
-// malformed values, zero-filled slots, capacity handling.
+// ---- K3: windows: mirror copy + class sort + single-class batches -----------------------
 // per-value contribution to the window totals (returned by value: accumulators passed by
 // reference were merged into one dynamically-addressed update and spilled to scratch)
 struct Acc {
@@ -757,25 +569,22 @@ struct Acc {
     uint64_t pay;
 };
 
-#ifdef RR_DEC_NOINL
-#define RR_COLD __noinline__
-#else
-#define RR_COLD __forceinline__
-#endif
 // Values whose descriptors need a whole-value pass the walks cannot make (duplicate keys of a
-// hash table, re-sorting a skiplist) are queued for fixup_kernel: fix[0] counts them, their
-// indices follow the FIX_HDR header words (capacity n: a value is queued at most once).
-constexpr uint32_t FIX_HDR = 4;   // [0] queued, [1] error word, [2] bad delta, [3] payload delta
-__device__ __forceinline__ void queue_fixup(uint64_t *fix, uint64_t v) {
-    const uint64_t i = atomicAdd((unsigned long long *)fix, 1ull);
-    reinterpret_cast<uint32_t *>(fix + FIX_HDR)[i] = (uint32_t)v;
+// hash table, re-sorting a skiplist) are marked for the window's fixup (fixup_window): FIX_MARK
+// in the record's status, and a count in the window's LDS word.
+constexpr uint32_t FIX_MARK_ST = 0x8000;   // (= FIX_MARK, below)
+__device__ __forceinline__ uint32_t mark_fixup(uint32_t *nfix) {
+    atomicAdd(nfix, 1u);
+    return FIX_MARK_ST;
 }
 
-// (eb, r: the value's first descriptor slot and its reservation)
-__device__ RR_COLD Acc exact_value(const uint8_t *__restrict__ blob, uint64_t v,
+// The exact parser, lane = value v (from global memory): the reference's status codes for
+// malformed values, zero-filled slots, capacity handling.  (eb, r: the value's first
+// descriptor slot and its reservation)
+__device__ __forceinline__ Acc exact_value(const uint8_t *__restrict__ blob, uint64_t v,
                                            const uint64_t *__restrict__ offsets, uint64_t eb, uint64_t r,
                                            rr_value *__restrict__ values, rr_elem *__restrict__ elems, uint64_t cap,
-                                           uint64_t *fix) {
+                                           uint32_t *nfix) {
     uint64_t pay = 0;
     const uint64_t o_lo = offsets[v], o_hi = offsets[v + 1];
     const uint8_t *b = blob + o_lo;
@@ -795,32 +604,20 @@ __device__ RR_COLD Acc exact_value(const uint8_t *__restrict__ blob, uint64_t v,
         pay += e.payload;
         const uint32_t t = ld_u8(b);
         const uint64_t keys = t == RR_TYPE_HASH_HT ? ne / 2 : ne;
-        if (((t == RR_TYPE_SET_HT || t == RR_TYPE_HASH_HT) && keys >= 2) || e.unsorted) queue_fixup(fix, v);
+        if (((t == RR_TYPE_SET_HT || t == RR_TYPE_HASH_HT) && keys >= 2) || e.unsorted) status |= mark_fixup(nfix);
     }
     const uint32_t len = (uint32_t)(o_hi - o_lo);
     put_value(values + v, len ? ld_u8(b) : 0, pr.enc, status, len >= 5 ? ld_u32(b + 1) : 0, (uint32_t)ne,
               (uint32_t)eb);
-    return Acc{status != RR_OK ? 1u : 0u, pay};
+    return Acc{(status & ~FIX_MARK_ST) != RR_OK ? 1u : 0u, pay};
 }
 
-// ziplists: 1 = grouped walks on one backward prevlen chain (do_ziplist_bg, RR_ZL_VPB values
-// per batch), 0 = two lanes per value walking from both ends (do_ziplist, DEC_BL / 2 values)
-#ifndef RR_ZL_BACK
-#define RR_ZL_BACK 1
-#endif
+// Values per batch of a class (a class with more values in the chunk gets several batches):
+// the grouped walks give each value G = min(GMAX, 64 / count) lanes, so fewer values per batch
+// means more lanes per value.  Measured: 8 or 12 ziplists per batch 3-15 % slower than 16,
+// 32 ziplists 7 % slower; 8 or 16 Lists per batch within noise.
 #ifndef RR_ZL_VPB
 #define RR_ZL_VPB 16
-#endif
-#ifndef RR_ZL_PIPE   // 1: ziplist batches run do_ziplist_bp (compile-time group size, pipelined rounds)
-#define RR_ZL_PIPE 1
-#endif
-#if RR_ZL_BACK
-constexpr uint32_t ZL_VPB = RR_ZL_VPB;
-#endif
-// hash tables: 1 = grouped walks (do_ht_g) whenever the batch gives a value enough lanes to
-// hold its keys, with RR_HH_VPB hashes / RR_HT_VPB sets per batch; 0 = lane per value (do_ht)
-#ifndef RR_HT_GROUPED
-#define RR_HT_GROUPED 1
 #endif
 #ifndef RR_HH_VPB
 #define RR_HH_VPB 8
@@ -828,51 +625,29 @@ constexpr uint32_t ZL_VPB = RR_ZL_VPB;
 #ifndef RR_HT_VPB
 #define RR_HT_VPB 16
 #endif
-#ifndef RR_LIST_PIPE   // 1: List batches run do_list_bp (compile-time group size, pipelined rounds)
-#define RR_LIST_PIPE 1     // (LIST batch 17.3K -> 12.1K cycles with 16 Lists per batch)
-#endif
-#ifndef RR_LIST_VPB   // Lists per batch (grouped: fewer Lists per batch, more lanes per List)
-#if RR_LIST_PIPE
+#ifndef RR_LIST_VPB
 #define RR_LIST_VPB 16
-#else
-#define RR_LIST_VPB 64
 #endif
-#endif
-// class batch order: heaviest walks first (longest-job-first over the window's waves)
-#ifndef RR_DEC_ORDER
-#define RR_DEC_ORDER C_ZL, C_SL, C_HH, C_HT, C_LIST, C_EXACT, C_IS, C_STR
-#endif
-__constant__ uint32_t CLASS_ORDER[C_N] = {RR_DEC_ORDER};
-// the class of batch-order slot k from registers (a select chain over the compile-time order:
-// no constant-memory load on each batch's path)
-__device__ __forceinline__ uint32_t class_at(uint32_t k) {
-    constexpr uint32_t ord[C_N] = {RR_DEC_ORDER};
-    uint32_t c = ord[0];
-#pragma unroll
-    for (uint32_t i = 1; i < C_N; ++i) c = k == i ? ord[i] : c;
-    return c;
+__device__ __forceinline__ uint32_t class_vpb(uint32_t c) {
+    return c == C_ZL ? RR_ZL_VPB : c == C_HH ? RR_HH_VPB : c == C_HT ? RR_HT_VPB : c == C_LIST ? RR_LIST_VPB : RR_WAVE;
 }
-#ifndef RR_DEC_BREG   // 1: the batch loop keeps the chunk's batch prefixes in registers
-#define RR_DEC_BREG 0   // (measured: decode_kernel -2.6 % in one trace, calls mixed, cfg 3 +1.5 %)
-#endif
+// class batch order: heaviest walks first (longest-job-first over the window's waves; hash-first
+// instead of ziplist-first measured within noise)
+__constant__ uint32_t CLASS_ORDER[C_N] = {C_ZL, C_SL, C_HH, C_HT, C_LIST, C_EXACT, C_IS, C_STR};
 
-// One single-class batch: lane < cnt decodes value v (byte offsets relative to the source,
-// whose byte 0 is batch offset B).
 // One single-class batch, run by the whole wave: lane < cnt (active) decodes value v (byte
 // offsets relative to the source, whose byte 0 is batch offset B).  The walks run the wave in
 // lock-step (rr_decode_class.h); values they reject, and the EXACT class, go to the exact
-// parser lane by lane.
-// G lanes per value (grouped walks, rr_decode_class.h), this lane being lane g of its group;
+// parser lane by lane.  G lanes per value (grouped walks), this lane being lane g of its group;
 // the group's lane 0 records the value (or runs the exact parser), every lane returns the
-// payload of the elements it stored.
-// (eb_v, r_v: value v's first descriptor slot and its reservation, for active lanes)
+// payload of the elements it stored.  (eb_v, r_v: value v's first descriptor slot and its
+// reservation, for active lanes)
 template <class Src>
 __device__ __forceinline__ Acc run_batch(const Src &src, uint32_t c, bool active, uint64_t v, uint32_t G, uint32_t g,
-                                         uint64_t B, rsrc_t E,
-                                         uint64_t eb0, const uint8_t *__restrict__ blob,
+                                         uint64_t B, rsrc_t E, uint64_t eb0, const uint8_t *__restrict__ blob,
                                          const uint64_t *__restrict__ offsets, uint64_t eb_v, uint64_t r_v,
                                          rr_value *__restrict__ values, rr_elem *__restrict__ elems, uint64_t cap,
-                                         uint64_t *fix) {
+                                         uint32_t *nfix) {
     // (one exact_value call site: the parser is large and every inlined copy costs I-cache)
     bool exact = c == C_EXACT;
     Acc acc{0, 0};
@@ -903,1093 +678,35 @@ __device__ __forceinline__ Acc run_batch(const Src &src, uint32_t c, bool active
             do_intset_g(src, H, l, active, G, g);
             ne = H.f9();
             enc = H.f5();
-        } else if (c == C_LIST) {
-#if RR_LIST_PIPE   // grouped, software-pipelined (G a power of two)
+        } else if (c == C_LIST) {   // grouped, software-pipelined (G a power of two)
             if (G >= 16) fail = do_list_bp<16>(src, l, active, g, ne, vp);
             else if (G >= 8) fail = do_list_bp<8>(src, l, active, g, ne, vp);
             else if (G >= 4) fail = do_list_bp<4>(src, l, active, g, ne, vp);
             else if (G >= 2) fail = do_list_bp<2>(src, l, active, g, ne, vp);
             else fail = do_list_bp<1>(src, l, active, g, ne, vp);
-#else
-            fail = do_list_g(src, l, active, G, g, ne, vp);
-#endif
         } else if (c == C_HT || c == C_HH) {   // grouped (G > 1) or lane per value (do_ht)
             if (G > 1) fail = do_ht_g(src, H, l, active, G, g, ne, vp, fixup, c == C_HH);
             else fail = do_ht(src, H, l, active, ne, vp, fixup, c == C_HH);
         } else if (c == C_SL) {
             fail = do_skiplist_g(src, H, l, active, G, g, ne, vp);
-        } else {
-#if RR_ZL_BACK && RR_ZL_PIPE   // C_ZL: grouped, software-pipelined (G a power of two >= 4)
+        } else {   // C_ZL: grouped on one backward prevlen chain, software-pipelined (G 4, 8 or 16)
             if (G >= 16) fail = do_ziplist_bp<16>(src, l, active, g, ne, vp);
             else if (G >= 8) fail = do_ziplist_bp<8>(src, l, active, g, ne, vp);
             else fail = do_ziplist_bp<4>(src, l, active, g, ne, vp);
-#elif RR_ZL_BACK   // C_ZL: grouped, one backward prevlen chain per value
-            fail = do_ziplist_bg(src, l, active, G, g, ne, vp);
-#else            // C_ZL: G == 2, lane 1 of the pair walks backward
-            fail = do_ziplist(src, l, active, g != 0, ne, vp);
-#endif
         }
         exact = fail;
         if (active && !fail) {
             if (g == 0) {
-                if (fixup && l.ok) queue_fixup(fix, v);
-                put_value(values + v, H.type(), enc, l.ok ? RR_OK : RR_E_CAPACITY, H.lru(), ne, (uint32_t)eb);
+                const uint32_t st = !l.ok ? (uint32_t)RR_E_CAPACITY : fixup ? mark_fixup(nfix) : (uint32_t)RR_OK;
+                put_value(values + v, H.type(), enc, st, H.lru(), ne, (uint32_t)eb);
                 acc.bad = l.ok ? 0u : 1u;
             }
             acc.pay = l.ok ? vp : 0;
         }
         active &= g == 0;   // the exact parser runs once per value, on the group's lane 0
     }
-    if (active && exact) acc = exact_value(blob, v, offsets, eb_v, r_v, values, elems, cap, fix);
+    if (active && exact) acc = exact_value(blob, v, offsets, eb_v, r_v, values, elems, cap, nfix);
     return acc;
-}
-
-// the unstaged (global-memory) instantiation: cold path, kept out of line in RR_DEC_NOINL
-// builds so the hot staged code stays small
-__device__ RR_COLD Acc run_batch_g(const GlbSrc &src, uint32_t c, bool active, uint64_t v, uint32_t G, uint32_t g,
-                                   uint64_t B, rsrc_t E, uint64_t eb0, const uint8_t *__restrict__ blob,
-                                   const uint64_t *__restrict__ offsets, uint64_t eb_v, uint64_t r_v,
-                                   rr_value *__restrict__ values, rr_elem *__restrict__ elems, uint64_t cap,
-                                   uint64_t *fix) {
-    return run_batch(src, c, active, v, G, g, B, E, eb0, blob, offsets, eb_v, r_v, values, elems, cap, fix);
-}
-
-// Workgroup per byte WINDOW of W bytes: window t owns the values whose first byte lies in
-// [t*W, (t+1)*W) (first_val from K1).  The workgroup
-//   1. streams the window into the mirror arena and, from the same loads, stages the bytes of
-//      its values (the window + the tail of its last value, up to SLACK more) into LDS;
-//   2. per chunk of <= PMAX of its values: counting-sorts them by class in LDS;
-//   3. its waves take single-class batches of <= 64 values, heaviest class first, and walk +
-//      emit them from LDS (from global memory when the values did not fit the stage).
-// Probe build (make VARIANT=probe EXTRA=-DRR_PROBE, tools/probe_decode.py): per-window phase
-// cycles and per-class batch cycles / counts / lanes into a buffer set by rr_probe_set
-// (PROBE_WORDS u64 per window).  Diagnostics only; the product build has none of it.
-#ifdef RR_PROBE
-constexpr uint32_t PROBE_WORDS = 32;
-__device__ uint64_t *g_probe;
-extern "C" int rr_probe_set(void *p) { return hipMemcpyToSymbol(HIP_SYMBOL(g_probe), &p, sizeof(p)) == hipSuccess ? 0 : -1; }
-#define PROBE(...) __VA_ARGS__
-#else
-#define PROBE(...)
-#endif
-
-// lanes per walk batch: a class's values in a chunk are cut into batches of at most DEC_BL, so
-// a class with few values per window can still spread over several waves
-#ifndef RR_DEC_BL
-#define RR_DEC_BL 64
-#endif
-constexpr uint32_t DEC_BL = RR_DEC_BL;
-static_assert(DEC_BL >= 2 && DEC_BL <= RR_WAVE && DEC_BL % 2 == 0, "batch lanes");
-// values per batch of a class (a class with more values in the chunk gets several batches)
-__device__ __forceinline__ uint32_t class_vpb(uint32_t c) {
-#if RR_ZL_BACK
-    if (c == C_ZL) return ZL_VPB;
-#else
-    if (c == C_ZL) return DEC_BL / 2;   // two lanes each
-#endif
-#if RR_HT_GROUPED
-    if (c == C_HH) return RR_HH_VPB;
-    if (c == C_HT) return RR_HT_VPB;
-#endif
-    if (c == C_LIST) return RR_LIST_VPB;
-    return DEC_BL;
-}
-// 1: the mirror-arena copy is written by waves that ran out of walk batches (step 4), not
-// during staging
-#ifndef RR_DEC_LATECOPY
-#define RR_DEC_LATECOPY 0
-#endif
-#ifndef RR_DEC_PF   // persistent workgroups, next window's arena copy overlapped with the walks
-#define RR_DEC_PF 0
-#endif
-#ifndef RR_DEC_OVL   // the window's loads in flight under the class sort (fused copy builds)
-#define RR_DEC_OVL 1
-#endif
-#if RR_DEC_LATECOPY   // (the overlap applies to the fused copy)
-#undef RR_DEC_OVL
-#define RR_DEC_OVL 0
-#endif
-#ifndef RR_DEC_OVL_K  // granules (16 B) per thread loaded before the sort (the rest after it)
-#define RR_DEC_OVL_K 9
-#endif
-// 1: the window's loads, arena stores and stage writes go through buffer resources with no
-// exec-mask branches (out-of-range loads read zeros, out-of-range stores are dropped, unstaged
-// granules are written to a dummy LDS slot), and the workgroup's barriers order LDS only.
-// The branch joins of the guarded copy made the compiler's wait-count pass wait for each
-// store's acknowledgement before the next store, and the conditional loads made the sort's
-// first barrier wait for all of them (vmcnt(0)).
-#ifndef RR_DEC_BFREE
-#define RR_DEC_BFREE 1
-#endif
-#ifndef RR_DEC_BALANCE   // 1: a class's values split evenly over its batches
-#define RR_DEC_BALANCE 0
-#endif
-#ifndef RR_DEC_PRIO   // wave priority during the walks (0: none; see the batch loop)
-#define RR_DEC_PRIO 0
-#endif
-#ifndef RR_DEC_KE   // window granules per thread loaded before the class bytes (the rest after)
-#define RR_DEC_KE 2
-#endif
-#if RR_DEC_BFREE
-#define DEC_SYNC() lds_barrier()
-#else
-#define DEC_SYNC() __syncthreads()
-#endif
-#ifndef RR_DEC_EARLY  // late-copy builds: write the arena copy from the stage before the walks, not after
-#define RR_DEC_EARLY 0
-#endif
-#ifndef RR_DEC_GLDS   // late-copy staging by global_load_lds (LDS-DMA) instead of register loads
-#define RR_DEC_GLDS 0
-#endif
-#ifndef RR_DEC_SU   // 16-byte staging loads in flight per thread (late-copy staging)
-#define RR_DEC_SU 4
-#endif
-#if RR_DEC_LATECOPY
-#define PROBE_OR_LATE(...) __VA_ARGS__
-#else
-#define PROBE_OR_LATE(...)
-#endif
-// Two 512-thread workgroups per CU = 4 waves per SIMD, so at most 128 VGPRs: the allocator is
-// told so (left to itself it takes 137 for the hash-table walk and the CU holds one workgroup).
-#ifndef RR_DEC_WPE
-#define RR_DEC_WPE 4
-#endif
-#ifndef RR_DEC_EBPF   // 1: the window's elem_base words touched under the sort (cache-warm batch loads)
-#define RR_DEC_EBPF 0
-#endif
-#ifndef RR_DEC_ATOT   // 1: decode_kernel adds its windows' totals atomically (no fold in decode_post)
-#define RR_DEC_ATOT 1
-#endif
-#if RR_DEC_WPE > 0
-#define DEC_WPE_ATTR __attribute__((amdgpu_waves_per_eu(RR_DEC_WPE)))
-#else
-#define DEC_WPE_ATTR
-#endif
-template <uint32_t W, uint32_t SLACK, uint32_t NW, uint32_t PMAX>
-__global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_kernel(const uint8_t *__restrict__ blob, uint64_t data_cap,
-                                                              const uint64_t *__restrict__ offsets, uint64_t n,
-                                                              const uint32_t *__restrict__ first_val,
-                                                              const uint8_t *__restrict__ cls,
-                                                              const uint64_t *__restrict__ ebase,
-                                                              rr_value *__restrict__ values,
-                                                              rr_elem *__restrict__ elems, uint64_t elem_cap,
-                                                              uint8_t *__restrict__ arena, uint64_t *__restrict__ stats,
-                                                              uint64_t *fix, uint32_t nwin, rr_totals *tot) {
-    constexpr uint32_t NT = NW * RR_WAVE, STAGE = W + SLACK;
-    static_assert(PMAX % NT == 0 && W % 16 == 0 && SLACK % 16 == 0, "tile shape");
-#ifndef RR_DEC_LDSPAD   // diagnostics: extra LDS per workgroup (e.g. to hold one workgroup per CU)
-#define RR_DEC_LDSPAD 0
-#endif
-    __shared__ __attribute__((aligned(16))) uint8_t stage[STAGE + 64 + RR_DEC_LDSPAD];
-    __shared__ uint16_t perm[PMAX];
-    __shared__ uint32_t ccount[C_N], cbase[C_N], ccur[C_N], bpre[C_N + 1];
-    __shared__ uint32_t next_batch;
-    __shared__ uint32_t next_copy;   // (late-copy and persistent builds)
-    (void)next_copy;
-    __shared__ uint64_t red[2][NW];
-    PROBE(__shared__ uint64_t prb[PROBE_WORDS]; uint64_t pt0 = __builtin_amdgcn_s_memtime(), pt1 = 0, pt2 = 0;
-          if (threadIdx.x < PROBE_WORDS) prb[threadIdx.x] = 0;)
-    const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid / RR_WAVE;
-#if RR_DEC_PF
-    // persistent: this workgroup's windows blockIdx.x, + gridDim.x, ...; while a window's longest
-    // walks run, the waves with no batch left copy the NEXT window to the arena (global ->
-    // global), which also leaves its bytes in the L2 for that window's LDS stage
-    for (uint32_t tile = blockIdx.x, it = 0; tile < nwin; tile += gridDim.x, ++it) {
-    if (it) DEC_SYNC();   // the previous window is done with the LDS
-    if (tid == 0) next_copy = 0;
-    PROBE(pt0 = __builtin_amdgcn_s_memtime(); if (threadIdx.x < PROBE_WORDS) prb[threadIdx.x] = 0;)
-#else
-    {
-    const uint32_t tile = blockIdx.x, it = 0;
-    (void)nwin;
-    (void)it;
-#endif
-    const uint64_t padded = (offsets[n] + 15) & ~15ull;
-    const uint64_t W0 = (uint64_t)tile * W;
-    const uint64_t W1 = W0 + W < padded ? W0 + W : padded;
-    // the arena copy starts at the call's first value (a call over a slice of a larger buffer —
-    // the chunks of rr_decode_batch_host — copies only its own bytes); the stage always lies
-    // past it (S0 >= offsets[v_lo] >= offsets[0])
-    const uint64_t A0 = W0 > (offsets[0] & ~15ull) ? W0 : (offsets[0] & ~15ull);
-#if RR_DEC_OVL && RR_DEC_BFREE
-    // the window's own granules [A0, W1) first: their range needs only offsets[0] and
-    // offsets[n], not first_val -> offsets, so the loads go out at the window's start; the
-    // stage's tail [W1, ov_e) (the last values' bytes past the window) follows the sort.  The
-    // arena gets [A0, W1) (stores past it are dropped); g = A0 / 16 + tid + k * NT is at byte
-    // offset 16 (tid + k NT)
-    constexpr uint32_t KM = W / 16 / NT;   // granules per thread of a whole window
-    static_assert(W % (16 * NT) == 0, "window granules per thread");
-    const uint64_t ov_a = A0 >> 4, ov_w1 = W1 >> 4;
-    const uint32_t ov_mb = ov_w1 > ov_a ? (uint32_t)((ov_w1 - ov_a) * 16) : 0u;
-    const rsrc_t ov_RM = make_rsrc(blob + A0, ov_mb);
-    const rsrc_t ov_RA = make_rsrc(arena + A0, ov_mb);
-    // KE granules per thread go out before the first_val -> offsets / class-byte loads, the rest
-    // after the class bytes: the sort waits (vmcnt, in issue order) for the class bytes and
-    // therefore for the early granules only
-    constexpr uint32_t KE = RR_DEC_KE < KM ? RR_DEC_KE : KM;
-    u32x4 ov_m[KM];
-#pragma unroll
-    for (uint32_t k = 0; k < KE; ++k)
-        ov_m[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ov_RM, (int)((tid + k * NT) * 16), 0, 0));
-#endif
-    const uint64_t v_lo = first_val[tile], v_hi = first_val[tile + 1];
-    uint64_t S0 = W0, S1 = W0;
-    if (v_hi > v_lo) {
-        S0 = offsets[v_lo] & ~15ull;
-        S1 = (offsets[v_hi] + 15) & ~15ull;
-    }
-    const bool staged = S1 - S0 <= STAGE;
-    const uint64_t cap = elem_cap < 0xFFFFFFFFull ? elem_cap : 0xFFFFFFFFull;   // elem_base is 32-bit
-
-    // the first chunk's class bytes, loaded before the copy so their latency hides under it
-    uint32_t cls0[PMAX / NT];
-#pragma unroll
-    for (uint32_t j = 0; j < PMAX / NT; ++j) {
-        const uint64_t v = v_lo + j * NT + tid;
-        cls0[j] = v < v_hi ? (uint32_t)cls[v] : C_N;
-    }
-#if RR_DEC_EBPF
-    // the first chunk's elem_base words touched now, in flight under the sort (into this CU's
-    // L1 and the L2), so each batch's per-value elem_base loads hit the cache instead of memory
-    uint32_t ebpf = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < PMAX / NT; ++j) {
-        const uint64_t v = v_lo + j * NT + tid;
-        ebpf |= (uint32_t)ebase[v < v_hi ? v : v_lo];
-    }
-#endif
-#if RR_DEC_OVL && RR_DEC_BFREE
-#pragma unroll
-    for (uint32_t k = KE; k < KM; ++k)
-        ov_m[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ov_RM, (int)((tid + k * NT) * 16), 0, 0));
-    // the stage's tail [W1, S1): at most SLACK bytes, KT granules per thread, also in flight
-    // under the sort
-    constexpr uint32_t KT = (SLACK / 16 + NT - 1) / NT;
-    const uint64_t ov_t0 = ov_w1 > ov_a ? ov_w1 : ov_a;
-    const uint64_t ov_te = (staged && S1 > W1 ? S1 : W1) >> 4;
-    const rsrc_t ov_RT = make_rsrc(blob + ov_t0 * 16, ov_te > ov_t0 ? (uint32_t)((ov_te - ov_t0) * 16) : 0u);
-    u32x4 ov_t[KT];
-#pragma unroll
-    for (uint32_t k = 0; k < KT; ++k)
-        ov_t[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ov_RT, (int)((tid + k * NT) * 16), 0, 0));
-#endif
-
-#if RR_DEC_LATECOPY
-    // 1. value bytes -> LDS only; the window's arena copy is written in step 4 by waves that
-    //    have run out of batches, overlapping the longest walks
-    if (tid == 0) next_copy = 0;
-#if RR_DEC_GLDS
-    // every stage load in flight at once, straight to LDS (no VGPRs): wave w fills the 1 KiB
-    // blocks w, w + NW, ... (lane-linear: lane l's 16 bytes land at block + 16 l)
-    if (staged) {
-        const uint64_t cs0 = S0 >> 4, cs1 = S1 >> 4;
-        const uint32_t nblk = (uint32_t)((cs1 - cs0 + RR_WAVE - 1) / RR_WAVE);
-        for (uint32_t b = wave; b < nblk; b += NW) {
-            const uint64_t g = cs0 + (uint64_t)b * RR_WAVE + lane;
-            if (g < cs1)
-                __builtin_amdgcn_global_load_lds((const void *)(blob + g * 16),
-                                                 (__attribute__((address_space(3))) void *)(stage + b * 16 * RR_WAVE),
-                                                 16, 0, 0);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-#else
-    if (staged) {
-        const u32x4 *src = reinterpret_cast<const u32x4 *>(blob);
-        u32x4 *lds = reinterpret_cast<u32x4 *>(stage);
-        const uint64_t cs0 = S0 >> 4, cs1 = S1 >> 4;
-        uint64_t c = cs0 + tid;
-        for (; c + (RR_DEC_SU - 1) * NT < cs1; c += RR_DEC_SU * NT) {
-            u32x4 x[RR_DEC_SU];
-#pragma unroll
-            for (int k = 0; k < RR_DEC_SU; ++k) x[k] = src[c + k * NT];
-#pragma unroll
-            for (int k = 0; k < RR_DEC_SU; ++k) lds[c + k * NT - cs0] = x[k];
-        }
-        for (; c < cs1; c += NT) lds[c - cs0] = src[c];
-    }
-#endif
-#else
-#if RR_DEC_OVL
-    // 1''. the common case (the window and its values' tail fit RR_DEC_OVL_K granules per
-    //      thread): the loads are issued here and land while the class sort below runs; the
-    //      arena stores and the LDS stage writes follow the sort (plain loads survive its
-    //      barriers).  The sort reads no global memory, so none of its waits drain them.
-    const uint64_t eb0 = ebase[v_lo], eb1 = ebase[v_hi];
-    const uint64_t ov_s0 = S0 >> 4, ov_e = (staged && S1 > W1 ? S1 : W1) >> 4;
-    const bool ovl = !(RR_DEC_PF && it > 0);
-#if RR_DEC_BFREE
-    typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
-    lds_u32x4 *ov_lds = (lds_u32x4 *)(__attribute__((address_space(3))) uint8_t *)stage;
-    // granule g's stage slot, or the dummy slot just past the stage (reads past the stage see
-    // garbage there, which the walks never use: every read is checked against its value's end)
-    auto ov_slot = [&](uint64_t g) __attribute__((always_inline)) -> uint32_t {
-        return (staged & (g >= ov_s0) & (g < ov_e)) ? (uint32_t)(g - ov_s0) : STAGE / 16;
-    };
-    auto ov_finish = [&]() __attribute__((always_inline)) {
-#pragma unroll
-        for (uint32_t k = 0; k < KM; ++k) {
-#ifndef RR_ABLATE_NOCOPY
-            __builtin_amdgcn_raw_buffer_store_b128(ov_m[k], ov_RA, (int)((tid + k * NT) * 16), 0, 2 /* nt */);
-#endif
-            ov_lds[ov_slot(ov_a + tid + (uint64_t)k * NT)] = ov_m[k];
-        }
-        // the stage's tail [W1, ov_e): LDS only
-#pragma unroll
-        for (uint32_t k = 0; k < KT; ++k) ov_lds[ov_slot(ov_t0 + tid + (uint64_t)k * NT)] = ov_t[k];
-    };
-    if (ovl) {
-    } else
-#else
-    const uint64_t ov_w1 = W1 >> 4;
-    u32x4 ov_x[RR_DEC_OVL_K];
-    if (ovl) {
-        const u32x4 *src = reinterpret_cast<const u32x4 *>(blob);
-#pragma unroll
-        for (int k = 0; k < RR_DEC_OVL_K; ++k) {
-            const uint64_t g = (A0 >> 4) + tid + (uint64_t)k * NT;
-            ov_x[k] = g < ov_e ? src[g] : u32x4{0u, 0u, 0u, 0u};
-        }
-    }
-    auto ov_finish = [&]() __attribute__((always_inline)) {
-        const u32x4 *src = reinterpret_cast<const u32x4 *>(blob);
-        u32x4 *dst = reinterpret_cast<u32x4 *>(arena);
-        u32x4 *lds = reinterpret_cast<u32x4 *>(stage);
-#pragma unroll
-        for (int k = 0; k < RR_DEC_OVL_K; ++k) {
-            const uint64_t g = (A0 >> 4) + tid + (uint64_t)k * NT;
-#ifndef RR_ABLATE_NOCOPY
-            if (g < ov_w1) __builtin_nontemporal_store(ov_x[k], dst + g);
-#endif
-            if (staged && g >= ov_s0 && g < ov_e) lds[g - ov_s0] = ov_x[k];
-        }
-        // the rest of the window (beyond the prefetched granules), loaded now
-        uint64_t c = (A0 >> 4) + tid + (uint64_t)RR_DEC_OVL_K * NT;
-        for (; c + 3 * NT < ov_e; c += 4 * NT) {
-            u32x4 x[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) x[k] = src[c + k * NT];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const uint64_t cc = c + k * NT;
-#ifndef RR_ABLATE_NOCOPY
-                if (cc < ov_w1) __builtin_nontemporal_store(x[k], dst + cc);
-#endif
-                if (staged && cc >= ov_s0) lds[cc - ov_s0] = x[k];
-            }
-        }
-        for (; c < ov_e; c += NT) {
-            const u32x4 x = src[c];
-#ifndef RR_ABLATE_NOCOPY
-            if (c < ov_w1) __builtin_nontemporal_store(x, dst + c);
-#endif
-            if (staged && c >= ov_s0) lds[c - ov_s0] = x;
-        }
-    };
-    if (ovl) {
-    } else
-#endif   // RR_DEC_BFREE
-#endif
-    if (RR_DEC_PF && it > 0) {
-        // 1'. the arena copy was made during the previous window: value bytes -> LDS only
-        //     (L2-hot: that copy just read them)
-        if (staged) {
-            const u32x4 *src = reinterpret_cast<const u32x4 *>(blob);
-            u32x4 *lds = reinterpret_cast<u32x4 *>(stage);
-            const uint64_t cs0 = S0 >> 4, cs1 = S1 >> 4;
-            uint64_t c = cs0 + tid;
-            for (; c + 3 * NT < cs1; c += 4 * NT) {
-                u32x4 x[4];
-#pragma unroll
-                for (int k = 0; k < 4; ++k) x[k] = src[c + k * NT];
-#pragma unroll
-                for (int k = 0; k < 4; ++k) lds[c + k * NT - cs0] = x[k];
-            }
-            for (; c < cs1; c += NT) lds[c - cs0] = src[c];
-        }
-    } else
-    // 1. window -> arena, value bytes -> LDS (one load feeds both)
-    {
-        const u32x4 *src = reinterpret_cast<const u32x4 *>(blob);
-        u32x4 *dst = reinterpret_cast<u32x4 *>(arena);
-        u32x4 *lds = reinterpret_cast<u32x4 *>(stage);
-        const uint64_t cw1 = W1 >> 4, cs0 = S0 >> 4;
-        const uint64_t ce = (staged && S1 > W1 ? S1 : W1) >> 4;
-        uint64_t c = (A0 >> 4) + tid;
-        for (; c + 3 * NT < ce; c += 4 * NT) {
-            u32x4 x[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) x[k] = src[c + k * NT];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const uint64_t cc = c + k * NT;
-#ifndef RR_ABLATE_NOCOPY   // timing-only builds (tools/)
-                if (cc < cw1) __builtin_nontemporal_store(x[k], dst + cc);
-#endif
-                if (staged && cc >= cs0) lds[cc - cs0] = x[k];
-            }
-        }
-        for (; c < ce; c += NT) {
-            const u32x4 x = src[c];
-#ifndef RR_ABLATE_NOCOPY
-            if (c < cw1) __builtin_nontemporal_store(x, dst + c);
-#endif
-            if (staged && c >= cs0) lds[c - cs0] = x;
-        }
-    }
-#endif
-#if RR_DEC_LATECOPY && RR_DEC_EARLY
-    // 1b. the window's arena copy straight from the LDS stage (bytes before S0, and windows
-    //     that are not staged, from global memory), before the walks start
-    __syncthreads();   // the stage is complete
-    {
-        const u32x4 *src = reinterpret_cast<const u32x4 *>(blob);
-        u32x4 *dst = reinterpret_cast<u32x4 *>(arena);
-        const u32x4 *lds = reinterpret_cast<const u32x4 *>(stage);
-        const uint64_t cw0 = W0 >> 4, cw1 = W1 >> 4, cs0 = S0 >> 4, cs1 = staged ? S1 >> 4 : cs0;
-        for (uint64_t g = cw0 + tid; g < cw1; g += NT) {
-            const u32x4 x = g >= cs0 && g < cs1 ? lds[g - cs0] : src[g];
-#ifndef RR_ABLATE_NOCOPY
-            __builtin_nontemporal_store(x, dst + g);
-#endif
-        }
-    }
-#endif
-    // values that do not fit the stage are read from global memory; if even their 32-bit
-    // window-relative byte or slot offsets could overflow, the exact parser takes them
-#if !RR_DEC_OVL
-    const uint64_t eb0 = ebase[v_lo], eb1 = ebase[v_hi];
-#endif
-    const bool far = (!staged && S1 - S0 > 0xFFFFFF00ull) || (eb1 - eb0) * 16 >= NOSLOT;
-    const LdsSrc lsrc{(lds_cptr)stage};
-    const GlbSrc gsrc{make_rsrc(blob + S0, (uint32_t)(data_cap - S0 < 0xFFFFFFFFull ? data_cap - S0 : 0xFFFFFFFFull))};
-    // the window's descriptor slots [eb0, eb1), cut at the capacity
-    const uint64_t ecut = eb1 < cap ? eb1 : cap;
-    const rsrc_t E = make_rsrc(reinterpret_cast<const uint8_t *>(elems + eb0),
-                               far || ecut <= eb0 ? 0u : (uint32_t)((ecut - eb0) * 16));
-
-    uint64_t bad = 0, pay = 0;
-#ifdef RR_ABLATE   // timing-only builds (tools/): 1 = copy + stage only, 2 = + class sort, no batches
-    const uint64_t v_end = RR_ABLATE == 1 ? v_lo : v_hi;
-#else
-    const uint64_t v_end = v_hi;
-#endif
-    // 2. counting sort of a chunk of values by class (ballot per class, one LDS atomic per
-    //    class per wave-round) into perm, class bases and batch prefixes
-    auto sort_chunk = [&](uint64_t c0) __attribute__((always_inline)) {
-        const uint32_t nv = (uint32_t)(v_hi - c0 < PMAX ? v_hi - c0 : PMAX);
-        if (tid < C_N) { ccount[tid] = 0; ccur[tid] = 0; }
-        if (tid == 0) next_batch = 0;
-        DEC_SYNC();   // also: the previous chunk's batches are done
-        PROBE(if (c0 == v_lo) pt1 = __builtin_amdgcn_s_memtime();)
-        uint32_t myc[PMAX / NT];
-#pragma unroll
-        for (uint32_t j = 0; j < PMAX / NT; ++j) {
-            const uint32_t i = j * NT + tid;
-            const uint32_t ci = c0 == v_lo ? cls0[j] : i < nv ? (uint32_t)cls[c0 + i] : C_N;
-            myc[j] = i < nv ? (far ? C_EXACT : ci) : C_N;
-            if (j * NT + wave * RR_WAVE >= nv) continue;   // (wave-uniform) no values in this round
-#pragma unroll
-            for (uint32_t c = 0; c < C_N; ++c) {
-                const uint64_t m = __ballot(myc[j] == c);
-                if (m && lane == 0) atomicAdd(&ccount[c], (uint32_t)__popcll(m));
-            }
-        }
-        DEC_SYNC();
-        if (tid == 0) {
-            uint32_t s = 0, bs = 0;
-            for (uint32_t k = 0; k < C_N; ++k) {
-                const uint32_t c = CLASS_ORDER[k];
-                const uint32_t vpb = class_vpb(c);
-                cbase[c] = s;
-                bpre[k] = bs;
-                s += ccount[c];
-                bs += (ccount[c] + vpb - 1) / vpb;
-            }
-            bpre[C_N] = bs;
-        }
-        DEC_SYNC();
-#pragma unroll
-        for (uint32_t j = 0; j < PMAX / NT; ++j) {
-            const uint32_t i = j * NT + tid;
-            if (j * NT + wave * RR_WAVE >= nv) continue;
-#pragma unroll
-            for (uint32_t c = 0; c < C_N; ++c) {
-                const uint64_t m = __ballot(myc[j] == c);
-                if (m) {
-                    uint32_t at = 0;
-                    if (lane == 0) at = atomicAdd(&ccur[c], (uint32_t)__popcll(m));
-                    at = __builtin_amdgcn_readfirstlane(at);   // (lane 0 took the atomic)
-                    if (myc[j] == c) perm[cbase[c] + at + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = (uint16_t)i;
-                }
-            }
-        }
-    };
-    if (v_end > v_lo) sort_chunk(v_lo);   // (with the window's loads still in flight)
-#if RR_DEC_OVL
-    if (ovl) ov_finish();   // they have landed under the sort
-#if RR_DEC_EBPF
-    asm volatile("" ::"v"(ebpf));   // (landed with the window's loads: keeps the touch alive)
-#endif
-#endif
-    for (uint64_t c0 = v_lo; c0 < v_end; c0 += PMAX) {
-        if (c0 != v_lo) {
-            DEC_SYNC();   // every wave is done with the previous chunk's batches
-            sort_chunk(c0);
-        }
-        DEC_SYNC();   // the stage and the chunk's sort are complete
-
-        PROBE(if (c0 == v_lo) pt2 = __builtin_amdgcn_s_memtime();)
-        // 3. single-class batches, taken dynamically by the waves
-#if defined(RR_ABLATE) && RR_ABLATE == 2
-        const uint32_t nb = 0;
-#else
-        const uint32_t nb = bpre[C_N];
-#endif
-#if RR_DEC_BREG   // the chunk's batch prefixes, read once (wave-uniform)
-        uint32_t bp[C_N + 1];
-#pragma unroll
-        for (uint32_t k = 0; k <= C_N; ++k) bp[k] = __builtin_amdgcn_readfirstlane(bpre[k]);
-#endif
-        for (;;) {
-            uint32_t bi = 0;
-            if (lane == 0) bi = atomicAdd(&next_batch, 1u);
-            bi = __builtin_amdgcn_readfirstlane(bi);
-            if (bi >= nb) break;
-#if RR_DEC_BREG
-            uint32_t k = 0, bk = bp[0];
-#pragma unroll
-            for (uint32_t i = 1; i < C_N; ++i) {
-                const bool ge = bi >= bp[i];
-                k = ge ? i : k;
-                bk = ge ? bp[i] : bk;
-            }
-            const uint32_t c = class_at(k);
-#define BPRE_K bk
-#else
-            uint32_t k = 0;
-            while (bi >= bpre[k + 1]) ++k;
-            const uint32_t c = CLASS_ORDER[k];
-#define BPRE_K bpre[k]
-#endif
-#if RR_DEC_BALANCE   // the class's values split evenly over its batches (same batch count)
-            const uint32_t vpb0 = class_vpb(c), nbc = (ccount[c] + vpb0 - 1) / vpb0;
-            const uint32_t vpb = (ccount[c] + nbc - 1) / nbc;
-#else
-            const uint32_t vpb = class_vpb(c);
-#endif
-            const uint32_t first = cbase[c] + (bi - BPRE_K) * vpb;
-            const uint32_t cnt = min(ccount[c] - (bi - BPRE_K) * vpb, vpb);
-#undef BPRE_K
-#ifdef RR_SKIP_CLASSES   // timing-only builds (tools/): skip the batches of these classes
-            if ((RR_SKIP_CLASSES >> c) & 1) continue;
-#endif
-            PROBE(const uint64_t tb0 = __builtin_amdgcn_s_memtime();)
-#if RR_DEC_PRIO == 1   // the long chained classes issue ahead of the other waves of their SIMD
-            if (c == C_HH || c == C_ZL || c == C_LIST || c == C_HT) __builtin_amdgcn_s_setprio(2);
-#elif RR_DEC_PRIO == 2   // every walk ahead of the copy / sort phases of the other workgroup
-            __builtin_amdgcn_s_setprio(1);
-#endif
-            // lanes per value: ziplists 2 (two-ended walk), chained classes 64 / cnt (grouped walks)
-            const bool grouped = c == C_LIST || c == C_SL || c == C_IS || (RR_ZL_BACK && c == C_ZL);
-            const uint32_t Gw = max(1u, min(GMAX, (uint32_t)RR_WAVE / cnt));
-#if RR_HT_GROUPED   // grouped hash-table walks when a value gets lanes enough for its keys
-            const bool htg = (c == C_HT || c == C_HH) && Gw >= ht_group_min(c == C_HH);
-#else
-            const bool htg = false;
-#endif
-            // (hash tables: a power of two, so a value's lanes lie in one DPP row, do_ht_g)
-            const uint32_t Gh = 1u << (31 - __builtin_clz(Gw));
-            const bool pow2 = htg || (RR_ZL_PIPE && c == C_ZL) || (RR_LIST_PIPE && c == C_LIST);   // (ziplists: G 4, 8 or 16)
-            const uint32_t G = __builtin_amdgcn_readfirstlane((c == C_ZL && !RR_ZL_BACK) ? 2u : pow2 ? Gh : grouped ? Gw : 1u);
-            const uint32_t li = lane / G, g = lane - li * G;   // the value's index in the batch
-            const bool active = li < cnt;
-            const uint64_t v = c0 + (active ? perm[first + li] : 0u);
-            uint64_t eb_v = eb0, r_v = 0;
-            if (active) { eb_v = ebase[v]; r_v = ebase[v + 1] - eb_v; }
-#ifndef RR_DEC_NOGLOBAL
-            const Acc a = staged ? run_batch(lsrc, c, active, v, G, g, S0, E, eb0, blob, offsets, eb_v, r_v, values, elems,
-                                             cap, fix)
-                                 : run_batch_g(gsrc, c, active, v, G, g, S0, E, eb0, blob, offsets, eb_v, r_v, values,
-                                               elems, cap, fix);
-#else   // timing-only builds (tools/): no unstaged walks (wrong for windows that overflow the stage)
-            const Acc a = run_batch(lsrc, c, active, v, G, g, S0, E, eb0, blob, offsets, eb_v, r_v, values, elems, cap, fix);
-            (void)gsrc;
-#endif
-#if RR_DEC_PRIO
-            __builtin_amdgcn_s_setprio(0);
-#endif
-            bad += a.bad;
-            pay += a.pay;
-            PROBE(if (lane == 0) {
-                atomicAdd((unsigned long long *)&prb[3 + c], (unsigned long long)(__builtin_amdgcn_s_memtime() - tb0));
-                atomicAdd((unsigned long long *)&prb[3 + C_N + c], 1ull);
-                atomicAdd((unsigned long long *)&prb[3 + 2 * C_N + c], (unsigned long long)cnt);
-            })
-        }
-    }
-#if RR_DEC_PF
-    {   // 4'. the next window's mirror-arena copy, 4 KiB tasks taken by waves with no batch left
-        const uint32_t ntile = tile + gridDim.x;
-        const uint64_t nW0 = (uint64_t)ntile * W, nW1 = nW0 + W < padded ? nW0 + W : padded;
-        if (ntile < nwin && nW1 > nW0) {
-            if (v_end == v_lo) DEC_SYNC();   // (no chunk ran: order next_copy's reset)
-            const uint64_t cw0 = nW0 >> 4, cw1 = nW1 >> 4;
-            constexpr uint32_t TASK = 4 * RR_WAVE;   // 16-byte granules per task
-            const uint32_t ntask = (uint32_t)((cw1 - cw0 + TASK - 1) / TASK);
-            // buffer resources over the next window: no exec-mask branches around the stores
-            const rsrc_t RL = make_rsrc(blob + nW0, (uint32_t)(nW1 - nW0));
-            const rsrc_t RA = make_rsrc(arena + nW0, (uint32_t)(nW1 - nW0));
-            for (;;) {
-                uint32_t ti = 0;
-                if (lane == 0) ti = atomicAdd(&next_copy, 1u);
-                ti = __builtin_amdgcn_readfirstlane(ti);
-                if (ti >= ntask) break;
-                u32x4 x[4];
-#pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    x[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                         RL, (int)((ti * TASK + lane + k * RR_WAVE) * 16), 0, 0));
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-#ifndef RR_ABLATE_NOCOPY
-                    __builtin_amdgcn_raw_buffer_store_b128(x[k], RA, (int)((ti * TASK + lane + k * RR_WAVE) * 16), 0, 2);
-#endif
-                }
-            }
-        }
-    }
-#endif
-#if RR_DEC_LATECOPY && !RR_DEC_EARLY
-    // 4. the window's mirror-arena copy in 4 KiB tasks, taken by each wave as soon as it has no
-    //    batch left (from the LDS stage where the window's bytes are staged, else from global)
-    {
-        if (v_end == v_lo) __syncthreads();   // (no chunk ran: order next_copy's reset)
-        const u32x4 *src = reinterpret_cast<const u32x4 *>(blob);
-        u32x4 *dst = reinterpret_cast<u32x4 *>(arena);
-        const u32x4 *lds = reinterpret_cast<const u32x4 *>(stage);
-        const uint64_t cw0 = W0 >> 4, cw1 = W1 >> 4, cs0 = S0 >> 4, cs1 = staged ? S1 >> 4 : cs0;
-        constexpr uint32_t TASK = 4 * RR_WAVE;   // 16-byte granules per task
-        const uint32_t ntask = (uint32_t)((cw1 - cw0 + TASK - 1) / TASK);
-        for (;;) {
-            uint32_t ti = 0;
-            if (lane == 0) ti = atomicAdd(&next_copy, 1u);
-            ti = __builtin_amdgcn_readfirstlane(ti);
-            if (ti >= ntask) break;
-            const uint64_t g0 = cw0 + (uint64_t)ti * TASK + lane;
-            u32x4 x[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const uint64_t g = g0 + k * RR_WAVE;
-                if (g < cw1) x[k] = g >= cs0 && g < cs1 ? lds[g - cs0] : src[g];
-            }
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const uint64_t g = g0 + k * RR_WAVE;
-                if (g < cw1) __builtin_nontemporal_store(x[k], dst + g);
-            }
-        }
-    }
-#endif
-    bad = wave_sum_fast(bad);
-    pay = wave_sum_fast(pay);
-    if (lane == 0) { red[0][wave] = bad; red[1][wave] = pay; }
-    DEC_SYNC();
-    if (tid == 0) {
-        uint64_t tb = 0, tp = 0;
-        for (uint32_t w = 0; w < NW; ++w) { tb += red[0][w]; tp += red[1][w]; }
-#if RR_DEC_ATOT
-        // the window's {bad, payload} straight into the call's totals (zeroed by count_kernel):
-        // two non-returning atomics per window, ~7K per call spread over the kernel, so
-        // decode_post has no fold to do (7.3 -> 5.6 us)
-        (void)stats;
-        if (tot && tb) atomicAdd((unsigned long long *)&tot->n_bad, (unsigned long long)tb);
-        if (tot && tp) atomicAdd((unsigned long long *)&tot->payload, (unsigned long long)tp);
-#else
-        (void)tot;
-        stats[3 * (uint64_t)tile + 0] = tb;
-        stats[3 * (uint64_t)tile + 1] = tp;
-        stats[3 * (uint64_t)tile + 2] = 0;
-#endif
-        PROBE(prb[0] = pt1 - pt0; prb[1] = pt2 - pt1; prb[2] = __builtin_amdgcn_s_memtime() - pt2; prb[28] = v_hi - v_lo;
-              prb[29] = staged; if (g_probe) for (uint32_t i = 0; i < PROBE_WORDS; ++i) g_probe[(uint64_t)tile * PROBE_WORDS + i] = prb[i];)
-    }
-    }   // window
-}
-
-// ---- fused decode: one pass over the windows -------------------------------------------
-// decode_fused_kernel replaces count_kernel + scan_kernel + decode_kernel: a window classifies
-// and reserves its own values from its LDS stage (pass A, thread per value; a List walks its
-// length chain in LDS), publishes the window's descriptor total right away, sorts its values by
-// class and lays out their window-relative slot offsets while the earlier windows' totals come
-// in, then resolves its first slot by a decoupled look-back over the windows (rr_device.h) and
-// walks + emits the single-class batches as decode_kernel does.  No value header is read from
-// global memory twice.  dec_index_kernel before it only reads the offsets (the first value of
-// every window) and zeroes the call's words.
-
-// reserve_classify over a byte source (the LDS stage, or global memory through a buffer
-// resource for a window whose values overflow the stage): same results, byte for byte
-__device__ __forceinline__ uint64_t rfl64(uint64_t x) {   // a wave-uniform 64-bit value into SGPRs
-    return (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)x) |
-           ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)) << 32);
-}
-
-template <class Src>
-__device__ __forceinline__ void classify_reserve_src(const Src &S, uint32_t q, uint64_t L, const uint8_t *b_glb,
-                                                     uint32_t &c, uint64_t &r) {
-    r = 0;
-    c = C_EXACT;
-    if (L < 5) return;
-    uint32_t d[6];
-    S.template get<6>(q, d);
-    const uint32_t t = d[0] & 0xFF;
-    const uint32_t f5 = __builtin_amdgcn_alignbyte(d[2], d[1], 1), f9 = __builtin_amdgcn_alignbyte(d[3], d[2], 1);
-    const uint32_t f13 = __builtin_amdgcn_alignbyte(d[4], d[3], 1);
-    const uint64_t u5 = (uint64_t)f5 | ((uint64_t)f9 << 32);
-    switch (t) {
-        case RR_TYPE_STRING: {
-            if (L < 6) return;
-            r = 1;
-            const uint32_t enc = (d[1] >> 8) & 0xFF;
-            const uint64_t rest = L - 6;
-            if (enc == RR_ENC_INT) c = rest == 8 ? C_STR : C_EXACT;
-            else if (enc == RR_ENC_EMBSTR) c = rest <= RR_EMBSTR_SIZE_LIMIT ? C_STR : C_EXACT;
-            else if (enc == RR_ENC_RAW) c = rest <= 0xFFFFFFFFull ? C_STR : C_EXACT;
-            return;
-        }
-        case RR_TYPE_LIST_QUICKLIST: {   // the length chain (the count the walk will take)
-            c = C_LIST;
-            uint64_t p = 5, n = 0;
-            while (p < L) {
-                if (L - p < 4) break;
-                uint32_t x[1];
-                S.template get<1>(q + (uint32_t)p, x);
-                const uint64_t l = x[0];
-                if (l > L - p - 4) break;
-                ++n;
-                p += 4 + l;
-            }
-            r = n;
-            return;
-        }
-        default:
-            break;
-    }
-    if (L < 13) return;
-    switch (t) {
-        case RR_TYPE_SET_INTSET: {
-            const uint64_t w = f5, cnt = f9;
-            const bool ok = (w == 2 || w == 4 || w == 8) && L - 13 == w * cnt;
-            r = ok ? cnt : 0;
-            c = ok ? C_IS : C_EXACT;
-            return;
-        }
-        case RR_TYPE_SET_HT: { const uint64_t m = (L - 13) / 8; r = u5 < m ? u5 : m; c = C_HT; return; }
-        case RR_TYPE_HASH_HT: { const uint64_t m = (L - 13) / 8; r = u5 > m / 2 ? m : 2 * u5; c = C_HH; return; }
-        case RR_TYPE_ZSET_SKIPLIST: { const uint64_t m = (L - 13) / 16; r = 2 * (u5 < m ? u5 : m); c = C_SL; return; }
-        case RR_TYPE_HASH_ZIPLIST:
-        case RR_TYPE_ZSET_ZIPLIST: {
-            const uint64_t Lz = u5;
-            c = (L >= 24 && Lz == L - 13 && f13 == Lz) ? C_ZL : C_EXACT;
-            if (Lz != L - 13 || Lz < 11) return;
-            const uint64_t zllen = (d[5] >> 8) & 0xFFFF;
-            if (zllen != 0xFFFF) { const uint64_t m = (Lz - 11) / 2; r = 1 + (zllen < m ? zllen : m); return; }
-            r = 1 + zl_walk_count_g(b_glb + 13, Lz);   // (a saturated count: rare, from global memory)
-            return;
-        }
-        default:
-            return;
-    }
-}
-
-// zeroes the call's words (window look-back state, fixup header, totals) and finds the first
-// value of every window from the offsets alone
-__global__ __launch_bounds__(256) void dec_index_kernel(const uint64_t *__restrict__ offsets, uint64_t n,
-                                                        uint32_t *__restrict__ first_val, uint32_t nwin, uint32_t win,
-                                                        uint64_t *zero_words, uint32_t nzero, rr_totals *tot) {
-    zero_call_words(zero_words, nzero, tot);
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i > n) return;
-    const uint64_t o_hi = offsets[i];
-    const uint64_t w_lo = i == 0 ? 0 : offsets[i - 1] / win + 1;
-    const uint64_t w_hi = i == n ? nwin : o_hi / win;
-    for (uint64_t w = w_lo; w <= w_hi && w <= nwin; ++w) first_val[w] = (uint32_t)i;
-}
-
-template <uint32_t W, uint32_t SLACK, uint32_t NW, uint32_t PMAX>
-__global__ __launch_bounds__(NW * RR_WAVE) DEC_WPE_ATTR void decode_fused_kernel(
-    const uint8_t *__restrict__ blob, uint64_t data_cap, const uint64_t *__restrict__ offsets, uint64_t n,
-    const uint32_t *__restrict__ first_val, uint8_t *__restrict__ cls, uint32_t *__restrict__ cnt,
-    rr_value *__restrict__ values, rr_elem *__restrict__ elems, uint64_t elem_cap, uint8_t *__restrict__ arena,
-    uint64_t *__restrict__ stats, uint64_t *fix, uint32_t nwin, uint64_t *lb_state, uint64_t *lb_groups,
-    uint64_t *total) {
-    constexpr uint32_t NT = NW * RR_WAVE, STAGE = W + SLACK;
-    // a chunk of values is one pass-A round: thread i holds value i of every chunk, so the class
-    // and reservation it wrote for a later chunk are its own writes when it reads them back
-    static_assert(PMAX == NT && W % 16 == 0 && SLACK % 16 == 0, "tile shape");
-    __shared__ __attribute__((aligned(16))) uint8_t stage[STAGE + 64];
-    __shared__ uint16_t perm[PMAX];
-    __shared__ uint32_t eloc[PMAX + 1];   // window-relative first slot of the chunk's values
-    __shared__ uint32_t ccount[C_N], cbase[C_N], ccur[C_N], bpre[C_N + 1];
-    __shared__ uint32_t next_batch;
-    __shared__ uint64_t red[2][NW];
-    __shared__ uint64_t sh_eb0;
-    PROBE(__shared__ uint64_t prb[PROBE_WORDS]; uint64_t pt0 = __builtin_amdgcn_s_memtime(), pt1 = 0, pt2 = 0;
-          if (threadIdx.x < PROBE_WORDS) prb[threadIdx.x] = 0;)
-    const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid / RR_WAVE;
-    const uint32_t tile = blockIdx.x;
-    const uint64_t padded = (offsets[n] + 15) & ~15ull;
-    const uint64_t W0 = (uint64_t)tile * W;
-    const uint64_t W1 = W0 + W < padded ? W0 + W : padded;
-    const uint64_t A0 = W0 > (offsets[0] & ~15ull) ? W0 : (offsets[0] & ~15ull);
-    // 1. the window's loads (as decode_kernel: buffer resources, no exec-mask branches)
-    constexpr uint32_t KM = W / 16 / NT;
-    static_assert(W % (16 * NT) == 0, "window granules per thread");
-    const uint64_t ov_a = A0 >> 4, ov_w1 = W1 >> 4;
-    const uint32_t ov_mb = ov_w1 > ov_a ? (uint32_t)((ov_w1 - ov_a) * 16) : 0u;
-    const rsrc_t ov_RM = make_rsrc(blob + A0, ov_mb);
-    const rsrc_t ov_RA = make_rsrc(arena + A0, ov_mb);
-    u32x4 ov_m[KM];
-#pragma unroll
-    for (uint32_t k = 0; k < KM; ++k)
-        ov_m[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ov_RM, (int)((tid + k * NT) * 16), 0, 0));
-    const uint64_t v_lo = first_val[tile], v_hi = first_val[tile + 1];
-    uint64_t S0 = W0, S1 = W0;
-    if (v_hi > v_lo) {
-        S0 = offsets[v_lo] & ~15ull;
-        S1 = (offsets[v_hi] + 15) & ~15ull;
-    }
-    const bool staged = S1 - S0 <= STAGE;
-    const uint64_t cap = elem_cap < 0xFFFFFFFFull ? elem_cap : 0xFFFFFFFFull;   // elem_base is 32-bit
-    constexpr uint32_t KT = (SLACK / 16 + NT - 1) / NT;
-    const uint64_t ov_t0 = ov_w1 > ov_a ? ov_w1 : ov_a;
-    const uint64_t ov_te = (staged && S1 > W1 ? S1 : W1) >> 4;
-    const rsrc_t ov_RT = make_rsrc(blob + ov_t0 * 16, ov_te > ov_t0 ? (uint32_t)((ov_te - ov_t0) * 16) : 0u);
-    u32x4 ov_t[KT];
-#pragma unroll
-    for (uint32_t k = 0; k < KT; ++k)
-        ov_t[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ov_RT, (int)((tid + k * NT) * 16), 0, 0));
-    // the window's first values' offsets, loaded while the window lands
-    const uint64_t v0 = v_lo + tid;
-    uint64_t o0 = 0, o1 = 0;
-    if (v0 < v_hi) { o0 = offsets[v0]; o1 = offsets[v0 + 1]; }
-    // 2. window -> arena (nontemporal), value bytes -> the LDS stage
-    {
-        const uint64_t ov_s0 = S0 >> 4;
-        typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
-        lds_u32x4 *ov_lds = (lds_u32x4 *)(__attribute__((address_space(3))) uint8_t *)stage;
-        auto ov_slot = [&](uint64_t g) __attribute__((always_inline)) -> uint32_t {
-            return (staged & (g >= ov_s0) & (g < ov_te)) ? (uint32_t)(g - ov_s0) : STAGE / 16;
-        };
-#pragma unroll
-        for (uint32_t k = 0; k < KM; ++k) {
-            __builtin_amdgcn_raw_buffer_store_b128(ov_m[k], ov_RA, (int)((tid + k * NT) * 16), 0, 2 /* nt */);
-            ov_lds[ov_slot(ov_a + tid + (uint64_t)k * NT)] = ov_m[k];
-        }
-#pragma unroll
-        for (uint32_t k = 0; k < KT; ++k) ov_lds[ov_slot(ov_t0 + tid + (uint64_t)k * NT)] = ov_t[k];
-    }
-    const bool far = !staged && S1 - S0 > 0xFFFFFF00ull;
-    const LdsSrc lsrc{(lds_cptr)stage};
-    const GlbSrc gsrc{make_rsrc(blob + S0, (uint32_t)(data_cap - S0 < 0xFFFFFFFFull ? data_cap - S0 : 0xFFFFFFFFull))};
-    DEC_SYNC();   // the stage is complete
-    PROBE(pt1 = __builtin_amdgcn_s_memtime();)
-
-    // 3. pass A: class and reservation of every value of the window (thread per value); the
-    //    first chunk's stay in registers, later chunks' go to cls / cnt for the same thread
-    uint32_t c_first = C_N;
-    uint64_t r_first = 0, agg = 0;
-    for (uint64_t r0 = v_lo; r0 < v_hi; r0 += NT) {
-        const uint64_t v = r0 + tid;
-        uint32_t c = C_N;
-        uint64_t r = 0;
-        if (v < v_hi) {
-            const uint64_t o = r0 == v_lo ? o0 : offsets[v], o_end = r0 == v_lo ? o1 : offsets[v + 1];
-            const uint64_t L = o_end - o;
-            if (far) {
-                c = C_EXACT;
-                r = reserve_g(blob + o, L);
-            } else if (staged) {
-                classify_reserve_src(lsrc, (uint32_t)(o - S0), L, blob + o, c, r);
-            } else {
-                classify_reserve_src(gsrc, (uint32_t)(o - S0), L, blob + o, c, r);
-            }
-            r = r < 0xFFFFFFFFull ? r : 0xFFFFFFFFull;
-            if (r0 == v_lo) { c_first = c; r_first = r; }
-        }
-        agg += r;
-    }
-    // (a later chunk classifies its values again in step 4: a class written to global memory
-    // here and read back there could come from a stale line of the CU's L1, which the other
-    // workgroup on the CU may have filled; only multi-chunk windows pay this)
-    (void)cls; (void)cnt;
-    agg = wave_sum(agg);
-    if (lane == 0) red[0][wave] = agg;
-    DEC_SYNC();
-    agg = 0;
-#pragma unroll
-    for (uint32_t w = 0; w < NW; ++w) agg += red[0][w];
-    agg = rfl64(agg);
-#ifdef RR_FUSED_NOLB   // timing-only builds (tools/): no look-back (every window's first slot is 0: wrong)
-    const bool nolb = true;
-#else
-    const bool nolb = false;
-#endif
-    if (wave == 0 && !nolb) lb_publish(lb_state, lb_groups, tile, agg);   // the window's total, as early as possible
-    // a window whose descriptor byte offsets overflow the 32-bit slot resource: exact parser
-    const bool far2 = far || agg * 16 >= NOSLOT;
-    PROBE(pt2 = __builtin_amdgcn_s_memtime();)
-
-    uint64_t bad = 0, pay = 0;
-    bool have_eb0 = false;
-    uint64_t eb0 = 0;
-    uint32_t run = 0;   // window-relative slots of the earlier chunks
-    for (uint64_t c0 = v_lo; c0 < v_hi; c0 += PMAX) {
-        const uint32_t nv = (uint32_t)(v_hi - c0 < PMAX ? v_hi - c0 : PMAX);
-        if (tid < C_N) { ccount[tid] = 0; ccur[tid] = 0; }
-        if (tid == 0) next_batch = 0;
-        DEC_SYNC();   // (also: every wave is done with the previous chunk's batches)
-        // 4. counting sort of the chunk by class + its window-relative slot offsets
-        const uint64_t v = c0 + tid;
-        const bool in = tid < nv;
-        uint32_t myc = C_N, myr = 0;
-        if (in) {
-            if (c0 == v_lo) { myc = c_first; myr = (uint32_t)r_first; }
-            else {
-                const uint64_t o = offsets[v], L = offsets[v + 1] - o;
-                uint64_t r = 0;
-                if (far) { myc = C_EXACT; r = reserve_g(blob + o, L); }
-                else if (staged) classify_reserve_src(lsrc, (uint32_t)(o - S0), L, blob + o, myc, r);
-                else classify_reserve_src(gsrc, (uint32_t)(o - S0), L, blob + o, myc, r);
-                myr = (uint32_t)(r < 0xFFFFFFFFull ? r : 0xFFFFFFFFull);
-            }
-            myc = far2 ? C_EXACT : myc;
-        }
-        if (wave * RR_WAVE < nv) {
-#pragma unroll
-            for (uint32_t c = 0; c < C_N; ++c) {
-                const uint64_t m = __ballot(myc == c);
-                if (m && lane == 0) atomicAdd(&ccount[c], (uint32_t)__popcll(m));
-            }
-        }
-        const uint64_t incl = wave_incl_scan((uint64_t)myr);
-        if (lane == RR_WAVE - 1) red[1][wave] = incl;
-        DEC_SYNC();
-        uint64_t wpre = 0, ctot = 0;
-#pragma unroll
-        for (uint32_t w = 0; w < NW; ++w) {
-            const uint64_t x = red[1][w];
-            wpre += w < wave ? x : 0;
-            ctot += x;
-        }
-        ctot = rfl64(ctot);
-        if (in) eloc[tid] = run + (uint32_t)(wpre + incl - myr);
-        if (tid == 0) {
-            eloc[nv] = run + (uint32_t)ctot;
-            uint32_t s = 0, bs = 0;
-            for (uint32_t k = 0; k < C_N; ++k) {
-                const uint32_t c = CLASS_ORDER[k];
-                const uint32_t vpb = class_vpb(c);
-                cbase[c] = s;
-                bpre[k] = bs;
-                s += ccount[c];
-                bs += (ccount[c] + vpb - 1) / vpb;
-            }
-            bpre[C_N] = bs;
-        }
-        run += (uint32_t)ctot;
-        DEC_SYNC();
-        if (wave * RR_WAVE < nv) {
-#pragma unroll
-            for (uint32_t c = 0; c < C_N; ++c) {
-                const uint64_t m = __ballot(myc == c);
-                if (m) {
-                    uint32_t at = 0;
-                    if (lane == 0) at = atomicAdd(&ccur[c], (uint32_t)__popcll(m));
-                    at = __builtin_amdgcn_readfirstlane(at);   // (lane 0 took the atomic)
-                    if (myc == c) perm[cbase[c] + at + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = (uint16_t)tid;
-                }
-            }
-        }
-        // 5. the window's first slot: the look-back over the earlier windows' totals (resolved
-        //    once, by wave 0, after the first chunk's sort — their totals had time to arrive)
-        if (!have_eb0) {
-            if (nolb) { if (tid == 0) sh_eb0 = 0; }
-            else if (wave == 0) {
-                const uint64_t pre = lb_resolve(lb_state, lb_groups, tile, nwin, agg, fix + 1);
-                if (lane == 0) {
-                    sh_eb0 = pre;
-                    if (tile == nwin - 1) *total = pre + agg;
-                }
-            }
-            have_eb0 = true;
-        }
-        DEC_SYNC();   // the chunk's sort, its slot offsets and the window's first slot are complete
-        eb0 = rfl64(sh_eb0);
-        // the window's descriptor slots [eb0, eb0 + agg), cut at the capacity
-        const uint64_t eb1 = eb0 + agg;
-        const uint64_t ecut = eb1 < cap ? eb1 : cap;
-        const rsrc_t E = make_rsrc(reinterpret_cast<const uint8_t *>(elems + eb0),
-                                   far2 || ecut <= eb0 ? 0u : (uint32_t)((ecut - eb0) * 16));
-        // 6. single-class batches, taken dynamically by the waves
-        const uint32_t nb = __builtin_amdgcn_readfirstlane(bpre[C_N]);
-        for (;;) {
-            uint32_t bi = 0;
-            if (lane == 0) bi = atomicAdd(&next_batch, 1u);
-            bi = __builtin_amdgcn_readfirstlane(bi);
-            if (bi >= nb) break;
-            uint32_t k = 0;
-            while (bi >= bpre[k + 1]) ++k;
-            const uint32_t c = CLASS_ORDER[k];
-            const uint32_t vpb = class_vpb(c);
-            const uint32_t first = cbase[c] + (bi - bpre[k]) * vpb;
-            const uint32_t bcnt = min(ccount[c] - (bi - bpre[k]) * vpb, vpb);
-            PROBE(const uint64_t tb0 = __builtin_amdgcn_s_memtime();)
-            const bool grouped = c == C_LIST || c == C_SL || c == C_IS || (RR_ZL_BACK && c == C_ZL);
-            const uint32_t Gw = max(1u, min(GMAX, (uint32_t)RR_WAVE / bcnt));
-#if RR_HT_GROUPED
-            const bool htg = (c == C_HT || c == C_HH) && Gw >= ht_group_min(c == C_HH);
-#else
-            const bool htg = false;
-#endif
-            const uint32_t Gh = 1u << (31 - __builtin_clz(Gw));
-            const bool pow2 = htg || (RR_ZL_PIPE && c == C_ZL) || (RR_LIST_PIPE && c == C_LIST);   // (ziplists: G 4, 8 or 16)
-            const uint32_t G = __builtin_amdgcn_readfirstlane((c == C_ZL && !RR_ZL_BACK) ? 2u : pow2 ? Gh : grouped ? Gw : 1u);
-            const uint32_t li = lane / G, g = lane - li * G;
-            const bool active = li < bcnt;
-            const uint32_t pi = active ? perm[first + li] : 0u;
-            const uint64_t vv = c0 + pi;
-            const uint64_t eb_v = eb0 + eloc[pi], r_v = active ? eloc[pi + 1] - eloc[pi] : 0;
-            const Acc a = staged ? run_batch(lsrc, c, active, vv, G, g, S0, E, eb0, blob, offsets, eb_v, r_v, values,
-                                             elems, cap, fix)
-                                 : run_batch_g(gsrc, c, active, vv, G, g, S0, E, eb0, blob, offsets, eb_v, r_v, values,
-                                               elems, cap, fix);
-            bad += a.bad;
-            pay += a.pay;
-            PROBE(if (lane == 0) {
-                atomicAdd((unsigned long long *)&prb[3 + c], (unsigned long long)(__builtin_amdgcn_s_memtime() - tb0));
-                atomicAdd((unsigned long long *)&prb[3 + C_N + c], 1ull);
-                atomicAdd((unsigned long long *)&prb[3 + 2 * C_N + c], (unsigned long long)bcnt);
-            })
-        }
-    }
-    if (v_hi == v_lo && wave == 0 && !nolb) {   // a window with no values still takes part in the look-back
-        const uint64_t pre = lb_resolve(lb_state, lb_groups, tile, nwin, agg, fix + 1);
-        if (lane == 0 && tile == nwin - 1) *total = pre + agg;
-    }
-    bad = wave_sum_fast(bad);
-    pay = wave_sum_fast(pay);
-    if (lane == 0) { red[0][wave] = bad; red[1][wave] = pay; }
-    DEC_SYNC();
-    if (tid == 0) {
-        uint64_t tb = 0, tp = 0;
-        for (uint32_t w = 0; w < NW; ++w) { tb += red[0][w]; tp += red[1][w]; }
-        stats[3 * (uint64_t)tile + 0] = tb;
-        stats[3 * (uint64_t)tile + 1] = tp;
-        stats[3 * (uint64_t)tile + 2] = 0;
-        PROBE(prb[0] = pt1 - pt0; prb[1] = pt2 - pt1; prb[2] = __builtin_amdgcn_s_memtime() - pt2; prb[28] = v_hi - v_lo;
-              prb[29] = staged; if (g_probe) for (uint32_t i = 0; i < PROBE_WORDS; ++i) g_probe[(uint64_t)tile * PROBE_WORDS + i] = prb[i];)
-    }
 }
 
 struct ElemV {
@@ -2002,16 +719,10 @@ __device__ __forceinline__ ElemV get_elem(const rr_elem *e) {
     return ElemV{(uint64_t)w.x | ((uint64_t)w.y << 32), w.z, w.w & 0xFF};
 }
 
-#ifndef RR_SCAN_DPP   // 1: block_excl_scan's wave scan in DPP (u32) when no lane's value reaches 2^26
-#define RR_SCAN_DPP 1
-#endif
 template <uint32_t NT>
 __device__ __forceinline__ uint64_t block_excl_scan(uint64_t x, uint64_t *wsum, uint64_t &total) {
-#if RR_SCAN_DPP   // (64 lanes below 2^26 each: the wave's sum fits 32 bits; else the u64 shuffles)
-    const uint64_t incl = __ballot(x >= (1ull << 26)) == 0 ? (uint64_t)wave_incl_scan_u32((uint32_t)x) : wave_incl_scan(x);
-#else
-    const uint64_t incl = wave_incl_scan(x);
-#endif
+    // (the wave scan in DPP when no lane's value reaches 2^26: the wave's sum fits 32 bits)
+    const uint64_t incl = wave_incl_scan_fast(x);
     const uint32_t wv = threadIdx.x / RR_WAVE;
     if (lane_id() == RR_WAVE - 1) wsum[wv] = incl;
     lds_barrier();
@@ -2026,26 +737,28 @@ __device__ __forceinline__ uint64_t block_excl_scan(uint64_t x, uint64_t *wsum, 
     return pre + incl - x;
 }
 
-// ---- K4: fixup of queued values ----------------------------------------------------------
-// A workgroup per queued value (atomic ticket over the list the walks filled):
+// ---- the fixup of marked values (end of a window) ---------------------------------------
+// Values whose descriptors need a whole-value pass the walks cannot make carry FIX_MARK in their
+// record's status and are counted in the window's LDS word; after its batches the window's
+// workgroup finds them among its value records and fixes each one with all its threads:
 //   SET_HT / HASH_HT  exact duplicate-key test — fingerprints of (length, first and last 8
-//                     bytes) in an LDS open-addressing table, byte comparison on a fingerprint
-//                     match; a value with more keys than fit runs in several passes, each over
-//                     one residue class of the fingerprints.  A hash with a repeated field gets
-//                     RR_E_DUP (desHash's serverAssert, rock_serdes.c:399-400); a set keeps the
-//                     first copy of each member (desSet's dictAdd, :297): later copies are marked
-//                     and the descriptors compacted in place, the freed tail slots zeroed.
+//                     bytes) in an LDS open-addressing table (the window's stage, now free),
+//                     byte comparison on a fingerprint match; a value with more keys than fit
+//                     runs in several passes, each over one residue class of the fingerprints.
+//                     A hash with a repeated field gets RR_E_DUP (desHash's serverAssert,
+//                     rock_serdes.c:399-400); a set keeps the first copy of each member
+//                     (desSet's dictAdd, :297): later copies are marked and the descriptors
+//                     compacted in place, the freed tail slots zeroed.
 //   ZSET_SKIPLIST     pairs re-sorted in place into serZset's order (descending score, then
 //                     member, equal keys in blob order — the skiplist desZset builds, t_zset.c:
 //                     132-180) by a bitonic network over the descriptor pairs in global memory.
-// Totals changes go to fix[2] (bad values) / fix[3] (payload, two's complement), folded by the
-// finalize kernel.  Only values the walks could not clear arrive here: none in a batch of
-// serObject output whose hash tables hold at most HT_FP_KEYS keys, barring 16-bit fingerprint
-// collisions.
-constexpr uint32_t FIX_NT = 256, FIX_TAB = 8192, FIX_TAB_BITS = 13, FIX_PASS_KEYS = 2048;
-#ifndef RR_POST_FOLD_BLOCKS   // blocks of the decode's post kernel that fold the window totals
-#define RR_POST_FOLD_BLOCKS 32
-#endif
+// Totals changes go straight into the call's totals.  Only values the walks could not clear are
+// marked: none in a batch of serObject output whose hash tables hold at most HT_FP_KEYS keys,
+// barring 16-bit fingerprint collisions.  (Round 3 ran this as a fourth launch over a global
+// queue: 5.6 us with an empty queue.)
+constexpr uint32_t FIX_MARK = FIX_MARK_ST;   // rr_value.status bit: the value awaits its fixup
+constexpr uint32_t FIX_TAB = 8192, FIX_TAB_BITS = 13, FIX_PASS_KEYS = 2048;
+constexpr uint32_t FIX_LDS = FIX_TAB * 8 + 64 * 8 + 64;   // table, wave sums, flag (bytes of the stage)
 
 // 32-bit fingerprint of a member: length, first and last 8 bytes (bytes of the member only)
 __device__ __forceinline__ uint32_t member_fp(const uint8_t *__restrict__ blob, uint64_t off, uint32_t len) {
@@ -2084,6 +797,7 @@ __device__ __forceinline__ bool pair_before(const uint8_t *__restrict__ blob, co
     return oa < ob;   // equal keys: blob order (the member's arena offset is its blob offset)
 }
 
+template <uint32_t NT>
 __device__ void fix_sort_skiplist(const uint8_t *__restrict__ blob, rr_elem *__restrict__ el, uint32_t np) {
     uint4 *P = reinterpret_cast<uint4 *>(el);   // pair i = P[2i] (member), P[2i + 1] (score)
     uint32_t m = 1;
@@ -2092,7 +806,7 @@ __device__ void fix_sort_skiplist(const uint8_t *__restrict__ blob, rr_elem *__r
     // mirrored positions): positions >= np act as +infinity and are never touched
     for (uint32_t k = 2; k <= m; k <<= 1) {
         for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-            for (uint32_t t = threadIdx.x; t < m / 2; t += FIX_NT) {
+            for (uint32_t t = threadIdx.x; t < m / 2; t += NT) {
                 uint32_t lo, hi;
                 if (j == k >> 1) {
                     const uint32_t blk = t / j, o = t % j;
@@ -2116,125 +830,449 @@ __device__ void fix_sort_skiplist(const uint8_t *__restrict__ blob, rr_elem *__r
     }
 }
 
-__device__ __forceinline__ void fixup_values(const uint8_t *__restrict__ blob, uint64_t *fix,
-                                             rr_value *__restrict__ values, rr_elem *__restrict__ elems,
-                                             rr_totals *out) {
-    __shared__ unsigned long long tab[FIX_TAB];
-    __shared__ uint64_t wsum[FIX_NT / RR_WAVE];
-    __shared__ uint32_t sh_flag;   // bit 0: a duplicate key, bit 1: a pass overflowed the table
+// One marked value v, by the whole workgroup (every thread calls it with the same v); lds:
+// FIX_LDS bytes.  Clears the mark.
+template <uint32_t NT>
+__device__ void fixup_value(const uint8_t *__restrict__ blob, uint64_t v, rr_value *__restrict__ values,
+                            rr_elem *__restrict__ elems, rr_totals *out, uint8_t *lds) {
+    unsigned long long *tab = reinterpret_cast<unsigned long long *>(lds);
+    uint64_t *wsum = reinterpret_cast<uint64_t *>(lds + FIX_TAB * 8);
+    uint32_t *flag = reinterpret_cast<uint32_t *>(lds + FIX_TAB * 8 + 64 * 8);   // bit 0: a duplicate key,
+                                                                                  // bit 1: a pass overflowed
     const uint32_t tid = threadIdx.x;
-    const uint64_t nq = fix[0];
-    const uint32_t *list = reinterpret_cast<const uint32_t *>(fix + FIX_HDR);
-    // queued values are rare (none in serObject output with small hash tables): a static
-    // stride over the queue, no ticket atomics on an empty one
-    for (uint64_t t = blockIdx.x; t < nq; t += gridDim.x) {
-        if (tid == 0) sh_flag = 0;
-        __syncthreads();
-        const uint32_t v = list[t];
-        const uint4 rv = reinterpret_cast<const uint4 *>(values)[v];
-        const uint32_t type = rv.x & 0xFF, n = rv.z;
-        rr_elem *el = elems + rv.w;
-        if (type == RR_TYPE_ZSET_SKIPLIST) {
-            fix_sort_skiplist(blob, el, n / 2);
-        } else {
-            const uint32_t per = type == RR_TYPE_SET_HT ? 1 : 2, nk = n / per;
-            uint32_t K = (nk + FIX_PASS_KEYS - 1) / FIX_PASS_KEYS;
-            for (;;) {
-                for (uint32_t r = 0; r < K; ++r) {
-                    for (uint32_t j = tid; j < FIX_TAB; j += FIX_NT) tab[j] = 0;
-                    __syncthreads();
-                    for (uint32_t i = tid; i < nk; i += FIX_NT) {
-                        const ElemV e = get_elem(el + (uint64_t)i * per);
-                        const uint32_t fp = member_fp(blob, e.data, e.len);
-                        if (fp % K != r) continue;
-                        const unsigned long long ent = ((unsigned long long)fp << 32) | (i + 1u);
-                        uint32_t h = (fp * 0x9E3779B1u) >> (32 - FIX_TAB_BITS), probes = 0;
-                        for (;;) {
-                            unsigned long long cur = tab[h];
-                            if (cur == 0) {
-                                cur = atomicCAS(&tab[h], 0ull, ent);
-                                if (cur == 0) break;   // first of its key so far
-                            }
-                            if ((uint32_t)(cur >> 32) == fp) {
-                                const uint32_t j = (uint32_t)cur - 1u;
-                                const ElemV o = get_elem(el + (uint64_t)j * per);
-                                if (o.len == e.len && bytes_equal(blob, o.data, e.data, e.len)) {
-                                    uint32_t later = i;
-                                    if (i < j) {   // this copy comes first: it takes the slot
-                                        if (atomicCAS(&tab[h], cur, ent) != cur) continue;
-                                        later = j;
-                                    }
-                                    // mark the later copy (rsv = 1) for compaction
-                                    reinterpret_cast<uint16_t *>(el + (uint64_t)later * per)[7] = 1;
-                                    atomicOr(&sh_flag, 1u);
-                                    break;
-                                }
-                            }
-                            h = (h + 1) & (FIX_TAB - 1);
-                            if (++probes == FIX_TAB) { atomicOr(&sh_flag, 2u); break; }
-                        }
-                    }
-                    __syncthreads();
-                    if (sh_flag & 2) break;
-                }
-                if (!(sh_flag & 2)) break;
-                K *= 2;   // a residue class overflowed the table: finer classes (marks stay valid)
+    if (tid == 0) *flag = 0;
+    __syncthreads();
+    const uint4 rv = reinterpret_cast<const uint4 *>(values)[v];
+    const uint32_t type = rv.x & 0xFF, n = rv.z;
+    rr_elem *el = elems + rv.w;
+    bool drop_all = false;   // (a hash with a repeated field)
+    if (type == RR_TYPE_ZSET_SKIPLIST) {
+        fix_sort_skiplist<NT>(blob, el, n / 2);
+    } else {
+        const uint32_t per = type == RR_TYPE_SET_HT ? 1 : 2, nk = n / per;
+        uint32_t K = (nk + FIX_PASS_KEYS - 1) / FIX_PASS_KEYS;
+        for (;;) {
+            for (uint32_t r = 0; r < K; ++r) {
+                for (uint32_t j = tid; j < FIX_TAB; j += NT) tab[j] = 0;
                 __syncthreads();
-                if (tid == 0) sh_flag &= ~2u;
+                for (uint32_t i = tid; i < nk; i += NT) {
+                    const ElemV e = get_elem(el + (uint64_t)i * per);
+                    const uint32_t fp = member_fp(blob, e.data, e.len);
+                    if (fp % K != r) continue;
+                    const unsigned long long ent = ((unsigned long long)fp << 32) | (i + 1u);
+                    uint32_t h = (fp * 0x9E3779B1u) >> (32 - FIX_TAB_BITS), probes = 0;
+                    for (;;) {
+                        unsigned long long cur = tab[h];
+                        if (cur == 0) {
+                            cur = atomicCAS(&tab[h], 0ull, ent);
+                            if (cur == 0) break;   // first of its key so far
+                        }
+                        if ((uint32_t)(cur >> 32) == fp) {
+                            const uint32_t j = (uint32_t)cur - 1u;
+                            const ElemV o = get_elem(el + (uint64_t)j * per);
+                            if (o.len == e.len && bytes_equal(blob, o.data, e.data, e.len)) {
+                                uint32_t later = i;
+                                if (i < j) {   // this copy comes first: it takes the slot
+                                    if (atomicCAS(&tab[h], cur, ent) != cur) continue;
+                                    later = j;
+                                }
+                                // mark the later copy (rsv = 1) for compaction
+                                reinterpret_cast<uint16_t *>(el + (uint64_t)later * per)[7] = 1;
+                                atomicOr(flag, 1u);
+                                break;
+                            }
+                        }
+                        h = (h + 1) & (FIX_TAB - 1);
+                        if (++probes == FIX_TAB) { atomicOr(flag, 2u); break; }
+                    }
+                }
+                __syncthreads();
+                if (*flag & 2) break;
+            }
+            if (!(*flag & 2)) break;
+            K *= 2;   // a residue class overflowed the table: finer classes (marks stay valid)
+            __syncthreads();
+            if (tid == 0) *flag &= ~2u;
+            __syncthreads();
+        }
+        if (*flag & 1) {
+            // compact the kept descriptors forward (a chunk is read before it is written, and
+            // writes never pass the chunk's own positions), zero the freed tail
+            drop_all = per == 2;
+            uint64_t kept = 0, dropped = 0;
+            for (uint32_t c0 = 0; c0 < n; c0 += NT) {
+                const uint32_t i = c0 + tid;
+                uint4 d = make_uint4(0, 0, 0, 0);
+                if (i < n) d = reinterpret_cast<const uint4 *>(el)[i];
+                const bool keep = i < n && (per == 2 || (d.w >> 16) == 0);
+                uint64_t tot;
+                const uint64_t pos = block_excl_scan<NT>(keep ? 1u : 0u, wsum, tot);
+                dropped += i < n && !keep ? d.z : 0;
+                __syncthreads();
+                if (keep && per == 1) reinterpret_cast<uint4 *>(el)[kept + pos] = d;
+                if (per == 2 && i < n) dropped += d.z;   // a hash with a repeated field loses all
+                kept += tot;
                 __syncthreads();
             }
-            if (sh_flag & 1) {
-                // compact the kept descriptors forward (a chunk is read before it is written,
-                // and writes never pass the chunk's own positions), zero the freed tail
-                uint64_t kept = 0, dropped = 0;
-                for (uint32_t c0 = 0; c0 < n; c0 += FIX_NT) {
-                    const uint32_t i = c0 + tid;
-                    uint4 d = make_uint4(0, 0, 0, 0);
-                    if (i < n) d = reinterpret_cast<const uint4 *>(el)[i];
-                    const bool keep = i < n && (per == 2 || (d.w >> 16) == 0);
-                    uint64_t tot;
-                    const uint64_t pos = block_excl_scan<FIX_NT>(keep ? 1u : 0u, wsum, tot);
-                    dropped += i < n && !keep ? d.z : 0;
-                    __syncthreads();
-                    if (keep && per == 1) reinterpret_cast<uint4 *>(el)[kept + pos] = d;
-                    if (per == 2 && i < n) dropped += d.z;   // a hash with a repeated field loses all
-                    kept += tot;
-                    __syncthreads();
-                }
-                const uint32_t nk2 = per == 2 ? 0u : (uint32_t)kept;
-                for (uint32_t i = nk2 + tid; i < n; i += FIX_NT) reinterpret_cast<uint4 *>(el)[i] = make_uint4(0, 0, 0, 0);
-                dropped = wave_sum(dropped);
-                if (lane_id() == 0 && dropped && out)
-                    atomicAdd((unsigned long long *)&out->payload, (unsigned long long)(0ull - dropped));
-                if (tid == 0) {
-                    uint4 w = rv;
-                    w.z = nk2;
-                    if (per == 2) {
-                        w.x = (rv.x & 0xFFFFu) | ((uint32_t)RR_E_DUP << 16);
-                        if (out) atomicAdd((unsigned long long *)&out->n_bad, 1ull);
-                    }
-                    reinterpret_cast<uint4 *>(values)[v] = w;
-                }
+            const uint32_t nk2 = per == 2 ? 0u : (uint32_t)kept;
+            for (uint32_t i = nk2 + tid; i < n; i += NT) reinterpret_cast<uint4 *>(el)[i] = make_uint4(0, 0, 0, 0);
+            dropped = wave_sum(dropped);
+            if (lane_id() == 0 && dropped && out)
+                atomicAdd((unsigned long long *)&out->payload, (unsigned long long)(0ull - dropped));
+            if (tid == 0) {
+                uint4 w = rv;
+                w.z = nk2;
+                if (per == 2 && out) atomicAdd((unsigned long long *)&out->n_bad, 1ull);
+                w.x = (rv.x & 0xFFFFu) | ((per == 2 ? (uint32_t)RR_E_DUP : (uint32_t)RR_OK) << 16);
+                reinterpret_cast<uint4 *>(values)[v] = w;
             }
         }
+    }
+    if (tid == 0 && !drop_all && !(*flag & 1)) {   // the mark cleared (the status is RR_OK)
+        uint4 w = rv;
+        w.x = rv.x & 0xFFFFu;
+        reinterpret_cast<uint4 *>(values)[v] = w;
+    }
+    __syncthreads();
+}
+
+// The window's marked values [v_lo, v_hi): found by their records' status (every thread one
+// value per round, a ballot and an LDS list), fixed one by one.  The caller makes the window's
+// record and descriptor stores visible to the workgroup first (__syncthreads).
+template <uint32_t NT>
+__device__ void fixup_window(const uint8_t *__restrict__ blob, uint64_t v_lo, uint64_t v_hi,
+                             rr_value *__restrict__ values, rr_elem *__restrict__ elems, rr_totals *out,
+                             uint8_t *lds) {
+    uint32_t *list = reinterpret_cast<uint32_t *>(lds + FIX_LDS);   // NT + 1 words past the fixup's own
+    for (uint64_t r0 = v_lo; r0 < v_hi; r0 += NT) {
+        if (threadIdx.x == 0) list[NT] = 0;
         __syncthreads();
+        const uint64_t v = r0 + threadIdx.x;
+        if (v < v_hi && ((reinterpret_cast<const uint4 *>(values)[v].x >> 16) & FIX_MARK))
+            list[atomicAdd(&list[NT], 1u)] = threadIdx.x;
+        __syncthreads();
+        const uint32_t m = list[NT];
+        for (uint32_t k = 0; k < m; ++k) fixup_value<NT>(blob, r0 + list[k], values, elems, out, lds);
     }
 }
 
-// ---- K4: the decode's last kernel: the fixup pass over the queued values (their totals
-// changes added straight into the zeroed totals), then the fold of the windows' totals
-__global__ __launch_bounds__(FIX_NT) void decode_post_kernel(const uint8_t *__restrict__ blob, uint64_t *fix,
-                                                             rr_value *__restrict__ values,
-                                                             rr_elem *__restrict__ elems,
-                                                             const uint64_t *__restrict__ stats, uint64_t *state,
-                                                             uint32_t ntiles, const uint64_t *__restrict__ offsets,
-                                                             uint64_t n, rr_totals *out) {
-    fixup_values(blob, fix, values, elems, out);
-#if RR_DEC_ATOT   // (block 0 only: the bytes, the descriptor total and the error word)
-    if (out) fold_totals(stats, state, 0, offsets, n, 2, out, nullptr, fix + 1, 1);
+// a wave-uniform 64-bit value into SGPRs
+__device__ __forceinline__ uint64_t rfl64(uint64_t x) {
+    return (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)x) |
+           ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)) << 32);
+}
+
+// Probe build (tools/probe_decode.py, -DRR_PROBE): per-window phase cycles and per-class batch
+// cycles / counts / lanes into a buffer set by rr_probe_set (PROBE_WORDS u64 per window).
+// Diagnostics only; the product build has none of it.
+#ifdef RR_PROBE
+constexpr uint32_t PROBE_WORDS = 32;
+__device__ uint64_t *g_probe;
+extern "C" int rr_probe_set(void *p) { return hipMemcpyToSymbol(HIP_SYMBOL(g_probe), &p, sizeof(p)) == hipSuccess ? 0 : -1; }
+#define PROBE(...) __VA_ARGS__
 #else
-    if (out) fold_totals(stats, state, ntiles, offsets, n, 2, out, nullptr, fix + 1, RR_POST_FOLD_BLOCKS);
+#define PROBE(...)
 #endif
+// Timing-only ablations (tools/, wrong results): -DRR_ABLATE=1 copy + stage only, 2 + the class
+// sort (no batches), 3 no arena copy, 4 no descriptor stores (rr_decode_class.h).
+#ifndef RR_ABLATE
+#define RR_ABLATE 0
+#endif
+
+// Window granules (16 B) per thread loaded before the first_val -> offsets / class-byte loads
+// (the rest after the class bytes): measured 8 before 6 % slower, none before 2 % slower.
+constexpr uint32_t DEC_KE = 2;
+// Two 512-thread workgroups per CU = 4 waves per SIMD, so at most 128 VGPRs: the allocator is
+// told so (left to itself it takes 137 for the hash-table walk and the CU holds one workgroup).
+constexpr int DEC_WPE = 4;
+
+// Workgroup per byte WINDOW of W bytes: window t owns the values whose first byte lies in
+// [t*W, (t+1)*W) (first_val from K1).  The workgroup
+//   1. loads the window (buffer resources: no exec-mask branches; loads past the range read
+//      zeros, stores past it are dropped, unstaged granules go to a dummy LDS slot) and the tail
+//      of its last value (up to SLACK more) while it
+//   2. counting-sorts a chunk of <= PMAX of its values by class in LDS (the sort reads no
+//      global memory, so none of its waits drain the loads), then writes the window to the
+//      mirror arena (nontemporal) and the LDS stage;
+//   3. its waves take single-class batches of <= 64 values, heaviest class first, and walk +
+//      emit them from LDS (from global memory when the values did not fit the stage).
+// Every barrier orders LDS only (lds_barrier): __syncthreads() would make each wave wait for
+// the acknowledgement of its streaming arena stores.
+//
+// Descriptor slots: the window's first slot eb0 is the sum of count_kernel's totals of the
+// windows before it (two loads per lane: the groups before its group, the windows before it in
+// its group); each chunk scans its values' reservations in LDS (eloc) while it sorts them, so
+// no scan launch runs between count_kernel and this kernel.
+template <uint32_t W, uint32_t SLACK, uint32_t NW, uint32_t PMAX>
+__global__ __launch_bounds__(NW * RR_WAVE) __attribute__((amdgpu_waves_per_eu(DEC_WPE))) void decode_kernel(
+    const uint8_t *__restrict__ blob, uint64_t data_cap, const uint64_t *__restrict__ offsets, uint64_t n,
+    const uint32_t *__restrict__ first_val, const uint8_t *__restrict__ cls, const uint32_t *__restrict__ counts,
+    const uint64_t *__restrict__ wtot, const uint64_t *__restrict__ gtot, rr_value *__restrict__ values,
+    rr_elem *__restrict__ elems, uint64_t elem_cap, uint8_t *__restrict__ arena, uint32_t nwin, rr_totals *tot) {
+    constexpr uint32_t NT = NW * RR_WAVE, STAGE = W + SLACK;
+    static_assert(PMAX == NT, "a chunk is one value per thread (the slot scan)");
+    static_assert(W % 16 == 0 && SLACK % 16 == 0, "tile shape");
+    static_assert(FIX_LDS + 4 * (NT + 1) <= STAGE, "the fixup reuses the stage");
+    __shared__ __attribute__((aligned(16))) uint8_t stage[STAGE + 64];
+    __shared__ uint32_t nfix;             // values of the window marked for the fixup
+    __shared__ uint16_t perm[PMAX];
+    __shared__ uint32_t eloc[PMAX + 1];   // chunk-relative first slot of each value, then the chunk's slots
+    __shared__ uint64_t wpart[2][NW];     // wave sums: [0] the window's first slot, [1] the chunk's slot scan
+    __shared__ uint32_t ccount[C_N], cbase[C_N], ccur[C_N], bpre[C_N + 1];
+    __shared__ uint32_t next_batch;
+    __shared__ uint64_t red[2][NW];
+    PROBE(__shared__ uint64_t prb[PROBE_WORDS]; uint64_t pt0 = __builtin_amdgcn_s_memtime(), pt1 = 0, pt2 = 0;
+          if (threadIdx.x < PROBE_WORDS) prb[threadIdx.x] = 0;)
+    const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid / RR_WAVE;
+    const uint32_t tile = blockIdx.x;
+    if (tid == 0) nfix = 0;   // (ordered before the batches by the sort's first barrier)
+    // 0. the loads of the window's first slot go out first (reduced under the sort)
+    const uint32_t grp = tile / WGROUP, gi = tile % WGROUP;
+    uint64_t pre = tid < gi ? wtot[(uint64_t)grp * WGROUP + tid] : 0;
+    for (uint32_t k = tid; k < grp; k += NT) pre += gtot[k];
+    const uint64_t padded = (offsets[n] + 15) & ~15ull;
+    const uint64_t W0 = (uint64_t)tile * W;
+    const uint64_t W1 = W0 + W < padded ? W0 + W : padded;
+    // the arena copy starts at the call's first value (a call over a slice of a larger buffer —
+    // the chunks of rr_decode_batch_host — copies only its own bytes); the stage always lies
+    // past it (S0 >= offsets[v_lo] >= offsets[0])
+    const uint64_t A0 = W0 > (offsets[0] & ~15ull) ? W0 : (offsets[0] & ~15ull);
+    // the window's own granules [A0, W1) first: their range needs only offsets[0] and
+    // offsets[n], not first_val -> offsets, so the loads go out at the window's start; the
+    // stage's tail [W1, ov_e) (the last values' bytes past the window) follows.  The arena gets
+    // [A0, W1) (stores past it are dropped); granule A0 / 16 + tid + k * NT is at byte offset
+    // 16 (tid + k NT)
+    constexpr uint32_t KM = W / 16 / NT;   // granules per thread of a whole window
+    static_assert(W % (16 * NT) == 0, "window granules per thread");
+    const uint64_t ov_a = A0 >> 4, ov_w1 = W1 >> 4;
+    const uint32_t ov_mb = ov_w1 > ov_a ? (uint32_t)((ov_w1 - ov_a) * 16) : 0u;
+    const rsrc_t ov_RM = make_rsrc(blob + A0, ov_mb);
+    const rsrc_t ov_RA = make_rsrc(arena + A0, ov_mb);
+    // KE granules per thread go out before the first_val -> offsets / class-byte loads, the rest
+    // after the class bytes: the sort waits (vmcnt, in issue order) for the class bytes and
+    // therefore for the early granules only
+    constexpr uint32_t KE = DEC_KE < KM ? DEC_KE : KM;
+    u32x4 ov_m[KM];
+#pragma unroll
+    for (uint32_t k = 0; k < KE; ++k)
+        ov_m[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ov_RM, (int)((tid + k * NT) * 16), 0, 0));
+    const uint64_t v_lo = first_val[tile], v_hi = first_val[tile + 1];
+    uint64_t S0 = W0, S1 = W0;
+    if (v_hi > v_lo) {
+        S0 = offsets[v_lo] & ~15ull;
+        S1 = (offsets[v_hi] + 15) & ~15ull;
+    }
+    const bool staged = S1 - S0 <= STAGE;
+    const uint64_t cap = elem_cap < 0xFFFFFFFFull ? elem_cap : 0xFFFFFFFFull;   // elem_base is 32-bit
+
+    // the first chunk's class bytes and reservations, loaded before the rest of the window so
+    // their latency hides under it
+    const uint32_t cls0 = v_lo + tid < v_hi ? (uint32_t)cls[v_lo + tid] : C_N;
+    const uint32_t cnt0 = v_lo + tid < v_hi ? counts[v_lo + tid] : 0u;
+#pragma unroll
+    for (uint32_t k = KE; k < KM; ++k)
+        ov_m[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ov_RM, (int)((tid + k * NT) * 16), 0, 0));
+    // the stage's tail [W1, S1): at most SLACK bytes, KT granules per thread, also in flight
+    // under the sort
+    constexpr uint32_t KT = (SLACK / 16 + NT - 1) / NT;
+    const uint64_t ov_t0 = ov_w1 > ov_a ? ov_w1 : ov_a;
+    const uint64_t ov_te = (staged && S1 > W1 ? S1 : W1) >> 4;
+    const rsrc_t ov_RT = make_rsrc(blob + ov_t0 * 16, ov_te > ov_t0 ? (uint32_t)((ov_te - ov_t0) * 16) : 0u);
+    u32x4 ov_t[KT];
+#pragma unroll
+    for (uint32_t k = 0; k < KT; ++k)
+        ov_t[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ov_RT, (int)((tid + k * NT) * 16), 0, 0));
+
+    pre = wave_sum_fast(pre);
+    if (lane == 0) wpart[0][wave] = pre;   // (read after the sort's first barrier)
+    auto first_slot = [&]() __attribute__((always_inline)) {
+        uint64_t s = 0;
+#pragma unroll
+        for (uint32_t w = 0; w < NW; ++w) s += wpart[0][w];
+        return s;
+    };
+    const uint64_t ov_s0 = S0 >> 4;
+    typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
+    lds_u32x4 *ov_lds = (lds_u32x4 *)(__attribute__((address_space(3))) uint8_t *)stage;
+    // granule g's stage slot, or the dummy slot just past the stage (reads past the stage see
+    // garbage there, which the walks never use: every read is checked against its value's end)
+    auto ov_slot = [&](uint64_t g) __attribute__((always_inline)) -> uint32_t {
+        return (staged & (g >= ov_s0) & (g < ov_te)) ? (uint32_t)(g - ov_s0) : STAGE / 16;
+    };
+    // the window's loads have landed (under the sort): arena stores, LDS stage writes
+    auto ov_finish = [&]() __attribute__((always_inline)) {
+#pragma unroll
+        for (uint32_t k = 0; k < KM; ++k) {
+            if (RR_ABLATE != 3)
+                __builtin_amdgcn_raw_buffer_store_b128(ov_m[k], ov_RA, (int)((tid + k * NT) * 16), 0, 2 /* nt */);
+            ov_lds[ov_slot(ov_a + tid + (uint64_t)k * NT)] = ov_m[k];
+        }
+        // the stage's tail [W1, ov_te): LDS only
+#pragma unroll
+        for (uint32_t k = 0; k < KT; ++k) ov_lds[ov_slot(ov_t0 + tid + (uint64_t)k * NT)] = ov_t[k];
+    };
+
+    // values that do not fit the stage are read from global memory; if even their 32-bit
+    // window-relative byte or slot offsets could overflow, the exact parser takes them (the
+    // slots bounded as rr_decode_elem_bound does: a value's descriptors past its first take >= 2
+    // bytes each; a staged window never comes near)
+    const bool far = (!staged && S1 - S0 > 0xFFFFFF00ull) || ((S1 - S0) / 2 + (v_hi - v_lo)) * 16 >= NOSLOT;
+    const LdsSrc lsrc{(lds_cptr)stage};
+    const GlbSrc gsrc{make_rsrc(blob + S0, (uint32_t)(data_cap - S0 < 0xFFFFFFFFull ? data_cap - S0 : 0xFFFFFFFFull))};
+
+    uint64_t bad = 0, pay = 0, eb0 = 0, run = 0;   // run: the slots of the earlier chunks
+    const uint64_t v_end = RR_ABLATE == 1 ? v_lo : v_hi;
+    // 2. counting sort of a chunk of values by class (ballot per class, one LDS atomic per
+    //    class per wave-round) into perm, class bases and batch prefixes
+    //    class per wave-round) into perm, class bases and batch prefixes; and the scan of the
+    //    chunk's reservations into eloc (returns the chunk's slots)
+    auto sort_chunk = [&](uint64_t c0) __attribute__((always_inline)) -> uint64_t {
+        const uint32_t nv = (uint32_t)(v_hi - c0 < PMAX ? v_hi - c0 : PMAX);
+        if (tid < C_N) { ccount[tid] = 0; ccur[tid] = 0; }
+        if (tid == 0) next_batch = 0;
+        lds_barrier();   // also: the previous chunk's batches are done
+        PROBE(if (c0 == v_lo) pt1 = __builtin_amdgcn_s_memtime();)
+        const uint32_t i = tid;
+        const uint32_t ci = c0 == v_lo ? cls0 : i < nv ? (uint32_t)cls[c0 + i] : C_N;
+        const uint32_t ri = c0 == v_lo ? cnt0 : i < nv ? counts[c0 + i] : 0u;
+        const uint32_t myc = i < nv ? (far ? C_EXACT : ci) : C_N;
+        if (wave * RR_WAVE < nv) {   // (wave-uniform)
+#pragma unroll
+            for (uint32_t c = 0; c < C_N; ++c) {
+                const uint64_t m = __ballot(myc == c);
+                if (m && lane == 0) atomicAdd(&ccount[c], (uint32_t)__popcll(m));
+            }
+        }
+        const uint64_t incl = wave_incl_scan_fast((uint64_t)ri);
+        if (lane == RR_WAVE - 1) wpart[1][wave] = incl;
+        lds_barrier();
+        if (tid == 0) {
+            uint32_t s = 0, bs = 0;
+            for (uint32_t k = 0; k < C_N; ++k) {
+                const uint32_t c = CLASS_ORDER[k];
+                const uint32_t vpb = class_vpb(c);
+                cbase[c] = s;
+                bpre[k] = bs;
+                s += ccount[c];
+                bs += (ccount[c] + vpb - 1) / vpb;
+            }
+            bpre[C_N] = bs;
+        }
+        uint64_t wpre = 0, ctot = 0;
+#pragma unroll
+        for (uint32_t w = 0; w < NW; ++w) {
+            const uint64_t x = wpart[1][w];
+            wpre += w < wave ? x : 0;
+            ctot += x;
+        }
+        // (u32, saturated: slots past 2^32 - 1 fail capacity whatever their exact place)
+        const uint64_t mine = wpre + incl - ri;
+        if (i < nv) eloc[i] = (uint32_t)(mine < 0xFFFFFFFFull ? mine : 0xFFFFFFFFull);
+        if (tid == 0) eloc[nv] = (uint32_t)(ctot < 0xFFFFFFFFull ? ctot : 0xFFFFFFFFull);
+        lds_barrier();
+        if (wave * RR_WAVE < nv) {
+#pragma unroll
+            for (uint32_t c = 0; c < C_N; ++c) {
+                const uint64_t m = __ballot(myc == c);
+                if (m) {
+                    uint32_t at = 0;
+                    if (lane == 0) at = atomicAdd(&ccur[c], (uint32_t)__popcll(m));
+                    at = __builtin_amdgcn_readfirstlane(at);   // (lane 0 took the atomic)
+                    if (myc == c) perm[cbase[c] + at + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = (uint16_t)i;
+                }
+            }
+        }
+        return rfl64(ctot);   // (wave-uniform: kept in SGPRs)
+    };
+    uint64_t ctot = 0;
+    if (v_end > v_lo) {
+        ctot = sort_chunk(v_lo);   // (with the window's loads still in flight)
+        eb0 = rfl64(first_slot());   // (the waves' sums are behind the sort's first barrier)
+    }    if (v_end > v_lo) sort_chunk(v_lo);   // (with the window's loads still in flight)
+    ov_finish();                          // they have landed under the sort
+    for (uint64_t c0 = v_lo; c0 < v_end; c0 += PMAX) {
+        if (c0 != v_lo) {
+            lds_barrier();   // every wave is done with the previous chunk's batches
+            run += ctot;
+            ctot = sort_chunk(c0);
+        }
+        lds_barrier();   // the stage and the chunk's sort are complete
+        // the chunk's descriptor slots [eb_c, eb_c + ctot), cut at the capacity
+        const uint64_t eb_c = eb0 + run, ecut = eb_c + ctot < cap ? eb_c + ctot : cap;
+        const rsrc_t E = make_rsrc(reinterpret_cast<const uint8_t *>(elems + eb_c),
+                                   far || ecut <= eb_c ? 0u : (uint32_t)((ecut - eb_c) * 16));
+
+        PROBE(if (c0 == v_lo) pt2 = __builtin_amdgcn_s_memtime();)
+        // 3. single-class batches, taken dynamically by the waves
+        const uint32_t nb = RR_ABLATE == 2 ? 0u : bpre[C_N];
+        for (;;) {
+            uint32_t bi = 0;
+            if (lane == 0) bi = atomicAdd(&next_batch, 1u);
+            bi = __builtin_amdgcn_readfirstlane(bi);
+            if (bi >= nb) break;
+            uint32_t k = 0;
+            while (bi >= bpre[k + 1]) ++k;
+            const uint32_t c = CLASS_ORDER[k];
+            const uint32_t vpb = class_vpb(c);
+            const uint32_t first = cbase[c] + (bi - bpre[k]) * vpb;
+            const uint32_t cnt = min(ccount[c] - (bi - bpre[k]) * vpb, vpb);
+            PROBE(const uint64_t tb0 = __builtin_amdgcn_s_memtime();)
+            // lanes per value: the chained classes 64 / cnt (grouped walks; a power of two for
+            // Lists, ziplists and hash tables, so a value's lanes lie in one DPP row), hash
+            // tables grouped only when a value gets lanes enough to hold its keys (do_ht_g)
+            const bool grouped = c == C_LIST || c == C_SL || c == C_IS || c == C_ZL;
+            const uint32_t Gw = max(1u, min(GMAX, (uint32_t)RR_WAVE / cnt));
+            const bool htg = (c == C_HT || c == C_HH) && Gw >= ht_group_min(c == C_HH);
+            const uint32_t Gh = 1u << (31 - __builtin_clz(Gw));
+            const bool pow2 = htg || c == C_ZL || c == C_LIST;
+            const uint32_t G = __builtin_amdgcn_readfirstlane(pow2 ? Gh : grouped ? Gw : 1u);
+            const uint32_t li = lane / G, g = lane - li * G;   // the value's index in the batch
+            const bool active = li < cnt;
+            const uint32_t pi = active ? perm[first + li] : 0u;
+            const uint64_t v = c0 + pi;
+            uint64_t eb_v = eb_c, r_v = 0;
+            if (active) {
+                const uint32_t e0 = eloc[pi], e1 = eloc[pi + 1];
+                eb_v = e1 == 0xFFFFFFFFu ? 1ull << 40 : eb_c + e0;   // (saturated: past every capacity)
+                r_v = e1 - e0;
+            }
+            const Acc a = staged ? run_batch(lsrc, c, active, v, G, g, S0, E, eb_c, blob, offsets, eb_v, r_v, values,
+                                             elems, cap, &nfix)
+                                 : run_batch(gsrc, c, active, v, G, g, S0, E, eb_c, blob, offsets, eb_v, r_v, values,
+                                             elems, cap, &nfix);
+            bad += a.bad;
+            pay += a.pay;
+            PROBE(if (lane == 0) {
+                atomicAdd((unsigned long long *)&prb[3 + c], (unsigned long long)(__builtin_amdgcn_s_memtime() - tb0));
+                atomicAdd((unsigned long long *)&prb[3 + C_N + c], 1ull);
+                atomicAdd((unsigned long long *)&prb[3 + 2 * C_N + c], (unsigned long long)cnt);
+            })
+        }
+    }
+    bad = wave_sum_fast(bad);
+    pay = wave_sum_fast(pay);
+    if (lane == 0) { red[0][wave] = bad; red[1][wave] = pay; }
+    lds_barrier();
+    // 4. the window's marked values (rare: none in serObject output but fingerprint collisions),
+    //    in the stage's LDS once every wave's records and descriptors are visible to the others
+    if (nfix) {
+        __syncthreads();
+        fixup_window<NT>(blob, v_lo, v_hi, values, elems, tot, stage);
+    }
+    if (tid == 0) {
+        uint64_t tb = 0, tp = 0;
+        for (uint32_t w = 0; w < NW; ++w) { tb += red[0][w]; tp += red[1][w]; }
+        // the window's {bad, payload} straight into the call's totals (zeroed by count_kernel):
+        // two non-returning atomics per window, ~7K per call spread over the kernel
+        if (tot && tb) atomicAdd((unsigned long long *)&tot->n_bad, (unsigned long long)tb);
+        if (tot && tp) atomicAdd((unsigned long long *)&tot->payload, (unsigned long long)tp);
+        // the call's bytes, and its descriptor slots: the last window's first slot + its own
+        // (plain stores, one writer each: no fold launch)
+        if (tot && tile == 0) tot->bytes = offsets[n];
+        if (tot && tile == nwin - 1) tot->n_elems = first_slot() + run + ctot;
+        PROBE(prb[0] = pt1 - pt0; prb[1] = pt2 - pt1; prb[2] = __builtin_amdgcn_s_memtime() - pt2; prb[28] = v_hi - v_lo;
+              prb[29] = staged; if (g_probe) for (uint32_t i = 0; i < PROBE_WORDS; ++i) g_probe[(uint64_t)tile * PROBE_WORDS + i] = prb[i];)
+    }
 }
 
 // ---------------------------------------------------------------------------------------- encode
@@ -2388,54 +1426,9 @@ __device__ __forceinline__ ElemCost task_cost(uint32_t type, uint32_t enc, uint6
             return elem_cost(type, enc, k, e, acap);
     }
 }
-// two block-wide exclusive scans sharing one barrier (ws: [2][NT / RR_WAVE])
-#ifndef RR_ENC_SIZE_DPP   // 1: E1's per-round wave scans in DPP (u32) when no lane's cost reaches 2^26
-#define RR_ENC_SIZE_DPP 1
-#endif
-template <uint32_t NT>
-__device__ __forceinline__ void block_excl_scan2(uint64_t x, uint64_t y, uint64_t (*ws)[NT / RR_WAVE], uint64_t &ex,
-                                                 uint64_t &ey, uint64_t &tx, uint64_t &ty) {
-#if RR_ENC_SIZE_DPP   // (64 lanes below 2^26 each: the wave's sums fit 32 bits; else the u64 shuffles)
-    const bool small = __ballot((x | y) >= (1ull << 26)) == 0;
-    const uint64_t ix = small ? (uint64_t)wave_incl_scan_u32((uint32_t)x) : wave_incl_scan(x);
-    const uint64_t iy = small ? (uint64_t)wave_incl_scan_u32((uint32_t)y) : wave_incl_scan(y);
-#else
-    const uint64_t ix = wave_incl_scan(x), iy = wave_incl_scan(y);
-#endif
-    const uint32_t wv = threadIdx.x / RR_WAVE;
-    if (lane_id() == RR_WAVE - 1) { ws[0][wv] = ix; ws[1][wv] = iy; }
-    lds_barrier();
-    uint64_t px = 0, py = 0, sx = 0, sy = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < NT / RR_WAVE; ++k) {
-        const uint64_t a = ws[0][k], b = ws[1][k];
-        px += k < wv ? a : 0;
-        py += k < wv ? b : 0;
-        sx += a;
-        sy += b;
-    }
-    ex = px + ix - x;
-    ey = py + iy - y;
-    tx = sx;
-    ty = sy;
-}
-
-#ifndef RR_ENC_SIZE_U   // task rounds whose descriptors are loaded together
-#define RR_ENC_SIZE_U 2
-#endif
-#ifndef RR_ENC_SHORT   // values with at most this many tasks are costed by their own lane
-#define RR_ENC_SHORT 4
-#endif
-constexpr uint32_t ENC_SHORT = RR_ENC_SHORT;
-#ifndef RR_ENC_SIZE_PF   // descriptor lines of a long value prefetched by E1 before its task rounds
-#define RR_ENC_SIZE_PF 0
-#endif
-#ifndef RR_ENC_SIZE_SEG   // 1: E1 sums a value's task costs by wave-segmented LDS atomics (no per-round barrier)
-#define RR_ENC_SIZE_SEG 1
-#endif
-#ifndef RR_ENC_SIZE_MAP   // 1: E1 maps tasks to values through an LDS map (blocks of <= ENC_MAPCAP tasks)
-#define RR_ENC_SIZE_MAP 1
-#endif
+// E1 constants: task rounds whose descriptors are loaded together; values with at most ENC_SHORT
+// tasks are costed by their own lane
+constexpr uint32_t ENC_SIZE_U = 2, ENC_SHORT = 4;
 constexpr uint32_t ENC_MAPCAP = 4096;
 // Task -> value map of a round of NT values (the value's index at each of its tasks, u8), from
 // the task bases: the value with tasks writes its index at its first task (the head), then a
@@ -2443,24 +1436,6 @@ constexpr uint32_t ENC_MAPCAP = 4096;
 // was zeroed beforehand, ordered by a barrier) never win: 16 positions a thread, the carry across
 // threads by a DPP max scan and the waves' maxima in LDS.  Returns whether the round's tt tasks
 // fit the map (block-uniform); ends with an LDS barrier either way.
-// The last j in [0, NT) with tb[j] <= t, for a non-decreasing tb[0..NT] with tb[0] <= t: two
-// rounds of independent LDS reads instead of log2(NT) dependent ones — the 16 bucket heads
-// tb[16k] (compared all at once), then the 16 entries of the chosen bucket (four 16-byte reads).
-template <uint32_t NT>
-__device__ __forceinline__ uint32_t search_last_le(const uint32_t *tb, uint32_t t) {
-    static_assert(NT == 256, "16 buckets of 16");
-    uint32_t b = 0;
-#pragma unroll
-    for (uint32_t k = 1; k < 16; ++k) b += tb[16 * k] <= t ? 1u : 0u;
-    const uint4 *q = reinterpret_cast<const uint4 *>(tb + 16 * b);
-    uint32_t c = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < 4; ++k) {
-        const uint4 x = q[k];
-        c += (x.x <= t ? 1u : 0u) + (x.y <= t ? 1u : 0u) + (x.z <= t ? 1u : 0u) + (x.w <= t ? 1u : 0u);
-    }
-    return 16 * b + c - 1;
-}
 template <uint32_t NT>
 __device__ __forceinline__ bool build_task_map(uint8_t *tmap, uint32_t *wmax, uint32_t base, uint32_t ntask,
                                                uint64_t tt) {
@@ -2492,16 +1467,8 @@ __device__ __forceinline__ bool build_task_map(uint8_t *tmap, uint32_t *wmax, ui
     }
     return usemap;
 }
-#ifndef RR_ENC_SIZE_WPE   // waves per SIMD E1 is built for (0: the compiler's choice)
-#define RR_ENC_SIZE_WPE 0
-#endif
-#if RR_ENC_SIZE_WPE > 0
-#define ENC_SIZE_WPE_ATTR __attribute__((amdgpu_waves_per_eu(RR_ENC_SIZE_WPE)))
-#else
-#define ENC_SIZE_WPE_ATTR
-#endif
 template <uint32_t NT, uint32_t U>
-__global__ __launch_bounds__(NT) ENC_SIZE_WPE_ATTR void enc_size_kernel(const rr_value *__restrict__ values,
+__global__ __launch_bounds__(NT) void enc_size_kernel(const rr_value *__restrict__ values,
                                                       const rr_elem *__restrict__ elems, uint64_t n,
                                                       uint64_t ecap, uint64_t acap,
                                                       uint64_t *__restrict__ sizes, uint64_t *__restrict__ stats,
@@ -2509,17 +1476,15 @@ __global__ __launch_bounds__(NT) ENC_SIZE_WPE_ATTR void enc_size_kernel(const rr
     zero_call_words(zero_words, nzero, tot);
     __shared__ uint32_t tb[NT + 1];                  // first task of each value
     __shared__ uint32_t s_el[NT], s_te[NT], s_bad[NT];
-    __shared__ uint64_t s_b0[NT], s_b1[NT], s_p0[NT], s_p1[NT];   // byte / payload scans at the first task, after the last
-    __shared__ uint64_t ws0[NT / RR_WAVE], ws[2][2][NT / RR_WAVE];
+    __shared__ uint64_t s_b1[NT], s_p1[NT];   // the value's byte / payload sums (short values: their own lane's)
+    __shared__ uint64_t ws0[NT / RR_WAVE];
     __shared__ uint64_t red[3][NT / RR_WAVE];
-#if RR_ENC_SIZE_MAP
     // task -> value map of the block when it has at most ENC_MAPCAP tasks (build_task_map): one
     // LDS read per task instead of a binary search of the task bases
     __shared__ __attribute__((aligned(16))) uint8_t tmap[ENC_MAPCAP];
     __shared__ uint32_t wmax[NT / RR_WAVE];
     reinterpret_cast<uint4 *>(tmap)[threadIdx.x] = make_uint4(0, 0, 0, 0);   // (ordered before the
                                                                              // heads by the scan's barrier)
-#endif
     const uint32_t tid = threadIdx.x;
     const uint64_t v = (uint64_t)blockIdx.x * NT + tid;
     uint32_t type = 0, enc = 0, ntask = 0, hdr = 0, bad = 0;
@@ -2570,51 +1535,30 @@ __global__ __launch_bounds__(NT) ENC_SIZE_WPE_ATTR void enc_size_kernel(const rr
         }
         ntask = 0;
     }
-#if RR_ENC_SIZE_PF
-    // a long value's lane requests the first RR_ENC_SIZE_PF 64-byte lines of its descriptors
-    // while the short values' lanes load theirs, so the task rounds' loads later hit the L2
-    // (the OR keeps the loads; it is consumed once, after the rounds)
-    uint32_t pfacc = 0;
-    if (ntask > ENC_SHORT) {
-        const uint32_t *d = reinterpret_cast<const uint32_t *>(elems + eb);
-        const uint32_t lines = (uint32_t)((ne + 3) / 4);   // 4 descriptors per 64-byte line
-#pragma unroll
-        for (uint32_t k = 0; k < RR_ENC_SIZE_PF; ++k) pfacc |= d[16 * (k < lines ? k : lines - 1)];
-    }
-#endif
     s_el[tid] = (uint32_t)eb;
     s_te[tid] = type | (enc << 8);
     s_bad[tid] = bad;
-    s_b0[tid] = s_p0[tid] = 0;
     s_b1[tid] = sh_b;
     s_p1[tid] = sh_p;
     uint64_t TT;
     const uint32_t base = (uint32_t)block_excl_scan<NT>(ntask, ws0, TT);
     tb[tid] = base;
     if (tid == NT - 1) tb[NT] = base + ntask;
-#if RR_ENC_SIZE_MAP
     const bool usemap = build_task_map<NT>(tmap, wmax, base, ntask, TT);
-#else
-    lds_barrier();
-#endif
     auto fetch = [&](uint64_t t, uint32_t &pj, ElemV &pe) {
         pj = 0;
         pe = ElemV{0, 0, 0};
         if (t < TT) {
             uint32_t lo = 0;
-#if RR_ENC_SIZE_MAP
             if (usemap) lo = tmap[t];
             else
-#endif
 #pragma unroll
-            for (uint32_t s = NT / 2; s > 0; s >>= 1)
-                if (tb[lo + s] <= t) lo += s;
+                for (uint32_t s = NT / 2; s > 0; s >>= 1)
+                    if (tb[lo + s] <= t) lo += s;
             pj = lo;
             pe = get_elem(elems + s_el[lo] + (uint32_t)(t - tb[lo]));
         }
     };
-    uint64_t runb = 0, runp = 0;
-    uint32_t par = 0;
     for (uint64_t g0 = 0; g0 < TT; g0 += U * NT) {
         uint32_t j[U];
         ElemV e[U];
@@ -2626,17 +1570,14 @@ __global__ __launch_bounds__(NT) ENC_SIZE_WPE_ATTR void enc_size_kernel(const rr
             const uint64_t t = g0 + u * NT + tid;
             const bool act = t < TT;
             ElemCost c{0, 0, false};
-            uint32_t k = 0;
             if (act) {
-                k = (uint32_t)(t - tb[j[u]]);
                 const uint32_t te = s_te[j[u]];
-                c = task_cost(te & 0xFF, te >> 8, k, e[u], acap);
+                c = task_cost(te & 0xFF, te >> 8, (uint32_t)(t - tb[j[u]]), e[u], acap);
             }
-#if RR_ENC_SIZE_SEG
             // wave-segmented sums, no block barrier per round: a wave's tasks run over a few
             // values in order; each value's run in the wave adds (inclusive scan at its last
             // task) - (exclusive scan at its first task) to the value's sums with two LDS atomics
-            (void)k;
+            // (a block scan and barrier per round measured 81 -> 73 us without)
             const bool small = __ballot((c.bytes | c.pay) >= (1ull << 26)) == 0;
             const uint64_t ib = small ? (uint64_t)wave_incl_scan_u32((uint32_t)c.bytes) : wave_incl_scan(c.bytes);
             const uint64_t ip = small ? (uint64_t)wave_incl_scan_u32((uint32_t)c.pay) : wave_incl_scan(c.pay);
@@ -2653,30 +1594,14 @@ __global__ __launch_bounds__(NT) ENC_SIZE_WPE_ATTR void enc_size_kernel(const rr
                 atomicAdd((unsigned long long *)&s_p1[j[u]], (unsigned long long)ip);
             }
             if (act && c.bad) s_bad[j[u]] = 1;
-            (void)par; (void)runb; (void)runp; (void)ws;
-#else
-            uint64_t exb, exp, tb_, tp_;
-            block_excl_scan2<NT>(c.bytes, c.pay, ws[par], exb, exp, tb_, tp_);
-            par ^= 1;
-            if (act) {
-                if (k == 0) { s_b0[j[u]] = runb + exb; s_p0[j[u]] = runp + exp; }
-                if (t + 1 == tb[j[u] + 1]) { s_b1[j[u]] = runb + exb + c.bytes; s_p1[j[u]] = runp + exp + c.pay; }
-                if (c.bad) s_bad[j[u]] = 1;
-            }
-            runb += tb_;
-            runp += tp_;
-#endif
         }
     }
     lds_barrier();
-#if RR_ENC_SIZE_PF
-    asm volatile("" ::"v"(pfacc));
-#endif
     uint64_t size = 0, pay = 0;
     if (v < n) {
         bad = s_bad[tid];
-        size = bad ? 0 : hdr + (s_b1[tid] - s_b0[tid]);
-        pay = bad ? 0 : s_p1[tid] - s_p0[tid];
+        size = bad ? 0 : hdr + s_b1[tid];
+        pay = bad ? 0 : s_p1[tid];
         sizes[v] = size;
     }
     uint64_t sb = wave_sum_fast(bad), sp = wave_sum_fast(pay), sn = wave_sum_fast(ne);
@@ -2695,20 +1620,13 @@ __global__ __launch_bounds__(NT) ENC_SIZE_WPE_ATTR void enc_size_kernel(const rr
 // passes data_cap is not written (rock_serdes has no such case: sds grows; the batch API
 // bounds the output): it counts as bad and its payload is taken back out of the totals
 // (stored as a two's-complement negative, folded by the same modular sum).
-#ifndef RR_ENC_FOLD4   // 1: E4's block 0 folds the tile totals (no finalize launch)
-#define RR_ENC_FOLD4 1   // (encode cfg 4 -1 %, cfg 2 / 3 within noise)
-#endif
-#ifndef RR_ENC_ATOT   // 1: E3 adds the totals atomically and sets the bytes (no finalize launch)
-#define RR_ENC_ATOT 0   // (measured: encode +7 %: 11.7K same-address atomics inside a 5 us kernel serialize)
-#endif
 template <uint32_t W>
 __global__ __launch_bounds__(256) void enc_index_kernel(const rr_value *__restrict__ values,
                                                         const rr_elem *__restrict__ elems, uint64_t n,
                                                         uint64_t ecap, uint64_t acap,
                                                         const uint64_t *__restrict__ offsets, uint64_t cap,
                                                         uint32_t *__restrict__ fv, uint64_t nwin,
-                                                        uint64_t *__restrict__ stats, rr_totals *tot,
-                                                        uint64_t *err) {
+                                                        uint64_t *__restrict__ stats) {
     __shared__ uint64_t red[2][4];
     const uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint64_t bad = 0, pay = 0;
@@ -2736,23 +1654,8 @@ __global__ __launch_bounds__(256) void enc_index_kernel(const rr_value *__restri
         uint64_t s = 0;
         if (threadIdx.x < 2)
             for (uint32_t k = 0; k < blockDim.x / RR_WAVE; ++k) s += red[threadIdx.x][k];
-#if RR_ENC_ATOT
-        // this block's totals and E1's for the same 256 values straight into the call's totals
-        // (zeroed by E1's block 0, a kernel earlier): {bad, payload, descriptors}, no finalize
-        // launch; the last value's thread sets the bytes (or the device-failure mark)
-        (void)stats;
-        s += stats[-3 * (int64_t)gridDim.x + 3 * (int64_t)blockIdx.x + threadIdx.x];   // (E1's tile stats)
-        unsigned long long *f = reinterpret_cast<unsigned long long *>(tot);
-        if (tot && s) atomicAdd(threadIdx.x == 0 ? &f[2] : threadIdx.x == 1 ? &f[3] : &f[0], (unsigned long long)s);
-#else
-        (void)tot;
-        (void)err;
         stats[3 * (uint64_t)blockIdx.x + threadIdx.x] = s;
-#endif
     }
-#if RR_ENC_ATOT
-    if (tot && v + 1 == n) tot->bytes = lb_load(err) ? ~0ull : offsets[n];
-#endif
 }
 
 #ifdef RR_PROBE
@@ -2773,18 +1676,6 @@ __device__ __forceinline__ uint64_t rr_stamp() {
 #define EPROBE(...)
 #endif
 
-#ifndef RR_ENC_TPF
-#define RR_ENC_TPF 1
-#endif
-#ifndef RR_ENC_ROT   // 1: the granule copies' store order rotated per lane group (LDS bank spread)
-#define RR_ENC_ROT 0   // (measured: within noise, cfg 2 / 3 +1-2 %)
-#endif
-#ifndef RR_ENC_SEARCH2   // 1: E4's task -> value search in two rounds of independent LDS reads
-#define RR_ENC_SEARCH2 0   // (measured: E4 343.6 -> 365 us: more LDS instructions in an issue-bound kernel)
-#endif
-#ifndef RR_ENC_EMIT_MAP   // 1: E4 maps tasks to values through an LDS map (build_task_map)
-#define RR_ENC_EMIT_MAP 0   // (measured: E4 +2 %, its 4 KiB more LDS per workgroup)
-#endif
 
 // ---- E4: window emission -------------------------------------------------------------------
 // Blob layout per type (serObject rock_serdes.c:512-535): a value is a header of h bytes then
@@ -2800,21 +1691,9 @@ __device__ __forceinline__ uint32_t enc_hdr(uint32_t type) {
                                           type == RR_TYPE_ZSET_ZIPLIST) ? 5u : 13u;
 }
 
-// The window image: byte writes at absolute output positions, clipped to [w0, w0 + span).
-// Naturally aligned LDS stores only: a misaligned ds_write costs ~7 aligned ones on gfx950
-// (tools/micro/lds_align.hip: misaligned b32/b64/b128 all ~0.45 ms vs 0.06-0.10 ms aligned).
-// lds_put writes the low nb (<= 8) bytes of v at image offset d: ascending alignment steps
-// (1, 2, 4), then descending sizes (8, 4, 2, 1); every store lands on its natural alignment.
-__device__ __forceinline__ void lds_put(uint8_t *img, uint32_t d, uint64_t v, uint32_t nb) {
-    uint32_t r = nb;
-    if ((d & 1) && r >= 1) { img[d] = (uint8_t)v; v >>= 8; d += 1; r -= 1; }
-    if ((d & 2) && r >= 2) { *reinterpret_cast<uint16_t *>(img + d) = (uint16_t)v; v >>= 16; d += 2; r -= 2; }
-    if ((d & 4) && r >= 4) { *reinterpret_cast<uint32_t *>(img + d) = (uint32_t)v; v >>= 32; d += 4; r -= 4; }
-    if (r & 8) { *reinterpret_cast<uint64_t *>(img + d) = v; return; }
-    if (r & 4) { *reinterpret_cast<uint32_t *>(img + d) = (uint32_t)v; v >>= 32; d += 4; }
-    if (r & 2) { *reinterpret_cast<uint16_t *>(img + d) = (uint16_t)v; v >>= 16; d += 2; }
-    if (r & 1) img[d] = (uint8_t)v;
-}
+// Naturally aligned LDS stores only in the window image: a misaligned ds_write costs ~7 aligned
+// ones on gfx950 (tools/micro/lds_align.hip: misaligned b32/b64/b128 all ~0.45 ms vs 0.06-0.10
+// ms aligned).
 
 // x < 10^8 as 8 ASCII digits, the most significant in byte 0: 4-digit halves, 2-digit pairs,
 // digits (exact reciprocal multiplies for these ranges)
@@ -2831,12 +1710,6 @@ __device__ __forceinline__ uint64_t swar8(uint32_t x) {
     return ((uint64_t)four(hi) | ((uint64_t)four(lo) << 32)) + 0x3030303030303030ull;
 }
 
-#ifndef RR_ENC_OR   // 1: fields OR-ed into the zeroed image (one or two aligned 64-bit LDS atomics)
-#define RR_ENC_OR 1
-#endif
-#ifndef RR_ENC_ALIGNED   // 1: granule copies for pieces aligned with their image offset mod 16
-#define RR_ENC_ALIGNED 1
-#endif
 // lds_or writes the low nb (<= 8) bytes of v at image offset d into an image whose bytes there
 // are still zero (the image is zeroed first and no two fields overlap): the field OR-ed into the
 // one or two naturally aligned 8-byte words it touches, no-return LDS atomics, no branches on
@@ -2861,11 +1734,7 @@ struct Img {
     // little-endian field of nb (<= 8) bytes
     __device__ __forceinline__ void field(uint64_t pos, uint64_t v, uint32_t nb) const {
         const uint64_t d = pos - w0;
-#if RR_ENC_OR
         if (d < span && d + nb <= span) lds_or(img, (uint32_t)d, v, nb);
-#else
-        if (d < span && d + nb <= span) lds_put(img, (uint32_t)d, v, nb);
-#endif
         else
             for (uint32_t i = 0; i < nb; ++i) put(pos + i, (uint32_t)(v >> (8 * i)) & 0xFF);
     }
@@ -2993,16 +1862,10 @@ struct Img {
 constexpr uint64_t JQ_SRC = (1ull << 40) - 1;
 
 
+// waves per SIMD the emit kernel is built for (74 VGPRs, no spills; 5: E4 345 us, 6: 307 us)
+constexpr int ENC_WPE = 6;
 template <uint32_t W, uint32_t NT, uint32_t RCAP>
-#ifdef RR_ENC_NVGPR   // (tuning: a hard VGPR budget for the emit kernel)
-#define ENC_NVGPR_ATTR __attribute__((amdgpu_num_vgpr(RR_ENC_NVGPR)))
-#else
-#define ENC_NVGPR_ATTR
-#endif
-#ifndef RR_ENC_WPE   // waves per SIMD the emit kernel is built for
-#define RR_ENC_WPE 6      // (74 VGPRs, no spills; 5: E4 345 us, 6: 307 us)
-#endif
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(RR_ENC_WPE))) ENC_NVGPR_ATTR void enc_emit_kernel(const rr_value *__restrict__ values,
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(ENC_WPE))) void enc_emit_kernel(const rr_value *__restrict__ values,
                                                       const rr_elem *__restrict__ elems,
                                                       const uint8_t *__restrict__ arena, uint64_t n,
                                                       uint8_t *__restrict__ out, uint64_t cap,
@@ -3011,13 +1874,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(RR_ENC_WPE))
                                                       const uint64_t *__restrict__ stats, uint32_t ntiles,
                                                       rr_totals *tot, uint64_t *err) {
     static_assert(W <= 65536 && W % 64 == 0, "image offsets are 16-bit, pieces 64-byte blocks");
-#if RR_ENC_FOLD4
-    // block 0 folds E1's and E3's tile totals into the call's totals before its window (the
-    // finalize launch's work, hidden under the other windows)
-    if (tot) fold_totals(stats, nullptr, ntiles, offsets, n, 0, tot, nullptr, err, 1);
-#else
-    (void)stats; (void)ntiles; (void)tot; (void)err;
-#endif
+    // block 0 folds E1's and E3's tile totals into the call's totals before its window (a
+    // separate finalize launch's work, hidden under the other windows: encode cfg 4 -1 %)
+    if (tot && blockIdx.x == 0) fold_totals(stats, ntiles, offsets, n, tot, err);
     static_assert(RCAP >= 2 && W / 64 + RCAP < 65536, "run piece bases are 16-bit");
     constexpr uint32_t RTOP = 1u << (31 - __builtin_clz(RCAP - 1));   // largest power of two < RCAP
     __shared__ uint4 img4[W / 16];
@@ -3032,10 +1891,6 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(RR_ENC_WPE))
     __shared__ uint64_t sh_nrp;            // runs reserved | pieces reserved << 32
     __shared__ uint32_t sh_pend;           // pieces of the queued runs, when the queue overflowed
     __shared__ uint32_t sh_unal;           // some queued run is not aligned with its image offset mod 16
-#if RR_ENC_EMIT_MAP   // task -> value map of a value round (build_task_map)
-    __shared__ __attribute__((aligned(16))) uint8_t tmap[ENC_MAPCAP];
-    __shared__ uint32_t wmax[NT / RR_WAVE];
-#endif
     uint8_t *img = reinterpret_cast<uint8_t *>(img4);
     const uint32_t tid = threadIdx.x;
     const uint64_t total = offsets[n];
@@ -3081,9 +1936,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(RR_ENC_WPE))
         if (queued && r < RCAP) {
             rq_a[r] = src | ((uint64_t)l << 40);
             rq_dp[r] = dst | (p0 << 16);
-#if RR_ENC_ALIGNED
             if ((reinterpret_cast<uintptr_t>(arena) + src - dst) & 15) sh_unal = 1;
-#endif
         } else {   // queue full (rare; keeps the kernel small): byte copy
             if (queued && r == RCAP) sh_pend = p0;
             for (uint32_t i = 0; i < l; ++i) img[dst + i] = arena[src + i];
@@ -3093,9 +1946,6 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(RR_ENC_WPE))
     for (uint64_t vb = v0; vb < vend; vb += NT) {
         const uint64_t v = vb + tid;
         uint32_t tasks = 0;
-#if RR_ENC_EMIT_MAP   // (the previous round's last reads of the map are behind its closing barrier)
-        reinterpret_cast<uint4 *>(tmap)[tid] = make_uint4(0, 0, 0, 0);
-#endif
         if (v < vend) {
             const uint64_t a = offsets[v], b = offsets[v + 1];
             const uint4 x = reinterpret_cast<const uint4 *>(values)[v];
@@ -3121,32 +1971,21 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(RR_ENC_WPE))
         const uint32_t base = (uint32_t)block_excl_scan<NT>(tasks, wsum[0], tt);
         tb[tid] = base;
         if (tid == NT - 1) tb[NT] = base + tasks;
-#if RR_ENC_EMIT_MAP
-        const bool usemap = build_task_map<NT>(tmap, wmax, base, tasks, tt);
-#else
         lds_barrier();
-#endif
         EPROBE(const uint64_t eth = rr_stamp(); ent += tt;)
         uint64_t run = 0;   // element bytes of the earlier task rounds
-        // task rounds in groups of TPF: every round's descriptor is loaded up front, so a
-        // group costs one memory round trip
+        // (an LDS task -> value map as in E1 measured E4 +2 %, its 4 KiB more LDS per workgroup;
+        // the search in two rounds of independent LDS reads +6 %: more LDS instructions in an
+        // issue-bound kernel; four rounds' descriptors loaded together +12 %)
         auto fetch = [&](uint64_t t, uint32_t &pj, ElemV &pe) {
             pj = 0;
             pe = ElemV{0, 0, 0};
             if (t < tt) {
                 // last value j with tb[j] <= t
                 uint32_t lo = 0;
-#if RR_ENC_EMIT_MAP
-                if (usemap) lo = tmap[t];
-                else
-#endif
-#if RR_ENC_SEARCH2
-                lo = search_last_le<NT>(tb, (uint32_t)t);
-#else
 #pragma unroll
                 for (uint32_t s = NT / 2; s > 0; s >>= 1)
                     if (tb[lo + s] <= t) lo += s;
-#endif
                 pj = lo;
                 pe = get_elem(elems + sv_el[lo] + (uint32_t)(t - tb[lo]));
             }
@@ -3199,30 +2038,12 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(RR_ENC_WPE))
             run += rt;
             EPROBE(asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); const uint64_t rs2 = rr_stamp(); twr += rs2 - rs1;)
         };
-        // task rounds in groups of four: the group's descriptors are loaded up front, so a
-        // group costs one memory round trip
-#if RR_ENC_TPF == 1
         for (uint64_t g0 = 0; g0 < tt; g0 += NT) {
             uint32_t j0;
             ElemV e0;
             fetch(g0 + tid, j0, e0);
             round(g0, j0, e0);
         }
-#else
-        for (uint64_t g0 = 0; g0 < tt; g0 += 4 * NT) {
-            uint32_t j0, j1, j2, j3;
-            ElemV e0, e1, e2, e3;
-            fetch(g0 + tid, j0, e0);
-            fetch(g0 + NT + tid, j1, e1);
-            fetch(g0 + 2 * NT + tid, j2, e2);
-            fetch(g0 + 3 * NT + tid, j3, e3);
-            EPROBE(asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); tf += rr_stamp() - eth;)
-            round(g0, j0, e0);
-            if (g0 + NT < tt) round(g0 + NT, j1, e1);
-            if (g0 + 2 * NT < tt) round(g0 + 2 * NT, j2, e2);
-            if (g0 + 3 * NT < tt) round(g0 + 3 * NT, j3, e3);
-        }
-#endif
         lds_barrier();
         EPROBE(const uint64_t ett = rr_stamp(); etk += ett - eth;)
     }
@@ -3234,28 +2055,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(RR_ENC_WPE))
     const uint32_t npc = sh_pend != 0xFFFFFFFFu ? sh_pend : (uint32_t)(sh_nrp >> 32);
     auto piece = [&](uint32_t b, uint64_t &ps, uint32_t &pd, uint32_t &pl) {
         uint32_t lo = 0;   // (steps from the largest power of two below RCAP: every index reachable)
-#if RR_ENC_SEARCH2
-        // the last queued run whose first piece <= b, in three rounds of seven independent LDS
-        // reads (stride 64, 8, 1) instead of nine dependent ones: rq_dp[i] < (b + 1) << 16 is a
-        // prefix-true predicate over the runs [0, nr)
-        static_assert(RCAP == 512, "three levels of 8");
-        (void)RTOP;
-        const uint32_t key = (b + 1) << 16;
-#pragma unroll
-        for (uint32_t st = 64; st > 0; st >>= 3) {
-            uint32_t c = 0;
-#pragma unroll
-            for (uint32_t k = 1; k < 8; ++k) {
-                const uint32_t i = lo + k * st;
-                c += (i < nr && rq_dp[i < RCAP ? i : RCAP - 1] < key) ? 1u : 0u;
-            }
-            lo += c * st;
-        }
-#else
 #pragma unroll
         for (uint32_t s = RTOP; s > 0; s >>= 1)
             if (lo + s < nr && (rq_dp[lo + s] >> 16) <= b) lo += s;
-#endif
         const uint64_t a = rq_a[lo];
         const uint32_t dp = rq_dp[lo], dst = dp & 0xFFFF, l = (uint32_t)(a >> 40), k = b - (dp >> 16);
         const uint32_t d0 = k == 0 ? dst : ((dst >> 6) + k) << 6;
@@ -3264,7 +2066,6 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(RR_ENC_WPE))
         pd = d0;
         pl = e > d0 ? e - d0 : 0;   // (inside one 64-byte block by construction)
     };
-#if RR_ENC_ALIGNED
     // Every run aligned with its image offset mod 16 (any arena that keeps the blob layout, the
     // decode's mirror arena included): pieces move whole granules (RR_AL_LOAD / RR_AL_STORE).
     // A window with any other run takes the byte plan below for all its pieces.
@@ -3275,19 +2076,14 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(RR_ENC_WPE))
             uint32_t d0, l0, d1 = 0, l1 = 0;
             piece(j, s0, d0, l0);
             if (two) piece(j + NT, s1, d1, l1);
-#if RR_ENC_ROT
-            const uint32_t rot = (lane_id() >> 2) & 3;
-#else
-            const uint32_t rot = 0;
-#endif
+            const uint32_t rot = 0;   // (rotated per lane group for LDS bank spread: within noise)
             RR_AL_LOAD(xa, s0, d0, l0, rot)
             RR_AL_LOAD(xb, s1, d1, l1, rot)
             RR_AL_STORE(xa, d0, l0, rot)
             RR_AL_STORE(xb, d1, l1, rot)
         }
     } else
-#endif
-    for (uint32_t j = tid; j < npc; j += 2 * NT) {
+        for (uint32_t j = tid; j < npc; j += 2 * NT) {
         const bool two = j + NT < npc;
         uint64_t s0, s1 = 0;
         uint32_t d0, l0, d1 = 0, l1 = 0;
@@ -3329,8 +2125,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(RR_ENC_WPE))
 #ifndef RR_DEC_NW
 #define RR_DEC_NW 8
 #endif
-#ifndef RR_DEC_PMAX
-#define RR_DEC_PMAX 1024
+#ifndef RR_DEC_PMAX   // values per sort chunk: one per thread (the chunk's slot scan)
+#define RR_DEC_PMAX (RR_DEC_NW * RR_WAVE)
 #endif
 constexpr uint32_t DEC_W = RR_DEC_W, DEC_NW = RR_DEC_NW;
 #define DECODE_KERNEL decode_kernel<RR_DEC_W, RR_DEC_SLACK, RR_DEC_NW, RR_DEC_PMAX>
@@ -3354,118 +2150,37 @@ static uint64_t scan_tiles(uint64_t n) { return (n + SCAN_TILE - 1) / SCAN_TILE;
 // offsets[n] own no values and copy nothing
 static uint64_t dec_windows(uint64_t data_cap) { return data_cap / DEC_W + 1; }
 
-#ifndef RR_DEC_FUSED   // 1: dec_index_kernel + decode_fused_kernel; 0: count + scan + decode_kernel
-#define RR_DEC_FUSED 0
-#endif
-#if RR_DEC_FUSED
-// the fused kernel's chunk is one pass-A round of the workgroup's threads
-#undef RR_DEC_PMAX
-#define RR_DEC_PMAX (RR_DEC_NW * RR_WAVE)
-#define DECODE_FUSED_KERNEL decode_fused_kernel<RR_DEC_W, RR_DEC_SLACK, RR_DEC_NW, RR_DEC_PMAX>
-// Decode scratch (uint64 words): [HDR] [window look-back: state nwin, groups] [descriptor total,
-// 1] [fixup header, then its u32 list of up to n values] [window stats, 3 per window] [first_val
-// u32, nwin+1] [reservations u32, n] [class bytes, n].  dec_index_kernel zeroes the look-back
-// words, the total and the fixup header.
+// Decode scratch (uint64 words): [HDR] [window sums, nwin] [group sums, nwin / WGROUP + 1]
+// [reservations u32, n] [first_val u32, nwin + 1] [class bytes, n].  The sums are zeroed by one
+// memset per call; count_kernel's block 0 zeroes the totals.
+// Launches: memset, count_kernel, decode_kernel.  (Round 3 ran a look-back scan of the
+// reservations between the two — 15.4 us on config 4 — and a fourth kernel for the fixup and
+// the totals fold — 5.6 us.  Measured dead ends, in git history: a fused single-pass decode
+// with a window-level look-back, 0.401 vs 0.353 ms — the look-back waits ~5 us per window
+// generation; count + scan in one launch with an in-kernel look-back, +40 us.)
+static uint64_t dec_groups(uint64_t nw) { return nw / WGROUP + 1; }
 extern "C" uint64_t rr_decode_scratch_words(uint64_t data_cap, uint64_t n) {
     const uint64_t nw = dec_windows(data_cap);
-    return RR_SCRATCH_HDR + nw + (nw + LB_GROUP - 1) / LB_GROUP + FIX_HDR + (n + 2) / 2 + 1 + 3 * nw + (nw + 2) / 2 +
-           (n + 2) / 2 + (n + 7) / 8 + 2;
+    return RR_SCRATCH_HDR + nw + dec_groups(nw) + (n + 2) / 2 + (nw + 2) / 2 + (n + 7) / 8 + 2;
 }
 
 extern "C" hipError_t rr_launch_decode(const uint8_t *blob, const uint64_t *offsets, uint64_t n, rr_value *values,
                                        rr_elem *elems, uint64_t elem_cap, uint8_t *arena, uint64_t *scratch,
                                        uint64_t data_cap, rr_totals *totals, hipStream_t stream) {
     const uint32_t nw = (uint32_t)dec_windows(data_cap);
-    uint64_t *lb_state = scratch + RR_SCRATCH_HDR;
-    uint64_t *lb_groups = lb_state + nw;
-    const uint64_t lb_words = nw + (nw + LB_GROUP - 1) / LB_GROUP;
-    uint64_t *total = lb_state + lb_words;
-    uint64_t *fix = total + 1;                           // header words, then the u32 list
-    uint64_t *stats = fix + FIX_HDR + (n + 2) / 2;
-    uint32_t *first_val = reinterpret_cast<uint32_t *>(stats + 3 * (uint64_t)nw);
-    uint32_t *cnt = first_val + ((nw + 2) & ~1u);
-    uint8_t *cls = reinterpret_cast<uint8_t *>(cnt + ((n + 2) & ~1ull));
-    hipLaunchKernelGGL(dec_index_kernel, dim3((uint32_t)((n + 1 + 255) / 256)), dim3(256), 0, stream, offsets, n,
-                       first_val, nw, DEC_W, lb_state, (uint32_t)(lb_words + 1 + FIX_HDR), totals);
-    hipLaunchKernelGGL((DECODE_FUSED_KERNEL), dim3(nw), dim3(DEC_NW * RR_WAVE), 0, stream, blob, data_cap, offsets, n,
-                       first_val, cls, cnt, values, elems, elem_cap, arena, stats, fix, nw, lb_state, lb_groups, total);
-    static uint32_t post_grid = 0;
-    if (!post_grid) post_grid = resident_grid(decode_post_kernel, FIX_NT, false);
-    hipLaunchKernelGGL(decode_post_kernel, dim3(post_grid), dim3(FIX_NT), 0, stream, blob, fix, values, elems, stats,
-                       total, nw, offsets, n, totals);
-    return hipGetLastError();
-}
-#else
-// Decode scratch (uint64 words): [HDR] [scan: ticket, look-back state + groups] [fixup header,
-// then its u32 list of up to n values] [counts -> elem_base, n+1] [window stats, 3 per window]
-// [first_val u32, nwin+1] [class bytes, n].  The look-back words and the fixup header are
-// zeroed by one memset per call.
-#ifndef RR_COUNT_SCAN   // 1: count_scan_kernel (one launch); 0: count_kernel + scan_kernel
-#define RR_COUNT_SCAN 0     // (measured: the 3.9K in-kernel look-backs cost +40 us on cfg 4, +50 on cfg 2)
-#endif
-static uint32_t cs_tiles(uint64_t n) { return (uint32_t)((n + 1 + CS_NT - 1) / CS_NT); }
-// look-back words of the reservation scan: count_scan_kernel's 256-value blocks, or scan_kernel's
-// ticket + 4096-value tiles
-static uint64_t dec_lb_words(uint64_t n) {
-#if RR_COUNT_SCAN
-    const uint64_t t = cs_tiles(n);
-    return t + (t + LB_GROUP - 1) / LB_GROUP;
-#else
-    const uint64_t st = scan_tiles(n);
-    return 1 + st + (st + LB_GROUP - 1) / LB_GROUP;
-#endif
-}
-extern "C" uint64_t rr_decode_scratch_words(uint64_t data_cap, uint64_t n) {
-    const uint64_t nw = dec_windows(data_cap);
-    return RR_SCRATCH_HDR + dec_lb_words(n) + FIX_HDR + (n + 2) / 2 + (n + 1) + 3 * nw + (nw + 2) / 2 + (n + 7) / 8 + 2;
-}
-
-extern "C" hipError_t rr_launch_decode(const uint8_t *blob, const uint64_t *offsets, uint64_t n, rr_value *values,
-                                       rr_elem *elems, uint64_t elem_cap, uint8_t *arena, uint64_t *scratch,
-                                       uint64_t data_cap, rr_totals *totals, hipStream_t stream) {
-    const uint32_t st = (uint32_t)scan_tiles(n), nw = (uint32_t)dec_windows(data_cap);
-    (void)st;
-    uint64_t *lb = scratch + RR_SCRATCH_HDR;
-    const uint64_t lb_words = dec_lb_words(n);
-    uint64_t *fix = lb + lb_words;                      // header words, then the u32 list
-    uint64_t *counts = fix + FIX_HDR + (n + 2) / 2;
-    uint64_t *stats = counts + n + 1;
-    uint32_t *first_val = reinterpret_cast<uint32_t *>(stats + 3 * (uint64_t)nw);
+    uint64_t *wtot = scratch + RR_SCRATCH_HDR;
+    uint64_t *gtot = wtot + nw;
+    uint32_t *counts = reinterpret_cast<uint32_t *>(gtot + dec_groups(nw));
+    uint32_t *first_val = counts + ((n + 2) & ~1ull);
     uint8_t *cls = reinterpret_cast<uint8_t *>(first_val + ((nw + 2) & ~1u));
-#if RR_COUNT_SCAN   // reservations, classes and elem_base in one launch (count_scan_kernel), after one
-                    // memset of its look-back words and the fixup header (contiguous: scratch layout)
-    {
-        const uint32_t nb = cs_tiles(n);
-        if (hipMemsetAsync(lb, 0, (lb_words + FIX_HDR) * sizeof(uint64_t), stream) != hipSuccess) return hipGetLastError();
-        hipLaunchKernelGGL(count_scan_kernel, dim3(nb), dim3(CS_NT), 0, stream, blob, offsets, n, first_val, nw, DEC_W,
-                           counts, cls, lb, lb + nb, nb, fix + 1, totals);
-    }
-#else
+    const hipError_t e = hipMemsetAsync(wtot, 0, (nw + dec_groups(nw)) * sizeof(uint64_t), stream);
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL(count_kernel, dim3((uint32_t)((n + 1 + 255) / 256)), dim3(256), 0, stream, blob, offsets, n,
-                       first_val, nw, DEC_W, counts, cls, lb, (uint32_t)(lb_words + FIX_HDR), totals);
-    if (st) hipLaunchKernelGGL(scan_kernel, dim3(st), dim3(256), 0, stream, counts, n, lb, st, fix + 1);
-#endif
-#if RR_DEC_PF
-    static uint32_t dec_grid = 0;
-    if (!dec_grid) dec_grid = resident_grid(DECODE_KERNEL, DEC_NW * RR_WAVE, false);
-    const uint32_t grid = nw < dec_grid ? nw : dec_grid;
-#else
-    const uint32_t grid = nw;
-#endif
-    hipLaunchKernelGGL((DECODE_KERNEL), dim3(grid), dim3(DEC_NW * RR_WAVE), 0, stream, blob, data_cap, offsets, n,
-                       first_val, cls, counts, values, elems, elem_cap, arena, stats, fix, nw, totals);
-    static uint32_t post_grid = 0;
-#ifdef RR_POST_GRID   // (tuning: a fixed post grid instead of the resident one)
-    if (!post_grid) post_grid = RR_POST_GRID;
-#else
-    if (!post_grid) post_grid = resident_grid(decode_post_kernel, FIX_NT, false);
-#endif
-    hipLaunchKernelGGL(decode_post_kernel, dim3(post_grid), dim3(FIX_NT), 0, stream, blob, fix, values, elems, stats,
-                       counts + n, nw, offsets, n, totals);
+                       first_val, nw, DEC_W, counts, cls, wtot, gtot, nullptr, 0u, totals);
+    hipLaunchKernelGGL((DECODE_KERNEL), dim3(nw), dim3(DEC_NW * RR_WAVE), 0, stream, blob, data_cap, offsets, n,
+                       first_val, cls, counts, wtot, gtot, values, elems, elem_cap, arena, nw, totals);
     return hipGetLastError();
 }
-
-#endif   // RR_DEC_FUSED
 
 // Encode scratch (uint64 words): [HDR] [scan: ticket, look-back state + groups]
 // [tile stats, 3 per 256 values, twice] [first value per output window u32, nwin+1].
@@ -3487,9 +2202,8 @@ extern "C" hipError_t rr_launch_encode(const rr_value *values, const rr_elem *el
                                        const uint8_t *arena, uint64_t arena_cap, uint64_t n, uint8_t *out,
                                        uint64_t cap, uint64_t *offsets, uint64_t *scratch, rr_totals *totals,
                                        hipStream_t stream) {
-    hipError_t e;
     if (n == 0) {
-        e = hipMemsetAsync(offsets, 0, sizeof(uint64_t), stream);
+        hipError_t e = hipMemsetAsync(offsets, 0, sizeof(uint64_t), stream);
         if (e == hipSuccess && totals) e = hipMemsetAsync(totals, 0, sizeof(rr_totals), stream);
         return e;
     }
@@ -3500,19 +2214,14 @@ extern "C" hipError_t rr_launch_encode(const rr_value *values, const rr_elem *el
     uint64_t *err = lb + lb_words;   // device error word (look-back timeout)
     uint64_t *stats = err + 1;
     uint32_t *fv = reinterpret_cast<uint32_t *>(stats + 6 * (uint64_t)t);
-    hipLaunchKernelGGL((enc_size_kernel<256, RR_ENC_SIZE_U>), dim3(t), dim3(256), 0, stream, values, elems, n, elem_cap, arena_cap, offsets,
+    hipLaunchKernelGGL((enc_size_kernel<256, ENC_SIZE_U>), dim3(t), dim3(256), 0, stream, values, elems, n, elem_cap, arena_cap, offsets,
                        stats, lb, (uint32_t)(lb_words + 1), totals);
     hipLaunchKernelGGL(scan_kernel, dim3(st), dim3(256), 0, stream, offsets, n, lb, st, err);
     hipLaunchKernelGGL(enc_index_kernel<ENC_W>, dim3(t), dim3(256), 0, stream, values, elems, n, elem_cap, arena_cap,
-                       offsets, cap, fv, nw, stats + 3 * (uint64_t)t, totals, err);
+                       offsets, cap, fv, nw, stats + 3 * (uint64_t)t);
     hipLaunchKernelGGL((enc_emit_kernel<ENC_W, ENC_NT, ENC_RCAP>), dim3((uint32_t)nw), dim3(ENC_NT), 0, stream,
-                       values, elems, arena, n, out, cap, offsets, fv, stats, 2 * t, RR_ENC_FOLD4 ? totals : nullptr,
-                       err);
-    e = hipGetLastError();
-#if !RR_ENC_ATOT && !RR_ENC_FOLD4
-    if (e == hipSuccess && totals) e = launch_finalize(stats, lb, 2 * t, offsets, n, 0, totals, stream, err);
-#endif
-    return e;
+                       values, elems, arena, n, out, cap, offsets, fv, stats, 2 * t, totals, err);
+    return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------------------- shards

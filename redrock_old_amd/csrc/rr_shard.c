@@ -89,6 +89,74 @@ uint64_t rr_gather_layout(const uint64_t *shard_elems, int nranks, uint64_t *ele
     return e;
 }
 
+/* ---- the transfer schedules (rr_serdes.h): the pairing rr_split / rr_gather post ---------- */
+static int xfer(rr_xfer *out, int m, int peer, int dir, int buf, uint64_t offset, uint64_t bytes) {
+    if (bytes == 0) return m;   /* (both sides skip it: both know the plan) */
+    out[m].peer = peer;
+    out[m].dir = dir;
+    out[m].buf = buf;
+    out[m].rsv = 0;
+    out[m].offset = offset;
+    out[m].bytes = bytes;
+    return m + 1;
+}
+
+int rr_split_schedule(const rr_shard *plan, int nranks, int rank, int root, rr_xfer *out) {
+    if (!plan || !out || nranks < 1 || rank < 0 || rank >= nranks || root < 0 || root >= nranks) return -1;
+    int m = 0;
+    if (rank == root) {
+        for (int k = 0; k < nranks; k++) {
+            if (k == root) continue;
+            const rr_shard *p = &plan[k];
+            m = xfer(out, m, k, RR_XFER_SEND, RR_BUF_WHOLE_DATA, p->b0, p->b1 - p->b0);
+            m = xfer(out, m, k, RR_XFER_SEND, RR_BUF_WHOLE_OFFSETS, p->v0 * sizeof(uint64_t),
+                     (p->v1 - p->v0 + 1) * sizeof(uint64_t));
+        }
+    } else {
+        const rr_shard *p = &plan[rank];
+        m = xfer(out, m, root, RR_XFER_RECV, RR_BUF_MINE_DATA, 0, p->b1 - p->b0);
+        m = xfer(out, m, root, RR_XFER_RECV, RR_BUF_MINE_OFFSETS, 0, (p->v1 - p->v0 + 1) * sizeof(uint64_t));
+    }
+    return m;
+}
+
+int rr_gather_schedule(const rr_shard *plan, const uint64_t *shard_elems, int nranks, int rank, int root,
+                       rr_xfer *out) {
+    if (!plan || !shard_elems || !out || nranks < 1 || rank < 0 || rank >= nranks || root < 0 || root >= nranks)
+        return -1;
+    int m = 0;
+    if (rank == root) {
+        uint64_t at = 0;   /* rr_gather_layout's placement, shard by shard */
+        for (int k = 0; k < nranks; k++) {
+            const uint64_t nv = plan[k].v1 - plan[k].v0;
+            if (k != root) {
+                m = xfer(out, m, k, RR_XFER_RECV, RR_BUF_WHOLE_VALUES, plan[k].v0 * sizeof(rr_value), nv * sizeof(rr_value));
+                m = xfer(out, m, k, RR_XFER_RECV, RR_BUF_WHOLE_ELEMS, at * sizeof(rr_elem), shard_elems[k] * sizeof(rr_elem));
+            }
+            at += shard_elems[k];
+            if (at > 0xFFFFFFFFull) return -1;   /* elem_base is 32-bit */
+        }
+    } else {
+        const uint64_t nv = plan[rank].v1 - plan[rank].v0;
+        m = xfer(out, m, root, RR_XFER_SEND, RR_BUF_MINE_VALUES, 0, nv * sizeof(rr_value));
+        m = xfer(out, m, root, RR_XFER_SEND, RR_BUF_MINE_ELEMS, 0, shard_elems[rank] * sizeof(rr_elem));
+    }
+    return m;
+}
+
+/* post a schedule inside one ncclGroup (the group is always closed, whatever a call inside it
+ * returns); bufs[] = the device base of each RR_BUF_* */
+static ncclResult_t post_schedule(rr_comm *c, const rr_xfer *x, int m, uint8_t *const *bufs, hipStream_t s) {
+    ncclResult_t r = ncclGroupStart();
+    for (int i = 0; i < m && r == ncclSuccess; i++) {
+        uint8_t *p = bufs[x[i].buf] + x[i].offset;
+        r = x[i].dir == RR_XFER_SEND ? ncclSend(p, x[i].bytes, ncclUint8, x[i].peer, c->nc, s)
+                                     : ncclRecv(p, x[i].bytes, ncclUint8, x[i].peer, c->nc, s);
+    }
+    const ncclResult_t r2 = ncclGroupEnd();
+    return r == ncclSuccess ? r2 : r;
+}
+
 int rr_comm_get_id(uint8_t id[RR_COMM_ID_BYTES]) {
     ncclUniqueId u;
     NCCLCHK(ncclGetUniqueId(&u));
@@ -174,23 +242,18 @@ int rr_split(rr_comm *c, const rr_blob_batch *whole, const rr_shard *plan, int r
     if (rc) return rc;
     if (bad) return bad;
     if (any_bad) return rr_fail(RR_API_EINVAL, "rr_split: another rank's arguments are invalid");
-    /* the group is always closed, whatever a call inside it returns */
-    ncclResult_t r = ncclGroupStart();
-    if (r == ncclSuccess) {
-        if (c->rank == root) {
-            for (int k = 0; k < c->nranks && r == ncclSuccess; k++) {
-                if (k == root) continue;
-                const rr_shard *p = &plan[k];
-                if (p->b1 > p->b0) r = ncclSend(whole->data + p->b0, p->b1 - p->b0, ncclUint8, k, c->nc, s);
-                if (r == ncclSuccess) r = ncclSend(whole->offsets + p->v0, p->v1 - p->v0 + 1, ncclUint64, k, c->nc, s);
-            }
-        } else {
-            if (nb) r = ncclRecv(mine->data, nb, ncclUint8, root, c->nc, s);
-            if (r == ncclSuccess) r = ncclRecv(mine->offsets, nv + 1, ncclUint64, root, c->nc, s);
-        }
-        const ncclResult_t r2 = ncclGroupEnd();
-        if (r == ncclSuccess) r = r2;
+    rr_xfer *x = (rr_xfer *)malloc(sizeof(rr_xfer) * 2 * (size_t)c->nranks);
+    if (!x) return rr_fail(RR_API_ENOMEM, "malloc");
+    const int m = rr_split_schedule(plan, c->nranks, c->rank, root, x);
+    uint8_t *bufs[8] = {0};
+    if (c->rank == root) {
+        bufs[RR_BUF_WHOLE_DATA] = (uint8_t *)whole->data;
+        bufs[RR_BUF_WHOLE_OFFSETS] = (uint8_t *)whole->offsets;
     }
+    bufs[RR_BUF_MINE_DATA] = mine->data;
+    bufs[RR_BUF_MINE_OFFSETS] = (uint8_t *)mine->offsets;
+    const ncclResult_t r = m < 0 ? ncclInvalidArgument : post_schedule(c, x, m, bufs, s);
+    free(x);
     if (r != ncclSuccess) return rr_fail(RR_API_EHIP, "rr_split: %s", ncclGetErrorString(r));
     if (c->rank == root) {   /* the root's own shard: a device copy (nothing if it decodes in place) */
         if (mine->data != whole->data + me->b0 && nb)
@@ -243,20 +306,18 @@ int rr_gather(rr_comm *c, const rr_flat_batch *mine, uint64_t mine_elems, const 
     if (rc == RR_API_OK && (any_bad || root_bad))
         rc = bad ? bad : rbad ? rbad : rr_fail(RR_API_EINVAL, "rr_gather: another rank's arguments are invalid");
     if (rc == RR_API_OK) rr_gather_layout(cnt, R, at);
-    if (rc == RR_API_OK) {   /* the group is always closed, whatever a call inside it returns */
-        ncclResult_t r = ncclGroupStart();
-        for (int k = 0; k < R && r == ncclSuccess; k++) {
-            const uint64_t nv = plan[k].v1 - plan[k].v0;
-            if (c->rank == root && k != root) {
-                if (nv) r = ncclRecv(whole->values + plan[k].v0, nv * sizeof(rr_value), ncclUint8, k, c->nc, s);
-                if (r == ncclSuccess && cnt[k]) r = ncclRecv(whole->elems + at[k], cnt[k] * sizeof(rr_elem), ncclUint8, k, c->nc, s);
-            } else if (c->rank != root && k == c->rank) {
-                if (nv) r = ncclSend(mine->values, nv * sizeof(rr_value), ncclUint8, root, c->nc, s);
-                if (r == ncclSuccess && cnt[k]) r = ncclSend(mine->elems, cnt[k] * sizeof(rr_elem), ncclUint8, root, c->nc, s);
-            }
+    if (rc == RR_API_OK) {
+        rr_xfer *x = (rr_xfer *)malloc(sizeof(rr_xfer) * 2 * (size_t)R);
+        const int m = x ? rr_gather_schedule(plan, cnt, R, c->rank, root, x) : -1;
+        uint8_t *bufs[8] = {0};
+        bufs[RR_BUF_MINE_VALUES] = (uint8_t *)mine->values;
+        bufs[RR_BUF_MINE_ELEMS] = (uint8_t *)mine->elems;
+        if (c->rank == root) {
+            bufs[RR_BUF_WHOLE_VALUES] = (uint8_t *)whole->values;
+            bufs[RR_BUF_WHOLE_ELEMS] = (uint8_t *)whole->elems;
         }
-        const ncclResult_t r2 = ncclGroupEnd();
-        if (r == ncclSuccess) r = r2;
+        const ncclResult_t r = m < 0 ? ncclInvalidArgument : post_schedule(c, x, m, bufs, s);
+        free(x);
         if (r != ncclSuccess) rc = rr_fail(RR_API_EHIP, "rr_gather: %s", ncclGetErrorString(r));
     }
     if (rc == RR_API_OK && c->rank == root) {

@@ -9,10 +9,13 @@
  *                 status == 0  -> serObject(desObject(b)) must be the blob serObject writes for
  *                                 the object desObject built (the fixture's "reencoded", lru
  *                                 masked to 24 bits), and desString must keep the caller's lru.
- * Then the fork-child route: in-process (rr_compat_test_as_child) and through a real fork whose
- * child decodes every valid fixture through the parent's decode service.
+ * Then the fork-child route: in-process (rr_compat_test_as_child) and through real forks — a
+ * child that decodes every valid fixture through the parent's decode service, a child killed
+ * between its request and the reply followed by one that must get its own reply, and a child
+ * whose service was shut down, which must panic rather than wait.
  * Exit status 0 when every check passes.
  */
+#include <signal.h>
 #include <stdio.h>
 #include <string.h>
 #include <sys/wait.h>
@@ -180,8 +183,49 @@ int main(void) {
     int wst = -1;
     CHECK(pid > 0 && waitpid(pid, &wst, 0) == pid, "fork / waitpid");
     CHECK(WIFEXITED(wst) && WEXITSTATUS(wst) == 0, "forked child: decode differs or failed (wait status %d)", wst);
+
+    /* a child killed between its request and the reply (killRDBChild): the next child must get
+     * its own reply, not the dead child's (every fork has its own connection) */
+    const size_t ia = 0, ib = nok - 1;
+    const pid_t pa = fork();
+    if (pa == 0) _exit(rr_compat_test_send_only(bufs[ia], lens[ia]) == 0 ? 0 : 2);
+    CHECK(pa > 0 && waitpid(pa, &wst, 0) == pa && WIFEXITED(wst) && WEXITSTATUS(wst) == 0, "request-only child");
+    const pid_t pb = fork();
+    if (pb == 0) {
+        robj *o = desObject(bufs[ib], lens[ib]);
+        _exit(obj_eq(o, pobj[ib]) ? 0 : 1);
+    }
+    CHECK(pb > 0 && waitpid(pb, &wst, 0) == pb && WIFEXITED(wst) && WEXITSTATUS(wst) == 0,
+          "child after a killed child: wrong object (a stale reply?), status %d", wst);
+
+    /* the parent's service ends while a child is about to call: the child must fail (panic,
+     * exit 3), not wait forever; an alarm turns a hang into a failure */
+    int sync_fd[2];
+    CHECK(pipe(sync_fd) == 0, "pipe");
+    const pid_t pc = fork();
+    if (pc == 0) {
+        char c;
+        close(sync_fd[1]);
+        signal(SIGPIPE, SIG_IGN);   /* as Redis runs (server.c setupSignalHandlers) */
+        alarm(20);
+        if (read(sync_fd[0], &c, 1) != 1) _exit(4);
+        jmp_buf jb;
+        mr_panic_jmp = &jb;
+        if (setjmp(jb) == 0) {
+            (void)desObject(bufs[ia], lens[ia]);
+            _exit(5);   /* decoded through a service that was shut down */
+        }
+        _exit(3);
+    }
+    close(sync_fd[0]);
+    rr_compat_test_drop_services();
+    CHECK(write(sync_fd[1], "x", 1) == 1, "sync write");
+    close(sync_fd[1]);
+    CHECK(pc > 0 && waitpid(pc, &wst, 0) == pc && WIFEXITED(wst) && WEXITSTATUS(wst) == 3,
+          "child of a dead service: expected a panic (exit 3), wait status %d", wst);
+
     for (size_t i = 0; i < nok; i++) decrRefCount(pobj[i]);
     printf("compat shim: %d fixtures round-tripped, %d rejected with a panic, batch of %zu, child route %zu + %d, "
-           "forked child %zu; %d failures\n", checked, panics, nok, nok, child_panics, nok, fails);
+           "forked children 4; %d failures\n", checked, panics, nok, nok, child_panics, fails);
     return fails ? 1 : 0;
 }

@@ -1,10 +1,10 @@
 """Sharding across ranks through the C library's own plan, placement and
 rebase: rr_shard_plan (the rule shard_plan_kernel runs for rr_split_plan), rr_gather_layout
 (where rr_gather puts each shard's descriptors) and rr_flat_rebase_host / rr_flat_rebase (the
-placement flat_rebase_kernel applies on the root).  CPU tests: gloo with world size 2, the
-transfers in rr_split's / rr_gather's pairing (the root sends each peer its bytes + offsets;
-every peer sends the root its records + descriptors after an all-gather of the descriptor
-counts), the C oracle as the per-shard decoder (the checker stands in for the device on CPU).
+placement flat_rebase_kernel applies on the root).  CPU tests: gloo with world sizes 2 and 3
+running the C library's own transfer schedules (rr_split_schedule / rr_gather_schedule: the
+exact lists rr_split and rr_gather post inside their ncclGroup), the C oracle as the per-shard
+decoder (the checker stands in for the device on CPU).
 GPU tests: every shard decoded through the HIP C-ABI, placed by the device rebase, and the RCCL
 entry points with one rank."""
 import os
@@ -116,6 +116,25 @@ def _t(a):
     return torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).copy())
 
 
+def _run_schedule(xfers, bufs):
+    """Post a C transfer schedule over gloo (isend / irecv, all in flight, as inside rr_split's
+    ncclGroup), then land the received bytes in their buffers."""
+    ops, landing = [], []
+    for peer, direction, buf, off, nbytes in xfers:
+        view = bufs[buf][off:off + nbytes]
+        assert len(view) == nbytes, (buf, off, nbytes, len(bufs[buf]))
+        if direction == rr.XFER_SEND:
+            ops.append(dist.isend(torch.from_numpy(view.copy()), peer))
+        else:
+            t = torch.empty(nbytes, dtype=torch.uint8)
+            ops.append(dist.irecv(t, peer))
+            landing.append((view, t))
+    for op in ops:
+        op.wait()
+    for view, t in landing:
+        view[:] = t.numpy()
+
+
 def _worker(rank, world, port, cfg, n, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -131,52 +150,43 @@ def _worker(rank, world, port, cfg, n, q):
         dist.broadcast(plan_t, root)
         plan = plan_t.numpy().view(np.uint64).reshape(world, 4)
         v0, v1, b0, b1 = (int(x) for x in plan[rank])
-        # rr_split: the root sends each peer its bytes and offsets; the peer rebases them to 0
+        # rr_split: the C schedule, then the root's own shard by a local copy and the rebase of
+        # the offsets to 0 (offsets_rebase_kernel)
+        bufs = {rr.BUF_MINE_DATA: np.zeros((b1 - b0 + 15) & ~15, np.uint8),
+                rr.BUF_MINE_OFFSETS: np.zeros((v1 - v0 + 1) * 8, np.uint8)}
         if rank == root:
-            for k in range(world):
-                if k == root:
-                    continue
-                kb0, kb1, kv0, kv1 = int(plan[k, 2]), int(plan[k, 3]), int(plan[k, 0]), int(plan[k, 1])
-                if kb1 > kb0:
-                    dist.send(_t(data[kb0:kb1]), k)
-                dist.send(_t(offs[kv0:kv1 + 1]), k)
-            d, o = shard_of(data, offs, v0, v1)
-        else:
-            buf = torch.zeros(b1 - b0, dtype=torch.uint8)
-            if b1 > b0:
-                dist.recv(buf, root)
-            ob = torch.zeros((v1 - v0 + 1) * 8, dtype=torch.uint8)
-            dist.recv(ob, root)
-            d = np.zeros((b1 - b0 + 15) & ~15, np.uint8)
-            d[: b1 - b0] = buf.numpy()
-            o = ob.numpy().view(np.uint64) - np.uint64(b0)
+            bufs[rr.BUF_WHOLE_DATA] = data
+            bufs[rr.BUF_WHOLE_OFFSETS] = offs.view(np.uint8)
+            bufs[rr.BUF_MINE_DATA][: b1 - b0] = data[b0:b1]
+            bufs[rr.BUF_MINE_OFFSETS][:] = offs[v0:v1 + 1].view(np.uint8)
+        _run_schedule(rr.split_schedule(plan, rank, root), bufs)
+        d = bufs[rr.BUF_MINE_DATA]
+        o = bufs[rr.BUF_MINE_OFFSETS].view(np.uint64) - np.uint64(b0)
         sv, se, _, _ = cpu.decode(d, o)
-        # rr_gather: all-gather of the descriptor counts, peers send records + descriptors,
-        # the root places them (rr_gather_layout) and rebases them (rr_flat_rebase_host)
+        # rr_gather: all-gather of the descriptor counts, the C schedule (peers send records +
+        # descriptors, the root receives them at their places), the root's own shard copied in,
+        # then every shard rebased at its place (rr_gather_layout, rr_flat_rebase_host)
         ne = torch.zeros(world, dtype=torch.int64)
         dist.all_gather_into_tensor(ne, torch.tensor([len(se)], dtype=torch.int64))
         ne = [int(x) for x in ne]
+        bufs = {rr.BUF_MINE_VALUES: np.ascontiguousarray(sv).view(np.uint8).reshape(-1),
+                rr.BUF_MINE_ELEMS: np.ascontiguousarray(se).view(np.uint8).reshape(-1)}
         if rank == root:
-            parts = []
+            at, tot = rr.gather_layout(ne)
+            wv = np.zeros(n, rr.VALUE_DT)
+            we = np.zeros(tot, rr.ELEM_DT)
+            wv[v0:v1] = sv
+            we[int(at[root]):int(at[root]) + len(se)] = se
+            bufs[rr.BUF_WHOLE_VALUES] = wv.view(np.uint8).reshape(-1)
+            bufs[rr.BUF_WHOLE_ELEMS] = we.view(np.uint8).reshape(-1)
+        _run_schedule(rr.gather_schedule(plan, ne, rank, root), bufs)
+        if rank == root:
             for k in range(world):
-                if k == root:
-                    parts.append((sv, se))
-                    continue
-                kv = int(plan[k, 1] - plan[k, 0])
-                vb = torch.zeros(kv * 16, dtype=torch.uint8)
-                eb = torch.zeros(ne[k] * 16, dtype=torch.uint8)
-                if kv:
-                    dist.recv(vb, k)
-                if ne[k]:
-                    dist.recv(eb, k)
-                parts.append((vb.numpy().view(rr.VALUE_DT), eb.numpy().view(rr.ELEM_DT)))
-            wv, we, _, _ = cpu.decode(data, offs)
-            assert_flat_equal(place(plan, parts, n), (wv, we), f"split/gather cfg {cfg}")
-        else:
-            if v1 > v0:
-                dist.send(_t(sv), root)
-            if ne[rank]:
-                dist.send(_t(se), root)
+                kv0, kv1, kb0 = int(plan[k, 0]), int(plan[k, 1]), int(plan[k, 2])
+                ea = int(at[k])
+                rr.flat_rebase_host(wv[kv0:kv1], we[ea:ea + ne[k]], ea, kb0)
+            xv, xe, _, _ = cpu.decode(data, offs)
+            assert_flat_equal((wv, we), (xv, xe), f"split/gather cfg {cfg} world {world}")
         q.put((rank, "ok", v0, v1 - v0))
     except Exception as ex:   # report to the parent
         q.put((rank, repr(ex), -1, -1))
@@ -184,19 +194,44 @@ def _worker(rank, world, port, cfg, n, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("cfg,n", [(4, 4000), (10, 300), (10, 0), (2, 700)])
-def test_split_gather_gloo_world2(cfg, n):
+@pytest.mark.parametrize("cfg,n,world", [(4, 4000, 2), (10, 300, 2), (10, 0, 2), (2, 700, 2), (4, 3000, 3),
+                                         (10, 2, 3)])
+def test_split_gather_gloo(cfg, n, world):
+    """The C schedules run over gloo; (10, 2, 3): two values over three ranks, so a shard is empty."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, cfg, n, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, cfg, n, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted(q.get(timeout=240) for _ in procs)
     for p in procs:
         p.join(timeout=60)
-    assert [r[1] for r in res] == ["ok", "ok"], res
-    assert res[0][2] == 0 and res[0][3] + res[1][3] == n and res[1][2] == res[0][3]
+    assert [r[1] for r in res] == ["ok"] * world, res
+    assert res[0][2] == 0 and sum(r[3] for r in res) == n
+    assert all(res[k + 1][2] == res[k][2] + res[k][3] for k in range(world - 1))
+    if (cfg, n, world) == (10, 2, 3):
+        assert any(r[3] == 0 for r in res)
+
+
+def test_schedules_pair_up():
+    """Every send one rank's schedule posts is a receive of the same size in its peer's, in the
+    same order per pair (what lets ncclGroup and gloo match them)."""
+    for g, n in [(1, 100), (3, 1000), (8, 5000), (4, 2)]:
+        _, offs = rr.gen_batch(4, n)
+        plan = rr.shard_plan(offs, g)
+        ne = [int(x) for x in np.random.default_rng(g).integers(0, 500, g)]
+        for root in range(g):
+            for sched in (lambda r: rr.split_schedule(plan, r, root), lambda r: rr.gather_schedule(plan, ne, r, root)):
+                lists = {r: sched(r) for r in range(g)}
+                for r in range(g):
+                    for peer in range(g):
+                        sends = [x[4] for x in lists[r] if x[0] == peer and x[1] == rr.XFER_SEND]
+                        recvs = [x[4] for x in lists[peer] if x[0] == r and x[1] == rr.XFER_RECV]
+                        assert sends == recvs, (g, root, r, peer)
+                assert all(x[4] > 0 for xs in lists.values() for x in xs)   # no zero-byte transfer
+    with pytest.raises(rr.RRError):   # a gather placed past 2^32 - 1 descriptors
+        rr.gather_schedule(rr.shard_plan(np.array([0, 1, 2], np.uint64), 2), [2 ** 31, 2 ** 31], 0, 0)
 
 
 @pytest.mark.gpu
