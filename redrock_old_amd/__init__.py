@@ -34,6 +34,8 @@ STATUS_NAMES = {0: "OK", 1: "SHORT", 2: "TYPE", 3: "STR_ENC", 4: "STR_INTLEN", 5
                 12: "ENCODE", 13: "DUP", 14: "NAN"}
 
 CONFIG_MIXED = 4
+CTX_NO_SMALL = 1          # rr_ctx_set_options: no one-launch small-batch kernels
+SMALL_N, SMALL_BYTES = 4096, 128 * 1024   # the one-launch kernels' limits (rr_serdes.h)
 
 
 class RRError(RuntimeError):
@@ -83,7 +85,7 @@ EXPORTS = ["rr_ctx_create", "rr_ctx_destroy", "rr_ctx_reserve", "rr_last_error",
            "rr_gen_batch", "rr_host_batch_free", "rr_gen_default_seed", "rr_shard_plan", "rr_flat_rebase",
            "rr_comm_get_id", "rr_comm_init", "rr_comm_destroy", "rr_split_plan", "rr_split", "rr_gather",
            "rr_flat_rebase_host", "rr_gather_layout", "rr_copy_device", "rr_gen_sizes", "rr_gen_range",
-           "rr_split_schedule", "rr_gather_schedule"]
+           "rr_split_schedule", "rr_gather_schedule", "rr_ctx_set_options"]
 COMM_ID_BYTES = 128
 # include/rr_snappy.h (GPU block compression)
 SNAPPY_EXPORTS = ["rr_snappy_max_compressed_length", "rr_snappy_compress_bound", "rr_snappy_compress_batch",
@@ -116,6 +118,8 @@ def lib():
     L.rr_ctx_destroy.argtypes = [vp]
     L.rr_ctx_destroy.restype = None
     L.rr_ctx_reserve.argtypes = [vp, u64, u64]
+    if hasattr(L, "rr_ctx_set_options"):   # (RR_LIB: an older build for A/B timing may predate it)
+        L.rr_ctx_set_options.argtypes = [vp, C.c_uint]
     L.rr_last_error.restype = C.c_char_p
     L.rr_decode_batch.argtypes = [vp, C.POINTER(BlobBatch), C.POINTER(FlatBatch), vp, vp]
     L.rr_encode_batch.argtypes = [vp, C.POINTER(FlatBatch), C.POINTER(BlobBatch), vp, vp]
@@ -289,6 +293,10 @@ class Engine:
             self.close()
         except Exception:
             pass
+
+    def set_options(self, flags: int):
+        """RR_CTX_* flags (CTX_NO_SMALL: every call takes the batch pipeline)."""
+        _check(self._L.rr_ctx_set_options(self._ctx, flags))
 
     def reserve(self, n: int, nbytes: int = 0):
         _check(self._L.rr_ctx_reserve(self._ctx, n, nbytes))

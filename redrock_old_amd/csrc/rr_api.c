@@ -65,6 +65,7 @@ void rr_ctx_destroy(rr_ctx *c) {
     dfree(&c->d_elems, &c->c_elems); dfree(&c->d_arena, &c->c_arena); dfree(&c->d_out, &c->c_out);
     dfree(&c->d_ooff, &c->c_ooff);
     if (c->d_totals) hipFree(c->d_totals);
+    if (c->h_small) hipHostFree(c->h_small);
     if (c->pipe_ready) {
         for (int k = 0; k < RR_HOST_MAXCHUNK; k++) { hipEventDestroy(c->ev_up[k]); hipEventDestroy(c->ev_dec[k]); }
         hipStreamDestroy(c->up);
@@ -111,6 +112,14 @@ int rr_mark_scratch(rr_ctx *c, hipStream_t stream) {
     return RR_API_OK;
 }
 
+int rr_ctx_set_options(rr_ctx *c, unsigned flags) {
+    if (!c || (flags & ~RR_CTX_NO_SMALL)) return fail(RR_API_EINVAL, "rr_ctx_set_options: bad argument");
+    c->options = flags;
+    return RR_API_OK;
+}
+#define SMALL_DEC(c, n, cap) (!((c)->options & RR_CTX_NO_SMALL) && rr_small_decode_fits((n), (cap)))
+#define SMALL_ENC(c, n, cap) (!((c)->options & RR_CTX_NO_SMALL) && rr_small_encode_fits((n), (cap)))
+
 int rr_ctx_reserve(rr_ctx *c, uint64_t n_values, uint64_t n_bytes) {
     if (!c) return fail(RR_API_EINVAL, "ctx is NULL");
     uint64_t a = rr_encode_scratch_words(n_values, (n_bytes + 15) & ~15ull), b = rr_decode_scratch_words((n_bytes + 15) & ~15ull, n_values);
@@ -135,6 +144,12 @@ int rr_decode_batch(rr_ctx *c, const rr_blob_batch *in, rr_flat_batch *out, rr_t
     if (!aligned16(in->data) || !aligned16(out->arena)) return fail(RR_API_EINVAL, "data/arena not 16-byte aligned");
     if (in->data_cap & 15) return fail(RR_API_EINVAL, "data_cap must be a multiple of 16");
     if (out->arena_cap < in->data_cap) return fail(RR_API_EINVAL, "arena_cap < data_cap");
+    if (SMALL_DEC(c, in->n, in->data_cap)) {   /* one launch, no scratch */
+        HIPCHK(hipSetDevice(c->device));
+        HIPCHK(rr_launch_decode_small(in->data, in->offsets, in->n, out->values, out->elems, out->elem_cap, out->arena,
+                                      d_totals, (hipStream_t)stream));
+        return RR_API_OK;
+    }
     int rc = ensure_scratch(c, rr_decode_scratch_words(in->data_cap, in->n), (hipStream_t)stream);
     if (rc) return rc;
     HIPCHK(rr_launch_decode(in->data, in->offsets, in->n, out->values, out->elems, out->elem_cap, out->arena,
@@ -149,6 +164,12 @@ int rr_encode_batch(rr_ctx *c, const rr_flat_batch *in, rr_blob_batch *out, rr_t
     if (!out->offsets) return fail(RR_API_EINVAL, "NULL offsets");
     if (in->n && (!in->values || !out->data)) return fail(RR_API_EINVAL, "NULL buffer");
     if ((uintptr_t)out->data & 15) return fail(RR_API_EINVAL, "out->data must be 16-byte aligned");
+    if (SMALL_ENC(c, in->n, out->data_cap)) {   /* one launch, no scratch */
+        HIPCHK(hipSetDevice(c->device));
+        HIPCHK(rr_launch_encode_small(in->values, in->elems, in->elem_cap, in->arena, in->arena_cap, in->n, out->data,
+                                      out->data_cap, out->offsets, d_totals, (hipStream_t)stream));
+        return RR_API_OK;
+    }
     int rc = ensure_scratch(c, rr_encode_scratch_words(in->n, out->data_cap), (hipStream_t)stream);
     if (rc) return rc;
     HIPCHK(rr_launch_encode(in->values, in->elems, in->elem_cap, in->arena, in->arena_cap, in->n, out->data,
@@ -289,6 +310,51 @@ static int decode_host_pipelined(rr_ctx *c, const uint8_t *data, const uint64_t 
     return rc;
 }
 
+/* ---- small batches through the host entry points --------------------------------------
+ * One pinned host buffer, mapped into the device, holds the call's input and output: the
+ * one-launch kernel reads the input from it (16-byte loads over PCIe) and writes the records
+ * there; the host copies in before the launch and out after one stream synchronisation.  No
+ * device staging, no transfer calls: the per-value path of the compat shim (desObject /
+ * serObject) pays one launch and one synchronisation. */
+static int small_grow(rr_ctx *c, size_t need) {
+    if (need <= c->c_small && c->h_small) return RR_API_OK;
+    if (c->h_small) HIPCHK(hipHostFree(c->h_small));
+    c->h_small = c->d_small = NULL;
+    c->c_small = 0;
+    const size_t want = need + need / 2 + 4096;
+    HIPCHK(hipHostMalloc((void **)&c->h_small, want, hipHostMallocMapped));
+    HIPCHK(hipHostGetDevicePointer((void **)&c->d_small, c->h_small, 0));
+    c->c_small = want;
+    return RR_API_OK;
+}
+#define AL16(x) (((x) + 15) & ~(size_t)15)
+
+static int decode_host_small(rr_ctx *c, const uint8_t *data, const uint64_t *offsets, uint64_t n, rr_value *values,
+                             rr_elem *elems, uint64_t elem_cap, uint8_t *arena, rr_totals *totals) {
+    const uint64_t bytes = offsets[n];
+    const size_t o_off = 0, o_dat = AL16((n + 1) * sizeof(uint64_t)), o_tot = o_dat + AL16(bytes) + 16,
+                 o_val = o_tot + sizeof(rr_totals), o_el = AL16(o_val + n * sizeof(rr_value)),
+                 end = o_el + elem_cap * sizeof(rr_elem);
+    int rc = small_grow(c, end);
+    if (rc) return rc;
+    uint8_t *h = c->h_small, *d = c->d_small;
+    /* the previous call on this context is done with the buffer (its own synchronisation) */
+    memcpy(h + o_off, offsets, (n + 1) * sizeof(uint64_t));
+    if (bytes) memcpy(h + o_dat, data, bytes);
+    memset(h + o_dat + bytes, 0, AL16(bytes) + 16 - bytes);
+    HIPCHK(rr_launch_decode_small(d + o_dat, (const uint64_t *)(d + o_off), n, (rr_value *)(d + o_val),
+                                  (rr_elem *)(d + o_el), elem_cap, NULL, (rr_totals *)(d + o_tot), c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    rr_totals t;
+    memcpy(&t, h + o_tot, sizeof t);
+    if (n) memcpy(values, h + o_val, n * sizeof(rr_value));
+    const uint64_t ne = t.n_elems < elem_cap ? t.n_elems : elem_cap;
+    if (ne && elems) memcpy(elems, h + o_el, ne * sizeof(rr_elem));
+    if (bytes && arena) memcpy(arena, data, bytes);   /* the arena mirrors the blob bytes */
+    if (totals) *totals = t;
+    return RR_API_OK;
+}
+
 int rr_decode_batch_host(rr_ctx *c, const uint8_t *data, const uint64_t *offsets, uint64_t n, rr_value *values,
                          rr_elem *elems, uint64_t elem_cap, uint8_t *arena, rr_totals *totals) {
     if (!c || !offsets || (n && (!data || !values))) return fail(RR_API_EINVAL, "NULL argument");
@@ -299,6 +365,7 @@ int rr_decode_batch_host(rr_ctx *c, const uint8_t *data, const uint64_t *offsets
     HIPCHK(hipSetDevice(c->device));
     uint64_t bytes = offsets[n];
     size_t pbytes = (size_t)((bytes + 15) & ~15ull);
+    if (SMALL_DEC(c, n, pbytes)) return decode_host_small(c, data, offsets, n, values, elems, elem_cap, arena, totals);
     GROW(c->d_in, c->c_in, pbytes + 16);
     GROW(c->d_off, c->c_off, (n + 1) * sizeof(uint64_t));
     GROW(c->d_vals, c->c_vals, (n ? n : 1) * sizeof(rr_value));
@@ -338,11 +405,38 @@ int rr_decode_batch_host(rr_ctx *c, const uint8_t *data, const uint64_t *offsets
     return RR_API_OK;
 }
 
+static int encode_host_small(rr_ctx *c, const rr_value *values, const rr_elem *elems, uint64_t n_elems,
+                             const uint8_t *arena, uint64_t arena_bytes, uint64_t n, uint8_t *data, uint64_t data_cap,
+                             uint64_t *offsets, rr_totals *totals) {
+    const size_t o_val = 0, o_el = AL16(n * sizeof(rr_value)), o_ar = o_el + AL16(n_elems * sizeof(rr_elem)),
+                 o_off = o_ar + AL16(arena_bytes), o_tot = o_off + AL16((n + 1) * sizeof(uint64_t)),
+                 o_out = o_tot + 32, end = o_out + AL16(data_cap) + 16;
+    int rc = small_grow(c, end);
+    if (rc) return rc;
+    uint8_t *h = c->h_small, *d = c->d_small;
+    memcpy(h + o_val, values, n * sizeof(rr_value));
+    if (n_elems) memcpy(h + o_el, elems, n_elems * sizeof(rr_elem));
+    if (arena_bytes) memcpy(h + o_ar, arena, arena_bytes);
+    HIPCHK(rr_launch_encode_small((const rr_value *)(d + o_val), (const rr_elem *)(d + o_el), n_elems, d + o_ar,
+                                  arena_bytes, n, d + o_out, data_cap, (uint64_t *)(d + o_off),
+                                  (rr_totals *)(d + o_tot), c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    rr_totals t;
+    memcpy(&t, h + o_tot, sizeof t);
+    memcpy(offsets, h + o_off, (n + 1) * sizeof(uint64_t));
+    const uint64_t nb = t.bytes < data_cap ? t.bytes : data_cap;
+    if (nb) memcpy(data, h + o_out, nb);
+    if (totals) *totals = t;
+    return RR_API_OK;
+}
+
 int rr_encode_batch_host(rr_ctx *c, const rr_value *values, const rr_elem *elems, uint64_t n_elems,
                          const uint8_t *arena, uint64_t arena_bytes, uint64_t n, uint8_t *data, uint64_t data_cap,
                          uint64_t *offsets, rr_totals *totals) {
     if (!c || !offsets || (n && (!values || !data))) return fail(RR_API_EINVAL, "NULL argument");
     HIPCHK(hipSetDevice(c->device));
+    if (SMALL_ENC(c, n, data_cap))
+        return encode_host_small(c, values, elems, n_elems, arena, arena_bytes, n, data, data_cap, offsets, totals);
     GROW(c->d_vals, c->c_vals, (n ? n : 1) * sizeof(rr_value));
     GROW(c->d_elems, c->c_elems, (n_elems ? n_elems : 1) * sizeof(rr_elem));
     GROW(c->d_arena, c->c_arena, arena_bytes + 16);

@@ -9,6 +9,7 @@
 
 struct rr_ctx {
     int device;
+    unsigned options;            /* RR_CTX_* */
     hipStream_t stream;          /* used by the host entry points */
     uint64_t *scratch;           /* look-back words + counters */
     uint64_t scratch_words;
@@ -23,6 +24,10 @@ struct rr_ctx {
     hipStream_t up, down;
     hipEvent_t ev_up[RR_HOST_MAXCHUNK], ev_dec[RR_HOST_MAXCHUNK];
     rr_totals *d_ktot, *h_ktot;   /* device / pinned host, RR_HOST_MAXCHUNK each */
+    /* small batches through the host entry points: one pinned buffer mapped into the device,
+     * which the one-launch kernels read their input from and write their output to */
+    uint8_t *h_small, *d_small;
+    size_t c_small;
 };
 
 /* the context's scratch: grow to `words` (waits on the previous call through an event; fails

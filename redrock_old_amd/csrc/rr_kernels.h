@@ -38,6 +38,14 @@ hipError_t rr_launch_flat_rebase(rr_value *values, uint64_t n, rr_elem *elems, u
                                  uint64_t byte_add, hipStream_t stream);
 uint64_t rr_encode_scratch_words(uint64_t n, uint64_t data_cap);
 hipError_t rr_launch_copy(uint8_t *dst, const uint8_t *src, uint64_t bytes, hipStream_t stream);
+/* small batches (one workgroup, one launch): whether a batch qualifies, and the launches */
+int rr_small_decode_fits(uint64_t n, uint64_t data_cap);
+int rr_small_encode_fits(uint64_t n, uint64_t data_cap);
+hipError_t rr_launch_decode_small(const uint8_t *blob, const uint64_t *offsets, uint64_t n, rr_value *values,
+                                  rr_elem *elems, uint64_t elem_cap, uint8_t *arena, rr_totals *totals, hipStream_t stream);
+hipError_t rr_launch_encode_small(const rr_value *values, const rr_elem *elems, uint64_t elem_cap, const uint8_t *arena,
+                                  uint64_t arena_cap, uint64_t n, uint8_t *out, uint64_t cap, uint64_t *offsets,
+                                  rr_totals *totals, hipStream_t stream);
 
 #ifdef __cplusplus
 }

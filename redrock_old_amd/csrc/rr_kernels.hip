@@ -331,7 +331,8 @@ __device__ __forceinline__ void fold_totals(const uint64_t *__restrict__ stats, 
 // ---- K1: reservation + class per value ------------------------------------------------
 // reserve(i) = the descriptor slots value i owns (rr_format.h): header fields only, plus the
 // length chain of a List.  Equal to the decoded count for every valid blob.
-__device__ __forceinline__ uint64_t zl_walk_count_g(const uint8_t *zl, uint64_t L) {
+template <typename P>
+__device__ __forceinline__ uint64_t zl_walk_count_g(P zl, uint64_t L) {
     uint64_t p = 10, n = 0;
     while (p < L - 1 && zl[p] != 0xFF) {
         const uint64_t q = p + (zl[p] < 254 ? 1 : 5);
@@ -379,9 +380,14 @@ __device__ __forceinline__ void head24(const uint8_t *blob, uint64_t o, uint64_t
     }
 }
 typedef uint32_t u32_ua __attribute__((aligned(1)));   // unaligned dword (one global_load_dword)
-// The descriptor reservation (rr_format.h) and the walk class of a value from its header dwords.
-__device__ __forceinline__ void reserve_classify(const uint8_t *b, uint64_t L, const uint32_t (&d)[6],
-                                                 uint64_t &r, uint32_t &c) {
+// a List length field: one unaligned dword load from global memory (gfx950 serves it from one
+// line; an aligned pair + alignbyte measured count 52.5 -> 54.6 us), byte reads from LDS
+__device__ __forceinline__ uint32_t len_u32(const uint8_t *p) { return *reinterpret_cast<const u32_ua *>(p); }
+__device__ __forceinline__ uint32_t len_u32(lds_cptr p) { return ld_u32(p); }
+// The descriptor reservation (rr_format.h) and the walk class of a value from its header dwords
+// (b: the value's bytes, in global memory or an LDS stage).
+template <typename P>
+__device__ __forceinline__ void reserve_classify(P b, uint64_t L, const uint32_t (&d)[6], uint64_t &r, uint32_t &c) {
     r = 0;
     c = C_EXACT;
     if (L < 5) return;
@@ -405,9 +411,7 @@ __device__ __forceinline__ void reserve_classify(const uint8_t *b, uint64_t L, c
             uint64_t p = 5, n = 0;
             while (p < L) {
                 if (L - p < 4) break;
-                // one unaligned dword load (gfx950 serves it from one line; an aligned pair +
-                // alignbyte measured count 52.5 -> 54.6 us)
-                const uint64_t l = *reinterpret_cast<const u32_ua *>(b + p);
+                const uint64_t l = len_u32(b + p);
                 if (l > L - p - 4) break;
                 ++n;
                 p += 4 + l;
@@ -578,17 +582,17 @@ __device__ __forceinline__ uint32_t mark_fixup(uint32_t *nfix) {
     return FIX_MARK_ST;
 }
 
-// The exact parser, lane = value v (from global memory): the reference's status codes for
-// malformed values, zero-filled slots, capacity handling.  (eb, r: the value's first
-// descriptor slot and its reservation)
-__device__ __forceinline__ Acc exact_value(const uint8_t *__restrict__ blob, uint64_t v,
-                                           const uint64_t *__restrict__ offsets, uint64_t eb, uint64_t r,
-                                           rr_value *__restrict__ values, rr_elem *__restrict__ elems, uint64_t cap,
-                                           uint32_t *nfix) {
+// The exact parser, lane = value v: the reference's status codes for malformed values,
+// zero-filled slots, capacity handling.  src: the batch's bytes from batch offset src0 on
+// (global memory, or an LDS stage); eb, r: the value's first descriptor slot and its reservation.
+template <typename P>
+__device__ __forceinline__ Acc exact_value(P src, uint64_t src0, uint64_t v, const uint64_t *__restrict__ offsets,
+                                           uint64_t eb, uint64_t r, rr_value *__restrict__ values,
+                                           rr_elem *__restrict__ elems, uint64_t cap, uint32_t *nfix) {
     uint64_t pay = 0;
     const uint64_t o_lo = offsets[v], o_hi = offsets[v + 1];
-    const uint8_t *b = blob + o_lo;
-    Parsed pr = parse_value<false, const uint8_t *>(b, o_lo, o_hi - o_lo, nullptr);
+    const P b = src + (o_lo - src0);
+    Parsed pr = parse_value<false, P>(b, o_lo, o_hi - o_lo, nullptr);
     uint32_t status = pr.status;
     uint64_t ne = pr.n;
     if (status == RR_OK && ne != r) status = RR_E_COUNT;
@@ -600,7 +604,7 @@ __device__ __forceinline__ Acc exact_value(const uint8_t *__restrict__ blob, uin
     } else if (!fits) {
         status = RR_E_CAPACITY;
     } else {
-        Parsed e = parse_value<true, const uint8_t *>(b, o_lo, o_hi - o_lo, elems + eb);
+        Parsed e = parse_value<true, P>(b, o_lo, o_hi - o_lo, elems + eb);
         pay += e.payload;
         const uint32_t t = ld_u8(b);
         const uint64_t keys = t == RR_TYPE_HASH_HT ? ne / 2 : ne;
@@ -705,7 +709,7 @@ __device__ __forceinline__ Acc run_batch(const Src &src, uint32_t c, bool active
         }
         active &= g == 0;   // the exact parser runs once per value, on the group's lane 0
     }
-    if (active && exact) acc = exact_value(blob, v, offsets, eb_v, r_v, values, elems, cap, nfix);
+    if (active && exact) acc = exact_value(blob, 0, v, offsets, eb_v, r_v, values, elems, cap, nfix);
     return acc;
 }
 
@@ -1008,7 +1012,8 @@ __global__ __launch_bounds__(NW * RR_WAVE) __attribute__((amdgpu_waves_per_eu(DE
     const uint8_t *__restrict__ blob, uint64_t data_cap, const uint64_t *__restrict__ offsets, uint64_t n,
     const uint32_t *__restrict__ first_val, const uint8_t *__restrict__ cls, const uint32_t *__restrict__ counts,
     const uint64_t *__restrict__ wtot, const uint64_t *__restrict__ gtot, rr_value *__restrict__ values,
-    rr_elem *__restrict__ elems, uint64_t elem_cap, uint8_t *__restrict__ arena, uint32_t nwin, rr_totals *tot) {
+    rr_elem *__restrict__ elems, uint64_t elem_cap, uint8_t *__restrict__ arena, uint32_t nwin, uint32_t win,
+    rr_totals *tot) {
     constexpr uint32_t NT = NW * RR_WAVE, STAGE = W + SLACK;
     static_assert(PMAX == NT, "a chunk is one value per thread (the slot scan)");
     static_assert(W % 16 == 0 && SLACK % 16 == 0, "tile shape");
@@ -1031,8 +1036,8 @@ __global__ __launch_bounds__(NW * RR_WAVE) __attribute__((amdgpu_waves_per_eu(DE
     uint64_t pre = tid < gi ? wtot[(uint64_t)grp * WGROUP + tid] : 0;
     for (uint32_t k = tid; k < grp; k += NT) pre += gtot[k];
     const uint64_t padded = (offsets[n] + 15) & ~15ull;
-    const uint64_t W0 = (uint64_t)tile * W;
-    const uint64_t W1 = W0 + W < padded ? W0 + W : padded;
+    const uint64_t W0 = (uint64_t)tile * win;   // (win <= W: the call's window size, launch_decode)
+    const uint64_t W1 = W0 + win < padded ? W0 + win : padded;
     // the arena copy starts at the call's first value (a call over a slice of a larger buffer —
     // the chunks of rr_decode_batch_host — copies only its own bytes); the stage always lies
     // past it (S0 >= offsets[v_lo] >= offsets[0])
@@ -1272,6 +1277,94 @@ __global__ __launch_bounds__(NW * RR_WAVE) __attribute__((amdgpu_waves_per_eu(DE
         if (tot && tile == nwin - 1) tot->n_elems = first_slot() + run + ctot;
         PROBE(prb[0] = pt1 - pt0; prb[1] = pt2 - pt1; prb[2] = __builtin_amdgcn_s_memtime() - pt2; prb[28] = v_hi - v_lo;
               prb[29] = staged; if (g_probe) for (uint32_t i = 0; i < PROBE_WORDS; ++i) g_probe[(uint64_t)tile * PROBE_WORDS + i] = prb[i];)
+    }
+}
+
+// ---- small batches: the whole decode in one launch --------------------------------------
+// The per-value callers (desObject on the rock thread, rock.c:468; the restore queue,
+// rock.c:302-383) hand over one or a few values at a time, where the pipeline's launches, not
+// bytes, are the cost.  A batch of at most SMALL_N values in at most SMALL_BYTES is decoded by
+// ONE workgroup in ONE launch: its bytes staged into LDS with 16-byte loads (the source may be
+// pinned host memory mapped into the device: rr_decode_batch_host), the reservations from the
+// headers (count_kernel's rule), an in-block scan for the slots, the exact parser per value
+// from LDS (the reference's statuses; the walks' results are the parser's by construction), the
+// fixup of marked values, and the totals — the same records, descriptors, arena and totals as
+// the pipeline, byte for byte.
+constexpr uint32_t SMALL_NT = 1024, SMALL_VPT = 4, SMALL_N = SMALL_NT * SMALL_VPT;
+constexpr uint32_t SMALL_BYTES = 128 * 1024;   // (one workgroup: up to 160 KiB of LDS)
+constexpr uint32_t SMALL_STAGE = SMALL_BYTES + 8192;   // + the reads past a value's end; >= the fixup's LDS
+static_assert(FIX_LDS + 4 * (SMALL_NT + 1) <= SMALL_STAGE, "the fixup reuses the stage");
+
+__global__ __launch_bounds__(SMALL_NT) void decode_small_kernel(const uint8_t *__restrict__ blob,
+                                                                const uint64_t *__restrict__ offsets, uint64_t n,
+                                                                rr_value *__restrict__ values,
+                                                                rr_elem *__restrict__ elems, uint64_t elem_cap,
+                                                                uint8_t *__restrict__ arena, rr_totals *tot) {
+    __shared__ __attribute__((aligned(16))) uint8_t stage[SMALL_STAGE];
+    __shared__ uint64_t wsum[SMALL_NT / RR_WAVE], red[2][SMALL_NT / RR_WAVE];
+    __shared__ uint32_t nfix;
+    const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid / RR_WAVE;
+    if (tid == 0) nfix = 0;
+    if (tid < 4) reinterpret_cast<uint64_t *>(tot)[tid] = 0;   // (the fixup adds into them)
+    const uint64_t B0 = offsets[0] & ~15ull, B1 = (offsets[n] + 15) & ~15ull;
+    // my values: v0 .. v0 + SMALL_VPT - 1 (consecutive: the block scan runs in value order)
+    const uint64_t v0 = (uint64_t)tid * SMALL_VPT;
+    uint64_t o[SMALL_VPT + 1];
+#pragma unroll
+    for (uint32_t j = 0; j <= SMALL_VPT; ++j) o[j] = offsets[v0 + j < n ? v0 + j : n];
+    // 1. the bytes into the stage (and the mirror arena), 16-byte granules, every load in flight
+    typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
+    lds_u32x4 *st4 = (lds_u32x4 *)(__attribute__((address_space(3))) uint8_t *)stage;
+    const uint32_t ng = (uint32_t)((B1 - B0) >> 4);
+    const u32x4 *src4 = reinterpret_cast<const u32x4 *>(blob + B0);
+    for (uint32_t g = tid; g < ng; g += SMALL_NT) {
+        const u32x4 x = src4[g];
+        st4[g] = x;
+        if (arena) reinterpret_cast<u32x4 *>(arena + B0)[g] = x;
+    }
+    __syncthreads();
+    const lds_cptr S = (lds_cptr)stage;
+    // 2. reservations from the headers (count_kernel's rule) and their block scan
+    uint64_t r[SMALL_VPT], sum = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < SMALL_VPT; ++j) {
+        r[j] = 0;
+        if (v0 + j < n) {
+            const uint32_t q = (uint32_t)(o[j] - B0);
+            uint32_t d[6];
+            LdsSrc{S}.get<6>(q, d);   // (reads up to 28 bytes past q: inside the stage's slack)
+            uint32_t c;
+            reserve_classify(S + q, o[j + 1] - o[j], d, r[j], c);
+        }
+        sum += r[j];
+    }
+    uint64_t total;
+    uint64_t eb = block_excl_scan<SMALL_NT>(sum, wsum, total);
+    // 3. the exact parser per value, from the stage
+    const uint64_t cap = elem_cap < 0xFFFFFFFFull ? elem_cap : 0xFFFFFFFFull;   // elem_base is 32-bit
+    uint64_t bad = 0, pay = 0;
+#pragma unroll 1
+    for (uint32_t j = 0; j < SMALL_VPT; ++j) {
+        if (v0 + j < n) {
+            const Acc a = exact_value(S, B0, v0 + j, offsets, eb, r[j], values, elems, cap, &nfix);
+            bad += a.bad;
+            pay += a.pay;
+        }
+        eb += r[j];
+    }
+    bad = wave_sum_fast(bad);
+    pay = wave_sum_fast(pay);
+    if (lane == 0) { red[0][wave] = bad; red[1][wave] = pay; }
+    __syncthreads();   // (also: every record and descriptor visible to the workgroup, for the fixup)
+    // 4. marked values (duplicate keys, unsorted skiplists), in the stage's LDS
+    if (nfix) fixup_window<SMALL_NT>(blob, 0, n, values, elems, tot, stage);
+    if (tid == 0) {
+        uint64_t tb = 0, tp = 0;
+        for (uint32_t w = 0; w < SMALL_NT / RR_WAVE; ++w) { tb += red[0][w]; tp += red[1][w]; }
+        atomicAdd((unsigned long long *)&tot->n_bad, (unsigned long long)tb);
+        atomicAdd((unsigned long long *)&tot->payload, (unsigned long long)tp);
+        tot->n_elems = total;
+        tot->bytes = offsets[n];
     }
 }
 
@@ -2113,7 +2206,159 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(ENC_WPE))) v
            })
 }
 
+// ---- small batches: the whole encode in one launch --------------------------------------
+// serObject runs once per evicted key on the main thread (rock.c:691, from the <= 64-pick loop
+// at rock_hotkey.c:347).  A batch of at most SMALL_N values whose output is at most
+// SMALL_BYTES (data_cap) is encoded by ONE workgroup in ONE launch: sizes per value
+// (encode_size, E1's rule and statuses), an in-block scan for the offsets, the capacity cut
+// (E3's), each value written by its lane into a zeroed LDS image (serObject's layout, E4's
+// bytes), the image stored with 16-byte stores (the output may be pinned host memory mapped
+// into the device: rr_encode_batch_host), the totals.  Same offsets, bytes and totals as the
+// pipeline.
+__device__ __forceinline__ void img_le(uint8_t *img, uint64_t p, uint64_t v, uint32_t nb) {
+    for (uint32_t i = 0; i < nb; ++i) img[p + i] = (uint8_t)(v >> (8 * i));
+}
+__device__ __forceinline__ void img_copy(uint8_t *img, uint64_t p, const uint8_t *__restrict__ src, uint64_t len) {
+    for (uint64_t i = 0; i < len; ++i) img[p + i] = src[i];
+}
+// serObject's bytes of one encodable value (rock_serdes.c:512-535) at image offset p
+__device__ void emit_value_small(uint8_t *img, uint64_t p, const uint4 &x, const rr_elem *__restrict__ elems,
+                                 const uint8_t *__restrict__ arena) {
+    const uint32_t type = x.x & 0xFF, enc = (x.x >> 8) & 0xFF, ne = x.z;
+    const rr_elem *el = elems + x.w;
+    img_le(img, p, type | ((uint64_t)(x.y & RR_LRU_MASK) << 8), 5);   // serObjectType + lru
+    p += 5;
+    switch (type) {
+        case RR_TYPE_STRING: {                                         // serString :114-128
+            const ElemV e = get_elem(el);
+            img[p++] = (uint8_t)enc;
+            if (enc == RR_ENC_INT) img_le(img, p, e.data, 8);
+            else img_copy(img, p, arena + e.data, e.len);
+            return;
+        }
+        case RR_TYPE_HASH_ZIPLIST:                                     // serHash :314-331
+        case RR_TYPE_ZSET_ZIPLIST: {                                   // serZset :417-428
+            const ElemV e = get_elem(el);
+            img_le(img, p, e.len, 8);
+            img_copy(img, p + 8, arena + e.data, e.len);
+            return;
+        }
+        case RR_TYPE_LIST_QUICKLIST:                                   // serList :162-188
+            for (uint32_t k = 0; k < ne; ++k) {
+                const ElemV e = get_elem(el + k);
+                if (e.kind == RR_K_INT) {   // sdsll2str
+                    const uint32_t l = dec_write(img + p + 4, (int64_t)e.data);
+                    img_le(img, p, l, 4);
+                    p += 4 + l;
+                } else {
+                    img_le(img, p, e.len, 4);
+                    img_copy(img, p + 4, arena + e.data, e.len);
+                    p += 4 + e.len;
+                }
+            }
+            return;
+        case RR_TYPE_SET_INTSET:                                       // serSet :217-233
+            img_le(img, p, enc | ((uint64_t)ne << 32), 8);
+            p += 8;
+            for (uint32_t k = 0; k < ne; ++k, p += enc) img_le(img, p, get_elem(el + k).data, enc);
+            return;
+        default: {                                                     // HT set / hash :234-245, :332-346; skiplist :429-446
+            img_le(img, p, type == RR_TYPE_SET_HT ? ne : ne / 2, 8);
+            p += 8;
+            for (uint32_t k = 0; k < ne; ++k) {
+                const ElemV e = get_elem(el + k);
+                if (type == RR_TYPE_ZSET_SKIPLIST && (k & 1)) { img_le(img, p, e.data, 8); p += 8; continue; }
+                img_le(img, p, e.len, 8);
+                img_copy(img, p + 8, arena + e.data, e.len);
+                p += 8 + e.len;
+            }
+            return;
+        }
+    }
+}
+
+__global__ __launch_bounds__(SMALL_NT) void encode_small_kernel(const rr_value *__restrict__ values,
+                                                                const rr_elem *__restrict__ elems, uint64_t ecap,
+                                                                const uint8_t *__restrict__ arena, uint64_t acap,
+                                                                uint64_t n, uint8_t *__restrict__ out, uint64_t cap,
+                                                                uint64_t *__restrict__ offsets, rr_totals *tot) {
+    __shared__ __attribute__((aligned(16))) uint8_t img[SMALL_BYTES + 16];
+    __shared__ uint64_t wsum[SMALL_NT / RR_WAVE], red[3][SMALL_NT / RR_WAVE];
+    const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid / RR_WAVE;
+    const uint64_t v0 = (uint64_t)tid * SMALL_VPT;
+    uint4 x[SMALL_VPT];
+    uint64_t sz[SMALL_VPT], pv[SMALL_VPT], sum = 0, bad = 0, pay = 0, nel = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < SMALL_VPT; ++j) {
+        sz[j] = pv[j] = 0;
+        x[j] = make_uint4(0, 0, 0, 0);
+        if (v0 + j < n) {
+            x[j] = reinterpret_cast<const uint4 *>(values)[v0 + j];
+            uint32_t st;
+            sz[j] = encode_size(x[j].x & 0xFF, (x[j].x >> 8) & 0xFF, x[j].x >> 16, x[j].w, x[j].z, elems, ecap, acap, st,
+                                pv[j]);
+            bad += st != RR_OK ? 1u : 0u;
+            nel += x[j].z;
+        }
+        sum += sz[j];
+    }
+    uint64_t total;
+    uint64_t a = block_excl_scan<SMALL_NT>(sum, wsum, total);
+    const uint64_t lim = total < cap ? total : cap;   // (cap <= SMALL_BYTES: rr_small_encode_fits)
+    for (uint32_t k = tid; k < (SMALL_BYTES + 16) / 16; k += SMALL_NT) reinterpret_cast<uint4 *>(img)[k] = make_uint4(0, 0, 0, 0);
+    __syncthreads();
+#pragma unroll 1
+    for (uint32_t j = 0; j < SMALL_VPT; ++j) {
+        if (v0 + j < n) {
+            offsets[v0 + j] = a;
+            const uint64_t b = a + sz[j];
+            if (b > cap && sz[j]) { bad += 1; }                     // past data_cap: not written (E3)
+            else {
+                pay += pv[j];
+                if (sz[j]) emit_value_small(img, a, x[j], elems, arena);
+            }
+            a = b;
+        }
+    }
+    if (tid == 0) offsets[n] = total;
+    bad = wave_sum_fast(bad);
+    pay = wave_sum_fast(pay);
+    nel = wave_sum_fast(nel);
+    if (lane == 0) { red[0][wave] = bad; red[1][wave] = pay; red[2][wave] = nel; }
+    __syncthreads();
+    // the image out: 16-byte stores, bytes at a partial end (as E4)
+    const uint32_t full = (uint32_t)(lim >> 4);
+    for (uint32_t c = tid; c < full; c += SMALL_NT) reinterpret_cast<uint4 *>(out)[c] = reinterpret_cast<const uint4 *>(img)[c];
+    if (tid < (lim & 15)) out[16ull * full + tid] = img[16u * full + tid];
+    if (tid == 0) {
+        uint64_t tb = 0, tp = 0, tn = 0;
+        for (uint32_t w = 0; w < SMALL_NT / RR_WAVE; ++w) { tb += red[0][w]; tp += red[1][w]; tn += red[2][w]; }
+        tot->n_bad = tb;
+        tot->payload = tp;
+        tot->n_elems = tn;
+        tot->bytes = total;
+    }
+}
+
 }  // namespace
+
+extern "C" int rr_small_decode_fits(uint64_t n, uint64_t data_cap) { return n <= SMALL_N && data_cap <= SMALL_BYTES; }
+extern "C" hipError_t rr_launch_decode_small(const uint8_t *blob, const uint64_t *offsets, uint64_t n, rr_value *values,
+                                             rr_elem *elems, uint64_t elem_cap, uint8_t *arena, rr_totals *totals,
+                                             hipStream_t stream) {
+    hipLaunchKernelGGL(decode_small_kernel, dim3(1), dim3(SMALL_NT), 0, stream, blob, offsets, n, values, elems, elem_cap,
+                       arena, totals);
+    return hipGetLastError();
+}
+
+extern "C" int rr_small_encode_fits(uint64_t n, uint64_t data_cap) { return n > 0 && n <= SMALL_N && data_cap <= SMALL_BYTES; }
+extern "C" hipError_t rr_launch_encode_small(const rr_value *values, const rr_elem *elems, uint64_t elem_cap,
+                                             const uint8_t *arena, uint64_t arena_cap, uint64_t n, uint8_t *out,
+                                             uint64_t cap, uint64_t *offsets, rr_totals *totals, hipStream_t stream) {
+    hipLaunchKernelGGL(encode_small_kernel, dim3(1), dim3(SMALL_NT), 0, stream, values, elems, elem_cap, arena, arena_cap,
+                       n, out, cap, offsets, totals);
+    return hipGetLastError();
+}
 
 // ---------------------------------------------------------------------------------------- launch
 #ifndef RR_DEC_W
@@ -2148,7 +2393,21 @@ static uint64_t scan_tiles(uint64_t n) { return (n + SCAN_TILE - 1) / SCAN_TILE;
 
 // windows: sized from data_cap (>= offsets[n], host-known without a sync); windows past
 // offsets[n] own no values and copy nothing
-static uint64_t dec_windows(uint64_t data_cap) { return data_cap / DEC_W + 1; }
+// The window size of a call: the batch cut into whole generations of the resident windows (two
+// per CU), each window as close to DEC_W as that allows — so the last generation is not a
+// partial one that leaves most CUs idle (config 4 at 1M values: 14 generations of 69.4 KiB
+// windows instead of 13.2 of 72 KiB), and a small batch spreads over every CU instead of a
+// few full windows (config 1 at 100K values: 512 windows of 13.7 KiB instead of 98).
+constexpr uint64_t DEC_WMIN = 1024;
+static uint32_t dec_win(uint64_t data_cap) {
+    static uint64_t slots = 0;
+    if (!slots) slots = resident_grid(DECODE_KERNEL, DEC_NW * RR_WAVE, false);
+    const uint64_t per_gen = slots * DEC_W, gens = (data_cap + per_gen - 1) / per_gen;
+    uint64_t w = gens ? (data_cap + gens * slots - 1) / (gens * slots) : DEC_WMIN;
+    w = (w + 15) & ~15ull;
+    return (uint32_t)(w < DEC_WMIN ? DEC_WMIN : w > DEC_W ? DEC_W : w);
+}
+static uint64_t dec_windows(uint64_t data_cap) { return data_cap / dec_win(data_cap) + 1; }
 
 // Decode scratch (uint64 words): [HDR] [window sums, nwin] [group sums, nwin / WGROUP + 1]
 // [reservations u32, n] [first_val u32, nwin + 1] [class bytes, n].  The sums are zeroed by one
@@ -2167,7 +2426,7 @@ extern "C" uint64_t rr_decode_scratch_words(uint64_t data_cap, uint64_t n) {
 extern "C" hipError_t rr_launch_decode(const uint8_t *blob, const uint64_t *offsets, uint64_t n, rr_value *values,
                                        rr_elem *elems, uint64_t elem_cap, uint8_t *arena, uint64_t *scratch,
                                        uint64_t data_cap, rr_totals *totals, hipStream_t stream) {
-    const uint32_t nw = (uint32_t)dec_windows(data_cap);
+    const uint32_t win = dec_win(data_cap), nw = (uint32_t)(data_cap / win + 1);
     uint64_t *wtot = scratch + RR_SCRATCH_HDR;
     uint64_t *gtot = wtot + nw;
     uint32_t *counts = reinterpret_cast<uint32_t *>(gtot + dec_groups(nw));
@@ -2176,9 +2435,9 @@ extern "C" hipError_t rr_launch_decode(const uint8_t *blob, const uint64_t *offs
     const hipError_t e = hipMemsetAsync(wtot, 0, (nw + dec_groups(nw)) * sizeof(uint64_t), stream);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(count_kernel, dim3((uint32_t)((n + 1 + 255) / 256)), dim3(256), 0, stream, blob, offsets, n,
-                       first_val, nw, DEC_W, counts, cls, wtot, gtot, nullptr, 0u, totals);
+                       first_val, nw, win, counts, cls, wtot, gtot, nullptr, 0u, totals);
     hipLaunchKernelGGL((DECODE_KERNEL), dim3(nw), dim3(DEC_NW * RR_WAVE), 0, stream, blob, data_cap, offsets, n,
-                       first_val, cls, counts, wtot, gtot, values, elems, elem_cap, arena, nw, totals);
+                       first_val, cls, counts, wtot, gtot, values, elems, elem_cap, arena, nw, win, totals);
     return hipGetLastError();
 }
 

@@ -27,6 +27,20 @@ def built_libs():
 
 @pytest.fixture(scope="session")
 def engine():
+    """The batch pipeline (count + decode windows, the four encode kernels) for every batch size:
+    RR_CTX_NO_SMALL, so small test batches still exercise the walks.  The one-launch kernels
+    small batches take by default are tested through `engine_small` (tests/test_gpu_small.py)."""
+    import redrock_old_amd as rr
+    eng = rr.Engine(0)
+    eng.set_options(rr.CTX_NO_SMALL)
+    yield eng
+    eng.close()
+
+
+@pytest.fixture(scope="session")
+def engine_small():
+    """A context with the default options: batches of at most 4096 values in at most 128 KiB
+    take the one-launch kernels."""
     import redrock_old_amd as rr
     eng = rr.Engine(0)
     yield eng

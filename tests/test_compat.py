@@ -148,13 +148,49 @@ def test_rdb_flat_restore_on_gpu(tmp_path):
     assert "0 failures" in r.stdout
 
 
-if __name__ == "__main__":   # python tests/test_compat.py bench [config k]  (GPU box): keys/s of the restore paths
+def build_latency(tmp):
+    """tests/c/bench_latency.c: per-call latency of desObject / serObject through the shim, the
+    batch C-ABI with one value per call (one-launch kernels / pipeline), and the faithful CPU
+    restatement (the oracle: test infrastructure, linked only into this bench)."""
+    exe = os.path.join(tmp, "bench_latency")
+    oracle = os.path.join(ROOT, "oracle")
+    cmd = ["gcc", "-std=gnu11", "-O2", "-Wall", "-Werror", "-Wno-unused-function", "-DRR_REDIS_TREE", "-pthread",
+           "-I", os.path.join(ROOT, "tests", "c", "miniredis"), "-I", os.path.join(ROOT, "include"), "-I", oracle,
+           os.path.join(ROOT, "redrock_old_amd", "compat", "rock_serdes_compat.c"),
+           os.path.join(ROOT, "tests", "c", "miniredis", "miniredis.c"),
+           os.path.join(ROOT, "tests", "c", "bench_latency.c"),
+           "-L", os.path.join(ROOT, "redrock_old_amd"), "-lrr_serdes", "-Wl,-rpath," + os.path.join(ROOT, "redrock_old_amd"),
+           "-L", oracle, "-lrr_oracle", "-Wl,-rpath," + oracle, "-lm", "-o", exe]
+    subprocess.run(cmd, check=True)
+    return exe
+
+
+def test_latency_bench_builds(tmp_path):
+    assert os.path.exists(build_latency(str(tmp_path)))
+
+
+@pytest.mark.gpu
+def test_per_value_latency_path(tmp_path):
+    """The unchanged per-value callers' path: every desObject / serObject of 300 config-4
+    values goes through the one-launch kernels and round-trips (the bench checks every blob)."""
+    r = subprocess.run([build_latency(str(tmp_path)), "4", "300"], capture_output=True, text=True, timeout=120)
+    print(r.stdout, r.stderr)
+    assert r.returncode == 0, r.stdout + r.stderr
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["roundtrip_bad"] == 0
+
+
+if __name__ == "__main__":   # python tests/test_compat.py bench [config k] | latency [config k]  (GPU box)
     import sys
     import tempfile
-    if sys.argv[1:2] == ["bench"]:
+    if sys.argv[1:2] == ["bench"]:   # keys/s of the restore paths
         with tempfile.TemporaryDirectory() as d:
             r = subprocess.run([build_rdb(d, bench=True), "bench"] + sys.argv[2:4], capture_output=True, text=True,
                                timeout=600)
+            print(r.stdout, r.stderr)
+    if sys.argv[1:2] == ["latency"]:   # per-call latency of the one-value signatures
+        with tempfile.TemporaryDirectory() as d:
+            r = subprocess.run([build_latency(d)] + sys.argv[2:4], capture_output=True, text=True, timeout=600)
             print(r.stdout, r.stderr)
 
 

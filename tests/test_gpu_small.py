@@ -1,0 +1,187 @@
+"""The one-launch small-batch kernels (decode_small_kernel / encode_small_kernel in
+rr_kernels.hip): the route of the unchanged per-value callers — desObject per restored key
+(rock.c:468), serObject per evicted key (rock.c:691, rock_hotkey.c:347).  Every case runs
+through the C-ABI on `engine_small` (default options) and is checked bit for bit against the
+CPU oracle, the golden vectors, and the batch pipeline (`engine`, RR_CTX_NO_SMALL) on the same
+inputs: records, descriptors, arena, totals, encoded bytes and offsets."""
+import struct
+
+import numpy as np
+import pytest
+
+import redrock_old_amd as rr
+from oracle import cpu
+
+from helpers import assert_flat_equal, batch_from_blobs, expected_flat, golden
+
+pytestmark = pytest.mark.gpu
+
+
+def _blobs(cfg, n, seed=None):
+    data, offs = rr.gen_batch(cfg, n, seed)
+    return [bytes(data[offs[i]:offs[i + 1]]) for i in range(n)]
+
+
+def _fits(blobs):
+    return len(blobs) <= rr.SMALL_N and ((sum(len(b) for b in blobs) + 15) & ~15) <= rr.SMALL_BYTES
+
+
+def _check(engine_small, engine, blobs, what, reencode=True):
+    """decode (host path) on the one-launch kernel == oracle == pipeline; encode back."""
+    assert _fits(blobs), what
+    data, offs = batch_from_blobs(blobs)
+    v, e, a, t = engine_small.decode_host(data, offs)
+    ov, oe, oa, ot = cpu.decode(data, offs)
+    assert_flat_equal((v, e), (ov, oe), what)
+    assert t == ot, (what, t, ot)
+    assert np.array_equal(a, oa[:len(a)]), what
+    pv, pe, pa, pt = engine.decode_host(data, offs)
+    assert_flat_equal((v, e), (pv, pe), what + " vs pipeline")
+    assert t == pt
+    if reencode:   # (an output capacity within the one-launch limit)
+        out, ooffs, t2 = engine_small.encode_host(v, e, a, data_cap=int(offs[-1]) + 16)
+        xo, xoffs, xt = cpu.encode(ov, oe, oa)
+        assert t2 == xt and np.array_equal(ooffs, xoffs) and np.array_equal(out, xo), what
+    return v, e, a, t
+
+
+@pytest.mark.parametrize("cfg", [1, 2, 3, 4, 10])
+def test_single_values(engine_small, engine, cfg):
+    """n = 1: every value of a batch decoded and encoded on its own (the per-key calls)."""
+    for i, b in enumerate(_blobs(cfg, 40 if cfg != 10 else 48, seed=70 + cfg)):
+        if not _fits([b]):
+            continue
+        v, e, a, t = _check(engine_small, engine, [b], f"cfg {cfg} value {i}")
+        if cfg != 10:   # (serObject output: it re-encodes to itself)
+            out, ooffs, _ = engine_small.encode_host(v, e, a, data_cap=len(b) + 16)
+            assert out.tobytes() == b
+
+
+@pytest.mark.parametrize("cfg", [2, 3, 4, 10])
+def test_63_values(engine_small, engine, cfg):
+    blobs = [b for b in _blobs(cfg, 400, seed=63 + cfg)]
+    batch, total = [], 0
+    for b in blobs:   # the first 63 that fit the one-launch limits together
+        if len(batch) == 63:
+            break
+        if total + len(b) + 16 <= rr.SMALL_BYTES:
+            batch.append(b)
+            total += len(b)
+    assert len(batch) == 63
+    _check(engine_small, engine, batch, f"cfg {cfg} n 63")
+
+
+def test_4096_small_values(engine_small, engine):
+    """n = 4096 (the one-launch limit): the config-4 values of at most 30 bytes (INT and
+    EMBSTR strings, small intsets / lists / ziplists)."""
+    data, offs = rr.gen_batch(4, 40000, seed=4096)
+    blobs = [bytes(data[offs[i]:offs[i + 1]]) for i in range(40000) if offs[i + 1] - offs[i] <= 30][:4096]
+    assert len(blobs) == 4096
+    _check(engine_small, engine, blobs, "n 4096")
+
+
+def test_golden_vectors(engine_small, engine):
+    """The K1-K9 known answers and the edge fixtures (malformed ones included), in batches that
+    fit: records against the hand-derived golden flat forms."""
+    G = golden()
+    fx = [f for f in G["kats"] + G["edges"] if len(bytes.fromhex(f["blob"])) < rr.SMALL_BYTES // 2]
+    i = 0
+    while i < len(fx):
+        part, total = [], 0
+        while i < len(fx) and total + len(bytes.fromhex(fx[i]["blob"])) + 16 <= rr.SMALL_BYTES:
+            part.append(fx[i])
+            total += len(bytes.fromhex(fx[i]["blob"]))
+            i += 1
+        blobs = [bytes.fromhex(f["blob"]) for f in part]
+        data, offs = batch_from_blobs(blobs)
+        v, e, a, t = engine_small.decode_host(data, offs)
+        assert_flat_equal((v, e), expected_flat(part), "golden")
+        _check(engine_small, engine, blobs, "golden vs oracle", reencode=False)
+
+
+def test_fuzzed_blobs(engine_small, engine):
+    """Byte flips and truncations of edge-case values: statuses and descriptors match."""
+    rng = np.random.default_rng(11)
+    src = [b for b in _blobs(10, 240) if len(b) < 2000]
+    blobs = []
+    for b in src:
+        m = bytearray(b)
+        r = rng.integers(0, 3)
+        if r == 0 and len(m):
+            m[rng.integers(0, len(m))] ^= 1 << int(rng.integers(0, 8))
+        elif r == 1 and len(m):
+            m = m[:int(rng.integers(0, len(m)))]
+        blobs.append(bytes(m))
+        if sum(len(x) for x in blobs) > rr.SMALL_BYTES - 4096:
+            break
+    _check(engine_small, engine, blobs, "fuzz", reencode=False)
+
+
+def _sl(pairs):
+    body = b"".join(struct.pack("<Q", len(m)) + m + struct.pack("<d", s) for m, s in pairs)
+    return bytes([5]) + struct.pack("<I", 7) + struct.pack("<Q", len(pairs)) + body
+
+
+def _ht(members, hash_=False):
+    body = b"".join(struct.pack("<Q", len(m)) + m for m in members)
+    return bytes([4 if hash_ else 2]) + struct.pack("<I", 3) + struct.pack("<Q", len(members) // (2 if hash_ else 1)) + body
+
+
+def test_fixups_in_one_launch(engine_small, engine):
+    """The marked values — a set with repeated members (first copy kept), a hash with a repeated
+    field (RR_E_DUP), an unsorted skiplist (re-sorted), a NaN score (RR_E_NAN), a set of more
+    than 16 keys — fixed inside the one-launch kernel."""
+    blobs = [_ht([b"a", b"b", b"a", b"c", b"b"]), _ht([b"f", b"1", b"g", b"2", b"f", b"3"], hash_=True),
+             _sl([(b"x", 1.0), (b"y", 3.0), (b"z", 2.0)]), _sl([(b"x", 3.0), (b"y", float("nan"))]),
+             _ht([b"m%d" % k for k in range(40)] + [b"m7"])]
+    blobs += _blobs(4, 30, seed=9)
+    v, e, a, t = _check(engine_small, engine, blobs, "fixups", reencode=False)
+    assert list(v["status"][:4]) == [0, 13, 0, 14]
+
+
+def test_device_entry_points(engine_small, engine):
+    """rr_decode_batch / rr_encode_batch with device buffers within the limits (data_cap <=
+    128 KiB): the one-launch kernels, equal to the pipeline's device calls."""
+    import torch
+    dev = torch.device("cuda:0")
+    blobs = _blobs(4, 200, seed=3)[:100]
+    data, offs = batch_from_blobs(blobs)
+    n, nb = len(offs) - 1, int(offs[-1])
+    cap = rr.elem_bound(n, nb)
+    res = []
+    for eng in (engine_small, engine):
+        d_data = torch.from_numpy(data).to(dev)
+        d_offs = torch.from_numpy(offs.view(np.int64)).to(dev)
+        d_vals = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
+        d_elems = torch.zeros(cap * 16, dtype=torch.uint8, device=dev)
+        d_arena = torch.zeros(len(data), dtype=torch.uint8, device=dev)
+        d_tot = torch.full((4,), -1, dtype=torch.int64, device=dev)
+        eng.decode_device(d_data, d_offs, d_vals, d_elems, d_arena, d_tot)
+        d_out = torch.zeros(len(data), dtype=torch.uint8, device=dev)
+        d_oo = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+        d_t2 = torch.full((4,), -1, dtype=torch.int64, device=dev)
+        eng.encode_device(d_vals, d_elems, d_arena, d_out, d_oo, d_t2)
+        torch.cuda.synchronize()
+        res.append([x.cpu().numpy() for x in (d_vals, d_elems, d_arena, d_tot, d_out, d_oo, d_t2)])
+    for x, y in zip(res[0], res[1]):
+        assert np.array_equal(x, y)
+    assert res[0][4][:nb].tobytes() == data[:nb].tobytes()
+
+
+def test_capacity_cuts(engine_small, engine):
+    """elem_cap below the descriptors (RR_E_CAPACITY from the cut on) and data_cap below the
+    encoded bytes (values past it not written, their bytes zero): as the pipeline."""
+    blobs = _blobs(4, 120, seed=12)
+    data, offs = batch_from_blobs(blobs)
+    _, oe, _, _ = cpu.decode(data, offs)
+    cap = len(oe) // 2
+    a1 = engine_small.decode_host(data, offs, elem_cap=cap)
+    a2 = engine.decode_host(data, offs, elem_cap=cap)
+    assert_flat_equal(a1[:2], a2[:2], "elem_cap cut")
+    assert a1[3] == a2[3] and a1[3]["n_bad"] > 0
+    v, e, a, _ = engine.decode_host(data, offs)
+    dcap = int(offs[60]) + 7
+    o1 = engine_small.encode_host(v, e, a, data_cap=dcap)
+    o2 = engine.encode_host(v, e, a, data_cap=dcap)
+    assert np.array_equal(o1[1], o2[1]) and o1[2] == o2[2] and o1[2]["n_bad"] > 0
+    assert o1[0].tobytes()[:dcap] == o2[0].tobytes()[:dcap]
