@@ -67,9 +67,14 @@ void rr_ctx_destroy(rr_ctx *c) {
     if (c->d_totals) hipFree(c->d_totals);
     if (c->h_small) hipHostFree(c->h_small);
     if (c->pipe_ready) {
-        for (int k = 0; k < RR_HOST_MAXCHUNK; k++) { hipEventDestroy(c->ev_up[k]); hipEventDestroy(c->ev_dec[k]); }
+        for (int k = 0; k < RR_HOST_MAXCHUNK; k++) {
+            hipEventDestroy(c->ev_up[k]); hipEventDestroy(c->ev_dec[k]);
+            hipEventDestroy(c->ev_arena[k]); hipEventDestroy(c->ev_enc[k]); hipEventDestroy(c->ev_need[k]);
+        }
         hipStreamDestroy(c->up);
         hipStreamDestroy(c->down);
+        hipStreamDestroy(c->aux);
+        hipHostFree(c->h_need);
         hipFree(c->d_ktot);
         hipHostFree(c->h_ktot);
     }
@@ -212,10 +217,15 @@ static int pipe_init(rr_ctx *c) {
     if (c->pipe_ready) return RR_API_OK;
     HIPCHK(hipStreamCreateWithFlags(&c->up, hipStreamNonBlocking));
     HIPCHK(hipStreamCreateWithFlags(&c->down, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
     for (int k = 0; k < RR_HOST_MAXCHUNK; k++) {
         HIPCHK(hipEventCreateWithFlags(&c->ev_up[k], hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&c->ev_dec[k], hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&c->ev_arena[k], hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&c->ev_enc[k], hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&c->ev_need[k], hipEventDisableTiming));
     }
+    HIPCHK(hipHostMalloc((void **)&c->h_need, RR_HOST_MAXCHUNK * RR_NEED_BLOCKS * sizeof(uint64_t), hipHostMallocMapped));
     HIPCHK(hipMalloc((void **)&c->d_ktot, RR_HOST_MAXCHUNK * sizeof(rr_totals)));
     HIPCHK(hipHostMalloc((void **)&c->h_ktot, RR_HOST_MAXCHUNK * sizeof(rr_totals), hipHostMallocDefault));
     c->pipe_ready = 1;
@@ -430,6 +440,132 @@ static int encode_host_small(rr_ctx *c, const rr_value *values, const rr_elem *e
     return RR_API_OK;
 }
 
+/* ---- pipelined host encode -------------------------------------------------------------
+ * A batch whose records + descriptors + arena pass RR_HOST_CHUNK goes in chunks of whole values
+ * (balanced by descriptors; at most RR_HOST_MAXCHUNK).  Everything goes up on the `up` stream,
+ * queued at once: the records, then per chunk the descriptors its values reach (from their
+ * records: a growing prefix) and one slice of the arena.  Chunk k's encode runs on the context
+ * stream once its descriptors are in and the arena prefix its payloads reach (arena_need_kernel,
+ * on the `aux` stream as soon as those descriptors land) has been uploaded; it writes its blobs
+ * into its own 16-byte aligned region of the output staging, its offsets are rebased past the
+ * earlier chunks' bytes on the device, and its blobs and offsets go down on the `down` stream
+ * while later chunks are still going up.  Every chunk's encode is the whole call's restricted to
+ * its values (full descriptor and arena capacities, the output capacity left after the earlier
+ * chunks): results are identical to one call. */
+#define RR_NEED_MAXK RR_HOST_MAXCHUNK
+static int encode_host_pipelined_run(rr_ctx *c, const rr_value *values, const rr_elem *elems, uint64_t n_elems,
+                                     const uint8_t *arena, uint64_t arena_bytes, uint64_t n, uint8_t *data,
+                                     uint64_t data_cap, uint64_t *offsets, rr_totals *totals, const uint64_t *cut,
+                                     const uint64_t *eneed, int K) {
+    rr_value *d_vals = (rr_value *)c->d_vals;
+    rr_elem *d_elems = (rr_elem *)c->d_elems;
+    uint8_t *d_arena = (uint8_t *)c->d_arena, *d_out = (uint8_t *)c->d_out;
+    uint64_t *d_ooff = (uint64_t *)c->d_ooff;
+    /* the previous host call on this context is done with the staging buffers */
+    HIPCHK(hipEventRecord(c->ev_dec[0], c->stream));
+    HIPCHK(hipStreamWaitEvent(c->up, c->ev_dec[0], 0));
+    if (n) HIPCHK(hipMemcpyAsync(d_vals, values, n * sizeof(rr_value), hipMemcpyHostToDevice, c->up));
+    uint64_t e_done = 0;
+    for (int k = 0; k < K; k++) {
+        if (eneed[k] > e_done) {
+            HIPCHK(hipMemcpyAsync(d_elems + e_done, elems + e_done, (eneed[k] - e_done) * sizeof(rr_elem),
+                                  hipMemcpyHostToDevice, c->up));
+            e_done = eneed[k];
+        }
+        HIPCHK(hipEventRecord(c->ev_up[k], c->up));
+        const uint64_t a0 = arena_bytes * (uint64_t)k / K, a1 = arena_bytes * (uint64_t)(k + 1) / K;
+        if (a1 > a0) HIPCHK(hipMemcpyAsync(d_arena + a0, arena + a0, a1 - a0, hipMemcpyHostToDevice, c->up));
+        HIPCHK(hipEventRecord(c->ev_arena[k], c->up));
+        /* which arena bytes the chunk reads: as soon as its descriptors are in */
+        HIPCHK(hipStreamWaitEvent(c->aux, c->ev_up[k], 0));
+        HIPCHK(rr_launch_arena_need(d_vals + cut[k], cut[k + 1] - cut[k], d_elems, n_elems, arena_bytes,
+                                    (uint64_t *)c->h_need + (size_t)k * RR_NEED_BLOCKS, c->aux));
+        HIPCHK(hipEventRecord(c->ev_need[k], c->aux));
+    }
+    rr_totals sum = {0, 0, 0, 0};
+    uint64_t base = 0, region = 0;   /* output bytes of the earlier chunks; their staging space */
+    for (int k = 0; k < K; k++) {
+        const uint64_t v0 = cut[k], nk = cut[k + 1] - v0;
+        HIPCHK(hipEventSynchronize(c->ev_need[k]));
+        uint64_t need = 0;
+        for (int b = 0; b < RR_NEED_BLOCKS; b++) {
+            const uint64_t x = c->h_need[(size_t)k * RR_NEED_BLOCKS + b];
+            need = x > need ? x : need;
+        }
+        int j = -1;   /* the last arena slice the chunk reads */
+        for (int s = 0; s < K && need; s++)
+            if (arena_bytes * (uint64_t)s / K < need) j = s;
+        HIPCHK(hipStreamWaitEvent(c->stream, c->ev_up[k], 0));
+        if (j >= 0) HIPCHK(hipStreamWaitEvent(c->stream, c->ev_arena[j], 0));
+        const uint64_t cap = data_cap > base ? data_cap - base : 0;
+        rr_flat_batch in = {d_vals + v0, d_elems, d_arena, nk, n_elems, arena_bytes};
+        rr_blob_batch out = {d_out + region, d_ooff + v0, nk, cap};
+        int rc = rr_encode_batch(c, &in, &out, c->d_ktot + k, c->stream);
+        if (rc) return rc;
+        HIPCHK(rr_launch_offsets_rebase(d_ooff + v0, nk + 1, 0ull - base, c->stream));
+        HIPCHK(hipMemcpyAsync(&c->h_ktot[k], c->d_ktot + k, sizeof(rr_totals), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipEventRecord(c->ev_enc[k], c->stream));
+        HIPCHK(hipEventSynchronize(c->ev_enc[k]));   /* (later chunks keep going up meanwhile) */
+        const rr_totals t = c->h_ktot[k];
+        if (t.bytes == ~0ull) return fail(RR_API_EDEVICE, "encode: device-side failure (look-back timeout)");
+        HIPCHK(hipStreamWaitEvent(c->down, c->ev_enc[k], 0));
+        HIPCHK(hipMemcpyAsync(offsets + v0, d_ooff + v0, (nk + (k == K - 1)) * sizeof(uint64_t), hipMemcpyDeviceToHost,
+                              c->down));
+        const uint64_t nb = t.bytes < cap ? t.bytes : cap;
+        if (nb) HIPCHK(hipMemcpyAsync(data + base, d_out + region, nb, hipMemcpyDeviceToHost, c->down));
+        base += t.bytes;
+        region += (nb + 15) & ~15ull;
+        sum.n_elems += t.n_elems;
+        sum.n_bad += t.n_bad;
+        sum.payload += t.payload;
+    }
+    HIPCHK(hipStreamSynchronize(c->down));
+    sum.bytes = base;
+    if (totals) *totals = sum;
+    return RR_API_OK;
+}
+
+/* Cuts by descriptors (the encode's work) and, per chunk, the descriptor prefix its values
+ * reach (the valid ones: status RR_OK, descriptors inside n_elems — what the encode reads).  The
+ * staging output needs room for every chunk's 16-byte aligned region. */
+static int encode_host_pipelined(rr_ctx *c, const rr_value *values, const rr_elem *elems, uint64_t n_elems,
+                                 const uint8_t *arena, uint64_t arena_bytes, uint64_t n, uint8_t *data,
+                                 uint64_t data_cap, uint64_t *offsets, rr_totals *totals) {
+    int rc = pipe_init(c);
+    if (rc) return rc;
+    uint64_t cut[RR_HOST_MAXCHUNK + 1], eneed[RR_HOST_MAXCHUNK];
+    const uint64_t in_bytes = n * sizeof(rr_value) + n_elems * sizeof(rr_elem) + arena_bytes;
+    uint64_t K = (in_bytes + RR_HOST_CHUNK - 1) / RR_HOST_CHUNK;
+    if (K > RR_HOST_MAXCHUNK) K = RR_HOST_MAXCHUNK;
+    if (K > n) K = n;
+    uint64_t tot = 0;
+    for (uint64_t v = 0; v < n; v++) tot += values[v].n_elems + 1;   /* (+1: every value costs) */
+    int m = 0;
+    uint64_t acc = 0, emax = 0;
+    cut[0] = 0;
+    for (uint64_t v = 0; v < n; v++) {
+        const uint64_t eb = values[v].elem_base, ne = values[v].n_elems;
+        if (values[v].status == RR_OK && eb + ne <= n_elems && eb + ne > emax) emax = eb + ne;
+        acc += ne + 1;
+        if (m + 1 < (int)K && acc >= tot / K * (uint64_t)(m + 1) && v + 1 < n) {
+            eneed[m] = emax;
+            cut[++m] = v + 1;
+        }
+    }
+    eneed[m] = emax;
+    cut[++m] = n;
+    GROW(c->d_out, c->c_out, data_cap + 16 * (size_t)m + 16);
+    rc = encode_host_pipelined_run(c, values, elems, n_elems, arena, arena_bytes, n, data, data_cap, offsets, totals,
+                                   cut, eneed, m);
+    if (rc != RR_API_OK) {   /* transfers in flight must not outlive the call */
+        (void)hipStreamSynchronize(c->up);
+        (void)hipStreamSynchronize(c->aux);
+        (void)hipStreamSynchronize(c->down);
+        (void)hipStreamSynchronize(c->stream);
+    }
+    return rc;
+}
+
 int rr_encode_batch_host(rr_ctx *c, const rr_value *values, const rr_elem *elems, uint64_t n_elems,
                          const uint8_t *arena, uint64_t arena_bytes, uint64_t n, uint8_t *data, uint64_t data_cap,
                          uint64_t *offsets, rr_totals *totals) {
@@ -442,6 +578,8 @@ int rr_encode_batch_host(rr_ctx *c, const rr_value *values, const rr_elem *elems
     GROW(c->d_arena, c->c_arena, arena_bytes + 16);
     GROW(c->d_out, c->c_out, data_cap + 16);
     GROW(c->d_ooff, c->c_ooff, (n + 1) * sizeof(uint64_t));
+    if (n > 1 && n * sizeof(rr_value) + n_elems * sizeof(rr_elem) + arena_bytes > RR_HOST_CHUNK)
+        return encode_host_pipelined(c, values, elems, n_elems, arena, arena_bytes, n, data, data_cap, offsets, totals);
     if (n) HIPCHK(hipMemcpyAsync(c->d_vals, values, n * sizeof(rr_value), hipMemcpyHostToDevice, c->stream));
     if (n_elems) HIPCHK(hipMemcpyAsync(c->d_elems, elems, n_elems * sizeof(rr_elem), hipMemcpyHostToDevice, c->stream));
     if (arena_bytes) HIPCHK(hipMemcpyAsync(c->d_arena, arena, arena_bytes, hipMemcpyHostToDevice, c->stream));

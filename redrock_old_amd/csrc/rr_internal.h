@@ -21,9 +21,11 @@ struct rr_ctx {
     rr_totals *d_totals;
     /* pipelined host decode (rr_api.c): transfer streams, per-chunk events and totals */
     int pipe_ready;
-    hipStream_t up, down;
+    hipStream_t up, down, aux;
     hipEvent_t ev_up[RR_HOST_MAXCHUNK], ev_dec[RR_HOST_MAXCHUNK];
     rr_totals *d_ktot, *h_ktot;   /* device / pinned host, RR_HOST_MAXCHUNK each */
+    uint64_t *h_need;             /* pinned, mapped: per chunk, the arena bytes its encode reads */
+    hipEvent_t ev_arena[RR_HOST_MAXCHUNK], ev_enc[RR_HOST_MAXCHUNK], ev_need[RR_HOST_MAXCHUNK];
     /* small batches through the host entry points: one pinned buffer mapped into the device,
      * which the one-launch kernels read their input from and write their output to */
     uint8_t *h_small, *d_small;

@@ -38,6 +38,11 @@ hipError_t rr_launch_flat_rebase(rr_value *values, uint64_t n, rr_elem *elems, u
                                  uint64_t byte_add, hipStream_t stream);
 uint64_t rr_encode_scratch_words(uint64_t n, uint64_t data_cap);
 hipError_t rr_launch_copy(uint8_t *dst, const uint8_t *src, uint64_t bytes, hipStream_t stream);
+/* the pipelined host encode: the end of the arena bytes the valid values [0, n) read, as
+ * RR_NEED_BLOCKS partial maxima into mapped host words */
+#define RR_NEED_BLOCKS 32
+hipError_t rr_launch_arena_need(const rr_value *values, uint64_t n, const rr_elem *elems, uint64_t elem_cap,
+                                uint64_t arena_cap, uint64_t *need, hipStream_t stream);
 /* small batches (one workgroup, one launch): whether a batch qualifies, and the launches */
 int rr_small_decode_fits(uint64_t n, uint64_t data_cap);
 int rr_small_encode_fits(uint64_t n, uint64_t data_cap);

@@ -2351,6 +2351,47 @@ extern "C" hipError_t rr_launch_decode_small(const uint8_t *blob, const uint64_t
     return hipGetLastError();
 }
 
+// ---- the pipelined host encode: which arena bytes a chunk of values reads ----------------
+// The largest end (data + len) of the STR / ZLRAW descriptors of the values the encode will read
+// (status RR_OK, descriptors inside elem_cap: encode_size's conditions), clamped to arena_cap:
+// each of NEED_BLOCKS workgroups stores its part's maximum into a word of mapped host memory,
+// and the host lets the chunk's encode start once that much of the arena has been uploaded.
+__global__ __launch_bounds__(1024) void arena_need_kernel(const rr_value *__restrict__ values, uint64_t n,
+                                                          const rr_elem *__restrict__ elems, uint64_t ecap,
+                                                          uint64_t acap, uint64_t *need) {
+    __shared__ uint64_t wm[16];
+    uint64_t m = 0;
+    for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (uint64_t)gridDim.x * blockDim.x) {
+        const uint4 x = reinterpret_cast<const uint4 *>(values)[v];
+        const uint64_t eb = x.w, ne = x.z;
+        if ((x.x >> 16) != RR_OK || eb + ne > ecap) continue;
+        for (uint64_t k = 0; k < ne; ++k) {
+            const uint4 d = reinterpret_cast<const uint4 *>(elems + eb)[k];
+            const uint32_t kind = d.w & 0xFF;
+            if (kind == RR_K_STR || kind == RR_K_ZLRAW) {
+                const uint64_t end = ((uint64_t)d.x | ((uint64_t)d.y << 32)) + d.z;
+                m = end > m ? end : m;
+            }
+        }
+    }
+    for (int o = RR_WAVE / 2; o > 0; o >>= 1) {
+        const uint64_t y = __shfl_xor(m, o, RR_WAVE);
+        m = y > m ? y : m;
+    }
+    if (lane_id() == 0) wm[threadIdx.x / RR_WAVE] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (uint32_t w = 0; w < blockDim.x / RR_WAVE; ++w) m = wm[w] > m ? wm[w] : m;
+        need[blockIdx.x] = m < acap ? m : acap;
+    }
+}
+extern "C" hipError_t rr_launch_arena_need(const rr_value *values, uint64_t n, const rr_elem *elems, uint64_t elem_cap,
+                                           uint64_t arena_cap, uint64_t *need, hipStream_t stream) {
+    hipLaunchKernelGGL(arena_need_kernel, dim3(RR_NEED_BLOCKS), dim3(1024), 0, stream, values, n, elems, elem_cap, arena_cap,
+                       need);
+    return hipGetLastError();
+}
+
 extern "C" int rr_small_encode_fits(uint64_t n, uint64_t data_cap) { return n > 0 && n <= SMALL_N && data_cap <= SMALL_BYTES; }
 extern "C" hipError_t rr_launch_encode_small(const rr_value *values, const rr_elem *elems, uint64_t elem_cap,
                                              const uint8_t *arena, uint64_t arena_cap, uint64_t n, uint8_t *out,

@@ -194,3 +194,43 @@ def test_windows_with_more_runs_than_the_run_queue(engine):
     a2 = np.concatenate([np.zeros(1, np.uint8), a, np.zeros(16, np.uint8)])
     out2, ooffs2, t3 = _check_against_oracle(engine, v, e2, a2)
     assert np.array_equal(out2, data[:int(offs[-1])])
+
+
+def _reversed_layout(v, e, a):
+    """The same flat batch with the descriptor ranges and the payloads laid out in reverse value
+    order: the first values' payloads sit at the arena's end."""
+    n = len(v)
+    e2 = np.zeros_like(e)
+    v2 = v.copy()
+    arena2 = bytearray()
+    pos = 0
+    for i in range(n - 1, -1, -1):
+        b, c = int(v["elem_base"][i]), int(v["n_elems"][i])
+        seg = e[b:b + c].copy()
+        for k in range(c):
+            if seg["kind"][k] in (rr.K_STR, rr.K_ZLRAW):
+                src, ln = int(e["data"][b + k]), int(seg["len"][k])
+                seg["data"][k] = len(arena2)
+                arena2 += a[src:src + ln].tobytes()
+        e2[pos:pos + c] = seg
+        v2["elem_base"][i] = pos
+        pos += c
+    return v2, e2, np.frombuffer(bytes(arena2) + bytes(16), np.uint8)
+
+
+@pytest.mark.parametrize("layout", ["mirror", "reversed"])
+def test_host_encode_pipelined_matches_one_call(engine, layout):
+    """rr_encode_batch_host on inputs past 16 MiB runs in chunks (uploads, encodes and downloads
+    overlapped; each chunk waits for the arena prefix its payloads reach): bytes, offsets and
+    totals equal the oracle's one-call encode — with the decoder's mirror arena, with a layout
+    whose first values' payloads are uploaded last, and with data_caps that cut a value."""
+    data, offs = rr.gen_batch(4, 60000, seed=61)
+    v, e, a, t = engine.decode_host(data, offs)
+    if layout == "reversed":
+        v, e, a = _reversed_layout(v, e, a)
+    assert len(v) * 16 + len(e) * 16 + len(a) > 16 << 20   # the chunked path
+    nb = int(offs[-1])
+    out, ooffs, t2 = _check_against_oracle(engine, v, e, a)
+    assert np.array_equal(out, data[:nb]) and t2["bytes"] == nb
+    for cap in (int(offs[30000]) + 5, int(offs[59000]), nb // 7):
+        _check_against_oracle(engine, v, e, a, data_cap=cap)
