@@ -182,6 +182,14 @@ int rr_encode_batch(rr_ctx *c, const rr_flat_batch *in, rr_blob_batch *out, rr_t
     return mark_scratch(c, (hipStream_t)stream);
 }
 
+/* diagnostics (tools/time_copy.py; not in rr_serdes.h): one of the copy kernel's shapes */
+int rr_copy_shape(rr_ctx *c, void *dst, const void *src, uint64_t bytes, int shape, void *stream) {
+    if (!c || (bytes && (!dst || !src)) || (((uintptr_t)dst | (uintptr_t)src) & 15)) return fail(RR_API_EINVAL, "rr_copy_shape");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(rr_launch_copy_shape((uint8_t *)dst, (const uint8_t *)src, bytes, shape, (hipStream_t)stream));
+    return RR_API_OK;
+}
+
 int rr_copy_device(rr_ctx *c, void *dst, const void *src, uint64_t bytes, void *stream) {
     if (!c || (bytes && (!dst || !src))) return fail(RR_API_EINVAL, "NULL argument");
     if (((uintptr_t)dst | (uintptr_t)src) & 15) return fail(RR_API_EINVAL, "rr_copy_device: pointers must be 16-byte aligned");

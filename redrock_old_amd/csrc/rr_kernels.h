@@ -38,6 +38,7 @@ hipError_t rr_launch_flat_rebase(rr_value *values, uint64_t n, rr_elem *elems, u
                                  uint64_t byte_add, hipStream_t stream);
 uint64_t rr_encode_scratch_words(uint64_t n, uint64_t data_cap);
 hipError_t rr_launch_copy(uint8_t *dst, const uint8_t *src, uint64_t bytes, hipStream_t stream);
+hipError_t rr_launch_copy_shape(uint8_t *dst, const uint8_t *src, uint64_t bytes, int shape, hipStream_t stream);
 /* the pipelined host encode: the end of the arena bytes the valid values [0, n) read, as
  * RR_NEED_BLOCKS partial maxima into mapped host words */
 #define RR_NEED_BLOCKS 32

@@ -1483,18 +1483,20 @@ __device__ uint64_t encode_size(uint32_t type, uint32_t enc, uint32_t vstatus, u
     return 0;
 }
 
-// Encode runs as five launches (one memset, no inter-workgroup waits beyond the scan's
-// look-back):
+// Encode runs as a memset and three kernels, with no inter-workgroup waits:
 //   E1 enc_size_kernel  workgroup per 256 values, element-parallel: blob size (0 for an
-//                       unencodable value) into offsets[v], per-tile {bad, payload, descriptors};
-//   E2 scan_kernel      in-place exclusive scan -> offsets[0..n];
-//   E3 enc_index_kernel thread per value: first value of every W-byte output window, and the
-//                       values that would cross data_cap (RR_E_CAPACITY, payload taken back);
+//                       unencodable value), its offset inside the block into offsets[v], the
+//                       block's bytes into btot[b] and (atomically) its group's of 64 blocks
+//                       into gtot; per-tile {bad, payload, descriptors};
+//   E3 enc_index_kernel thread per value, the same blocks: the block's first byte from the
+//                       group and block sums before it (two loads per lane), offsets[v] made
+//                       global, the first value of every W-byte output window, and the values
+//                       that would cross data_cap (RR_E_CAPACITY, payload taken back);
 //   E4 enc_emit_kernel  workgroup per W-byte output window: builds the window's bytes in an
 //                       LDS image (headers and length fields by element-parallel tasks,
 //                       payloads by 64-byte copy pieces), then stores it with 16-byte
-//                       coalesced stores;
-//   E5 finalize         totals.
+//                       coalesced stores; its block 0 folds the totals.
+// (Round 3 ran a look-back scan of the sizes as E2, 15 us on config 4.)
 // Output bytes past the last value that fits (and of a value that does not fit) are zero.
 
 // ---- E1: blob size per value -----------------------------------------------------------
@@ -1565,6 +1567,7 @@ __global__ __launch_bounds__(NT) void enc_size_kernel(const rr_value *__restrict
                                                       const rr_elem *__restrict__ elems, uint64_t n,
                                                       uint64_t ecap, uint64_t acap,
                                                       uint64_t *__restrict__ sizes, uint64_t *__restrict__ stats,
+                                                      uint64_t *__restrict__ btot, uint64_t *gtot,
                                                       uint64_t *zero_words, uint32_t nzero, rr_totals *tot) {
     zero_call_words(zero_words, nzero, tot);
     __shared__ uint32_t tb[NT + 1];                  // first task of each value
@@ -1695,7 +1698,14 @@ __global__ __launch_bounds__(NT) void enc_size_kernel(const rr_value *__restrict
         bad = s_bad[tid];
         size = bad ? 0 : hdr + s_b1[tid];
         pay = bad ? 0 : s_p1[tid];
-        sizes[v] = size;
+    }
+    // the value's offset inside the block; the block's bytes (E3 adds the blocks before it)
+    uint64_t btotal;
+    const uint64_t inb = block_excl_scan<NT>(size, ws0, btotal);
+    if (v < n) sizes[v] = inb;
+    if (tid == 0) {
+        btot[blockIdx.x] = btotal;
+        if (btotal) atomicAdd((unsigned long long *)&gtot[blockIdx.x / WGROUP], (unsigned long long)btotal);
     }
     uint64_t sb = wave_sum_fast(bad), sp = wave_sum_fast(pay), sn = wave_sum_fast(ne);
     const uint32_t wv = tid / RR_WAVE;
@@ -1716,15 +1726,35 @@ __global__ __launch_bounds__(NT) void enc_size_kernel(const rr_value *__restrict
 template <uint32_t W>
 __global__ __launch_bounds__(256) void enc_index_kernel(const rr_value *__restrict__ values,
                                                         const rr_elem *__restrict__ elems, uint64_t n,
-                                                        uint64_t ecap, uint64_t acap,
-                                                        const uint64_t *__restrict__ offsets, uint64_t cap,
+                                                        uint64_t ecap, uint64_t acap, uint64_t *__restrict__ offsets,
+                                                        const uint64_t *__restrict__ btot,
+                                                        const uint64_t *__restrict__ gtot, uint64_t cap,
                                                         uint32_t *__restrict__ fv, uint64_t nwin,
                                                         uint64_t *__restrict__ stats) {
-    __shared__ uint64_t red[2][4];
-    const uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    __shared__ uint64_t red[2][4], wpre[4];
+    const uint32_t tid = threadIdx.x, blk = blockIdx.x;
+    const uint64_t v = (uint64_t)blk * blockDim.x + tid;
+    // the block's first byte: the groups of WGROUP blocks before it, the blocks before it in its
+    // group (E1's sums)
+    const uint32_t grp = blk / WGROUP, gi = blk % WGROUP;
+    uint64_t pre = tid < gi ? btot[(uint64_t)grp * WGROUP + tid] : 0;
+    for (uint32_t k = tid; k < grp; k += blockDim.x) pre += gtot[k];
+    pre = wave_sum_fast(pre);
+    if (lane_id() == 0) wpre[tid / RR_WAVE] = pre;
+    // my offset inside the block and the next value's (the block's last: the block's bytes), read
+    // before any thread of the block overwrites offsets with the global ones
+    uint64_t ia = 0, ib = 0;
+    if (v < n) {
+        ia = offsets[v];
+        ib = tid + 1 < blockDim.x && v + 1 < n ? offsets[v + 1] : btot[blk];
+    }
+    __syncthreads();
+    const uint64_t P = wpre[0] + wpre[1] + wpre[2] + wpre[3];
     uint64_t bad = 0, pay = 0;
     if (v < n) {
-        const uint64_t a = offsets[v], b = offsets[v + 1];
+        const uint64_t a = P + ia, b = P + ib;
+        offsets[v] = a;
+        if (v + 1 == n) offsets[n] = b;
         if (b > a) {
             uint64_t w_hi = (b - 1) / W;
             if (w_hi > nwin) w_hi = nwin;
@@ -2482,8 +2512,9 @@ extern "C" hipError_t rr_launch_decode(const uint8_t *blob, const uint64_t *offs
     return hipGetLastError();
 }
 
-// Encode scratch (uint64 words): [HDR] [scan: ticket, look-back state + groups]
-// [tile stats, 3 per 256 values, twice] [first value per output window u32, nwin+1].
+// Encode scratch (uint64 words): [HDR] [error word] [tile stats, 3 per 256 values, twice]
+// [block sums, t] [group sums, t / WGROUP + 1] [first value per output window u32, nwin+1].
+// E1's block 0 zeroes the error word and the totals; the group sums are zeroed by a memset.
 #ifndef RR_ENC_W
 #define RR_ENC_W 16384
 #endif
@@ -2494,8 +2525,8 @@ constexpr uint32_t ENC_W = RR_ENC_W, ENC_NT = 256, ENC_RCAP = RR_ENC_RCAP;
 static uint64_t enc_windows(uint64_t data_cap) { return data_cap / ENC_W + 1; }
 
 extern "C" uint64_t rr_encode_scratch_words(uint64_t n, uint64_t data_cap) {
-    const uint64_t st = scan_tiles(n), t = (n + 255) / 256, nw = enc_windows(data_cap);
-    return RR_SCRATCH_HDR + 1 + st + (st + LB_GROUP - 1) / LB_GROUP + 1 + 6 * t + (nw + 2) / 2 + 2;
+    const uint64_t t = (n + 255) / 256, nw = enc_windows(data_cap);
+    return RR_SCRATCH_HDR + 1 + 6 * t + t + t / WGROUP + 1 + (nw + 2) / 2 + 2;
 }
 
 extern "C" hipError_t rr_launch_encode(const rr_value *values, const rr_elem *elems, uint64_t elem_cap,
@@ -2507,18 +2538,18 @@ extern "C" hipError_t rr_launch_encode(const rr_value *values, const rr_elem *el
         if (e == hipSuccess && totals) e = hipMemsetAsync(totals, 0, sizeof(rr_totals), stream);
         return e;
     }
-    const uint32_t st = (uint32_t)scan_tiles(n), t = (uint32_t)((n + 255) / 256);
+    const uint32_t t = (uint32_t)((n + 255) / 256);
     const uint64_t nw = enc_windows(cap);
-    uint64_t *lb = scratch + RR_SCRATCH_HDR;
-    const uint64_t lb_words = 1 + st + (st + LB_GROUP - 1) / LB_GROUP;
-    uint64_t *err = lb + lb_words;   // device error word (look-back timeout)
+    uint64_t *err = scratch + RR_SCRATCH_HDR;   // device error word (no look-back left to set it)
     uint64_t *stats = err + 1;
-    uint32_t *fv = reinterpret_cast<uint32_t *>(stats + 6 * (uint64_t)t);
-    hipLaunchKernelGGL((enc_size_kernel<256, ENC_SIZE_U>), dim3(t), dim3(256), 0, stream, values, elems, n, elem_cap, arena_cap, offsets,
-                       stats, lb, (uint32_t)(lb_words + 1), totals);
-    hipLaunchKernelGGL(scan_kernel, dim3(st), dim3(256), 0, stream, offsets, n, lb, st, err);
+    uint64_t *btot = stats + 6 * (uint64_t)t, *gtot = btot + t;
+    uint32_t *fv = reinterpret_cast<uint32_t *>(gtot + t / WGROUP + 1);
+    const hipError_t e = hipMemsetAsync(gtot, 0, (t / WGROUP + 1) * sizeof(uint64_t), stream);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((enc_size_kernel<256, ENC_SIZE_U>), dim3(t), dim3(256), 0, stream, values, elems, n, elem_cap,
+                       arena_cap, offsets, stats, btot, gtot, err, 1u, totals);
     hipLaunchKernelGGL(enc_index_kernel<ENC_W>, dim3(t), dim3(256), 0, stream, values, elems, n, elem_cap, arena_cap,
-                       offsets, cap, fv, nw, stats + 3 * (uint64_t)t);
+                       offsets, btot, gtot, cap, fv, nw, stats + 3 * (uint64_t)t);
     hipLaunchKernelGGL((enc_emit_kernel<ENC_W, ENC_NT, ENC_RCAP>), dim3((uint32_t)nw), dim3(ENC_NT), 0, stream,
                        values, elems, arena, n, out, cap, offsets, fv, stats, 2 * t, totals, err);
     return hipGetLastError();
@@ -2619,27 +2650,58 @@ extern "C" hipError_t rr_launch_flat_rebase(rr_value *values, uint64_t n, rr_ele
 // COPY_U * 256 * 16 bytes (≫ 256 CUs' worth of workgroups), blocks dealt over the XCDs in
 // order.  Bytes past the end read as zeros and their stores are dropped (buffer range), so
 // there is no tail branch.  Used by bench.py as `copy_ref`; no part of the serdes path.
-constexpr uint32_t COPY_U = 8, COPY_NT = 256;
-__global__ __launch_bounds__(COPY_NT) void copy_kernel(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst,
-                                                       uint64_t bytes) {
-    const uint64_t base = (uint64_t)blockIdx.x * (COPY_U * COPY_NT * 16);
-    const uint64_t left = bytes - base;
-    const uint32_t span = left < COPY_U * COPY_NT * 16 ? (uint32_t)left : COPY_U * COPY_NT * 16;
-    const rsrc_t RS = make_rsrc(src + base, span), RD = make_rsrc(dst + base, span);
-    u32x4 x[COPY_U];
+//
+// Shapes (rr_copy_shape, tools/time_copy.py): U 16-byte loads in flight per lane, NT threads, a
+// workgroup per U * NT * 16 bytes (one pass) or a resident grid striding over the buffer, and
+// nontemporal (aux 2) or default-policy stores.
+template <uint32_t U, uint32_t NT, bool NTS>
+__global__ __launch_bounds__(NT) void copy_kernel(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst,
+                                                  uint64_t bytes) {
+    constexpr uint64_t TILE = (uint64_t)U * NT * 16;
+    for (uint64_t base = (uint64_t)blockIdx.x * TILE; base < bytes; base += (uint64_t)gridDim.x * TILE) {
+        const uint64_t left = bytes - base;
+        const uint32_t span = left < TILE ? (uint32_t)left : (uint32_t)TILE;
+        const rsrc_t RS = make_rsrc(src + base, span), RD = make_rsrc(dst + base, span);
+        u32x4 x[U];
 #pragma unroll
-    for (uint32_t k = 0; k < COPY_U; ++k)
-        x[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(RS, (int)((threadIdx.x + k * COPY_NT) * 16), 0, 0));
+        for (uint32_t k = 0; k < U; ++k)
+            x[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(RS, (int)((threadIdx.x + k * NT) * 16), 0, 0));
 #pragma unroll
-    for (uint32_t k = 0; k < COPY_U; ++k)
-        __builtin_amdgcn_raw_buffer_store_b128(x[k], RD, (int)((threadIdx.x + k * COPY_NT) * 16), 0, 2 /* nt */);
+        for (uint32_t k = 0; k < U; ++k)
+            __builtin_amdgcn_raw_buffer_store_b128(x[k], RD, (int)((threadIdx.x + k * NT) * 16), 0, NTS ? 2 : 0);
+    }
+}
+
+template <uint32_t U, uint32_t NT, bool NTS>
+static hipError_t launch_copy_shape(uint8_t *dst, const uint8_t *src, uint64_t bytes, uint32_t grid, hipStream_t stream) {
+    const uint64_t tiles = (bytes + (uint64_t)U * NT * 16 - 1) / ((uint64_t)U * NT * 16);
+    if (grid == 0 || grid > tiles) grid = (uint32_t)tiles;
+    hipLaunchKernelGGL((copy_kernel<U, NT, NTS>), dim3(grid), dim3(NT), 0, stream, src, dst, bytes);
+    return hipGetLastError();
+}
+
+// shape: 0 = the default below; 1-8 = the alternatives timed by tools/time_copy.py (diagnostics)
+extern "C" hipError_t rr_launch_copy_shape(uint8_t *dst, const uint8_t *src, uint64_t bytes, int shape,
+                                           hipStream_t stream) {
+    if (bytes == 0) return hipSuccess;
+    int dev = 0, cus = 256;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    switch (shape) {
+        case 1: return launch_copy_shape<16, 256, true>(dst, src, bytes, 0, stream);
+        case 2: return launch_copy_shape<4, 256, true>(dst, src, bytes, 0, stream);
+        case 3: return launch_copy_shape<8, 256, false>(dst, src, bytes, 0, stream);
+        case 4: return launch_copy_shape<8, 256, true>(dst, src, bytes, (uint32_t)cus * 8, stream);
+        case 5: return launch_copy_shape<8, 512, true>(dst, src, bytes, 0, stream);
+        case 6: return launch_copy_shape<16, 256, true>(dst, src, bytes, (uint32_t)cus * 4, stream);
+        case 7: return launch_copy_shape<4, 1024, true>(dst, src, bytes, 0, stream);
+        case 8: return launch_copy_shape<8, 256, false>(dst, src, bytes, (uint32_t)cus * 8, stream);
+        default: return launch_copy_shape<8, 256, true>(dst, src, bytes, 0, stream);
+    }
 }
 
 extern "C" hipError_t rr_launch_copy(uint8_t *dst, const uint8_t *src, uint64_t bytes, hipStream_t stream) {
-    if (bytes == 0) return hipSuccess;
-    const uint64_t blocks = (bytes + COPY_U * COPY_NT * 16 - 1) / (COPY_U * COPY_NT * 16);
-    hipLaunchKernelGGL(copy_kernel, dim3((uint32_t)blocks), dim3(COPY_NT), 0, stream, src, dst, bytes);
-    return hipGetLastError();
+    return rr_launch_copy_shape(dst, src, bytes, 0, stream);
 }
 
 // ---- the look-back scan for other launchers (rr_snappy.hip) --------------------------------

@@ -9,3 +9,4 @@ timeout -k 10 300 python tests/test_compat.py latency 4 2000 > gpurun_out/latenc
 bash tools/ab_decode.sh "prev s1" "4 3 2 1" > /dev/null && cat gpurun_out/ab.log
 bash tools/kstats_decode.sh gpurun_out/ks4 librr_serdes.so 4
 bash tools/kstats_decode.sh gpurun_out/ks1 librr_serdes.so 1
+timeout -k 10 400 python bench.py > gpurun_out/bench.log 2>&1; tail -c 3000 gpurun_out/bench.log
