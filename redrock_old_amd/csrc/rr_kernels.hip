@@ -318,15 +318,15 @@ __device__ __forceinline__ void fold_totals(const uint64_t *__restrict__ stats, 
 }
 
 // ---------------------------------------------------------------------------------------- decode
-// Four launches, no inter-workgroup waits except the scan's look-back:
+// A memset and two launches, no inter-workgroup waits:
 //   K1 count_kernel   thread per value: its descriptor reservation (rr_format.h) and its walk
-//                     class (rr_decode_class.h; header checks done here);
-//   K2 scan_kernel    exclusive scan of the reservations -> elem_base of every value;
-//   K3 decode_kernel  workgroup per tile of DEC_T values: streams the tile's bytes into the
-//                     mirror arena, sorts the tile's values by class in LDS, then its waves take
-//                     64-value single-class batches (heaviest class first) and walk + emit them
-//                     from L2-hot global memory;
-//   K4 finalize       totals.
+//                     class (rr_decode_class.h; header checks done here), first_val per byte
+//                     window, the reservations summed per window and per group of windows;
+//   K3 decode_kernel  workgroup per byte window: its first slot from the window / group sums,
+//                     the window's bytes into the mirror arena and an LDS stage, then per chunk
+//                     of 512 values a class sort and a slot scan in LDS, and single-class batches
+//                     (heaviest class first) walked from the stage by the waves; the window's
+//                     marked values fixed at its end, its totals added atomically.
 
 // ---- K1: reservation + class per value ------------------------------------------------
 // reserve(i) = the descriptor slots value i owns (rr_format.h): header fields only, plus the
@@ -514,13 +514,10 @@ __global__ __launch_bounds__(256) void count_kernel(const uint8_t *__restrict__ 
     run_sum(gtot, g, in & (lane == 0 || wp / WGROUP != g), in & (lane == RR_WAVE - 1 || wn / WGROUP != g));
 }
 
-// ---- K2: exclusive scan of the reservations -> elem_base -------------------------------
+// ---- exclusive scan of u64 sizes (rr_launch_scan_u64: the snappy kernels' block lengths) ----
 // 4096 values per 256-thread workgroup, tile ids from an atomic ticket (so a tile only waits
 // on tiles already running), decoupled look-back between tiles (two-level, rr_device.h).
-#ifndef RR_SCAN_PT
-#define RR_SCAN_PT 16
-#endif
-constexpr uint32_t SCAN_PER_THREAD = RR_SCAN_PT;
+constexpr uint32_t SCAN_PER_THREAD = 16;
 constexpr uint32_t SCAN_TILE = 256 * SCAN_PER_THREAD;
 
 __global__ __launch_bounds__(256) void scan_kernel(uint64_t *__restrict__ counts, uint64_t n, uint64_t *lb,
@@ -1051,23 +1048,42 @@ __global__ __launch_bounds__(NW * RR_WAVE) __attribute__((amdgpu_waves_per_eu(DE
     static_assert(W % (16 * NT) == 0, "window granules per thread");
     const uint64_t ov_a = A0 >> 4, ov_w1 = W1 >> 4;
     const uint32_t ov_mb = ov_w1 > ov_a ? (uint32_t)((ov_w1 - ov_a) * 16) : 0u;
-    const rsrc_t ov_RM = make_rsrc(blob + A0, ov_mb);
     const rsrc_t ov_RA = make_rsrc(arena + A0, ov_mb);
     // KE granules per thread go out before the first_val -> offsets / class-byte loads, the rest
     // after the class bytes: the sort waits (vmcnt, in issue order) for the class bytes and
     // therefore for the early granules only
     constexpr uint32_t KE = DEC_KE < KM ? DEC_KE : KM;
+    constexpr uint32_t KT = (SLACK / 16 + NT - 1) / NT;   // granules per thread of the stage's tail
+    // KE granules per thread of the window go out first, over the window's range only
     u32x4 ov_m[KM];
+    {
+        const rsrc_t ov_R0 = make_rsrc(blob + A0, ov_mb);
 #pragma unroll
-    for (uint32_t k = 0; k < KE; ++k)
-        ov_m[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ov_RM, (int)((tid + k * NT) * 16), 0, 0));
+        for (uint32_t k = 0; k < KE; ++k)
+            ov_m[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ov_R0, (int)((tid + k * NT) * 16), 0, 0));
+    }
     const uint64_t v_lo = first_val[tile], v_hi = first_val[tile + 1];
+    // The main loads cover W bytes from A0: the window [A0, W1) (win <= W) and, when the call's
+    // window is smaller than W, the start of the stage's tail; the tail loads KT * NT more
+    // granules.  A window is staged when its values' bytes [S0, S1) fit the stage and lie
+    // inside what those loads cover.
+    const uint64_t ov_me = ov_a + (uint64_t)KM * NT, ov_cover = ov_me + (uint64_t)KT * NT;
     uint64_t S0 = W0, S1 = W0;
     if (v_hi > v_lo) {
         S0 = offsets[v_lo] & ~15ull;
         S1 = (offsets[v_hi] + 15) & ~15ull;
     }
-    const bool staged = S1 - S0 <= STAGE;
+    const bool staged = S1 - S0 <= STAGE && (S1 >> 4) <= ov_cover;
+    // the stage's last granule (exclusive) and the main loads' range: the window, plus the tail's
+    // start when staged (the arena stores stay inside [A0, W1): ov_RA)
+    const uint64_t ov_te = (staged && S1 > W1 ? S1 : W1) >> 4;
+    const uint64_t ov_mend = ov_te < ov_me ? ov_te : ov_me;
+    const rsrc_t ov_RM = make_rsrc(blob + A0, ov_mend > ov_a ? (uint32_t)((ov_mend - ov_a) * 16) : 0u);
+    if (ov_mend > ov_w1 && ov_w1 < ov_a + (uint64_t)KE * NT) {   // (a window under KE * NT granules: the
+#pragma unroll                                                     //  early loads stopped at W1)
+        for (uint32_t k = 0; k < KE; ++k)
+            ov_m[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ov_RM, (int)((tid + k * NT) * 16), 0, 0));
+    }
     const uint64_t cap = elem_cap < 0xFFFFFFFFull ? elem_cap : 0xFFFFFFFFull;   // elem_base is 32-bit
 
     // the first chunk's class bytes and reservations, loaded before the rest of the window so
@@ -1077,11 +1093,9 @@ __global__ __launch_bounds__(NW * RR_WAVE) __attribute__((amdgpu_waves_per_eu(DE
 #pragma unroll
     for (uint32_t k = KE; k < KM; ++k)
         ov_m[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ov_RM, (int)((tid + k * NT) * 16), 0, 0));
-    // the stage's tail [W1, S1): at most SLACK bytes, KT granules per thread, also in flight
-    // under the sort
-    constexpr uint32_t KT = (SLACK / 16 + NT - 1) / NT;
-    const uint64_t ov_t0 = ov_w1 > ov_a ? ov_w1 : ov_a;
-    const uint64_t ov_te = (staged && S1 > W1 ? S1 : W1) >> 4;
+    // the rest of the stage's tail [ov_me, ov_te): KT granules per thread, also in flight under
+    // the sort
+    const uint64_t ov_t0 = ov_me;
     const rsrc_t ov_RT = make_rsrc(blob + ov_t0 * 16, ov_te > ov_t0 ? (uint32_t)((ov_te - ov_t0) * 16) : 0u);
     u32x4 ov_t[KT];
 #pragma unroll
@@ -1112,7 +1126,7 @@ __global__ __launch_bounds__(NW * RR_WAVE) __attribute__((amdgpu_waves_per_eu(DE
                 __builtin_amdgcn_raw_buffer_store_b128(ov_m[k], ov_RA, (int)((tid + k * NT) * 16), 0, 2 /* nt */);
             ov_lds[ov_slot(ov_a + tid + (uint64_t)k * NT)] = ov_m[k];
         }
-        // the stage's tail [W1, ov_te): LDS only
+        // the rest of the stage's tail [ov_me, ov_te): LDS only
 #pragma unroll
         for (uint32_t k = 0; k < KT; ++k) ov_lds[ov_slot(ov_t0 + tid + (uint64_t)k * NT)] = ov_t[k];
     };
@@ -1128,7 +1142,6 @@ __global__ __launch_bounds__(NW * RR_WAVE) __attribute__((amdgpu_waves_per_eu(DE
     uint64_t bad = 0, pay = 0, eb0 = 0, run = 0;   // run: the slots of the earlier chunks
     const uint64_t v_end = RR_ABLATE == 1 ? v_lo : v_hi;
     // 2. counting sort of a chunk of values by class (ballot per class, one LDS atomic per
-    //    class per wave-round) into perm, class bases and batch prefixes
     //    class per wave-round) into perm, class bases and batch prefixes; and the scan of the
     //    chunk's reservations into eloc (returns the chunk's slots)
     auto sort_chunk = [&](uint64_t c0) __attribute__((always_inline)) -> uint64_t {
@@ -1193,8 +1206,8 @@ __global__ __launch_bounds__(NW * RR_WAVE) __attribute__((amdgpu_waves_per_eu(DE
     if (v_end > v_lo) {
         ctot = sort_chunk(v_lo);   // (with the window's loads still in flight)
         eb0 = rfl64(first_slot());   // (the waves' sums are behind the sort's first barrier)
-    }    if (v_end > v_lo) sort_chunk(v_lo);   // (with the window's loads still in flight)
-    ov_finish();                          // they have landed under the sort
+    }
+    ov_finish();                         // they have landed under the sort
     for (uint64_t c0 = v_lo; c0 < v_end; c0 += PMAX) {
         if (c0 != v_lo) {
             lds_barrier();   // every wave is done with the previous chunk's batches
@@ -2441,11 +2454,9 @@ extern "C" hipError_t rr_launch_encode_small(const rr_value *values, const rr_el
 #ifndef RR_DEC_NW
 #define RR_DEC_NW 8
 #endif
-#ifndef RR_DEC_PMAX   // values per sort chunk: one per thread (the chunk's slot scan)
-#define RR_DEC_PMAX (RR_DEC_NW * RR_WAVE)
-#endif
 constexpr uint32_t DEC_W = RR_DEC_W, DEC_NW = RR_DEC_NW;
-#define DECODE_KERNEL decode_kernel<RR_DEC_W, RR_DEC_SLACK, RR_DEC_NW, RR_DEC_PMAX>
+// (values per sort chunk: one per thread, the chunk's slot scan)
+#define DECODE_KERNEL decode_kernel<RR_DEC_W, RR_DEC_SLACK, RR_DEC_NW, RR_DEC_NW * RR_WAVE>
 
 // Resident workgroup count for a persistent launch: occupancy query minus one block per CU
 // (the API over-reports by one for SGPR-heavy kernels, MI355X_MICROARCH.md §Residency).

@@ -38,9 +38,6 @@ constexpr uint32_t MARGIN = 15;            // kInputMarginBytes
 #define RR_SNZ_DEC_WIN 20480
 #endif
 constexpr uint32_t SNZ_DEC_WIN = RR_SNZ_DEC_WIN;
-#ifndef RR_SNZ_LIT16   // 1: long literals copied 16 bytes per lane, two 1 KiB chunks per round trip
-#define RR_SNZ_LIT16 1
-#endif
 // staged fragment bytes per wave; 0 (default): the compressor reads its input in place through
 // the buffer resource, so a wave holds only the 32 KiB hash table (4 waves per CU instead of 3)
 #ifndef RR_SNZ_FRAG
@@ -121,12 +118,188 @@ struct Win {
 
 __device__ __forceinline__ void wait_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
+// lane mod off for off <= 64: (lane + 0.5) / off is at least 1 / 129 away from an integer, far
+// beyond v_rcp_f32's error, so the truncated product is the exact quotient
+__device__ __forceinline__ uint32_t lane_mod(uint32_t lane, uint32_t off) {
+    const uint32_t k = (uint32_t)(((float)lane + 0.5f) * __builtin_amdgcn_rcpf((float)off));
+    return lane - k * off;
+}
+
+// Tag decoding shared by both paths (snappy.cc:808 DecompressAllTags, oracle/rr_snappy.c):
+// t holds the 5+ bytes from the tag on (uniform).  Literals: hdr = 1 + extra length bytes,
+// len = the literal's bytes; copies: hdr = 1 + offset bytes, len / off of the back-reference.
+struct Tag {
+    uint32_t hdr, len, off;
+    bool lit;
+};
+__device__ __forceinline__ Tag decode_tag(uint64_t t) {
+    const uint32_t c = (uint32_t)t & 0xFF, ty = c & 3, v = (uint32_t)(t >> 8);
+    Tag g;
+    g.lit = ty == 0;
+    if (g.lit) {
+        g.len = (c >> 2) + 1;
+        g.hdr = 1;
+        g.off = 0;
+        if (g.len >= 61) {
+            const uint32_t nb = g.len - 60;
+            g.len = (nb == 4 ? v : v & ((1u << (8 * nb)) - 1)) + 1;   // (0: 2^32 wrapped)
+            g.hdr += nb;
+        }
+    } else {
+        const uint32_t nb = ty == 1 ? 1u : ty == 2 ? 2u : 4u;
+        g.hdr = 1 + nb;
+        g.len = ty == 1 ? 4 + ((c >> 2) & 7) : (c >> 2) + 1;
+        g.off = ty == 1 ? ((c >> 5) << 8) | (v & 0xFF) : ty == 2 ? v & 0xFFFF : v;
+    }
+    return g;
+}
+
+// A block whose output fits the LDS window, decompressed in place: the compressed bytes staged
+// at the window's end with every load in flight (one round trip), the output assembled from the
+// window's start, every later read from LDS.  Each tag's writes stay below the compressed bytes
+// not yet read — a literal's destination at least 8 bytes below its source, a back-reference's
+// end below the next tag — else the block bails out (*bail) to the global path.  The next tag's
+// bytes are read before the current tag's copy, so the parse overlaps the copies.
+//   R: the block's dwords from its 4-aligned base, s0 + clen bytes (s0: the block's first byte);
+//   returns the status (RR_SNAPPY_*) with the output in win[0, expected).
+__device__ uint32_t dec_block_lds(rsrc_t R, uint32_t s0, uint32_t clen, uint32_t expected, lds_u8 *win, uint32_t wcap,
+                                  bool &bail) {
+    lds_u32 *win32 = (lds_u32 *)win;
+    typedef __attribute__((address_space(3))) u32x4_t lds_u32x4;
+    const uint32_t lane = lane_id(), end = s0 + clen, ng = (end + 15) >> 4;
+    const uint32_t D = wcap + 16 - 16 * ng;   // (the allocation's last 16 bytes: reads past the end)
+    {
+        constexpr uint32_t SG = (SNZ_DEC_WIN + 16) / 16 / WAVE + 1;
+        u32x4_t g[SG];
+#pragma unroll
+        for (uint32_t j = 0; j < SG; ++j) g[j] = __builtin_amdgcn_raw_buffer_load_b128(R, (int)(16 * (lane + WAVE * j)), 0, 0);
+        lds_u32x4 *d4 = (lds_u32x4 *)(win + D);
+#pragma unroll
+        for (uint32_t j = 0; j < SG; ++j)
+            if (lane + WAVE * j < ng) d4[lane + WAVE * j] = g[j];
+    }
+    // the two dwords holding 8 bytes at LDS address a (uniform), read into VGPRs; taken into
+    // SGPRs (and shifted) only where they are used, so the read's latency can hide under
+    // whatever comes between
+    struct Rd {
+        uint32_t lo, hi, sh;
+    };
+    auto rd = [&](uint32_t a) __attribute__((always_inline)) -> Rd {
+        return Rd{win32[a >> 2], win32[(a >> 2) + 1], 8 * (a & 3)};
+    };
+    auto take = [](const Rd &r) __attribute__((always_inline)) -> uint64_t {
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)r.lo);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)r.hi);
+        return (((uint64_t)hi << 32) | lo) >> r.sh;
+    };
+    uint32_t p = s0;
+    uint64_t t = take(rd(D + p));
+    while (t & 0x80) { ++p; t >>= 8; }   // the preamble (validated by snz_len_kernel: <= 5 bytes)
+    ++p;
+    Rd tr = rd(D + p);
+    uint32_t pos = 0;
+    while (p < end) {
+        const Tag g = decode_tag(take(tr));
+        if (p + g.hdr > end) return RR_SNAPPY_E_TRUNC;
+        const uint32_t q = p + g.hdr;   // the literal's bytes / the next tag
+        uint32_t pn = q;
+        if (g.lit) {
+            if (g.len == 0 || g.len > end - q) return RR_SNAPPY_E_TRUNC;
+            if (g.len > expected - pos) return RR_SNAPPY_E_OVERFLOW;
+            pn = q + g.len;
+            if (D + q < pos + 8) { bail = true; return RR_SNAPPY_OK; }
+        } else {
+            if (g.off == 0 || g.off > pos) return RR_SNAPPY_E_OFFSET;
+            if (g.len > expected - pos) return RR_SNAPPY_E_OVERFLOW;
+            if (pos + g.len > D + pn) { bail = true; return RR_SNAPPY_OK; }
+        }
+        tr = rd(D + pn);   // the next tag, read under this one's copy
+        if (g.lit) {
+            const uint32_t src = D + q;
+            if (g.len <= WAVE) {
+                const uint8_t x = lane < g.len ? win[src + lane] : 0;
+                if (lane < g.len) win[pos + lane] = x;
+            } else {
+                // bytes to a 4-aligned destination, then 16 bytes per lane from five aligned
+                // source dwords (the last dword may spill up to 3 bytes past the literal, below
+                // the source: overwritten by the next element before anything reads them)
+                const uint32_t h = (4u - (pos & 3)) & 3;
+                {
+                    const uint8_t x = lane < h ? win[src + lane] : 0;
+                    if (lane < h) win[pos + lane] = x;
+                }
+                const uint32_t d0 = pos + h, q0 = src + h, body = g.len - h, a0 = q0 & ~3u, sh = q0 & 3;
+                for (uint32_t i = 0; i < body; i += 16 * WAVE) {
+                    const uint32_t k = i + 16 * lane, s = k < body ? (a0 + k) >> 2 : 0u;   // (idle lanes: word 0)
+                    const uint32_t x0 = win32[s], x1 = win32[s + 1], x2 = win32[s + 2], x3 = win32[s + 3], x4 = win32[s + 4];
+                    lds_u32 *w = win32 + ((d0 + k) >> 2);
+                    if (k < body) w[0] = __builtin_amdgcn_alignbyte(x1, x0, sh);
+                    if (k + 4 < body) w[1] = __builtin_amdgcn_alignbyte(x2, x1, sh);
+                    if (k + 8 < body) w[2] = __builtin_amdgcn_alignbyte(x3, x2, sh);
+                    if (k + 12 < body) w[3] = __builtin_amdgcn_alignbyte(x4, x3, sh);
+                }
+            }
+        } else {
+            // out[pos + j] = out[pos - off + j % off]: every source byte already written
+            uint32_t j = lane;
+            if (g.off < g.len) j = lane_mod(lane, g.off);
+            const uint8_t x = lane < g.len ? win[pos - g.off + j] : 0;
+            if (lane < g.len) win[pos + lane] = x;
+        }
+        pos += g.len;
+        p = pn;
+    }
+    return pos == expected ? RR_SNAPPY_OK : RR_SNAPPY_E_LENGTH;
+}
+
+// A block past the LDS window (or one that bailed out of it): the compressed bytes through a
+// register window, the output straight into global memory (a back-reference reads its source
+// back through the L2 once the wave's earlier stores have drained).
+__device__ uint32_t dec_block_global(rsrc_t R, uint32_t s0, uint32_t clen, uint32_t expected, rsrc_t Ro) {
+    const uint32_t lane = lane_id(), end = s0 + clen;
+    Win W;
+    W.R = R;
+    W.load(s0);
+    uint32_t p = s0;
+    while (W.bytes(p) & 0x80) ++p;   // the preamble (already validated)
+    ++p;
+    uint32_t pos = 0;
+    while (p < end) {
+        W.track(p);
+        const Tag g = decode_tag(W.bytes(p));
+        if (p + g.hdr > end) return RR_SNAPPY_E_TRUNC;
+        p += g.hdr;
+        if (g.lit) {
+            if (g.len == 0 || g.len > end - p) return RR_SNAPPY_E_TRUNC;
+            if (g.len > expected - pos) return RR_SNAPPY_E_OVERFLOW;
+            for (uint32_t i = 0; i < g.len; i += WAVE) {
+                const uint32_t k = i + lane;
+                if (k < g.len)
+                    __builtin_amdgcn_raw_buffer_store_b8(__builtin_amdgcn_raw_buffer_load_b8(R, (int)(p + k), 0, 0), Ro,
+                                                         (int)(pos + k), 0, 0);
+            }
+            p += g.len;
+        } else {
+            if (g.off == 0 || g.off > pos) return RR_SNAPPY_E_OFFSET;
+            if (g.len > expected - pos) return RR_SNAPPY_E_OVERFLOW;
+            uint32_t j = lane;
+            if (g.off < g.len) j = lane_mod(lane, g.off);
+            wait_stores();   // the wave's earlier output has reached the L2
+            const uint8_t x = lane < g.len ? __builtin_amdgcn_raw_buffer_load_b8(Ro, (int)(pos - g.off + j), 0, 17) : 0;
+            if (lane < g.len) __builtin_amdgcn_raw_buffer_store_b8(x, Ro, (int)(pos + lane), 0, 0);
+        }
+        pos += g.len;
+    }
+    return pos == expected ? RR_SNAPPY_OK : RR_SNAPPY_E_LENGTH;
+}
+
 __global__ __launch_bounds__(WAVE) void snz_dec_kernel(const uint8_t *__restrict__ in, uint64_t in_cap,
                                                        const uint64_t *__restrict__ in_offs, uint64_t n,
                                                        uint8_t *__restrict__ out, uint64_t out_cap,
                                                        const uint64_t *__restrict__ out_offs,
                                                        uint8_t *__restrict__ status, uint32_t wcap) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t win[];
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    lds_u8 *win = (lds_u8 *)smem;
     lds_u32 *win32 = (lds_u32 *)win;
     const uint32_t lane = lane_id();
     for (uint64_t b = blockIdx.x; b < n; b += gridDim.x) {
@@ -138,156 +311,38 @@ __global__ __launch_bounds__(WAVE) void snz_dec_kernel(const uint8_t *__restrict
         }
         const uint32_t expected = (uint32_t)(o1 - o0);
         const uint64_t c0 = in_offs[b], clen = in_offs[b + 1] - c0;
-        const uint32_t s0 = (uint32_t)(c0 & 3), end = s0 + (uint32_t)clen;
-        Win W;
-        W.R = mkr(in + (c0 - s0), in_cap - (c0 - s0));   // (whole dwords: the buffer's padding, not past it)
-        W.load(s0);
-        uint32_t p = s0;
-        while (W.bytes(p) & 0x80) ++p;   // the preamble (already validated)
-        ++p;
-        const bool inl = expected <= wcap;
+        const uint32_t s0 = (uint32_t)(c0 & 3);
+        const uint64_t base = c0 - s0;   // (whole dwords: the buffer's padding, not past it)
         uint8_t *gout = out + o0;
         const rsrc_t Ro = mkr(gout, expected);
-        uint32_t pos = 0, st = RR_SNAPPY_OK;
-        while (p < end) {
-            W.track(p);
-            const uint64_t t = W.bytes(p);
-            const uint32_t c = (uint32_t)t & 0xFF;
-            if ((c & 3) == 0) {   // literal
-                uint32_t len = (c >> 2) + 1, hdr = 1;
-                if (len >= 61) {
-                    const uint32_t nb = len - 60;
-                    if (p + 1 + nb > end) { st = RR_SNAPPY_E_TRUNC; break; }
-                    const uint32_t v = (uint32_t)(t >> 8);
-                    len = (nb == 4 ? v : v & ((1u << (8 * nb)) - 1)) + 1;
-                    hdr += nb;
-                    if (len == 0) { st = RR_SNAPPY_E_TRUNC; break; }   // (2^32 wrapped: more than any block)
+        uint32_t st = RR_SNAPPY_OK;
+        bool bail = !(expected <= wcap && ((s0 + clen + 15) & ~15ull) <= wcap);
+        if (!bail) {
+            const uint64_t span = (s0 + clen + 15) & ~15ull;
+            st = dec_block_lds(mkr(in + base, span < in_cap - base ? span : in_cap - base), s0, (uint32_t)clen, expected,
+                               win, wcap, bail);
+            if (!bail && st == RR_SNAPPY_OK) {   // LDS -> output: bytes to a 4-aligned address, 16 B per lane, bytes
+                const uint32_t g0 = (uint32_t)((uintptr_t)gout & 3), hh = min((4u - g0) & 3, expected);
+                const uint32_t t0 = hh + ((expected - hh) & ~3u);
+                if (lane < hh) __builtin_amdgcn_raw_buffer_store_b8(win[lane], Ro, (int)lane, 0, 0);
+                // five LDS dwords -> four output dwords, one dwordx4 store (output dword-aligned);
+                // the last partial group of dwords one at a time
+                const uint32_t sh = hh & 3, t16 = hh + ((t0 - hh) & ~15u);
+                for (uint32_t j = hh + 16 * lane; j < t16; j += 16 * WAVE) {
+                    const uint32_t a = j >> 2;
+                    const uint32_t w0 = win32[a], w1 = win32[a + 1], w2 = win32[a + 2], w3 = win32[a + 3], w4 = win32[a + 4];
+                    const u32x4_t v = {__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
+                                       __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh)};
+                    __builtin_amdgcn_raw_buffer_store_b128(v, Ro, (int)j, 0, 0);
                 }
-                p += hdr;
-                if (len > end - p) { st = RR_SNAPPY_E_TRUNC; break; }
-                if (len > expected - pos) { st = RR_SNAPPY_E_OVERFLOW; break; }
-                if (inl && len <= WAVE && p + len <= W.wb + Win::SPAN) {
-                    // a short literal inside the register window: lane k gathers byte p + k from
-                    // the lane holding it (ds_bpermute, no memory access)
-                    const uint32_t r = p + lane - W.wb, src = (r >> 4) & (WAVE - 1), k4 = (r >> 2) & 3;
-                    const uint32_t y0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src * 4), (int)W.x[0]);
-                    const uint32_t y1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src * 4), (int)W.x[1]);
-                    const uint32_t y2 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src * 4), (int)W.x[2]);
-                    const uint32_t y3 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src * 4), (int)W.x[3]);
-                    uint32_t y = k4 == 0 ? y0 : k4 == 1 ? y1 : k4 == 2 ? y2 : y3;
-                    if (lane < len) win[pos + lane] = (uint8_t)(y >> (8 * (r & 3)));
-                } else if (inl) {
-                    // bytes up to a 4-aligned output position, then whole dwords (a lane's dword
-                    // from two aligned source dwords; the last may spill up to 3 bytes past the
-                    // literal, which the next element overwrites before anything reads them)
-                    const uint32_t h = min((4u - (pos & 3)) & 3, len);
-                    if (lane < h) win[pos + lane] = __builtin_amdgcn_raw_buffer_load_b8(W.R, (int)(p + lane), 0, 0);
-                    const uint32_t d0 = pos + h, q0 = p + h, body = len - h;
-#if RR_SNZ_LIT16
-                    // 16 bytes per lane (one dwordx4 + one dword load from the dword-aligned source,
-                    // four alignbyte dwords), two 1 KiB chunks in flight per round trip
-                    const uint32_t a0 = q0 & ~3u, sh = q0 & 3;
-                    // the window the next tag needs, loaded beside the literal's bytes (one round
-                    // trip for both instead of a reload after the copy)
-                    const uint32_t pn = p + len, nwb = pn & ~15u;
-                    const bool slide = pn + 8 > W.wb + Win::SPAN;
-                    u32x4_t nx = {W.x[0], W.x[1], W.x[2], W.x[3]};
-                    if (slide) nx = __builtin_amdgcn_raw_buffer_load_b128(W.R, (int)(nwb + 16 * lane), 0, 0);
-                    for (uint32_t i = 0; i < body; i += 32 * WAVE) {
-                        const uint32_t kA = i + 16 * lane, kB = kA + 16 * WAVE;
-                        const auto xA = __builtin_amdgcn_raw_buffer_load_b128(W.R, (int)(a0 + kA), 0, 0);
-                        const uint32_t eA = __builtin_amdgcn_raw_buffer_load_b32(W.R, (int)(a0 + kA + 16), 0, 0);
-                        const auto xB = __builtin_amdgcn_raw_buffer_load_b128(W.R, (int)(a0 + kB), 0, 0);
-                        const uint32_t eB = __builtin_amdgcn_raw_buffer_load_b32(W.R, (int)(a0 + kB + 16), 0, 0);
-                        lds_u32 *wA = win32 + ((d0 + kA) >> 2), *wB = win32 + ((d0 + kB) >> 2);
-                        if (kA < body) wA[0] = __builtin_amdgcn_alignbyte(xA[1], xA[0], sh);
-                        if (kA + 4 < body) wA[1] = __builtin_amdgcn_alignbyte(xA[2], xA[1], sh);
-                        if (kA + 8 < body) wA[2] = __builtin_amdgcn_alignbyte(xA[3], xA[2], sh);
-                        if (kA + 12 < body) wA[3] = __builtin_amdgcn_alignbyte(eA, xA[3], sh);
-                        if (kB < body) wB[0] = __builtin_amdgcn_alignbyte(xB[1], xB[0], sh);
-                        if (kB + 4 < body) wB[1] = __builtin_amdgcn_alignbyte(xB[2], xB[1], sh);
-                        if (kB + 8 < body) wB[2] = __builtin_amdgcn_alignbyte(xB[3], xB[2], sh);
-                        if (kB + 12 < body) wB[3] = __builtin_amdgcn_alignbyte(eB, xB[3], sh);
-                    }
-                    if (slide) {
-                        W.wb = nwb;
-                        W.x[0] = nx[0]; W.x[1] = nx[1]; W.x[2] = nx[2]; W.x[3] = nx[3];
-                    }
-#else
-                    for (uint32_t i = 0; i < body; i += 4 * WAVE) {
-                        const uint32_t k = i + 4 * lane;
-                        if (k < body) {
-                            const uint32_t q = q0 + k, a = q & ~3u;
-                            const uint32_t lo = __builtin_amdgcn_raw_buffer_load_b32(W.R, (int)a, 0, 0);
-                            const uint32_t hi = __builtin_amdgcn_raw_buffer_load_b32(W.R, (int)a + 4, 0, 0);
-                            win32[(d0 + k) >> 2] = __builtin_amdgcn_alignbyte(hi, lo, q & 3);
-                        }
-                    }
-#endif
-                } else {
-                    for (uint32_t i = 0; i < len; i += WAVE) {
-                        const uint32_t k = i + lane;
-                        if (k < len)
-                            __builtin_amdgcn_raw_buffer_store_b8(__builtin_amdgcn_raw_buffer_load_b8(W.R, (int)(p + k), 0, 0),
-                                                                 Ro, (int)(pos + k), 0, 0);
-                    }
+                for (uint32_t j = t16 + 4 * lane; j < t0; j += 4 * WAVE) {
+                    const uint32_t a = j >> 2;
+                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_amdgcn_alignbyte(win32[a + 1], win32[a], j & 3), Ro, (int)j, 0, 0);
                 }
-                pos += len;
-                p += len;
-            } else {              // copy with a 1-, 2- or 4-byte offset
-                const uint32_t ty = c & 3, nb = ty == 1 ? 1u : ty == 2 ? 2u : 4u;
-                if (p + 1 + nb > end) { st = RR_SNAPPY_E_TRUNC; break; }
-                const uint32_t v = (uint32_t)(t >> 8);
-                const uint32_t len = ty == 1 ? 4 + ((c >> 2) & 7) : (c >> 2) + 1;
-                const uint32_t off = ty == 1 ? ((c >> 5) << 8) | (v & 0xFF) : ty == 2 ? v & 0xFFFF : v;
-                p += 1 + nb;
-                if (off == 0 || off > pos) { st = RR_SNAPPY_E_OFFSET; break; }
-                if (len > expected - pos) { st = RR_SNAPPY_E_OVERFLOW; break; }
-                // out[pos + j] = out[pos - off + j % off]: every source byte is already written
-                uint32_t j = lane;
-                if (off < len) {
-                    const uint32_t q = (uint32_t)(((float)lane + 0.5f) * (1.0f / (float)off));
-                    j = lane - q * off;
-                }
-                if (inl) {
-                    const uint8_t x = lane < len ? win[pos - off + j] : 0;
-                    if (lane < len) win[pos + lane] = x;
-                } else {
-                    wait_stores();   // the wave's earlier output has reached the L2
-                    const uint8_t x = lane < len ? __builtin_amdgcn_raw_buffer_load_b8(Ro, (int)(pos - off + j), 0, 17) : 0;
-                    if (lane < len) __builtin_amdgcn_raw_buffer_store_b8(x, Ro, (int)(pos + lane), 0, 0);
-                }
-                pos += len;
+                if (t0 + lane < expected) __builtin_amdgcn_raw_buffer_store_b8(win[t0 + lane], Ro, (int)(t0 + lane), 0, 0);
             }
         }
-        if (st == RR_SNAPPY_OK && pos != expected) st = RR_SNAPPY_E_LENGTH;
-        if (inl && st == RR_SNAPPY_OK) {   // LDS -> output: bytes to a 4-aligned address, dwords, bytes
-            const uint32_t g0 = (uint32_t)((uintptr_t)gout & 3), hh = min((4u - g0) & 3, expected);
-            const uint32_t t0 = hh + ((expected - hh) & ~3u);
-            if (lane < hh) __builtin_amdgcn_raw_buffer_store_b8(win[lane], Ro, (int)lane, 0, 0);
-#if RR_SNZ_LIT16
-            // 16 bytes per lane: five LDS dwords -> four output dwords, one dwordx4 store (output
-            // dword-aligned); the last partial group of dwords one at a time
-            const uint32_t sh = hh & 3, t16 = hh + ((t0 - hh) & ~15u);
-            for (uint32_t j = hh + 16 * lane; j < t16; j += 16 * WAVE) {
-                const uint32_t a = j >> 2;
-                const uint32_t w0 = win32[a], w1 = win32[a + 1], w2 = win32[a + 2], w3 = win32[a + 3], w4 = win32[a + 4];
-                const u32x4_t v = {__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
-                                   __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh)};
-                __builtin_amdgcn_raw_buffer_store_b128(v, Ro, (int)j, 0, 0);
-            }
-            for (uint32_t j = t16 + 4 * lane; j < t0; j += 4 * WAVE) {
-                const uint32_t a = j >> 2;
-                __builtin_amdgcn_raw_buffer_store_b32(__builtin_amdgcn_alignbyte(win32[a + 1], win32[a], j & 3), Ro, (int)j, 0, 0);
-            }
-#else
-            for (uint32_t j = hh + 4 * lane; j < t0; j += 4 * WAVE) {
-                const uint32_t a = j >> 2;
-                __builtin_amdgcn_raw_buffer_store_b32(__builtin_amdgcn_alignbyte(win32[a + 1], win32[a], j & 3), Ro, (int)j, 0, 0);
-            }
-#endif
-            if (t0 + lane < expected) __builtin_amdgcn_raw_buffer_store_b8(win[t0 + lane], Ro, (int)(t0 + lane), 0, 0);
-        }
+        if (bail) st = dec_block_global(mkr(in + base, in_cap - base), s0, (uint32_t)clen, expected, Ro);
         if (lane == 0) status[b] = (uint8_t)st;
     }
 }
@@ -374,9 +429,6 @@ __device__ __forceinline__ uint32_t match_len(const Frag &F, uint32_t a, uint32_
 #ifndef RR_SNZ_K   // most probes a compressor step-1 round evaluates at once (1: the serial loop)
 #define RR_SNZ_K 16
 #endif
-#ifndef RR_SNZ_K0  // the first round's width after a match
-#define RR_SNZ_K0 16
-#endif
 __device__ void compress_fragment(const Frag &F, uint32_t fn, lds_u16 *table, uint32_t ts, lds_u32 *mark, Out &O) {
     const uint32_t shift = 32 - log2floor(ts);
     uint32_t ip = 0, next_emit = 0;
@@ -395,7 +447,7 @@ __device__ void compress_fragment(const Frag &F, uint32_t fn, lds_u16 *table, ui
             (void)next_hash;
             {
                 const uint32_t lane = lane_id();
-                uint32_t P0 = ip, S0 = 32, K = RR_SNZ_K0;   // a round's width doubles while nothing matches
+                uint32_t P0 = ip, S0 = 32, K = RR_SNZ_K < 16 ? RR_SNZ_K : 16;   // (doubling up to RR_SNZ_K while nothing matches)
                 for (;;) {
                     uint32_t P = P0, S = S0;
                     if (S0 + K <= 64) {   // the stride is 1 for the whole round (the common case)
@@ -414,7 +466,7 @@ __device__ void compress_fragment(const Frag &F, uint32_t fn, lds_u16 *table, ui
                     const uint32_t x = F.ld32(act ? P : 0);
                     const uint32_t H = hash32(x, shift);
                     int prev = -1;
-#if RR_SNZ_K == 16 && RR_SNZ_K0 == 16
+#if RR_SNZ_K == 16
                     // (one 16-lane DPP row: lane j sees lane j - r by a row shift, no LDS round trip)
 #define SNZ_ROW_SHR(r) { \
         const uint32_t hk = (uint32_t)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)H, 0x110 + (r), 0xF, 0xF, false); \
@@ -591,7 +643,7 @@ extern "C" hipError_t rr_launch_snappy_decompress(const uint8_t *in, uint64_t in
                        status, lb, (uint32_t)lbw);
     hipError_t e = rr_launch_scan_u64(out_offs, n, lb, err, stream);
     if (e != hipSuccess || n == 0) return e != hipSuccess ? e : hipGetLastError();
-    hipLaunchKernelGGL(snz_dec_kernel, dim3(grid_for(n, 1u << 20)), dim3(WAVE), SNZ_DEC_WIN + 16, stream, in, in_cap, in_offs, n, out,
+    hipLaunchKernelGGL(snz_dec_kernel, dim3(grid_for(n, 1u << 20)), dim3(WAVE), SNZ_DEC_WIN + 48, stream, in, in_cap, in_offs, n, out,
                        out_cap, (const uint64_t *)out_offs, status, SNZ_DEC_WIN);
     return hipGetLastError();
 }

@@ -9,11 +9,15 @@ import os
 import struct
 import subprocess
 
+import sys
+
 import pytest
 
-from helpers import golden
-
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:   # (run as a script: `python tests/test_compat.py latency`)
+    sys.path.insert(0, ROOT)
+
+from helpers import golden  # noqa: E402
 
 
 def _c_bytes(b):

@@ -1,17 +1,13 @@
 #!/bin/bash
-# Round-4 GPU step: the GPU suite, snappy timings (new decompressor vs the round-3 build), the
-# per-value latency bench, decode / encode A/B against the round-3 build, copy shapes, per-kernel
-# times of the decode on configs 4 and 1, the bench line.
+# Round-4 GPU step: the GPU suite, snappy PMC passes, then the timing legs of gpu_r4b.
 set -e
 mkdir -p gpurun_out
 rc=0; timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 240 --timeout-method thread > gpurun_out/t.log 2>&1 || rc=$?
 grep -E "^FAILED|passed|failed" gpurun_out/t.log | tail -30
 [ $rc -le 1 ] || exit $rc
-for c in 4 3; do
-  timeout -k 10 200 python tools/time_snappy.py $c 1000000 5 >> gpurun_out/snz.log 2>&1
-  RR_LIB=librr_serdes_prev.so timeout -k 10 200 python tools/time_snappy.py $c 1000000 5 >> gpurun_out/snz.log 2>&1
-done
-cat gpurun_out/snz.log
+for c in 4 3; do timeout -k 10 200 python tools/time_snappy.py $c 1000000 5 >> gpurun_out/snz.log 2>&1; done; cat gpurun_out/snz.log
+bash tools/pmc_snappy.sh gpurun_out/pmc_snz 4
+python3 tools/pmc_by_kernel.py -a gpurun_out/pmc_snz/sq1 gpurun_out/pmc_snz/sq2 > gpurun_out/pmc_snz.txt; cat gpurun_out/pmc_snz.txt
 timeout -k 10 300 python tests/test_compat.py latency 4 2000 > gpurun_out/latency.log 2>&1; cat gpurun_out/latency.log
 bash tools/ab_decode.sh "prev" "4 1" > /dev/null && cat gpurun_out/ab.log
 bash tools/ab_encode.sh "prev" "4" > /dev/null && cat gpurun_out/ab_enc.log
