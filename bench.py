@@ -266,6 +266,7 @@ def main():
 
     # roofline of the decode kernel (SURVEY.md §8d algorithmic bytes, per launch, this rank)
     alg_bytes = nb + 16 * n + 16 * n_elems + payload
+    traffic = measured_traffic(args.config, n, nb)
     achieved = alg_bytes / (ev_dec * 1e-3) / 1e9
     enc_alg = 16 * n + 16 * n_elems + int(tot2[3]) + nb + 8 * (n + 1)
     enc_achieved = enc_alg / (ev_enc * 1e-3) / 1e9
@@ -294,9 +295,10 @@ def main():
         "encode": {"gib_s": round(enc_gib_s, 2), "ms_per_step": round(wall_enc / args.steps * 1e3, 4),
                    "event_ms_per_launch": round(ev_enc, 4),
                    "roofline_achieved_GBs": round(enc_achieved, 1)},
-        "roofline": {"bound": "hbm", "kernel": "rr_decode_batch (count + scan + decode + post kernels)",
+        "roofline": {"bound": "hbm", "kernel": "rr_decode_batch (memset + count_kernel + decode_kernel)",
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": measured_traffic(args.config, n, nb),
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic[0],
+                     "traffic_source": traffic[1],
                      "alg_bytes_per_launch": alg_bytes,
                      "frac_of_copy": round(achieved / copy_ref["GBs"], 4) if copy_ref["GBs"] else None},
         "copy_ref": copy_ref,
@@ -458,8 +460,10 @@ def snappy_leg(rr, torch, eng, stream, d_data, nb, timed, args, cpu_too):
 
 
 def measured_traffic(config, n, nb):
-    """HBM bytes per decode call from the committed rocprofv3 PMC summary of this workload
-    (tools/profile_bench.sh + tools/traffic_summary.py), or None if none matches."""
+    """HBM bytes per decode call from the newest committed rocprofv3 PMC summary of this workload
+    (tools/profile_bench.sh + tools/traffic_summary.py) and that file's name — the counters are
+    collected in their own runs (rocprofv3 --pmc cannot ride along a timed run), so the line says
+    which profile they come from — or (None, None) if none matches."""
     import glob
     for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_decode_summary.json")), reverse=True):
         try:
@@ -467,10 +471,10 @@ def measured_traffic(config, n, nb):
                 d = json.load(f)
             w = d.get("workload") or {}
             if (w.get("config"), w.get("n"), w.get("blob_bytes")) == (config, n, nb) and d.get("traffic_bytes_per_call"):
-                return int(d["traffic_bytes_per_call"])
+                return int(d["traffic_bytes_per_call"]), os.path.relpath(p, ROOT)
         except (OSError, ValueError):
             continue
-    return None
+    return None, None
 
 
 def cpu_baseline(data, offs, nb, budget_s):

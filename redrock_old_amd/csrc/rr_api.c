@@ -152,7 +152,7 @@ int rr_decode_batch(rr_ctx *c, const rr_blob_batch *in, rr_flat_batch *out, rr_t
     if (SMALL_DEC(c, in->n, in->data_cap)) {   /* one launch, no scratch */
         HIPCHK(hipSetDevice(c->device));
         HIPCHK(rr_launch_decode_small(in->data, in->offsets, in->n, out->values, out->elems, out->elem_cap, out->arena,
-                                      d_totals, (hipStream_t)stream));
+                                      d_totals, NULL, 0, (hipStream_t)stream));
         return RR_API_OK;
     }
     int rc = ensure_scratch(c, rr_decode_scratch_words(in->data_cap, in->n), (hipStream_t)stream);
@@ -172,7 +172,7 @@ int rr_encode_batch(rr_ctx *c, const rr_flat_batch *in, rr_blob_batch *out, rr_t
     if (SMALL_ENC(c, in->n, out->data_cap)) {   /* one launch, no scratch */
         HIPCHK(hipSetDevice(c->device));
         HIPCHK(rr_launch_encode_small(in->values, in->elems, in->elem_cap, in->arena, in->arena_cap, in->n, out->data,
-                                      out->data_cap, out->offsets, d_totals, (hipStream_t)stream));
+                                      out->data_cap, out->offsets, d_totals, NULL, 0, (hipStream_t)stream));
         return RR_API_OK;
     }
     int rc = ensure_scratch(c, rr_encode_scratch_words(in->n, out->data_cap), (hipStream_t)stream);
@@ -347,11 +347,32 @@ static int small_grow(rr_ctx *c, size_t need) {
 }
 #define AL16(x) (((x) + 15) & ~(size_t)15)
 
+/* Wait for a one-launch kernel by its completion word in the mapped staging (signal_done in
+ * rr_kernels.hip) instead of a stream synchronisation.  The stream is polled now and then, so a
+ * kernel that faulted (the stream reports an error) or ended without the word cannot hang it. */
+static int small_wait(rr_ctx *c, const uint32_t *flag, uint32_t seq) {
+    for (uint64_t k = 1;; ++k) {
+        if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq) return RR_API_OK;
+        if ((k & 4095) == 0) {
+            const hipError_t q = hipStreamQuery(c->stream);
+            if (q == hipSuccess) {
+                if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq) return RR_API_OK;
+                return fail(RR_API_EDEVICE, "one-launch kernel ended without its completion word");
+            }
+            if (q != hipErrorNotReady) {
+                (void)hipGetLastError();
+                return fail(RR_API_EDEVICE, hipGetErrorString(q));
+            }
+        }
+        __builtin_ia32_pause();
+    }
+}
+
 static int decode_host_small(rr_ctx *c, const uint8_t *data, const uint64_t *offsets, uint64_t n, rr_value *values,
                              rr_elem *elems, uint64_t elem_cap, uint8_t *arena, rr_totals *totals) {
     const uint64_t bytes = offsets[n];
     const size_t o_off = 0, o_dat = AL16((n + 1) * sizeof(uint64_t)), o_tot = o_dat + AL16(bytes) + 16,
-                 o_val = o_tot + sizeof(rr_totals), o_el = AL16(o_val + n * sizeof(rr_value)),
+                 o_flag = o_tot + sizeof(rr_totals), o_val = AL16(o_flag + 4), o_el = AL16(o_val + n * sizeof(rr_value)),
                  end = o_el + elem_cap * sizeof(rr_elem);
     int rc = small_grow(c, end);
     if (rc) return rc;
@@ -360,9 +381,14 @@ static int decode_host_small(rr_ctx *c, const uint8_t *data, const uint64_t *off
     memcpy(h + o_off, offsets, (n + 1) * sizeof(uint64_t));
     if (bytes) memcpy(h + o_dat, data, bytes);
     memset(h + o_dat + bytes, 0, AL16(bytes) + 16 - bytes);
+    uint32_t seq = ++c->small_seq;
+    if (!seq) seq = ++c->small_seq;   /* (0 is the cleared word) */
+    __atomic_store_n((uint32_t *)(h + o_flag), 0u, __ATOMIC_RELAXED);
     HIPCHK(rr_launch_decode_small(d + o_dat, (const uint64_t *)(d + o_off), n, (rr_value *)(d + o_val),
-                                  (rr_elem *)(d + o_el), elem_cap, NULL, (rr_totals *)(d + o_tot), c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
+                                  (rr_elem *)(d + o_el), elem_cap, NULL, (rr_totals *)(d + o_tot),
+                                  (uint32_t *)(d + o_flag), seq, c->stream));
+    rc = small_wait(c, (const uint32_t *)(h + o_flag), seq);
+    if (rc) return rc;
     rr_totals t;
     memcpy(&t, h + o_tot, sizeof t);
     if (n) memcpy(values, h + o_val, n * sizeof(rr_value));
@@ -428,17 +454,21 @@ static int encode_host_small(rr_ctx *c, const rr_value *values, const rr_elem *e
                              uint64_t *offsets, rr_totals *totals) {
     const size_t o_val = 0, o_el = AL16(n * sizeof(rr_value)), o_ar = o_el + AL16(n_elems * sizeof(rr_elem)),
                  o_off = o_ar + AL16(arena_bytes), o_tot = o_off + AL16((n + 1) * sizeof(uint64_t)),
-                 o_out = o_tot + 32, end = o_out + AL16(data_cap) + 16;
+                 o_flag = o_tot + 32, o_out = o_flag + 16, end = o_out + AL16(data_cap) + 16;
     int rc = small_grow(c, end);
     if (rc) return rc;
     uint8_t *h = c->h_small, *d = c->d_small;
     memcpy(h + o_val, values, n * sizeof(rr_value));
     if (n_elems) memcpy(h + o_el, elems, n_elems * sizeof(rr_elem));
     if (arena_bytes) memcpy(h + o_ar, arena, arena_bytes);
+    uint32_t seq = ++c->small_seq;
+    if (!seq) seq = ++c->small_seq;   /* (0 is the cleared word) */
+    __atomic_store_n((uint32_t *)(h + o_flag), 0u, __ATOMIC_RELAXED);
     HIPCHK(rr_launch_encode_small((const rr_value *)(d + o_val), (const rr_elem *)(d + o_el), n_elems, d + o_ar,
                                   arena_bytes, n, d + o_out, data_cap, (uint64_t *)(d + o_off),
-                                  (rr_totals *)(d + o_tot), c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
+                                  (rr_totals *)(d + o_tot), (uint32_t *)(d + o_flag), seq, c->stream));
+    rc = small_wait(c, (const uint32_t *)(h + o_flag), seq);
+    if (rc) return rc;
     rr_totals t;
     memcpy(&t, h + o_tot, sizeof t);
     memcpy(offsets, h + o_off, (n + 1) * sizeof(uint64_t));

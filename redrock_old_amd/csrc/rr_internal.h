@@ -29,6 +29,7 @@ struct rr_ctx {
     /* small batches through the host entry points: one pinned buffer mapped into the device,
      * which the one-launch kernels read their input from and write their output to */
     uint8_t *h_small, *d_small;
+    uint32_t small_seq;   /* the one-launch kernels' completion words (small_wait) */
     size_t c_small;
 };
 

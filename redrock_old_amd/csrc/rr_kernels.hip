@@ -459,20 +459,39 @@ __device__ __forceinline__ void zero_call_words(uint64_t *words, uint32_t nwords
 
 // Per value: its reservation (u32; a value that would need 2^32 slots fails capacity anyway),
 // its class and first_val.  Per window: the reservations of its values summed into wtot[w], and
-// per group of WGROUP windows into gtot[w / WGROUP] (both zeroed by a memset before the launch):
-// a window's values are consecutive, so each run of one window (group) in a wave adds its sum
-// with two non-returning atomics — the inclusive wave scan at its last lane, minus the
-// exclusive scan at its first.  decode_kernel then finds its first descriptor slot from at most
-// two loads per lane (the groups before it, the windows before it in its group): no scan launch.
-constexpr uint32_t WGROUP = 64;
-__global__ __launch_bounds__(256) void count_kernel(const uint8_t *__restrict__ blob,
-                                                    const uint64_t *__restrict__ offsets, uint64_t n,
-                                                    uint32_t *__restrict__ first_val, uint32_t nwin, uint32_t win,
-                                                    uint32_t *__restrict__ counts, uint8_t *__restrict__ cls,
-                                                    uint64_t *wtot, uint64_t *gtot,
-                                                    uint64_t *zero_words, uint32_t nzero, rr_totals *tot) {
+// per group of WGROUP windows into gtot[w / WGROUP] (both zeroed by a memset before the launch).
+// A window's values are consecutive, so each run of one window (group) in a wave adds its sum
+// with two LDS atomics — the inclusive wave scan at its last lane, minus the exclusive scan at
+// its first — into the workgroup's table of the windows (groups) it touches; the table then
+// goes to global memory with one atomic per touched window (group) per workgroup.  (Global
+// atomics straight from the waves serialize on the same words: ~16 waves per 72 KiB window and
+// ~1K per group of config 1's 70-byte values — count 52 -> 162 us.)  decode_kernel then finds
+// its first descriptor slot from at most two loads per lane (the groups before it, the windows
+// before it in its group): no scan launch.
+// o / win for the call's (runtime) window size without a 64-bit integer division (~50
+// instructions): a double-precision reciprocal — o < 2^53, so the product is within one of the
+// quotient — and one correction
+__device__ __forceinline__ uint64_t div_win(uint64_t o, uint32_t win, double rcp) {
+    uint64_t q = (uint64_t)((double)o * rcp);
+    const int64_t rem = (int64_t)(o - q * win);
+    q = rem < 0 ? q - 1 : rem >= (int64_t)win ? q + 1 : q;
+    return q;
+}
+constexpr uint32_t WGROUP = 16;   // (64: ~260 same-address atomics per group sum on config 1)
+constexpr uint32_t CNT_NT = 256, CNT_LW = CNT_NT, CNT_LG = 8;   // (a workgroup's values start in <= 256 windows)
+__global__ __launch_bounds__(CNT_NT) void count_kernel(const uint8_t *__restrict__ blob,
+                                                       const uint64_t *__restrict__ offsets, uint64_t n,
+                                                       uint32_t *__restrict__ first_val, uint32_t nwin, uint32_t win,
+                                                       uint32_t *__restrict__ counts, uint8_t *__restrict__ cls,
+                                                       uint64_t *wtot, uint64_t *gtot,
+                                                       uint64_t *zero_words, uint32_t nzero, rr_totals *tot) {
+    __shared__ uint64_t lw[CNT_LW], lg[CNT_LG];
     zero_call_words(zero_words, nzero, tot);
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t tid = threadIdx.x;
+    lw[tid] = 0;
+    if (tid < CNT_LG) lg[tid] = 0;
+    const uint64_t b0 = (uint64_t)blockIdx.x * CNT_NT;
+    const uint64_t i = b0 + tid;
     const uint64_t ic = i < n ? i : n;   // (every lane stays for the wave scans; i == n: first_val's sentinel)
     // the three offsets in one round trip (loads at clamped indices, no guard branch whose join
     // made the compiler wait for the first two before issuing the third), the header granules
@@ -480,13 +499,15 @@ __global__ __launch_bounds__(256) void count_kernel(const uint8_t *__restrict__ 
     const uint64_t o_hi = offsets[ic];
     const uint64_t o_lo = offsets[ic ? ic - 1 : 0];
     const uint64_t b1 = offsets[ic < n ? ic + 1 : n];
+    const double rcp = 1.0 / (double)win;
+    const uint32_t wf = (uint32_t)div_win(offsets[b0 < n ? b0 : n], win, rcp), gf = wf / WGROUP;   // the block's first window / group
     uint32_t d[6];
     if (i < n) head24(blob, o_hi, b1, d);
     if (i <= n) {
         // first_val[w] = first value whose first byte is at or after w*win (windows past the
         // last value start, and the sentinel nwin, get n)
-        const uint64_t w_lo = i == 0 ? 0 : o_lo / win + 1;
-        const uint64_t w_hi = i == n ? nwin : o_hi / win;
+        const uint64_t w_lo = i == 0 ? 0 : div_win(o_lo, win, rcp) + 1;
+        const uint64_t w_hi = i == n ? nwin : div_win(o_hi, win, rcp);
         for (uint64_t w = w_lo; w <= w_hi && w <= nwin; ++w) first_val[w] = (uint32_t)i;
     }
     uint64_t r = 0;
@@ -496,22 +517,30 @@ __global__ __launch_bounds__(256) void count_kernel(const uint8_t *__restrict__ 
         reserve_classify(blob + o_hi, b1 - o_hi, d, r, c);
         counts[i] = (uint32_t)(r < 0xFFFFFFFFull ? r : 0xFFFFFFFFull);
         cls[i] = (uint8_t)c;
-        w = (uint32_t)(o_hi / win);
+        w = (uint32_t)div_win(o_hi, win, rcp);
     }
     const uint64_t incl = wave_incl_scan_fast(r);
     const uint32_t lane = lane_id(), wp = wave_from_prev(w), wn = wave_from_next(w);
     const bool in = i < n;
-    auto run_sum = [&](uint64_t *t, uint32_t k, bool head, bool tail) __attribute__((always_inline)) {
+    lds_barrier();   // (the tables are zero)
+    // a run's sum into the table slot k (u64 adds wrap: a slot's total is its runs' sum), or
+    // straight to global memory past the table (values longer than a window: rare)
+    auto run_sum = [&](uint64_t *lt, uint32_t nl, uint64_t *t, uint32_t k, uint32_t k0, bool head, bool tail)
+        __attribute__((always_inline)) {
+        uint64_t *dst = k - k0 < nl ? lt + (k - k0) : t + k;
         if (head && tail) {
-            if (r) atomicAdd((unsigned long long *)&t[k], (unsigned long long)r);
+            if (r) atomicAdd((unsigned long long *)dst, (unsigned long long)r);
         } else {
-            if (head && incl != r) atomicAdd((unsigned long long *)&t[k], (unsigned long long)(0ull - (incl - r)));
-            if (tail && incl) atomicAdd((unsigned long long *)&t[k], (unsigned long long)incl);
+            if (head && incl != r) atomicAdd((unsigned long long *)dst, (unsigned long long)(0ull - (incl - r)));
+            if (tail && incl) atomicAdd((unsigned long long *)dst, (unsigned long long)incl);
         }
     };
-    run_sum(wtot, w, in & (lane == 0 || wp != w), in & (lane == RR_WAVE - 1 || wn != w));
+    run_sum(lw, CNT_LW, wtot, w, wf, in & (lane == 0 || wp != w), in & (lane == RR_WAVE - 1 || wn != w));
     const uint32_t g = w / WGROUP;
-    run_sum(gtot, g, in & (lane == 0 || wp / WGROUP != g), in & (lane == RR_WAVE - 1 || wn / WGROUP != g));
+    run_sum(lg, CNT_LG, gtot, g, gf, in & (lane == 0 || wp / WGROUP != g), in & (lane == RR_WAVE - 1 || wn / WGROUP != g));
+    lds_barrier();
+    if (lw[tid]) atomicAdd((unsigned long long *)&wtot[wf + tid], (unsigned long long)lw[tid]);
+    if (tid < CNT_LG && lg[tid]) atomicAdd((unsigned long long *)&gtot[gf + tid], (unsigned long long)lg[tid]);
 }
 
 // ---- exclusive scan of u64 sizes (rr_launch_scan_u64: the snappy kernels' block lengths) ----
@@ -1041,49 +1070,36 @@ __global__ __launch_bounds__(NW * RR_WAVE) __attribute__((amdgpu_waves_per_eu(DE
     const uint64_t A0 = W0 > (offsets[0] & ~15ull) ? W0 : (offsets[0] & ~15ull);
     // the window's own granules [A0, W1) first: their range needs only offsets[0] and
     // offsets[n], not first_val -> offsets, so the loads go out at the window's start; the
-    // stage's tail [W1, ov_e) (the last values' bytes past the window) follows.  The arena gets
+    // stage's tail [W1, ov_te) (the last values' bytes past the window) follows.  The arena gets
     // [A0, W1) (stores past it are dropped); granule A0 / 16 + tid + k * NT is at byte offset
     // 16 (tid + k NT)
     constexpr uint32_t KM = W / 16 / NT;   // granules per thread of a whole window
     static_assert(W % (16 * NT) == 0, "window granules per thread");
     const uint64_t ov_a = A0 >> 4, ov_w1 = W1 >> 4;
     const uint32_t ov_mb = ov_w1 > ov_a ? (uint32_t)((ov_w1 - ov_a) * 16) : 0u;
+    const rsrc_t ov_RM = make_rsrc(blob + A0, ov_mb);
     const rsrc_t ov_RA = make_rsrc(arena + A0, ov_mb);
     // KE granules per thread go out before the first_val -> offsets / class-byte loads, the rest
     // after the class bytes: the sort waits (vmcnt, in issue order) for the class bytes and
     // therefore for the early granules only
     constexpr uint32_t KE = DEC_KE < KM ? DEC_KE : KM;
-    constexpr uint32_t KT = (SLACK / 16 + NT - 1) / NT;   // granules per thread of the stage's tail
-    // KE granules per thread of the window go out first, over the window's range only
     u32x4 ov_m[KM];
-    {
-        const rsrc_t ov_R0 = make_rsrc(blob + A0, ov_mb);
 #pragma unroll
-        for (uint32_t k = 0; k < KE; ++k)
-            ov_m[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ov_R0, (int)((tid + k * NT) * 16), 0, 0));
-    }
+    for (uint32_t k = 0; k < KE; ++k)
+        ov_m[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ov_RM, (int)((tid + k * NT) * 16), 0, 0));
     const uint64_t v_lo = first_val[tile], v_hi = first_val[tile + 1];
-    // The main loads cover W bytes from A0: the window [A0, W1) (win <= W) and, when the call's
-    // window is smaller than W, the start of the stage's tail; the tail loads KT * NT more
-    // granules.  A window is staged when its values' bytes [S0, S1) fit the stage and lie
-    // inside what those loads cover.
-    const uint64_t ov_me = ov_a + (uint64_t)KM * NT, ov_cover = ov_me + (uint64_t)KT * NT;
     uint64_t S0 = W0, S1 = W0;
     if (v_hi > v_lo) {
         S0 = offsets[v_lo] & ~15ull;
         S1 = (offsets[v_hi] + 15) & ~15ull;
     }
-    const bool staged = S1 - S0 <= STAGE && (S1 >> 4) <= ov_cover;
-    // the stage's last granule (exclusive) and the main loads' range: the window, plus the tail's
-    // start when staged (the arena stores stay inside [A0, W1): ov_RA)
-    const uint64_t ov_te = (staged && S1 > W1 ? S1 : W1) >> 4;
-    const uint64_t ov_mend = ov_te < ov_me ? ov_te : ov_me;
-    const rsrc_t ov_RM = make_rsrc(blob + A0, ov_mend > ov_a ? (uint32_t)((ov_mend - ov_a) * 16) : 0u);
-    if (ov_mend > ov_w1 && ov_w1 < ov_a + (uint64_t)KE * NT) {   // (a window under KE * NT granules: the
-#pragma unroll                                                     //  early loads stopped at W1)
-        for (uint32_t k = 0; k < KE; ++k)
-            ov_m[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ov_RM, (int)((tid + k * NT) * 16), 0, 0));
-    }
+    // the stage's tail [W1, S1) comes from KT granules per thread past the window; a window is
+    // staged when its values' bytes [S0, S1) fit the stage and its tail fits those granules (a
+    // call window smaller than W leaves stage room unused: a longer tail walks from global
+    // memory)
+    constexpr uint32_t KT = (SLACK / 16 + NT - 1) / NT;
+    const uint64_t ov_t0 = ov_w1 > ov_a ? ov_w1 : ov_a;
+    const bool staged = S1 - S0 <= STAGE && (S1 >> 4) <= ov_t0 + (uint64_t)KT * NT;
     const uint64_t cap = elem_cap < 0xFFFFFFFFull ? elem_cap : 0xFFFFFFFFull;   // elem_base is 32-bit
 
     // the first chunk's class bytes and reservations, loaded before the rest of the window so
@@ -1093,9 +1109,8 @@ __global__ __launch_bounds__(NW * RR_WAVE) __attribute__((amdgpu_waves_per_eu(DE
 #pragma unroll
     for (uint32_t k = KE; k < KM; ++k)
         ov_m[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ov_RM, (int)((tid + k * NT) * 16), 0, 0));
-    // the rest of the stage's tail [ov_me, ov_te): KT granules per thread, also in flight under
-    // the sort
-    const uint64_t ov_t0 = ov_me;
+    // the stage's tail, also in flight under the sort
+    const uint64_t ov_te = (staged && S1 > W1 ? S1 : W1) >> 4;
     const rsrc_t ov_RT = make_rsrc(blob + ov_t0 * 16, ov_te > ov_t0 ? (uint32_t)((ov_te - ov_t0) * 16) : 0u);
     u32x4 ov_t[KT];
 #pragma unroll
@@ -1124,9 +1139,12 @@ __global__ __launch_bounds__(NW * RR_WAVE) __attribute__((amdgpu_waves_per_eu(DE
         for (uint32_t k = 0; k < KM; ++k) {
             if (RR_ABLATE != 3)
                 __builtin_amdgcn_raw_buffer_store_b128(ov_m[k], ov_RA, (int)((tid + k * NT) * 16), 0, 2 /* nt */);
-            ov_lds[ov_slot(ov_a + tid + (uint64_t)k * NT)] = ov_m[k];
+            // (a window smaller than W: the main loads' granules past W1 read zeros, and the
+            // tail loads bring those stage slots)
+            const uint64_t g = ov_a + tid + (uint64_t)k * NT;
+            ov_lds[g < ov_w1 ? ov_slot(g) : STAGE / 16] = ov_m[k];
         }
-        // the rest of the stage's tail [ov_me, ov_te): LDS only
+        // the stage's tail [W1, ov_te): LDS only
 #pragma unroll
         for (uint32_t k = 0; k < KT; ++k) ov_lds[ov_slot(ov_t0 + tid + (uint64_t)k * NT)] = ov_t[k];
     };
@@ -1305,17 +1323,32 @@ __global__ __launch_bounds__(NW * RR_WAVE) __attribute__((amdgpu_waves_per_eu(DE
 // the pipeline, byte for byte.
 constexpr uint32_t SMALL_NT = 1024, SMALL_VPT = 4, SMALL_N = SMALL_NT * SMALL_VPT;
 constexpr uint32_t SMALL_BYTES = 128 * 1024;   // (one workgroup: up to 160 KiB of LDS)
+constexpr uint32_t SMALL_GW = 32;   // batches of at most this many values: one wave per value, grouped walks
+constexpr uint32_t SMALL_EIN = 16 * 1024;   // encode inputs up to this size staged in LDS
 constexpr uint32_t SMALL_STAGE = SMALL_BYTES + 8192;   // + the reads past a value's end; >= the fixup's LDS
 static_assert(FIX_LDS + 4 * (SMALL_NT + 1) <= SMALL_STAGE, "the fixup reuses the stage");
+
+// The host entry points wait for a one-launch kernel by spinning on a word of their mapped
+// staging instead of a stream synchronisation (~4 us less per call): every thread's writes made
+// visible system-wide, then one lane stores the call's sequence number (a vector store).
+__device__ __forceinline__ void signal_done(uint32_t *done, uint32_t seq) {
+    if (!done) return;
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 __global__ __launch_bounds__(SMALL_NT) void decode_small_kernel(const uint8_t *__restrict__ blob,
                                                                 const uint64_t *__restrict__ offsets, uint64_t n,
                                                                 rr_value *__restrict__ values,
                                                                 rr_elem *__restrict__ elems, uint64_t elem_cap,
-                                                                uint8_t *__restrict__ arena, rr_totals *tot) {
+                                                                uint8_t *__restrict__ arena, rr_totals *tot,
+                                                                uint32_t *done, uint32_t seq) {
     __shared__ __attribute__((aligned(16))) uint8_t stage[SMALL_STAGE];
     __shared__ uint64_t wsum[SMALL_NT / RR_WAVE], red[2][SMALL_NT / RR_WAVE];
     __shared__ uint32_t nfix;
+    __shared__ uint64_t s_off[SMALL_GW + 1], s_eb[SMALL_GW], s_r[SMALL_GW];
+    __shared__ uint32_t s_cls[SMALL_GW];
     const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid / RR_WAVE;
     if (tid == 0) nfix = 0;
     if (tid < 4) reinterpret_cast<uint64_t *>(tot)[tid] = 0;   // (the fixup adds into them)
@@ -1337,33 +1370,68 @@ __global__ __launch_bounds__(SMALL_NT) void decode_small_kernel(const uint8_t *_
     }
     __syncthreads();
     const lds_cptr S = (lds_cptr)stage;
-    // 2. reservations from the headers (count_kernel's rule) and their block scan
+    // 2. reservations and walk classes from the headers (count_kernel's rule) and their block scan
     uint64_t r[SMALL_VPT], sum = 0;
+    uint32_t cl[SMALL_VPT];
 #pragma unroll
     for (uint32_t j = 0; j < SMALL_VPT; ++j) {
         r[j] = 0;
+        cl[j] = C_EXACT;
         if (v0 + j < n) {
             const uint32_t q = (uint32_t)(o[j] - B0);
             uint32_t d[6];
             LdsSrc{S}.get<6>(q, d);   // (reads up to 28 bytes past q: inside the stage's slack)
-            uint32_t c;
-            reserve_classify(S + q, o[j + 1] - o[j], d, r[j], c);
+            reserve_classify(S + q, o[j + 1] - o[j], d, r[j], cl[j]);
         }
         sum += r[j];
     }
     uint64_t total;
     uint64_t eb = block_excl_scan<SMALL_NT>(sum, wsum, total);
-    // 3. the exact parser per value, from the stage
     const uint64_t cap = elem_cap < 0xFFFFFFFFull ? elem_cap : 0xFFFFFFFFull;   // elem_base is 32-bit
     uint64_t bad = 0, pay = 0;
-#pragma unroll 1
-    for (uint32_t j = 0; j < SMALL_VPT; ++j) {
-        if (v0 + j < n) {
-            const Acc a = exact_value(S, B0, v0 + j, offsets, eb, r[j], values, elems, cap, &nfix);
+    if (n <= SMALL_GW) {
+        // 3a. a few values (the per-key calls): one wave per value, the value's class walk on
+        //     all the lanes the batch loop would give a lone value (rr_decode_class.h), its
+        //     offsets from LDS; the exact parser for the EXACT class and for values a walk rejects
+        if (v0 <= n) {
+#pragma unroll
+            for (uint32_t j = 0; j <= SMALL_VPT; ++j)
+                if (v0 + j <= n) s_off[v0 + j] = o[j];
+#pragma unroll
+            for (uint32_t j = 0; j < SMALL_VPT; ++j)
+                if (v0 + j < n) { s_cls[v0 + j] = cl[j]; s_eb[v0 + j] = eb; s_r[v0 + j] = r[j]; eb += r[j]; }
+        }
+        __syncthreads();
+        const LdsSrc lsrc{S};
+        for (uint32_t v = wave; v < n; v += SMALL_NT / RR_WAVE) {
+            const uint32_t c = s_cls[v];
+            const uint64_t ev = s_eb[v], rv = s_r[v];
+            Acc a{0, 0};
+            if (c == C_EXACT) {
+                if (lane == 0) a = exact_value(S, B0, v, s_off, ev, rv, values, elems, cap, &nfix);
+            } else {
+                const bool grouped = c == C_LIST || c == C_SL || c == C_IS || c == C_ZL;
+                const bool htg = (c == C_HT || c == C_HH) && GMAX >= ht_group_min(c == C_HH);
+                const uint32_t G = grouped || htg ? GMAX : 1u;
+                const rsrc_t E = make_rsrc(reinterpret_cast<const uint8_t *>(elems + ev),
+                                           ev < cap ? (uint32_t)((cap - ev < rv ? cap - ev : rv) * 16) : 0u);
+                a = run_batch(lsrc, c, lane < G, v, G, lane & (G - 1), B0, E, ev, blob, s_off, ev, rv, values, elems, cap,
+                              &nfix);
+            }
             bad += a.bad;
             pay += a.pay;
         }
-        eb += r[j];
+    } else {
+        // 3b. the exact parser per value, from the stage
+#pragma unroll 1
+        for (uint32_t j = 0; j < SMALL_VPT; ++j) {
+            if (v0 + j < n) {
+                const Acc a = exact_value(S, B0, v0 + j, offsets, eb, r[j], values, elems, cap, &nfix);
+                bad += a.bad;
+                pay += a.pay;
+            }
+            eb += r[j];
+        }
     }
     bad = wave_sum_fast(bad);
     pay = wave_sum_fast(pay);
@@ -1379,6 +1447,7 @@ __global__ __launch_bounds__(SMALL_NT) void decode_small_kernel(const uint8_t *_
         tot->n_elems = total;
         tot->bytes = offsets[n];
     }
+    signal_done(done, seq);
 }
 
 // ---------------------------------------------------------------------------------------- encode
@@ -2324,10 +2393,45 @@ __global__ __launch_bounds__(SMALL_NT) void encode_small_kernel(const rr_value *
                                                                 const rr_elem *__restrict__ elems, uint64_t ecap,
                                                                 const uint8_t *__restrict__ arena, uint64_t acap,
                                                                 uint64_t n, uint8_t *__restrict__ out, uint64_t cap,
-                                                                uint64_t *__restrict__ offsets, rr_totals *tot) {
+                                                                uint64_t *__restrict__ offsets, rr_totals *tot,
+                                                                uint32_t *done, uint32_t seq) {
     __shared__ __attribute__((aligned(16))) uint8_t img[SMALL_BYTES + 16];
     __shared__ uint64_t wsum[SMALL_NT / RR_WAVE], red[3][SMALL_NT / RR_WAVE];
+    __shared__ u32x4 ein[SMALL_EIN / 16];
     const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid / RR_WAVE;
+    // The inputs into LDS first when they fit SMALL_EIN (the per-key calls): one 16-byte load per
+    // thread, all in flight, instead of the emission's dependent loads — over PCIe when the inputs
+    // are the host entry point's mapped staging.  (Nothing read past the arena's end.)
+    {
+        static_assert(SMALL_EIN / 16 <= SMALL_NT, "one granule per thread");
+        const uint64_t gv = n, ge = ecap, ga = (acap + 15) / 16;
+        if ((gv + ge + ga) * 16 <= SMALL_EIN && ((uintptr_t)values & 15) == 0 && ((uintptr_t)elems & 15) == 0 &&
+            ((uintptr_t)arena & 15) == 0) {   // (uniform)
+            const uint64_t g = tid;
+            if (g < gv + ge + ga) {
+                u32x4 x;
+                if (g < gv) {
+                    x = reinterpret_cast<const u32x4 *>(values)[g];
+                } else if (g < gv + ge) {
+                    x = reinterpret_cast<const u32x4 *>(elems)[g - gv];
+                } else {
+                    const uint64_t k = g - gv - ge;
+                    if (16 * k + 16 <= acap) {
+                        x = reinterpret_cast<const u32x4 *>(arena)[k];
+                    } else {   // the last, partial granule
+                        uint8_t b[16] = {};
+                        for (uint32_t i = 0; i < acap - 16 * k; ++i) b[i] = arena[16 * k + i];
+                        __builtin_memcpy(&x, b, 16);
+                    }
+                }
+                ein[g] = x;
+            }
+            values = reinterpret_cast<const rr_value *>(ein);
+            elems = reinterpret_cast<const rr_elem *>(ein + gv);
+            arena = reinterpret_cast<const uint8_t *>(ein + gv + ge);
+            __syncthreads();
+        }
+    }
     const uint64_t v0 = (uint64_t)tid * SMALL_VPT;
     uint4 x[SMALL_VPT];
     uint64_t sz[SMALL_VPT], pv[SMALL_VPT], sum = 0, bad = 0, pay = 0, nel = 0;
@@ -2381,6 +2485,7 @@ __global__ __launch_bounds__(SMALL_NT) void encode_small_kernel(const rr_value *
         tot->n_elems = tn;
         tot->bytes = total;
     }
+    signal_done(done, seq);
 }
 
 }  // namespace
@@ -2388,9 +2493,9 @@ __global__ __launch_bounds__(SMALL_NT) void encode_small_kernel(const rr_value *
 extern "C" int rr_small_decode_fits(uint64_t n, uint64_t data_cap) { return n <= SMALL_N && data_cap <= SMALL_BYTES; }
 extern "C" hipError_t rr_launch_decode_small(const uint8_t *blob, const uint64_t *offsets, uint64_t n, rr_value *values,
                                              rr_elem *elems, uint64_t elem_cap, uint8_t *arena, rr_totals *totals,
-                                             hipStream_t stream) {
+                                             uint32_t *done, uint32_t seq, hipStream_t stream) {
     hipLaunchKernelGGL(decode_small_kernel, dim3(1), dim3(SMALL_NT), 0, stream, blob, offsets, n, values, elems, elem_cap,
-                       arena, totals);
+                       arena, totals, done, seq);
     return hipGetLastError();
 }
 
@@ -2438,9 +2543,10 @@ extern "C" hipError_t rr_launch_arena_need(const rr_value *values, uint64_t n, c
 extern "C" int rr_small_encode_fits(uint64_t n, uint64_t data_cap) { return n > 0 && n <= SMALL_N && data_cap <= SMALL_BYTES; }
 extern "C" hipError_t rr_launch_encode_small(const rr_value *values, const rr_elem *elems, uint64_t elem_cap,
                                              const uint8_t *arena, uint64_t arena_cap, uint64_t n, uint8_t *out,
-                                             uint64_t cap, uint64_t *offsets, rr_totals *totals, hipStream_t stream) {
+                                             uint64_t cap, uint64_t *offsets, rr_totals *totals, uint32_t *done,
+                                             uint32_t seq, hipStream_t stream) {
     hipLaunchKernelGGL(encode_small_kernel, dim3(1), dim3(SMALL_NT), 0, stream, values, elems, elem_cap, arena, arena_cap,
-                       n, out, cap, offsets, totals);
+                       n, out, cap, offsets, totals, done, seq);
     return hipGetLastError();
 }
 
@@ -2665,7 +2771,7 @@ extern "C" hipError_t rr_launch_flat_rebase(rr_value *values, uint64_t n, rr_ele
 // Shapes (rr_copy_shape, tools/time_copy.py): U 16-byte loads in flight per lane, NT threads, a
 // workgroup per U * NT * 16 bytes (one pass) or a resident grid striding over the buffer, and
 // nontemporal (aux 2) or default-policy stores.
-template <uint32_t U, uint32_t NT, bool NTS>
+template <uint32_t U, uint32_t NT, bool NTS, bool NTL = false>
 __global__ __launch_bounds__(NT) void copy_kernel(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst,
                                                   uint64_t bytes) {
     constexpr uint64_t TILE = (uint64_t)U * NT * 16;
@@ -2676,22 +2782,26 @@ __global__ __launch_bounds__(NT) void copy_kernel(const uint8_t *__restrict__ sr
         u32x4 x[U];
 #pragma unroll
         for (uint32_t k = 0; k < U; ++k)
-            x[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(RS, (int)((threadIdx.x + k * NT) * 16), 0, 0));
+            x[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(RS, (int)((threadIdx.x + k * NT) * 16), 0,
+                                                                                 NTL ? 2 : 0));
 #pragma unroll
         for (uint32_t k = 0; k < U; ++k)
             __builtin_amdgcn_raw_buffer_store_b128(x[k], RD, (int)((threadIdx.x + k * NT) * 16), 0, NTS ? 2 : 0);
     }
 }
 
-template <uint32_t U, uint32_t NT, bool NTS>
+template <uint32_t U, uint32_t NT, bool NTS, bool NTL = false>
 static hipError_t launch_copy_shape(uint8_t *dst, const uint8_t *src, uint64_t bytes, uint32_t grid, hipStream_t stream) {
     const uint64_t tiles = (bytes + (uint64_t)U * NT * 16 - 1) / ((uint64_t)U * NT * 16);
     if (grid == 0 || grid > tiles) grid = (uint32_t)tiles;
-    hipLaunchKernelGGL((copy_kernel<U, NT, NTS>), dim3(grid), dim3(NT), 0, stream, src, dst, bytes);
+    hipLaunchKernelGGL((copy_kernel<U, NT, NTS, NTL>), dim3(grid), dim3(NT), 0, stream, src, dst, bytes);
     return hipGetLastError();
 }
 
-// shape: 0 = the default below; 1-8 = the alternatives timed by tools/time_copy.py (diagnostics)
+// shape: 0 = the default below; 1-8 = the alternatives timed by tools/time_copy.py (diagnostics).
+// Measured (497 MB, read + write bytes): 4 granules per thread with nontemporal loads and stores
+// 6.36 TB/s, 1 per thread 6.30, nontemporal stores only 5.85-5.89 (2 or 4 per thread), 8 per
+// thread (round 3's) 5.56, a resident-size grid 5.72.
 extern "C" hipError_t rr_launch_copy_shape(uint8_t *dst, const uint8_t *src, uint64_t bytes, int shape,
                                            hipStream_t stream) {
     if (bytes == 0) return hipSuccess;
@@ -2699,15 +2809,15 @@ extern "C" hipError_t rr_launch_copy_shape(uint8_t *dst, const uint8_t *src, uin
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     switch (shape) {
-        case 1: return launch_copy_shape<16, 256, true>(dst, src, bytes, 0, stream);
+        case 1: return launch_copy_shape<8, 256, true>(dst, src, bytes, 0, stream);   // (round 3's)
         case 2: return launch_copy_shape<4, 256, true>(dst, src, bytes, 0, stream);
-        case 3: return launch_copy_shape<8, 256, false>(dst, src, bytes, 0, stream);
-        case 4: return launch_copy_shape<8, 256, true>(dst, src, bytes, (uint32_t)cus * 8, stream);
-        case 5: return launch_copy_shape<8, 512, true>(dst, src, bytes, 0, stream);
-        case 6: return launch_copy_shape<16, 256, true>(dst, src, bytes, (uint32_t)cus * 4, stream);
+        case 3: return launch_copy_shape<2, 256, true>(dst, src, bytes, 0, stream);
+        case 4: return launch_copy_shape<1, 256, true>(dst, src, bytes, 0, stream);
+        case 5: return launch_copy_shape<4, 256, true, true>(dst, src, bytes, 0, stream);
+        case 6: return launch_copy_shape<2, 512, true>(dst, src, bytes, 0, stream);
         case 7: return launch_copy_shape<4, 1024, true>(dst, src, bytes, 0, stream);
-        case 8: return launch_copy_shape<8, 256, false>(dst, src, bytes, (uint32_t)cus * 8, stream);
-        default: return launch_copy_shape<8, 256, true>(dst, src, bytes, 0, stream);
+        case 8: return launch_copy_shape<4, 256, true>(dst, src, bytes, (uint32_t)cus * 16, stream);
+        default: return launch_copy_shape<4, 256, true, true>(dst, src, bytes, 0, stream);   // (= 5: 6.36 TB/s)
     }
 }
 

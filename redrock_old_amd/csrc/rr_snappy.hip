@@ -118,6 +118,18 @@ struct Win {
 
 __device__ __forceinline__ void wait_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
+// wave64 inclusive scan (u32) in DPP: row shifts within each 16-lane row, then the rows' last
+// lanes carried up by row_bcast:15 / row_bcast:31 (as rr_device.h's wave_incl_scan_u32)
+__device__ __forceinline__ uint32_t scan_u32(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);
+    return x;
+}
+
 // lane mod off for off <= 64: (lane + 0.5) / off is at least 1 / 129 away from an integer, far
 // beyond v_rcp_f32's error, so the truncated product is the exact quotient
 __device__ __forceinline__ uint32_t lane_mod(uint32_t lane, uint32_t off) {
@@ -156,10 +168,17 @@ __device__ __forceinline__ Tag decode_tag(uint64_t t) {
 
 // A block whose output fits the LDS window, decompressed in place: the compressed bytes staged
 // at the window's end with every load in flight (one round trip), the output assembled from the
-// window's start, every later read from LDS.  Each tag's writes stay below the compressed bytes
-// not yet read — a literal's destination at least 8 bytes below its source, a back-reference's
-// end below the next tag — else the block bails out (*bail) to the global path.  The next tag's
-// bytes are read before the current tag's copy, so the parse overlaps the copies.
+// window's start, every later read from LDS.  Two phases per batch of up to 64 tags:
+//   A. the tag chain, serially and lean: each tag's size from its first bytes (one LDS read and a
+//      dozen scalar instructions), its start written into lane k of a VGPR;
+//   B. the batch's 64 tags decoded at once, one per lane (VALU), their output positions by a
+//      wave scan, every check of the serial decoder per lane (the first failing tag's verdict is
+//      the block's); then the literals copied, then the back-references in stream order (a
+//      back-reference reads only output before its own position: earlier literals and earlier
+//      back-references).
+// Each tag's writes stay below the compressed bytes not yet read — a literal's destination at
+// least 8 bytes below its source, a back-reference's end below the next tag — else the block
+// bails out (*bail) to the global path.
 //   R: the block's dwords from its 4-aligned base, s0 + clen bytes (s0: the block's first byte);
 //   returns the status (RR_SNAPPY_*) with the output in win[0, expected).
 __device__ uint32_t dec_block_lds(rsrc_t R, uint32_t s0, uint32_t clen, uint32_t expected, lds_u8 *win, uint32_t wcap,
@@ -178,76 +197,115 @@ __device__ uint32_t dec_block_lds(rsrc_t R, uint32_t s0, uint32_t clen, uint32_t
         for (uint32_t j = 0; j < SG; ++j)
             if (lane + WAVE * j < ng) d4[lane + WAVE * j] = g[j];
     }
-    // the two dwords holding 8 bytes at LDS address a (uniform), read into VGPRs; taken into
-    // SGPRs (and shifted) only where they are used, so the read's latency can hide under
-    // whatever comes between
-    struct Rd {
-        uint32_t lo, hi, sh;
-    };
-    auto rd = [&](uint32_t a) __attribute__((always_inline)) -> Rd {
-        return Rd{win32[a >> 2], win32[(a >> 2) + 1], 8 * (a & 3)};
-    };
-    auto take = [](const Rd &r) __attribute__((always_inline)) -> uint64_t {
-        const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)r.lo);
-        const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)r.hi);
-        return (((uint64_t)hi << 32) | lo) >> r.sh;
+    // 8 bytes at LDS address a (uniform; two dwords, in SGPRs)
+    auto rd8 = [&](uint32_t a) __attribute__((always_inline)) -> uint64_t {
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)win32[a >> 2]);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)win32[(a >> 2) + 1]);
+        return (((uint64_t)hi << 32) | lo) >> (8 * (a & 3));
     };
     uint32_t p = s0;
-    uint64_t t = take(rd(D + p));
-    while (t & 0x80) { ++p; t >>= 8; }   // the preamble (validated by snz_len_kernel: <= 5 bytes)
-    ++p;
-    Rd tr = rd(D + p);
+    {
+        uint64_t t = rd8(D + p);
+        while (t & 0x80) { ++p; t >>= 8; }   // the preamble (validated by snz_len_kernel: <= 5 bytes)
+        ++p;
+    }
     uint32_t pos = 0;
     while (p < end) {
-        const Tag g = decode_tag(take(tr));
-        if (p + g.hdr > end) return RR_SNAPPY_E_TRUNC;
-        const uint32_t q = p + g.hdr;   // the literal's bytes / the next tag
-        uint32_t pn = q;
-        if (g.lit) {
-            if (g.len == 0 || g.len > end - q) return RR_SNAPPY_E_TRUNC;
-            if (g.len > expected - pos) return RR_SNAPPY_E_OVERFLOW;
-            pn = q + g.len;
-            if (D + q < pos + 8) { bail = true; return RR_SNAPPY_OK; }
-        } else {
-            if (g.off == 0 || g.off > pos) return RR_SNAPPY_E_OFFSET;
-            if (g.len > expected - pos) return RR_SNAPPY_E_OVERFLOW;
-            if (pos + g.len > D + pn) { bail = true; return RR_SNAPPY_OK; }
+        // A. up to 64 tag starts
+        uint32_t tp = 0, nt = 0;
+        do {
+            const uint64_t t = rd8(D + p);
+            const uint32_t c = (uint32_t)t & 0xFF, ty = c & 3, c6 = (c >> 2) + 1;
+            uint32_t sz;
+            if (ty == 0) {
+                const uint32_t nb = c6 > 60 ? c6 - 60 : 0u;
+                const uint64_t len = nb ? ((t >> 8) & ((1ull << (8 * nb)) - 1)) + 1 : c6;
+                sz = len > end - p ? end - p + 1 : (uint32_t)(1 + nb + len);   // (past the end: phase B's TRUNC)
+            } else {
+                sz = ty == 1 ? 2u : ty == 2 ? 3u : 5u;
+            }
+            tp = lane == nt ? p : tp;
+            ++nt;
+            p += sz;
+        } while (nt < WAVE && p < end);
+        // B. the batch's tags, one per lane
+        const bool act = lane < nt;
+        const uint32_t a = D + (act ? tp : 0);
+        const uint32_t lo = win32[a >> 2], hi = win32[(a >> 2) + 1], sh = a & 3;
+        const uint32_t b0 = __builtin_amdgcn_alignbyte(hi, lo, sh);
+        const uint32_t v = sh == 3 ? hi : __builtin_amdgcn_alignbyte(hi, lo, sh + 1);   // the 4 bytes after the tag byte
+        const uint32_t c = b0 & 0xFF, ty = c & 3, c6 = (c >> 2) + 1;
+        const bool lit = ty == 0;
+        const uint32_t nb = lit ? (c6 > 60 ? c6 - 60 : 0u) : ty == 3 ? 4u : ty;
+        const uint32_t vv = nb >= 4 ? v : v & ((1u << (8 * nb)) - 1);
+        const uint32_t len = lit ? (nb ? vv + 1 : c6) : ty == 1 ? 4 + ((c >> 2) & 7) : c6;   // (0: 2^32 wrapped)
+        const uint32_t off = ty == 1 ? ((c >> 5) << 8) | vv : vv;
+        const uint32_t tq = tp + 1 + nb;   // the literal's bytes / the next tag
+        const uint32_t tpn = lit ? tq + len : tq;
+        // output positions: the exclusive scan of the lengths (each clamped past `expected`: a
+        // longer one fails its check whatever the scan says)
+        const uint32_t ol = act ? (len < expected + 1 ? len : expected + 1) : 0u;
+        const uint32_t tpos = pos + scan_u32(ol) - ol;
+        // the serial decoder's checks, in its order (0 = none, 4 = bail out)
+        uint32_t code = 0;
+        if (act) {
+            if (tq > end) code = RR_SNAPPY_E_TRUNC;
+            else if (lit) code = len == 0 || len > end - tq ? RR_SNAPPY_E_TRUNC : len > expected - tpos ? RR_SNAPPY_E_OVERFLOW
+                                 : D + tq < tpos + 8 ? 0xFFu : 0u;
+            else code = off == 0 || off > tpos ? RR_SNAPPY_E_OFFSET : len > expected - tpos ? RR_SNAPPY_E_OVERFLOW
+                        : tpos + len > D + tpn ? 0xFFu : 0u;
         }
-        tr = rd(D + pn);   // the next tag, read under this one's copy
-        if (g.lit) {
-            const uint32_t src = D + q;
-            if (g.len <= WAVE) {
-                const uint8_t x = lane < g.len ? win[src + lane] : 0;
-                if (lane < g.len) win[pos + lane] = x;
+        const uint64_t badm = __ballot(code != 0);
+        if (badm) {
+            const uint32_t f = (uint32_t)__builtin_amdgcn_readlane((int)code, (int)__builtin_ctzll(badm));
+            if (f == 0xFFu) bail = true;
+            return f == 0xFFu ? RR_SNAPPY_OK : f;
+        }
+        // the literals
+        uint64_t m = __ballot(act && lit);
+        while (m) {
+            const int k = (int)__builtin_ctzll(m);
+            m &= m - 1;
+            const uint32_t dpos = (uint32_t)__builtin_amdgcn_readlane((int)tpos, k);
+            const uint32_t src = D + (uint32_t)__builtin_amdgcn_readlane((int)tq, k);
+            const uint32_t l = (uint32_t)__builtin_amdgcn_readlane((int)len, k);
+            if (l <= WAVE) {
+                const uint8_t x = lane < l ? win[src + lane] : 0;
+                if (lane < l) win[dpos + lane] = x;
             } else {
                 // bytes to a 4-aligned destination, then 16 bytes per lane from five aligned
                 // source dwords (the last dword may spill up to 3 bytes past the literal, below
-                // the source: overwritten by the next element before anything reads them)
-                const uint32_t h = (4u - (pos & 3)) & 3;
+                // its source: overwritten by a later element before anything reads them)
+                const uint32_t h = (4u - (dpos & 3)) & 3;
                 {
                     const uint8_t x = lane < h ? win[src + lane] : 0;
-                    if (lane < h) win[pos + lane] = x;
+                    if (lane < h) win[dpos + lane] = x;
                 }
-                const uint32_t d0 = pos + h, q0 = src + h, body = g.len - h, a0 = q0 & ~3u, sh = q0 & 3;
+                const uint32_t d0 = dpos + h, q0 = src + h, body = l - h, a0 = q0 & ~3u, s3 = q0 & 3;
                 for (uint32_t i = 0; i < body; i += 16 * WAVE) {
-                    const uint32_t k = i + 16 * lane, s = k < body ? (a0 + k) >> 2 : 0u;   // (idle lanes: word 0)
-                    const uint32_t x0 = win32[s], x1 = win32[s + 1], x2 = win32[s + 2], x3 = win32[s + 3], x4 = win32[s + 4];
-                    lds_u32 *w = win32 + ((d0 + k) >> 2);
-                    if (k < body) w[0] = __builtin_amdgcn_alignbyte(x1, x0, sh);
-                    if (k + 4 < body) w[1] = __builtin_amdgcn_alignbyte(x2, x1, sh);
-                    if (k + 8 < body) w[2] = __builtin_amdgcn_alignbyte(x3, x2, sh);
-                    if (k + 12 < body) w[3] = __builtin_amdgcn_alignbyte(x4, x3, sh);
+                    const uint32_t k4 = i + 16 * lane, sa = k4 < body ? (a0 + k4) >> 2 : 0u;   // (idle lanes: word 0)
+                    const uint32_t x0 = win32[sa], x1 = win32[sa + 1], x2 = win32[sa + 2], x3 = win32[sa + 3], x4 = win32[sa + 4];
+                    lds_u32 *w = win32 + ((d0 + k4) >> 2);
+                    if (k4 < body) w[0] = __builtin_amdgcn_alignbyte(x1, x0, s3);
+                    if (k4 + 4 < body) w[1] = __builtin_amdgcn_alignbyte(x2, x1, s3);
+                    if (k4 + 8 < body) w[2] = __builtin_amdgcn_alignbyte(x3, x2, s3);
+                    if (k4 + 12 < body) w[3] = __builtin_amdgcn_alignbyte(x4, x3, s3);
                 }
             }
-        } else {
-            // out[pos + j] = out[pos - off + j % off]: every source byte already written
-            uint32_t j = lane;
-            if (g.off < g.len) j = lane_mod(lane, g.off);
-            const uint8_t x = lane < g.len ? win[pos - g.off + j] : 0;
-            if (lane < g.len) win[pos + lane] = x;
         }
-        pos += g.len;
-        p = pn;
+        // the back-references, in stream order: out[pos + j] = out[pos - off + j % off]
+        m = __ballot(act && !lit);
+        while (m) {
+            const int k = (int)__builtin_ctzll(m);
+            m &= m - 1;
+            const uint32_t dpos = (uint32_t)__builtin_amdgcn_readlane((int)tpos, k);
+            const uint32_t o = (uint32_t)__builtin_amdgcn_readlane((int)off, k);
+            const uint32_t l = (uint32_t)__builtin_amdgcn_readlane((int)len, k);
+            const uint32_t j = o < l ? lane_mod(lane, o) : lane;
+            const uint8_t x = lane < l ? win[dpos - o + j] : 0;
+            if (lane < l) win[dpos + lane] = x;
+        }
+        pos = (uint32_t)__builtin_amdgcn_readlane((int)(tpos + ol), (int)(nt - 1));
     }
     return pos == expected ? RR_SNAPPY_OK : RR_SNAPPY_E_LENGTH;
 }

@@ -34,10 +34,11 @@ for c in ("FETCH_SIZE", "WRITE_SIZE"):
             disp[k].add(r["Dispatch_Id"])
         for k in acc:
             per[k][c] = acc[k] / len(disp[k]) * 1024   # KB -> bytes, per dispatch
+# (each pipeline also runs one hipMemsetAsync of its window / group sums: a few KB, not counted)
 if "enc_emit_kernel" in per:   # RR_PROFILE=encode run (one decode call precedes the encode steps)
-    pipeline = ("enc_size_kernel", "scan_kernel", "enc_index_kernel", "enc_emit_kernel", "finalize_kernel")
+    pipeline = ("enc_size_kernel", "enc_index_kernel", "enc_emit_kernel")
 else:
-    pipeline = ("count_kernel", "scan_kernel", "decode_kernel", "decode_post_kernel")
+    pipeline = ("count_kernel", "decode_kernel")
 res["pipeline"] = list(pipeline)
 tot = 0.0
 for k in pipeline:
