@@ -152,7 +152,7 @@ int rr_decode_batch(rr_ctx *c, const rr_blob_batch *in, rr_flat_batch *out, rr_t
     if (SMALL_DEC(c, in->n, in->data_cap)) {   /* one launch, no scratch */
         HIPCHK(hipSetDevice(c->device));
         HIPCHK(rr_launch_decode_small(in->data, in->offsets, in->n, out->values, out->elems, out->elem_cap, out->arena,
-                                      d_totals, NULL, 0, (hipStream_t)stream));
+                                      in->data_cap, d_totals, NULL, 0, (hipStream_t)stream));
         return RR_API_OK;
     }
     int rc = ensure_scratch(c, rr_decode_scratch_words(in->data_cap, in->n), (hipStream_t)stream);
@@ -385,7 +385,7 @@ static int decode_host_small(rr_ctx *c, const uint8_t *data, const uint64_t *off
     if (!seq) seq = ++c->small_seq;   /* (0 is the cleared word) */
     __atomic_store_n((uint32_t *)(h + o_flag), 0u, __ATOMIC_RELAXED);
     HIPCHK(rr_launch_decode_small(d + o_dat, (const uint64_t *)(d + o_off), n, (rr_value *)(d + o_val),
-                                  (rr_elem *)(d + o_el), elem_cap, NULL, (rr_totals *)(d + o_tot),
+                                  (rr_elem *)(d + o_el), elem_cap, NULL, AL16(bytes), (rr_totals *)(d + o_tot),
                                   (uint32_t *)(d + o_flag), seq, c->stream));
     rc = small_wait(c, (const uint32_t *)(h + o_flag), seq);
     if (rc) return rc;

@@ -49,8 +49,8 @@ hipError_t rr_launch_arena_need(const rr_value *values, uint64_t n, const rr_ele
 int rr_small_decode_fits(uint64_t n, uint64_t data_cap);
 int rr_small_encode_fits(uint64_t n, uint64_t data_cap);
 hipError_t rr_launch_decode_small(const uint8_t *blob, const uint64_t *offsets, uint64_t n, rr_value *values,
-                                  rr_elem *elems, uint64_t elem_cap, uint8_t *arena, rr_totals *totals, uint32_t *done,
-                                  uint32_t seq, hipStream_t stream);
+                                  rr_elem *elems, uint64_t elem_cap, uint8_t *arena, uint64_t data_cap, rr_totals *totals,
+                                  uint32_t *done, uint32_t seq, hipStream_t stream);
 hipError_t rr_launch_encode_small(const rr_value *values, const rr_elem *elems, uint64_t elem_cap, const uint8_t *arena,
                                   uint64_t arena_cap, uint64_t n, uint8_t *out, uint64_t cap, uint64_t *offsets,
                                   rr_totals *totals, uint32_t *done, uint32_t seq, hipStream_t stream);

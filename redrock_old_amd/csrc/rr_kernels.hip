@@ -1342,31 +1342,46 @@ __global__ __launch_bounds__(SMALL_NT) void decode_small_kernel(const uint8_t *_
                                                                 const uint64_t *__restrict__ offsets, uint64_t n,
                                                                 rr_value *__restrict__ values,
                                                                 rr_elem *__restrict__ elems, uint64_t elem_cap,
-                                                                uint8_t *__restrict__ arena, rr_totals *tot,
-                                                                uint32_t *done, uint32_t seq) {
+                                                                uint8_t *__restrict__ arena, uint64_t data_cap,
+                                                                rr_totals *tot, uint32_t *done, uint32_t seq) {
     __shared__ __attribute__((aligned(16))) uint8_t stage[SMALL_STAGE];
     __shared__ uint64_t wsum[SMALL_NT / RR_WAVE], red[2][SMALL_NT / RR_WAVE];
     __shared__ uint32_t nfix;
     __shared__ uint64_t s_off[SMALL_GW + 1], s_eb[SMALL_GW], s_r[SMALL_GW];
     __shared__ uint32_t s_cls[SMALL_GW];
+    __shared__ rr_totals s_tot;   // (the fixup's adjustments; the call's totals are stored once, at the end)
     const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid / RR_WAVE;
     if (tid == 0) nfix = 0;
-    if (tid < 4) reinterpret_cast<uint64_t *>(tot)[tid] = 0;   // (the fixup adds into them)
-    const uint64_t B0 = offsets[0] & ~15ull, B1 = (offsets[n] + 15) & ~15ull;
+    if (tid < 4) reinterpret_cast<uint64_t *>(&s_tot)[tid] = 0;
+    // 1. the whole buffer [0, data_cap) into the stage, 16-byte granules, every load in flight
+    //    beside the offsets loads (no wait for offsets[0] / offsets[n] first: the inputs may be
+    //    the host entry point's mapped staging, a PCIe round trip each); the mirror arena gets
+    //    [offsets[0], offsets[n]) rounded to granules, as the pipeline's window copy
+    constexpr uint64_t B0 = 0;
+    const uint32_t ng = (uint32_t)(data_cap >> 4);
+    const u32x4 *src4 = reinterpret_cast<const u32x4 *>(blob);
+    constexpr uint32_t SG = SMALL_BYTES / 16 / SMALL_NT;
+    u32x4 gx[SG];
+#pragma unroll
+    for (uint32_t k = 0; k < SG; ++k) {
+        const uint32_t g = tid + k * SMALL_NT;
+        gx[k] = g < ng ? src4[g] : u32x4{0u, 0u, 0u, 0u};
+    }
     // my values: v0 .. v0 + SMALL_VPT - 1 (consecutive: the block scan runs in value order)
     const uint64_t v0 = (uint64_t)tid * SMALL_VPT;
     uint64_t o[SMALL_VPT + 1];
 #pragma unroll
     for (uint32_t j = 0; j <= SMALL_VPT; ++j) o[j] = offsets[v0 + j < n ? v0 + j : n];
-    // 1. the bytes into the stage (and the mirror arena), 16-byte granules, every load in flight
+    const uint64_t on = offsets[n], a0 = offsets[0] >> 4, a1 = (on + 15) >> 4;   // (uniform)
     typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
     lds_u32x4 *st4 = (lds_u32x4 *)(__attribute__((address_space(3))) uint8_t *)stage;
-    const uint32_t ng = (uint32_t)((B1 - B0) >> 4);
-    const u32x4 *src4 = reinterpret_cast<const u32x4 *>(blob + B0);
-    for (uint32_t g = tid; g < ng; g += SMALL_NT) {
-        const u32x4 x = src4[g];
-        st4[g] = x;
-        if (arena) reinterpret_cast<u32x4 *>(arena + B0)[g] = x;
+#pragma unroll
+    for (uint32_t k = 0; k < SG; ++k) {
+        const uint32_t g = tid + k * SMALL_NT;
+        if (g < ng) {
+            st4[g] = gx[k];
+            if (arena && g >= a0 && g < a1) reinterpret_cast<u32x4 *>(arena)[g] = gx[k];
+        }
     }
     __syncthreads();
     const lds_cptr S = (lds_cptr)stage;
@@ -1438,14 +1453,14 @@ __global__ __launch_bounds__(SMALL_NT) void decode_small_kernel(const uint8_t *_
     if (lane == 0) { red[0][wave] = bad; red[1][wave] = pay; }
     __syncthreads();   // (also: every record and descriptor visible to the workgroup, for the fixup)
     // 4. marked values (duplicate keys, unsorted skiplists), in the stage's LDS
-    if (nfix) fixup_window<SMALL_NT>(blob, 0, n, values, elems, tot, stage);
+    if (nfix) fixup_window<SMALL_NT>(blob, 0, n, values, elems, &s_tot, stage);
     if (tid == 0) {
         uint64_t tb = 0, tp = 0;
         for (uint32_t w = 0; w < SMALL_NT / RR_WAVE; ++w) { tb += red[0][w]; tp += red[1][w]; }
-        atomicAdd((unsigned long long *)&tot->n_bad, (unsigned long long)tb);
-        atomicAdd((unsigned long long *)&tot->payload, (unsigned long long)tp);
+        tot->n_bad = tb + s_tot.n_bad;
+        tot->payload = tp + s_tot.payload;
         tot->n_elems = total;
-        tot->bytes = offsets[n];
+        tot->bytes = on;
     }
     signal_done(done, seq);
 }
@@ -2389,6 +2404,66 @@ __device__ void emit_value_small(uint8_t *img, uint64_t p, const uint4 &x, const
     }
 }
 
+// The same bytes with the whole wave on one value (the per-key calls, n <= SMALL_GW): lane 0
+// writes the header, the elements go one per lane — sizes, a wave scan for their offsets, each
+// lane its element's fields and payload — and a single string / ziplist payload is copied by
+// all lanes.
+__device__ void emit_value_wave(uint8_t *img, uint64_t p, const uint4 &x, const rr_elem *__restrict__ elems,
+                                const uint8_t *__restrict__ arena) {
+    const uint32_t lane = lane_id();
+    const uint32_t type = x.x & 0xFF, enc = (x.x >> 8) & 0xFF, ne = x.z;
+    const rr_elem *el = elems + x.w;
+    if (lane == 0) img_le(img, p, type | ((uint64_t)(x.y & RR_LRU_MASK) << 8), 5);   // serObjectType + lru
+    p += 5;
+    if (type == RR_TYPE_STRING || type == RR_TYPE_HASH_ZIPLIST || type == RR_TYPE_ZSET_ZIPLIST) {
+        const ElemV e = get_elem(el);
+        const bool str = type == RR_TYPE_STRING;
+        if (lane == 0) {
+            if (str) img[p] = (uint8_t)enc;
+            else img_le(img, p, e.len, 8);
+            if (str && enc == RR_ENC_INT) img_le(img, p + 1, e.data, 8);
+        }
+        if (!(str && enc == RR_ENC_INT)) {
+            const uint64_t q = p + (str ? 1 : 8);
+            for (uint64_t i = lane; i < e.len; i += RR_WAVE) img[q + i] = arena[e.data + i];
+        }
+        return;
+    }
+    const bool list = type == RR_TYPE_LIST_QUICKLIST, is = type == RR_TYPE_SET_INTSET;
+    if (lane == 0 && !list) img_le(img, p, is ? (enc | ((uint64_t)ne << 32)) : type == RR_TYPE_SET_HT ? ne : ne / 2, 8);
+    if (!list) p += 8;
+    for (uint32_t b = 0; b < ne; b += RR_WAVE) {
+        const uint32_t k = b + lane;
+        const bool act = k < ne;
+        const ElemV e = act ? get_elem(el + k) : ElemV{0, 0, 0};
+        // this element's bytes (serList :162-188, serSet :217-245, serHash :332-346, serZset :429-446)
+        uint32_t sz = 0;
+        if (act) {
+            if (list) sz = 4 + (e.kind == RR_K_INT ? sdec_len((int64_t)e.data) : e.len);
+            else if (is) sz = enc;
+            else if (type == RR_TYPE_ZSET_SKIPLIST && (k & 1)) sz = 8;
+            else sz = 8 + e.len;
+        }
+        const uint32_t incl = wave_incl_scan_u32(sz);
+        const uint64_t q = p + incl - sz;
+        if (act) {
+            if (list && e.kind == RR_K_INT) {
+                const uint32_t l = dec_write(img + q + 4, (int64_t)e.data);
+                img_le(img, q, l, 4);
+            } else if (list) {
+                img_le(img, q, e.len, 4);
+                img_copy(img, q + 4, arena + e.data, e.len);
+            } else if (is || (type == RR_TYPE_ZSET_SKIPLIST && (k & 1))) {
+                img_le(img, q, e.data, sz);
+            } else {
+                img_le(img, q, e.len, 8);
+                img_copy(img, q + 8, arena + e.data, e.len);
+            }
+        }
+        p += (uint32_t)__builtin_amdgcn_readlane((int)incl, RR_WAVE - 1);
+    }
+}
+
 __global__ __launch_bounds__(SMALL_NT) void encode_small_kernel(const rr_value *__restrict__ values,
                                                                 const rr_elem *__restrict__ elems, uint64_t ecap,
                                                                 const uint8_t *__restrict__ arena, uint64_t acap,
@@ -2398,6 +2473,7 @@ __global__ __launch_bounds__(SMALL_NT) void encode_small_kernel(const rr_value *
     __shared__ __attribute__((aligned(16))) uint8_t img[SMALL_BYTES + 16];
     __shared__ uint64_t wsum[SMALL_NT / RR_WAVE], red[3][SMALL_NT / RR_WAVE];
     __shared__ u32x4 ein[SMALL_EIN / 16];
+    __shared__ uint64_t s_at[SMALL_GW];   // (the wave path: each value's image offset, ~0 = not written)
     const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid / RR_WAVE;
     // The inputs into LDS first when they fit SMALL_EIN (the per-key calls): one 16-byte load per
     // thread, all in flight, instead of the emission's dependent loads — over PCIe when the inputs
@@ -2454,18 +2530,24 @@ __global__ __launch_bounds__(SMALL_NT) void encode_small_kernel(const rr_value *
     const uint64_t lim = total < cap ? total : cap;   // (cap <= SMALL_BYTES: rr_small_encode_fits)
     for (uint32_t k = tid; k < (SMALL_BYTES + 16) / 16; k += SMALL_NT) reinterpret_cast<uint4 *>(img)[k] = make_uint4(0, 0, 0, 0);
     __syncthreads();
+    const bool wave_path = n <= SMALL_GW;   // (uniform)
 #pragma unroll 1
     for (uint32_t j = 0; j < SMALL_VPT; ++j) {
         if (v0 + j < n) {
             offsets[v0 + j] = a;
             const uint64_t b = a + sz[j];
+            const bool emit = !(b > cap && sz[j]) && sz[j];
             if (b > cap && sz[j]) { bad += 1; }                     // past data_cap: not written (E3)
-            else {
-                pay += pv[j];
-                if (sz[j]) emit_value_small(img, a, x[j], elems, arena);
-            }
+            else pay += pv[j];
+            if (wave_path) s_at[v0 + j] = emit ? a : ~0ull;
+            else if (emit) emit_value_small(img, a, x[j], elems, arena);
             a = b;
         }
+    }
+    if (wave_path) {
+        __syncthreads();
+        for (uint32_t v = wave; v < n; v += SMALL_NT / RR_WAVE)
+            if (s_at[v] != ~0ull) emit_value_wave(img, s_at[v], reinterpret_cast<const uint4 *>(values)[v], elems, arena);
     }
     if (tid == 0) offsets[n] = total;
     bad = wave_sum_fast(bad);
@@ -2492,10 +2574,10 @@ __global__ __launch_bounds__(SMALL_NT) void encode_small_kernel(const rr_value *
 
 extern "C" int rr_small_decode_fits(uint64_t n, uint64_t data_cap) { return n <= SMALL_N && data_cap <= SMALL_BYTES; }
 extern "C" hipError_t rr_launch_decode_small(const uint8_t *blob, const uint64_t *offsets, uint64_t n, rr_value *values,
-                                             rr_elem *elems, uint64_t elem_cap, uint8_t *arena, rr_totals *totals,
-                                             uint32_t *done, uint32_t seq, hipStream_t stream) {
+                                             rr_elem *elems, uint64_t elem_cap, uint8_t *arena, uint64_t data_cap,
+                                             rr_totals *totals, uint32_t *done, uint32_t seq, hipStream_t stream) {
     hipLaunchKernelGGL(decode_small_kernel, dim3(1), dim3(SMALL_NT), 0, stream, blob, offsets, n, values, elems, elem_cap,
-                       arena, totals, done, seq);
+                       arena, data_cap, totals, done, seq);
     return hipGetLastError();
 }
 

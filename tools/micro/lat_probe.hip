@@ -98,7 +98,7 @@ int main() {
     CK(hipMemcpy(doff, o, 16, hipMemcpyHostToDevice));
     for (int i = 0; i < K; ++i) {
         const double t0 = now_us();
-        CK(rr_launch_decode_small(dblob, doff, 1, dval, del, 4096, NULL, dtot, NULL, 0, s));
+        CK(rr_launch_decode_small(dblob, doff, 1, dval, del, 4096, NULL, (len + 15) & ~15ull, dtot, NULL, 0, s));
         CK(hipStreamSynchronize(s));
         t[i] = now_us() - t0;
     }
@@ -109,7 +109,7 @@ int main() {
     // kernel time alone (events)
     for (int i = 0; i < K; ++i) {
         CK(hipEventRecord(e0, s));
-        CK(rr_launch_decode_small(dblob, doff, 1, dval, del, 4096, NULL, dtot, NULL, 0, s));
+        CK(rr_launch_decode_small(dblob, doff, 1, dval, del, 4096, NULL, (len + 15) & ~15ull, dtot, NULL, 0, s));
         CK(hipEventRecord(e1, s));
         CK(hipEventSynchronize(e1));
         float ms;
@@ -147,7 +147,7 @@ int main() {
             CK(hipMemcpy(doff, oo, 16, hipMemcpyHostToDevice));
             for (int i = 0; i < 200; ++i) {
                 CK(hipEventRecord(e0, s));
-                CK(rr_launch_decode_small(dblob, doff, 1, dval, del, 4096, NULL, dtot, NULL, 0, s));
+                CK(rr_launch_decode_small(dblob, doff, 1, dval, del, 4096, NULL, (l + 15) & ~15ull, dtot, NULL, 0, s));
                 CK(hipEventRecord(e1, s));
                 CK(hipEventSynchronize(e1));
                 float ms;
