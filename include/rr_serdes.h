@@ -14,11 +14,11 @@
  *   - return value: RR_API_OK (0) or a negative RR_API_E* code for the whole call;
  *   - per-value status in rr_value.status (0 = OK), counted into rr_totals.n_bad;
  *   - caller-owned buffers; one rr_ctx per host thread; no hidden host synchronisation in the
- *     device entry points (graph-capturable after rr_ctx_reserve: decode = a memset + 2
- *     kernels, encode = a memset + 3 kernels, a batch of at most 4096 values in at most
- *     128 KiB = ONE kernel; all on the caller's stream).  The only wait is when the context's scratch must
- *     grow: it waits for the context's previous call to finish (an event, not a device sync) —
- *     and under graph capture it fails instead.
+ *     device entry points (graph-capturable after rr_ctx_reserve: decode = 3 kernels,
+ *     encode = 4 kernels, a batch of at most 4096 values in at most 128 KiB = ONE kernel; all
+ *     on the caller's stream).  The only wait is when the context's scratch must grow: it
+ *     waits for the context's previous call to finish (an event, not a device sync) — and
+ *     under graph capture it fails instead.
  * Plain C: no HIP or torch types in any signature.  Streams are passed as void* (hipStream_t).
  */
 #ifndef RR_SERDES_H

@@ -1,14 +1,16 @@
 // rr_kernels.hip — CDNA4 (gfx950) decode and encode kernels for RedRock value blobs.
 //
-// Decode (blob batch -> flat batch): memset + count / scan / decode / finalize launches.
-//   count: thread per value, descriptor reservation + walk class; scan: reservations ->
-//   elem_base; decode: workgroup per 64 KiB blob window, streams the window into the MIRROR
-//   arena (every payload lands at its blob offset) and into LDS, sorts the window's values by
-//   class, walks + emits single-class 64-value batches (lane = value).  Details at K1-K4.
-// Encode (flat batch -> blob batch): memset + size / scan / index / emit / finalize launches.
-//   size: thread per value; scan: sizes -> offsets; index: first value of each 16 KiB output
-//   window; emit: workgroup per output window builds the window's bytes in LDS
-//   (element-parallel tasks, aligned stores) and stores it coalesced.  Details at E1-E5.
+// Decode (blob batch -> flat batch): zero + count + decode launches.
+//   count: thread per value, descriptor reservation + walk class, per-window reservation sums;
+//   decode: workgroup per byte window (~72 KiB), its first slot from the sums, streams the
+//   window into the MIRROR arena (every payload lands at its blob offset) and into LDS, sorts
+//   each chunk of its values by class, walks + emits single-class batches.  Details at K1/K3.
+// Encode (flat batch -> blob batch): zero + size + index + emit launches.
+//   size: blob sizes and in-block offsets per 256 values; index: global offsets and the first
+//   value of each 16 KiB output window; emit: workgroup per output window builds the window's
+//   bytes in LDS (element-parallel tasks, aligned stores) and stores it coalesced.  Details at
+//   E1-E4.
+// Small batches (<= 4096 values, <= 128 KiB): one workgroup, one launch each way.
 //
 // No MFMA: this is byte/record work bounded by HBM.
 #include <hip/hip_runtime.h>
@@ -450,7 +452,7 @@ __device__ __forceinline__ void reserve_classify(P b, uint64_t L, const uint32_t
 }
 
 // Block 0 also zeroes the pipeline's per-call words (look-back state, fixup header) and the
-// totals: later kernels of the same stream use them, so no separate memset launch is needed.
+// totals: later kernels of the same stream use them, so no separate launch is needed.
 __device__ __forceinline__ void zero_call_words(uint64_t *words, uint32_t nwords, rr_totals *tot) {
     if (blockIdx.x != 0) return;
     for (uint32_t k = threadIdx.x; k < nwords; k += blockDim.x) words[k] = 0;
@@ -459,7 +461,7 @@ __device__ __forceinline__ void zero_call_words(uint64_t *words, uint32_t nwords
 
 // Per value: its reservation (u32; a value that would need 2^32 slots fails capacity anyway),
 // its class and first_val.  Per window: the reservations of its values summed into wtot[w], and
-// per group of WGROUP windows into gtot[w / WGROUP] (both zeroed by a memset before the launch).
+// per group of WGROUP windows into gtot[w / WGROUP] (both zeroed by zero_kernel before the launch).
 // A window's values are consecutive, so each run of one window (group) in a wave adds its sum
 // with two LDS atomics — the inclusive wave scan at its last lane, minus the exclusive scan at
 // its first — into the workgroup's table of the windows (groups) it touches; the table then
@@ -478,10 +480,16 @@ __device__ __forceinline__ uint64_t div_win(uint64_t o, uint32_t win, double rcp
     return q;
 }
 constexpr uint32_t WGROUP = 16;   // (64: ~260 same-address atomics per group sum on config 1)
+// The call's sums zeroed by one small kernel: hipMemsetAsync of a size that is not a multiple of
+// 16 bytes runs two fill kernels (~4.7 us each in the traces, config 1 at 100K values)
+__global__ __launch_bounds__(1024) void zero_kernel(uint64_t *__restrict__ w, uint64_t nwords) {
+    for (uint64_t k = threadIdx.x; k < nwords; k += 1024) w[k] = 0;
+}
 constexpr uint32_t CNT_NT = 256, CNT_LW = CNT_NT, CNT_LG = 8;   // (a workgroup's values start in <= 256 windows)
 __global__ __launch_bounds__(CNT_NT) void count_kernel(const uint8_t *__restrict__ blob,
                                                        const uint64_t *__restrict__ offsets, uint64_t n,
-                                                       uint32_t *__restrict__ first_val, uint32_t nwin, uint32_t win,
+                                                       uint32_t *__restrict__ first_val, uint64_t *__restrict__ first_off,
+                                                       uint32_t nwin, uint32_t win,
                                                        uint32_t *__restrict__ counts, uint8_t *__restrict__ cls,
                                                        uint64_t *wtot, uint64_t *gtot,
                                                        uint64_t *zero_words, uint32_t nzero, rr_totals *tot) {
@@ -505,10 +513,13 @@ __global__ __launch_bounds__(CNT_NT) void count_kernel(const uint8_t *__restrict
     if (i < n) head24(blob, o_hi, b1, d);
     if (i <= n) {
         // first_val[w] = first value whose first byte is at or after w*win (windows past the
-        // last value start, and the sentinel nwin, get n)
+        // last value start, and the sentinel nwin, get n), first_off[w] = that value's offset
         const uint64_t w_lo = i == 0 ? 0 : div_win(o_lo, win, rcp) + 1;
         const uint64_t w_hi = i == n ? nwin : div_win(o_hi, win, rcp);
-        for (uint64_t w = w_lo; w <= w_hi && w <= nwin; ++w) first_val[w] = (uint32_t)i;
+        for (uint64_t w = w_lo; w <= w_hi && w <= nwin; ++w) {
+            first_val[w] = (uint32_t)i;
+            first_off[w] = o_hi;   // (its first byte: decode_kernel's stage range without an offsets round trip)
+        }
     }
     uint64_t r = 0;
     uint32_t w = 0xFFFFFFFFu;   // (lanes past n: a window no value has)
@@ -1036,7 +1047,8 @@ constexpr int DEC_WPE = 4;
 template <uint32_t W, uint32_t SLACK, uint32_t NW, uint32_t PMAX>
 __global__ __launch_bounds__(NW * RR_WAVE) __attribute__((amdgpu_waves_per_eu(DEC_WPE))) void decode_kernel(
     const uint8_t *__restrict__ blob, uint64_t data_cap, const uint64_t *__restrict__ offsets, uint64_t n,
-    const uint32_t *__restrict__ first_val, const uint8_t *__restrict__ cls, const uint32_t *__restrict__ counts,
+    const uint32_t *__restrict__ first_val, const uint64_t *__restrict__ first_off, const uint8_t *__restrict__ cls,
+    const uint32_t *__restrict__ counts,
     const uint64_t *__restrict__ wtot, const uint64_t *__restrict__ gtot, rr_value *__restrict__ values,
     rr_elem *__restrict__ elems, uint64_t elem_cap, uint8_t *__restrict__ arena, uint32_t nwin, uint32_t win,
     rr_totals *tot) {
@@ -1087,11 +1099,13 @@ __global__ __launch_bounds__(NW * RR_WAVE) __attribute__((amdgpu_waves_per_eu(DE
 #pragma unroll
     for (uint32_t k = 0; k < KE; ++k)
         ov_m[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ov_RM, (int)((tid + k * NT) * 16), 0, 0));
+    // (the values' first offsets come with first_val: one round trip, not first_val -> offsets)
     const uint64_t v_lo = first_val[tile], v_hi = first_val[tile + 1];
+    const uint64_t f_lo = first_off[tile], f_hi = first_off[tile + 1];
     uint64_t S0 = W0, S1 = W0;
     if (v_hi > v_lo) {
-        S0 = offsets[v_lo] & ~15ull;
-        S1 = (offsets[v_hi] + 15) & ~15ull;
+        S0 = f_lo & ~15ull;
+        S1 = (f_hi + 15) & ~15ull;
     }
     // the stage's tail [W1, S1) comes from KT granules per thread past the window; a window is
     // staged when its values' bytes [S0, S1) fit the stage and its tail fits those granules (a
@@ -1580,7 +1594,7 @@ __device__ uint64_t encode_size(uint32_t type, uint32_t enc, uint32_t vstatus, u
     return 0;
 }
 
-// Encode runs as a memset and three kernels, with no inter-workgroup waits:
+// Encode runs as zero_kernel and three kernels, with no inter-workgroup waits:
 //   E1 enc_size_kernel  workgroup per 256 values, element-parallel: blob size (0 for an
 //                       unencodable value), its offset inside the block into offsets[v], the
 //                       block's bytes into btot[b] and (atomically) its group's of 64 blocks
@@ -2404,6 +2418,31 @@ __device__ void emit_value_small(uint8_t *img, uint64_t p, const uint4 &x, const
     }
 }
 
+// encode_size with the whole wave on one value (its elements one per lane): the same size,
+// payload and status
+__device__ uint64_t encode_size_wave(uint32_t type, uint32_t enc, uint32_t vstatus, uint64_t eb, uint64_t n,
+                                     const rr_elem *elems, uint64_t ecap, uint64_t acap, uint32_t &st, uint64_t &pay) {
+    const bool multi = (type == RR_TYPE_LIST_QUICKLIST || type == RR_TYPE_SET_HT || type == RR_TYPE_HASH_HT ||
+                        type == RR_TYPE_ZSET_SKIPLIST || (type == RR_TYPE_SET_INTSET && (enc == 2 || enc == 4 || enc == 8))) &&
+                       vstatus == RR_OK && eb + n <= ecap &&
+                       !((type == RR_TYPE_HASH_HT || type == RR_TYPE_ZSET_SKIPLIST) && (n & 1));
+    if (!multi) return encode_size(type, enc, vstatus, eb, n, elems, ecap, acap, st, pay);
+    uint64_t sz = 0, p = 0;
+    bool bad = false;
+    for (uint64_t i = lane_id(); i < n; i += RR_WAVE) {
+        const ElemCost c = elem_cost(type, enc, i, get_elem(elems + eb + i), acap);
+        sz += c.bytes;
+        p += c.pay;
+        bad |= c.bad;
+    }
+    sz = wave_sum_fast(sz) + (type == RR_TYPE_LIST_QUICKLIST ? 5 : 13);
+    p = wave_sum_fast(p);
+    if (__ballot(bad)) { st = RR_E_ENCODE; pay = 0; return 0; }
+    st = RR_OK;
+    pay = p;
+    return sz;
+}
+
 // The same bytes with the whole wave on one value (the per-key calls, n <= SMALL_GW): lane 0
 // writes the header, the elements go one per lane — sizes, a wave scan for their offsets, each
 // lane its element's fields and payload — and a single string / ziplist payload is copied by
@@ -2474,6 +2513,8 @@ __global__ __launch_bounds__(SMALL_NT) void encode_small_kernel(const rr_value *
     __shared__ uint64_t wsum[SMALL_NT / RR_WAVE], red[3][SMALL_NT / RR_WAVE];
     __shared__ u32x4 ein[SMALL_EIN / 16];
     __shared__ uint64_t s_at[SMALL_GW];   // (the wave path: each value's image offset, ~0 = not written)
+    __shared__ uint64_t s_sz[SMALL_GW], s_pv[SMALL_GW];   // (the wave path: sizes, payloads, statuses)
+    __shared__ uint32_t s_st[SMALL_GW];
     const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid / RR_WAVE;
     // The inputs into LDS first when they fit SMALL_EIN (the per-key calls): one 16-byte load per
     // thread, all in flight, instead of the emission's dependent loads — over PCIe when the inputs
@@ -2509,6 +2550,19 @@ __global__ __launch_bounds__(SMALL_NT) void encode_small_kernel(const rr_value *
         }
     }
     const uint64_t v0 = (uint64_t)tid * SMALL_VPT;
+    const bool wave_path = n <= SMALL_GW;   // (uniform)
+    if (wave_path) {
+        // the few values' sizes with a wave on each (its elements one per lane)
+        for (uint32_t v = wave; v < n; v += SMALL_NT / RR_WAVE) {
+            const uint4 xv = reinterpret_cast<const uint4 *>(values)[v];
+            uint32_t st;
+            uint64_t pv;
+            const uint64_t sz = encode_size_wave(xv.x & 0xFF, (xv.x >> 8) & 0xFF, xv.x >> 16, xv.w, xv.z, elems, ecap, acap,
+                                                 st, pv);
+            if (lane == 0) { s_sz[v] = sz; s_pv[v] = pv; s_st[v] = st; }
+        }
+        __syncthreads();
+    }
     uint4 x[SMALL_VPT];
     uint64_t sz[SMALL_VPT], pv[SMALL_VPT], sum = 0, bad = 0, pay = 0, nel = 0;
 #pragma unroll
@@ -2518,8 +2572,14 @@ __global__ __launch_bounds__(SMALL_NT) void encode_small_kernel(const rr_value *
         if (v0 + j < n) {
             x[j] = reinterpret_cast<const uint4 *>(values)[v0 + j];
             uint32_t st;
-            sz[j] = encode_size(x[j].x & 0xFF, (x[j].x >> 8) & 0xFF, x[j].x >> 16, x[j].w, x[j].z, elems, ecap, acap, st,
-                                pv[j]);
+            if (wave_path) {
+                sz[j] = s_sz[v0 + j];
+                pv[j] = s_pv[v0 + j];
+                st = s_st[v0 + j];
+            } else {
+                sz[j] = encode_size(x[j].x & 0xFF, (x[j].x >> 8) & 0xFF, x[j].x >> 16, x[j].w, x[j].z, elems, ecap, acap, st,
+                                    pv[j]);
+            }
             bad += st != RR_OK ? 1u : 0u;
             nel += x[j].z;
         }
@@ -2528,9 +2588,8 @@ __global__ __launch_bounds__(SMALL_NT) void encode_small_kernel(const rr_value *
     uint64_t total;
     uint64_t a = block_excl_scan<SMALL_NT>(sum, wsum, total);
     const uint64_t lim = total < cap ? total : cap;   // (cap <= SMALL_BYTES: rr_small_encode_fits)
-    for (uint32_t k = tid; k < (SMALL_BYTES + 16) / 16; k += SMALL_NT) reinterpret_cast<uint4 *>(img)[k] = make_uint4(0, 0, 0, 0);
+    for (uint32_t k = tid; k < (lim + 31) / 16; k += SMALL_NT) reinterpret_cast<uint4 *>(img)[k] = make_uint4(0, 0, 0, 0);
     __syncthreads();
-    const bool wave_path = n <= SMALL_GW;   // (uniform)
 #pragma unroll 1
     for (uint32_t j = 0; j < SMALL_VPT; ++j) {
         if (v0 + j < n) {
@@ -2680,9 +2739,9 @@ static uint32_t dec_win(uint64_t data_cap) {
 static uint64_t dec_windows(uint64_t data_cap) { return data_cap / dec_win(data_cap) + 1; }
 
 // Decode scratch (uint64 words): [HDR] [window sums, nwin] [group sums, nwin / WGROUP + 1]
-// [reservations u32, n] [first_val u32, nwin + 1] [class bytes, n].  The sums are zeroed by one
-// memset per call; count_kernel's block 0 zeroes the totals.
-// Launches: memset, count_kernel, decode_kernel.  (Round 3 ran a look-back scan of the
+// [reservations u32, n] [first_val u32, nwin + 1] [first_off, nwin + 1] [class bytes, n].  The
+// sums are zeroed by zero_kernel per call; count_kernel's block 0 zeroes the totals.
+// Launches: zero_kernel, count_kernel, decode_kernel.  (Round 3 ran a look-back scan of the
 // reservations between the two — 15.4 us on config 4 — and a fourth kernel for the fixup and
 // the totals fold — 5.6 us.  Measured dead ends, in git history: a fused single-pass decode
 // with a window-level look-back, 0.401 vs 0.353 ms — the look-back waits ~5 us per window
@@ -2690,7 +2749,7 @@ static uint64_t dec_windows(uint64_t data_cap) { return data_cap / dec_win(data_
 static uint64_t dec_groups(uint64_t nw) { return nw / WGROUP + 1; }
 extern "C" uint64_t rr_decode_scratch_words(uint64_t data_cap, uint64_t n) {
     const uint64_t nw = dec_windows(data_cap);
-    return RR_SCRATCH_HDR + nw + dec_groups(nw) + (n + 2) / 2 + (nw + 2) / 2 + (n + 7) / 8 + 2;
+    return RR_SCRATCH_HDR + nw + dec_groups(nw) + (n + 2) / 2 + (nw + 2) / 2 + (nw + 1) + (n + 7) / 8 + 2;
 }
 
 extern "C" hipError_t rr_launch_decode(const uint8_t *blob, const uint64_t *offsets, uint64_t n, rr_value *values,
@@ -2701,19 +2760,19 @@ extern "C" hipError_t rr_launch_decode(const uint8_t *blob, const uint64_t *offs
     uint64_t *gtot = wtot + nw;
     uint32_t *counts = reinterpret_cast<uint32_t *>(gtot + dec_groups(nw));
     uint32_t *first_val = counts + ((n + 2) & ~1ull);
-    uint8_t *cls = reinterpret_cast<uint8_t *>(first_val + ((nw + 2) & ~1u));
-    const hipError_t e = hipMemsetAsync(wtot, 0, (nw + dec_groups(nw)) * sizeof(uint64_t), stream);
-    if (e != hipSuccess) return e;
+    uint64_t *first_off = reinterpret_cast<uint64_t *>(first_val + ((nw + 2) & ~1u));
+    uint8_t *cls = reinterpret_cast<uint8_t *>(first_off + nw + 1);
+    hipLaunchKernelGGL(zero_kernel, dim3(1), dim3(1024), 0, stream, wtot, (uint64_t)nw + dec_groups(nw));
     hipLaunchKernelGGL(count_kernel, dim3((uint32_t)((n + 1 + 255) / 256)), dim3(256), 0, stream, blob, offsets, n,
-                       first_val, nw, win, counts, cls, wtot, gtot, nullptr, 0u, totals);
+                       first_val, first_off, nw, win, counts, cls, wtot, gtot, nullptr, 0u, totals);
     hipLaunchKernelGGL((DECODE_KERNEL), dim3(nw), dim3(DEC_NW * RR_WAVE), 0, stream, blob, data_cap, offsets, n,
-                       first_val, cls, counts, wtot, gtot, values, elems, elem_cap, arena, nw, win, totals);
+                       first_val, first_off, cls, counts, wtot, gtot, values, elems, elem_cap, arena, nw, win, totals);
     return hipGetLastError();
 }
 
 // Encode scratch (uint64 words): [HDR] [error word] [tile stats, 3 per 256 values, twice]
 // [block sums, t] [group sums, t / WGROUP + 1] [first value per output window u32, nwin+1].
-// E1's block 0 zeroes the error word and the totals; the group sums are zeroed by a memset.
+// E1's block 0 zeroes the error word and the totals; the group sums are zeroed by zero_kernel.
 #ifndef RR_ENC_W
 #define RR_ENC_W 16384
 #endif
@@ -2743,8 +2802,7 @@ extern "C" hipError_t rr_launch_encode(const rr_value *values, const rr_elem *el
     uint64_t *stats = err + 1;
     uint64_t *btot = stats + 6 * (uint64_t)t, *gtot = btot + t;
     uint32_t *fv = reinterpret_cast<uint32_t *>(gtot + t / WGROUP + 1);
-    const hipError_t e = hipMemsetAsync(gtot, 0, (t / WGROUP + 1) * sizeof(uint64_t), stream);
-    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(zero_kernel, dim3(1), dim3(1024), 0, stream, gtot, t / WGROUP + 1);
     hipLaunchKernelGGL((enc_size_kernel<256, ENC_SIZE_U>), dim3(t), dim3(256), 0, stream, values, elems, n, elem_cap,
                        arena_cap, offsets, stats, btot, gtot, err, 1u, totals);
     hipLaunchKernelGGL(enc_index_kernel<ENC_W>, dim3(t), dim3(256), 0, stream, values, elems, n, elem_cap, arena_cap,

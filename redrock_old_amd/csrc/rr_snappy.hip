@@ -31,11 +31,12 @@ constexpr uint32_t FRAG = 1u << 16;        // snappy kBlockSize (snappy.h:197-19
 constexpr uint32_t TAB_MIN = 1u << 8;      // kMinHashTableSize
 constexpr uint32_t TAB_MAX = 1u << 14;     // kMaxHashTableSize
 constexpr uint32_t MARGIN = 15;            // kInputMarginBytes
-// LDS output window per wave: RocksDB blocks are cut at ~16 KiB (block_size, rocksdbapi.cc:77)
-// plus at most one entry; 20 KiB holds those with 7 waves per CU (32 KiB: 4 waves, half the
-// throughput), and a longer block decompresses straight into global memory
+// LDS window per wave (the block decompressed in place in it): RocksDB blocks are cut at ~16 KiB
+// (block_size, rocksdbapi.cc:77) plus at most one entry; 18 KiB holds those up to a 2 KiB last
+// entry with 8 waves per CU (20 KiB: 7 waves, 11 % slower on config 4; 17.5 KiB: 9 waves, +3 %
+// more but 1.5 KiB of room), and a longer block decompresses straight into global memory
 #ifndef RR_SNZ_DEC_WIN
-#define RR_SNZ_DEC_WIN 20480
+#define RR_SNZ_DEC_WIN 18432
 #endif
 constexpr uint32_t SNZ_DEC_WIN = RR_SNZ_DEC_WIN;
 // staged fragment bytes per wave; 0 (default): the compressor reads its input in place through
