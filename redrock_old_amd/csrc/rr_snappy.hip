@@ -276,22 +276,23 @@ __device__ uint32_t dec_block_lds(rsrc_t R, uint32_t s0, uint32_t clen, uint32_t
             } else {
                 // bytes to a 4-aligned destination, then 16 bytes per lane from five aligned
                 // source dwords (the last dword may spill up to 3 bytes past the literal, below
-                // its source: overwritten by a later element before anything reads them)
+                // its source: overwritten by a later element before anything reads them); the
+                // head bytes are read with the first chunk and written with it (one LDS round trip)
                 const uint32_t h = (4u - (dpos & 3)) & 3;
-                {
-                    const uint8_t x = lane < h ? win[src + lane] : 0;
-                    if (lane < h) win[dpos + lane] = x;
-                }
+                const uint8_t hx = lane < h ? win[src + lane] : 0;
                 const uint32_t d0 = dpos + h, q0 = src + h, body = l - h, a0 = q0 & ~3u, s3 = q0 & 3;
-                for (uint32_t i = 0; i < body; i += 16 * WAVE) {
+                uint32_t i = 0;
+                do {   // (body > 60: at least one chunk)
                     const uint32_t k4 = i + 16 * lane, sa = k4 < body ? (a0 + k4) >> 2 : 0u;   // (idle lanes: word 0)
                     const uint32_t x0 = win32[sa], x1 = win32[sa + 1], x2 = win32[sa + 2], x3 = win32[sa + 3], x4 = win32[sa + 4];
+                    if (i == 0 && lane < h) win[dpos + lane] = hx;
                     lds_u32 *w = win32 + ((d0 + k4) >> 2);
                     if (k4 < body) w[0] = __builtin_amdgcn_alignbyte(x1, x0, s3);
                     if (k4 + 4 < body) w[1] = __builtin_amdgcn_alignbyte(x2, x1, s3);
                     if (k4 + 8 < body) w[2] = __builtin_amdgcn_alignbyte(x3, x2, s3);
                     if (k4 + 12 < body) w[3] = __builtin_amdgcn_alignbyte(x4, x3, s3);
-                }
+                    i += 16 * WAVE;
+                } while (i < body);
             }
         }
         // the back-references, in stream order: out[pos + j] = out[pos - off + j % off]
