@@ -61,6 +61,7 @@ void rr_ctx_destroy(rr_ctx *c) {
     if (!c) return;
     hipSetDevice(c->device);
     if (c->scratch) hipFree(c->scratch);
+    if (c->dsums) hipFree(c->dsums);
     dfree(&c->d_in, &c->c_in); dfree(&c->d_off, &c->c_off); dfree(&c->d_vals, &c->c_vals);
     dfree(&c->d_elems, &c->c_elems); dfree(&c->d_arena, &c->c_arena); dfree(&c->d_out, &c->c_out);
     dfree(&c->d_ooff, &c->c_ooff);
@@ -106,6 +107,32 @@ int rr_ensure_scratch(rr_ctx *c, uint64_t words, hipStream_t stream) {
     return RR_API_OK;
 }
 
+/* The decode's window and group sums (and its finish counter) and the encode's group sums live
+ * in a buffer of their own that is zero between calls — decode_kernel's last workgroup zeroes
+ * what the call used once every window has read its sums, the encode's E4 block 0 what E3 read —
+ * so no zeroing launch runs per call.  Zeroed once when (re)allocated:
+ * like the scratch, growing waits on the previous call and is refused under graph capture. */
+static int ensure_dsums(rr_ctx *c, uint64_t words, hipStream_t stream) {
+    if (c->dsums && words <= c->dsums_words) return RR_API_OK;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (stream && hipStreamIsCapturing(stream, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
+        return fail(RR_API_EINVAL, "decode sums too small under graph capture: call rr_ctx_reserve first");
+    HIPCHK(hipSetDevice(c->device));
+    if (c->dsums) {
+        if (c->scratch_used) HIPCHK(hipEventSynchronize(c->scratch_done));
+        hipFree(c->dsums);
+        c->dsums = NULL;
+        c->dsums_words = 0;
+    }
+    uint64_t want = words + words / 4 + 64;
+    if (hipMalloc((void **)&c->dsums, want * sizeof(uint64_t)) != hipSuccess)
+        return fail(RR_API_ENOMEM, "hipMalloc decode sums (%llu words)", (unsigned long long)want);
+    HIPCHK(hipMemsetAsync(c->dsums, 0, want * sizeof(uint64_t), stream));
+    if (!stream) HIPCHK(hipStreamSynchronize(NULL));
+    c->dsums_words = want;
+    return RR_API_OK;
+}
+
 /* after a call's launches: remember where its use of the scratch ends (not under capture: the
  * captured graph replays later, and capture never grows the scratch) */
 int rr_mark_scratch(rr_ctx *c, hipStream_t stream) {
@@ -128,7 +155,9 @@ int rr_ctx_set_options(rr_ctx *c, unsigned flags) {
 int rr_ctx_reserve(rr_ctx *c, uint64_t n_values, uint64_t n_bytes) {
     if (!c) return fail(RR_API_EINVAL, "ctx is NULL");
     uint64_t a = rr_encode_scratch_words(n_values, (n_bytes + 15) & ~15ull), b = rr_decode_scratch_words((n_bytes + 15) & ~15ull, n_values);
-    return ensure_scratch(c, a > b ? a : b, NULL);
+    int rc = ensure_scratch(c, a > b ? a : b, NULL);
+    uint64_t sd = rr_decode_sums_words((n_bytes + 15) & ~15ull), se = rr_encode_sums_words(n_values);
+    return rc ? rc : ensure_dsums(c, sd > se ? sd : se, NULL);
 }
 
 
@@ -156,9 +185,10 @@ int rr_decode_batch(rr_ctx *c, const rr_blob_batch *in, rr_flat_batch *out, rr_t
         return RR_API_OK;
     }
     int rc = ensure_scratch(c, rr_decode_scratch_words(in->data_cap, in->n), (hipStream_t)stream);
+    if (!rc) rc = ensure_dsums(c, rr_decode_sums_words(in->data_cap), (hipStream_t)stream);
     if (rc) return rc;
     HIPCHK(rr_launch_decode(in->data, in->offsets, in->n, out->values, out->elems, out->elem_cap, out->arena,
-                            c->scratch, in->data_cap, d_totals, (hipStream_t)stream));
+                            c->scratch, c->dsums, in->data_cap, d_totals, (hipStream_t)stream));
     return mark_scratch(c, (hipStream_t)stream);
 }
 
@@ -176,9 +206,10 @@ int rr_encode_batch(rr_ctx *c, const rr_flat_batch *in, rr_blob_batch *out, rr_t
         return RR_API_OK;
     }
     int rc = ensure_scratch(c, rr_encode_scratch_words(in->n, out->data_cap), (hipStream_t)stream);
+    if (!rc) rc = ensure_dsums(c, rr_encode_sums_words(in->n), (hipStream_t)stream);
     if (rc) return rc;
     HIPCHK(rr_launch_encode(in->values, in->elems, in->elem_cap, in->arena, in->arena_cap, in->n, out->data,
-                            out->data_cap, out->offsets, c->scratch, d_totals, (hipStream_t)stream));
+                            out->data_cap, out->offsets, c->scratch, c->dsums, d_totals, (hipStream_t)stream));
     return mark_scratch(c, (hipStream_t)stream);
 }
 

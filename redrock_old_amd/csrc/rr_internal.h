@@ -15,6 +15,8 @@ struct rr_ctx {
     uint64_t scratch_words;
     hipEvent_t scratch_done;     /* recorded after every call's last use of the scratch */
     int scratch_used;
+    uint64_t *dsums;             /* the decode's window/group sums: zero between calls */
+    uint64_t dsums_words;
     /* device staging for host entry points */
     void *d_in, *d_off, *d_vals, *d_elems, *d_arena, *d_out, *d_ooff;
     size_t c_in, c_off, c_vals, c_elems, c_arena, c_out, c_ooff;

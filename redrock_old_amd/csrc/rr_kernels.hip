@@ -461,7 +461,8 @@ __device__ __forceinline__ void zero_call_words(uint64_t *words, uint32_t nwords
 
 // Per value: its reservation (u32; a value that would need 2^32 slots fails capacity anyway),
 // its class and first_val.  Per window: the reservations of its values summed into wtot[w], and
-// per group of WGROUP windows into gtot[w / WGROUP] (both zeroed by zero_kernel before the launch).
+// per group of WGROUP windows into gtot[w / WGROUP] (both zero on entry: decode_kernel's last
+// workgroup of the previous call zeroed them).
 // A window's values are consecutive, so each run of one window (group) in a wave adds its sum
 // with two LDS atomics — the inclusive wave scan at its last lane, minus the exclusive scan at
 // its first — into the workgroup's table of the windows (groups) it touches; the table then
@@ -480,11 +481,9 @@ __device__ __forceinline__ uint64_t div_win(uint64_t o, uint32_t win, double rcp
     return q;
 }
 constexpr uint32_t WGROUP = 16;   // (64: ~260 same-address atomics per group sum on config 1)
-// The call's sums zeroed by one small kernel: hipMemsetAsync of a size that is not a multiple of
-// 16 bytes runs two fill kernels (~4.7 us each in the traces, config 1 at 100K values)
-__global__ __launch_bounds__(1024) void zero_kernel(uint64_t *__restrict__ w, uint64_t nwords) {
-    for (uint64_t k = threadIdx.x; k < nwords; k += 1024) w[k] = 0;
-}
+// (The sums are zero on entry without a zeroing launch: the previous call's last workgroup
+// zeroed them.  A zeroing kernel cost ~4.5 us a call, hipMemsetAsync of a size that is not a
+// multiple of 16 bytes two fill kernels of ~4.7 us — a sixth of config 1's 100K-value call.)
 constexpr uint32_t CNT_NT = 256, CNT_LW = CNT_NT, CNT_LG = 8;   // (a workgroup's values start in <= 256 windows)
 __global__ __launch_bounds__(CNT_NT) void count_kernel(const uint8_t *__restrict__ blob,
                                                        const uint64_t *__restrict__ offsets, uint64_t n,
@@ -1049,9 +1048,9 @@ __global__ __launch_bounds__(NW * RR_WAVE) __attribute__((amdgpu_waves_per_eu(DE
     const uint8_t *__restrict__ blob, uint64_t data_cap, const uint64_t *__restrict__ offsets, uint64_t n,
     const uint32_t *__restrict__ first_val, const uint64_t *__restrict__ first_off, const uint8_t *__restrict__ cls,
     const uint32_t *__restrict__ counts,
-    const uint64_t *__restrict__ wtot, const uint64_t *__restrict__ gtot, rr_value *__restrict__ values,
+    uint64_t *wtot, const uint64_t *gtot, rr_value *__restrict__ values,   // (wtot: also zeroed at the end)
     rr_elem *__restrict__ elems, uint64_t elem_cap, uint8_t *__restrict__ arena, uint32_t nwin, uint32_t win,
-    rr_totals *tot) {
+    rr_totals *tot, uint32_t *fin, uint64_t nsums) {
     constexpr uint32_t NT = NW * RR_WAVE, STAGE = W + SLACK;
     static_assert(PMAX == NT, "a chunk is one value per thread (the slot scan)");
     static_assert(W % 16 == 0 && SLACK % 16 == 0, "tile shape");
@@ -1062,7 +1061,7 @@ __global__ __launch_bounds__(NW * RR_WAVE) __attribute__((amdgpu_waves_per_eu(DE
     __shared__ uint32_t eloc[PMAX + 1];   // chunk-relative first slot of each value, then the chunk's slots
     __shared__ uint64_t wpart[2][NW];     // wave sums: [0] the window's first slot, [1] the chunk's slot scan
     __shared__ uint32_t ccount[C_N], cbase[C_N], ccur[C_N], bpre[C_N + 1];
-    __shared__ uint32_t next_batch;
+    __shared__ uint32_t next_batch, last_win;
     __shared__ uint64_t red[2][NW];
     PROBE(__shared__ uint64_t prb[PROBE_WORDS]; uint64_t pt0 = __builtin_amdgcn_s_memtime(), pt1 = 0, pt2 = 0;
           if (threadIdx.x < PROBE_WORDS) prb[threadIdx.x] = 0;)
@@ -1322,6 +1321,17 @@ __global__ __launch_bounds__(NW * RR_WAVE) __attribute__((amdgpu_waves_per_eu(DE
         if (tot && tile == nwin - 1) tot->n_elems = first_slot() + run + ctot;
         PROBE(prb[0] = pt1 - pt0; prb[1] = pt2 - pt1; prb[2] = __builtin_amdgcn_s_memtime() - pt2; prb[28] = v_hi - v_lo;
               prb[29] = staged; if (g_probe) for (uint32_t i = 0; i < PROBE_WORDS; ++i) g_probe[(uint64_t)tile * PROBE_WORDS + i] = prb[i];)
+        // the last window to finish (every other one has read its sums, at its start) zeroes
+        // the call's sums and the counter for the next call: no zeroing launch per call.
+        // Relaxed: the sums' loads returned before each window's increment, and the zeroes
+        // need only reach the next call, past the kernel boundary (acquire-release at agent
+        // scope writes back and invalidates the XCD's L2 at every window: 0.35 -> 0.81 ms)
+        last_win = __hip_atomic_fetch_add(fin, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nwin - 1;
+    }
+    lds_barrier();
+    if (last_win) {
+        for (uint64_t k = tid; k < nsums; k += NT) wtot[k] = 0;   // (wtot, then gtot and the counter)
+        if (tid == 0) *fin = 0;
     }
 }
 
@@ -1594,7 +1604,8 @@ __device__ uint64_t encode_size(uint32_t type, uint32_t enc, uint32_t vstatus, u
     return 0;
 }
 
-// Encode runs as zero_kernel and three kernels, with no inter-workgroup waits:
+// Encode runs as three kernels, with no inter-workgroup waits (E4's block 0 zeroes the group
+// sums for the next call):
 //   E1 enc_size_kernel  workgroup per 256 values, element-parallel: blob size (0 for an
 //                       unencodable value), its offset inside the block into offsets[v], the
 //                       block's bytes into btot[b] and (atomically) its group's of 64 blocks
@@ -2106,8 +2117,12 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(ENC_WPE))) v
                                                       const uint64_t *__restrict__ offsets,
                                                       const uint32_t *__restrict__ fv,
                                                       const uint64_t *__restrict__ stats, uint32_t ntiles,
-                                                      rr_totals *tot, uint64_t *err) {
+                                                      rr_totals *tot, uint64_t *err, uint64_t *zsums, uint32_t nzsums) {
     static_assert(W <= 65536 && W % 64 == 0, "image offsets are 16-bit, pieces 64-byte blocks");
+    // block 0 also zeroes E1's group sums, which E3 (done) read: they are zero for the next call
+    // without a zeroing launch (the context keeps them in its zero-between-calls buffer)
+    if (blockIdx.x == 0)
+        for (uint32_t k = threadIdx.x; k < nzsums; k += NT) zsums[k] = 0;
     // block 0 folds E1's and E3's tile totals into the call's totals before its window (a
     // separate finalize launch's work, hidden under the other windows: encode cfg 4 -1 %)
     if (tot && blockIdx.x == 0) fold_totals(stats, ntiles, offsets, n, tot, err);
@@ -2738,10 +2753,10 @@ static uint32_t dec_win(uint64_t data_cap) {
 }
 static uint64_t dec_windows(uint64_t data_cap) { return data_cap / dec_win(data_cap) + 1; }
 
-// Decode scratch (uint64 words): [HDR] [window sums, nwin] [group sums, nwin / WGROUP + 1]
-// [reservations u32, n] [first_val u32, nwin + 1] [first_off, nwin + 1] [class bytes, n].  The
-// sums are zeroed by zero_kernel per call; count_kernel's block 0 zeroes the totals.
-// Launches: zero_kernel, count_kernel, decode_kernel.  (Round 3 ran a look-back scan of the
+// Decode scratch (uint64 words): [HDR] [reservations u32, n] [first_val u32, nwin + 1]
+// [first_off, nwin + 1] [class bytes, n].  The window and group sums are in a buffer of their
+// own (rr_decode_sums_words), zero between calls; count_kernel's block 0 zeroes the totals.
+// Launches: count_kernel, decode_kernel.  (Round 3 ran a look-back scan of the
 // reservations between the two — 15.4 us on config 4 — and a fourth kernel for the fixup and
 // the totals fold — 5.6 us.  Measured dead ends, in git history: a fused single-pass decode
 // with a window-level look-back, 0.401 vs 0.353 ms — the look-back waits ~5 us per window
@@ -2749,30 +2764,37 @@ static uint64_t dec_windows(uint64_t data_cap) { return data_cap / dec_win(data_
 static uint64_t dec_groups(uint64_t nw) { return nw / WGROUP + 1; }
 extern "C" uint64_t rr_decode_scratch_words(uint64_t data_cap, uint64_t n) {
     const uint64_t nw = dec_windows(data_cap);
-    return RR_SCRATCH_HDR + nw + dec_groups(nw) + (n + 2) / 2 + (nw + 2) / 2 + (nw + 1) + (n + 7) / 8 + 2;
+    return RR_SCRATCH_HDR + (n + 2) / 2 + (nw + 2) / 2 + (nw + 1) + (n + 7) / 8 + 2;
+}
+// The sums buffer: [window sums, nwin] [group sums, nwin / WGROUP + 1] [finish counter]
+extern "C" uint64_t rr_decode_sums_words(uint64_t data_cap) {
+    const uint64_t nw = dec_windows(data_cap);
+    return nw + dec_groups(nw) + 1;
 }
 
 extern "C" hipError_t rr_launch_decode(const uint8_t *blob, const uint64_t *offsets, uint64_t n, rr_value *values,
                                        rr_elem *elems, uint64_t elem_cap, uint8_t *arena, uint64_t *scratch,
-                                       uint64_t data_cap, rr_totals *totals, hipStream_t stream) {
+                                       uint64_t *sums, uint64_t data_cap, rr_totals *totals, hipStream_t stream) {
     const uint32_t win = dec_win(data_cap), nw = (uint32_t)(data_cap / win + 1);
-    uint64_t *wtot = scratch + RR_SCRATCH_HDR;
+    uint64_t *wtot = sums;
     uint64_t *gtot = wtot + nw;
-    uint32_t *counts = reinterpret_cast<uint32_t *>(gtot + dec_groups(nw));
+    uint32_t *fin = reinterpret_cast<uint32_t *>(gtot + dec_groups(nw));
+    uint32_t *counts = reinterpret_cast<uint32_t *>(scratch + RR_SCRATCH_HDR);
     uint32_t *first_val = counts + ((n + 2) & ~1ull);
     uint64_t *first_off = reinterpret_cast<uint64_t *>(first_val + ((nw + 2) & ~1u));
     uint8_t *cls = reinterpret_cast<uint8_t *>(first_off + nw + 1);
-    hipLaunchKernelGGL(zero_kernel, dim3(1), dim3(1024), 0, stream, wtot, (uint64_t)nw + dec_groups(nw));
     hipLaunchKernelGGL(count_kernel, dim3((uint32_t)((n + 1 + 255) / 256)), dim3(256), 0, stream, blob, offsets, n,
                        first_val, first_off, nw, win, counts, cls, wtot, gtot, nullptr, 0u, totals);
     hipLaunchKernelGGL((DECODE_KERNEL), dim3(nw), dim3(DEC_NW * RR_WAVE), 0, stream, blob, data_cap, offsets, n,
-                       first_val, first_off, cls, counts, wtot, gtot, values, elems, elem_cap, arena, nw, win, totals);
+                       first_val, first_off, cls, counts, wtot, gtot, values, elems, elem_cap, arena, nw, win, totals,
+                       fin, (uint64_t)nw + dec_groups(nw) + 1);
     return hipGetLastError();
 }
 
 // Encode scratch (uint64 words): [HDR] [error word] [tile stats, 3 per 256 values, twice]
 // [block sums, t] [group sums, t / WGROUP + 1] [first value per output window u32, nwin+1].
-// E1's block 0 zeroes the error word and the totals; the group sums are zeroed by zero_kernel.
+// E1's block 0 zeroes the error word and the totals.  The group sums are in the context's
+// zero-between-calls buffer (rr_encode_sums_words): E4's block 0 zeroes them (E3 read them).
 #ifndef RR_ENC_W
 #define RR_ENC_W 16384
 #endif
@@ -2784,13 +2806,14 @@ static uint64_t enc_windows(uint64_t data_cap) { return data_cap / ENC_W + 1; }
 
 extern "C" uint64_t rr_encode_scratch_words(uint64_t n, uint64_t data_cap) {
     const uint64_t t = (n + 255) / 256, nw = enc_windows(data_cap);
-    return RR_SCRATCH_HDR + 1 + 6 * t + t + t / WGROUP + 1 + (nw + 2) / 2 + 2;
+    return RR_SCRATCH_HDR + 1 + 6 * t + t + (nw + 2) / 2 + 2;
 }
+extern "C" uint64_t rr_encode_sums_words(uint64_t n) { return (n + 255) / 256 / WGROUP + 1; }
 
 extern "C" hipError_t rr_launch_encode(const rr_value *values, const rr_elem *elems, uint64_t elem_cap,
                                        const uint8_t *arena, uint64_t arena_cap, uint64_t n, uint8_t *out,
-                                       uint64_t cap, uint64_t *offsets, uint64_t *scratch, rr_totals *totals,
-                                       hipStream_t stream) {
+                                       uint64_t cap, uint64_t *offsets, uint64_t *scratch, uint64_t *sums,
+                                       rr_totals *totals, hipStream_t stream) {
     if (n == 0) {
         hipError_t e = hipMemsetAsync(offsets, 0, sizeof(uint64_t), stream);
         if (e == hipSuccess && totals) e = hipMemsetAsync(totals, 0, sizeof(rr_totals), stream);
@@ -2800,15 +2823,14 @@ extern "C" hipError_t rr_launch_encode(const rr_value *values, const rr_elem *el
     const uint64_t nw = enc_windows(cap);
     uint64_t *err = scratch + RR_SCRATCH_HDR;   // device error word (no look-back left to set it)
     uint64_t *stats = err + 1;
-    uint64_t *btot = stats + 6 * (uint64_t)t, *gtot = btot + t;
-    uint32_t *fv = reinterpret_cast<uint32_t *>(gtot + t / WGROUP + 1);
-    hipLaunchKernelGGL(zero_kernel, dim3(1), dim3(1024), 0, stream, gtot, t / WGROUP + 1);
+    uint64_t *btot = stats + 6 * (uint64_t)t, *gtot = sums;
+    uint32_t *fv = reinterpret_cast<uint32_t *>(btot + t);
     hipLaunchKernelGGL((enc_size_kernel<256, ENC_SIZE_U>), dim3(t), dim3(256), 0, stream, values, elems, n, elem_cap,
                        arena_cap, offsets, stats, btot, gtot, err, 1u, totals);
     hipLaunchKernelGGL(enc_index_kernel<ENC_W>, dim3(t), dim3(256), 0, stream, values, elems, n, elem_cap, arena_cap,
                        offsets, btot, gtot, cap, fv, nw, stats + 3 * (uint64_t)t);
     hipLaunchKernelGGL((enc_emit_kernel<ENC_W, ENC_NT, ENC_RCAP>), dim3((uint32_t)nw), dim3(ENC_NT), 0, stream,
-                       values, elems, arena, n, out, cap, offsets, fv, stats, 2 * t, totals, err);
+                       values, elems, arena, n, out, cap, offsets, fv, stats, 2 * t, totals, err, gtot, t / WGROUP + 1);
     return hipGetLastError();
 }
 

@@ -204,6 +204,27 @@ def test_device_api_matches_host_api(engine):
     assert torch.equal(d_out[:nb], d_data[:nb])
 
 
+def test_sums_zero_between_calls():
+    """The window/group sums live in a context buffer that must be zero on entry: decode_kernel's
+    last workgroup (encode: E3's last block) zeroes what its call used.  Calls of changing sizes
+    on one fresh context — growing, shrinking, decode and encode interleaved, repeated on the
+    device API — each equal the oracle (a sum left over from an earlier call would shift every
+    later window's descriptor slots)."""
+    eng = rr.Engine(0)
+    try:
+        for cfg, n in [(4, 30000), (1, 200000), (4, 5000), (3, 20000), (4, 30000), (2, 90000), (4, 5000)]:
+            data, offs = rr.gen_batch(cfg, n, seed=77 + n)
+            v, e, a, t = eng.decode_host(data, offs)
+            ov, oe, oa, ot = cpu.decode(data, offs, nthreads=8)
+            assert_flat_equal((v, e), (ov, oe), f"config {cfg} n={n}")
+            assert t == ot
+            out, ooffs, t2 = eng.encode_host(v, e, a)
+            assert np.array_equal(ooffs, offs) and np.array_equal(out, data[:int(offs[-1])])
+            assert t2["n_elems"] == t["n_elems"] and t2["payload"] == t["payload"]
+    finally:
+        eng.close()
+
+
 @pytest.mark.parametrize("cfg", [4, 3, 2])
 def test_full_size_mixed_roundtrip(engine, cfg):
     """1M-value batches at BASELINE.json's sizes (config 4 mixed = the headline, config 3 Hash
