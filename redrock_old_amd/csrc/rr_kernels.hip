@@ -386,9 +386,39 @@ typedef uint32_t u32_ua __attribute__((aligned(1)));   // unaligned dword (one g
 // line; an aligned pair + alignbyte measured count 52.5 -> 54.6 us), byte reads from LDS
 __device__ __forceinline__ uint32_t len_u32(const uint8_t *p) { return *reinterpret_cast<const u32_ua *>(p); }
 __device__ __forceinline__ uint32_t len_u32(lds_cptr p) { return ld_u32(p); }
-// The descriptor reservation (rr_format.h) and the walk class of a value from its header dwords
-// (b: the value's bytes, in global memory or an LDS stage).
+// A List's reservation: its element count, from the chain of u32 length fields (b: the value's
+// bytes, in global memory or an LDS stage)
 template <typename P>
+__device__ __forceinline__ uint64_t list_count(P b, uint64_t L) {
+    uint64_t p = 5, n = 0;
+    while (p < L) {
+        if (L - p < 4) break;
+        const uint64_t l = len_u32(b + p);
+        if (l > L - p - 4) break;
+        ++n;
+        p += 4 + l;
+    }
+    return n;
+}
+// The same from a List staged in LDS (count_kernel; L < 2^32): 32-bit positions, each length
+// field from two aligned dword reads and an alignbyte (one LDS round trip per element)
+__device__ __forceinline__ uint32_t list_count_lds(uint32_t b, uint32_t L) {   // b: LDS byte address of byte 0
+    typedef const __attribute__((address_space(3))) uint32_t *lds_u32p;
+    uint32_t p = 5, n = 0;
+    while (p <= L && L - p >= 4) {
+        const uint32_t a = b + p, a4 = a & ~3u;
+        const uint32_t lo = *(lds_u32p)(uintptr_t)a4, hi = *(lds_u32p)(uintptr_t)(a4 + 4);
+        const uint32_t l = __builtin_amdgcn_alignbyte(hi, lo, a & 3);
+        if (l > L - p - 4) break;
+        ++n;
+        p += 4 + l;
+    }
+    return n;
+}
+// The descriptor reservation (rr_format.h) and the walk class of a value from its header dwords
+// (b: the value's bytes, in global memory or an LDS stage).  LIST_LATER: a List's count is left
+// to the caller (count_kernel walks it from LDS), r = 0.
+template <bool LIST_LATER = false, typename P>
 __device__ __forceinline__ void reserve_classify(P b, uint64_t L, const uint32_t (&d)[6], uint64_t &r, uint32_t &c) {
     r = 0;
     c = C_EXACT;
@@ -410,15 +440,7 @@ __device__ __forceinline__ void reserve_classify(P b, uint64_t L, const uint32_t
         }
         case RR_TYPE_LIST_QUICKLIST: {
             c = C_LIST;
-            uint64_t p = 5, n = 0;
-            while (p < L) {
-                if (L - p < 4) break;
-                const uint64_t l = len_u32(b + p);
-                if (l > L - p - 4) break;
-                ++n;
-                p += 4 + l;
-            }
-            r = n;
+            if (!LIST_LATER) r = list_count(b, L);
             return;
         }
         default:
@@ -485,6 +507,10 @@ constexpr uint32_t WGROUP = 16;   // (64: ~260 same-address atomics per group su
 // zeroed them.  A zeroing kernel cost ~4.5 us a call, hipMemsetAsync of a size that is not a
 // multiple of 16 bytes two fill kernels of ~4.7 us — a sixth of config 1's 100K-value call.)
 constexpr uint32_t CNT_NT = 256, CNT_LW = CNT_NT, CNT_LG = 8;   // (a workgroup's values start in <= 256 windows)
+// a wave's List stage (16 KiB a workgroup: 8 workgroups still fit a CU; measured count_kernel
+// 53.5 us at 4 KiB, 53.8 at 8 KiB, 62.7 at 2 KiB; walking from global memory 58.1, with no List
+// walk at all — a timing-only build — 30.9)
+constexpr uint32_t CNT_LB = 4096;
 __global__ __launch_bounds__(CNT_NT) void count_kernel(const uint8_t *__restrict__ blob,
                                                        const uint64_t *__restrict__ offsets, uint64_t n,
                                                        uint32_t *__restrict__ first_val, uint64_t *__restrict__ first_off,
@@ -493,6 +519,7 @@ __global__ __launch_bounds__(CNT_NT) void count_kernel(const uint8_t *__restrict
                                                        uint64_t *wtot, uint64_t *gtot,
                                                        uint64_t *zero_words, uint32_t nzero, rr_totals *tot) {
     __shared__ uint64_t lw[CNT_LW], lg[CNT_LG];
+    __shared__ __attribute__((aligned(16))) uint8_t lstage[CNT_NT / RR_WAVE][CNT_LB];
     zero_call_words(zero_words, nzero, tot);
     const uint32_t tid = threadIdx.x;
     lw[tid] = 0;
@@ -522,15 +549,50 @@ __global__ __launch_bounds__(CNT_NT) void count_kernel(const uint8_t *__restrict
     }
     uint64_t r = 0;
     uint32_t w = 0xFFFFFFFFu;   // (lanes past n: a window no value has)
+    uint32_t c = C_N;
     if (i < n) {
-        uint32_t c;
-        reserve_classify(blob + o_hi, b1 - o_hi, d, r, c);
-        counts[i] = (uint32_t)(r < 0xFFFFFFFFull ? r : 0xFFFFFFFFull);
+        reserve_classify<true>(blob + o_hi, b1 - o_hi, d, r, c);
         cls[i] = (uint8_t)c;
         w = (uint32_t)div_win(o_hi, win, rcp);
     }
+    // Lists: the length chain from LDS.  The wave stages its Lists' bytes with direct-to-LDS
+    // loads, CNT_LB bytes at a time (Lists in lane order, as many as fit), then each List lane
+    // walks its copy: a memory round trip per pack instead of one per element (a dependent
+    // global load per element made the wave's longest List its critical path).  A List longer
+    // than the stage walks from global memory.
+    const uint32_t lane = lane_id(), wave = tid / RR_WAVE;
+    {
+        const uint64_t L = b1 - o_hi, s0 = (o_hi + 5) & ~15ull;
+        const bool lst = i < n && c == C_LIST && L > 5;
+        const uint32_t ng = lst ? (uint32_t)((((o_hi + L + 15) & ~15ull) - s0) >> 4) : 0u;   // its granules
+        if (lst && ng > CNT_LB / 16) r = list_count(blob + o_hi, L);
+        uint64_t todo = __ballot(lst && ng <= CNT_LB / 16);
+        while (todo) {
+            const bool mine = (todo >> lane) & 1;
+            const uint32_t incl = wave_incl_scan_u32(mine ? ng : 0u), ex = incl - (mine ? ng : 0u);
+            const bool inpack = mine && incl <= CNT_LB / 16;   // (the first List of todo always fits)
+            const uint64_t pack = __ballot(inpack);
+            for (uint64_t m = pack; m; m &= m - 1) {
+                const int j = __builtin_ctzll(m);
+                const uint64_t sj = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)s0, j) |
+                                    ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(s0 >> 32), j) << 32);
+                const uint32_t gj = (uint32_t)__builtin_amdgcn_readlane((int)ng, j);
+                const uint32_t ej = (uint32_t)__builtin_amdgcn_readlane((int)ex, j);
+                for (uint32_t k0 = 0; k0 < gj; k0 += RR_WAVE)
+                    if (k0 + lane < gj)
+                        __builtin_amdgcn_global_load_lds((const void *)(blob + sj + 16ull * (k0 + lane)),
+                                                         (__attribute__((address_space(3))) void *)(lstage[wave] + 16 * (ej + k0)),
+                                                         16, 0, 0);
+            }
+            __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the pack has landed (this wave's own stage)
+            if (inpack)
+                r = list_count_lds((uint32_t)(uintptr_t)(lds_cptr)(lstage[wave] + 16 * ex + ((o_hi + 5) & 15)) - 5u, (uint32_t)L);
+            todo &= ~pack;
+        }
+    }
+    if (i < n) counts[i] = (uint32_t)(r < 0xFFFFFFFFull ? r : 0xFFFFFFFFull);
     const uint64_t incl = wave_incl_scan_fast(r);
-    const uint32_t lane = lane_id(), wp = wave_from_prev(w), wn = wave_from_next(w);
+    const uint32_t wp = wave_from_prev(w), wn = wave_from_next(w);
     const bool in = i < n;
     lds_barrier();   // (the tables are zero)
     // a run's sum into the table slot k (u64 adds wrap: a slot's total is its runs' sum), or
