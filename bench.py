@@ -235,7 +235,7 @@ def main():
                 "host_e2e_encode": {"gib_s": round(nb * 5 / wall_enc_host / 2 ** 30, 2),
                                     "ms_per_step": round(wall_enc_host / 5 * 1e3, 3), "roundtrip_bit_exact": enc_ok,
                                     "what": "rr_encode_batch_host on pinned host buffers: records+descriptors+arena "
-                                            "up, encode, blobs+offsets down (one stream)"},
+                                            "up, encode, blobs+offsets down, chunked so uploads, encodes and downloads overlap"},
                 "host_e2e_serial": {"gib_s": round(nb * 5 / wall_ser / 2 ** 30, 2),
                                     "ms_per_step": round(wall_ser / 5 * 1e3, 3),
                                     "what": "the same transfers in one stream, back to back (no overlap)"}}

@@ -34,7 +34,7 @@ for c in ("FETCH_SIZE", "WRITE_SIZE"):
             disp[k].add(r["Dispatch_Id"])
         for k in acc:
             per[k][c] = acc[k] / len(disp[k]) * 1024   # KB -> bytes, per dispatch
-# (each pipeline also runs one hipMemsetAsync of its window / group sums: a few KB, not counted)
+# (no zeroing launch: the sums are zero between calls, restored by the pipelines themselves)
 if "enc_emit_kernel" in per:   # RR_PROFILE=encode run (one decode call precedes the encode steps)
     pipeline = ("enc_size_kernel", "enc_index_kernel", "enc_emit_kernel")
 else:
