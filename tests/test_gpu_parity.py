@@ -225,6 +225,76 @@ def test_sums_zero_between_calls():
         eng.close()
 
 
+def test_graph_replay_decode_encode():
+    """Decode + encode captured in a HIP graph (torch.cuda.CUDAGraph) after rr_ctx_reserve, then
+    replayed: no zeroing launch runs, so every replay relies on the previous one's kernels having
+    left the sums zero.  Each replay's records, descriptors and re-encoded blobs equal the host
+    path's; replays over a second batch copied into the same input buffers as well."""
+    import torch
+    dev = torch.device("cuda:0")
+    eng = rr.Engine(0)
+    try:
+        data, offs = rr.gen_batch(4, 30000, seed=4242)
+        n = len(offs) - 1
+        data3, offs3 = rr.gen_batch(1, n, seed=4244)   # (replayed later through the same buffers)
+        nb = (max(int(offs[-1]), int(offs3[-1])) + 15) & ~15
+        cap = max(rr.elem_bound(n, int(offs[-1])), rr.elem_bound(n, int(offs3[-1])))
+        d_data = torch.zeros(nb, dtype=torch.uint8, device=dev)
+        d_offs = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+        d_vals = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
+        d_elems = torch.zeros(cap * 16, dtype=torch.uint8, device=dev)
+        d_arena = torch.zeros(nb, dtype=torch.uint8, device=dev)
+        d_tot = torch.zeros(4, dtype=torch.int64, device=dev)
+        d_out = torch.zeros(nb, dtype=torch.uint8, device=dev)
+        d_ooffs = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+        d_tot2 = torch.zeros(4, dtype=torch.int64, device=dev)
+        eng.reserve(n, nb)
+
+        def load(dd, oo):
+            d_data.zero_()
+            d_data[:dd.size].copy_(torch.from_numpy(dd))
+            d_offs.copy_(torch.from_numpy(oo.view(np.int64)))
+
+        def check(dd, oo):
+            hv, he, ha, ht = eng.decode_host(dd, oo)
+            tot = d_tot.cpu().numpy().view(np.uint64)
+            v = d_vals.cpu().numpy().view(rr.VALUE_DT)
+            e = d_elems.cpu().numpy().view(rr.ELEM_DT)[:int(tot[0])]
+            assert_flat_equal((v, e), (hv, he), "graph replay")
+            assert int(tot[0]) == ht["n_elems"] and int(tot[3]) == ht["payload"]
+            assert np.array_equal(d_ooffs.cpu().numpy().view(np.uint64), oo)
+            m = int(oo[-1])
+            assert torch.equal(d_out[:m], d_data[:m])
+
+        load(data, offs)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):   # (one eager call first, as torch's capture recipe asks)
+            eng.decode_device(d_data, d_offs, d_vals, d_elems, d_arena, d_tot, stream=s)
+            eng.encode_device(d_vals, d_elems, d_arena, d_out, d_ooffs, d_tot2, stream=s)
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            cs = torch.cuda.current_stream()
+            eng.decode_device(d_data, d_offs, d_vals, d_elems, d_arena, d_tot, stream=cs)
+            eng.encode_device(d_vals, d_elems, d_arena, d_out, d_ooffs, d_tot2, stream=cs)
+        for _ in range(3):
+            d_vals.zero_(); d_elems.zero_(); d_out.zero_()
+            g.replay()
+            torch.cuda.synchronize()
+            check(data, offs)
+        # the graph's launches are sized by the first batch's n: a second batch of the same count
+        # through the same buffers (config 1 values, fewer bytes: other windows, other sums)
+        load(data3, offs3)
+        for _ in range(2):
+            g.replay()
+            torch.cuda.synchronize()
+            check(data3, offs3)
+    finally:
+        eng.close()
+
+
 @pytest.mark.parametrize("cfg", [4, 3, 2])
 def test_full_size_mixed_roundtrip(engine, cfg):
     """1M-value batches at BASELINE.json's sizes (config 4 mixed = the headline, config 3 Hash
