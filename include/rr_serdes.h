@@ -14,8 +14,8 @@
  *   - return value: RR_API_OK (0) or a negative RR_API_E* code for the whole call;
  *   - per-value status in rr_value.status (0 = OK), counted into rr_totals.n_bad;
  *   - caller-owned buffers; one rr_ctx per host thread; no hidden host synchronisation in the
- *     device entry points (graph-capturable after rr_ctx_reserve: decode = 3 kernels,
- *     encode = 4 kernels, a batch of at most 4096 values in at most 128 KiB = ONE kernel; all
+ *     device entry points (graph-capturable after rr_ctx_reserve: decode = 2 kernels,
+ *     encode = 3 kernels, a batch of at most 4096 values in at most 128 KiB = ONE kernel; all
  *     on the caller's stream).  The only wait is when the context's scratch must grow: it
  *     waits for the context's previous call to finish (an event, not a device sync) — and
  *     under graph capture it fails instead.
@@ -77,7 +77,9 @@ typedef struct rr_totals {
 int  rr_ctx_create(int device, rr_ctx **out);
 void rr_ctx_destroy(rr_ctx *ctx);
 /* Make scratch space for batches up to n_values values / n_bytes blob bytes (the device calls
- * grow it on demand too, but growing allocates; call this first when capturing graphs). */
+ * grow it on demand too, but growing allocates; call this first when capturing graphs).  This
+ * also sizes the context's window-sums buffer, which the calls keep zero between calls (their
+ * own last workgroups zero it: no zeroing launch). */
 int  rr_ctx_reserve(rr_ctx *ctx, uint64_t n_values, uint64_t n_bytes);
 /* Options of a context (RR_CTX_* flags; 0 by default).  RR_CTX_NO_SMALL: every call takes the
  * batch pipeline, also a batch small enough for the one-launch kernels (at most 4096 values in
