@@ -1469,7 +1469,9 @@ __global__ __launch_bounds__(SMALL_NT) void decode_small_kernel(const uint8_t *_
             if (arena && g >= a0 && g < a1) reinterpret_cast<u32x4 *>(arena)[g] = gx[k];
         }
     }
-    __syncthreads();
+    // LDS-only barriers from here to the fixup: __syncthreads() would wait for the arena stores'
+    // acknowledgements — a PCIe round trip when the arena is the host entry point's mapped staging
+    lds_barrier();
     const lds_cptr S = (lds_cptr)stage;
     // 2. reservations and walk classes from the headers (count_kernel's rule) and their block scan
     uint64_t r[SMALL_VPT], sum = 0;
@@ -1502,7 +1504,7 @@ __global__ __launch_bounds__(SMALL_NT) void decode_small_kernel(const uint8_t *_
             for (uint32_t j = 0; j < SMALL_VPT; ++j)
                 if (v0 + j < n) { s_cls[v0 + j] = cl[j]; s_eb[v0 + j] = eb; s_r[v0 + j] = r[j]; eb += r[j]; }
         }
-        __syncthreads();
+        lds_barrier();
         const LdsSrc lsrc{S};
         for (uint32_t v = wave; v < n; v += SMALL_NT / RR_WAVE) {
             const uint32_t c = s_cls[v];
@@ -1537,9 +1539,13 @@ __global__ __launch_bounds__(SMALL_NT) void decode_small_kernel(const uint8_t *_
     bad = wave_sum_fast(bad);
     pay = wave_sum_fast(pay);
     if (lane == 0) { red[0][wave] = bad; red[1][wave] = pay; }
-    __syncthreads();   // (also: every record and descriptor visible to the workgroup, for the fixup)
-    // 4. marked values (duplicate keys, unsorted skiplists), in the stage's LDS
-    if (nfix) fixup_window<SMALL_NT>(blob, 0, n, values, elems, &s_tot, stage);
+    lds_barrier();
+    // 4. marked values (duplicate keys, unsorted skiplists), in the stage's LDS, once every
+    //    record and descriptor is visible to the workgroup (a full barrier only then)
+    if (nfix) {
+        __syncthreads();
+        fixup_window<SMALL_NT>(blob, 0, n, values, elems, &s_tot, stage);
+    }
     if (tid == 0) {
         uint64_t tb = 0, tp = 0;
         for (uint32_t w = 0; w < SMALL_NT / RR_WAVE; ++w) { tb += red[0][w]; tp += red[1][w]; }
@@ -2680,8 +2686,10 @@ __global__ __launch_bounds__(SMALL_NT) void encode_small_kernel(const rr_value *
             a = b;
         }
     }
+    // (LDS-only barriers after the offsets stores: __syncthreads() would wait for their
+    // acknowledgements, a PCIe round trip when they go to the host entry point's mapped staging)
     if (wave_path) {
-        __syncthreads();
+        lds_barrier();
         for (uint32_t v = wave; v < n; v += SMALL_NT / RR_WAVE)
             if (s_at[v] != ~0ull) emit_value_wave(img, s_at[v], reinterpret_cast<const uint4 *>(values)[v], elems, arena);
     }
@@ -2690,7 +2698,7 @@ __global__ __launch_bounds__(SMALL_NT) void encode_small_kernel(const rr_value *
     pay = wave_sum_fast(pay);
     nel = wave_sum_fast(nel);
     if (lane == 0) { red[0][wave] = bad; red[1][wave] = pay; red[2][wave] = nel; }
-    __syncthreads();
+    lds_barrier();
     // the image out: 16-byte stores, bytes at a partial end (as E4)
     const uint32_t full = (uint32_t)(lim >> 4);
     for (uint32_t c = tid; c < full; c += SMALL_NT) reinterpret_cast<uint4 *>(out)[c] = reinterpret_cast<const uint4 *>(img)[c];
