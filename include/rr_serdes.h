@@ -13,7 +13,9 @@
  * Conventions:
  *   - return value: RR_API_OK (0) or a negative RR_API_E* code for the whole call;
  *   - per-value status in rr_value.status (0 = OK), counted into rr_totals.n_bad;
- *   - caller-owned buffers; one rr_ctx per host thread; no hidden host synchronisation in the
+ *   - caller-owned buffers; one rr_ctx per host thread, and a context's calls never run at the
+ *     same time on the device (one stream, or streams the caller orders): they share the
+ *     context's scratch and its zero-between-calls sums; no hidden host synchronisation in the
  *     device entry points (graph-capturable after rr_ctx_reserve: decode = 2 kernels,
  *     encode = 3 kernels, a batch of at most 4096 values in at most 128 KiB = ONE kernel; all
  *     on the caller's stream).  The only wait is when the context's scratch must grow: it

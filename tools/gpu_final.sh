@@ -1,10 +1,7 @@
 #!/bin/bash
-# One GPU call: the parity subset, an encode A/B against librr_serdes_prev.so, then the round's
-# evidence (profiles, PMC, bench lines) and BASELINE.md's per-config rows.
+# Round-end check on the GPU box (repo root): the GPU suite, smoke(), and one default bench line.
 set -e
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/test_gpu_encode.py tests/test_gpu_parity.py -m gpu -x -q --timeout 240 \
-    --timeout-method thread -k "not config5 and not 10m" > gpurun_out/t.log 2>&1 && tail -1 gpurun_out/t.log
-[ -f redrock_old_amd/librr_serdes_prev.so ] && bash tools/ab_encode.sh "prev" "4 3" > /dev/null && cat gpurun_out/ab_enc.log
-bash tools/round_evidence.sh ${1:-r3}
-bash tools/baseline_table.sh
+timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 240 --timeout-method thread > gpurun_out/final_tests.log 2>&1; grep -E "passed|failed" gpurun_out/final_tests.log | tail -3
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/final_smoke.log 2>&1; tail -1 gpurun_out/final_smoke.log
+timeout -k 10 600 python -u bench.py --steps 20 --warmup 5 > gpurun_out/final_bench.log 2>&1; grep '^{' gpurun_out/final_bench.log | tail -1 | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], d['roofline']['frac'], d['encode']['gib_s'])"
