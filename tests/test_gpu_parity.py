@@ -119,6 +119,36 @@ def test_list_integer_parsing(engine):
     assert np.array_equal(out, data[:int(offs[-1])])
 
 
+def test_list_counts_staged_and_far(engine):
+    """count_kernel walks a List's length chain from an LDS stage of 4 KiB a wave (Lists packed
+    in lane order, several packs a wave) and walks longer Lists from global memory: Lists from
+    empty to ~40 KiB, truncated and overlong length fields, dense runs of Lists that take several
+    packs, all interleaved with strings — records and descriptors equal the oracle's."""
+    rng = np.random.default_rng(31)
+    blobs = []
+    for i in range(3000):
+        r = rng.random()
+        if r < 0.25:
+            blobs.append(bytes([0, 1, 0, 0, 0, 0]) + rng.integers(0, 256, int(rng.integers(0, 80))).astype(np.uint8).tobytes())
+            continue
+        k = int(rng.integers(0, 40)) if r < 0.9 else int(rng.integers(200, 2000))
+        b = bytes([14]) + struct.pack("<I", i & 0xFFFFFF)
+        for _ in range(k):
+            it = rng.integers(ord("a"), ord("z") + 1, int(rng.integers(0, 24))).astype(np.uint8).tobytes()
+            b += struct.pack("<I", len(it)) + it
+        m = rng.random()
+        if m < 0.03 and len(b) > 9:
+            b = b[:-int(rng.integers(1, 4))]                               # cut inside the last element
+        elif m < 0.06 and k:
+            b = b[:5] + struct.pack("<I", 0xFFFFFFF0) + b[9:]              # first length past the value
+        blobs.append(b)
+    data, offs = batch_from_blobs(blobs)
+    v, e, a, t = engine.decode_host(data, offs)
+    ov, oe, oa, ot = cpu.decode(data, offs)
+    assert t == ot
+    assert_flat_equal((v, e), (ov, oe), "lists staged / far")
+
+
 def test_empty_batch(engine):
     v, e, a, t = engine.decode_host(np.zeros(16, np.uint8), np.zeros(1, np.uint64))
     assert len(v) == 0 and t["n_elems"] == 0 and t["n_bad"] == 0
