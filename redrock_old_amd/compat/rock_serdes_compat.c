@@ -346,7 +346,7 @@ typedef struct {
     rr_value *vals;
     rr_elem *els;
     uint8_t *arena;
-    uint64_t nv, ne, na, cap_e, cap_a, out_bound;
+    uint64_t nv, ne, na, cap_v, cap_e, cap_a, out_bound;
 } flat_t;
 
 static rr_elem *add_elem(flat_t *f) {
@@ -468,21 +468,36 @@ static void flatten(flat_t *f, robj *o) {
     v->n_elems = (uint32_t)(f->ne - v->elem_base);
 }
 
+/* The serialize path's buffers, per thread and kept across calls (they only grow): the
+ * evictor's per-key serObject allocates nothing here after its first calls. */
+static __thread flat_t t_flat;
+static __thread uint64_t *t_offs;
+static __thread uint8_t *t_data;
+static __thread size_t t_offs_cap, t_data_cap;
+
 void rr_compat_ser_batch(robj *const *objs, size_t n, sds *out) {
     if (n == 0) return;
-    flat_t f;
-    memset(&f, 0, sizeof f);
-    f.vals = zmalloc(sizeof(rr_value) * n);
-    for (size_t i = 0; i < n; i++) flatten(&f, objs[i]);
-    uint64_t *offs = zmalloc(sizeof(uint64_t) * (n + 1));
-    uint8_t *data = zmalloc(f.out_bound + 16);
+    flat_t *f = &t_flat;
+    f->nv = f->ne = f->na = f->out_bound = 0;
+    if (n > f->cap_v) {
+        f->vals = zrealloc(f->vals, sizeof(rr_value) * n);
+        f->cap_v = n;
+    }
+    for (size_t i = 0; i < n; i++) flatten(f, objs[i]);
+    if (n + 1 > t_offs_cap) {
+        t_offs = zrealloc(t_offs, sizeof(uint64_t) * (n + 1));
+        t_offs_cap = n + 1;
+    }
+    if (f->out_bound + 16 > t_data_cap) {
+        t_data = zrealloc(t_data, f->out_bound + 16);
+        t_data_cap = f->out_bound + 16;
+    }
     rr_totals t;
-    if (rr_encode_batch_host(engine(), f.vals, f.els, f.ne, f.arena, f.na, n, data, f.out_bound + 16, offs, &t) !=
-        RR_API_OK)
+    if (rr_encode_batch_host(engine(), f->vals, f->els, f->ne, f->arena, f->na, n, t_data, f->out_bound + 16, t_offs,
+                             &t) != RR_API_OK)
         serverPanic("serObject: %s", rr_last_error());
     if (t.n_bad) serverPanic("serObject: %llu unencodable objects", (unsigned long long)t.n_bad);
-    for (size_t i = 0; i < n; i++) out[i] = sdsnewlen(data + offs[i], offs[i + 1] - offs[i]);
-    zfree(offs); zfree(data); zfree(f.vals); zfree(f.els); zfree(f.arena);
+    for (size_t i = 0; i < n; i++) out[i] = sdsnewlen(t_data + t_offs[i], t_offs[i + 1] - t_offs[i]);
 }
 
 sds serObject(robj *o) {
