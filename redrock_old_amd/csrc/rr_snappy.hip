@@ -489,7 +489,7 @@ __device__ __forceinline__ uint32_t match_len(const Frag &F, uint32_t a, uint32_
 #ifndef RR_SNZ_K   // most probes a compressor step-1 round evaluates at once (1: the serial loop)
 #define RR_SNZ_K 16
 #endif
-__device__ void compress_fragment(const Frag &F, uint32_t fn, lds_u16 *table, uint32_t ts, lds_u32 *mark, Out &O) {
+__device__ void compress_fragment(const Frag &F, uint32_t fn, lds_u16 *table, uint32_t ts, Out &O) {
     const uint32_t shift = 32 - log2floor(ts);
     uint32_t ip = 0, next_emit = 0;
     if (fn >= MARGIN) {
@@ -548,9 +548,15 @@ __device__ void compress_fragment(const Frag &F, uint32_t fn, lds_u16 *table, ui
                     const uint32_t sl = stop ? (uint32_t)__builtin_ctzll(stop) : K;
                     const bool hit = sl < K && ((__ballot(m) >> sl) & 1);
                     const bool commit = act && (lane < sl || (hit && lane == sl));
-                    mark[lane] = 0;
-                    if (commit && prev >= 0) mark[prev] = 1;
-                    if (commit && !mark[lane]) table[H] = (uint16_t)P;
+                    // the table gets each hash's last committing lane: every committing lane
+                    // with an earlier same-hash lane tells that lane it was overwritten — a
+                    // forward permute through the LDS crossbar, no LDS memory (a lane no one
+                    // writes reads 0: tools/micro/permute_probe.hip); the others send to lane
+                    // 63, which no round uses (K < 64).  (A 256-byte mark array in LDS held
+                    // the compressor at 4 waves per CU: 29.9 -> 30.5 GB/s on config 4.)
+                    const bool tell = commit && prev >= 0;
+                    const int over = __builtin_amdgcn_ds_permute((tell ? prev : (int)WAVE - 1) * 4, tell ? 1 : 0);
+                    if (commit && !over) table[H] = (uint16_t)P;
                     if (sl < K) {
                         if (!hit) goto remainder;
                         ip = rdl(P, sl);
@@ -610,7 +616,6 @@ __global__ __launch_bounds__(WAVE) void snz_comp_kernel(const uint8_t *__restric
     extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
     lds_u16 *table = (lds_u16 *)sm;
     lds_u8 *ib = (lds_u8 *)sm + 2 * TAB_MAX;
-    lds_u32 *mark = (lds_u32 *)(sm + 2 * TAB_MAX + SNZ_FRAG_LDS);   // WAVE words
     const uint32_t lane = lane_id();
     for (uint64_t b = blockIdx.x; b < n; b += gridDim.x) {
         const uint64_t c0 = in_offs[b], len = in_offs[b + 1] - c0;
@@ -644,7 +649,7 @@ __global__ __launch_bounds__(WAVE) void snz_comp_kernel(const uint8_t *__restric
                 for (uint32_t k = lane; k < nd; k += WAVE)
                     ((lds_u32 *)ib)[k] = __builtin_amdgcn_raw_buffer_load_b32(F.R, (int)(a0 + 4 * k), 0, 0);
             }
-            compress_fragment(F, fn, table, ts, mark, O);
+            compress_fragment(F, fn, table, ts, O);
         }
         if (lane == 0) sizes[b] = O.op;
     }
@@ -722,7 +727,7 @@ extern "C" hipError_t rr_launch_snappy_compress(const uint8_t *in, uint64_t in_c
     hipError_t e = rr_launch_scan_u64(slot_offs, n, lb, err, stream);
     if (e != hipSuccess) return e;
     if (n) {
-        const uint32_t smem = 2 * TAB_MAX + SNZ_FRAG_LDS + 4 * WAVE;
+        const uint32_t smem = 2 * TAB_MAX + SNZ_FRAG_LDS;   // (5 waves per CU at the default fragment size)
         hipLaunchKernelGGL(snz_comp_kernel, dim3(grid_for(n, 1u << 20)), dim3(WAVE), smem, stream, in, in_cap, in_offs, n, slots,
                            (const uint64_t *)slot_offs, out_offs, SNZ_FRAG_LDS);
     }
