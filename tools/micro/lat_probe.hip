@@ -160,6 +160,44 @@ int main() {
     }
     CK(hipMemcpy(dblob, hb.data + hb.offsets[0], len, hipMemcpyHostToDevice));
     CK(hipMemcpy(doff, o, 16, hipMemcpyHostToDevice));
+    // 4c. the one-launch encode kernel of the same value (its flat form from the decode above),
+    //     device buffers, HIP events; and a host-mapped completion word instead (launch + spin)
+    CK(rr_launch_decode_small(dblob, doff, 1, dval, del, 4096, NULL, (len + 15) & ~15ull, dtot, NULL, 0, s));
+    CK(hipStreamSynchronize(s));
+    rr_totals dt;
+    CK(hipMemcpy(&dt, dtot, sizeof dt, hipMemcpyDeviceToHost));
+    uint8_t *dout;
+    uint64_t *dooff;
+    CK(hipMalloc((void **)&dout, 1 << 16));
+    CK(hipMalloc((void **)&dooff, 16));
+    for (int i = 0; i < K; ++i) {
+        CK(hipEventRecord(e0, s));
+        CK(rr_launch_encode_small(dval, del, dt.n_elems, dblob, len, 1, dout, (len + 15) & ~15ull, dooff, dtot, NULL, 0, s));
+        CK(hipEventRecord(e1, s));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        t[i] = ms * 1e3;
+    }
+    const double enc_kernel = med(t, K);
+    for (int i = 0; i < K; ++i) {
+        const uint32_t seq = (uint32_t)(K + i) + 1;
+        const double t0 = now_us();
+        CK(rr_launch_encode_small(dval, del, dt.n_elems, dblob, len, 1, dout, (len + 15) & ~15ull, dooff, dtot, df, seq, s));
+        while (*(volatile uint32_t *)hf != seq) {}
+        t[i] = now_us() - t0;
+    }
+    CK(hipStreamSynchronize(s));
+    const double enc_spin = med(t, K);
+    for (int i = 0; i < K; ++i) {
+        const uint32_t seq = (uint32_t)(2 * K + i) + 1;
+        const double t0 = now_us();
+        CK(rr_launch_decode_small(dblob, doff, 1, dval, del, 4096, NULL, (len + 15) & ~15ull, dtot, df, seq, s));
+        while (*(volatile uint32_t *)hf != seq) {}
+        t[i] = now_us() - t0;
+    }
+    CK(hipStreamSynchronize(s));
+    const double dec_spin = med(t, K);
     // 5. the same through the host entry point (pinned mapped staging)
     rr_ctx *ctx;
     if (rr_ctx_create(0, &ctx) != RR_API_OK) return 4;
@@ -176,8 +214,9 @@ int main() {
     printf("{\"empty_launch_sync_us\": %.2f, \"launch_call_us\": %.2f, \"empty_launch_spin_us\": %.2f, "
            "\"decode_small_device_us\": %.2f, \"decode_small_kernel_event_us\": %.2f, \"decode_host_n1_us\": %.2f, "
            "\"value_bytes\": %llu, \"kernel_us_cfg1\": %.2f, \"kernel_us_cfg3\": %.2f, \"kernel_us_cfg4\": %.2f, "
-           "\"empty_event_us\": %.2f, \"empty1024_lds_event_us\": %.2f}\n",
+           "\"empty_event_us\": %.2f, \"empty1024_lds_event_us\": %.2f, \"encode_small_kernel_event_us\": %.2f, "
+           "\"encode_small_device_spin_us\": %.2f, \"decode_small_device_spin_us\": %.2f}\n",
            launch_sync, launch_only, launch_spin, small_dev, small_kernel, host_small, (unsigned long long)len,
-           per_cfg[0], per_cfg[1], per_cfg[2], ev_empty[0], ev_empty[1]);
+           per_cfg[0], per_cfg[1], per_cfg[2], ev_empty[0], ev_empty[1], enc_kernel, enc_spin, dec_spin);
     return 0;
 }
