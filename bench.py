@@ -11,7 +11,13 @@ bytes per launch / launch time vs 8 TB/s HBM3E) and, on rank 0 at N=1, the CPU b
 reference-faithful desObject restatement (oracle/rro_faithful.c) on the box's host cores.
 
 Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--n VALUES] [--config 4]
-Multi-GPU: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+Multi-GPU: `python bench.py --gpus N` starts its N ranks itself (one process per GPU, a
+torch.distributed.run child process started before anything touches the GPU; this process only
+waits for it and exits with its code), or run it under an outside launcher:
+python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+(WORLD_SIZE must then equal --gpus).  `--plan-only` prints the launch decision and the rank
+layout without any GPU call; `--launch-check` runs the N ranks over gloo on the CPU and has rank
+0 print the ranks that joined (tests/test_bench_launch.py).
 """
 import argparse
 import json
@@ -51,19 +57,82 @@ def parse():
     p.add_argument("--no-snappy", action="store_true", help="skip the snappy block-compression leg (row f3)")
     p.add_argument("--profile-only", action="store_true", help="decode steps only (for rocprofv3)")
     p.add_argument("--profile-encode", action="store_true", help="one decode, then encode steps only (for rocprofv3)")
+    p.add_argument("--plan-only", action="store_true", help="print the launch decision and rank layout, no GPU call")
+    p.add_argument("--launch-check", action="store_true",
+                   help="start the ranks as the bench would, join them over gloo on the CPU, report who joined")
     return p.parse_args()
+
+
+def launch_plan(gpus, env):
+    """How this process runs `--gpus N`: "direct" when it is already one rank of a job (WORLD_SIZE
+    set by an outside launcher; it must equal N) or N = 1; "spawn" when it must start the N ranks
+    itself.  Returns (plan dict, error string or None).  Pure: no GPU call, no torch import."""
+    ws = env.get("WORLD_SIZE")
+    if gpus < 1:
+        return None, f"--gpus {gpus}: need at least one GPU"
+    if ws is not None:
+        world = int(ws)
+        if world != gpus:
+            return None, f"WORLD_SIZE={world} but --gpus {gpus}: the launcher and the bench disagree"
+        return {"launch": "direct", "world": world, "rank": int(env.get("RANK", "0")),
+                "local_rank": int(env.get("LOCAL_RANK", "0"))}, None
+    if gpus == 1:
+        return {"launch": "direct", "world": 1, "rank": 0, "local_rank": 0}, None
+    return {"launch": "spawn", "world": gpus, "ranks": [{"rank": r, "local_rank": r, "device": f"cuda:{r}"}
+                                                         for r in range(gpus)]}, None
+
+
+def spawn_ranks(gpus, argv):
+    """Start `gpus` ranks of this script as one torch.distributed.run child process (a child, not
+    an exec: nothing here has touched the GPU, and the ranks are fresh processes), on 127.0.0.1
+    with a free port; returns the child's exit code."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + argv
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # (dmabuf IPC only on these hosts)
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def launch_check(world, rank):
+    """--launch-check inside a rank: join the job over gloo (no GPU) and report the ranks."""
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo")
+    t = torch.tensor([rank], dtype=torch.int64)
+    got = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(got, t)
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "world": dist.get_world_size(), "n_gpus": world,
+                          "ranks": [int(x.item()) for x in got]}), flush=True)
+    dist.destroy_process_group()
 
 
 def main():
     args = parse()
+    plan, err = launch_plan(args.gpus, os.environ)
+    if err:
+        print(f"bench.py: {err}", file=sys.stderr)
+        sys.exit(2)
+    if args.plan_only:
+        print(json.dumps(plan), flush=True)
+        return
+    if plan["launch"] == "spawn":   # before any GPU call: the ranks are fresh processes
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
+    if args.launch_check:
+        launch_check(plan["world"], plan["rank"])
+        return
     import torch
     import torch.distributed as dist
 
     import redrock_old_amd as rr
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    world, rank, local = plan["world"], plan["rank"], plan["local_rank"]
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))

@@ -120,6 +120,8 @@ def lib():
     L.rr_ctx_reserve.argtypes = [vp, u64, u64]
     if hasattr(L, "rr_ctx_set_options"):   # (RR_LIB: an older build for A/B timing may predate it)
         L.rr_ctx_set_options.argtypes = [vp, C.c_uint]
+    if hasattr(L, "rr_debug_fail_second"):   # test hook, not in rr_serdes.h
+        L.rr_debug_fail_second.argtypes = [vp]
     L.rr_last_error.restype = C.c_char_p
     L.rr_decode_batch.argtypes = [vp, C.POINTER(BlobBatch), C.POINTER(FlatBatch), vp, vp]
     L.rr_encode_batch.argtypes = [vp, C.POINTER(FlatBatch), C.POINTER(BlobBatch), vp, vp]
@@ -297,6 +299,10 @@ class Engine:
     def set_options(self, flags: int):
         """RR_CTX_* flags (CTX_NO_SMALL: every call takes the batch pipeline)."""
         _check(self._L.rr_ctx_set_options(self._ctx, flags))
+
+    def debug_fail_second(self):
+        """Test hook: the next pipeline call launches only its first kernel and fails."""
+        _check(self._L.rr_debug_fail_second(self._ctx))
 
     def reserve(self, n: int, nbytes: int = 0):
         _check(self._L.rr_ctx_reserve(self._ctx, n, nbytes))

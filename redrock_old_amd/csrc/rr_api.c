@@ -5,10 +5,12 @@
  * (a hipMemsetAsync of the look-back words + one kernel, no host sync) and host-pointer
  * variants that stage through pinned buffers and the context's device buffers.
  */
+#include <sched.h>
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "rr_internal.h"
 
@@ -113,10 +115,20 @@ int rr_ensure_scratch(rr_ctx *c, uint64_t words, hipStream_t stream) {
  * so no zeroing launch runs per call.  Zeroed once when (re)allocated:
  * like the scratch, growing waits on the previous call and is refused under graph capture. */
 static int ensure_dsums(rr_ctx *c, uint64_t words, hipStream_t stream) {
-    if (c->dsums && words <= c->dsums_words) return RR_API_OK;
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (stream && hipStreamIsCapturing(stream, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
-        return fail(RR_API_EINVAL, "decode sums too small under graph capture: call rr_ctx_reserve first");
+    const int capturing = stream && hipStreamIsCapturing(stream, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
+    if (c->dsums && words <= c->dsums_words) {
+        /* an earlier call failed between its two kernels (a launch error, a stream error seen
+         * by the host entry points): the sums it left behind would shift every later call's
+         * slots and offsets, so zero them once before the next call (not under capture: a
+         * memset node would re-zero on every replay, which is harmless but not what was asked) */
+        if (c->dsums_dirty && !capturing) {
+            HIPCHK(hipMemsetAsync(c->dsums, 0, c->dsums_words * sizeof(uint64_t), stream));
+            c->dsums_dirty = 0;
+        }
+        return RR_API_OK;
+    }
+    if (capturing) return fail(RR_API_EINVAL, "decode sums too small under graph capture: call rr_ctx_reserve first");
     HIPCHK(hipSetDevice(c->device));
     if (c->dsums) {
         if (c->scratch_used) HIPCHK(hipEventSynchronize(c->scratch_done));
@@ -130,6 +142,7 @@ static int ensure_dsums(rr_ctx *c, uint64_t words, hipStream_t stream) {
     HIPCHK(hipMemsetAsync(c->dsums, 0, want * sizeof(uint64_t), stream));
     if (!stream) HIPCHK(hipStreamSynchronize(NULL));
     c->dsums_words = want;
+    c->dsums_dirty = 0;
     return RR_API_OK;
 }
 
@@ -147,6 +160,14 @@ int rr_mark_scratch(rr_ctx *c, hipStream_t stream) {
 int rr_ctx_set_options(rr_ctx *c, unsigned flags) {
     if (!c || (flags & ~RR_CTX_NO_SMALL)) return fail(RR_API_EINVAL, "rr_ctx_set_options: bad argument");
     c->options = flags;
+    return RR_API_OK;
+}
+/* test hook (not in rr_serdes.h): the context's next pipeline decode or encode launches only
+ * its first kernel and fails, leaving the zero-between-calls sums as a failed second launch or
+ * an aborted stream would (tests/test_gpu_small.py) */
+int rr_debug_fail_second(rr_ctx *c) {
+    if (!c) return fail(RR_API_EINVAL, "ctx is NULL");
+    c->fail_second = 1;
     return RR_API_OK;
 }
 #define SMALL_DEC(c, n, cap) (!((c)->options & RR_CTX_NO_SMALL) && rr_small_decode_fits((n), (cap)))
@@ -187,9 +208,18 @@ int rr_decode_batch(rr_ctx *c, const rr_blob_batch *in, rr_flat_batch *out, rr_t
     int rc = ensure_scratch(c, rr_decode_scratch_words(in->data_cap, in->n), (hipStream_t)stream);
     if (!rc) rc = ensure_dsums(c, rr_decode_sums_words(in->data_cap), (hipStream_t)stream);
     if (rc) return rc;
-    HIPCHK(rr_launch_decode(in->data, in->offsets, in->n, out->values, out->elems, out->elem_cap, out->arena,
-                            c->scratch, c->dsums, in->data_cap, d_totals, (hipStream_t)stream));
-    return mark_scratch(c, (hipStream_t)stream);
+    const int first_only = c->fail_second;
+    c->fail_second = 0;
+    const hipError_t e = rr_launch_decode(in->data, in->offsets, in->n, out->values, out->elems, out->elem_cap,
+                                          out->arena, c->scratch, c->dsums, in->data_cap, d_totals, (hipStream_t)stream,
+                                          first_only);
+    rc = mark_scratch(c, (hipStream_t)stream);
+    if (e != hipSuccess || first_only) {
+        c->dsums_dirty = 1;
+        return first_only ? fail(RR_API_EHIP, "decode: second launch withheld (rr_debug_fail_second)")
+                          : fail(RR_API_EHIP, "decode launch: %s", hipGetErrorString(e));
+    }
+    return rc;
 }
 
 int rr_encode_batch(rr_ctx *c, const rr_flat_batch *in, rr_blob_batch *out, rr_totals *d_totals, void *stream) {
@@ -208,9 +238,18 @@ int rr_encode_batch(rr_ctx *c, const rr_flat_batch *in, rr_blob_batch *out, rr_t
     int rc = ensure_scratch(c, rr_encode_scratch_words(in->n, out->data_cap), (hipStream_t)stream);
     if (!rc) rc = ensure_dsums(c, rr_encode_sums_words(in->n), (hipStream_t)stream);
     if (rc) return rc;
-    HIPCHK(rr_launch_encode(in->values, in->elems, in->elem_cap, in->arena, in->arena_cap, in->n, out->data,
-                            out->data_cap, out->offsets, c->scratch, c->dsums, d_totals, (hipStream_t)stream));
-    return mark_scratch(c, (hipStream_t)stream);
+    const int first_only = c->fail_second;
+    c->fail_second = 0;
+    const hipError_t e = rr_launch_encode(in->values, in->elems, in->elem_cap, in->arena, in->arena_cap, in->n,
+                                          out->data, out->data_cap, out->offsets, c->scratch, c->dsums, d_totals,
+                                          (hipStream_t)stream, first_only);
+    rc = mark_scratch(c, (hipStream_t)stream);
+    if (e != hipSuccess || first_only) {
+        c->dsums_dirty = 1;
+        return first_only ? fail(RR_API_EHIP, "encode: second launch withheld (rr_debug_fail_second)")
+                          : fail(RR_API_EHIP, "encode launch: %s", hipGetErrorString(e));
+    }
+    return rc;
 }
 
 /* diagnostics (tools/time_copy.py; not in rr_serdes.h): one of the copy kernel's shapes */
@@ -352,6 +391,7 @@ static int decode_host_pipelined(rr_ctx *c, const uint8_t *data, const uint64_t 
     if (rc) return rc;
     rc = decode_host_pipelined_run(c, data, offsets, n, values, elems, elem_cap, arena, totals, bytes, pbytes, cut, K);
     if (rc != RR_API_OK && rc != 1) {
+        c->dsums_dirty = 1;   /* a chunk's kernels may not all have run */
         (void)hipStreamSynchronize(c->up);
         (void)hipStreamSynchronize(c->down);
         (void)hipStreamSynchronize(c->stream);
@@ -382,15 +422,27 @@ static int small_grow(rr_ctx *c, size_t need) {
  * rr_kernels.hip) instead of a stream synchronisation.  The stream is polled now and then, so a
  * kernel that faulted (the stream reports an error) or ended without the word cannot hang it. */
 static int small_wait(rr_ctx *c, const uint32_t *flag, uint32_t seq) {
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    int yielding = 0;
     for (uint64_t k = 1;; ++k) {
         if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq) return RR_API_OK;
-        if ((k & 4095) == 0) {
+        /* spin ~50 us (a lone call's kernel ends well inside it), then give the core away
+         * between polls: behind another context's long batch the caller (the Redis main
+         * thread, through the shim) must not burn a core until that batch drains */
+        if (yielding) sched_yield();
+        else if ((k & 255) == 0) {
+            clock_gettime(CLOCK_MONOTONIC, &t1);
+            yielding = (t1.tv_sec - t0.tv_sec) * 1000000000L + (t1.tv_nsec - t0.tv_nsec) > 50000L;
+        }
+        if ((k & 4095) == 0 || (yielding && (k & 63) == 0)) {
             const hipError_t q = hipStreamQuery(c->stream);
             if (q == hipSuccess) {
                 if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq) return RR_API_OK;
                 return fail(RR_API_EDEVICE, "one-launch kernel ended without its completion word");
             }
             if (q != hipErrorNotReady) {
+                c->dsums_dirty = 1;   /* (an earlier pipeline call on the stream may have stopped midway) */
                 (void)hipGetLastError();
                 return fail(RR_API_EDEVICE, hipGetErrorString(q));
             }
@@ -627,6 +679,7 @@ static int encode_host_pipelined(rr_ctx *c, const rr_value *values, const rr_ele
     rc = encode_host_pipelined_run(c, values, elems, n_elems, arena, arena_bytes, n, data, data_cap, offsets, totals,
                                    cut, eneed, m);
     if (rc != RR_API_OK) {   /* transfers in flight must not outlive the call */
+        c->dsums_dirty = 1;   /* a chunk's kernels may not all have run */
         (void)hipStreamSynchronize(c->up);
         (void)hipStreamSynchronize(c->aux);
         (void)hipStreamSynchronize(c->down);

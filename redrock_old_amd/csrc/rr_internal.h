@@ -17,6 +17,8 @@ struct rr_ctx {
     int scratch_used;
     uint64_t *dsums;             /* the decode's window/group sums: zero between calls */
     uint64_t dsums_words;
+    int dsums_dirty;             /* a call's second kernel may not have run: re-zero dsums first */
+    int fail_second;             /* test hook (rr_debug_fail_second): the next pipeline call stops after its first kernel */
     /* device staging for host entry points */
     void *d_in, *d_off, *d_vals, *d_elems, *d_arena, *d_out, *d_ooff;
     size_t c_in, c_off, c_vals, c_elems, c_arena, c_out, c_ooff;

@@ -20,13 +20,14 @@ extern "C" {
 /* sums: rr_decode_sums_words(data_cap) words that are zero on entry and are zero again when the
  * call's kernels end (decode_kernel's last workgroup restores them): the context keeps them in
  * a buffer of their own, zeroed once when allocated */
+/* first_only (test hook): launch only the first kernel, which leaves the sums non-zero */
 hipError_t rr_launch_decode(const uint8_t *blob, const uint64_t *offsets, uint64_t n, rr_value *values,
                             rr_elem *elems, uint64_t elem_cap, uint8_t *arena, uint64_t *scratch, uint64_t *sums,
-                            uint64_t data_cap, rr_totals *totals, hipStream_t stream);
+                            uint64_t data_cap, rr_totals *totals, hipStream_t stream, int first_only);
 uint64_t rr_decode_sums_words(uint64_t data_cap);
 hipError_t rr_launch_encode(const rr_value *values, const rr_elem *elems, uint64_t elem_cap, const uint8_t *arena,
                             uint64_t arena_cap, uint64_t n, uint8_t *out, uint64_t cap, uint64_t *offsets,
-                            uint64_t *scratch, uint64_t *sums, rr_totals *totals, hipStream_t stream);
+                            uint64_t *scratch, uint64_t *sums, rr_totals *totals, hipStream_t stream, int first_only);
 uint64_t rr_encode_sums_words(uint64_t n);
 uint64_t rr_decode_scratch_words(uint64_t data_cap, uint64_t n);
 uint64_t rr_scan_words(uint64_t n);

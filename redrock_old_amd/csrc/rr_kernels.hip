@@ -1415,15 +1415,24 @@ constexpr uint32_t SMALL_STAGE = SMALL_BYTES + 8192;   // + the reads past a val
 static_assert(FIX_LDS + 4 * (SMALL_NT + 1) <= SMALL_STAGE, "the fixup reuses the stage");
 
 // The host entry points wait for a one-launch kernel by spinning on a word of their mapped
-// staging instead of a stream synchronisation (~4 us less per call): the workgroup barrier
-// waits for every wave's stores to be acknowledged, then ONE system-scope release (one L2
-// writeback) and one lane's store of the call's sequence number (a vector store).  (A system
-// fence in every thread — sixteen waves, sixteen L2 writebacks — cost ~8 us a call:
-// tools/micro/lat_probe.hip, launch + spin 19.4 us against 11.4 us between HIP events.)
+// staging instead of a stream synchronisation (~4 us less per call).  The producer form of
+// MI355X_MICROARCH.md (inter-workgroup visibility, "valid forms"): every wave waits for its
+// OWN stores to be acknowledged (s_waitcnt vmcnt(0): on gfx950 __syncthreads() is a bare
+// s_barrier that waits for nothing in flight), then the barrier, so lane 0 signals only after
+// every wave's records, descriptors and totals have landed; lane 0's ONE system-scope release
+// (one L2 writeback), an explicit vmcnt(0) wait after it (the compiler may drop its own wait
+// after the writeback when the scoreboard looks empty), and the store of the call's sequence
+// number.  (A system fence in every thread — sixteen waves, sixteen L2 writebacks — cost ~8 us
+// a call: tools/micro/lat_probe.hip, launch + spin 19.4 us against 11.4 us between HIP events.)
 __device__ __forceinline__ void signal_done(uint32_t *done, uint32_t seq) {
     if (!done) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_store(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // (system scope)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(done, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 __global__ __launch_bounds__(SMALL_NT) void decode_small_kernel(const uint8_t *__restrict__ blob,
@@ -2846,7 +2855,8 @@ extern "C" uint64_t rr_decode_sums_words(uint64_t data_cap) {
 
 extern "C" hipError_t rr_launch_decode(const uint8_t *blob, const uint64_t *offsets, uint64_t n, rr_value *values,
                                        rr_elem *elems, uint64_t elem_cap, uint8_t *arena, uint64_t *scratch,
-                                       uint64_t *sums, uint64_t data_cap, rr_totals *totals, hipStream_t stream) {
+                                       uint64_t *sums, uint64_t data_cap, rr_totals *totals, hipStream_t stream,
+                                       int first_only) {
     const uint32_t win = dec_win(data_cap), nw = (uint32_t)(data_cap / win + 1);
     uint64_t *wtot = sums;
     uint64_t *gtot = wtot + nw;
@@ -2857,6 +2867,7 @@ extern "C" hipError_t rr_launch_decode(const uint8_t *blob, const uint64_t *offs
     uint8_t *cls = reinterpret_cast<uint8_t *>(first_off + nw + 1);
     hipLaunchKernelGGL(count_kernel, dim3((uint32_t)((n + 1 + 255) / 256)), dim3(256), 0, stream, blob, offsets, n,
                        first_val, first_off, nw, win, counts, cls, wtot, gtot, nullptr, 0u, totals);
+    if (first_only) return hipGetLastError();
     hipLaunchKernelGGL((DECODE_KERNEL), dim3(nw), dim3(DEC_NW * RR_WAVE), 0, stream, blob, data_cap, offsets, n,
                        first_val, first_off, cls, counts, wtot, gtot, values, elems, elem_cap, arena, nw, win, totals,
                        fin, (uint64_t)nw + dec_groups(nw) + 1);
@@ -2885,7 +2896,7 @@ extern "C" uint64_t rr_encode_sums_words(uint64_t n) { return (n + 255) / 256 / 
 extern "C" hipError_t rr_launch_encode(const rr_value *values, const rr_elem *elems, uint64_t elem_cap,
                                        const uint8_t *arena, uint64_t arena_cap, uint64_t n, uint8_t *out,
                                        uint64_t cap, uint64_t *offsets, uint64_t *scratch, uint64_t *sums,
-                                       rr_totals *totals, hipStream_t stream) {
+                                       rr_totals *totals, hipStream_t stream, int first_only) {
     if (n == 0) {
         hipError_t e = hipMemsetAsync(offsets, 0, sizeof(uint64_t), stream);
         if (e == hipSuccess && totals) e = hipMemsetAsync(totals, 0, sizeof(rr_totals), stream);
@@ -2899,6 +2910,7 @@ extern "C" hipError_t rr_launch_encode(const rr_value *values, const rr_elem *el
     uint32_t *fv = reinterpret_cast<uint32_t *>(btot + t);
     hipLaunchKernelGGL((enc_size_kernel<256, ENC_SIZE_U>), dim3(t), dim3(256), 0, stream, values, elems, n, elem_cap,
                        arena_cap, offsets, stats, btot, gtot, err, 1u, totals);
+    if (first_only) return hipGetLastError();
     hipLaunchKernelGGL(enc_index_kernel<ENC_W>, dim3(t), dim3(256), 0, stream, values, elems, n, elem_cap, arena_cap,
                        offsets, btot, gtot, cap, fv, nw, stats + 3 * (uint64_t)t);
     hipLaunchKernelGGL((enc_emit_kernel<ENC_W, ENC_NT, ENC_RCAP>), dim3((uint32_t)nw), dim3(ENC_NT), 0, stream,

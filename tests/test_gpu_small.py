@@ -185,3 +185,99 @@ def test_capacity_cuts(engine_small, engine):
     o2 = engine.encode_host(v, e, a, data_cap=dcap)
     assert np.array_equal(o1[1], o2[1]) and o1[2] == o2[2] and o1[2]["n_bad"] > 0
     assert o1[0].tobytes()[:dcap] == o2[0].tobytes()[:dcap]
+
+
+def test_golden_fixtures_one_per_call(engine_small):
+    """Every golden fixture (K1-K9 and the edge cases, malformed ones included) as its own n = 1
+    call — the route every desObject through the shim takes — against the hand-derived flat form."""
+    G = golden()
+    for f in G["kats"] + G["edges"]:
+        b = bytes.fromhex(f["blob"])
+        if not _fits([b]):
+            continue
+        data, offs = batch_from_blobs([b])
+        v, e, a, t = engine_small.decode_host(data, offs)
+        assert_flat_equal((v, e), expected_flat([f]), f.get("name", "fixture"))
+
+
+def test_handoff_under_uneven_load(engine_small):
+    """The one-launch kernels' completion hand-off (signal_done: every wave's stores
+    acknowledged, one system release, the flag) checked while a second context keeps the GPU
+    busy with 1M-value pipeline decodes on another stream: host-path decode and encode calls of
+    n = 1, 7, 63 and 4096 on one context, every record, descriptor, totals word, encoded byte and
+    offset against the oracle (MI355X_MICROARCH.md: test every hand-off under uneven load)."""
+    import torch
+    dev = torch.device("cuda:0")
+    load = rr.Engine(0)
+    load.set_options(rr.CTX_NO_SMALL)
+    ld, lo = rr.gen_batch(4, 1_000_000, seed=555)
+    d_data = torch.from_numpy(ld).to(dev)
+    d_offs = torch.from_numpy(lo.view(np.int64)).to(dev)
+    ln, lnb = len(lo) - 1, int(lo[-1])
+    d_vals = torch.empty(ln * 16, dtype=torch.uint8, device=dev)
+    d_elems = torch.empty(rr.elem_bound(ln, lnb) * 16, dtype=torch.uint8, device=dev)
+    d_arena = torch.empty(len(ld), dtype=torch.uint8, device=dev)
+    d_tot = torch.zeros(4, dtype=torch.int64, device=dev)
+    s = torch.cuda.Stream(dev)
+
+    def keep_busy():
+        if s.query():   # queue ~30 ms more whenever the loader's stream has drained
+            for _ in range(80):
+                load.decode_device(d_data, d_offs, d_vals, d_elems, d_arena, d_tot, stream=s)
+
+    # the cases: small batches of config-4 and edge values, with their oracle results
+    src = _blobs(4, 20000, seed=71) + _blobs(10, 400, seed=72)
+    tiny = [b for b in src if len(b) <= 30]
+    cases = []
+    for n, pool in ((1, src), (7, src), (63, [b for b in src if len(b) <= 1500]), (4096, tiny)):
+        for k in range(3):
+            part = pool[k * n:(k + 1) * n]
+            while part and not _fits(part):
+                part = part[:-1]
+            if len(part) < n:
+                continue
+            data, offs = batch_from_blobs(part)
+            ov, oe, oa, ot = cpu.decode(data, offs)
+            xo, xoffs, xt = cpu.encode(ov, oe, oa)
+            cases.append((f"n {n} #{k}", data, offs, (ov, oe, oa, ot), (xo, xoffs, xt)))
+    assert len(cases) >= 10
+    checked = 0
+    try:
+        for rep in range(6):
+            for what, data, offs, (ov, oe, oa, ot), (xo, xoffs, xt) in cases:
+                keep_busy()
+                v, e, a, t = engine_small.decode_host(data, offs)
+                assert_flat_equal((v, e), (ov, oe), what)
+                assert t == ot, (what, rep, t, ot)
+                if int(offs[-1]) + 16 <= rr.SMALL_BYTES:
+                    out, ooffs, t2 = engine_small.encode_host(ov, oe, oa, data_cap=int(offs[-1]) + 16)
+                    assert t2 == xt and np.array_equal(ooffs, xoffs) and np.array_equal(out, xo), (what, rep)
+                checked += 1
+        assert not s.query(), "the loader stream drained: the calls did not run beside a loaded GPU"
+    finally:
+        s.synchronize()
+        load.close()
+    assert checked == 6 * len(cases)
+
+
+def test_failed_second_launch_resets_sums(engine):
+    """A pipeline call that stops after its first kernel (a failed second launch, an aborted
+    stream) leaves the zero-between-calls window/group sums non-zero; the context re-zeroes
+    them before its next call, so later decodes and encodes are still exact."""
+    data, offs = rr.gen_batch(4, 20000, seed=31)
+    ov, oe, oa, ot = cpu.decode(data, offs)
+    engine.decode_host(data, offs)   # (the sums sized for this batch)
+    engine.debug_fail_second()
+    with pytest.raises(rr.RRError):
+        engine.decode_host(data, offs)
+    v, e, a, t = engine.decode_host(data, offs)
+    assert_flat_equal((v, e), (ov, oe), "decode after a withheld second launch")
+    assert t == ot
+    xo, xoffs, xt = cpu.encode(ov, oe, oa)
+    engine.debug_fail_second()
+    with pytest.raises(rr.RRError):
+        engine.encode_host(v, e, a)
+    out, ooffs, t2 = engine.encode_host(v, e, a)
+    assert t2 == xt and np.array_equal(ooffs, xoffs) and np.array_equal(out, xo)
+    v, e, a, t = engine.decode_host(data, offs)   # (and the decode after the encode's failure)
+    assert_flat_equal((v, e), (ov, oe), "decode after a withheld encode launch")
