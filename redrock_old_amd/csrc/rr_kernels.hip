@@ -1126,6 +1126,7 @@ __global__ __launch_bounds__(NW * RR_WAVE) __attribute__((amdgpu_waves_per_eu(DE
     __shared__ uint32_t next_batch, last_win;
     __shared__ uint64_t red[2][NW];
     PROBE(__shared__ uint64_t prb[PROBE_WORDS]; uint64_t pt0 = __builtin_amdgcn_s_memtime(), pt1 = 0, pt2 = 0;
+          const uint64_t prt0 = __builtin_amdgcn_s_memrealtime();
           if (threadIdx.x < PROBE_WORDS) prb[threadIdx.x] = 0;)
     const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid / RR_WAVE;
     const uint32_t tile = blockIdx.x;
@@ -1381,7 +1382,12 @@ __global__ __launch_bounds__(NW * RR_WAVE) __attribute__((amdgpu_waves_per_eu(DE
         // (plain stores, one writer each: no fold launch)
         if (tot && tile == 0) tot->bytes = offsets[n];
         if (tot && tile == nwin - 1) tot->n_elems = first_slot() + run + ctot;
+        // (timeline: start / end on the 100 MHz realtime clock, and where the workgroup ran:
+        //  HW_ID = wave, simd, pipe, CU, SH, SE bits; XCC_ID in bits 32+)
         PROBE(prb[0] = pt1 - pt0; prb[1] = pt2 - pt1; prb[2] = __builtin_amdgcn_s_memtime() - pt2; prb[28] = v_hi - v_lo;
+              prb[27] = prt0; prb[30] = __builtin_amdgcn_s_memrealtime();
+              prb[31] = (uint64_t)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11)) |
+                        ((uint64_t)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (15 << 11)) << 32);
               prb[29] = staged; if (g_probe) for (uint32_t i = 0; i < PROBE_WORDS; ++i) g_probe[(uint64_t)tile * PROBE_WORDS + i] = prb[i];)
         // the last window to finish (every other one has read its sums, at its start) zeroes
         // the call's sums and the counter for the next call: no zeroing launch per call.

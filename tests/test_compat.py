@@ -152,6 +152,27 @@ def test_rdb_flat_restore_on_gpu(tmp_path):
     assert "0 failures" in r.stdout
 
 
+def build_callpattern(tmp):
+    """tests/c/bench_callpattern.c: the shim inside the reference callers' patterns (evictor: k
+    serObject per cycle; restore: k desObject jobs), per-value shim vs batch forms vs the faithful
+    CPU restatement (the oracle, linked only into this bench)."""
+    exe = os.path.join(tmp, "bench_callpattern")
+    oracle = os.path.join(ROOT, "oracle")
+    cmd = ["gcc", "-std=gnu11", "-O2", "-Wall", "-Werror", "-Wno-unused-function", "-DRR_REDIS_TREE", "-pthread",
+           "-I", os.path.join(ROOT, "tests", "c", "miniredis"), "-I", os.path.join(ROOT, "include"), "-I", oracle,
+           os.path.join(ROOT, "redrock_old_amd", "compat", "rock_serdes_compat.c"),
+           os.path.join(ROOT, "tests", "c", "miniredis", "miniredis.c"),
+           os.path.join(ROOT, "tests", "c", "bench_callpattern.c"),
+           "-L", os.path.join(ROOT, "redrock_old_amd"), "-lrr_serdes", "-Wl,-rpath," + os.path.join(ROOT, "redrock_old_amd"),
+           "-L", oracle, "-lrr_oracle", "-Wl,-rpath," + oracle, "-lm", "-o", exe]
+    subprocess.run(cmd, check=True)
+    return exe
+
+
+def test_callpattern_bench_builds(tmp_path):
+    assert os.path.exists(build_callpattern(str(tmp_path)))
+
+
 def build_latency(tmp):
     """tests/c/bench_latency.c: per-call latency of desObject / serObject through the shim, the
     batch C-ABI with one value per call (one-launch kernels / pipeline), and the faithful CPU
@@ -184,13 +205,17 @@ def test_per_value_latency_path(tmp_path):
     assert line["roundtrip_bad"] == 0
 
 
-if __name__ == "__main__":   # python tests/test_compat.py bench [config k] | latency [config k]  (GPU box)
+if __name__ == "__main__":   # python tests/test_compat.py bench [config k] | latency [config k] | callpattern [config]  (GPU box)
     import sys
     import tempfile
     if sys.argv[1:2] == ["bench"]:   # keys/s of the restore paths
         with tempfile.TemporaryDirectory() as d:
             r = subprocess.run([build_rdb(d, bench=True), "bench"] + sys.argv[2:4], capture_output=True, text=True,
                                timeout=600)
+            print(r.stdout, r.stderr)
+    if sys.argv[1:2] == ["callpattern"]:   # the shim in the evictor / restore call patterns
+        with tempfile.TemporaryDirectory() as d:
+            r = subprocess.run([build_callpattern(d)] + sys.argv[2:3], capture_output=True, text=True, timeout=900)
             print(r.stdout, r.stderr)
     if sys.argv[1:2] == ["latency"]:   # per-call latency of the one-value signatures
         with tempfile.TemporaryDirectory() as d:

@@ -49,3 +49,8 @@ for c, nm in enumerate(names):
     if nbat:
         print(f"{nm:6s} batches {int(nbat):8d}  cycles/batch {p[:, 3 + c].sum() / nbat:9.0f}  "
               f"lanes/batch {p[:, 3 + 2 * NC + c].sum() / nbat:5.1f}")
+# the raw per-window words (timeline: [27] start / [30] end on the 100 MHz clock, [31] HW_ID |
+# XCC_ID << 32) for tools/timeline.py
+out = os.environ.get("PROBE_OUT")
+if out:
+    np.save(out, probe.cpu().numpy().reshape(nmax, 32)[:nwin])
