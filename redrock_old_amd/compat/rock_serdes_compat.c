@@ -15,6 +15,7 @@
 #ifndef RR_REDIS_TREE
 #define RR_REDIS_TREE 1
 #endif
+#include <poll.h>
 #include <pthread.h>
 #include <signal.h>
 #include <stdint.h>
@@ -80,8 +81,12 @@ static void *decode_service(void *arg) {
     sigemptyset(&pipe_set);
     sigaddset(&pipe_set, SIGPIPE);
     pthread_sigmask(SIG_BLOCK, &pipe_set, NULL);
+    /* the engine context only once the child's first request is there: the thread starts inside
+     * fork()'s prepare handler, and a child that never asks must cost no GPU context */
     rr_ctx *ctx = NULL;
-    if (rr_ctx_create(g_device, &ctx) == RR_API_OK) {
+    struct pollfd pf = {fd, POLLIN, 0};
+    char peek;
+    if (poll(&pf, 1, -1) > 0 && recv(fd, &peek, 1, MSG_PEEK) == 1 && rr_ctx_create(g_device, &ctx) == RR_API_OK) {
         rr_rdb_serve(fd, fd, echo_blob, NULL, NULL, ctx, 64);
         rr_ctx_destroy(ctx);
     }
@@ -498,6 +503,14 @@ void rr_compat_ser_batch(robj *const *objs, size_t n, sds *out) {
         serverPanic("serObject: %s", rr_last_error());
     if (t.n_bad) serverPanic("serObject: %llu unencodable objects", (unsigned long long)t.n_bad);
     for (size_t i = 0; i < n; i++) out[i] = sdsnewlen(t_data + t_offs[i], t_offs[i + 1] - t_offs[i]);
+    /* the thread's buffers keep their size between calls (the per-key serObject allocates
+     * nothing), but not a one-off large batch's: past 1 MiB and 4x this call's need, give it back */
+    const size_t big = 1u << 20;
+    if (t_data_cap > big && t_data_cap > 4 * (f->out_bound + 16)) { zfree(t_data); t_data = NULL; t_data_cap = 0; }
+    if (f->cap_a > big && f->cap_a > 4 * f->na) { zfree(f->arena); f->arena = NULL; f->cap_a = 0; }
+    if (f->cap_e * sizeof(rr_elem) > big && f->cap_e > 4 * f->ne) { zfree(f->els); f->els = NULL; f->cap_e = 0; }
+    if (f->cap_v * sizeof(rr_value) > big && f->cap_v > 4 * n) { zfree(f->vals); f->vals = NULL; f->cap_v = 0; }
+    if (t_offs_cap * sizeof(uint64_t) > big && t_offs_cap > 4 * (n + 1)) { zfree(t_offs); t_offs = NULL; t_offs_cap = 0; }
 }
 
 sds serObject(robj *o) {

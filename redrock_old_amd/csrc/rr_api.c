@@ -42,13 +42,22 @@ int rr_ctx_create(int device, rr_ctx **out) {
         free(c);
         return fail(RR_API_EHIP, "hipStreamCreate");
     }
+    int prio_lo = 0, prio_hi = 0;
+    (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+    if (hipStreamCreateWithPriority(&c->sstream, hipStreamNonBlocking, prio_hi) != hipSuccess) {
+        hipStreamDestroy(c->stream);
+        free(c);
+        return fail(RR_API_EHIP, "hipStreamCreateWithPriority");
+    }
     if (hipMalloc((void **)&c->d_totals, sizeof(rr_totals)) != hipSuccess) {
+        hipStreamDestroy(c->sstream);
         hipStreamDestroy(c->stream);
         free(c);
         return fail(RR_API_ENOMEM, "hipMalloc totals");
     }
     if (hipEventCreateWithFlags(&c->scratch_done, hipEventDisableTiming) != hipSuccess) {
         hipFree(c->d_totals);
+        hipStreamDestroy(c->sstream);
         hipStreamDestroy(c->stream);
         free(c);
         return fail(RR_API_EHIP, "hipEventCreate");
@@ -82,6 +91,7 @@ void rr_ctx_destroy(rr_ctx *c) {
         hipHostFree(c->h_ktot);
     }
     hipEventDestroy(c->scratch_done);
+    hipStreamDestroy(c->sstream);
     hipStreamDestroy(c->stream);
     free(c);
 }
@@ -109,22 +119,22 @@ int rr_ensure_scratch(rr_ctx *c, uint64_t words, hipStream_t stream) {
     return RR_API_OK;
 }
 
-/* The decode's window and group sums (and its finish counter) and the encode's group sums live
- * in a buffer of their own that is zero between calls — decode_kernel's last workgroup zeroes
- * what the call used once every window has read its sums, the encode's E4 block 0 what E3 read —
- * so no zeroing launch runs per call.  Zeroed once when (re)allocated:
- * like the scratch, growing waits on the previous call and is refused under graph capture. */
-static int ensure_dsums(rr_ctx *c, uint64_t words, hipStream_t stream) {
+/* The zero-between-calls sums (rr_internal.h): the encode's group sums, E4's block 0 zeroes
+ * what E3 read; the decode's window and group sums, double-buffered — each call adds into one
+ * half while its count_kernel zeroes what the previous call left in the other — plus a half for
+ * graph-captured decodes, which a captured zeroing kernel re-zeroes at every replay.  So no kernel has to
+ * learn that it finishes last (round 4 found that with a returning atomic at every window's end).
+ * Zeroed once when (re)allocated; like the scratch, growing waits on the previous call and is
+ * refused under graph capture.  A call that failed midway leaves dsums_dirty: the next call
+ * zeroes the whole buffer first. */
+static int ensure_dsums(rr_ctx *c, uint64_t dec_words, uint64_t enc_words, hipStream_t stream) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     const int capturing = stream && hipStreamIsCapturing(stream, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
-    if (c->dsums && words <= c->dsums_words) {
-        /* an earlier call failed between its two kernels (a launch error, a stream error seen
-         * by the host entry points): the sums it left behind would shift every later call's
-         * slots and offsets, so zero them once before the next call (not under capture: a
-         * memset node would re-zero on every replay, which is harmless but not what was asked) */
+    if (c->dsums && dec_words <= c->dsums_dec && enc_words <= c->dsums_enc) {
         if (c->dsums_dirty && !capturing) {
-            HIPCHK(hipMemsetAsync(c->dsums, 0, c->dsums_words * sizeof(uint64_t), stream));
+            HIPCHK(hipMemsetAsync(c->dsums, 0, (c->dsums_enc + 3 * c->dsums_dec) * sizeof(uint64_t), stream));
             c->dsums_dirty = 0;
+            c->dext[0] = c->dext[1] = 0;
         }
         return RR_API_OK;
     }
@@ -134,14 +144,17 @@ static int ensure_dsums(rr_ctx *c, uint64_t words, hipStream_t stream) {
         if (c->scratch_used) HIPCHK(hipEventSynchronize(c->scratch_done));
         hipFree(c->dsums);
         c->dsums = NULL;
-        c->dsums_words = 0;
     }
-    uint64_t want = words + words / 4 + 64;
-    if (hipMalloc((void **)&c->dsums, want * sizeof(uint64_t)) != hipSuccess)
-        return fail(RR_API_ENOMEM, "hipMalloc decode sums (%llu words)", (unsigned long long)want);
-    HIPCHK(hipMemsetAsync(c->dsums, 0, want * sizeof(uint64_t), stream));
+    uint64_t d = dec_words > c->dsums_dec ? dec_words : c->dsums_dec, e = enc_words > c->dsums_enc ? enc_words : c->dsums_enc;
+    d += d / 4 + 64;
+    e += e / 4 + 64;
+    if (hipMalloc((void **)&c->dsums, (e + 3 * d) * sizeof(uint64_t)) != hipSuccess)
+        return fail(RR_API_ENOMEM, "hipMalloc decode sums (%llu words)", (unsigned long long)(e + 3 * d));
+    HIPCHK(hipMemsetAsync(c->dsums, 0, (e + 3 * d) * sizeof(uint64_t), stream));
     if (!stream) HIPCHK(hipStreamSynchronize(NULL));
-    c->dsums_words = want;
+    c->dsums_enc = e;
+    c->dsums_dec = d;
+    c->dext[0] = c->dext[1] = 0;
     c->dsums_dirty = 0;
     return RR_API_OK;
 }
@@ -177,8 +190,8 @@ int rr_ctx_reserve(rr_ctx *c, uint64_t n_values, uint64_t n_bytes) {
     if (!c) return fail(RR_API_EINVAL, "ctx is NULL");
     uint64_t a = rr_encode_scratch_words(n_values, (n_bytes + 15) & ~15ull), b = rr_decode_scratch_words((n_bytes + 15) & ~15ull, n_values);
     int rc = ensure_scratch(c, a > b ? a : b, NULL);
-    uint64_t sd = rr_decode_sums_words((n_bytes + 15) & ~15ull), se = rr_encode_sums_words(n_values);
-    return rc ? rc : ensure_dsums(c, sd > se ? sd : se, NULL);
+    const uint64_t sd = rr_decode_sums_words((n_bytes + 15) & ~15ull), se = rr_encode_sums_words(n_values);
+    return rc ? rc : ensure_dsums(c, sd, se, NULL);
 }
 
 
@@ -205,14 +218,33 @@ int rr_decode_batch(rr_ctx *c, const rr_blob_batch *in, rr_flat_batch *out, rr_t
                                       in->data_cap, d_totals, NULL, 0, (hipStream_t)stream));
         return RR_API_OK;
     }
+    const uint64_t nsums = rr_decode_sums_words(in->data_cap);
     int rc = ensure_scratch(c, rr_decode_scratch_words(in->data_cap, in->n), (hipStream_t)stream);
-    if (!rc) rc = ensure_dsums(c, rr_decode_sums_words(in->data_cap), (hipStream_t)stream);
+    if (!rc) rc = ensure_dsums(c, nsums, 0, (hipStream_t)stream);
     if (rc) return rc;
     const int first_only = c->fail_second;
     c->fail_second = 0;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    const int capturing = stream && hipStreamIsCapturing((hipStream_t)stream, &cs) == hipSuccess &&
+                          cs != hipStreamCaptureStatusNone;
+    uint64_t *half[3];
+    for (int h = 0; h < 3; h++) half[h] = c->dsums + c->dsums_enc + (uint64_t)h * c->dsums_dec;
+    uint64_t *use, *zero = NULL, nzero = 0;
+    if (capturing) {   /* the graph's own half, re-zeroed by a captured kernel at every replay */
+        use = half[2];
+        HIPCHK(rr_launch_zero_words(use, nsums, (hipStream_t)stream));
+    } else {           /* this call's half; its count_kernel zeroes what the previous call left in the other */
+        const int x = c->dphase, y = 1 - x;
+        use = half[x];
+        zero = half[y];
+        nzero = c->dext[y];
+        c->dext[y] = 0;
+        c->dext[x] = nsums;
+        c->dphase = y;
+    }
     const hipError_t e = rr_launch_decode(in->data, in->offsets, in->n, out->values, out->elems, out->elem_cap,
-                                          out->arena, c->scratch, c->dsums, in->data_cap, d_totals, (hipStream_t)stream,
-                                          first_only);
+                                          out->arena, c->scratch, use, zero, nzero, in->data_cap, d_totals,
+                                          (hipStream_t)stream, first_only);
     rc = mark_scratch(c, (hipStream_t)stream);
     if (e != hipSuccess || first_only) {
         c->dsums_dirty = 1;
@@ -236,7 +268,7 @@ int rr_encode_batch(rr_ctx *c, const rr_flat_batch *in, rr_blob_batch *out, rr_t
         return RR_API_OK;
     }
     int rc = ensure_scratch(c, rr_encode_scratch_words(in->n, out->data_cap), (hipStream_t)stream);
-    if (!rc) rc = ensure_dsums(c, rr_encode_sums_words(in->n), (hipStream_t)stream);
+    if (!rc) rc = ensure_dsums(c, 0, rr_encode_sums_words(in->n), (hipStream_t)stream);
     if (rc) return rc;
     const int first_only = c->fail_second;
     c->fail_second = 0;
@@ -436,7 +468,7 @@ static int small_wait(rr_ctx *c, const uint32_t *flag, uint32_t seq) {
             yielding = (t1.tv_sec - t0.tv_sec) * 1000000000L + (t1.tv_nsec - t0.tv_nsec) > 50000L;
         }
         if ((k & 4095) == 0 || (yielding && (k & 63) == 0)) {
-            const hipError_t q = hipStreamQuery(c->stream);
+            const hipError_t q = hipStreamQuery(c->sstream);
             if (q == hipSuccess) {
                 if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq) return RR_API_OK;
                 return fail(RR_API_EDEVICE, "one-launch kernel ended without its completion word");
@@ -469,7 +501,7 @@ static int decode_host_small(rr_ctx *c, const uint8_t *data, const uint64_t *off
     __atomic_store_n((uint32_t *)(h + o_flag), 0u, __ATOMIC_RELAXED);
     HIPCHK(rr_launch_decode_small(d + o_dat, (const uint64_t *)(d + o_off), n, (rr_value *)(d + o_val),
                                   (rr_elem *)(d + o_el), elem_cap, NULL, AL16(bytes), (rr_totals *)(d + o_tot),
-                                  (uint32_t *)(d + o_flag), seq, c->stream));
+                                  (uint32_t *)(d + o_flag), seq, c->sstream));
     rc = small_wait(c, (const uint32_t *)(h + o_flag), seq);
     if (rc) return rc;
     rr_totals t;
@@ -549,7 +581,7 @@ static int encode_host_small(rr_ctx *c, const rr_value *values, const rr_elem *e
     __atomic_store_n((uint32_t *)(h + o_flag), 0u, __ATOMIC_RELAXED);
     HIPCHK(rr_launch_encode_small((const rr_value *)(d + o_val), (const rr_elem *)(d + o_el), n_elems, d + o_ar,
                                   arena_bytes, n, d + o_out, data_cap, (uint64_t *)(d + o_off),
-                                  (rr_totals *)(d + o_tot), (uint32_t *)(d + o_flag), seq, c->stream));
+                                  (rr_totals *)(d + o_tot), (uint32_t *)(d + o_flag), seq, c->sstream));
     rc = small_wait(c, (const uint32_t *)(h + o_flag), seq);
     if (rc) return rc;
     rr_totals t;

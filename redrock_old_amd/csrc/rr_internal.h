@@ -15,9 +15,15 @@ struct rr_ctx {
     uint64_t scratch_words;
     hipEvent_t scratch_done;     /* recorded after every call's last use of the scratch */
     int scratch_used;
-    uint64_t *dsums;             /* the decode's window/group sums: zero between calls */
-    uint64_t dsums_words;
-    int dsums_dirty;             /* a call's second kernel may not have run: re-zero dsums first */
+    /* The zero-between-calls sums: [encode group sums, enc words][decode half 0, dec words]
+     * [decode half 1][decode half for graph-captured calls].  A decode call adds its window and
+     * group sums into one half while its count_kernel zeroes what the previous call left in the
+     * other; the calls alternate (dphase), so no kernel has to find out that it finishes last. */
+    uint64_t *dsums;
+    uint64_t dsums_enc, dsums_dec;   /* words of the encode region / of each decode half */
+    uint64_t dext[2];                /* words each decode half holds non-zero (its last call's sums) */
+    int dphase;                      /* the half the next decode call uses */
+    int dsums_dirty;                 /* a call failed midway: re-zero the whole buffer first */
     int fail_second;             /* test hook (rr_debug_fail_second): the next pipeline call stops after its first kernel */
     /* device staging for host entry points */
     void *d_in, *d_off, *d_vals, *d_elems, *d_arena, *d_out, *d_ooff;
@@ -34,6 +40,8 @@ struct rr_ctx {
      * which the one-launch kernels read their input from and write their output to */
     uint8_t *h_small, *d_small;
     uint32_t small_seq;   /* the one-launch kernels' completion words (small_wait) */
+    hipStream_t sstream;  /* the one-launch host calls' stream: the device's highest priority, so a
+                           * per-key call is dispatched ahead of batch work queued elsewhere */
     size_t c_small;
 };
 

@@ -17,14 +17,16 @@
 extern "C" {
 #endif
 
-/* sums: rr_decode_sums_words(data_cap) words that are zero on entry and are zero again when the
- * call's kernels end (decode_kernel's last workgroup restores them): the context keeps them in
- * a buffer of their own, zeroed once when allocated */
-/* first_only (test hook): launch only the first kernel, which leaves the sums non-zero */
+/* sums: rr_decode_sums_words(data_cap) words, zero on entry (count_kernel adds the window and
+ * group sums into them, decode_kernel reads them); zero / nzero: words the call's count_kernel
+ * zeroes on the way (the other half of the context's double buffer).  first_only (test hook):
+ * launch only the first kernel. */
 hipError_t rr_launch_decode(const uint8_t *blob, const uint64_t *offsets, uint64_t n, rr_value *values,
                             rr_elem *elems, uint64_t elem_cap, uint8_t *arena, uint64_t *scratch, uint64_t *sums,
-                            uint64_t data_cap, rr_totals *totals, hipStream_t stream, int first_only);
+                            uint64_t *zero, uint64_t nzero, uint64_t data_cap, rr_totals *totals, hipStream_t stream,
+                            int first_only);
 uint64_t rr_decode_sums_words(uint64_t data_cap);
+hipError_t rr_launch_zero_words(uint64_t *words, uint64_t n, hipStream_t stream);
 hipError_t rr_launch_encode(const rr_value *values, const rr_elem *elems, uint64_t elem_cap, const uint8_t *arena,
                             uint64_t arena_cap, uint64_t n, uint8_t *out, uint64_t cap, uint64_t *offsets,
                             uint64_t *scratch, uint64_t *sums, rr_totals *totals, hipStream_t stream, int first_only);

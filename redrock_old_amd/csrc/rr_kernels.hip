@@ -483,8 +483,8 @@ __device__ __forceinline__ void zero_call_words(uint64_t *words, uint32_t nwords
 
 // Per value: its reservation (u32; a value that would need 2^32 slots fails capacity anyway),
 // its class and first_val.  Per window: the reservations of its values summed into wtot[w], and
-// per group of WGROUP windows into gtot[w / WGROUP] (both zero on entry: decode_kernel's last
-// workgroup of the previous call zeroed them).
+// per group of WGROUP windows into gtot[w / WGROUP] (both zero on entry: the previous call's
+// count_kernel zeroed this half of the context's double buffer; this call zeroes the other).
 // A window's values are consecutive, so each run of one window (group) in a wave adds its sum
 // with two LDS atomics — the inclusive wave scan at its last lane, minus the exclusive scan at
 // its first — into the workgroup's table of the windows (groups) it touches; the table then
@@ -503,9 +503,11 @@ __device__ __forceinline__ uint64_t div_win(uint64_t o, uint32_t win, double rcp
     return q;
 }
 constexpr uint32_t WGROUP = 16;   // (64: ~260 same-address atomics per group sum on config 1)
-// (The sums are zero on entry without a zeroing launch: the previous call's last workgroup
-// zeroed them.  A zeroing kernel cost ~4.5 us a call, hipMemsetAsync of a size that is not a
-// multiple of 16 bytes two fill kernels of ~4.7 us — a sixth of config 1's 100K-value call.)
+// (The sums are zero on entry without a zeroing launch: they are double-buffered, and each
+// call's count_kernel zeroes the half the previous call used.  A zeroing kernel cost ~4.5 us a
+// call, hipMemsetAsync of a size that is not a multiple of 16 bytes two fill kernels of ~4.7 us
+// — a sixth of config 1's 100K-value call.  Round 4 had decode_kernel's last workgroup zero them,
+// found by a returning atomic at every window's end: ~2 us of idle workgroup slot per window.)
 constexpr uint32_t CNT_NT = 256, CNT_LW = CNT_NT, CNT_LG = 8;   // (a workgroup's values start in <= 256 windows)
 // a wave's List stage (16 KiB a workgroup: 8 workgroups still fit a CU; measured count_kernel
 // 53.5 us at 4 KiB, 53.8 at 8 KiB, 62.7 at 2 KiB; walking from global memory 58.1, with no List
@@ -517,10 +519,15 @@ __global__ __launch_bounds__(CNT_NT) void count_kernel(const uint8_t *__restrict
                                                        uint32_t nwin, uint32_t win,
                                                        uint32_t *__restrict__ counts, uint8_t *__restrict__ cls,
                                                        uint64_t *wtot, uint64_t *gtot,
-                                                       uint64_t *zero_words, uint32_t nzero, rr_totals *tot) {
+                                                       uint64_t *zero_words, uint64_t nzero, rr_totals *tot) {
     __shared__ uint64_t lw[CNT_LW], lg[CNT_LG];
     __shared__ __attribute__((aligned(16))) uint8_t lstage[CNT_NT / RR_WAVE][CNT_LB];
-    zero_call_words(zero_words, nzero, tot);
+    if (blockIdx.x == 0 && tot && threadIdx.x < 4) reinterpret_cast<uint64_t *>(tot)[threadIdx.x] = 0;
+    {   // the other half of the context's sums, for the next call: a slice per block
+        const uint64_t per = (nzero + gridDim.x - 1) / gridDim.x, z0 = (uint64_t)blockIdx.x * per;
+        const uint64_t z1 = z0 + per < nzero ? z0 + per : nzero;
+        for (uint64_t k = z0 + threadIdx.x; k < z1; k += CNT_NT) zero_words[k] = 0;
+    }
     const uint32_t tid = threadIdx.x;
     lw[tid] = 0;
     if (tid < CNT_LG) lg[tid] = 0;
@@ -1110,9 +1117,9 @@ __global__ __launch_bounds__(NW * RR_WAVE) __attribute__((amdgpu_waves_per_eu(DE
     const uint8_t *__restrict__ blob, uint64_t data_cap, const uint64_t *__restrict__ offsets, uint64_t n,
     const uint32_t *__restrict__ first_val, const uint64_t *__restrict__ first_off, const uint8_t *__restrict__ cls,
     const uint32_t *__restrict__ counts,
-    uint64_t *wtot, const uint64_t *gtot, rr_value *__restrict__ values,   // (wtot: also zeroed at the end)
+    const uint64_t *wtot, const uint64_t *gtot, rr_value *__restrict__ values,
     rr_elem *__restrict__ elems, uint64_t elem_cap, uint8_t *__restrict__ arena, uint32_t nwin, uint32_t win,
-    rr_totals *tot, uint32_t *fin, uint64_t nsums) {
+    rr_totals *tot) {
     constexpr uint32_t NT = NW * RR_WAVE, STAGE = W + SLACK;
     static_assert(PMAX == NT, "a chunk is one value per thread (the slot scan)");
     static_assert(W % 16 == 0 && SLACK % 16 == 0, "tile shape");
@@ -1123,7 +1130,7 @@ __global__ __launch_bounds__(NW * RR_WAVE) __attribute__((amdgpu_waves_per_eu(DE
     __shared__ uint32_t eloc[PMAX + 1];   // chunk-relative first slot of each value, then the chunk's slots
     __shared__ uint64_t wpart[2][NW];     // wave sums: [0] the window's first slot, [1] the chunk's slot scan
     __shared__ uint32_t ccount[C_N], cbase[C_N], ccur[C_N], bpre[C_N + 1];
-    __shared__ uint32_t next_batch, last_win;
+    __shared__ uint32_t next_batch;
     __shared__ uint64_t red[2][NW];
     PROBE(__shared__ uint64_t prb[PROBE_WORDS]; uint64_t pt0 = __builtin_amdgcn_s_memtime(), pt1 = 0, pt2 = 0;
           const uint64_t prt0 = __builtin_amdgcn_s_memrealtime();
@@ -1389,17 +1396,8 @@ __global__ __launch_bounds__(NW * RR_WAVE) __attribute__((amdgpu_waves_per_eu(DE
               prb[31] = (uint64_t)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11)) |
                         ((uint64_t)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (15 << 11)) << 32);
               prb[29] = staged; if (g_probe) for (uint32_t i = 0; i < PROBE_WORDS; ++i) g_probe[(uint64_t)tile * PROBE_WORDS + i] = prb[i];)
-        // the last window to finish (every other one has read its sums, at its start) zeroes
-        // the call's sums and the counter for the next call: no zeroing launch per call.
-        // Relaxed: the sums' loads returned before each window's increment, and the zeroes
-        // need only reach the next call, past the kernel boundary (acquire-release at agent
-        // scope writes back and invalidates the XCD's L2 at every window: 0.35 -> 0.81 ms)
-        last_win = __hip_atomic_fetch_add(fin, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nwin - 1;
-    }
-    lds_barrier();
-    if (last_win) {
-        for (uint64_t k = tid; k < nsums; k += NT) wtot[k] = 0;   // (wtot, then gtot and the counter)
-        if (tid == 0) *fin = 0;
+        // (no returning atomic, no barrier after it: the workgroup's slot frees as soon as its
+        //  waves end — the sums are zeroed by the next call's count_kernel)
     }
 }
 
@@ -1415,7 +1413,13 @@ __global__ __launch_bounds__(NW * RR_WAVE) __attribute__((amdgpu_waves_per_eu(DE
 // the pipeline, byte for byte.
 constexpr uint32_t SMALL_NT = 1024, SMALL_VPT = 4, SMALL_N = SMALL_NT * SMALL_VPT;
 constexpr uint32_t SMALL_BYTES = 128 * 1024;   // (one workgroup: up to 160 KiB of LDS)
-constexpr uint32_t SMALL_GW = 32;   // batches of at most this many values: one wave per value, grouped walks
+// batches of at most this many values: one wave per value (the class walks on a wave / the
+// whole wave emitting one value); larger ones one lane per value (the exact parser / the byte
+// emitter) — which the host takes only for values of at most SMALL_LANE_BYTES on average
+// (rr_small_decode_fits): a lane walking a 500-byte value costs ~20 us (round 4: 64 config-4
+// values took 368 us through the lane path)
+constexpr uint32_t SMALL_GW = 256;
+constexpr uint64_t SMALL_LANE_BYTES = 64;
 constexpr uint32_t SMALL_EIN = 16 * 1024;   // encode inputs up to this size staged in LDS
 constexpr uint32_t SMALL_STAGE = SMALL_BYTES + 8192;   // + the reads past a value's end; >= the fixup's LDS
 static_assert(FIX_LDS + 4 * (SMALL_NT + 1) <= SMALL_STAGE, "the fixup reuses the stage");
@@ -2733,7 +2737,9 @@ __global__ __launch_bounds__(SMALL_NT) void encode_small_kernel(const rr_value *
 
 }  // namespace
 
-extern "C" int rr_small_decode_fits(uint64_t n, uint64_t data_cap) { return n <= SMALL_N && data_cap <= SMALL_BYTES; }
+extern "C" int rr_small_decode_fits(uint64_t n, uint64_t data_cap) {
+    return n <= SMALL_N && data_cap <= SMALL_BYTES && (n <= SMALL_GW || data_cap <= n * SMALL_LANE_BYTES);
+}
 extern "C" hipError_t rr_launch_decode_small(const uint8_t *blob, const uint64_t *offsets, uint64_t n, rr_value *values,
                                              rr_elem *elems, uint64_t elem_cap, uint8_t *arena, uint64_t data_cap,
                                              rr_totals *totals, uint32_t *done, uint32_t seq, hipStream_t stream) {
@@ -2783,7 +2789,9 @@ extern "C" hipError_t rr_launch_arena_need(const rr_value *values, uint64_t n, c
     return hipGetLastError();
 }
 
-extern "C" int rr_small_encode_fits(uint64_t n, uint64_t data_cap) { return n > 0 && n <= SMALL_N && data_cap <= SMALL_BYTES; }
+extern "C" int rr_small_encode_fits(uint64_t n, uint64_t data_cap) {
+    return n > 0 && n <= SMALL_N && data_cap <= SMALL_BYTES && (n <= SMALL_GW || data_cap <= n * SMALL_LANE_BYTES);
+}
 extern "C" hipError_t rr_launch_encode_small(const rr_value *values, const rr_elem *elems, uint64_t elem_cap,
                                              const uint8_t *arena, uint64_t arena_cap, uint64_t n, uint8_t *out,
                                              uint64_t cap, uint64_t *offsets, rr_totals *totals, uint32_t *done,
@@ -2806,6 +2814,7 @@ extern "C" hipError_t rr_launch_encode_small(const rr_value *values, const rr_el
 constexpr uint32_t DEC_W = RR_DEC_W, DEC_NW = RR_DEC_NW;
 // (values per sort chunk: one per thread, the chunk's slot scan)
 #define DECODE_KERNEL decode_kernel<RR_DEC_W, RR_DEC_SLACK, RR_DEC_NW, RR_DEC_NW * RR_WAVE>
+
 
 // Resident workgroup count for a persistent launch: occupancy query minus one block per CU
 // (the API over-reports by one for SGPR-heavy kernels, MI355X_MICROARCH.md §Residency).
@@ -2853,30 +2862,28 @@ extern "C" uint64_t rr_decode_scratch_words(uint64_t data_cap, uint64_t n) {
     const uint64_t nw = dec_windows(data_cap);
     return RR_SCRATCH_HDR + (n + 2) / 2 + (nw + 2) / 2 + (nw + 1) + (n + 7) / 8 + 2;
 }
-// The sums buffer: [window sums, nwin] [group sums, nwin / WGROUP + 1] [finish counter]
+// The sums (one half of the context's double buffer): [window sums, nwin] [group sums, nwin / WGROUP + 1]
 extern "C" uint64_t rr_decode_sums_words(uint64_t data_cap) {
     const uint64_t nw = dec_windows(data_cap);
-    return nw + dec_groups(nw) + 1;
+    return nw + dec_groups(nw);
 }
 
 extern "C" hipError_t rr_launch_decode(const uint8_t *blob, const uint64_t *offsets, uint64_t n, rr_value *values,
                                        rr_elem *elems, uint64_t elem_cap, uint8_t *arena, uint64_t *scratch,
-                                       uint64_t *sums, uint64_t data_cap, rr_totals *totals, hipStream_t stream,
-                                       int first_only) {
+                                       uint64_t *sums, uint64_t *zero, uint64_t nzero, uint64_t data_cap,
+                                       rr_totals *totals, hipStream_t stream, int first_only) {
     const uint32_t win = dec_win(data_cap), nw = (uint32_t)(data_cap / win + 1);
     uint64_t *wtot = sums;
     uint64_t *gtot = wtot + nw;
-    uint32_t *fin = reinterpret_cast<uint32_t *>(gtot + dec_groups(nw));
     uint32_t *counts = reinterpret_cast<uint32_t *>(scratch + RR_SCRATCH_HDR);
     uint32_t *first_val = counts + ((n + 2) & ~1ull);
     uint64_t *first_off = reinterpret_cast<uint64_t *>(first_val + ((nw + 2) & ~1u));
     uint8_t *cls = reinterpret_cast<uint8_t *>(first_off + nw + 1);
     hipLaunchKernelGGL(count_kernel, dim3((uint32_t)((n + 1 + 255) / 256)), dim3(256), 0, stream, blob, offsets, n,
-                       first_val, first_off, nw, win, counts, cls, wtot, gtot, nullptr, 0u, totals);
+                       first_val, first_off, nw, win, counts, cls, wtot, gtot, zero, nzero, totals);
     if (first_only) return hipGetLastError();
     hipLaunchKernelGGL((DECODE_KERNEL), dim3(nw), dim3(DEC_NW * RR_WAVE), 0, stream, blob, data_cap, offsets, n,
-                       first_val, first_off, cls, counts, wtot, gtot, values, elems, elem_cap, arena, nw, win, totals,
-                       fin, (uint64_t)nw + dec_groups(nw) + 1);
+                       first_val, first_off, cls, counts, wtot, gtot, values, elems, elem_cap, arena, nw, win, totals);
     return hipGetLastError();
 }
 
@@ -2954,6 +2961,19 @@ __global__ __launch_bounds__(64) void shard_plan_kernel(const uint64_t *__restri
     plan[4 * (uint64_t)k + 1] = cut[1];
     plan[4 * (uint64_t)k + 2] = offsets[cut[0]];
     plan[4 * (uint64_t)k + 3] = offsets[cut[1]];
+}
+
+// words[0, n) = 0 (the graph-captured decode's sums, re-zeroed at every replay: a captured
+// hipMemsetAsync measured as not re-running on replay on this stack, tools/graph_diag.py)
+__global__ __launch_bounds__(256) void zero_words_kernel(uint64_t *__restrict__ words, uint64_t n) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        words[i] = 0;
+}
+extern "C" hipError_t rr_launch_zero_words(uint64_t *words, uint64_t n, hipStream_t stream) {
+    if (!n) return hipSuccess;
+    const uint64_t b = (n + 255) / 256;
+    hipLaunchKernelGGL(zero_words_kernel, dim3((uint32_t)(b < 256 ? b : 256)), dim3(256), 0, stream, words, n);
+    return hipGetLastError();
 }
 
 // offsets[i] -= sub (a received shard's offsets, relative to its first byte)

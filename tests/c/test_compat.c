@@ -83,6 +83,7 @@ static int obj_eq(robj *a, robj *b) {
 }
 
 int main(void) {
+    setvbuf(stdout, NULL, _IONBF, 0);   /* (a crash keeps what was printed) */
     int checked = 0, panics = 0;
     robj *objs[N_FIXTURES];
     void *bufs[N_FIXTURES];

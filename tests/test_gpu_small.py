@@ -71,6 +71,18 @@ def test_63_values(engine_small, engine, cfg):
     _check(engine_small, engine, batch, f"cfg {cfg} n 63")
 
 
+@pytest.mark.parametrize("n", [200, 256, 300])
+def test_wave_route_limits(engine_small, engine, n):
+    """n = 200 and 256 config-4 values of at most 450 bytes: the one-launch kernels' wave-per-value
+    route at its limit (SMALL_GW); n = 300 of them averages above SMALL_LANE_BYTES, so the host
+    takes the pipeline instead of the lane route — the same results either way."""
+    blobs = [b for b in _blobs(4, 3000, seed=256 + n) if len(b) <= 450][:n]
+    assert len(blobs) == n
+    while not _fits(blobs):
+        blobs = blobs[:-1]
+    _check(engine_small, engine, blobs, f"n {len(blobs)}")
+
+
 def test_4096_small_values(engine_small, engine):
     """n = 4096 (the one-launch limit): the config-4 values of at most 30 bytes (INT and
     EMBSTR strings, small intsets / lists / ziplists)."""
@@ -196,6 +208,8 @@ def test_golden_fixtures_one_per_call(engine_small):
         if not _fits([b]):
             continue
         data, offs = batch_from_blobs([b])
+        if data.size == 0:   # (an empty blob: the host entry point wants a data buffer)
+            data = np.zeros(16, np.uint8)
         v, e, a, t = engine_small.decode_host(data, offs)
         assert_flat_equal((v, e), expected_flat([f]), f.get("name", "fixture"))
 
@@ -221,13 +235,13 @@ def test_handoff_under_uneven_load(engine_small):
     s = torch.cuda.Stream(dev)
 
     def keep_busy():
-        if s.query():   # queue ~30 ms more whenever the loader's stream has drained
-            for _ in range(80):
+        if s.query():   # queue ~50 ms more whenever the loader's stream has drained
+            for _ in range(150):
                 load.decode_device(d_data, d_offs, d_vals, d_elems, d_arena, d_tot, stream=s)
 
     # the cases: small batches of config-4 and edge values, with their oracle results
     src = _blobs(4, 20000, seed=71) + _blobs(10, 400, seed=72)
-    tiny = [b for b in src if len(b) <= 30]
+    tiny = [b for b in _blobs(4, 120000, seed=73) if len(b) <= 30]
     cases = []
     for n, pool in ((1, src), (7, src), (63, [b for b in src if len(b) <= 1500]), (4096, tiny)):
         for k in range(3):
@@ -240,24 +254,31 @@ def test_handoff_under_uneven_load(engine_small):
             ov, oe, oa, ot = cpu.decode(data, offs)
             xo, xoffs, xt = cpu.encode(ov, oe, oa)
             cases.append((f"n {n} #{k}", data, offs, (ov, oe, oa, ot), (xo, xoffs, xt)))
-    assert len(cases) >= 10
-    checked = 0
+    assert len(cases) == 12
+    import time
+    checked = busy = 0
+    lat = []
     try:
         for rep in range(6):
             for what, data, offs, (ov, oe, oa, ot), (xo, xoffs, xt) in cases:
                 keep_busy()
+                t0 = time.perf_counter()
                 v, e, a, t = engine_small.decode_host(data, offs)
+                lat.append(time.perf_counter() - t0)
                 assert_flat_equal((v, e), (ov, oe), what)
                 assert t == ot, (what, rep, t, ot)
                 if int(offs[-1]) + 16 <= rr.SMALL_BYTES:
                     out, ooffs, t2 = engine_small.encode_host(ov, oe, oa, data_cap=int(offs[-1]) + 16)
                     assert t2 == xt and np.array_equal(ooffs, xoffs) and np.array_equal(out, xo), (what, rep)
+                busy += not s.query()   # (the loader still had work queued when the call returned)
                 checked += 1
-        assert not s.query(), "the loader stream drained: the calls did not run beside a loaded GPU"
     finally:
         s.synchronize()
         load.close()
     assert checked == 6 * len(cases)
+    print(f"decode calls beside the load: median {1e6 * sorted(lat)[len(lat) // 2]:.1f} us, max {1e6 * max(lat):.1f} us; "
+          f"{busy} of {checked} returned while the load was still queued")
+    assert busy >= checked // 2, f"only {busy} of {checked} calls ran beside a loaded GPU"
 
 
 def test_failed_second_launch_resets_sums(engine):
