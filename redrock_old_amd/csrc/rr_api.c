@@ -55,13 +55,6 @@ int rr_ctx_create(int device, rr_ctx **out) {
         free(c);
         return fail(RR_API_ENOMEM, "hipMalloc totals");
     }
-    if (hipEventCreateWithFlags(&c->scratch_done, hipEventDisableTiming) != hipSuccess) {
-        hipFree(c->d_totals);
-        hipStreamDestroy(c->sstream);
-        hipStreamDestroy(c->stream);
-        free(c);
-        return fail(RR_API_EHIP, "hipEventCreate");
-    }
     *out = c;
     return RR_API_OK;
 }
@@ -90,16 +83,16 @@ void rr_ctx_destroy(rr_ctx *c) {
         hipFree(c->d_ktot);
         hipHostFree(c->h_ktot);
     }
-    hipEventDestroy(c->scratch_done);
     hipStreamDestroy(c->sstream);
     hipStreamDestroy(c->stream);
     free(c);
 }
 
-/* Grow the scratch.  Only the previous call's kernels can still be using the old buffer, and
- * scratch_done marks their end (whatever stream they ran on), so only that wait is needed — no
- * device-wide synchronisation.  Growing allocates, which a stream under graph capture cannot do:
- * size the scratch with rr_ctx_reserve before capturing. */
+/* Grow the scratch.  Kernels of earlier calls — on whatever stream, or replays of a captured
+ * graph — may still be using the old buffer: growing (rare: rr_ctx_reserve sizes it up front)
+ * waits for the device.  (Round 4 recorded an event after every call for this wait: one HIP call
+ * more per call, on the path small batches are bound by.)  Growing allocates, which a stream
+ * under graph capture cannot do: size the scratch with rr_ctx_reserve before capturing. */
 int rr_ensure_scratch(rr_ctx *c, uint64_t words, hipStream_t stream) {
     if (c->scratch && words <= c->scratch_words) return RR_API_OK;
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
@@ -107,7 +100,7 @@ int rr_ensure_scratch(rr_ctx *c, uint64_t words, hipStream_t stream) {
         return fail(RR_API_EINVAL, "scratch too small under graph capture: call rr_ctx_reserve first");
     HIPCHK(hipSetDevice(c->device));
     if (c->scratch) {
-        if (c->scratch_used) HIPCHK(hipEventSynchronize(c->scratch_done));
+        if (c->scratch_used) HIPCHK(hipDeviceSynchronize());
         hipFree(c->scratch);
         c->scratch = NULL;
     }
@@ -127,21 +120,23 @@ int rr_ensure_scratch(rr_ctx *c, uint64_t words, hipStream_t stream) {
  * Zeroed once when (re)allocated; like the scratch, growing waits on the previous call and is
  * refused under graph capture.  A call that failed midway leaves dsums_dirty: the next call
  * zeroes the whole buffer first. */
-static int ensure_dsums(rr_ctx *c, uint64_t dec_words, uint64_t enc_words, hipStream_t stream) {
+static int is_capturing(hipStream_t stream) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    const int capturing = stream && hipStreamIsCapturing(stream, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
+    return stream && hipStreamIsCapturing(stream, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
+}
+static int ensure_dsums(rr_ctx *c, uint64_t dec_words, uint64_t enc_words, hipStream_t stream) {
     if (c->dsums && dec_words <= c->dsums_dec && enc_words <= c->dsums_enc) {
-        if (c->dsums_dirty && !capturing) {
+        if (c->dsums_dirty && !is_capturing(stream)) {
             HIPCHK(hipMemsetAsync(c->dsums, 0, (c->dsums_enc + 3 * c->dsums_dec) * sizeof(uint64_t), stream));
             c->dsums_dirty = 0;
             c->dext[0] = c->dext[1] = 0;
         }
         return RR_API_OK;
     }
-    if (capturing) return fail(RR_API_EINVAL, "decode sums too small under graph capture: call rr_ctx_reserve first");
+    if (is_capturing(stream)) return fail(RR_API_EINVAL, "decode sums too small under graph capture: call rr_ctx_reserve first");
     HIPCHK(hipSetDevice(c->device));
     if (c->dsums) {
-        if (c->scratch_used) HIPCHK(hipEventSynchronize(c->scratch_done));
+        if (c->scratch_used) HIPCHK(hipDeviceSynchronize());
         hipFree(c->dsums);
         c->dsums = NULL;
     }
@@ -159,13 +154,9 @@ static int ensure_dsums(rr_ctx *c, uint64_t dec_words, uint64_t enc_words, hipSt
     return RR_API_OK;
 }
 
-/* after a call's launches: remember where its use of the scratch ends (not under capture: the
- * captured graph replays later, and capture never grows the scratch) */
+/* after a call's launches: the scratch has been used (a later growth waits for the device) */
 int rr_mark_scratch(rr_ctx *c, hipStream_t stream) {
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (stream && hipStreamIsCapturing(stream, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
-        return RR_API_OK;
-    HIPCHK(hipEventRecord(c->scratch_done, stream));
+    (void)stream;
     c->scratch_used = 1;
     return RR_API_OK;
 }
@@ -224,9 +215,7 @@ int rr_decode_batch(rr_ctx *c, const rr_blob_batch *in, rr_flat_batch *out, rr_t
     if (rc) return rc;
     const int first_only = c->fail_second;
     c->fail_second = 0;
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    const int capturing = stream && hipStreamIsCapturing((hipStream_t)stream, &cs) == hipSuccess &&
-                          cs != hipStreamCaptureStatusNone;
+    const int capturing = is_capturing((hipStream_t)stream);
     uint64_t *half[3];
     for (int h = 0; h < 3; h++) half[h] = c->dsums + c->dsums_enc + (uint64_t)h * c->dsums_dec;
     uint64_t *use, *zero = NULL, nzero = 0;

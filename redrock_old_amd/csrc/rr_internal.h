@@ -13,8 +13,7 @@ struct rr_ctx {
     hipStream_t stream;          /* used by the host entry points */
     uint64_t *scratch;           /* look-back words + counters */
     uint64_t scratch_words;
-    hipEvent_t scratch_done;     /* recorded after every call's last use of the scratch */
-    int scratch_used;
+    int scratch_used;            /* a call has used the scratch (growing it then waits for the device) */
     /* The zero-between-calls sums: [encode group sums, enc words][decode half 0, dec words]
      * [decode half 1][decode half for graph-captured calls].  A decode call adds its window and
      * group sums into one half while its count_kernel zeroes what the previous call left in the
