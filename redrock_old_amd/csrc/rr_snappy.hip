@@ -45,6 +45,11 @@ constexpr uint32_t SNZ_DEC_WIN = RR_SNZ_DEC_WIN;
 #define RR_SNZ_FRAG 0
 #endif
 constexpr uint32_t SNZ_FRAG_LDS = RR_SNZ_FRAG;
+// 1: the decompressor's tag chain through speculative sizes at 256 positions (a readlane a
+// tag); 0: one LDS read a tag
+#ifndef RR_SNZ_SPEC
+#define RR_SNZ_SPEC 1
+#endif
 
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
@@ -212,8 +217,41 @@ __device__ uint32_t dec_block_lds(rsrc_t R, uint32_t s0, uint32_t clen, uint32_t
     }
     uint32_t pos = 0;
     while (p < end) {
-        // A. up to 64 tag starts
+        // A. up to 64 tag starts.  The size a tag would have at each of the 256 positions from p
+        //    on (4 a lane, speculatively: one LDS round trip and a few VALU ops), then the chain
+        //    through them by readlanes — a few cycles a tag instead of an LDS round trip; a tag
+        //    that lands past the 256 positions (a long literal) starts the next round.
         uint32_t tp = 0, nt = 0;
+#if RR_SNZ_SPEC
+        do {
+            const uint32_t wp = p, ab = (D + wp) & ~3u, sh = (D + wp) & 3u;
+            const uint32_t w0 = win32[(ab >> 2) + lane], w1 = win32[(ab >> 2) + lane + 1], w2 = win32[(ab >> 2) + lane + 2];
+            const uint64_t x01 = ((uint64_t)w1 << 32) | w0, x12 = ((uint64_t)w2 << 32) | w1;
+            uint32_t sz4[4];
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j) {
+                const uint32_t o = sh + j;   // (0 .. 6: the position's bytes from the lane's three dwords)
+                const uint64_t t = o < 4 ? x01 >> (8 * o) : x12 >> (8 * (o - 4));
+                const uint32_t q = wp + 4 * lane + j, c = (uint32_t)t & 0xFF, ty = c & 3, c6 = (c >> 2) + 1;
+                const uint32_t nb = c6 > 60 ? c6 - 60 : 0u, v = (uint32_t)(t >> 8);
+                const uint64_t len = nb ? (uint64_t)(nb == 4 ? v : v & ((1u << (8 * nb)) - 1)) + 1 : c6;
+                const uint32_t rem = q < end ? end - q : 0u;
+                const uint32_t lsz = len >= rem ? rem + 1 : (uint32_t)(1 + nb + len);   // (past the end: phase B's TRUNC)
+                sz4[j] = ty == 0 ? lsz : ty == 1 ? 2u : ty == 2 ? 3u : 5u;
+            }
+            const uint32_t s01 = (sz4[0] & 0xFFFF) | (sz4[1] << 16), s23 = (sz4[2] & 0xFFFF) | (sz4[3] << 16);
+            // (sizes past 16 bits only on the last tag: rem + 1 <= the block's bytes < 2^16, or
+            //  a literal as long as the rest, which ends the block's chain either way)
+            do {
+                const uint32_t r = p - wp, l = r >> 2, j = r & 3;
+                const uint32_t pair = rdl(j < 2 ? s01 : s23, l);
+                const uint32_t sz = (j & 1) ? pair >> 16 : pair & 0xFFFF;
+                tp = lane == nt ? p : tp;
+                ++nt;
+                p += sz;
+            } while (nt < WAVE && p < end && p - wp < 4 * WAVE);
+        } while (nt < WAVE && p < end);
+#else
         do {
             const uint64_t t = rd8(D + p);
             const uint32_t c = (uint32_t)t & 0xFF, ty = c & 3, c6 = (c >> 2) + 1;
@@ -229,6 +267,7 @@ __device__ uint32_t dec_block_lds(rsrc_t R, uint32_t s0, uint32_t clen, uint32_t
             ++nt;
             p += sz;
         } while (nt < WAVE && p < end);
+#endif
         // B. the batch's tags, one per lane
         const bool act = lane < nt;
         const uint32_t a = D + (act ? tp : 0);
