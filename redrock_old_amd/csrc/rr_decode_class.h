@@ -208,7 +208,7 @@ __device__ __forceinline__ void put_desc(rsrc_t E, uint32_t off, uint64_t data, 
 #if defined(RR_ABLATE) && RR_ABLATE == 4   // timing-only builds (tools/): no descriptor stores
     asm volatile("" ::"v"(w.x), "v"(w.y), "v"(w.z), "v"(w.w), "v"(off));
 #else
-    __builtin_amdgcn_raw_buffer_store_b128(w, E, (int)off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(w, E, (int)off, 0, 0);   // (nontemporal: cfg 3 0.45 -> 0.73 ms, the L2 combines them)
 #endif
 }
 
