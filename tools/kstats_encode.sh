@@ -6,7 +6,7 @@ ROOT=$(pwd)
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 RR_LIB=$LIB timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT" -o run -- \
-    python3 "$ROOT/tools/time_encode.py" "$CFG" 1000000 20 > "$OUT/run.log" 2>&1
+    python3 "$ROOT/tools/time_encode.py" "$CFG" ${RR_N:-1000000} 20 > "$OUT/run.log" 2>&1
 rc=$?
 python3 "$ROOT/tools/kstats.py" $(find "$OUT" -name "*kernel_stats.csv")
 exit $rc
