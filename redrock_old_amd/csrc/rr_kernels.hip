@@ -2197,10 +2197,7 @@ constexpr uint64_t JQ_SRC = (1ull << 40) - 1;
 
 
 // waves per SIMD the emit kernel is built for (74 VGPRs, no spills; 5: E4 345 us, 6: 307 us)
-#ifndef RR_ENC_WPE
-#define RR_ENC_WPE 6
-#endif
-constexpr int ENC_WPE = RR_ENC_WPE;
+constexpr int ENC_WPE = 6;
 template <uint32_t W, uint32_t NT, uint32_t RCAP>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(ENC_WPE))) void enc_emit_kernel(const rr_value *__restrict__ values,
                                                       const rr_elem *__restrict__ elems,
