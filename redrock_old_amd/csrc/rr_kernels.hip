@@ -2208,6 +2208,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(ENC_WPE))) v
                                                       const uint64_t *__restrict__ stats, uint32_t ntiles,
                                                       rr_totals *tot, uint64_t *err, uint64_t *zsums, uint32_t nzsums) {
     static_assert(W <= 65536 && W % 64 == 0, "image offsets are 16-bit, pieces 64-byte blocks");
+    static_assert(W % (16 * NT) == 0, "image stores: whole 16-byte chunks per thread");
     // block 0 also zeroes E1's group sums, which E3 (done) read: they are zero for the next call
     // without a zeroing launch (the context keeps them in its zero-between-calls buffer)
     if (blockIdx.x == 0)
@@ -2221,28 +2222,45 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(ENC_WPE))) v
     __shared__ uint64_t rq_a[RCAP];        // run: arena offset | length << 40
     __shared__ uint32_t rq_dp[RCAP];       // run: image offset | first piece (pieces of earlier runs) << 16
     __shared__ __attribute__((aligned(16))) uint32_t tb[NT + 1];   // task base of each value of the round
-    __shared__ uint64_t sv_pos[NT];        // output position of the value's first task, less the
-                                           // element-byte scan there once its first task is costed
-    __shared__ uint32_t sv_el[NT];         // elem_base
-    __shared__ uint32_t sv_te[NT];         // type | enc << 8
+    // per value of the round: sv_pos, the output position of its first task (less the element-byte
+    // scan there once its first task is costed), sv_el its elem_base, sv_te type | enc << 8
+    __shared__ __attribute__((aligned(16))) uint64_t sv_raw[2 * NT];
+    uint64_t *const sv_pos = sv_raw;
+    uint32_t *const sv_el = reinterpret_cast<uint32_t *>(sv_raw + NT), *const sv_te = sv_el + NT;
     __shared__ uint64_t wsum[2][NT / RR_WAVE];
     __shared__ uint64_t sh_nrp;            // runs reserved | pieces reserved << 32
     __shared__ uint32_t sh_pend;           // pieces of the queued runs, when the queue overflowed
     __shared__ uint32_t sh_unal;           // some queued run is not aligned with its image offset mod 16
     uint8_t *img = reinterpret_cast<uint8_t *>(img4);
-    const uint32_t tid = threadIdx.x;
     const uint64_t total = offsets[n];
     const uint64_t lim = total < cap ? total : cap;
     const uint64_t w0 = (uint64_t)blockIdx.x * W;
     if (w0 >= lim) return;
+    // the first round of the window's records and offsets, at the kernel's start: buffer loads (no
+    // branches; lanes past the window's values read zeros), in flight under the image's zeroing
+    // (encode config 4 -1.5 %, config 2 -5 %, profiles/r5_encode_persistent_ab.txt "p0")
+    auto first_round = [&](uint64_t v0, uint64_t vend, uint64_t &a, uint64_t &b, uint4 &x) {
+        const uint32_t nv = vend - v0 < NT ? (uint32_t)(vend - v0) : NT;
+        const rsrc_t RO = make_rsrc(reinterpret_cast<const uint8_t *>(offsets + v0), (nv + 1) * 8u);
+        const rsrc_t RV = make_rsrc(reinterpret_cast<const uint8_t *>(values + v0), nv * 16u);
+        const uint32_t t = threadIdx.x;
+        a = __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(RO, (int)(t * 8), 0, 0));
+        b = __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(RO, (int)(t * 8 + 8), 0, 0));
+        x = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(RV, (int)(t * 16), 0, 0));
+    };
+    // the window's value range [v0, vend): the values holding its bytes (fv from E3)
+    const uint64_t v0 = fv[blockIdx.x];
+    const uint64_t vend = w0 + W < total ? (uint64_t)fv[blockIdx.x + 1] + 1 : n;
+    uint64_t pa, pb;
+    uint4 px;
+    first_round(v0, vend, pa, pb, px);
+    const uint32_t tid = threadIdx.x;
     EPROBE(uint64_t et0 = rr_stamp(), etk = 0, ent = 0, tf = 0, tsc = 0, twr = 0, tw1 = 0, tw2 = 0;)
     const uint64_t span = lim - w0 < W ? lim - w0 : W;
     const Img I{img, w0, span};
 #pragma unroll
     for (uint32_t k = tid; k < W / 16; k += NT) img4[k] = make_uint4(0, 0, 0, 0);
     if (tid == 0) { sh_nrp = 0; sh_pend = 0xFFFFFFFFu; sh_unal = 0; }
-    const uint64_t v0 = fv[blockIdx.x];
-    const uint64_t vend = w0 + W < total ? (uint64_t)fv[blockIdx.x + 1] + 1 : n;
     lds_barrier();
     EPROBE(const uint64_t et1 = rr_stamp();)
 
@@ -2284,9 +2302,14 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(ENC_WPE))) v
     for (uint64_t vb = v0; vb < vend; vb += NT) {
         const uint64_t v = vb + tid;
         uint32_t tasks = 0;
+        uint64_t a = pa, b = pb;
+        uint4 x = px;
+        if (vb != v0 && v < vend) {   // (rounds past the first: values of a window past NT)
+            a = offsets[v];
+            b = offsets[v + 1];
+            x = reinterpret_cast<const uint4 *>(values)[v];
+        }
         if (v < vend) {
-            const uint64_t a = offsets[v], b = offsets[v + 1];
-            const uint4 x = reinterpret_cast<const uint4 *>(values)[v];
             if (b > a && b <= cap) {
                 const uint32_t type = x.x & 0xFF, enc = (x.x >> 8) & 0xFF, ne = x.z;
                 // type, lru (5 bytes) then the type's fixed field: STRING enc (1), INTSET enc +
@@ -2435,13 +2458,18 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(ENC_WPE))) v
     lds_barrier();
     EPROBE(const uint64_t et3 = rr_stamp();)
 
-    // store the image: 16-byte chunks, bytes at a partial end
-    u32x4 *dst4 = reinterpret_cast<u32x4 *>(out + w0);
-    const u32x4 *src4 = reinterpret_cast<const u32x4 *>(img4);
-    const uint32_t full = (uint32_t)(span >> 4);
-    for (uint32_t c = tid; c < full; c += NT) __builtin_nontemporal_store(src4[c], dst4 + c);
-    const uint32_t tail = (uint32_t)(span & 15);
-    if (tid < tail) out[w0 + 16ull * full + tid] = img[16u * full + tid];
+    // store the image: 16-byte chunks (buffer stores: chunks past the window's span are dropped,
+    // every thread issues the same W / 16 / NT stores), then the bytes of a partial last chunk
+    {
+        const rsrc_t RS = make_rsrc(out + w0, (uint32_t)span & ~15u);
+        const u32x4 *src4 = reinterpret_cast<const u32x4 *>(img4);
+#pragma unroll
+        for (uint32_t k = 0; k < W / 16 / NT; ++k)
+            __builtin_amdgcn_raw_buffer_store_b128(src4[tid + k * NT], RS, (int)((tid + k * NT) * 16), 0, 2 /* nt */);
+        const uint32_t full = (uint32_t)(span >> 4), tail = (uint32_t)(span & 15);
+        const rsrc_t RT = make_rsrc(out + w0 + 16ull * full, tail);
+        __builtin_amdgcn_raw_buffer_store_b8(img[(16u * full + (tid & 15u)) & (W - 1)], RT, (int)tid, 0, 0);
+    }
     EPROBE(const uint64_t et4 = rr_stamp();
            if (tid == 0 && g_eprobe) {
                uint64_t *o = g_eprobe + (uint64_t)blockIdx.x * EPROBE_WORDS;
@@ -2904,6 +2932,7 @@ extern "C" uint64_t rr_encode_scratch_words(uint64_t n, uint64_t data_cap) {
     const uint64_t t = (n + 255) / 256, nw = enc_windows(data_cap);
     return RR_SCRATCH_HDR + 1 + 6 * t + t + (nw + 2) / 2 + 2;
 }
+
 extern "C" uint64_t rr_encode_sums_words(uint64_t n) { return (n + 255) / 256 / WGROUP + 1; }
 
 extern "C" hipError_t rr_launch_encode(const rr_value *values, const rr_elem *elems, uint64_t elem_cap,
