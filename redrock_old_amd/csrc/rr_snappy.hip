@@ -143,6 +143,35 @@ __device__ __forceinline__ uint32_t lane_mod(uint32_t lane, uint32_t off) {
     return lane - k * off;
 }
 
+// wave64 max (u32): the DPP scan's shape with max, read at the last lane
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t x) {
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false));
+    return rdl(x, WAVE - 1);
+}
+
+// Byte copies inside the LDS window, a lane each (lanes with `mine`): l bytes from s to d, 16 a
+// round (five aligned source dwords, realigned, then the bytes), every lane's reads of a round
+// before its writes.  The caller guarantees no copy of the set reads bytes another one writes.
+__device__ __forceinline__ void lane_copies(lds_u8 *win, bool mine, uint32_t s, uint32_t d, uint32_t l) {
+    lds_u32 *win32 = (lds_u32 *)win;
+    for (uint32_t r = 0; __ballot(mine && r < l); r += 16) {
+        const bool a = mine && r < l;
+        const uint32_t q = s + r, qa = a ? q >> 2 : 0u, sh = q & 3;
+        const uint32_t x0 = win32[qa], x1 = win32[qa + 1], x2 = win32[qa + 2], x3 = win32[qa + 3], x4 = win32[qa + 4];
+        const uint32_t w[4] = {__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh),
+                               __builtin_amdgcn_alignbyte(x3, x2, sh), __builtin_amdgcn_alignbyte(x4, x3, sh)};
+        const uint32_t nb = a ? (l - r < 16 ? l - r : 16u) : 0u;
+#pragma unroll
+        for (uint32_t i = 0; i < 16; ++i)
+            if (i < nb) win[d + r + i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+    }
+}
+
 // Tag decoding shared by both paths (snappy.cc:808 DecompressAllTags, oracle/rr_snappy.c):
 // t holds the 5+ bytes from the tag on (uniform).  Literals: hdr = 1 + extra length bytes,
 // len = the literal's bytes; copies: hdr = 1 + offset bytes, len / off of the back-reference.
@@ -301,8 +330,17 @@ __device__ uint32_t dec_block_lds(rsrc_t R, uint32_t s0, uint32_t clen, uint32_t
             if (f == 0xFFu) bail = true;
             return f == 0xFFu ? RR_SNAPPY_OK : f;
         }
-        // the literals
-        uint64_t m = __ballot(act && lit);
+        // the literals.  When every literal destination of the batch lies below every literal
+        // source (the usual case: the compressed bytes sit at the window's end, far above the
+        // output), the literals of at most 64 bytes are copied together, a lane each (no copy
+        // reads what another writes); the longer ones, and all of them otherwise, one after the
+        // other by the whole wave
+        const bool islit = act && lit;
+        uint64_t m = __ballot(islit);
+        if (m && wave_max_u32(islit ? tpos + len : 0u) <= ~wave_max_u32(islit ? ~(D + tq) : 0u)) {
+            lane_copies(win, islit && len <= WAVE, D + tq, tpos, len);
+            m = __ballot(islit && len > WAVE);
+        }
         while (m) {
             const int k = (int)__builtin_ctzll(m);
             m &= m - 1;
@@ -334,8 +372,17 @@ __device__ uint32_t dec_block_lds(rsrc_t R, uint32_t s0, uint32_t clen, uint32_t
                 } while (i < body);
             }
         }
-        // the back-references, in stream order: out[pos + j] = out[pos - off + j % off]
-        m = __ballot(act && !lit);
+        // the back-references: those that do not overlap themselves and read only output before
+        // the batch's first back-reference (final once the literals are in) together, a lane
+        // each; then the others in stream order: out[pos + j] = out[pos - off + j % off]
+        const bool iscop = act && !lit;
+        m = __ballot(iscop);
+        if (m) {
+            const uint32_t c0 = rdl(tpos, (uint32_t)__builtin_ctzll(m));
+            const bool indep = iscop && off >= len && tpos - off + len <= c0;
+            lane_copies(win, indep, tpos - off, tpos, len);
+            m = __ballot(iscop && !indep);
+        }
         while (m) {
             const int k = (int)__builtin_ctzll(m);
             m &= m - 1;
