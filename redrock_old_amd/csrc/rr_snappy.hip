@@ -45,8 +45,8 @@ constexpr uint32_t SNZ_DEC_WIN = RR_SNZ_DEC_WIN;
 #define RR_SNZ_FRAG 0
 #endif
 constexpr uint32_t SNZ_FRAG_LDS = RR_SNZ_FRAG;
-// 1: the decompressor's tag chain through speculative sizes at 256 positions (a readlane a
-// tag); 0: one LDS read a tag
+// the decompressor's tag chain through speculative tag sizes at 64 * RR_SNZ_SPEC positions (1,
+// 2 or 4 a lane; a readlane a tag); 0: one LDS read a tag
 #ifndef RR_SNZ_SPEC
 #define RR_SNZ_SPEC 1
 #endif
@@ -68,6 +68,29 @@ __device__ __forceinline__ uint32_t rdl(uint32_t v, uint32_t l) {
 }
 
 // ---- decompression ------------------------------------------------------------------------
+#ifdef RR_PROBE
+// Decompress probe (diagnostics; tools/probe_snappy.py): cycles (s_memtime) per phase summed over
+// the call's LDS-path blocks: stage, A (tag chain), B (tag decode + checks), literals,
+// back-references, output; [6] blocks, [7] batches, [8] tags
+__device__ unsigned long long g_snz_probe[9];
+extern "C" int rr_snz_probe_read(unsigned long long *out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_snz_probe), sizeof(g_snz_probe)) == hipSuccess ? 0 : -1;
+}
+extern "C" int rr_snz_probe_reset() {
+    static const unsigned long long z[9] = {0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_snz_probe), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+__device__ __forceinline__ uint64_t snz_stamp() {
+    uint64_t t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt lgkmcnt(0) vmcnt(0)\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#define SNZP(...) __VA_ARGS__
+#else
+#define SNZP(...)
+#endif
 __global__ __launch_bounds__(256) void snz_len_kernel(const uint8_t *__restrict__ in,
                                                       const uint64_t *__restrict__ in_offs, uint64_t n,
                                                       uint64_t *__restrict__ out_offs, uint8_t *__restrict__ status,
@@ -222,6 +245,7 @@ __device__ uint32_t dec_block_lds(rsrc_t R, uint32_t s0, uint32_t clen, uint32_t
     typedef __attribute__((address_space(3))) u32x4_t lds_u32x4;
     const uint32_t lane = lane_id(), end = s0 + clen, ng = (end + 15) >> 4;
     const uint32_t D = wcap + 16 - 16 * ng;   // (the allocation's last 16 bytes: reads past the end)
+    SNZP(uint64_t pt = snz_stamp(), pa = 0, pb = 0, pl = 0, pc = 0, nbat = 0, ntag = 0; const uint64_t p0 = pt;)
     {
         constexpr uint32_t SG = (SNZ_DEC_WIN + 16) / 16 / WAVE + 1;
         u32x4_t g[SG];
@@ -245,40 +269,49 @@ __device__ uint32_t dec_block_lds(rsrc_t R, uint32_t s0, uint32_t clen, uint32_t
         ++p;
     }
     uint32_t pos = 0;
+    SNZP(uint64_t pst; { const uint64_t t = snz_stamp(); pst = t - p0; pt = t; })
     while (p < end) {
-        // A. up to 64 tag starts.  The size a tag would have at each of the 256 positions from p
-        //    on (4 a lane, speculatively: one LDS round trip and a few VALU ops), then the chain
+        // A. up to 64 tag starts.  The size a tag would have at each of the 64 * PP positions from
+        //    p on (PP a lane, speculatively: one LDS round trip and a few VALU ops), then the chain
         //    through them by readlanes — a few cycles a tag instead of an LDS round trip; a tag
-        //    that lands past the 256 positions (a long literal) starts the next round.
+        //    that lands past those positions (a long literal) starts the next round.
         uint32_t tp = 0, nt = 0;
 #if RR_SNZ_SPEC
+        constexpr uint32_t PP = RR_SNZ_SPEC;   // positions a lane
+        static_assert(PP == 1 || PP == 2 || PP == 4, "positions a lane");
         do {
-            const uint32_t wp = p, ab = (D + wp) & ~3u, sh = (D + wp) & 3u;
-            const uint32_t w0 = win32[(ab >> 2) + lane], w1 = win32[(ab >> 2) + lane + 1], w2 = win32[(ab >> 2) + lane + 2];
+            const uint32_t wp = p, ab = (D + wp) & ~3u, bo = ((D + wp) & 3u) + PP * lane;
+            const uint32_t di = (ab >> 2) + (bo >> 2), bs = bo & 3;
+            const uint32_t w0 = win32[di], w1 = win32[di + 1], w2 = PP > 1 ? win32[di + 2] : 0u;   // (one position: 8 bytes hold it)
             const uint64_t x01 = ((uint64_t)w1 << 32) | w0, x12 = ((uint64_t)w2 << 32) | w1;
-            uint32_t sz4[4];
+            uint32_t sp[(PP + 1) / 2];
 #pragma unroll
-            for (uint32_t j = 0; j < 4; ++j) {
-                const uint32_t o = sh + j;   // (0 .. 6: the position's bytes from the lane's three dwords)
-                const uint64_t t = o < 4 ? x01 >> (8 * o) : x12 >> (8 * (o - 4));
-                const uint32_t q = wp + 4 * lane + j, c = (uint32_t)t & 0xFF, ty = c & 3, c6 = (c >> 2) + 1;
+            for (uint32_t j = 0; j < PP; ++j) {
+                const uint32_t o = bs + j;   // (0 .. 6: the position's bytes from the lane's three dwords)
+                const uint64_t t = PP == 1 ? x01 >> (8 * o) : o < 4 ? x01 >> (8 * o) : x12 >> (8 * (o - 4));
+                const uint32_t q = wp + PP * lane + j, c = (uint32_t)t & 0xFF, ty = c & 3, c6 = (c >> 2) + 1;
                 const uint32_t nb = c6 > 60 ? c6 - 60 : 0u, v = (uint32_t)(t >> 8);
                 const uint64_t len = nb ? (uint64_t)(nb == 4 ? v : v & ((1u << (8 * nb)) - 1)) + 1 : c6;
                 const uint32_t rem = q < end ? end - q : 0u;
                 const uint32_t lsz = len >= rem ? rem + 1 : (uint32_t)(1 + nb + len);   // (past the end: phase B's TRUNC)
-                sz4[j] = ty == 0 ? lsz : ty == 1 ? 2u : ty == 2 ? 3u : 5u;
+                const uint32_t sz = ty == 0 ? lsz : ty == 1 ? 2u : ty == 2 ? 3u : 5u;
+                if (PP == 1) sp[0] = sz;
+                else if (j & 1) sp[j >> 1] |= sz << 16;
+                else sp[j >> 1] = sz & 0xFFFF;
             }
-            const uint32_t s01 = (sz4[0] & 0xFFFF) | (sz4[1] << 16), s23 = (sz4[2] & 0xFFFF) | (sz4[3] << 16);
             // (sizes past 16 bits only on the last tag: rem + 1 <= the block's bytes < 2^16, or
             //  a literal as long as the rest, which ends the block's chain either way)
             do {
-                const uint32_t r = p - wp, l = r >> 2, j = r & 3;
-                const uint32_t pair = rdl(j < 2 ? s01 : s23, l);
-                const uint32_t sz = (j & 1) ? pair >> 16 : pair & 0xFFFF;
+                const uint32_t r = p - wp, l = r / PP, j = r % PP;
+                uint32_t v = sp[0];
+#pragma unroll
+                for (uint32_t k = 1; k < (PP + 1) / 2; ++k) v = (j >> 1) == k ? sp[k] : v;
+                const uint32_t pair = rdl(v, l);
+                const uint32_t sz = PP == 1 ? pair : (j & 1) ? pair >> 16 : pair & 0xFFFF;
                 tp = lane == nt ? p : tp;
                 ++nt;
                 p += sz;
-            } while (nt < WAVE && p < end && p - wp < 4 * WAVE);
+            } while (nt < WAVE && p < end && p - wp < PP * WAVE);
         } while (nt < WAVE && p < end);
 #else
         do {
@@ -297,6 +330,7 @@ __device__ uint32_t dec_block_lds(rsrc_t R, uint32_t s0, uint32_t clen, uint32_t
             p += sz;
         } while (nt < WAVE && p < end);
 #endif
+        SNZP({ const uint64_t t = snz_stamp(); pa += t - pt; pt = t; ++nbat; ntag += nt; })
         // B. the batch's tags, one per lane
         const bool act = lane < nt;
         const uint32_t a = D + (act ? tp : 0);
@@ -325,6 +359,7 @@ __device__ uint32_t dec_block_lds(rsrc_t R, uint32_t s0, uint32_t clen, uint32_t
                         : tpos + len > D + tpn ? 0xFFu : 0u;
         }
         const uint64_t badm = __ballot(code != 0);
+        SNZP({ const uint64_t t = snz_stamp(); pb += t - pt; pt = t; })
         if (badm) {
             const uint32_t f = (uint32_t)__builtin_amdgcn_readlane((int)code, (int)__builtin_ctzll(badm));
             if (f == 0xFFu) bail = true;
@@ -372,6 +407,7 @@ __device__ uint32_t dec_block_lds(rsrc_t R, uint32_t s0, uint32_t clen, uint32_t
                 } while (i < body);
             }
         }
+        SNZP({ const uint64_t t = snz_stamp(); pl += t - pt; pt = t; })
         // the back-references: those that do not overlap themselves and read only output before
         // the batch's first back-reference (final once the literals are in) together, a lane
         // each; then the others in stream order: out[pos + j] = out[pos - off + j % off]
@@ -394,7 +430,14 @@ __device__ uint32_t dec_block_lds(rsrc_t R, uint32_t s0, uint32_t clen, uint32_t
             if (lane < l) win[dpos + lane] = x;
         }
         pos = (uint32_t)__builtin_amdgcn_readlane((int)(tpos + ol), (int)(nt - 1));
+        SNZP({ const uint64_t t = snz_stamp(); pc += t - pt; pt = t; })
     }
+    SNZP(if (lane == 0) {
+        atomicAdd(&g_snz_probe[0], (unsigned long long)pst); atomicAdd(&g_snz_probe[1], (unsigned long long)pa);
+        atomicAdd(&g_snz_probe[2], (unsigned long long)pb); atomicAdd(&g_snz_probe[3], (unsigned long long)pl);
+        atomicAdd(&g_snz_probe[4], (unsigned long long)pc); atomicAdd(&g_snz_probe[6], 1ull);
+        atomicAdd(&g_snz_probe[7], (unsigned long long)nbat); atomicAdd(&g_snz_probe[8], (unsigned long long)ntag);
+    })
     return pos == expected ? RR_SNAPPY_OK : RR_SNAPPY_E_LENGTH;
 }
 
@@ -467,6 +510,7 @@ __global__ __launch_bounds__(WAVE) void snz_dec_kernel(const uint8_t *__restrict
             const uint64_t span = (s0 + clen + 15) & ~15ull;
             st = dec_block_lds(mkr(in + base, span < in_cap - base ? span : in_cap - base), s0, (uint32_t)clen, expected,
                                win, wcap, bail);
+            SNZP(const uint64_t po0 = snz_stamp();)
             if (!bail && st == RR_SNAPPY_OK) {   // LDS -> output: bytes to a 4-aligned address, 16 B per lane, bytes
                 const uint32_t g0 = (uint32_t)((uintptr_t)gout & 3), hh = min((4u - g0) & 3, expected);
                 const uint32_t t0 = hh + ((expected - hh) & ~3u);
@@ -487,6 +531,7 @@ __global__ __launch_bounds__(WAVE) void snz_dec_kernel(const uint8_t *__restrict
                 }
                 if (t0 + lane < expected) __builtin_amdgcn_raw_buffer_store_b8(win[t0 + lane], Ro, (int)(t0 + lane), 0, 0);
             }
+            SNZP(if (lane == 0) atomicAdd(&g_snz_probe[5], (unsigned long long)(snz_stamp() - po0));)
         }
         if (bail) st = dec_block_global(mkr(in + base, in_cap - base), s0, (uint32_t)clen, expected, Ro);
         if (lane == 0) status[b] = (uint8_t)st;

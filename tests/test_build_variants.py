@@ -30,6 +30,7 @@ VARIANTS = [
     ("rr_snappy.hip", "-DRR_SNZ_K=1"),
     ("rr_snappy.hip", "-DRR_SNZ_K=32"),
     ("rr_snappy.hip", "-DRR_SNZ_SPEC=0"),
+    ("rr_snappy.hip", "-DRR_PROBE"),
 ]
 
 
