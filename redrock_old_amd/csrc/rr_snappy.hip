@@ -365,17 +365,16 @@ __device__ uint32_t dec_block_lds(rsrc_t R, uint32_t s0, uint32_t clen, uint32_t
             if (f == 0xFFu) bail = true;
             return f == 0xFFu ? RR_SNAPPY_OK : f;
         }
-        // the literals.  When every literal destination of the batch lies below every literal
-        // source (the usual case: the compressed bytes sit at the window's end, far above the
-        // output), the literals of at most 64 bytes are copied together, a lane each (no copy
-        // reads what another writes); the longer ones, and all of them otherwise, one after the
-        // other by the whole wave
+        // the literals.  When every literal destination of the batch (and the up to 3 bytes a
+        // long literal's last dword spills past its end) lies below every literal source (the
+        // usual case: the compressed bytes sit at the window's end, far above the output), the
+        // literals longer than 64 bytes go first, one after the other by the whole wave, then the
+        // others together, a lane each (exact bytes: they land after any spill into them, and no
+        // copy reads what another writes); otherwise all of them one after the other
         const bool islit = act && lit;
         uint64_t m = __ballot(islit);
-        if (m && wave_max_u32(islit ? tpos + len : 0u) <= ~wave_max_u32(islit ? ~(D + tq) : 0u)) {
-            lane_copies(win, islit && len <= WAVE, D + tq, tpos, len);
-            m = __ballot(islit && len > WAVE);
-        }
+        const bool par = m && wave_max_u32(islit ? tpos + len + 4 : 0u) <= ~wave_max_u32(islit ? ~(D + tq) : 0u);
+        if (par) m = __ballot(islit && len > WAVE);
         while (m) {
             const int k = (int)__builtin_ctzll(m);
             m &= m - 1;
@@ -407,6 +406,7 @@ __device__ uint32_t dec_block_lds(rsrc_t R, uint32_t s0, uint32_t clen, uint32_t
                 } while (i < body);
             }
         }
+        if (par) lane_copies(win, islit && len <= WAVE, D + tq, tpos, len);
         SNZP({ const uint64_t t = snz_stamp(); pl += t - pt; pt = t; })
         // the back-references: those that do not overlap themselves and read only output before
         // the batch's first back-reference (final once the literals are in) together, a lane

@@ -204,3 +204,52 @@ def test_reference_baddata_and_corruption(engine):
     verdicts = [int(x) == 0 for x in st]
     assert verdicts[:3] == [False, False, False]
     assert verdicts[3:] == [v for _, _, v, _ in cases]
+
+
+def _lit(b):
+    """A literal tag with its bytes (snappy format: lengths <= 60 in the tag byte, else 1-2 more)."""
+    n = len(b)
+    if n <= 60:
+        return bytes([(n - 1) << 2]) + b
+    if n <= 256:
+        return bytes([60 << 2, n - 1]) + b
+    return bytes([61 << 2, (n - 1) & 0xFF, (n - 1) >> 8]) + b
+
+
+def _copy1(length, off):   # 1-byte-offset copy: 4 <= length <= 11, off < 2048
+    return bytes([1 | ((length - 4) << 2) | ((off >> 8) << 5), off & 0xFF])
+
+
+def _varint(v):
+    out = bytearray()
+    while v >= 0x80:
+        out.append((v & 0x7F) | 0x80)
+        v >>= 7
+    out.append(v)
+    return bytes(out)
+
+
+def test_consecutive_literals(engine):
+    """Streams with literal after literal (valid snappy that snappy's own compressor never writes):
+    a long literal's last dword may spill past its end in the LDS path, so the literal after it
+    must land after the spill. Every length mod 4 and every destination alignment, against the
+    oracle."""
+    rng = np.random.default_rng(7)
+    streams = []
+    for a in range(4):   # destination alignment of the long literal
+        for la in range(65, 73):   # long literal lengths: every value mod 4 (and mod 8)
+            for lb in (1, 2, 3, 5, 17, 64, 65, 70):
+                parts, out = [], b""
+                if a:
+                    x = rng.integers(0, 256, a, dtype=np.uint8).tobytes()
+                    parts.append(_lit(x)); out += x
+                for n_ in (la, lb, la + 3, 7):
+                    x = rng.integers(0, 256, n_, dtype=np.uint8).tobytes()
+                    parts.append(_lit(x)); out += x
+                parts.append(_copy1(8, 5)); out += bytes(out[len(out) - 5 + (i % 5)] for i in range(8))
+                x = rng.integers(0, 256, 90, dtype=np.uint8).tobytes()
+                parts.append(_lit(x)); out += x
+                s = _varint(len(out)) + b"".join(parts)
+                assert cpu.snappy_uncompress(s) == (0, out)
+                streams.append(s)
+    check_decompress(engine, streams, "consecutive literals")
