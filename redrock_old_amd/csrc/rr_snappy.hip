@@ -189,9 +189,23 @@ __device__ __forceinline__ void lane_copies(lds_u8 *win, bool mine, uint32_t s, 
         const uint32_t w[4] = {__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh),
                                __builtin_amdgcn_alignbyte(x3, x2, sh), __builtin_amdgcn_alignbyte(x4, x3, sh)};
         const uint32_t nb = a ? (l - r < 16 ? l - r : 16u) : 0u;
+        // destination-aligned: up to 3 head bytes, whole dwords (the stream realigned by the head),
+        // up to 3 tail bytes — at most 10 LDS writes instead of 16 byte writes
+        const uint32_t dst = d + r, h0 = (4u - (dst & 3)) & 3, h = h0 < nb ? h0 : nb;
+        const uint32_t fd = (nb - h) >> 2, tl = (nb - h) & 3;
 #pragma unroll
-        for (uint32_t i = 0; i < 16; ++i)
-            if (i < nb) win[d + r + i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+        for (uint32_t i = 0; i < 3; ++i)
+            if (i < h) win[dst + i] = (uint8_t)(w[0] >> (8 * i));
+        lds_u32 *dd = (lds_u32 *)(win + ((dst + h) & ~3u));
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k)
+            if (k < fd) dd[k] = __builtin_amdgcn_alignbyte(k + 1 < 4 ? w[k + 1] : 0u, w[k], h);
+        const uint32_t lo = fd == 0 ? w[0] : fd == 1 ? w[1] : fd == 2 ? w[2] : w[3];
+        const uint32_t hi = fd == 0 ? w[1] : fd == 1 ? w[2] : fd == 2 ? w[3] : 0u;
+        const uint32_t T = __builtin_amdgcn_alignbyte(hi, lo, h);
+#pragma unroll
+        for (uint32_t i = 0; i < 3; ++i)
+            if (i < tl) win[dst + h + 4 * fd + i] = (uint8_t)(T >> (8 * i));
     }
 }
 
@@ -287,8 +301,17 @@ __device__ uint32_t dec_block_lds(rsrc_t R, uint32_t s0, uint32_t clen, uint32_t
             uint32_t sp[(PP + 1) / 2];
 #pragma unroll
             for (uint32_t j = 0; j < PP; ++j) {
+                if (PP == 1) {   // (32-bit: the tag byte and the 4 bytes after it by alignbyte, len - 1)
+                    const uint32_t c = __builtin_amdgcn_alignbyte(w1, w0, bs) & 0xFF, ty = c & 3, c6 = (c >> 2) + 1;
+                    const uint32_t v = bs == 3 ? w1 : __builtin_amdgcn_alignbyte(w1, w0, bs + 1);
+                    const uint32_t q = wp + lane, nb = c6 > 60 ? c6 - 60 : 0u;
+                    const uint32_t lm1 = nb ? (nb == 4 ? v : v & ((1u << (8 * nb)) - 1)) : c6 - 1;
+                    const uint32_t lsz = q >= end ? 1u : lm1 >= end - q - 1 ? end - q + 1 : 2 + nb + lm1;   // (past the end: phase B's TRUNC)
+                    sp[0] = ty == 0 ? lsz : ty == 1 ? 2u : ty == 2 ? 3u : 5u;
+                    continue;
+                }
                 const uint32_t o = bs + j;   // (0 .. 6: the position's bytes from the lane's three dwords)
-                const uint64_t t = PP == 1 ? x01 >> (8 * o) : o < 4 ? x01 >> (8 * o) : x12 >> (8 * (o - 4));
+                const uint64_t t = o < 4 ? x01 >> (8 * o) : x12 >> (8 * (o - 4));
                 const uint32_t q = wp + PP * lane + j, c = (uint32_t)t & 0xFF, ty = c & 3, c6 = (c >> 2) + 1;
                 const uint32_t nb = c6 > 60 ? c6 - 60 : 0u, v = (uint32_t)(t >> 8);
                 const uint64_t len = nb ? (uint64_t)(nb == 4 ? v : v & ((1u << (8 * nb)) - 1)) + 1 : c6;
