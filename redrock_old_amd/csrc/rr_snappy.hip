@@ -301,13 +301,17 @@ __device__ uint32_t dec_block_lds(rsrc_t R, uint32_t s0, uint32_t clen, uint32_t
             uint32_t sp[(PP + 1) / 2];
 #pragma unroll
             for (uint32_t j = 0; j < PP; ++j) {
-                if (PP == 1) {   // (32-bit: the tag byte and the 4 bytes after it by alignbyte, len - 1)
-                    const uint32_t c = __builtin_amdgcn_alignbyte(w1, w0, bs) & 0xFF, ty = c & 3, c6 = (c >> 2) + 1;
-                    const uint32_t v = bs == 3 ? w1 : __builtin_amdgcn_alignbyte(w1, w0, bs + 1);
-                    const uint32_t q = wp + lane, nb = c6 > 60 ? c6 - 60 : 0u;
+                if (PP <= 2) {   // (32-bit: the tag byte and the 4 bytes after it by alignbyte, len - 1)
+                    const uint32_t o = bs + j;   // (0 .. 4)
+                    const uint32_t c = (o < 4 ? __builtin_amdgcn_alignbyte(w1, w0, o) : w1) & 0xFF, ty = c & 3, c6 = (c >> 2) + 1;
+                    const uint32_t v = o < 3 ? __builtin_amdgcn_alignbyte(w1, w0, o + 1) : o == 3 ? w1 : __builtin_amdgcn_alignbyte(w2, w1, 1);
+                    const uint32_t q = wp + PP * lane + j, nb = c6 > 60 ? c6 - 60 : 0u;
                     const uint32_t lm1 = nb ? (nb == 4 ? v : v & ((1u << (8 * nb)) - 1)) : c6 - 1;
                     const uint32_t lsz = q >= end ? 1u : lm1 >= end - q - 1 ? end - q + 1 : 2 + nb + lm1;   // (past the end: phase B's TRUNC)
-                    sp[0] = ty == 0 ? lsz : ty == 1 ? 2u : ty == 2 ? 3u : 5u;
+                    const uint32_t sz = ty == 0 ? lsz : ty == 1 ? 2u : ty == 2 ? 3u : 5u;
+                    if (PP == 1) sp[0] = sz;
+                    else if (j & 1) sp[j >> 1] |= sz << 16;
+                    else sp[j >> 1] = sz & 0xFFFF;
                     continue;
                 }
                 const uint32_t o = bs + j;   // (0 .. 6: the position's bytes from the lane's three dwords)
