@@ -1773,6 +1773,42 @@ __device__ __forceinline__ bool build_task_map(uint8_t *tmap, uint32_t *wmax, ui
     }
     return usemap;
 }
+#ifdef RR_PROBE
+// Encode probe (tools/probe_encode.py): per window {init, headers, tasks, copy, store, total,
+// values, tasks, pieces} in s_memrealtime ticks (100 MHz); diagnostics only.
+constexpr uint32_t EPROBE_WORDS = 13;
+__device__ uint64_t *g_eprobe;
+extern "C" int rr_eprobe_set(void *p) { return hipMemcpyToSymbol(HIP_SYMBOL(g_eprobe), &p, sizeof(p)) == hipSuccess ? 0 : -1; }
+__device__ __forceinline__ uint64_t rr_stamp() {
+    uint64_t t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#define EPROBE(...) __VA_ARGS__
+// E1 (enc_size_kernel) phases summed over the call's blocks: [0] head (records, the short
+// values' descriptors, the task scan and map), [1] the task rounds, [2] the sizes' scan and
+// stores, [3] blocks, [4] tasks, [5] rounds; s_memtime after every outstanding memory operation
+__device__ unsigned long long g_e1probe[6];
+extern "C" int rr_e1probe_read(unsigned long long *out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_e1probe), sizeof(g_e1probe)) == hipSuccess ? 0 : -1;
+}
+extern "C" int rr_e1probe_reset() {
+    static const unsigned long long z[6] = {0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_e1probe), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+__device__ __forceinline__ uint64_t e1_stamp() {
+    uint64_t t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#else
+#define EPROBE(...)
+#endif
+
 template <uint32_t NT, uint32_t U>
 __global__ __launch_bounds__(NT) void enc_size_kernel(const rr_value *__restrict__ values,
                                                       const rr_elem *__restrict__ elems, uint64_t n,
@@ -1781,6 +1817,7 @@ __global__ __launch_bounds__(NT) void enc_size_kernel(const rr_value *__restrict
                                                       uint64_t *__restrict__ btot, uint64_t *gtot,
                                                       uint64_t *zero_words, uint32_t nzero, rr_totals *tot) {
     zero_call_words(zero_words, nzero, tot);
+    EPROBE(const uint64_t e1t0 = e1_stamp(); uint64_t e1t1 = 0, e1nr = 0;)
     __shared__ uint32_t tb[NT + 1];                  // first task of each value
     __shared__ uint32_t s_el[NT], s_te[NT], s_bad[NT];
     __shared__ uint64_t s_b1[NT], s_p1[NT];   // the value's byte / payload sums (short values: their own lane's)
@@ -1852,6 +1889,7 @@ __global__ __launch_bounds__(NT) void enc_size_kernel(const rr_value *__restrict
     tb[tid] = base;
     if (tid == NT - 1) tb[NT] = base + ntask;
     const bool usemap = build_task_map<NT>(tmap, wmax, base, ntask, TT);
+    EPROBE(e1t1 = e1_stamp();)
     auto fetch = [&](uint64_t t, uint32_t &pj, ElemV &pe) {
         pj = 0;
         pe = ElemV{0, 0, 0};
@@ -1904,6 +1942,7 @@ __global__ __launch_bounds__(NT) void enc_size_kernel(const rr_value *__restrict
         }
     }
     lds_barrier();
+    EPROBE(const uint64_t e1t2 = e1_stamp(); e1nr = (TT + U * NT - 1) / (U * NT);)
     uint64_t size = 0, pay = 0;
     if (v < n) {
         bad = s_bad[tid];
@@ -1927,6 +1966,12 @@ __global__ __launch_bounds__(NT) void enc_size_kernel(const rr_value *__restrict
         for (uint32_t k = 0; k < NT / RR_WAVE; ++k) sum += red[tid][k];
         stats[3 * (uint64_t)blockIdx.x + tid] = sum;
     }
+    EPROBE(const uint64_t e1t3 = e1_stamp();
+           if (tid == 0) {
+               atomicAdd(&g_e1probe[0], (unsigned long long)(e1t1 - e1t0)); atomicAdd(&g_e1probe[1], (unsigned long long)(e1t2 - e1t1));
+               atomicAdd(&g_e1probe[2], (unsigned long long)(e1t3 - e1t2)); atomicAdd(&g_e1probe[3], 1ull);
+               atomicAdd(&g_e1probe[4], (unsigned long long)TT); atomicAdd(&g_e1probe[5], (unsigned long long)e1nr);
+           })
 }
 
 // ---- E3: window index + capacity check ---------------------------------------------------
@@ -1992,23 +2037,7 @@ __global__ __launch_bounds__(256) void enc_index_kernel(const rr_value *__restri
     }
 }
 
-#ifdef RR_PROBE
-// Encode probe (tools/probe_encode.py): per window {init, headers, tasks, copy, store, total,
-// values, tasks, pieces} in s_memrealtime ticks (100 MHz); diagnostics only.
-constexpr uint32_t EPROBE_WORDS = 13;
-__device__ uint64_t *g_eprobe;
-extern "C" int rr_eprobe_set(void *p) { return hipMemcpyToSymbol(HIP_SYMBOL(g_eprobe), &p, sizeof(p)) == hipSuccess ? 0 : -1; }
-__device__ __forceinline__ uint64_t rr_stamp() {
-    uint64_t t;
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    return t;
-}
-#define EPROBE(...) __VA_ARGS__
-#else
-#define EPROBE(...)
-#endif
+
 
 
 // ---- E4: window emission -------------------------------------------------------------------

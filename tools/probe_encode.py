@@ -49,3 +49,14 @@ print(f"cfg {cfg}: {len(p)} windows of {W} B, values/window {p[:, 6].mean():.1f}
 for i, name in [(0, "init"), (1, "headers"), (2, "tasks"), (10, " es+scan"), (11, " writes"), (9, "  field"), (12, "  decimal"),
                 (3, "copy"), (4, "store"), (5, "total")]:
     print(f"  {name:8s} mean {p[:, i].mean() * 10 / 1000:8.2f} us  p90 {np.percentile(p[:, i], 90) * 10 / 1000:8.2f} us")
+# E1 (enc_size_kernel): phases summed over one call's blocks (s_memtime cycles)
+assert L.rr_e1probe_reset() == 0
+eng.encode_device(d_vals, d_elems, d_arena, d_out, d_ooffs, d_tot)
+torch.cuda.synchronize()
+e1 = (C.c_ulonglong * 6)()
+assert L.rr_e1probe_read(e1) == 0
+blk = max(e1[3], 1)
+print(f"E1: {e1[3]} blocks, {e1[4] / blk:.0f} round tasks and {e1[5] / blk:.1f} rounds a block")
+tot = e1[0] + e1[1] + e1[2]
+for k, name in enumerate(["head", "rounds", "tail"]):
+    print(f"  {name:8s} {e1[k] / blk:10.0f} cycles/block  {e1[k] / max(tot, 1):6.3f}")
