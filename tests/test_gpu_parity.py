@@ -506,8 +506,15 @@ def test_fuzz_structured_decode_and_reencode(engine, cfg, n):
     length fields overwritten with small / boundary / huge values (counts, lengths, zlbytes /
     zltail / zllen, intset width and count, encoding bytes), inserted and swapped bytes.  The
     GPU's records, descriptors and totals equal the oracle's value for value, and every value
-    that decoded re-encodes to the oracle's bytes."""
-    rng = np.random.default_rng(1000 + cfg)
+    that decoded re-encodes to the oracle's bytes.  RR_FUZZ_ROUNDS=k repeats it with k seeds
+    (an extended run; the suite runs one)."""
+    import os
+    for k in range(int(os.environ.get("RR_FUZZ_ROUNDS", "1"))):
+        _fuzz_structured_round(engine, cfg, n, 1000 + cfg + 7919 * k)
+
+
+def _fuzz_structured_round(engine, cfg, n, seed):
+    rng = np.random.default_rng(seed)
     data, offs = rr.gen_batch(cfg, n)
     specials = [0, 1, 2, 3, 4, 7, 8, 15, 16, 0x7F, 0x80, 0xFE, 0xFF, 0xFFFF, 0x10000, 0x7FFFFFFF, 0xFFFFFFFF]
     blobs = []
@@ -538,7 +545,7 @@ def test_fuzz_structured_decode_and_reencode(engine, cfg, n):
     fdata, foffs = batch_from_blobs(blobs)
     v, e, a, t = engine.decode_host(fdata, foffs)
     ov, oe, oa, ot = cpu.decode(fdata, foffs, nthreads=8)
-    assert_flat_equal((v, e), (ov, oe), f"structured fuzz cfg {cfg}")
+    assert_flat_equal((v, e), (ov, oe), f"structured fuzz cfg {cfg} seed {seed}")
     assert t == ot
     assert (v["status"] != 0).any() and (v["status"] == 0).any()
     # every value that decoded re-encodes like the oracle's encode of the same flat batch
