@@ -92,7 +92,15 @@ def test_decompress_crafted(engine):
 
 
 def test_decompress_mutated(engine):
-    rng = np.random.default_rng(11)
+    """400 mutated streams a round (1-3 random bytes overwritten in five corpus streams): every
+    status and output equal to the oracle's.  RR_FUZZ_ROUNDS=k runs k seeds (an extended run)."""
+    import os
+    for k in range(int(os.environ.get("RR_FUZZ_ROUNDS", "1"))):
+        _mutated_round(engine, 11 + 7919 * k)
+
+
+def _mutated_round(engine, seed):
+    rng = np.random.default_rng(seed)
     c = corpus()
     streams = []
     for name in ("text_150k", "markup_100k", "blobs_cfg4_200k", "pattern_4", "zeros_100k"):
