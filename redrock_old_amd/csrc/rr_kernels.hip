@@ -2929,7 +2929,27 @@ extern "C" hipError_t rr_launch_decode(const uint8_t *blob, const uint64_t *offs
                                        rr_elem *elems, uint64_t elem_cap, uint8_t *arena, uint64_t *scratch,
                                        uint64_t *sums, uint64_t *zero, uint64_t nzero, uint64_t data_cap,
                                        rr_totals *totals, hipStream_t stream, int first_only) {
-    const uint32_t win = dec_win(data_cap), nw = (uint32_t)(data_cap / win + 1);
+    uint32_t win = dec_win(data_cap), nw = (uint32_t)(data_cap / win + 1);
+    // A small batch that fits one window per CU, at most a sort chunk (512 values) a window, gets
+    // one window per CU instead of two: config 1 at 100K values 22.0 -> 19.1 us, config 2 / 4 at
+    // 30K values -16 % / -10 %; at 200K config-1 values (781 a window) two per CU stay faster
+    // (profiles/r5_small_windows_ab.txt).  Fewer windows than dec_windows(data_cap): the scratch
+    // and the sums sized from data_cap still cover them.
+    static uint64_t cus = 0;
+    if (!cus) {
+        int dev = 0, c = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
+        cus = c > 0 ? (uint64_t)c : 1;
+    }
+    if (data_cap <= cus * DEC_W && n <= cus * DEC_NW * RR_WAVE) {
+        uint64_t w = ((data_cap + cus - 1) / cus + 15) & ~15ull;
+        w = w < DEC_WMIN ? DEC_WMIN : w;
+        if (w > win) {
+            win = (uint32_t)w;
+            nw = (uint32_t)(data_cap / win + 1);
+        }
+    }
     uint64_t *wtot = sums;
     uint64_t *gtot = wtot + nw;
     uint32_t *counts = reinterpret_cast<uint32_t *>(scratch + RR_SCRATCH_HDR);
