@@ -473,8 +473,9 @@ static void flatten(flat_t *f, robj *o) {
     v->n_elems = (uint32_t)(f->ne - v->elem_base);
 }
 
-/* The serialize path's buffers, per thread and kept across calls (they only grow): the
- * evictor's per-key serObject allocates nothing here after its first calls. */
+/* The serialize path's buffers, per thread and kept across calls: the evictor's per-key
+ * serObject allocates nothing here after its first calls (a one-off large batch's growth is
+ * given back at the end of rr_compat_ser_batch). */
 static __thread flat_t t_flat;
 static __thread uint64_t *t_offs;
 static __thread uint8_t *t_data;

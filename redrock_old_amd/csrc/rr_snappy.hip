@@ -40,7 +40,8 @@ constexpr uint32_t MARGIN = 15;            // kInputMarginBytes
 #endif
 constexpr uint32_t SNZ_DEC_WIN = RR_SNZ_DEC_WIN;
 // staged fragment bytes per wave; 0 (default): the compressor reads its input in place through
-// the buffer resource, so a wave holds only the 32 KiB hash table (4 waves per CU instead of 3)
+// the buffer resource, so a wave holds only the 32 KiB hash table (5 waves per CU instead of 3;
+// 18432 measured configs 4 / 3 5 % slower, config 2 +33 %: profiles/r5_snappy_compress_literal_ab.txt)
 #ifndef RR_SNZ_FRAG
 #define RR_SNZ_FRAG 0
 #endif
@@ -601,6 +602,7 @@ struct Frag {
 struct Out {
     rsrc_t R;
     uint32_t op;
+    uint32_t mis;   // the slot's address mod 4 (its base is any byte)
     __device__ __forceinline__ void put(uint32_t nbytes, uint64_t v) {   // up to 8 bytes, lanes < nbytes
         const uint32_t l = lane_id();
         if (l < nbytes) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(v >> (8 * l)), R, (int)(op + l), 0, 0);
@@ -614,9 +616,37 @@ struct Out {
             const uint32_t count = (log2floor(n1) >> 3) + 1;
             put(1 + count, (uint64_t)((59 + count) << 2) | ((uint64_t)n1 << 8));
         }
+        // the bytes: a head up to the first 4-aligned destination byte and a tail of < 4 as
+        // bytes, the body as aligned destination dwords, 4 a lane a round (1 KiB a wave: one
+        // load round trip per KiB instead of one per 64 bytes — an incompressible block is
+        // nearly all literal), each from two aligned source loads and an alignbyte
+        // (a literal of <= 64 bytes: one byte a lane, one round trip)
         const uint32_t l = lane_id();
-        for (uint32_t i = 0; i < len; i += WAVE)
-            if (i + l < len) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)F.byte(from + i + l), R, (int)(op + i + l), 0, 0);
+        if (len <= WAVE) {
+            if (l < len) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)F.byte(from + l), R, (int)(op + l), 0, 0);
+            op += len;
+            return;
+        }
+        const uint32_t h = (4u - ((mis + op) & 3u)) & 3u;
+        const uint32_t nd = (len - h) >> 2, s = from + h, d = op + h, t = h + 4 * nd;
+        // head and tail bytes loaded with the first round's dwords (stores before a load would
+        // make its wait cover them too), stored after it
+        const uint32_t hb = l < h ? F.byte(from + l) : 0u, tb = l < len - t ? F.byte(from + t + l) : 0u;
+        for (uint32_t i = 0; i < nd; i += 4 * WAVE) {
+            uint32_t v[4];
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j) {
+                const uint32_t k = i + j * WAVE + l;
+                v[j] = k < nd ? F.ld32(s + 4 * k) : 0u;
+            }
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j) {
+                const uint32_t k = i + j * WAVE + l;
+                if (k < nd) __builtin_amdgcn_raw_buffer_store_b32(v[j], R, (int)(d + 4 * k), 0, 0);
+            }
+        }
+        if (l < h) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)hb, R, (int)(op + l), 0, 0);
+        if (l < len - t) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)tb, R, (int)(op + t + l), 0, 0);
         op += len;
     }
     __device__ __forceinline__ void copy64(uint32_t offset, uint32_t len, bool allow_short) {   // EmitCopyAtMost64
@@ -784,6 +814,7 @@ __global__ __launch_bounds__(WAVE) void snz_comp_kernel(const uint8_t *__restric
         Out O;
         O.R = mkr(slots + slot_offs[b], slot_offs[b + 1] - slot_offs[b]);
         O.op = 0;
+        O.mis = (uint32_t)((uintptr_t)(slots + slot_offs[b]) & 3u);
         {   // varint32 length
             uint32_t v = (uint32_t)len, nb = 1;
             uint64_t enc = 0;
@@ -800,12 +831,26 @@ __global__ __launch_bounds__(WAVE) void snz_comp_kernel(const uint8_t *__restric
             const uint32_t ts = table_size(fn);
             for (uint32_t k = lane; k < ts / 2; k += WAVE) ((lds_u32 *)table)[k] = 0;
             F.g = s0 + (uint32_t)f;
-            F.sh = F.g & 3;
-            F.lds = fn + 8 <= fcap;
-            if (F.lds) {   // aligned dwords covering the fragment (+ pad), source alignment kept
-                const uint32_t a0 = F.g & ~3u, nd = (F.sh + fn + 8 + 3) / 4;
-                for (uint32_t k = lane; k < nd; k += WAVE)
-                    ((lds_u32 *)ib)[k] = __builtin_amdgcn_raw_buffer_load_b32(F.R, (int)(a0 + 4 * k), 0, 0);
+            F.sh = (uint32_t)((c0 + f) & 15);
+            F.lds = F.sh + fn + 8 <= fcap;
+            if (F.lds) {   // aligned granules covering the fragment (+ pad), source alignment kept:
+                           // every granule's load in flight at once, then the LDS stores
+                constexpr uint32_t SG = SNZ_FRAG_LDS ? (SNZ_FRAG_LDS + 15) / 16 / WAVE + 1 : 1;
+                const uint64_t ab = (c0 + f) & ~15ull;
+                const rsrc_t RS = mkr(in + ab, in_cap - ab);
+                const uint32_t ng = (F.sh + fn + 8 + 15) / 16;
+                u32x4_t v[SG];
+#pragma unroll
+                for (uint32_t k = 0; k < SG; ++k) {
+                    const uint32_t q = lane + k * WAVE;
+                    v[k] = q < ng ? __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(RS, (int)(16 * q), 0, 0))
+                                  : u32x4_t{0u, 0u, 0u, 0u};
+                }
+#pragma unroll
+                for (uint32_t k = 0; k < SG; ++k) {
+                    const uint32_t q = lane + k * WAVE;
+                    if (q < ng) reinterpret_cast<__attribute__((address_space(3))) u32x4_t *>(ib)[q] = v[k];
+                }
             }
             compress_fragment(F, fn, table, ts, O);
         }
