@@ -718,9 +718,12 @@ __device__ void compress_fragment(const Frag &F, uint32_t fn, lds_u16 *table, ui
                     // (one 16-lane DPP row: lane j sees lane j - r by a row shift, no LDS round trip)
                     // (farthest first, so the nearest equal lane is the last to write prev: no
                     // "not found yet" test in the chain)
+                    // (H + 1 is never 0, so lanes shifted in from outside the row read 0 by
+                    // bound_ctrl and the row shift folds into the compare: v_cmp_eq_u32_dpp)
+                    const uint32_t H1 = H + 1;
 #define SNZ_ROW_SHR(r) { \
-        const uint32_t hk = (uint32_t)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)H, 0x110 + (r), 0xF, 0xF, false); \
-        prev = hk == H ? (int)lane - (r) : prev; }
+        const uint32_t hk = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)H1, 0x110 + (r), 0xF, 0xF, true); \
+        prev = hk == H1 ? (int)lane - (r) : prev; }
                     SNZ_ROW_SHR(15) SNZ_ROW_SHR(14) SNZ_ROW_SHR(13) SNZ_ROW_SHR(12) SNZ_ROW_SHR(11)
                     SNZ_ROW_SHR(10) SNZ_ROW_SHR(9) SNZ_ROW_SHR(8) SNZ_ROW_SHR(7) SNZ_ROW_SHR(6)
                     SNZ_ROW_SHR(5) SNZ_ROW_SHR(4) SNZ_ROW_SHR(3) SNZ_ROW_SHR(2) SNZ_ROW_SHR(1)
