@@ -52,17 +52,30 @@ static pthread_mutex_t g_svc_mu = PTHREAD_MUTEX_INITIALIZER;
 #define RR_COMPAT_MAX_SVC 64
 static int g_svc_fds[RR_COMPAT_MAX_SVC];  /* service ends of the live connections (parent) */
 static int g_nsvc;
+/* the service threads, joinable: a thread still inside the HIP runtime (its context's teardown
+ * after its child exited) when the process exits would race the runtime's own teardown, so the
+ * owner's exit ends and joins them (compat_exit); a finished thread is joined when its slot is
+ * next needed.  0 free, 1 running, 2 finished */
+static pthread_t g_th[RR_COMPAT_MAX_SVC];
+static int g_th_state[RR_COMPAT_MAX_SVC];
 static int g_child_fd = -1;               /* this process's own connection (child end) */
 static int g_fork_fd = -1;                /* the connection opened for the fork in progress */
 static int g_as_child;                    /* test hook: route this process as a child would */
 
 static int in_child(void) { return g_as_child || (g_owner && getpid() != g_owner); }
 
+static void compat_exit(void);
+static int g_exit_hooked;
+static void exit_hook(void) {
+    if (!__atomic_exchange_n(&g_exit_hooked, 1, __ATOMIC_SEQ_CST)) atexit(compat_exit);
+}
+
 static rr_ctx *engine(void) {
     if (in_child()) serverPanic("rock serdes: the GPU engine cannot be used in a fork child (HIP is the parent's)");
     if (!g_ctx) {
         if (rr_ctx_create(g_device, &g_ctx) != RR_API_OK) serverPanic("rock serdes engine: %s", rr_last_error());
         if (!g_owner) g_owner = getpid();
+        exit_hook();
     }
     return g_ctx;
 }
@@ -76,7 +89,7 @@ static int echo_blob(void *user, size_t k, const int *dbis, const char *const *k
 
 /* one connection's service: until its child closes the other end, or a request fails */
 static void *decode_service(void *arg) {
-    const int fd = (int)(intptr_t)arg;
+    const int slot = (int)((intptr_t)arg >> 32), fd = (int)(uint32_t)(intptr_t)arg;
     sigset_t pipe_set;   /* a reply to a child that is gone: EPIPE on this thread, not SIGPIPE */
     sigemptyset(&pipe_set);
     sigaddset(&pipe_set, SIGPIPE);
@@ -87,6 +100,7 @@ static void *decode_service(void *arg) {
     struct pollfd pf = {fd, POLLIN, 0};
     char peek;
     if (poll(&pf, 1, -1) > 0 && recv(fd, &peek, 1, MSG_PEEK) == 1 && rr_ctx_create(g_device, &ctx) == RR_API_OK) {
+        exit_hook();
         rr_rdb_serve(fd, fd, echo_blob, NULL, NULL, ctx, 64);
         rr_ctx_destroy(ctx);
     }
@@ -94,6 +108,7 @@ static void *decode_service(void *arg) {
     for (int i = 0; i < g_nsvc; i++)
         if (g_svc_fds[i] == fd) { g_svc_fds[i] = g_svc_fds[--g_nsvc]; break; }
     close(fd);   /* the child's read sees EOF */
+    g_th_state[slot] = 2;
     pthread_mutex_unlock(&g_svc_mu);
     return NULL;
 }
@@ -102,15 +117,21 @@ static void *decode_service(void *arg) {
 static int open_connection(void) {
     int sv[2];
     pthread_t th;
-    if (g_nsvc == RR_COMPAT_MAX_SVC || socketpair(AF_UNIX, SOCK_STREAM, 0, sv) != 0) return -1;
+    int slot = -1;
+    for (int i = 0; i < RR_COMPAT_MAX_SVC; i++) {
+        if (g_th_state[i] == 2) { pthread_join(g_th[i], NULL); g_th_state[i] = 0; }   /* (it has returned) */
+        if (g_th_state[i] == 0 && slot < 0) slot = i;
+    }
+    if (slot < 0 || g_nsvc == RR_COMPAT_MAX_SVC || socketpair(AF_UNIX, SOCK_STREAM, 0, sv) != 0) return -1;
     g_svc_fds[g_nsvc++] = sv[0];
-    if (pthread_create(&th, NULL, decode_service, (void *)(intptr_t)sv[0]) != 0) {
+    if (pthread_create(&th, NULL, decode_service, (void *)(((intptr_t)slot << 32) | (intptr_t)(uint32_t)sv[0])) != 0) {
         g_nsvc--;
         close(sv[0]);
         close(sv[1]);
         return -1;
     }
-    pthread_detach(th);
+    g_th[slot] = th;
+    g_th_state[slot] = 1;
     return sv[1];
 }
 
@@ -135,12 +156,27 @@ static void atfork_parent(void) {
 }
 static void atfork_child(void) {
     g_ctx = NULL;   /* (the parent's context is not ours) */
+    memset(g_th_state, 0, sizeof g_th_state);   /* (nor its threads) */
     for (int i = 0; i < g_nsvc; i++) close(g_svc_fds[i]);   /* the parent's service ends */
     g_nsvc = 0;
     if (g_child_fd >= 0) close(g_child_fd);   /* the parent's own connection */
     g_child_fd = g_fork_fd;
     g_fork_fd = -1;
     pthread_mutex_unlock(&g_svc_mu);
+}
+/* the owner's exit: every service's connection shut down (its thread sees EOF, destroys its
+ * context, returns), then every thread joined, before the HIP runtime's own teardown (exit_hook
+ * registers this once the runtime is up, so it runs before every handler the runtime registered) */
+static void compat_exit(void) {
+    if (g_owner && getpid() != g_owner) return;   /* (a fork child: no threads of its own) */
+    pthread_mutex_lock(&g_svc_mu);
+    for (int i = 0; i < g_nsvc; i++) shutdown(g_svc_fds[i], SHUT_RDWR);
+    pthread_t th[RR_COMPAT_MAX_SVC];
+    int n = 0;
+    for (int i = 0; i < RR_COMPAT_MAX_SVC; i++)
+        if (g_th_state[i]) { th[n++] = g_th[i]; g_th_state[i] = 0; }
+    pthread_mutex_unlock(&g_svc_mu);
+    for (int i = 0; i < n; i++) pthread_join(th[i], NULL);
 }
 __attribute__((constructor)) static void compat_atfork_register(void) {
     pthread_atfork(atfork_prepare, atfork_parent, atfork_child);
