@@ -60,6 +60,10 @@ def parse():
     p.add_argument("--plan-only", action="store_true", help="print the launch decision and rank layout, no GPU call")
     p.add_argument("--launch-check", action="store_true",
                    help="start the ranks as the bench would, join them over gloo on the CPU, report who joined")
+    p.add_argument("--split-timeout", type=float, default=120.0,
+                   help="watchdog on the RCCL split/gather leg: past it every rank exits non-zero")
+    p.add_argument("--stall-rank", type=int, default=None,
+                   help="--launch-check only: this rank never joins (tests the watchdog's non-zero exit)")
     return p.parse_args()
 
 
@@ -99,14 +103,47 @@ def spawn_ranks(gpus, argv):
     return subprocess.run(cmd, env=env).returncode
 
 
-def launch_check(world, rank):
-    """--launch-check inside a rank: join the job over gloo (no GPU) and report the ranks."""
+WATCHDOG_EXIT = 3   # a collective that hangs fails the job: never rc 0
+
+
+def arm_watchdog(seconds, rank, on_fire=None):
+    """A collective that has not returned after `seconds` fails the job: rank 0 runs `on_fire`
+    (prints what it has), then every rank leaves with WATCHDOG_EXIT.  os._exit, because the hung
+    thread holds the collective; the exit is non-zero so a launcher (and the driver's SCALE run)
+    sees the hang instead of a clean rc 0.  Returns the started timer; cancel() it on success."""
+    import threading
+
+    def _bail():
+        try:
+            if rank == 0 and on_fire is not None:
+                on_fire()
+            print(f"bench.py: rank {rank}: collective watchdog fired after {seconds:.0f} s, exiting "
+                  f"{WATCHDOG_EXIT}", file=sys.stderr, flush=True)
+        finally:
+            os._exit(WATCHDOG_EXIT)
+
+    dog = threading.Timer(seconds, _bail)
+    dog.daemon = True
+    dog.start()
+    return dog
+
+
+def launch_check(world, rank, stall_rank=None, timeout=120.0):
+    """--launch-check inside a rank: join the job over gloo (no GPU) and report the ranks.  With
+    `stall_rank` that rank never enters the all-gather, so the others hang in it: the same watchdog
+    as the bench's split/gather leg must end every rank with a non-zero code."""
     import torch
     import torch.distributed as dist
     dist.init_process_group("gloo")
     t = torch.tensor([rank], dtype=torch.int64)
     got = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+    dog = arm_watchdog(timeout, rank, lambda: print(json.dumps({"launch_check": True, "world": world,
+                                                                "error": f"timeout after {timeout:.0f} s"}),
+                                                    flush=True))
+    if rank == stall_rank:
+        time.sleep(10 * timeout + 60)   # the watchdog ends this rank too
     dist.all_gather(got, t)
+    dog.cancel()
     if rank == 0:
         print(json.dumps({"launch_check": True, "world": dist.get_world_size(), "n_gpus": world,
                           "ranks": [int(x.item()) for x in got]}), flush=True)
@@ -125,7 +162,7 @@ def main():
     if plan["launch"] == "spawn":   # before any GPU call: the ranks are fresh processes
         sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
     if args.launch_check:
-        launch_check(plan["world"], plan["rank"])
+        launch_check(plan["world"], plan["rank"], args.stall_rank, args.split_timeout)
         return
     import torch
     import torch.distributed as dist
@@ -377,19 +414,13 @@ def main():
     }
 
     if not args.no_split:
-        # a hang in a collective must not cost the headline line: after 120 s rank 0 prints
-        # what it has and every rank leaves
-        import threading
+        # a hang in a collective must not hide the headline line, nor pass as success: after
+        # --split-timeout rank 0 prints what it has and every rank exits WATCHDOG_EXIT
+        def _report():
+            result["split_gather"] = {"error": f"timeout after {args.split_timeout:.0f} s"}
+            print(json.dumps(result), flush=True)
 
-        def _bail():
-            if rank == 0:
-                result["split_gather"] = {"error": "timeout after 120 s"}
-                print(json.dumps(result), flush=True)
-            os._exit(0)
-
-        dog = threading.Timer(120.0, _bail)
-        dog.daemon = True
-        dog.start()
+        dog = arm_watchdog(args.split_timeout, rank, _report)
         try:
             result["split_gather"] = split_gather_leg(rr, torch, dist, eng, world, rank, dev, stream, d_data, d_offs,
                                                       d_vals, d_elems, n, nb, n_elems)

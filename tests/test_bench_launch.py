@@ -54,3 +54,14 @@ def test_launch_check_joins_all_ranks():
     assert len(lines) == 1, r.stdout   # rank 0 alone prints
     out = json.loads(lines[0])
     assert out["world"] == 4 and out["n_gpus"] == 4 and out["ranks"] == [0, 1, 2, 3]
+
+
+def test_hung_collective_exits_nonzero():
+    """the split/gather watchdog must fail the job.  Rank 1 never joins the
+    all-gather, so ranks 0 and 2 hang in it; the watchdog (3 s here, 120 s in the bench) ends every
+    rank with a non-zero code, and the launcher's exit code is non-zero too."""
+    r = _run(["--gpus", "3", "--launch-check", "--stall-rank", "1", "--split-timeout", "3"], timeout=180)
+    assert r.returncode != 0, (r.stdout, r.stderr[-2000:])
+    assert "watchdog fired" in r.stderr
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1 and "timeout" in json.loads(lines[0])["error"]
