@@ -94,6 +94,9 @@ SNAPPY_EXPORTS = ["rr_snappy_max_compressed_length", "rr_snappy_compress_bound",
 RDB_EXPORTS = ["rr_rdb_request_batch", "rr_rdb_blobs_free", "rr_rdb_request_flat", "rr_rdb_flat_free", "rr_rdb_serve"]
 # include/rr_kv.h (batched store I/O around the GPU path, row f2; used from C)
 KV_EXPORTS = ["rr_kv_dump_batch", "rr_kv_restore_batch"]
+# include/rr_host.h (the host codec: RedRock's per-key call sites through the compat shim, row f1)
+HOST_EXPORTS = ["rr_host_reserve", "rr_host_decode_value", "rr_host_decode_batch", "rr_host_encode_size",
+                "rr_host_encode_value", "rr_host_encode_batch"]
 SNAPPY_STATUS = {0: "OK", 1: "HEADER", 2: "TRUNC", 3: "OFFSET", 4: "OVERFLOW", 5: "LENGTH", 6: "CAPACITY"}
 
 _lib = None
@@ -160,6 +163,15 @@ def lib():
     L.rr_snappy_decompress_batch.argtypes = [vp, C.POINTER(BlobBatch), C.POINTER(BlobBatch), vp, vp]
     L.rr_snappy_compress_batch_host.argtypes = [vp, vp, vp, u64, vp, u64, vp]
     L.rr_snappy_decompress_batch_host.argtypes = [vp, vp, vp, u64, vp, u64, vp, vp]
+    if hasattr(L, "rr_host_decode_batch"):   # (RR_LIB: an older build for A/B timing may predate it)
+        L.rr_host_reserve.argtypes = [vp, u64]
+        L.rr_host_reserve.restype = u64
+        L.rr_host_decode_value.argtypes = [vp, u64, u64, vp, vp, u64, C.POINTER(C.c_uint64)]
+        L.rr_host_decode_batch.argtypes = [vp, vp, u64, vp, vp, u64, vp, C.POINTER(Totals)]
+        L.rr_host_encode_size.argtypes = [vp, vp, u64, u64, C.POINTER(C.c_uint64)]
+        L.rr_host_encode_value.argtypes = [vp, vp, vp, vp]
+        L.rr_host_encode_value.restype = None
+        L.rr_host_encode_batch.argtypes = [vp, vp, u64, vp, u64, u64, vp, u64, vp, C.POINTER(Totals)]
     _lib = L
     return L
 
@@ -271,6 +283,53 @@ def gather_schedule(plan, shard_elems, rank: int, root: int = 0):
     ne = np.ascontiguousarray(shard_elems, np.uint64)
     out = (Xfer * (2 * g))()
     return _xfers(out, lib().rr_gather_schedule(arr, _ptr(ne), g, rank, root, out))
+
+
+# ---- the host codec (include/rr_host.h) ------------------------------------------------------
+# The CPU routing target of the compat shim for RedRock's per-key calls: explicit functions, never
+# reached from Engine (the GPU entry points have no CPU fallback).
+def host_decode(data: np.ndarray, offsets: np.ndarray, elem_cap: int | None = None):
+    """rr_host_decode_batch: (values, elems, arena, totals) with rr_decode_batch_host's contract."""
+    n = len(offsets) - 1
+    nbytes = int(offsets[-1])
+    if elem_cap is None:
+        elem_cap = elem_bound(n, nbytes)
+    data = np.ascontiguousarray(data, np.uint8)
+    offsets = np.ascontiguousarray(offsets, np.uint64)
+    values = np.zeros(n, VALUE_DT)
+    elems = np.zeros(max(elem_cap, 1), ELEM_DT)
+    arena = np.zeros(max(nbytes, 1), np.uint8)
+    t = Totals()
+    _check(lib().rr_host_decode_batch(_ptr(data), _ptr(offsets), n, _ptr(values), _ptr(elems), elem_cap,
+                                      _ptr(arena), C.byref(t)))
+    ne = min(int(t.n_elems), elem_cap)
+    return values, elems[:ne], arena[:nbytes], t.as_dict()
+
+
+def host_decode_value(blob: bytes, base: int = 0, cap: int = 64):
+    """rr_host_decode_value: (status, record, descriptors, need) of one blob."""
+    b = np.frombuffer(bytes(blob) or b"\0", np.uint8)
+    v = np.zeros(1, VALUE_DT)
+    e = np.zeros(max(cap, 1), ELEM_DT)
+    need = C.c_uint64()
+    st = lib().rr_host_decode_value(_ptr(b), len(blob), base, _ptr(v), _ptr(e), cap, C.byref(need))
+    return int(st), v[0], e[:min(int(v[0]["n_elems"]), cap)], int(need.value)
+
+
+def host_encode(values: np.ndarray, elems: np.ndarray, arena: np.ndarray, data_cap: int | None = None):
+    """rr_host_encode_batch: (data, offsets, totals) with rr_encode_batch_host's contract."""
+    n = len(values)
+    values = np.ascontiguousarray(values, VALUE_DT)
+    elems = np.ascontiguousarray(elems, ELEM_DT)
+    arena = np.ascontiguousarray(arena, np.uint8)
+    if data_cap is None:
+        data_cap = encode_bound(values, elems)
+    data = np.zeros(max(data_cap, 1), np.uint8)
+    offsets = np.zeros(n + 1, np.uint64)
+    t = Totals()
+    _check(lib().rr_host_encode_batch(_ptr(values), _ptr(elems), len(elems), _ptr(arena), arena.size, n, _ptr(data),
+                                      data_cap, _ptr(offsets), C.byref(t)))
+    return data[:int(offsets[-1])], offsets, t.as_dict()
 
 
 def elem_bound(n: int, nbytes: int) -> int:

@@ -1,0 +1,733 @@
+/*
+ * rr_host.c — the engine's host codec (include/rr_host.h): one RedRock value blob at a time on
+ * the calling CPU thread, with the GPU path's exact records, descriptors, statuses and bytes.
+ *
+ * It is what the compat shim runs for RedRock's per-key call sites (desObject at rock.c:468 and
+ * :538, serObject at rock.c:691); the shim sends batches above its measured crossover to the
+ * GPU.  The decode is a single forward pass per value that writes descriptors in place: hash
+ * table members and skiplist pairs are parsed straight into their slots and then checked there
+ * (duplicates by 64-bit key fingerprints, skiplist order by one adjacent-pair scan and a stable
+ * merge sort only when it fails), so a value costs one walk of its bytes and no allocation
+ * below 64 keys.  Reference lines per type are cited at each case (src/rock_serdes.c, ziplist.c,
+ * util.c, t_zset.c).
+ */
+#include <stdlib.h>
+#include <string.h>
+
+#include "../../include/rr_host.h"
+
+static inline uint32_t rd32(const uint8_t *p) { uint32_t x; memcpy(&x, p, 4); return x; }
+static inline uint64_t rd64(const uint8_t *p) { uint64_t x; memcpy(&x, p, 8); return x; }
+static inline void wr32(uint8_t *p, uint32_t x) { memcpy(p, &x, 4); }
+static inline void wr64(uint8_t *p, uint64_t x) { memcpy(p, &x, 8); }
+
+/* ---------------------------------------------------------------- integers and decimals */
+
+/* zipTryEncoding (ziplist.c:480-503) over string2ll (util.c:360-424): 1..31 bytes, an optional
+ * '-', no leading zero (but "0" itself), digits only, in int64 range.  A valid int64 has at most
+ * 19 digits, so the digit loop cannot overflow a u64 and longer strings are rejected up front. */
+static int zip_try_int(const uint8_t *s, uint64_t len, int64_t *out) {
+    if (len == 0 || len > 20) return 0;
+    const uint8_t *p = s, *e = s + len;
+    int neg = 0;
+    if (*p == '-') {
+        neg = 1;
+        if (++p == e) return 0;
+    }
+    if (*p < '1' || *p > '9') {
+        if (len == 1 && *s == '0') { *out = 0; return 1; }
+        return 0;
+    }
+    if (e - p > 19) return 0;
+    uint64_t v = 0;
+    for (; p < e; p++) {
+        const unsigned d = (unsigned)*p - '0';
+        if (d > 9) return 0;
+        v = v * 10 + d;
+    }
+    if (neg) {
+        if (v > (1ull << 63)) return 0;
+        *out = (int64_t)(0 - v);
+    } else {
+        if (v > (uint64_t)INT64_MAX) return 0;
+        *out = (int64_t)v;
+    }
+    return 1;
+}
+
+/* sdsll2str (sds.c:450-479) / ll2string: the decimal of a signed 64-bit value (LLONG_MIN's
+ * magnitude taken unsigned).  Two digits per step from a pair table, written from the end. */
+static const char k_pairs[201] =
+    "00010203040506070809101112131415161718192021222324252627282930313233343536373839"
+    "40414243444546474849505152535455565758596061626364656667686970717273747576777879"
+    "8081828384858687888990919293949596979899";
+
+static unsigned digits_u64(uint64_t v) {
+    unsigned n = 1;
+    while (v >= 10000) { v /= 10000; n += 4; }
+    if (v >= 10) n++;
+    if (v >= 100) n++;
+    if (v >= 1000) n++;
+    return n;
+}
+
+static unsigned dec_len(int64_t x) {
+    const uint64_t m = x < 0 ? 0 - (uint64_t)x : (uint64_t)x;
+    return digits_u64(m) + (x < 0);
+}
+
+static unsigned dec_write(uint8_t *out, int64_t x) {
+    uint64_t m = x < 0 ? 0 - (uint64_t)x : (uint64_t)x;
+    const unsigned n = dec_len(x);
+    uint8_t *p = out + n;
+    while (m >= 100) {
+        const unsigned r = (unsigned)(m % 100);
+        m /= 100;
+        p -= 2;
+        memcpy(p, k_pairs + 2 * r, 2);
+    }
+    if (m >= 10) { p -= 2; memcpy(p, k_pairs + 2 * m, 2); }
+    else *--p = (uint8_t)('0' + m);
+    if (x < 0) *--p = '-';
+    return n;
+}
+
+/* ---------------------------------------------------------------- reservations */
+
+/* the ziplist entry count behind a saturated zllen (0xFFFF): a walk that stops where the
+ * batch path's header-only count stops (rr_format.h "descriptor slots") */
+static uint64_t zl_walk_count(const uint8_t *zl, uint64_t L) {
+    uint64_t p = 10, n = 0;
+    while (p < L - 1 && zl[p] != 0xFF) {
+        const uint64_t q = p + (zl[p] < 254 ? 1 : 5);
+        if (q >= L - 1) break;
+        const uint8_t enc = zl[q];
+        uint64_t e;
+        if (enc < 0xC0) {
+            if ((enc & 0xC0) == 0x00) e = q + 1 + (enc & 0x3F);
+            else if ((enc & 0xC0) == 0x40) {
+                if (q + 2 > L - 1) break;
+                e = q + 2 + (((uint64_t)(enc & 0x3F) << 8) | zl[q + 1]);
+            } else {
+                if (q + 5 > L - 1) break;
+                e = q + 5 + (((uint64_t)zl[q + 1] << 24) | ((uint64_t)zl[q + 2] << 16) | ((uint64_t)zl[q + 3] << 8) | zl[q + 4]);
+            }
+        } else if (enc >= 0xF1 && enc <= 0xFD) e = q + 1;
+        else if (enc == 0xFE) e = q + 2;
+        else if (enc == 0xC0) e = q + 3;
+        else if (enc == 0xF0) e = q + 4;
+        else if (enc == 0xD0) e = q + 5;
+        else if (enc == 0xE0) e = q + 9;
+        else break;
+        if (e > L - 1) break;
+        n++;
+        p = e;
+    }
+    return n;
+}
+
+uint64_t rr_host_reserve(const uint8_t *b, uint64_t len) {
+    if (len < 5) return 0;
+    if (b[0] == RR_TYPE_STRING) return len >= 6;
+    if (b[0] == RR_TYPE_LIST_QUICKLIST) {   /* the length chain up to its first break */
+        uint64_t p = 5, n = 0;
+        while (len - p >= 4) {
+            const uint64_t l = rd32(b + p);
+            if (l > len - p - 4) break;
+            n++;
+            p += 4 + l;
+        }
+        return n;
+    }
+    if (len < 13) return 0;
+    const uint64_t body = len - 13;
+    switch (b[0]) {
+    case RR_TYPE_SET_INTSET: {
+        const uint64_t w = rd32(b + 5), c = rd32(b + 9);
+        return ((w == 2 || w == 4 || w == 8) && body == w * c) ? c : 0;
+    }
+    case RR_TYPE_SET_HT: { const uint64_t c = rd64(b + 5), m = body / 8; return c < m ? c : m; }
+    case RR_TYPE_HASH_HT: { const uint64_t c = rd64(b + 5), m = body / 8; return c > m / 2 ? m : 2 * c; }
+    case RR_TYPE_ZSET_SKIPLIST: { const uint64_t c = rd64(b + 5), m = body / 16; return 2 * (c < m ? c : m); }
+    case RR_TYPE_HASH_ZIPLIST:
+    case RR_TYPE_ZSET_ZIPLIST: {
+        const uint64_t L = rd64(b + 5);
+        if (L != body || L < 11) return 0;
+        const uint64_t zllen = (uint64_t)b[21] | ((uint64_t)b[22] << 8);
+        if (zllen == 0xFFFF) return 1 + zl_walk_count(b + 13, L);
+        const uint64_t m = (L - 11) / 2;
+        return 1 + (zllen < m ? zllen : m);
+    }
+    default: return 0;
+    }
+}
+
+/* ---------------------------------------------------------------- decode */
+
+typedef struct {
+    const uint8_t *b;     /* the blob */
+    uint64_t base;        /* descriptor offset of blob byte 0 */
+    rr_elem *el;
+    uint64_t cap, n;      /* slots at el, descriptors produced (written while n < cap) */
+} emit_t;
+
+static inline void put(emit_t *E, uint8_t kind, uint64_t data, uint32_t len, uint8_t zenc) {
+    if (E->n < E->cap) {
+        rr_elem *e = &E->el[E->n];
+        e->data = data;
+        e->len = len;
+        e->kind = kind;
+        e->zenc = zenc;
+        e->rsv = 0;
+    }
+    E->n++;
+}
+
+/* bytes of the STR descriptor e */
+static inline const uint8_t *str_at(const emit_t *E, const rr_elem *e) { return E->b + (e->data - E->base); }
+
+/* A ziplist's entries (ziplist.c:300-447: ZIP_DECODE_PREVLEN, ZIP_DECODE_LENGTH, zipIntSize,
+ * zipLoadInteger; header :193-256), each checked as one forward walk would: its prevlen is the
+ * size of the entry before it, its fields end inside the ziplist, the last one ends at the 0xFF
+ * byte; then zltail and zllen (unless saturated) agree.  zl sits at blob offset `at`. */
+static int zl_entries(emit_t *E, uint64_t at, uint64_t L) {
+    const uint8_t *zl = E->b + at;
+    if (L < 11 || rd32(zl) != L) return RR_E_ZL_CORRUPT;
+    const uint64_t end_byte = L - 1;
+    uint64_t p = 10, prev_size = 0, last = 10, cnt = 0;
+    while (p < end_byte && zl[p] != 0xFF) {
+        uint64_t q;
+        if (zl[p] < 254) {
+            if (zl[p] != prev_size) return RR_E_ZL_CORRUPT;
+            q = p + 1;
+        } else {
+            if (p + 5 > end_byte || rd32(zl + p + 1) != prev_size) return RR_E_ZL_CORRUPT;
+            q = p + 5;
+        }
+        if (q >= end_byte) return RR_E_ZL_CORRUPT;
+        const uint8_t enc = zl[q];
+        uint64_t e;
+        if (enc < 0xC0) {   /* string: 00pppppp | 01pppppp qqqqqqqq (BE) | 10xxxxxx + u32 BE */
+            uint64_t hdr, sl;
+            const uint8_t cls = enc & 0xC0;
+            if (cls == 0x00) { hdr = 1; sl = enc & 0x3F; }
+            else if (cls == 0x40) {
+                if (q + 2 > end_byte) return RR_E_ZL_CORRUPT;
+                hdr = 2; sl = ((uint64_t)(enc & 0x3F) << 8) | zl[q + 1];
+            } else {
+                if (q + 5 > end_byte) return RR_E_ZL_CORRUPT;
+                hdr = 5;
+                sl = ((uint64_t)zl[q + 1] << 24) | ((uint64_t)zl[q + 2] << 16) | ((uint64_t)zl[q + 3] << 8) | zl[q + 4];
+            }
+            e = q + hdr + sl;
+            if (e > end_byte) return RR_E_ZL_CORRUPT;
+            put(E, RR_K_STR, E->base + at + q + hdr, (uint32_t)sl, cls);
+        } else {
+            int64_t x;
+            const uint8_t *d = zl + q + 1;
+            if (enc >= 0xF1 && enc <= 0xFD) { e = q + 1; x = (int64_t)(enc & 0x0F) - 1; }   /* immediate 0..12 */
+            else if (enc == 0xFE) { e = q + 2; if (e > end_byte) return RR_E_ZL_CORRUPT; x = (int8_t)d[0]; }
+            else if (enc == 0xC0) { e = q + 3; if (e > end_byte) return RR_E_ZL_CORRUPT; int16_t y; memcpy(&y, d, 2); x = y; }
+            else if (enc == 0xF0) {   /* 24-bit: the three bytes as the top of an i32, shifted down (:552-556) */
+                e = q + 4;
+                if (e > end_byte) return RR_E_ZL_CORRUPT;
+                x = (int32_t)(((uint32_t)d[0] << 8) | ((uint32_t)d[1] << 16) | ((uint32_t)d[2] << 24)) >> 8;
+            } else if (enc == 0xD0) { e = q + 5; if (e > end_byte) return RR_E_ZL_CORRUPT; x = (int32_t)rd32(d); }
+            else if (enc == 0xE0) { e = q + 9; if (e > end_byte) return RR_E_ZL_CORRUPT; x = (int64_t)rd64(d); }
+            else return RR_E_ZL_CORRUPT;
+            put(E, RR_K_INT, (uint64_t)x, 0, enc);
+        }
+        cnt++;
+        prev_size = e - p;
+        last = p;
+        p = e;
+    }
+    if (p != end_byte || zl[p] != 0xFF) return RR_E_ZL_CORRUPT;   /* (0xFF early, or no 0xFF at the end) */
+    const uint64_t zllen = (uint64_t)zl[8] | ((uint64_t)zl[9] << 8);
+    if ((zllen != 0xFFFF && zllen != cnt) || rd32(zl + 4) != last || (cnt & 1)) return RR_E_ZL_CORRUPT;
+    return RR_OK;
+}
+
+/* A fingerprint of a key's bytes, for the duplicate tests (equal keys, equal fingerprints). */
+static uint64_t key_fp(const uint8_t *p, uint64_t n) {
+    uint64_t h = 0x9E3779B97F4A7C15ull ^ (n * 0xD6E8FEB86659FD93ull);
+    while (n >= 8) {
+        h = (h ^ rd64(p)) * 0xFF51AFD7ED558CCDull;
+        h ^= h >> 32;
+        p += 8;
+        n -= 8;
+    }
+    uint64_t w = 0;
+    memcpy(&w, p, n);
+    h = (h ^ w) * 0xC4CEB9FE1A85EC53ull;
+    return h ^ (h >> 29);
+}
+
+/* Marks key k (the STR descriptor at el[k * stride]) in dup[] when an earlier key has the same
+ * bytes: dictAdd's DICT_ERR (dict.c:265) on the later copy, so the first one stays.  Returns
+ * the number marked.  Fingerprints compared pairwise for a few keys, through an open-addressing
+ * table of key indices for more. */
+static uint64_t mark_dups(const emit_t *E, uint64_t k, uint64_t stride, uint8_t *dup) {
+    if (k < 2) return 0;
+    uint64_t fp_local[64], *fp = k <= 64 ? fp_local : (uint64_t *)malloc(sizeof(uint64_t) * k);
+    uint64_t d = 0;
+    for (uint64_t i = 0; i < k; i++) {
+        const rr_elem *e = &E->el[i * stride];
+        fp[i] = key_fp(str_at(E, e), e->len);
+    }
+#define SAME(i, j) (E->el[(i) * stride].len == E->el[(j) * stride].len && \
+                    !memcmp(str_at(E, &E->el[(i) * stride]), str_at(E, &E->el[(j) * stride]), E->el[(i) * stride].len))
+    if (k <= 32) {
+        for (uint64_t i = 1; i < k; i++)
+            for (uint64_t j = 0; j < i; j++)
+                if (fp[j] == fp[i] && !dup[j] && SAME(i, j)) { dup[i] = 1; d++; break; }
+    } else {
+        uint64_t sz = 64;
+        while (sz < 2 * k) sz <<= 1;
+        uint32_t *slot = (uint32_t *)malloc(sizeof(uint32_t) * sz);   /* key index + 1, 0 empty */
+        memset(slot, 0, sizeof(uint32_t) * sz);
+        for (uint64_t i = 0; i < k; i++) {
+            uint64_t h = fp[i] & (sz - 1);
+            for (;; h = (h + 1) & (sz - 1)) {
+                const uint32_t s = slot[h];
+                if (!s) { slot[h] = (uint32_t)(i + 1); break; }
+                if (fp[s - 1] == fp[i] && SAME(i, s - 1)) { dup[i] = 1; d++; break; }
+            }
+        }
+        free(slot);
+    }
+#undef SAME
+    if (fp != fp_local) free(fp);
+    return d;
+}
+
+/* zslInsert's order read back by serZset (t_zset.c:132-180, rock_serdes.c:430-440): pair a
+ * comes before pair b when its score is higher, or equal (as doubles: -0.0 == 0.0) with a
+ * member greater by sdscmp (sds.c:814-824).  Returns nonzero when a must precede b strictly. */
+static int sl_before(const emit_t *E, const rr_elem *a, const rr_elem *b) {
+    double sa, sb;
+    memcpy(&sa, &a[1].data, 8);
+    memcpy(&sb, &b[1].data, 8);
+    if (sa != sb) return sa > sb;
+    const uint32_t la = a[0].len, lb = b[0].len, m = la < lb ? la : lb;
+    const int c = m ? memcmp(str_at(E, &a[0]), str_at(E, &b[0]), m) : 0;
+    return c ? c > 0 : la > lb;
+}
+
+/* stable merge sort of np (member, score) pairs by sl_before (equal keys keep blob order) */
+static void sl_sort(const emit_t *E, rr_elem *pairs, uint64_t np) {
+    if (np < 2) return;
+    if (np <= 16) {   /* insertion sort */
+        for (uint64_t i = 1; i < np; i++) {
+            rr_elem t[2] = {pairs[2 * i], pairs[2 * i + 1]};
+            uint64_t j = i;
+            while (j > 0 && sl_before(E, t, &pairs[2 * (j - 1)])) {
+                pairs[2 * j] = pairs[2 * (j - 1)];
+                pairs[2 * j + 1] = pairs[2 * (j - 1) + 1];
+                j--;
+            }
+            pairs[2 * j] = t[0];
+            pairs[2 * j + 1] = t[1];
+        }
+        return;
+    }
+    rr_elem *tmp = (rr_elem *)malloc(sizeof(rr_elem) * 2 * np);
+    rr_elem *src = pairs, *dst = tmp;
+    for (uint64_t w = 1; w < np; w *= 2) {
+        for (uint64_t lo = 0; lo < np; lo += 2 * w) {
+            const uint64_t mid = lo + w < np ? lo + w : np, hi = lo + 2 * w < np ? lo + 2 * w : np;
+            uint64_t i = lo, j = mid, o = lo;
+            while (i < mid && j < hi) {
+                const uint64_t s = sl_before(E, &src[2 * j], &src[2 * i]) ? j++ : i++;
+                dst[2 * o] = src[2 * s];
+                dst[2 * o + 1] = src[2 * s + 1];
+                o++;
+            }
+            memcpy(dst + 2 * o, src + 2 * i, sizeof(rr_elem) * 2 * (mid - i));
+            o += mid - i;
+            memcpy(dst + 2 * o, src + 2 * j, sizeof(rr_elem) * 2 * (hi - j));
+        }
+        rr_elem *t = src; src = dst; dst = t;
+    }
+    if (src != pairs) memcpy(pairs, src, sizeof(rr_elem) * 2 * np);
+    free(tmp);
+}
+
+static int is_nan_bits(uint64_t s) { return (s & 0x7FF0000000000000ull) == 0x7FF0000000000000ull && (s << 12); }
+
+/* desObject (rock_serdes.c:538-564): the value record and its descriptors.  *slots = the slots
+ * the value owns when valid (SET_HT: one per blob member, duplicates included), *payload = the
+ * payload bytes its descriptors reference.  Structural defects (SHORT / TRUNC / COUNT / ...) are
+ * reported before DUP / NAN, and a value that needs more than E->cap slots returns
+ * RR_E_CAPACITY only once its structure is known good. */
+static int decode_one(emit_t *E, uint64_t len, rr_value *v, uint64_t *slots, uint64_t *payload) {
+    const uint8_t *b = E->b;
+    int st = RR_OK;
+    uint64_t pay = 0, nslots = 0;
+    v->type = len ? b[0] : 0;
+    v->enc = 0;
+    v->lru = len >= 5 ? rd32(b + 1) & RR_LRU_MASK : 0;
+    E->n = 0;
+    if (len < 5) { st = RR_E_SHORT; goto done; }                                  /* :539-542 */
+    uint64_t p = 5, rem = len - 5;
+    switch (b[0]) {
+    case RR_TYPE_STRING: {                                                        /* :133-158 */
+        if (len < 6) { st = RR_E_SHORT; break; }
+        const uint8_t enc = b[5];
+        const uint64_t n = len - 6;
+        v->enc = enc;
+        if (enc == RR_ENC_INT) {
+            if (n != 8) st = RR_E_STR_INTLEN;
+            else put(E, RR_K_INT, rd64(b + 6), 0, 0);
+        } else if (enc == RR_ENC_RAW || enc == RR_ENC_EMBSTR) {
+            if (enc == RR_ENC_EMBSTR && n > RR_EMBSTR_SIZE_LIMIT) st = RR_E_EMBSTR_LEN;
+            else if (n > 0xFFFFFFFFull) st = RR_E_CAPACITY;
+            else { put(E, RR_K_STR, E->base + 6, (uint32_t)n, 0); pay = n; }
+        } else st = RR_E_STR_ENC;
+        break;
+    }
+    case RR_TYPE_LIST_QUICKLIST:                                                  /* :191-214 */
+        while (rem) {   /* {u32 len, bytes} to the end; each pushed through zipTryEncoding */
+            if (rem < 4) { st = RR_E_TRUNC; break; }
+            const uint64_t l = rd32(b + p);
+            p += 4;
+            rem -= 4;
+            if (l > rem) { st = RR_E_TRUNC; break; }
+            int64_t x;
+            if (zip_try_int(b + p, l, &x)) put(E, RR_K_INT, (uint64_t)x, 0, 0);
+            else { put(E, RR_K_STR, E->base + p, (uint32_t)l, 0); pay += l; }
+            p += l;
+            rem -= l;
+        }
+        break;
+    case RR_TYPE_SET_INTSET: {                                                    /* :255-276 */
+        if (rem < 8) { st = RR_E_SHORT; break; }
+        const uint64_t w = rd32(b + 5), cnt = rd32(b + 9);
+        if ((w != 2 && w != 4 && w != 8) || rem - 8 != w * cnt) { st = RR_E_INTSET; break; }
+        v->enc = (uint8_t)w;
+        const uint8_t *q = b + 13;
+        if (w == 2) for (uint64_t i = 0; i < cnt; i++) { int16_t y; memcpy(&y, q + 2 * i, 2); put(E, RR_K_INT, (uint64_t)(int64_t)y, 0, 0); }
+        else if (w == 4) for (uint64_t i = 0; i < cnt; i++) put(E, RR_K_INT, (uint64_t)(int64_t)(int32_t)rd32(q + 4 * i), 0, 0);
+        else for (uint64_t i = 0; i < cnt; i++) put(E, RR_K_INT, rd64(q + 8 * i), 0, 0);
+        break;
+    }
+    case RR_TYPE_SET_HT:                                                          /* :277-303 */
+    case RR_TYPE_HASH_HT: {                                                       /* :368-404 */
+        if (rem < 8) { st = RR_E_SHORT; break; }
+        const uint64_t cnt = rd64(b + p);
+        const int per = b[0] == RR_TYPE_SET_HT ? 1 : 2;
+        uint64_t got = 0;
+        p += 8;
+        rem -= 8;
+        while (rem && st == RR_OK) {   /* members (a set) or field, value (a hash) into their slots */
+            for (int k = 0; k < per; k++) {
+                if (rem < 8) { st = RR_E_TRUNC; break; }
+                const uint64_t l = rd64(b + p);
+                p += 8;
+                rem -= 8;
+                if (l > rem) { st = RR_E_TRUNC; break; }
+                put(E, RR_K_STR, E->base + p, (uint32_t)l, 0);
+                p += l;
+                rem -= l;
+            }
+            got++;
+        }
+        if (st == RR_OK && got != cnt) st = RR_E_COUNT;                          /* :303, :404 */
+        if (st != RR_OK) break;
+        nslots = E->n;
+        if (E->n > E->cap) { st = RR_E_CAPACITY; break; }
+        const uint64_t nk = per == 1 ? E->n : E->n / 2;
+        uint8_t dup_local[64], *dup = nk <= 64 ? dup_local : (uint8_t *)malloc(nk);
+        memset(dup, 0, nk);
+        const uint64_t d = mark_dups(E, nk, (uint64_t)per, dup);
+        if (d && per == 2) st = RR_E_DUP;                                         /* :399-400 */
+        else {
+            if (d) {   /* a set keeps the first copy of a member (:297): compact in place */
+                uint64_t o = 0;
+                for (uint64_t i = 0; i < nk; i++)
+                    if (!dup[i]) E->el[o++] = E->el[i];
+                E->n = o;
+            }
+            for (uint64_t i = 0; i < E->n; i++) pay += E->el[i].len;
+        }
+        if (dup != dup_local) free(dup);
+        break;
+    }
+    case RR_TYPE_HASH_ZIPLIST:                                                    /* :356-366 */
+    case RR_TYPE_ZSET_ZIPLIST: {                                                  /* :455-466 */
+        if (rem < 8) { st = RR_E_SHORT; break; }
+        const uint64_t L = rd64(b + p);
+        if (rem - 8 != L) { st = RR_E_ZL_LEN; break; }
+        put(E, RR_K_ZLRAW, E->base + 13, (uint32_t)L, 0);   /* the raw ziplist, then its entries */
+        st = zl_entries(E, 13, L);
+        if (st == RR_OK) pay = L;
+        break;
+    }
+    case RR_TYPE_ZSET_SKIPLIST: {                                                 /* :467-501 */
+        if (rem < 8) { st = RR_E_SHORT; break; }
+        const uint64_t cnt = rd64(b + p);
+        p += 8;
+        rem -= 8;
+        for (uint64_t i = 0; i < cnt; i++) {   /* {u64 l, member, f64 score} pairs into their slots */
+            if (rem < 8) { st = RR_E_TRUNC; break; }
+            const uint64_t l = rd64(b + p);
+            p += 8;
+            rem -= 8;
+            if (l > rem || rem - l < 8) { st = RR_E_TRUNC; break; }
+            put(E, RR_K_STR, E->base + p, (uint32_t)l, 0);
+            put(E, RR_K_SCORE, rd64(b + p + l), 0, 0);
+            p += l + 8;
+            rem -= l + 8;
+        }
+        if (st == RR_OK && rem) st = RR_E_COUNT;                                  /* :501 */
+        if (st != RR_OK) break;
+        nslots = E->n;
+        if (E->n > E->cap) { st = RR_E_CAPACITY; break; }
+        const uint64_t np = E->n / 2;
+        for (uint64_t i = 0; i < np; i++)
+            if (is_nan_bits(E->el[2 * i + 1].data)) { st = RR_E_NAN; break; }    /* t_zset.c:137 */
+        if (st != RR_OK) break;
+        for (uint64_t i = 1; i < np; i++)   /* serZset's order already (every blob it wrote)? */
+            if (sl_before(E, &E->el[2 * i], &E->el[2 * (i - 1)])) { sl_sort(E, E->el, np); break; }
+        for (uint64_t i = 0; i < np; i++) pay += E->el[2 * i].len;
+        break;
+    }
+    default:
+        st = RR_E_TYPE;                                                           /* :560-562 */
+    }
+    if (st == RR_OK && b[0] != RR_TYPE_SET_HT && b[0] != RR_TYPE_HASH_HT && b[0] != RR_TYPE_ZSET_SKIPLIST) {
+        nslots = E->n;
+        if (E->n > E->cap) st = RR_E_CAPACITY;
+    }
+done:
+    if (st != RR_OK && st != RR_E_CAPACITY) { nslots = 0; pay = 0; }
+    v->status = (uint16_t)st;
+    v->n_elems = st == RR_OK ? (uint32_t)E->n : 0;
+    *slots = nslots;
+    *payload = st == RR_OK ? pay : 0;
+    return st;
+}
+
+int rr_host_decode_value(const uint8_t *blob, uint64_t len, uint64_t base, rr_value *v, rr_elem *el, uint64_t cap,
+                         uint64_t *need) {
+    emit_t E = {blob, base, el, cap, 0};
+    uint64_t slots, pay;
+    const int st = decode_one(&E, len, v, &slots, &pay);
+    if (need) *need = st == RR_OK || st == RR_E_CAPACITY ? slots : 0;
+    return st;
+}
+
+int rr_host_decode_batch(const uint8_t *data, const uint64_t *offsets, uint64_t n, rr_value *values, rr_elem *elems,
+                         uint64_t elem_cap, uint8_t *arena, rr_totals *totals) {
+    if ((n && (!offsets || !values || (!data && offsets[n]))) || (elem_cap && !elems)) return RR_API_EINVAL;
+    uint64_t base = 0, bad = 0, payload = 0;
+    rr_elem *scratch = NULL;
+    uint64_t scratch_cap = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        const uint64_t o = offsets[i], len = offsets[i + 1] - o;
+        const uint8_t *b = data + o;
+        rr_value *v = &values[i];
+        const uint64_t r = rr_host_reserve(b, len);
+        const int fits = base + r <= elem_cap;
+        emit_t E = {b, o, fits ? elems + base : scratch, r, 0};
+        if (!fits && r > scratch_cap) {   /* a capacity cut still needs the value's own verdict */
+            free(scratch);
+            scratch_cap = r;
+            scratch = (rr_elem *)malloc(sizeof(rr_elem) * (r ? r : 1));
+            E.el = scratch;
+        }
+        uint64_t slots, pay;
+        int st = decode_one(&E, len, v, &slots, &pay);
+        if (st == RR_OK && slots != r) st = RR_E_COUNT;
+        if (st != RR_OK) {
+            v->n_elems = 0;
+            if (fits && r) memset(elems + base, 0, sizeof(rr_elem) * r);   /* malformed: slots zero-filled */
+        } else if (!fits) {
+            st = RR_E_CAPACITY;   /* keeps its descriptor count, writes nothing */
+        } else {
+            if (E.n < r) memset(elems + base + E.n, 0, sizeof(rr_elem) * (r - E.n));   /* a set's dropped copies */
+            payload += pay;
+        }
+        v->status = (uint16_t)st;
+        v->elem_base = (uint32_t)base;
+        bad += st != RR_OK;
+        base += r;
+    }
+    free(scratch);
+    if (arena && n && offsets[n]) memcpy(arena, data, offsets[n]);   /* the arena mirrors the blobs */
+    if (totals) {
+        totals->n_elems = base;
+        totals->bytes = n ? offsets[n] : 0;
+        totals->n_bad = bad;
+        totals->payload = payload;
+    }
+    return RR_API_OK;
+}
+
+/* ---------------------------------------------------------------- encode */
+
+#define ARENA_OK(E, acap) ((E).data <= (acap) && (uint64_t)(E).len <= (acap) - (E).data)
+
+static int fits_width(int64_t x, unsigned w) {
+    return w == 8 || (w == 4 ? x >= INT32_MIN && x <= INT32_MAX : x >= INT16_MIN && x <= INT16_MAX);
+}
+
+int rr_host_encode_size(const rr_value *v, const rr_elem *elems, uint64_t elem_cap, uint64_t arena_cap,
+                        uint64_t *size) {
+    const uint64_t n = v->n_elems;
+    uint64_t s = 5;
+    *size = 0;
+    if (v->status != RR_OK || (uint64_t)v->elem_base + n > elem_cap) return RR_E_ENCODE;
+    const rr_elem *el = elems + v->elem_base;
+    switch (v->type) {
+    case RR_TYPE_STRING:                                                          /* :114-128 */
+        if (n != 1) return RR_E_ENCODE;
+        if (v->enc == RR_ENC_INT) {
+            if (el[0].kind != RR_K_INT) return RR_E_ENCODE;
+            s = 14;
+        } else {
+            if ((v->enc != RR_ENC_RAW && v->enc != RR_ENC_EMBSTR) || el[0].kind != RR_K_STR || !ARENA_OK(el[0], arena_cap))
+                return RR_E_ENCODE;
+            s = 6 + (uint64_t)el[0].len;
+        }
+        break;
+    case RR_TYPE_LIST_QUICKLIST:                                                  /* :162-188 */
+        for (uint64_t i = 0; i < n; i++) {
+            if (el[i].kind == RR_K_INT) s += 4 + dec_len((int64_t)el[i].data);
+            else if (el[i].kind == RR_K_STR && ARENA_OK(el[i], arena_cap)) s += 4 + (uint64_t)el[i].len;
+            else return RR_E_ENCODE;
+        }
+        break;
+    case RR_TYPE_SET_INTSET:                                                      /* :220-226 */
+        if (v->enc != 2 && v->enc != 4 && v->enc != 8) return RR_E_ENCODE;
+        for (uint64_t i = 0; i < n; i++)
+            if (el[i].kind != RR_K_INT || !fits_width((int64_t)el[i].data, v->enc)) return RR_E_ENCODE;
+        s = 13 + (uint64_t)v->enc * n;
+        break;
+    case RR_TYPE_SET_HT:                                                          /* :227-239 */
+    case RR_TYPE_HASH_HT:                                                         /* :322-339 */
+        if (v->type == RR_TYPE_HASH_HT && (n & 1)) return RR_E_ENCODE;
+        s += 8;
+        for (uint64_t i = 0; i < n; i++) {
+            if (el[i].kind != RR_K_STR || !ARENA_OK(el[i], arena_cap)) return RR_E_ENCODE;
+            s += 8 + (uint64_t)el[i].len;
+        }
+        break;
+    case RR_TYPE_HASH_ZIPLIST:                                                    /* :317-320 */
+    case RR_TYPE_ZSET_ZIPLIST:                                                    /* :420-423 */
+        if (n < 1 || el[0].kind != RR_K_ZLRAW || !ARENA_OK(el[0], arena_cap)) return RR_E_ENCODE;
+        s = 13 + (uint64_t)el[0].len;
+        break;
+    case RR_TYPE_ZSET_SKIPLIST:                                                   /* :425-440 */
+        if (n & 1) return RR_E_ENCODE;
+        s += 8;
+        for (uint64_t i = 0; i < n; i += 2) {
+            if (el[i].kind != RR_K_STR || !ARENA_OK(el[i], arena_cap) || el[i + 1].kind != RR_K_SCORE) return RR_E_ENCODE;
+            s += 16 + (uint64_t)el[i].len;
+        }
+        break;
+    default:
+        return RR_E_ENCODE;
+    }
+    *size = s;
+    return RR_OK;
+}
+
+static inline const uint8_t *payload_at(const uint8_t *arena, const rr_elem *e) {
+    return (const uint8_t *)((uintptr_t)arena + (uintptr_t)e->data);   /* (arena NULL: data is the address) */
+}
+
+void rr_host_encode_value(const rr_value *v, const rr_elem *elems, const uint8_t *arena, uint8_t *o) {
+    const rr_elem *el = elems + v->elem_base;
+    const uint64_t n = v->n_elems;
+    uint64_t p = 5;
+    o[0] = v->type;                                                               /* :514-518 */
+    wr32(o + 1, v->lru & RR_LRU_MASK);
+    switch (v->type) {
+    case RR_TYPE_STRING:
+        o[5] = v->enc;
+        if (v->enc == RR_ENC_INT) wr64(o + 6, el[0].data);
+        else memcpy(o + 6, payload_at(arena, &el[0]), el[0].len);
+        break;
+    case RR_TYPE_LIST_QUICKLIST:
+        for (uint64_t i = 0; i < n; i++) {
+            uint32_t l;
+            if (el[i].kind == RR_K_INT) l = dec_write(o + p + 4, (int64_t)el[i].data);
+            else { l = el[i].len; memcpy(o + p + 4, payload_at(arena, &el[i]), l); }
+            wr32(o + p, l);
+            p += 4 + (uint64_t)l;
+        }
+        break;
+    case RR_TYPE_SET_INTSET: {
+        const unsigned w = v->enc;
+        wr32(o + 5, w);
+        wr32(o + 9, (uint32_t)n);
+        p = 13;
+        for (uint64_t i = 0; i < n; i++, p += w) {
+            const uint64_t x = el[i].data;
+            memcpy(o + p, &x, w);   /* (little-endian: the low w bytes) */
+        }
+        break;
+    }
+    case RR_TYPE_SET_HT:
+    case RR_TYPE_HASH_HT:
+        wr64(o + 5, v->type == RR_TYPE_SET_HT ? n : n / 2);
+        p = 13;
+        for (uint64_t i = 0; i < n; i++) {
+            wr64(o + p, el[i].len);
+            memcpy(o + p + 8, payload_at(arena, &el[i]), el[i].len);
+            p += 8 + (uint64_t)el[i].len;
+        }
+        break;
+    case RR_TYPE_HASH_ZIPLIST:
+    case RR_TYPE_ZSET_ZIPLIST:
+        wr64(o + 5, el[0].len);
+        memcpy(o + 13, payload_at(arena, &el[0]), el[0].len);
+        break;
+    case RR_TYPE_ZSET_SKIPLIST:
+        wr64(o + 5, n / 2);
+        p = 13;
+        for (uint64_t i = 0; i < n; i += 2) {
+            wr64(o + p, el[i].len);
+            memcpy(o + p + 8, payload_at(arena, &el[i]), el[i].len);
+            p += 8 + (uint64_t)el[i].len;
+            wr64(o + p, el[i + 1].data);
+            p += 8;
+        }
+        break;
+    default:
+        break;
+    }
+}
+
+int rr_host_encode_batch(const rr_value *values, const rr_elem *elems, uint64_t elem_cap, const uint8_t *arena,
+                         uint64_t arena_cap, uint64_t n, uint8_t *data, uint64_t data_cap, uint64_t *offsets,
+                         rr_totals *totals) {
+    if (!offsets || (n && !values) || (elem_cap && !elems) || (data_cap && !data)) return RR_API_EINVAL;
+    uint64_t base = 0, bad = 0, payload = 0, descs = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        const rr_value *v = &values[i];
+        uint64_t s;
+        const int st = rr_host_encode_size(v, elems, elem_cap, arena_cap, &s);
+        offsets[i] = base;
+        descs += v->n_elems;
+        if (st != RR_OK || s > data_cap || base > data_cap - s) bad++;   /* unencodable, or past data_cap */
+        else {
+            rr_host_encode_value(v, elems, arena, data + base);
+            const rr_elem *el = elems + v->elem_base;
+            if (v->type == RR_TYPE_HASH_ZIPLIST || v->type == RR_TYPE_ZSET_ZIPLIST) payload += el[0].len;
+            else
+                for (uint32_t k = 0; k < v->n_elems; k++)
+                    if (el[k].kind == RR_K_STR) payload += el[k].len;
+        }
+        base += s;
+    }
+    offsets[n] = base;
+    if (totals) {
+        totals->n_elems = descs;
+        totals->bytes = base;
+        totals->n_bad = bad;
+        totals->payload = payload;
+    }
+    return RR_API_OK;
+}

@@ -63,3 +63,42 @@ def assert_flat_equal(a, b, what=""):
         i = int(bad[0]) if len(bad) else n
         raise AssertionError(f"{what}: descriptors differ (len {len(ea)} vs {len(eb)}); first #{i}: "
                              f"{ea[i] if i < len(ea) else None} vs {eb[i] if i < len(eb) else None}")
+
+
+FUZZ_SPECIALS = [0, 1, 2, 3, 4, 7, 8, 15, 16, 0x7F, 0x80, 0xFE, 0xFF, 0xFFFF, 0x10000, 0x7FFFFFFF, 0xFFFFFFFF]
+
+
+def structured_mutations(data, offs, seed, per_value=5):
+    """The structured fuzz corpus: per valid blob, `per_value` mutants — a bit flip, a truncation,
+    a random byte, a header field (counts / lengths / zlbytes / zltail / zllen / intset width and
+    count / encoding bytes) or an element length overwritten with a small / boundary / huge value,
+    inserted bytes, swapped bytes.  Returns the mutated blobs (the GPU suite and the host codec
+    test share it, so both are held to the oracle on the same inputs)."""
+    rng = np.random.default_rng(seed)
+    specials = FUZZ_SPECIALS
+    blobs = []
+    for i in range(len(offs) - 1):
+        b = bytes(data[offs[i]:offs[i + 1]])
+        for _ in range(per_value):
+            m = bytearray(b)
+            r = int(rng.integers(0, 7))
+            if r == 0 and m:
+                m[int(rng.integers(0, len(m)))] ^= 1 << int(rng.integers(0, 8))
+            elif r == 1 and m:
+                m = m[:int(rng.integers(0, len(m)))]
+            elif r == 2 and m:
+                m[int(rng.integers(0, len(m)))] = int(rng.integers(0, 256))
+            elif r == 3 and len(m) >= 9:   # a header field: bytes 5.. hold counts / lengths / ziplist words
+                at = int(rng.integers(5, min(len(m) - 3, 30)))
+                m[at:at + 4] = int(specials[int(rng.integers(len(specials)))]).to_bytes(4, "little")
+            elif r == 4 and len(m) >= 13:  # an element length field somewhere in the body
+                at = int(rng.integers(13, len(m) - 3)) if len(m) > 16 else 5
+                m[at:at + 4] = int(specials[int(rng.integers(len(specials)))]).to_bytes(4, "little")
+            elif r == 5 and m:
+                at = int(rng.integers(0, len(m)))
+                m[at:at] = bytes(rng.integers(0, 256, int(rng.integers(1, 9)), dtype=np.uint8))
+            elif r == 6 and len(m) > 2:
+                a, c = (int(x) for x in rng.integers(0, len(m), 2))
+                m[a], m[c] = m[c], m[a]
+            blobs.append(bytes(m))
+    return blobs

@@ -56,6 +56,17 @@ def test_library_exports_every_kv_symbol():
     assert sorted(rr.KV_EXPORTS) == syms
 
 
+def test_library_exports_every_host_symbol():
+    """include/rr_host.h (the host codec behind the compat shim's per-key calls): every declared
+    function is exported and bound."""
+    lib = rr.lib()
+    syms = declared_symbols("rr_host.h")
+    assert len(syms) == 6
+    for s in syms:
+        assert hasattr(lib, s), f"{s} declared in include/rr_host.h but not exported"
+    assert sorted(rr.HOST_EXPORTS) == syms
+
+
 def test_compat_header_symbols_defined(tmp_path):
     """Every function include/rock_serdes_compat.h declares (the legacy desString / serObject /
     desObject of rock_serdes.h:47-49 and the rr_compat_* batch forms) is defined by the shim,

@@ -9,7 +9,7 @@ import redrock_old_amd as rr
 from oracle import cpu
 from oracle import pyoracle as po
 
-from helpers import assert_flat_equal, batch_from_blobs, expected_flat, golden
+from helpers import assert_flat_equal, batch_from_blobs, expected_flat, golden, structured_mutations
 
 pytestmark = pytest.mark.gpu
 G = golden()
@@ -514,34 +514,8 @@ def test_fuzz_structured_decode_and_reencode(engine, cfg, n):
 
 
 def _fuzz_structured_round(engine, cfg, n, seed):
-    rng = np.random.default_rng(seed)
     data, offs = rr.gen_batch(cfg, n)
-    specials = [0, 1, 2, 3, 4, 7, 8, 15, 16, 0x7F, 0x80, 0xFE, 0xFF, 0xFFFF, 0x10000, 0x7FFFFFFF, 0xFFFFFFFF]
-    blobs = []
-    for i in range(len(offs) - 1):
-        b = bytes(data[offs[i]:offs[i + 1]])
-        for _ in range(5):
-            m = bytearray(b)
-            r = int(rng.integers(0, 7))
-            if r == 0 and m:
-                m[int(rng.integers(0, len(m)))] ^= 1 << int(rng.integers(0, 8))
-            elif r == 1 and m:
-                m = m[:int(rng.integers(0, len(m)))]
-            elif r == 2 and m:
-                m[int(rng.integers(0, len(m)))] = int(rng.integers(0, 256))
-            elif r == 3 and len(m) >= 9:   # a header field: bytes 5.. hold counts / lengths / ziplist words
-                at = int(rng.integers(5, min(len(m) - 3, 30)))
-                m[at:at + 4] = int(specials[int(rng.integers(len(specials)))]).to_bytes(4, "little")
-            elif r == 4 and len(m) >= 13:  # an element length field somewhere in the body
-                at = int(rng.integers(13, len(m) - 3)) if len(m) > 16 else 5
-                m[at:at + 4] = int(specials[int(rng.integers(len(specials)))]).to_bytes(4, "little")
-            elif r == 5 and m:
-                at = int(rng.integers(0, len(m)))
-                m[at:at] = bytes(rng.integers(0, 256, int(rng.integers(1, 9)), dtype=np.uint8))
-            elif r == 6 and len(m) > 2:
-                a, c = (int(x) for x in rng.integers(0, len(m), 2))
-                m[a], m[c] = m[c], m[a]
-            blobs.append(bytes(m))
+    blobs = structured_mutations(data, offs, seed)
     fdata, foffs = batch_from_blobs(blobs)
     v, e, a, t = engine.decode_host(fdata, foffs)
     ov, oe, oa, ot = cpu.decode(fdata, foffs, nthreads=8)
