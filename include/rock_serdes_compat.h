@@ -1,24 +1,24 @@
 /*
- * rock_serdes_compat.h — RedRock's legacy serdes entry points (src/rock_serdes.h:47-49) on
- * the MI355X engine, for a build inside a Redis tree.
+ * rock_serdes_compat.h — RedRock's legacy serdes entry points (src/rock_serdes.h:47-55) on the
+ * engine, for a build inside a Redis tree.
  *
  * The bodies are redrock_old_amd/compat/rock_serdes_compat.c.  They need Redis's robj / sds /
  * dict / quicklist / intset / skiplist (server.h), so this header declares them only when
  * compiled inside a RedRock tree: -DRR_REDIS_TREE, after #include "server.h".
  *
- *   desObject / desString   the blob goes through rr_decode_batch_host (the GPU decode), the
- *                           robj is built on the host from the flat records — heap objects
- *                           cannot be built on the device;
- *   serObject               the robj is flattened on the host, rr_encode_batch_host writes
- *                           the blob (the GPU encode), returned as a fresh zmalloc'd sds;
+ *   desObject / desString   one blob: the engine's host codec (rr_host.h) on the calling thread
+ *                           (the GPU path's exact verdicts and flat form), then the robj;
+ *   serObject               one robj: described in place and written by the host codec into a
+ *                           fresh zmalloc'd sds;
+ *   the batch forms         below the measured crossover the same host codec per value, at or
+ *                           above it the GPU (rr_decode_batch_host / rr_encode_batch_host);
  *   any nonzero per-value status, and any engine error, ends in serverPanic() — the
  *   reference aborts through serverAssert/serverPanic on the same inputs (rock_serdes.c).
  *
- * One value per call pays a kernel launch; the batch forms below are what the RedRock call
- * sites should use: the rock thread's restore queue (rock.c:302-383, one key per RockJob
- * today, server.h:1013-1019) and the fork child's snapshot loads (rock.c:527-540) restore
- * many keys per call, and the evictor (rock_hotkey.c:315-455) dumps many victims per call.
- * INTEGRATION.md shows the patches.
+ * So rock.c and rock_hotkey.c link against these unchanged: the per-key calls cost what the
+ * reference's own C costs, and no call of theirs waits on a GPU launch.  A fork child (BGSAVE /
+ * AOF rewrite, rock.c:527-550) always takes the host codec and never touches the HIP runtime.
+ * INTEGRATION.md shows the wiring.
  */
 #ifndef ROCK_SERDES_COMPAT_H
 #define ROCK_SERDES_COMPAT_H
@@ -34,7 +34,8 @@ sds serObject(robj *o);                 /* rock_serdes.h:48, rock_serdes.c:512 *
 robj *desObject(void *buf, size_t len); /* rock_serdes.h:49, rock_serdes.c:538 */
 
 /* Batch forms: n blobs -> n robj (out[i] == desObject(bufs[i], lens[i])), n robj -> n sds
- * (out[i] == serObject(objs[i])), one engine call each. */
+ * (out[i] == serObject(objs[i])): the host codec per value below the crossover, one GPU call at
+ * or above it (rr_compat_set_route). */
 void rr_compat_des_batch(void *const *bufs, const size_t *lens, size_t n, robj **out);
 void rr_compat_ser_batch(robj *const *objs, size_t n, sds *out);
 
@@ -56,20 +57,27 @@ void _test_ser_des_set(void);
 void _test_ser_des_hash(void);
 void _test_ser_des_zset(void);
 
-/* Fork children (rock.c:527-550).  A process that has used the engine opens, right before each
- * fork (pthread_atfork), a connection of the child's own with a decode service thread behind
- * it; desObject in the child sends its blobs there over a socket and builds the robj from the
- * flat records that come back, never touching the HIP runtime.  The service ends when the
- * child closes its end (exit, kill) and closes its own end when a request fails, so a child
- * never reads another child's reply and never waits on a dead service.
- * rr_compat_service_start opens this process's own connection (0 or -1);
- * rr_compat_test_as_child(1) makes this process route desObject as a child would;
- * rr_compat_test_send_only writes one FLAT request and returns without its reply (a child
- * killed mid-call); rr_compat_test_drop_services shuts every live service end down (tests). */
-int rr_compat_service_start(void);
+/* Routing of desObject / serObject and the batch forms: AUTO (the default) = the host codec
+ * below RR_COMPAT_GPU_MIN values per call (environment; a measured default), the GPU at or above
+ * it; HOST / GPU force one route (tests, benches).  A fork child (rock.c:527-550) never takes the
+ * GPU route: under AUTO or HOST it decodes on its own CPU, under GPU the engine panics rather than
+ * touch the parent's HIP runtime. */
+#define RR_COMPAT_ROUTE_AUTO 0
+#define RR_COMPAT_ROUTE_HOST 1
+#define RR_COMPAT_ROUTE_GPU  2
+void rr_compat_set_route(int route);
+
+/* Process exit: every GPU call through this shim is counted in flight; the owner's exit waits
+ * (at most 10 s) for the count to drain, and a thread calling in after the exit began parks
+ * rather than enter the HIP runtime being torn down (RedRock's rock thread, rock.c:615, is never
+ * joined).  A thread's engine context is destroyed when the thread ends.  Tests:
+ * rr_compat_in_flight = the GPU calls in flight; rr_compat_test_hold_teardown(ms) makes the next
+ * thread-exit context teardown sleep `ms` inside the count (rr_compat_test_holding says it
+ * started); rr_compat_test_as_child(1) routes this process as a fork child would. */
+int rr_compat_in_flight(void);
+void rr_compat_test_hold_teardown(int ms);
+int rr_compat_test_holding(void);
 void rr_compat_test_as_child(int on);
-int rr_compat_test_send_only(const void *blob, size_t len);
-void rr_compat_test_drop_services(void);
 #endif
 
 #endif

@@ -42,6 +42,11 @@ uint64_t rr_host_reserve(const uint8_t *b, uint64_t len);
 int rr_host_decode_value(const uint8_t *blob, uint64_t len, uint64_t base, rr_value *v, rr_elem *el,
                          uint64_t cap, uint64_t *need);
 
+/* The status and record (type, enc, status, lru, n_elems) rr_host_decode_value gives, without
+ * its descriptors: a Hash / ZSet ziplist is walked for its verdict only (a caller keeping the raw
+ * ziplist, as desObject does, needs no entry descriptors).  Returns v->status. */
+int rr_host_check_value(const uint8_t *blob, uint64_t len, rr_value *v);
+
 /* rr_decode_batch_host's contract on the CPU: elem_base = the reservations' prefix, a malformed
  * value's slots zero-filled, RR_E_CAPACITY past elem_cap, totals; arena (may be NULL) receives
  * the byte mirror of data.  Always RR_API_OK (RR_API_EINVAL for a NULL pointer). */

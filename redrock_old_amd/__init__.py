@@ -95,8 +95,8 @@ RDB_EXPORTS = ["rr_rdb_request_batch", "rr_rdb_blobs_free", "rr_rdb_request_flat
 # include/rr_kv.h (batched store I/O around the GPU path, row f2; used from C)
 KV_EXPORTS = ["rr_kv_dump_batch", "rr_kv_restore_batch"]
 # include/rr_host.h (the host codec: RedRock's per-key call sites through the compat shim, row f1)
-HOST_EXPORTS = ["rr_host_reserve", "rr_host_decode_value", "rr_host_decode_batch", "rr_host_encode_size",
-                "rr_host_encode_value", "rr_host_encode_batch"]
+HOST_EXPORTS = ["rr_host_reserve", "rr_host_decode_value", "rr_host_check_value", "rr_host_decode_batch",
+                "rr_host_encode_size", "rr_host_encode_value", "rr_host_encode_batch"]
 SNAPPY_STATUS = {0: "OK", 1: "HEADER", 2: "TRUNC", 3: "OFFSET", 4: "OVERFLOW", 5: "LENGTH", 6: "CAPACITY"}
 
 _lib = None
@@ -168,6 +168,7 @@ def lib():
         L.rr_host_reserve.restype = u64
         L.rr_host_decode_value.argtypes = [vp, u64, u64, vp, vp, u64, C.POINTER(C.c_uint64)]
         L.rr_host_decode_batch.argtypes = [vp, vp, u64, vp, vp, u64, vp, C.POINTER(Totals)]
+        L.rr_host_check_value.argtypes = [vp, u64, vp]
         L.rr_host_encode_size.argtypes = [vp, vp, u64, u64, C.POINTER(C.c_uint64)]
         L.rr_host_encode_value.argtypes = [vp, vp, vp, vp]
         L.rr_host_encode_value.restype = None
@@ -314,6 +315,19 @@ def host_decode_value(blob: bytes, base: int = 0, cap: int = 64):
     need = C.c_uint64()
     st = lib().rr_host_decode_value(_ptr(b), len(blob), base, _ptr(v), _ptr(e), cap, C.byref(need))
     return int(st), v[0], e[:min(int(v[0]["n_elems"]), cap)], int(need.value)
+
+
+def host_check(data: np.ndarray, offsets: np.ndarray) -> np.ndarray:
+    """rr_host_check_value per blob: the records (elem_base 0) rr_host_decode_value gives."""
+    data = np.ascontiguousarray(data, np.uint8)
+    n = len(offsets) - 1
+    out = np.zeros(n, VALUE_DT)
+    L = lib()
+    base = data.ctypes.data
+    for i in range(n):
+        o, ln = int(offsets[i]), int(offsets[i + 1] - offsets[i])
+        L.rr_host_check_value(C.c_void_p(base + o), ln, C.c_void_p(out.ctypes.data + 16 * i))
+    return out
 
 
 def host_encode(values: np.ndarray, elems: np.ndarray, arena: np.ndarray, data_cap: int | None = None):

@@ -1,203 +1,171 @@
 /*
- * rock_serdes_compat.c — bodies of RedRock's legacy serdes signatures (rock_serdes.h:47-49)
- * over the MI355X batch engine (include/rock_serdes_compat.h).
+ * rock_serdes_compat.c — bodies of RedRock's legacy serdes signatures (rock_serdes.h:47-55)
+ * over the engine (include/rock_serdes_compat.h).
  *
  * Built inside a Redis tree: it includes the tree's server.h and uses only the Redis API the
  * reference rock_serdes.c itself uses (robj constructors, sds, dict, quicklist, intset,
- * zslInsert, zmalloc).  The decode and encode of the bytes run on the GPU through
- * rr_decode_batch_host / rr_encode_batch_host; this file only turns flat records into heap
- * objects and back, which a GPU cannot do.  Abort semantics are the reference's: a blob the
- * reference would reject (any nonzero rr_value.status) ends in serverPanic.
+ * zslInsert, zmalloc).  Abort semantics are the reference's: a blob the reference would reject
+ * (any nonzero rr_value.status) ends in serverPanic.
  *
- * The repo's own unit test compiles this file against a minimal Redis model
- * (tests/c/miniredis) instead of a Redis tree.
+ * Routing.  RedRock's call sites are per key — desObject per rock-thread job (rock.c:468) and per
+ * key in the BGSAVE child (rock.c:538), serObject per evicted key (rock.c:691) — so a call of one
+ * value, and a batch form below the measured crossover, runs the engine's host codec
+ * (include/rr_host.h) on the calling thread: the GPU path's exact flat form, no launch, no PCIe.
+ * A batch at or above the crossover goes through the GPU entry points (rr_decode_batch_host /
+ * rr_encode_batch_host).  A fork child always takes the host codec: it must not touch the HIP
+ * runtime its parent initialised, and on the CPU it needs no help from the parent.  Either way
+ * this file turns flat records into heap objects and back, which a GPU cannot do.
+ *
+ * Process exit.  Threads that call in here are not the shim's own: RedRock's rock thread
+ * (rock.c:615) is never joined and loops on desObject (rock.c:552-596).  A thread inside the HIP
+ * runtime while exit() tears the runtime down crashes the process, so every engine (HIP) call
+ * is counted in flight; the owner's exit raises a closing flag, waits (bounded) for the count to
+ * drain, and any later caller parks instead of entering the runtime.  Host-codec calls touch no
+ * runtime and are never held.
+ *
+ * The repo's own unit tests compile this file against a minimal Redis model (tests/c/miniredis)
+ * instead of a Redis tree.
  */
 #ifndef RR_REDIS_TREE
 #define RR_REDIS_TREE 1
 #endif
-#include <poll.h>
 #include <pthread.h>
-#include <signal.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
-#include <sys/socket.h>
+#include <time.h>
 #include <unistd.h>
 
 #include "server.h"
 
 #include "rock_serdes_compat.h"
+#include "rr_host.h"
 
 static int g_device;
 static __thread rr_ctx *g_ctx;   /* one engine context per host thread (rr_serdes.h) */
 
 void rr_compat_set_device(int device) { g_device = device; }
 
-/* ---- fork children (rock.c:527-550: BGSAVE / AOF rewrite call desObject in a fork()ed child).
- * A child must not touch the HIP runtime its parent initialised, so in a child desObject does
- * not decode itself: it sends the blob over a socket to a decode service thread in the parent
- * (rr_rdb_serve's FLAT request, the blob standing in for the key) and builds the robj from the
- * flat records that come back.  rock.c needs no change.
- *
- * Every fork gets a connection of its own: right before the fork (pthread_atfork prepare) the
- * parent opens a socketpair and starts a service thread on one end; after the fork the parent
- * closes the child's end and the child closes every service end it inherited.  So the service
- * sees EOF when its child exits (killRDBChild on FLUSHALL, SHUTDOWN, replication changes) and
- * drops any response it still owed, and a later child can never read an earlier child's reply
- * or send into the middle of its request.  A service that fails (a decode error, a device
- * failure, a write error) closes its end: the child's request then fails and it panics instead
- * of waiting forever. */
-static pid_t g_owner;                     /* the process whose threads own GPU contexts */
-static pthread_mutex_t g_svc_mu = PTHREAD_MUTEX_INITIALIZER;
-#define RR_COMPAT_MAX_SVC 64
-static int g_svc_fds[RR_COMPAT_MAX_SVC];  /* service ends of the live connections (parent) */
-static int g_nsvc;
-/* the service threads, joinable: a thread still inside the HIP runtime (its context's teardown
- * after its child exited) when the process exits would race the runtime's own teardown, so the
- * owner's exit ends and joins them (compat_exit); a finished thread is joined when its slot is
- * next needed.  0 free, 1 running, 2 finished */
-static pthread_t g_th[RR_COMPAT_MAX_SVC];
-static int g_th_state[RR_COMPAT_MAX_SVC];
-static int g_child_fd = -1;               /* this process's own connection (child end) */
-static int g_fork_fd = -1;                /* the connection opened for the fork in progress */
-static int g_as_child;                    /* test hook: route this process as a child would */
+/* ---------------------------------------------------------------- routing */
+
+/* The crossover (values per call) from which a batch form goes to the GPU.  Measured with
+ * tests/c/bench_callpattern.c (profiles/r6_callpattern_cfg4.json): the robj a call builds or
+ * walks cost the same on either route, so the GPU route pays only for very large batches.
+ * RR_COMPAT_GPU_MIN overrides it (values; 0 = never). */
+#define RR_COMPAT_GPU_MIN_DEFAULT 65536
+static int g_route = RR_COMPAT_ROUTE_AUTO;
+static uint64_t g_gpu_min;
+static pthread_once_t g_cfg_once = PTHREAD_ONCE_INIT;
+
+static void read_config(void) {
+    const char *s = getenv("RR_COMPAT_GPU_MIN");
+    g_gpu_min = s ? strtoull(s, NULL, 10) : RR_COMPAT_GPU_MIN_DEFAULT;
+}
+
+void rr_compat_set_route(int route) { g_route = route; }
+
+static pid_t g_owner;   /* the process whose threads own GPU contexts */
+static int g_as_child;  /* test hook: route this process as a fork child would */
 
 static int in_child(void) { return g_as_child || (g_owner && getpid() != g_owner); }
 
-static void compat_exit(void);
+/* n values through the GPU entry points? */
+static int use_gpu(size_t n) {
+    if (in_child()) return g_route == RR_COMPAT_ROUTE_GPU;   /* (the engine then refuses, below) */
+    if (g_route != RR_COMPAT_ROUTE_AUTO) return g_route == RR_COMPAT_ROUTE_GPU;
+    pthread_once(&g_cfg_once, read_config);
+    return g_gpu_min && n >= g_gpu_min;
+}
+
+void rr_compat_test_as_child(int on) { g_as_child = on; }
+
+/* ---------------------------------------------------------------- engine calls and exit */
+
+static int g_inflight;          /* threads inside an engine (HIP) call */
+static int g_closing;           /* the owner's exit has begun */
+static pthread_t g_closer;      /* the thread running it (its own later calls pass) */
+static __thread int t_inflight; /* this thread's share of g_inflight */
+static int g_test_hold_ms, g_test_holding;
+
+/* The process is exiting under us: this thread must never enter (or re-enter) the runtime. */
+static __attribute__((noreturn)) void park(void) {
+    for (;;) pause();
+}
+
+static void engine_enter(void) {
+    __atomic_add_fetch(&g_inflight, 1, __ATOMIC_SEQ_CST);
+    t_inflight++;
+    if (__atomic_load_n(&g_closing, __ATOMIC_SEQ_CST) && !pthread_equal(pthread_self(), g_closer)) {
+        t_inflight--;
+        __atomic_sub_fetch(&g_inflight, 1, __ATOMIC_SEQ_CST);
+        park();
+    }
+}
+
+static void engine_leave(void) {
+    t_inflight--;
+    __atomic_sub_fetch(&g_inflight, 1, __ATOMIC_SEQ_CST);
+}
+
+/* The owner's exit: no new engine call, then the calls in flight drain (at most 10 s; a call
+ * stuck longer than that is a hung device, and the exit goes on).  exit_hook registers this once
+ * the runtime is up, so it runs before every exit handler the runtime registered. */
+static void compat_exit(void) {
+    if (g_owner && getpid() != g_owner) return;   /* (a fork child has no engine calls) */
+    g_closer = pthread_self();
+    __atomic_store_n(&g_closing, 1, __ATOMIC_SEQ_CST);
+    const struct timespec ms = {0, 1000000};
+    for (int i = 0; i < 10000 && __atomic_load_n(&g_inflight, __ATOMIC_SEQ_CST) > t_inflight; i++)
+        nanosleep(&ms, NULL);
+}
+
 static int g_exit_hooked;
 static void exit_hook(void) {
     if (!__atomic_exchange_n(&g_exit_hooked, 1, __ATOMIC_SEQ_CST)) atexit(compat_exit);
 }
 
+/* A thread's context is destroyed when the thread ends (a context per host thread), inside the
+ * engine count so an exit meanwhile waits for it. */
+static pthread_key_t g_ctx_key;
+static pthread_once_t g_key_once = PTHREAD_ONCE_INIT;
+
+static void ctx_at_thread_exit(void *p) {
+    if (in_child()) return;   /* (not ours to destroy) */
+    engine_enter();
+    const int hold = __atomic_exchange_n(&g_test_hold_ms, 0, __ATOMIC_SEQ_CST);
+    if (hold) {   /* test hook: a teardown still running when the process exits */
+        __atomic_store_n(&g_test_holding, 1, __ATOMIC_SEQ_CST);
+        const struct timespec t = {hold / 1000, (long)(hold % 1000) * 1000000};
+        nanosleep(&t, NULL);
+    }
+    rr_ctx_destroy((rr_ctx *)p);
+    g_ctx = NULL;
+    engine_leave();
+}
+
+static void make_key(void) { pthread_key_create(&g_ctx_key, ctx_at_thread_exit); }
+
+void rr_compat_test_hold_teardown(int ms) { __atomic_store_n(&g_test_hold_ms, ms, __ATOMIC_SEQ_CST); }
+int rr_compat_test_holding(void) { return __atomic_load_n(&g_test_holding, __ATOMIC_SEQ_CST); }
+int rr_compat_in_flight(void) { return __atomic_load_n(&g_inflight, __ATOMIC_SEQ_CST); }
+
+/* This thread's context, inside engine_enter / engine_leave. */
 static rr_ctx *engine(void) {
-    if (in_child()) serverPanic("rock serdes: the GPU engine cannot be used in a fork child (HIP is the parent's)");
+    if (in_child()) {
+        engine_leave();
+        serverPanic("rock serdes: the GPU engine cannot be used in a fork child (HIP is the parent's)");
+    }
     if (!g_ctx) {
-        if (rr_ctx_create(g_device, &g_ctx) != RR_API_OK) serverPanic("rock serdes engine: %s", rr_last_error());
+        if (rr_ctx_create(g_device, &g_ctx) != RR_API_OK) {
+            engine_leave();
+            serverPanic("rock serdes engine: %s", rr_last_error());
+        }
         if (!g_owner) g_owner = getpid();
         exit_hook();
+        pthread_once(&g_key_once, make_key);
+        pthread_setspecific(g_ctx_key, g_ctx);
     }
     return g_ctx;
-}
-
-static int echo_blob(void *user, size_t k, const int *dbis, const char *const *keys, const size_t *key_lens,
-                     void **vals, size_t *val_lens) {
-    (void)user; (void)dbis;
-    for (size_t i = 0; i < k; i++) { vals[i] = (void *)keys[i]; val_lens[i] = key_lens[i]; }
-    return 0;
-}
-
-/* one connection's service: until its child closes the other end, or a request fails */
-static void *decode_service(void *arg) {
-    const int slot = (int)((intptr_t)arg >> 32), fd = (int)(uint32_t)(intptr_t)arg;
-    sigset_t pipe_set;   /* a reply to a child that is gone: EPIPE on this thread, not SIGPIPE */
-    sigemptyset(&pipe_set);
-    sigaddset(&pipe_set, SIGPIPE);
-    pthread_sigmask(SIG_BLOCK, &pipe_set, NULL);
-    /* the engine context only once the child's first request is there: the thread starts inside
-     * fork()'s prepare handler, and a child that never asks must cost no GPU context */
-    rr_ctx *ctx = NULL;
-    struct pollfd pf = {fd, POLLIN, 0};
-    char peek;
-    if (poll(&pf, 1, -1) > 0 && recv(fd, &peek, 1, MSG_PEEK) == 1 && rr_ctx_create(g_device, &ctx) == RR_API_OK) {
-        exit_hook();
-        rr_rdb_serve(fd, fd, echo_blob, NULL, NULL, ctx, 64);
-        rr_ctx_destroy(ctx);
-    }
-    pthread_mutex_lock(&g_svc_mu);
-    for (int i = 0; i < g_nsvc; i++)
-        if (g_svc_fds[i] == fd) { g_svc_fds[i] = g_svc_fds[--g_nsvc]; break; }
-    close(fd);   /* the child's read sees EOF */
-    g_th_state[slot] = 2;
-    pthread_mutex_unlock(&g_svc_mu);
-    return NULL;
-}
-
-/* a new connection with its own service thread (g_svc_mu held): the child end, or -1 */
-static int open_connection(void) {
-    int sv[2];
-    pthread_t th;
-    int slot = -1;
-    for (int i = 0; i < RR_COMPAT_MAX_SVC; i++) {
-        if (g_th_state[i] == 2) { pthread_join(g_th[i], NULL); g_th_state[i] = 0; }   /* (it has returned) */
-        if (g_th_state[i] == 0 && slot < 0) slot = i;
-    }
-    if (slot < 0 || g_nsvc == RR_COMPAT_MAX_SVC || socketpair(AF_UNIX, SOCK_STREAM, 0, sv) != 0) return -1;
-    g_svc_fds[g_nsvc++] = sv[0];
-    if (pthread_create(&th, NULL, decode_service, (void *)(((intptr_t)slot << 32) | (intptr_t)(uint32_t)sv[0])) != 0) {
-        g_nsvc--;
-        close(sv[0]);
-        close(sv[1]);
-        return -1;
-    }
-    g_th[slot] = th;
-    g_th_state[slot] = 1;
-    return sv[1];
-}
-
-/* this process's own connection (the in-process child route of the tests) */
-int rr_compat_service_start(void) {
-    pthread_mutex_lock(&g_svc_mu);
-    if (g_child_fd < 0) g_child_fd = open_connection();
-    const int rc = g_child_fd >= 0 ? 0 : -1;
-    pthread_mutex_unlock(&g_svc_mu);
-    return rc;
-}
-
-/* the lock is held across the fork, so the child's copy of the registry is consistent */
-static void atfork_prepare(void) {
-    pthread_mutex_lock(&g_svc_mu);
-    if (g_owner && getpid() == g_owner && !g_as_child) g_fork_fd = open_connection();
-}
-static void atfork_parent(void) {
-    if (g_fork_fd >= 0) close(g_fork_fd);   /* the child's end is the child's alone */
-    g_fork_fd = -1;
-    pthread_mutex_unlock(&g_svc_mu);
-}
-static void atfork_child(void) {
-    g_ctx = NULL;   /* (the parent's context is not ours) */
-    memset(g_th_state, 0, sizeof g_th_state);   /* (nor its threads) */
-    for (int i = 0; i < g_nsvc; i++) close(g_svc_fds[i]);   /* the parent's service ends */
-    g_nsvc = 0;
-    if (g_child_fd >= 0) close(g_child_fd);   /* the parent's own connection */
-    g_child_fd = g_fork_fd;
-    g_fork_fd = -1;
-    pthread_mutex_unlock(&g_svc_mu);
-}
-/* the owner's exit: every service's connection shut down (its thread sees EOF, destroys its
- * context, returns), then every thread joined, before the HIP runtime's own teardown (exit_hook
- * registers this once the runtime is up, so it runs before every handler the runtime registered) */
-static void compat_exit(void) {
-    if (g_owner && getpid() != g_owner) return;   /* (a fork child: no threads of its own) */
-    pthread_mutex_lock(&g_svc_mu);
-    for (int i = 0; i < g_nsvc; i++) shutdown(g_svc_fds[i], SHUT_RDWR);
-    pthread_t th[RR_COMPAT_MAX_SVC];
-    int n = 0;
-    for (int i = 0; i < RR_COMPAT_MAX_SVC; i++)
-        if (g_th_state[i]) { th[n++] = g_th[i]; g_th_state[i] = 0; }
-    pthread_mutex_unlock(&g_svc_mu);
-    for (int i = 0; i < n; i++) pthread_join(th[i], NULL);
-}
-__attribute__((constructor)) static void compat_atfork_register(void) {
-    pthread_atfork(atfork_prepare, atfork_parent, atfork_child);
-}
-
-void rr_compat_test_as_child(int on) { g_as_child = on; }
-
-/* test hooks: a child that dies after sending a request (its reply must never reach another
- * child), and the parent's services ending (a waiting child must fail, not hang) */
-int rr_compat_test_send_only(const void *blob, size_t len) {
-    const int dbi = RR_RDB_FLAT_TAG, zero = 0;
-    const size_t one = 1;
-    return g_child_fd >= 0 && write(g_child_fd, &dbi, sizeof dbi) == sizeof dbi &&
-                   write(g_child_fd, &one, sizeof one) == sizeof one && write(g_child_fd, &zero, sizeof zero) == sizeof zero &&
-                   write(g_child_fd, &len, sizeof len) == sizeof len && write(g_child_fd, blob, len) == (ssize_t)len
-               ? 0 : -1;
-}
-void rr_compat_test_drop_services(void) {
-    pthread_mutex_lock(&g_svc_mu);
-    for (int i = 0; i < g_nsvc; i++) shutdown(g_svc_fds[i], SHUT_RDWR);
-    pthread_mutex_unlock(&g_svc_mu);
 }
 
 static const char *status_name(unsigned st) {
@@ -218,8 +186,9 @@ static int pair_by_offset(const void *a, const void *b) {
 }
 
 /* The object desObject (rock_serdes.c:538-564) builds for one decoded value: every
- * descriptor already says what the reference derives from the bytes (rr_format.h). */
-static robj *robj_from_flat(const rr_value *v, const rr_elem *el, const uint8_t *arena) {
+ * descriptor already says what the reference derives from the bytes (rr_format.h).  blob (may be
+ * NULL) = the value's own bytes, for the copies the reference makes straight from them. */
+static robj *robj_from_flat(const rr_value *v, const rr_elem *el, const uint8_t *arena, const uint8_t *blob) {
     robj *o = NULL;
     const uint32_t n = v->n_elems;
     switch (v->type) {
@@ -247,7 +216,8 @@ static robj *robj_from_flat(const rr_value *v, const rr_elem *el, const uint8_t 
         intset *is = zrealloc(o->ptr, sizeof(intset) + (size_t)w * n);
         is->encoding = w;
         is->length = n;
-        for (uint32_t i = 0; i < n; i++) memcpy((char *)is->contents + (size_t)i * w, &el[i].data, w);
+        if (blob) memcpy(is->contents, blob + 13, (size_t)w * n);   /* the blob's contents, as :270-273 */
+        else for (uint32_t i = 0; i < n; i++) memcpy((char *)is->contents + (size_t)i * w, &el[i].data, w);
         o->ptr = is;
         break;
     }
@@ -306,28 +276,38 @@ static robj *robj_from_flat(const rr_value *v, const rr_elem *el, const uint8_t 
     return o;
 }
 
-/* a child's batch: the parent's decode service decodes it, the robj are built here */
-static void des_batch_in_child(void *const *bufs, const size_t *lens, size_t n, robj **out) {
-    if (g_child_fd < 0)
-        serverPanic("desObject in a fork child: the parent's decode service is not running "
-                    "(the parent must use the engine before it forks)");
-    int *dbis = zmalloc(sizeof(int) * n);
-    for (size_t i = 0; i < n; i++) dbis[i] = 0;
-    rr_rdb_flat f;
-    if (rr_rdb_request_flat(g_child_fd, g_child_fd, dbis, (const char *const *)bufs, lens, n, &f) != RR_API_OK || f.n != n)
-        serverPanic("desObject in a fork child: %s", rr_last_error());
-    for (size_t i = 0; i < n; i++) {
-        if (f.values[i].status != RR_OK)   /* the reference's serverAssert / serverPanic site */
-            serverPanic("desObject: bad blob (%s, status %u)", status_name(f.values[i].status), f.values[i].status);
-        out[i] = robj_from_flat(&f.values[i], f.elems + f.values[i].elem_base, f.arena);
+/* desObject on the calling thread: the host codec into a stack buffer (a value of more than 64
+ * descriptors asks for its exact count and decodes again into the heap), then the robj. */
+static robj *des_host(const void *buf, size_t len) {
+    rr_elem local[64], *el = local;
+    rr_value v;
+    uint64_t need;
+    const uint8_t *b = buf;
+    if (len >= 13 && (b[0] == RR_TYPE_HASH_ZIPLIST || b[0] == RR_TYPE_ZSET_ZIPLIST)) {
+        /* kept as its raw bytes (:356-366, :455-466): the ziplist's verdict, no entry descriptors */
+        const int st = rr_host_check_value(b, len, &v);
+        if (st != RR_OK) serverPanic("desObject: bad blob (%s, status %u)", status_name((unsigned)st), (unsigned)st);
+        local[0].kind = RR_K_ZLRAW;
+        local[0].data = 13;
+        local[0].len = (uint32_t)(len - 13);
+        return robj_from_flat(&v, local, b, b);
     }
-    rr_rdb_flat_free(&f);
-    zfree(dbis);
+    int st = rr_host_decode_value(buf, len, 0, &v, el, 64, &need);
+    if (st == RR_E_CAPACITY) {
+        el = zmalloc(sizeof(rr_elem) * need);
+        st = rr_host_decode_value(buf, len, 0, &v, el, need, NULL);
+    }
+    if (st != RR_OK) {   /* the reference's serverAssert / serverPanic site */
+        if (el != local) zfree(el);
+        serverPanic("desObject: bad blob (%s, status %u)", status_name((unsigned)st), (unsigned)st);
+    }
+    robj *o = robj_from_flat(&v, el, buf, buf);
+    if (el != local) zfree(el);
+    return o;
 }
 
-void rr_compat_des_batch(void *const *bufs, const size_t *lens, size_t n, robj **out) {
-    if (n == 0) return;
-    if (in_child()) { des_batch_in_child(bufs, lens, n, out); return; }
+/* n blobs through the GPU: one rr_decode_batch_host, then the robj from the records */
+static void des_batch_gpu(void *const *bufs, const size_t *lens, size_t n, robj **out) {
     uint64_t *offs = zmalloc(sizeof(uint64_t) * (n + 1));
     offs[0] = 0;
     for (size_t i = 0; i < n; i++) offs[i + 1] = offs[i] + lens[i];
@@ -339,15 +319,23 @@ void rr_compat_des_batch(void *const *bufs, const size_t *lens, size_t n, robj *
     rr_value *vals = zmalloc(sizeof(rr_value) * n);
     rr_elem *els = zmalloc(sizeof(rr_elem) * (cap ? cap : 1));
     rr_totals t;
+    engine_enter();
     /* no arena download: it would mirror `data` byte for byte, so the descriptors index it */
-    if (rr_decode_batch_host(engine(), data, offs, n, vals, els, cap, NULL, &t) != RR_API_OK)
-        serverPanic("desObject: %s", rr_last_error());
+    const int rc = rr_decode_batch_host(engine(), data, offs, n, vals, els, cap, NULL, &t);
+    engine_leave();
+    if (rc != RR_API_OK) serverPanic("desObject: %s", rr_last_error());
     for (size_t i = 0; i < n; i++) {
         if (vals[i].status != RR_OK)   /* the reference's serverAssert / serverPanic site */
             serverPanic("desObject: bad blob (%s, status %u)", status_name(vals[i].status), vals[i].status);
-        out[i] = robj_from_flat(&vals[i], els + vals[i].elem_base, data);
+        out[i] = robj_from_flat(&vals[i], els + vals[i].elem_base, data, data + offs[i]);
     }
     zfree(offs); zfree(data); zfree(vals); zfree(els);
+}
+
+void rr_compat_des_batch(void *const *bufs, const size_t *lens, size_t n, robj **out) {
+    if (n == 0) return;
+    if (use_gpu(n)) { des_batch_gpu(bufs, lens, n, out); return; }
+    for (size_t i = 0; i < n; i++) out[i] = des_host(bufs[i], lens[i]);
 }
 
 void rr_compat_rdb_load_batch(int fd_req, int fd_resp, int dbid, sds *keys, size_t k, robj **out) {
@@ -361,7 +349,7 @@ void rr_compat_rdb_load_batch(int fd_req, int fd_resp, int dbid, sds *keys, size
     for (size_t i = 0; i < k; i++) {
         if (f.values[i].status != RR_OK)   /* desObject's assert sites, as in rr_compat_des_batch */
             serverPanic("desObject: bad blob (%s, status %u)", status_name(f.values[i].status), f.values[i].status);
-        out[i] = robj_from_flat(&f.values[i], f.elems + f.values[i].elem_base, f.arena);
+        out[i] = robj_from_flat(&f.values[i], f.elems + f.values[i].elem_base, f.arena, NULL);
     }
     rr_rdb_flat_free(&f);
     zfree(dbis);
@@ -369,9 +357,12 @@ void rr_compat_rdb_load_batch(int fd_req, int fd_resp, int dbid, sds *keys, size
 }
 
 robj *desObject(void *buf, size_t len) {
-    robj *o = NULL;
-    rr_compat_des_batch(&buf, &len, 1, &o);
-    return o;
+    if (use_gpu(1)) {
+        robj *o = NULL;
+        des_batch_gpu(&buf, &len, 1, &o);
+        return o;
+    }
+    return des_host(buf, len);
 }
 
 robj *desString(char *s, size_t len, uint32_t lru) {
@@ -388,6 +379,7 @@ typedef struct {
     rr_elem *els;
     uint8_t *arena;
     uint64_t nv, ne, na, cap_v, cap_e, cap_a, out_bound;
+    int by_ref;   /* STR descriptors hold the payload's address (the host codec, arena NULL) */
 } flat_t;
 
 static rr_elem *add_elem(flat_t *f) {
@@ -400,17 +392,21 @@ static rr_elem *add_elem(flat_t *f) {
     return e;
 }
 static void add_str(flat_t *f, const void *p, size_t len) {
+    rr_elem *e = add_elem(f);
+    e->kind = RR_K_STR;
+    e->len = (uint32_t)len;
+    f->out_bound += 8 + len;
+    if (f->by_ref) {
+        e->data = (uint64_t)(uintptr_t)p;
+        return;
+    }
     if (f->na + len > f->cap_a) {
         while (f->na + len > f->cap_a) f->cap_a = f->cap_a ? 2 * f->cap_a : 4096;
         f->arena = zrealloc(f->arena, f->cap_a);
     }
-    rr_elem *e = add_elem(f);
-    e->kind = RR_K_STR;
     e->data = f->na;
-    e->len = (uint32_t)len;
     if (len) memcpy(f->arena + f->na, p, len);
     f->na += len;
-    f->out_bound += 8 + len;
 }
 static void add_int(flat_t *f, long long v) {
     rr_elem *e = add_elem(f);
@@ -511,20 +507,49 @@ static void flatten(flat_t *f, robj *o) {
 
 /* The serialize path's buffers, per thread and kept across calls: the evictor's per-key
  * serObject allocates nothing here after its first calls (a one-off large batch's growth is
- * given back at the end of rr_compat_ser_batch). */
+ * given back at the end of ser_batch_gpu). */
 static __thread flat_t t_flat;
 static __thread uint64_t *t_offs;
 static __thread uint8_t *t_data;
 static __thread size_t t_offs_cap, t_data_cap;
 
-void rr_compat_ser_batch(robj *const *objs, size_t n, sds *out) {
-    if (n == 0) return;
-    flat_t *f = &t_flat;
+static void flat_reset(flat_t *f, size_t n, int by_ref) {
     f->nv = f->ne = f->na = f->out_bound = 0;
+    f->by_ref = by_ref;
     if (n > f->cap_v) {
         f->vals = zrealloc(f->vals, sizeof(rr_value) * n);
         f->cap_v = n;
     }
+}
+
+/* serObject on the calling thread: the robj described in place (descriptors hold its strings'
+ * addresses, nothing is copied), sized, and written by the host codec straight into the sds. */
+static sds ser_host(robj *o) {
+    if (o->type == OBJ_SET && o->encoding == OBJ_ENCODING_INTSET) {   /* :220-226: the intset's own bytes */
+        const intset *is = o->ptr;
+        const size_t nb = (size_t)is->encoding * is->length;
+        sds s = sdsnewlen(SDS_NOINIT, 13 + nb);
+        const uint32_t lru = o->lru, hdr[2] = {is->encoding, is->length};
+        s[0] = RR_TYPE_SET_INTSET;
+        memcpy(s + 1, &lru, 4);
+        memcpy(s + 5, hdr, 8);
+        memcpy(s + 13, is->contents, nb);
+        return s;
+    }
+    flat_t *f = &t_flat;
+    flat_reset(f, 1, 1);
+    flatten(f, o);
+    uint64_t size;
+    if (rr_host_encode_size(&f->vals[0], f->els, f->ne, UINT64_MAX, &size) != RR_OK)
+        serverPanic("serObject: unencodable object (type %u, encoding %u)", o->type, o->encoding);
+    sds s = sdsnewlen(SDS_NOINIT, size);
+    rr_host_encode_value(&f->vals[0], f->els, NULL, (uint8_t *)s);
+    return s;
+}
+
+static void ser_batch_gpu(robj *const *objs, size_t n, sds *out) {
+    flat_t *f = &t_flat;
+    flat_reset(f, n, 0);
     for (size_t i = 0; i < n; i++) flatten(f, objs[i]);
     if (n + 1 > t_offs_cap) {
         t_offs = zrealloc(t_offs, sizeof(uint64_t) * (n + 1));
@@ -535,13 +560,15 @@ void rr_compat_ser_batch(robj *const *objs, size_t n, sds *out) {
         t_data_cap = f->out_bound + 16;
     }
     rr_totals t;
-    if (rr_encode_batch_host(engine(), f->vals, f->els, f->ne, f->arena, f->na, n, t_data, f->out_bound + 16, t_offs,
-                             &t) != RR_API_OK)
-        serverPanic("serObject: %s", rr_last_error());
+    engine_enter();
+    const int rc = rr_encode_batch_host(engine(), f->vals, f->els, f->ne, f->arena, f->na, n, t_data,
+                                        f->out_bound + 16, t_offs, &t);
+    engine_leave();
+    if (rc != RR_API_OK) serverPanic("serObject: %s", rr_last_error());
     if (t.n_bad) serverPanic("serObject: %llu unencodable objects", (unsigned long long)t.n_bad);
     for (size_t i = 0; i < n; i++) out[i] = sdsnewlen(t_data + t_offs[i], t_offs[i + 1] - t_offs[i]);
-    /* the thread's buffers keep their size between calls (the per-key serObject allocates
-     * nothing), but not a one-off large batch's: past 1 MiB and 4x this call's need, give it back */
+    /* the thread's buffers keep their size between calls, but not a one-off large batch's: past
+     * 1 MiB and 4x this call's need, give it back */
     const size_t big = 1u << 20;
     if (t_data_cap > big && t_data_cap > 4 * (f->out_bound + 16)) { zfree(t_data); t_data = NULL; t_data_cap = 0; }
     if (f->cap_a > big && f->cap_a > 4 * f->na) { zfree(f->arena); f->arena = NULL; f->cap_a = 0; }
@@ -550,10 +577,19 @@ void rr_compat_ser_batch(robj *const *objs, size_t n, sds *out) {
     if (t_offs_cap * sizeof(uint64_t) > big && t_offs_cap > 4 * (n + 1)) { zfree(t_offs); t_offs = NULL; t_offs_cap = 0; }
 }
 
+void rr_compat_ser_batch(robj *const *objs, size_t n, sds *out) {
+    if (n == 0) return;
+    if (use_gpu(n)) { ser_batch_gpu(objs, n, out); return; }
+    for (size_t i = 0; i < n; i++) out[i] = ser_host(objs[i]);
+}
+
 sds serObject(robj *o) {
-    sds s = NULL;
-    rr_compat_ser_batch(&o, 1, &s);
-    return s;
+    if (use_gpu(1)) {
+        sds s = NULL;
+        ser_batch_gpu(&o, 1, &s);
+        return s;
+    }
+    return ser_host(o);
 }
 
 /* ---------------------------------------------------------------- rock_serdes.h:51-55

@@ -186,56 +186,85 @@ static inline void put(emit_t *E, uint8_t kind, uint64_t data, uint32_t len, uin
 /* bytes of the STR descriptor e */
 static inline const uint8_t *str_at(const emit_t *E, const rr_elem *e) { return E->b + (e->data - E->base); }
 
+/* Entry sizes from the encoding byte alone (ziplist.c:300-330 ZIP_DECODE_LENGTH, zipIntSize
+ * :446-466), for the encodings that need nothing else: a 6-bit string (00pppppp: 1 + length) and
+ * every integer (1 + its width; the immediates 0xF1..0xFD: 1).  0 = decode the slow way (14- and
+ * 32-bit strings, invalid integer encodings).  ZL_IW = an integer encoding's width. */
+static uint8_t ZL_ESIZE[256], ZL_IW[256];
+static void zl_tables(void) {
+    for (int c = 0; c < 64; c++) ZL_ESIZE[c] = (uint8_t)(1 + c);
+    static const uint8_t enc[5] = {0xFE, 0xC0, 0xF0, 0xD0, 0xE0}, w[5] = {1, 2, 3, 4, 8};
+    for (int i = 0; i < 5; i++) { ZL_ESIZE[enc[i]] = (uint8_t)(1 + w[i]); ZL_IW[enc[i]] = w[i]; }
+    for (int c = 0xF1; c <= 0xFD; c++) ZL_ESIZE[c] = 1;
+}
+static void __attribute__((constructor)) rr_host_init(void) { zl_tables(); }
+
+/* the little-endian integer of `w` bytes at the low end of raw, sign-extended (w = 3: the
+ * 24-bit form, zipLoadInteger :552-556) */
+static inline int64_t sext(uint64_t raw, unsigned w) {
+    const unsigned sh = 64 - 8 * w;
+    return (int64_t)(raw << sh) >> sh;
+}
+
 /* A ziplist's entries (ziplist.c:300-447: ZIP_DECODE_PREVLEN, ZIP_DECODE_LENGTH, zipIntSize,
  * zipLoadInteger; header :193-256), each checked as one forward walk would: its prevlen is the
  * size of the entry before it, its fields end inside the ziplist, the last one ends at the 0xFF
- * byte; then zltail and zllen (unless saturated) agree.  zl sits at blob offset `at`. */
+ * byte; then zltail and zllen (unless saturated) agree.  zl sits at blob offset `at`.  The
+ * common entry (1-byte prevlen, a 6-bit string or an integer, 9 bytes from the end or more)
+ * takes a table-driven step with its integer read by one 8-byte load; the rest the full decode. */
 static int zl_entries(emit_t *E, uint64_t at, uint64_t L) {
     const uint8_t *zl = E->b + at;
     if (L < 11 || rd32(zl) != L) return RR_E_ZL_CORRUPT;
-    const uint64_t end_byte = L - 1;
+    const uint64_t end_byte = L - 1, base = E->base + at;
     uint64_t p = 10, prev_size = 0, last = 10, cnt = 0;
-    while (p < end_byte && zl[p] != 0xFF) {
-        uint64_t q;
-        if (zl[p] < 254) {
-            if (zl[p] != prev_size) return RR_E_ZL_CORRUPT;
-            q = p + 1;
-        } else {
-            if (p + 5 > end_byte || rd32(zl + p + 1) != prev_size) return RR_E_ZL_CORRUPT;
-            q = p + 5;
-        }
-        if (q >= end_byte) return RR_E_ZL_CORRUPT;
-        const uint8_t enc = zl[q];
+    while (p < end_byte) {
+        const uint8_t b0 = zl[p], enc = zl[p + 1];
+        if (b0 == 0xFF) break;
         uint64_t e;
-        if (enc < 0xC0) {   /* string: 00pppppp | 01pppppp qqqqqqqq (BE) | 10xxxxxx + u32 BE */
-            uint64_t hdr, sl;
-            const uint8_t cls = enc & 0xC0;
-            if (cls == 0x00) { hdr = 1; sl = enc & 0x3F; }
-            else if (cls == 0x40) {
-                if (q + 2 > end_byte) return RR_E_ZL_CORRUPT;
-                hdr = 2; sl = ((uint64_t)(enc & 0x3F) << 8) | zl[q + 1];
-            } else {
-                if (q + 5 > end_byte) return RR_E_ZL_CORRUPT;
-                hdr = 5;
-                sl = ((uint64_t)zl[q + 1] << 24) | ((uint64_t)zl[q + 2] << 16) | ((uint64_t)zl[q + 3] << 8) | zl[q + 4];
-            }
-            e = q + hdr + sl;
+        if (b0 < 254 && ZL_ESIZE[enc] && p + 9 <= end_byte) {
+            if (b0 != prev_size) return RR_E_ZL_CORRUPT;
+            e = p + 1 + ZL_ESIZE[enc];
             if (e > end_byte) return RR_E_ZL_CORRUPT;
-            put(E, RR_K_STR, E->base + at + q + hdr, (uint32_t)sl, cls);
+            if (enc < 0xC0) put(E, RR_K_STR, base + p + 2, enc & 0x3F, 0);
+            else {
+                const unsigned w = ZL_IW[enc];
+                put(E, RR_K_INT, (uint64_t)(w ? sext(rd64(zl + p + 2), w) : (int64_t)(enc & 0x0F) - 1), 0, enc);
+            }
         } else {
-            int64_t x;
-            const uint8_t *d = zl + q + 1;
-            if (enc >= 0xF1 && enc <= 0xFD) { e = q + 1; x = (int64_t)(enc & 0x0F) - 1; }   /* immediate 0..12 */
-            else if (enc == 0xFE) { e = q + 2; if (e > end_byte) return RR_E_ZL_CORRUPT; x = (int8_t)d[0]; }
-            else if (enc == 0xC0) { e = q + 3; if (e > end_byte) return RR_E_ZL_CORRUPT; int16_t y; memcpy(&y, d, 2); x = y; }
-            else if (enc == 0xF0) {   /* 24-bit: the three bytes as the top of an i32, shifted down (:552-556) */
-                e = q + 4;
+            uint64_t q;
+            if (b0 < 254) {
+                if (b0 != prev_size) return RR_E_ZL_CORRUPT;
+                q = p + 1;
+            } else {
+                if (p + 5 > end_byte || rd32(zl + p + 1) != prev_size) return RR_E_ZL_CORRUPT;
+                q = p + 5;
+            }
+            if (q >= end_byte) return RR_E_ZL_CORRUPT;
+            const uint8_t c = zl[q];
+            if (c < 0xC0) {   /* string: 00pppppp | 01pppppp qqqqqqqq (BE) | 10xxxxxx + u32 BE */
+                uint64_t hdr, sl;
+                const uint8_t cls = c & 0xC0;
+                if (cls == 0x00) { hdr = 1; sl = c & 0x3F; }
+                else if (cls == 0x40) {
+                    if (q + 2 > end_byte) return RR_E_ZL_CORRUPT;
+                    hdr = 2; sl = ((uint64_t)(c & 0x3F) << 8) | zl[q + 1];
+                } else {
+                    if (q + 5 > end_byte) return RR_E_ZL_CORRUPT;
+                    hdr = 5;
+                    sl = ((uint64_t)zl[q + 1] << 24) | ((uint64_t)zl[q + 2] << 16) | ((uint64_t)zl[q + 3] << 8) | zl[q + 4];
+                }
+                e = q + hdr + sl;
                 if (e > end_byte) return RR_E_ZL_CORRUPT;
-                x = (int32_t)(((uint32_t)d[0] << 8) | ((uint32_t)d[1] << 16) | ((uint32_t)d[2] << 24)) >> 8;
-            } else if (enc == 0xD0) { e = q + 5; if (e > end_byte) return RR_E_ZL_CORRUPT; x = (int32_t)rd32(d); }
-            else if (enc == 0xE0) { e = q + 9; if (e > end_byte) return RR_E_ZL_CORRUPT; x = (int64_t)rd64(d); }
-            else return RR_E_ZL_CORRUPT;
-            put(E, RR_K_INT, (uint64_t)x, 0, enc);
+                put(E, RR_K_STR, base + q + hdr, (uint32_t)sl, cls);
+            } else {
+                const unsigned w = ZL_IW[c];
+                if (!ZL_ESIZE[c]) return RR_E_ZL_CORRUPT;   /* (not an integer encoding) */
+                e = q + 1 + w;
+                if (e > end_byte) return RR_E_ZL_CORRUPT;
+                uint64_t raw = 0;
+                memcpy(&raw, zl + q + 1, w);
+                put(E, RR_K_INT, (uint64_t)(w ? sext(raw, w) : (int64_t)(c & 0x0F) - 1), 0, c);
+            }
         }
         cnt++;
         prev_size = e - p;
@@ -245,6 +274,65 @@ static int zl_entries(emit_t *E, uint64_t at, uint64_t L) {
     if (p != end_byte || zl[p] != 0xFF) return RR_E_ZL_CORRUPT;   /* (0xFF early, or no 0xFF at the end) */
     const uint64_t zllen = (uint64_t)zl[8] | ((uint64_t)zl[9] << 8);
     if ((zllen != 0xFFFF && zllen != cnt) || rd32(zl + 4) != last || (cnt & 1)) return RR_E_ZL_CORRUPT;
+    return RR_OK;
+}
+
+/* The verdict of zl_entries without its descriptors (the compat shim's desObject keeps a
+ * ziplist as its raw bytes, rock_serdes.c:356-366, and needs only to know it parses): the same
+ * checks, with the common entry's step reduced to two byte loads, a table load and an add. */
+static int zl_verdict(const uint8_t *zl, uint64_t L, uint64_t *count) {
+    if (L < 11 || rd32(zl) != L) return RR_E_ZL_CORRUPT;
+    const uint64_t end_byte = L - 1;
+    uint64_t p = 10, prev_size = 0, last = 10, cnt = 0;
+    for (;;) {
+        while (p + 9 <= end_byte) {   /* 1-byte prevlen equal to the last size, a table encoding */
+            const uint8_t b0 = zl[p], c = zl[p + 1];
+            uint64_t sz;
+            if (__builtin_expect(c < 0x40, 1)) sz = (uint64_t)c + 1;   /* (a 6-bit string: no table load on the chain) */
+            else sz = ZL_ESIZE[c];
+            if (b0 != prev_size || b0 >= 254 || !sz) break;
+            const uint64_t e = p + 1 + sz;
+            if (e > end_byte) return RR_E_ZL_CORRUPT;
+            cnt++;
+            prev_size = e - p;
+            last = p;
+            p = e;
+        }
+        if (p >= end_byte || zl[p] == 0xFF) break;
+        uint64_t q, e;   /* the full step (as zl_entries) */
+        if (zl[p] < 254) {
+            if (zl[p] != prev_size) return RR_E_ZL_CORRUPT;
+            q = p + 1;
+        } else {
+            if (p + 5 > end_byte || rd32(zl + p + 1) != prev_size) return RR_E_ZL_CORRUPT;
+            q = p + 5;
+        }
+        if (q >= end_byte) return RR_E_ZL_CORRUPT;
+        const uint8_t c = zl[q];
+        if (c < 0xC0) {
+            const uint8_t cls = c & 0xC0;
+            if (cls == 0x00) e = q + 1 + (c & 0x3F);
+            else if (cls == 0x40) {
+                if (q + 2 > end_byte) return RR_E_ZL_CORRUPT;
+                e = q + 2 + (((uint64_t)(c & 0x3F) << 8) | zl[q + 1]);
+            } else {
+                if (q + 5 > end_byte) return RR_E_ZL_CORRUPT;
+                e = q + 5 + (((uint64_t)zl[q + 1] << 24) | ((uint64_t)zl[q + 2] << 16) | ((uint64_t)zl[q + 3] << 8) | zl[q + 4]);
+            }
+        } else {
+            if (!ZL_ESIZE[c]) return RR_E_ZL_CORRUPT;
+            e = q + 1 + ZL_IW[c];
+        }
+        if (e > end_byte) return RR_E_ZL_CORRUPT;
+        cnt++;
+        prev_size = e - p;
+        last = p;
+        p = e;
+    }
+    if (p != end_byte || zl[p] != 0xFF) return RR_E_ZL_CORRUPT;
+    const uint64_t zllen = (uint64_t)zl[8] | ((uint64_t)zl[9] << 8);
+    if ((zllen != 0xFFFF && zllen != cnt) || rd32(zl + 4) != last || (cnt & 1)) return RR_E_ZL_CORRUPT;
+    *count = cnt;
     return RR_OK;
 }
 
@@ -514,6 +602,29 @@ int rr_host_decode_value(const uint8_t *blob, uint64_t len, uint64_t base, rr_va
     uint64_t slots, pay;
     const int st = decode_one(&E, len, v, &slots, &pay);
     if (need) *need = st == RR_OK || st == RR_E_CAPACITY ? slots : 0;
+    return st;
+}
+
+int rr_host_check_value(const uint8_t *blob, uint64_t len, rr_value *v) {
+    if (len >= 13 && (blob[0] == RR_TYPE_HASH_ZIPLIST || blob[0] == RR_TYPE_ZSET_ZIPLIST)) {   /* :356-366, :455-466 */
+        const uint64_t L = rd64(blob + 5);
+        uint64_t cnt = 0;
+        int st = L != len - 13 ? RR_E_ZL_LEN : zl_verdict(blob + 13, L, &cnt);
+        v->type = blob[0];
+        v->enc = 0;
+        v->lru = rd32(blob + 1) & RR_LRU_MASK;
+        v->status = (uint16_t)st;
+        v->n_elems = st == RR_OK ? (uint32_t)(1 + cnt) : 0;
+        return st;
+    }
+    rr_elem local[256];
+    uint64_t need;
+    int st = rr_host_decode_value(blob, len, 0, v, local, 256, &need);
+    if (st == RR_E_CAPACITY) {
+        rr_elem *el = (rr_elem *)malloc(sizeof(rr_elem) * need);
+        st = rr_host_decode_value(blob, len, 0, v, el, need, NULL);
+        free(el);
+    }
     return st;
 }
 

@@ -12,10 +12,12 @@ void *zrealloc(void *ptr, size_t size) { void *p = realloc(ptr, size ? size : 1)
 void zfree(void *ptr) { free(ptr); }
 
 typedef struct { size_t len; } sdshdr_t;
+const char *SDS_NOINIT = "SDS_NOINIT";
 sds sdsnewlen(const void *init, size_t initlen) {
     sdshdr_t *h = zmalloc(sizeof *h + initlen + 1);
     h->len = initlen;
     char *s = (char *)(h + 1);
+    if (init == SDS_NOINIT) init = NULL;
     if (initlen && init) memcpy(s, init, initlen);
     s[initlen] = 0;
     return s;
@@ -141,9 +143,14 @@ robj *createObject(int type, void *ptr) {
     return o;
 }
 robj *createRawStringObject(const char *ptr, size_t len) { return createObject(OBJ_STRING, sdsnewlen(ptr, len)); }
-robj *createEmbeddedStringObject(const char *ptr, size_t len) {
-    robj *o = createObject(OBJ_STRING, sdsnewlen(ptr, len));
-    o->encoding = OBJ_ENCODING_EMBSTR;
+robj *createEmbeddedStringObject(const char *ptr, size_t len) {   /* object.c:84: robj + sds, one allocation */
+    robj *o = zmalloc(sizeof(robj) + sizeof(sdshdr_t) + len + 1);
+    sdshdr_t *h = (sdshdr_t *)(o + 1);
+    char *s = (char *)(h + 1);
+    h->len = len;
+    if (len && ptr && ptr != SDS_NOINIT) memcpy(s, ptr, len);
+    s[len] = 0;
+    o->type = OBJ_STRING; o->encoding = OBJ_ENCODING_EMBSTR; o->ptr = s; o->refcount = 1; o->lru = 0;
     return o;
 }
 robj *createStringObjectFromLongLongForValue(long long value) {
@@ -188,7 +195,7 @@ static void dictFree(dict *d, int keys, int vals) {
 }
 void decrRefCount(robj *o) {
     switch (o->type) {
-    case OBJ_STRING: if (o->encoding != OBJ_ENCODING_INT) sdsfree(o->ptr); break;
+    case OBJ_STRING: if (o->encoding == OBJ_ENCODING_RAW) sdsfree(o->ptr); break;   /* (EMBSTR: inside o) */
     case OBJ_LIST: {
         quicklist *ql = o->ptr;
         for (size_t i = 0; i < ql->n; i++) zfree(ql->e[i].s);

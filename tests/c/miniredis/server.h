@@ -19,6 +19,7 @@
 #include <stdint.h>
 
 typedef char *sds;
+extern const char *SDS_NOINIT;   /* sds.h:37: sdsnewlen leaves the buffer uninitialised */
 sds sdsnewlen(const void *init, size_t initlen);
 size_t sdslen(const sds s);
 void sdsfree(sds s);

@@ -1,21 +1,24 @@
 /*
  * test_compat.c — unit test of the legacy-signature shim (redrock_old_amd/compat/
- * rock_serdes_compat.c) through desObject / desString / serObject and the batch forms,
- * over the golden fixtures (tests/golden/kat.json, K1-K9 + edge cases; written into
- * fixtures.h by tests/test_compat.py).  Links the engine library (the decode / encode run on
- * the GPU) and the minimal Redis model (tests/c/miniredis).
+ * rock_serdes_compat.c) through desObject / desString / serObject and the batch forms, over the
+ * golden fixtures (tests/golden/kat.json, K1-K9 + edge cases + the reference's test shapes;
+ * written into fixtures.h by tests/test_compat.py), linked with the minimal Redis model
+ * (tests/c/miniredis) and the engine library.
  *
- * Every fixture:  status != 0  -> desObject must panic (the reference's serverAssert site);
- *                 status == 0  -> serObject(desObject(b)) must be the blob serObject writes for
- *                                 the object desObject built (the fixture's "reencoded", lru
- *                                 masked to 24 bits), and desString must keep the caller's lru.
- * Then the fork-child route: in-process (rr_compat_test_as_child) and through real forks — a
- * child that decodes every valid fixture through the parent's decode service, a child killed
- * between its request and the reply followed by one that must get its own reply, and a child
- * whose service was shut down, which must panic rather than wait.
+ * Every fixture, on each route:  status != 0 -> desObject must panic (the reference's
+ *                                serverAssert site);
+ *                                status == 0 -> serObject(desObject(b)) must be the blob serObject
+ *                                writes for the object desObject built (the fixture's
+ *                                "reencoded", lru masked to 24 bits), and desString must keep the
+ *                                caller's lru.
+ *   host   (CPU suite)  the host codec route (the default for one value); the batch forms; the
+ *                       fork-child route in-process and through a real fork (the child decodes on
+ *                       its own CPU; forced onto the GPU route it must refuse, not touch HIP).
+ *   gpu    (GPU suite)  the host checks, then the same fixtures through the GPU route: every
+ *                       object equal to the host route's, every blob equal; a fork after the
+ *                       parent used the GPU.
  * Exit status 0 when every check passes.
  */
-#include <signal.h>
 #include <stdio.h>
 #include <string.h>
 #include <sys/wait.h>
@@ -26,10 +29,9 @@
 #include "fixtures.h"
 
 static int fails;
-#define CHECK(c, ...) do { if (!(c)) { fails++; printf("FAIL %s: ", fx->name); printf(__VA_ARGS__); printf("\n"); } } while (0)
+#define CHECK(c, ...) do { if (!(c)) { fails++; printf("FAIL %s: ", fx ? fx->name : "-"); printf(__VA_ARGS__); printf("\n"); } } while (0)
 
-/* Structural equality of two objects of the minimal Redis model (no serObject: a fork child
- * must not touch the GPU the parent's encode would use). */
+/* Structural equality of two objects of the minimal Redis model. */
 static int sds_eq(sds a, sds b) { return sdslen(a) == sdslen(b) && !memcmp(a, b, sdslen(a)); }
 static int dict_eq(dict *a, dict *b, int vals) {
     if (dictSize(a) != dictSize(b)) return 0;
@@ -82,151 +84,157 @@ static int obj_eq(robj *a, robj *b) {
     }
 }
 
-int main(void) {
-    setvbuf(stdout, NULL, _IONBF, 0);   /* (a crash keeps what was printed) */
-    int checked = 0, panics = 0;
-    robj *objs[N_FIXTURES];
-    void *bufs[N_FIXTURES];
-    size_t lens[N_FIXTURES], nok = 0;
-    const fixture_t *okfx[N_FIXTURES];
+static void *bufs[N_FIXTURES];
+static size_t lens[N_FIXTURES], nok;
+static const fixture_t *okfx[N_FIXTURES];
+
+/* every fixture through the one-value signatures on the current route; returns the panics */
+static int one_value_route(const char *route, robj **keep) {
+    int panics = 0;
+    const fixture_t *fx = NULL;
+    nok = 0;
     for (int i = 0; i < N_FIXTURES; i++) {
-        const fixture_t *fx = &FIXTURES[i];
+        fx = &FIXTURES[i];
         jmp_buf jb;
         mr_panic_jmp = &jb;
         robj *volatile o = NULL;
         if (setjmp(jb) == 0) {
             o = desObject((void *)fx->blob, fx->len);
         } else {
-            CHECK(fx->status != 0, "desObject panicked on a valid blob: %s", mr_panic_msg);
+            CHECK(fx->status != 0, "%s: desObject panicked on a valid blob: %s", route, mr_panic_msg);
             if (fx->status) panics++;
             continue;
         }
-        CHECK(fx->status == 0, "desObject accepted a blob the reference rejects (status %d)", fx->status);
+        mr_panic_jmp = NULL;
+        CHECK(fx->status == 0, "%s: desObject accepted a blob the reference rejects (status %d)", route, fx->status);
         if (fx->status) continue;
         sds s = serObject(o);
-        CHECK(sdslen(s) == fx->out_len && !memcmp(s, fx->out, fx->out_len), "serObject(desObject(b)) differs (%zu vs %zu bytes)",
-              sdslen(s), fx->out_len);
+        CHECK(sdslen(s) == fx->out_len && !memcmp(s, fx->out, fx->out_len),
+              "%s: serObject(desObject(b)) differs (%zu vs %zu bytes)", route, sdslen(s), fx->out_len);
         if (fx->blob[0] == 0) {   /* String: desString keeps the caller's lru */
             robj *o2 = desString((char *)fx->blob, fx->len, 77);
-            CHECK(o2->lru == 77 && o2->type == OBJ_STRING && o2->encoding == o->encoding, "desString");
+            CHECK(o2->lru == 77 && o2->type == OBJ_STRING && o2->encoding == o->encoding, "%s: desString", route);
             decrRefCount(o2);
         }
         sdsfree(s);
-        decrRefCount(o);
+        if (keep) keep[nok] = o;
+        else decrRefCount(o);
         bufs[nok] = (void *)fx->blob;
         lens[nok] = fx->len;
         okfx[nok++] = fx;
-        checked++;
     }
-    /* the batch forms: every valid fixture in one decode call and one encode call */
     mr_panic_jmp = NULL;
-    rr_compat_des_batch(bufs, lens, nok, objs);
+    return panics;
+}
+
+/* the batch forms on the current route: every valid fixture in one call each way */
+static void batch_route(const char *route) {
+    robj *objs[N_FIXTURES];
     sds outs[N_FIXTURES];
-    rr_compat_ser_batch(objs, nok, outs);
-    for (size_t i = 0; i < nok; i++) {
-        const fixture_t *fx = okfx[i];
-        CHECK(sdslen(outs[i]) == fx->out_len && !memcmp(outs[i], fx->out, fx->out_len), "batch round trip differs");
-        sdsfree(outs[i]);
-        decrRefCount(objs[i]);
-    }
-    /* a fork child's route (rock.c:538): desObject through the parent's decode service thread
-     * (the process routes as a child; the service decodes on the GPU), then the objects compared
-     * through serObject back in parent mode; the engine itself must refuse child use */
     const fixture_t *fx = NULL;
-    CHECK(rr_compat_service_start() == 0, "decode service start");
-    rr_compat_test_as_child(1);
     rr_compat_des_batch(bufs, lens, nok, objs);
-    int child_panics = 0;
-    for (int i = 0; i < N_FIXTURES; i++) {
-        if (!FIXTURES[i].status) continue;
-        jmp_buf jb;
-        mr_panic_jmp = &jb;
-        if (setjmp(jb) == 0) (void)desObject((void *)FIXTURES[i].blob, FIXTURES[i].len);
-        else child_panics++;
-    }
-    {
-        jmp_buf jb;
-        mr_panic_jmp = &jb;
-        volatile int refused = 0;
-        if (setjmp(jb) == 0) (void)serObject(objs[0]);
-        else refused = strstr(mr_panic_msg, "fork child") != NULL;
-        CHECK(refused, "serObject in a child must refuse the GPU: %s", mr_panic_msg);
-        mr_panic_jmp = NULL;
-    }
-    rr_compat_test_as_child(0);
     rr_compat_ser_batch(objs, nok, outs);
     for (size_t i = 0; i < nok; i++) {
         fx = okfx[i];
-        CHECK(sdslen(outs[i]) == fx->out_len && !memcmp(outs[i], fx->out, fx->out_len), "child-route round trip differs");
+        CHECK(sdslen(outs[i]) == fx->out_len && !memcmp(outs[i], fx->out, fx->out_len), "%s: batch round trip differs", route);
         sdsfree(outs[i]);
         decrRefCount(objs[i]);
     }
-    fx = &FIXTURES[0];
-    CHECK(child_panics == panics, "child route rejected %d malformed blobs, parent %d", child_panics, panics);
+}
 
-    /* a real fork (rock.c:536-538): the parent decodes every valid fixture on its GPU (its engine
-     * context exists), then forks; the child's desObject goes through the parent's decode
-     * service and must build the same objects.  The child leaves with _exit: it never touches
-     * the HIP runtime, not even through exit handlers. */
-    robj *pobj[N_FIXTURES];
-    for (size_t i = 0; i < nok; i++) pobj[i] = desObject(bufs[i], lens[i]);
+/* a real fork (rock.c:536-538) after the parent decoded the valid fixtures (pobj): the child's
+ * desObject (default route) must build the same objects on its own CPU; the child leaves with
+ * _exit (it never touches the HIP runtime, not even through exit handlers) */
+static void forked_child_route(robj **pobj, int parent_used_gpu) {
+    const fixture_t *fx = NULL;
     fflush(stdout);
     const pid_t pid = fork();
     if (pid == 0) {
         int bad = 0;
+        rr_compat_set_route(RR_COMPAT_ROUTE_AUTO);
         for (size_t i = 0; i < nok; i++) {
             robj *o = desObject(bufs[i], lens[i]);
             if (!obj_eq(o, pobj[i])) bad++;
+            sds s = serObject(o);
+            if (sdslen(s) != okfx[i]->out_len || memcmp(s, okfx[i]->out, okfx[i]->out_len)) bad++;
+            sdsfree(s);
             decrRefCount(o);
         }
         _exit(bad ? 1 : 0);
     }
     int wst = -1;
     CHECK(pid > 0 && waitpid(pid, &wst, 0) == pid, "fork / waitpid");
-    CHECK(WIFEXITED(wst) && WEXITSTATUS(wst) == 0, "forked child: decode differs or failed (wait status %d)", wst);
+    CHECK(WIFEXITED(wst) && WEXITSTATUS(wst) == 0, "forked child: decode differs (wait status %d)", wst);
 
-    /* a child killed between its request and the reply (killRDBChild): the next child must get
-     * its own reply, not the dead child's (every fork has its own connection) */
-    const size_t ia = 0, ib = nok - 1;
-    const pid_t pa = fork();
-    if (pa == 0) _exit(rr_compat_test_send_only(bufs[ia], lens[ia]) == 0 ? 0 : 2);
-    CHECK(pa > 0 && waitpid(pa, &wst, 0) == pa && WIFEXITED(wst) && WEXITSTATUS(wst) == 0, "request-only child");
-    const pid_t pb = fork();
-    if (pb == 0) {
-        robj *o = desObject(bufs[ib], lens[ib]);
-        _exit(obj_eq(o, pobj[ib]) ? 0 : 1);
-    }
-    CHECK(pb > 0 && waitpid(pb, &wst, 0) == pb && WIFEXITED(wst) && WEXITSTATUS(wst) == 0,
-          "child after a killed child: wrong object (a stale reply?), status %d", wst);
-
-    /* the parent's service ends while a child is about to call: the child must fail (panic,
-     * exit 3), not wait forever; an alarm turns a hang into a failure */
-    int sync_fd[2];
-    CHECK(pipe(sync_fd) == 0, "pipe");
+    /* forced onto the GPU route, the child of a parent whose HIP runtime is up must refuse (panic,
+     * exit 3) rather than touch it */
+    if (!parent_used_gpu) return;
     const pid_t pc = fork();
     if (pc == 0) {
-        char c;
-        close(sync_fd[1]);
-        signal(SIGPIPE, SIG_IGN);   /* as Redis runs (server.c setupSignalHandlers) */
-        alarm(20);
-        if (read(sync_fd[0], &c, 1) != 1) _exit(4);
+        rr_compat_set_route(RR_COMPAT_ROUTE_GPU);
         jmp_buf jb;
         mr_panic_jmp = &jb;
         if (setjmp(jb) == 0) {
-            (void)desObject(bufs[ia], lens[ia]);
-            _exit(5);   /* decoded through a service that was shut down */
+            (void)desObject(bufs[0], lens[0]);
+            _exit(5);
         }
-        _exit(3);
+        _exit(strstr(mr_panic_msg, "fork child") ? 3 : 4);
     }
-    close(sync_fd[0]);
-    rr_compat_test_drop_services();
-    CHECK(write(sync_fd[1], "x", 1) == 1, "sync write");
-    close(sync_fd[1]);
     CHECK(pc > 0 && waitpid(pc, &wst, 0) == pc && WIFEXITED(wst) && WEXITSTATUS(wst) == 3,
-          "child of a dead service: expected a panic (exit 3), wait status %d", wst);
+          "child forced onto the GPU route: expected a refusal (exit 3), wait status %d", wst);
+}
 
-    for (size_t i = 0; i < nok; i++) decrRefCount(pobj[i]);
-    printf("compat shim: %d fixtures round-tripped, %d rejected with a panic, batch of %zu, child route %zu + %d, "
-           "forked children 4; %d failures\n", checked, panics, nok, nok, child_panics, fails);
+int main(int argc, char **argv) {
+    setvbuf(stdout, NULL, _IONBF, 0);   /* (a crash keeps what was printed) */
+    const int gpu = argc > 1 && !strcmp(argv[1], "gpu");
+    const fixture_t *fx = NULL;
+    robj *hobj[N_FIXTURES];
+
+    /* the host route: one value per call (RedRock's call sites), the batch forms */
+    rr_compat_set_route(RR_COMPAT_ROUTE_HOST);
+    const int panics = one_value_route("host", hobj);
+    const size_t nvalid = nok;
+    batch_route("host");
+
+    /* the fork-child route in-process: desObject on the host, the GPU route refused */
+    rr_compat_test_as_child(1);
+    rr_compat_set_route(RR_COMPAT_ROUTE_AUTO);
+    const int child_panics = one_value_route("child", NULL);
+    CHECK(child_panics == panics && nok == nvalid, "child route rejected %d malformed blobs, parent %d", child_panics,
+          panics);
+    {
+        rr_compat_set_route(RR_COMPAT_ROUTE_GPU);
+        jmp_buf jb;
+        mr_panic_jmp = &jb;
+        volatile int refused = 0;
+        if (setjmp(jb) == 0) (void)desObject(bufs[0], lens[0]);
+        else refused = strstr(mr_panic_msg, "fork child") != NULL;
+        mr_panic_jmp = NULL;
+        CHECK(refused, "the engine must refuse a child: %s", mr_panic_msg);
+        CHECK(rr_compat_in_flight() == 0, "a refused call left %d engine calls in flight", rr_compat_in_flight());
+    }
+    rr_compat_test_as_child(0);
+
+    int gpu_checked = 0;
+    if (gpu) {   /* the GPU route: the same verdicts, the same objects, the same blobs */
+        rr_compat_set_route(RR_COMPAT_ROUTE_GPU);
+        robj *gobj[N_FIXTURES];
+        const int gpanics = one_value_route("gpu", gobj);
+        CHECK(gpanics == panics && nok == nvalid, "gpu route rejected %d malformed blobs, host %d", gpanics, panics);
+        for (size_t i = 0; i < nok; i++) {
+            fx = okfx[i];
+            CHECK(obj_eq(gobj[i], hobj[i]), "gpu route's object differs from the host route's");
+            decrRefCount(gobj[i]);
+            gpu_checked++;
+        }
+        batch_route("gpu");
+        CHECK(rr_compat_in_flight() == 0, "%d engine calls still in flight", rr_compat_in_flight());
+    }
+    fx = NULL;
+    forked_child_route(hobj, gpu);   /* (after the GPU route: the parent's HIP runtime is up) */
+    for (size_t i = 0; i < nvalid; i++) decrRefCount(hobj[i]);
+    printf("compat shim: %zu fixtures round-tripped, %d rejected with a panic (host route, batch, child route)%s%s; "
+           "%d failures\n", nvalid, panics, gpu ? ", gpu route objects equal: " : "", gpu ? (gpu_checked ? "yes" : "no") : "",
+           fails);
     return fails ? 1 : 0;
 }

@@ -61,7 +61,7 @@ def test_library_exports_every_host_symbol():
     function is exported and bound."""
     lib = rr.lib()
     syms = declared_symbols("rr_host.h")
-    assert len(syms) == 6
+    assert len(syms) == 7
     for s in syms:
         assert hasattr(lib, s), f"{s} declared in include/rr_host.h but not exported"
     assert sorted(rr.HOST_EXPORTS) == syms

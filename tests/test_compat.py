@@ -1,9 +1,9 @@
-"""The legacy-signature compat shim (SURVEY.md §8f row f1): redrock_old_amd/compat/
-rock_serdes_compat.c — desObject / desString / serObject (rock_serdes.h:47-49) plus batch
-forms over the engine's C-ABI — compiled as C with a minimal Redis model (tests/c/miniredis)
-into a C test program (tests/c/test_compat.c) that runs every golden fixture through the
-legacy signatures.  CPU: the program compiles and links against the engine library.  GPU:
-it runs (the shim's decode and encode are the GPU engine) and passes."""
+"""The legacy-signature compat shim (SURVEY.md §8b, §8f row f1): redrock_old_amd/compat/
+rock_serdes_compat.c — desObject / desString / serObject (rock_serdes.h:47-55) plus batch forms —
+compiled as C with a minimal Redis model (tests/c/miniredis) into C test programs that run every
+golden fixture through the legacy signatures.  CPU: the host-codec route (RedRock's per-key calls,
+a fork child's calls) end to end.  GPU: the same fixtures through the GPU route, equal objects and
+blobs, and the process exit with foreign threads inside the engine (tests/c/test_compat_exit.c)."""
 import json
 import os
 import struct
@@ -47,14 +47,14 @@ def write_fixtures(path):
         fh.write("\n".join(lines) + "\n")
 
 
-def build(tmp):
+def build(tmp, prog="test_compat"):
     write_fixtures(os.path.join(tmp, "fixtures.h"))
-    exe = os.path.join(tmp, "test_compat")
+    exe = os.path.join(tmp, prog)
     cmd = ["gcc", "-std=gnu11", "-O1", "-Wall", "-Werror", "-Wno-unused-function", "-DRR_REDIS_TREE",
            "-I", os.path.join(ROOT, "tests", "c", "miniredis"), "-I", os.path.join(ROOT, "include"), "-I", tmp,
            os.path.join(ROOT, "redrock_old_amd", "compat", "rock_serdes_compat.c"),
            os.path.join(ROOT, "tests", "c", "miniredis", "miniredis.c"),
-           os.path.join(ROOT, "tests", "c", "test_compat.c"),
+           os.path.join(ROOT, "tests", "c", prog + ".c"),
            "-L", os.path.join(ROOT, "redrock_old_amd"), "-lrr_serdes", "-lpthread",
            "-Wl,-rpath," + os.path.join(ROOT, "redrock_old_amd"), "-o", exe]
     subprocess.run(cmd, check=True)
@@ -103,13 +103,44 @@ def test_rock_c_call_set_runs_on_gpu(tmp_path):
     assert "0 failures" in r.stdout
 
 
-@pytest.mark.gpu
-def test_compat_shim_round_trips_fixtures_on_gpu(tmp_path):
+def test_compat_shim_host_route_cpu(tmp_path):
+    """RedRock's per-key calls through the shim with no GPU: every golden fixture through
+    desObject / desString / serObject on the host codec (the verdicts, the objects, the bytes
+    serObject writes), the batch forms, the fork-child route in-process and through real forks
+    (a child forced onto the GPU route refuses instead of touching HIP)."""
     exe = build(str(tmp_path))
-    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    r = subprocess.run([exe, "host"], capture_output=True, text=True, timeout=120)
     print(r.stdout, r.stderr)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "0 failures" in r.stdout
+
+
+@pytest.mark.gpu
+def test_compat_shim_round_trips_fixtures_on_gpu(tmp_path):
+    """The host-route checks, then every fixture through the GPU route: the same verdicts, objects
+    equal to the host route's, the same blobs; a fork after the parent used the GPU."""
+    exe = build(str(tmp_path))
+    r = subprocess.run([exe, "gpu"], capture_output=True, text=True, timeout=120)
+    print(r.stdout, r.stderr)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "0 failures" in r.stdout and "objects equal: yes" in r.stdout
+
+
+def test_compat_exit_program_builds(tmp_path):
+    assert os.path.exists(build(str(tmp_path), "test_compat_exit"))
+
+
+@pytest.mark.gpu
+def test_compat_exit_with_foreign_threads_in_engine(tmp_path):
+    """exit() while one thread's context teardown is held inside the engine
+    (test hook, 400 ms) and another thread loops desObject on the GPU route, as RedRock's
+    never-joined rock thread does (rock.c:615, :552-596).  The shim's exit handler waits for the
+    calls in flight and parks later callers before the HIP runtime's teardown: exit status 0."""
+    exe = build(str(tmp_path), "test_compat_exit")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=60)
+    print(r.stdout, r.stderr)
+    assert r.returncode == 0, (r.returncode, r.stdout + r.stderr)
+    assert "thread A's teardown held" in r.stdout
 
 
 # ---- row f4: batched snapshot restore over the fork-child pipes (include/rr_rdb.h) --------

@@ -21,6 +21,13 @@ def _same_decode(data, offs, what, elem_cap=None):
     v, e, a, t = rr.host_decode(data, offs, elem_cap)
     ov, oe, oa, ot = cpu.decode(data, offs, elem_cap)
     assert_flat_equal((v, e), (ov, oe), what)
+    # rr_host_check_value (the shim's verdict-only walk of ziplists): the same records, CAPACITY
+    # aside (it has no elem_cap), elem_base 0
+    c = rr.host_check(data, offs)
+    want = ov.copy()
+    want["elem_base"] = 0
+    cut = want["status"] == 11
+    assert np.array_equal(c[~cut], want[~cut]), what
     assert t == ot, (what, t, ot)
     assert np.array_equal(a, oa)
     return v, e, a, t
