@@ -227,13 +227,15 @@ def test_latency_bench_builds(tmp_path):
 
 @pytest.mark.gpu
 def test_per_value_latency_path(tmp_path):
-    """The unchanged per-value callers' path: every desObject / serObject of 300 config-4
-    values goes through the one-launch kernels and round-trips (the bench checks every blob)."""
+    """The unchanged per-value callers' path: every desObject / serObject of 300 config-4 values
+    on the default route (the host codec) and forced onto the GPU route (the one-launch kernels)
+    round-trips (the bench checks every blob)."""
     r = subprocess.run([build_latency(str(tmp_path)), "4", "300"], capture_output=True, text=True, timeout=120)
     print(r.stdout, r.stderr)
     assert r.returncode == 0, r.stdout + r.stderr
     line = json.loads(r.stdout.strip().splitlines()[-1])
-    assert line["roundtrip_bad"] == 0
+    assert line["roundtrip_bad"] == 0 and line["gpu"]
+    assert line["shim_gpu_route_desObject_us"]["median"] > 0 and line["shim_desObject_us"]["median"] > 0
 
 
 if __name__ == "__main__":   # python tests/test_compat.py bench [config k] | latency [config k] | callpattern [config]  (GPU box)
