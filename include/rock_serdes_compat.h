@@ -58,8 +58,9 @@ void _test_ser_des_hash(void);
 void _test_ser_des_zset(void);
 
 /* Routing of desObject / serObject and the batch forms: AUTO (the default) = the host codec
- * below RR_COMPAT_GPU_MIN values per call (environment; a measured default), the GPU at or above
- * it; HOST / GPU force one route (tests, benches).  A fork child (rock.c:527-550) never takes the
+ * below the measured crossover (values per call: RR_COMPAT_GPU_MIN_SER, default 16384, for the
+ * encode; RR_COMPAT_GPU_MIN_DES, default 0 = never, for the decode; environment), the GPU at or
+ * above it; HOST / GPU force one route (tests, benches).  A fork child (rock.c:527-550) never takes the
  * GPU route: under AUTO or HOST it decodes on its own CPU, under GPU the engine panics rather than
  * touch the parent's HIP runtime. */
 #define RR_COMPAT_ROUTE_AUTO 0

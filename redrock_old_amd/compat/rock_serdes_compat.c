@@ -48,33 +48,46 @@ void rr_compat_set_device(int device) { g_device = device; }
 
 /* ---------------------------------------------------------------- routing */
 
-/* The crossover (values per call) from which a batch form goes to the GPU.  Measured with
- * tests/c/bench_callpattern.c (profiles/r6_callpattern_cfg4.json): the robj a call builds or
- * walks cost the same on either route, so the GPU route pays only for very large batches.
- * RR_COMPAT_GPU_MIN overrides it (values; 0 = never). */
-#define RR_COMPAT_GPU_MIN_DEFAULT 65536
+/* The crossovers (values per call) from which a batch form goes to the GPU, measured with
+ * tests/c/bench_callpattern.c on the GPU box (profiles/r6_callpattern_cfg4.json): the robj a call
+ * builds or walks cost the same on either route, and a GPU call adds a launch, the staging copies
+ * and the PCIe round trip.  Serialize: the GPU route is 7-10 % faster from 16,384 values.
+ * Deserialize: the host route is as fast or faster at every k measured (1 to 65,536), so it
+ * never goes to the GPU by default.  RR_COMPAT_GPU_MIN_SER / RR_COMPAT_GPU_MIN_DES override them
+ * (values; 0 = never). */
+#define RR_COMPAT_GPU_MIN_SER_DEFAULT 16384
+#define RR_COMPAT_GPU_MIN_DES_DEFAULT 0
 static int g_route = RR_COMPAT_ROUTE_AUTO;
-static uint64_t g_gpu_min;
+static uint64_t g_gpu_min_ser, g_gpu_min_des;
 static pthread_once_t g_cfg_once = PTHREAD_ONCE_INIT;
 
 static void read_config(void) {
-    const char *s = getenv("RR_COMPAT_GPU_MIN");
-    g_gpu_min = s ? strtoull(s, NULL, 10) : RR_COMPAT_GPU_MIN_DEFAULT;
+    const char *s = getenv("RR_COMPAT_GPU_MIN_SER"), *d = getenv("RR_COMPAT_GPU_MIN_DES");
+    g_gpu_min_ser = s ? strtoull(s, NULL, 10) : RR_COMPAT_GPU_MIN_SER_DEFAULT;
+    g_gpu_min_des = d ? strtoull(d, NULL, 10) : RR_COMPAT_GPU_MIN_DES_DEFAULT;
 }
 
 void rr_compat_set_route(int route) { g_route = route; }
 
-static pid_t g_owner;   /* the process whose threads own GPU contexts */
-static int g_as_child;  /* test hook: route this process as a fork child would */
+static pid_t g_owner;    /* the process whose threads own GPU contexts */
+static int g_forked;     /* this process is a fork child of an owner (its HIP runtime is the parent's) */
+static int g_as_child;   /* test hook: route this process as a fork child would */
 
-static int in_child(void) { return g_as_child || (g_owner && getpid() != g_owner); }
+/* (set in the child by pthread_atfork: no getpid() system call per desObject) */
+static void atfork_child(void) {
+    if (g_owner) g_forked = 1;
+}
+__attribute__((constructor)) static void compat_atfork_register(void) { pthread_atfork(NULL, NULL, atfork_child); }
 
-/* n values through the GPU entry points? */
-static int use_gpu(size_t n) {
+static int in_child(void) { return g_as_child || g_forked; }
+
+/* n values (encode: ser = 1) through the GPU entry points? */
+static int use_gpu(size_t n, int ser) {
     if (in_child()) return g_route == RR_COMPAT_ROUTE_GPU;   /* (the engine then refuses, below) */
     if (g_route != RR_COMPAT_ROUTE_AUTO) return g_route == RR_COMPAT_ROUTE_GPU;
     pthread_once(&g_cfg_once, read_config);
-    return g_gpu_min && n >= g_gpu_min;
+    const uint64_t min = ser ? g_gpu_min_ser : g_gpu_min_des;
+    return min && n >= min;
 }
 
 void rr_compat_test_as_child(int on) { g_as_child = on; }
@@ -111,7 +124,7 @@ static void engine_leave(void) {
  * stuck longer than that is a hung device, and the exit goes on).  exit_hook registers this once
  * the runtime is up, so it runs before every exit handler the runtime registered. */
 static void compat_exit(void) {
-    if (g_owner && getpid() != g_owner) return;   /* (a fork child has no engine calls) */
+    if (g_forked) return;   /* (a fork child has no engine calls) */
     g_closer = pthread_self();
     __atomic_store_n(&g_closing, 1, __ATOMIC_SEQ_CST);
     const struct timespec ms = {0, 1000000};
@@ -334,7 +347,7 @@ static void des_batch_gpu(void *const *bufs, const size_t *lens, size_t n, robj 
 
 void rr_compat_des_batch(void *const *bufs, const size_t *lens, size_t n, robj **out) {
     if (n == 0) return;
-    if (use_gpu(n)) { des_batch_gpu(bufs, lens, n, out); return; }
+    if (use_gpu(n, 0)) { des_batch_gpu(bufs, lens, n, out); return; }
     for (size_t i = 0; i < n; i++) out[i] = des_host(bufs[i], lens[i]);
 }
 
@@ -357,7 +370,7 @@ void rr_compat_rdb_load_batch(int fd_req, int fd_resp, int dbid, sds *keys, size
 }
 
 robj *desObject(void *buf, size_t len) {
-    if (use_gpu(1)) {
+    if (use_gpu(1, 0)) {
         robj *o = NULL;
         des_batch_gpu(&buf, &len, 1, &o);
         return o;
@@ -579,12 +592,12 @@ static void ser_batch_gpu(robj *const *objs, size_t n, sds *out) {
 
 void rr_compat_ser_batch(robj *const *objs, size_t n, sds *out) {
     if (n == 0) return;
-    if (use_gpu(n)) { ser_batch_gpu(objs, n, out); return; }
+    if (use_gpu(n, 1)) { ser_batch_gpu(objs, n, out); return; }
     for (size_t i = 0; i < n; i++) out[i] = ser_host(objs[i]);
 }
 
 sds serObject(robj *o) {
-    if (use_gpu(1)) {
+    if (use_gpu(1, 1)) {
         sds s = NULL;
         ser_batch_gpu(&o, 1, &s);
         return s;
