@@ -19,8 +19,9 @@
  *     device entry points (graph-capturable after rr_ctx_reserve: decode = 2 kernels,
  *     encode = 3 kernels, a batch of at most 4096 values in at most 128 KiB = ONE kernel; all
  *     on the caller's stream).  The only wait is when the context's scratch must grow: it
- *     waits for the context's previous call to finish (an event, not a device sync) — and
- *     under graph capture it fails instead.
+ *     waits for the whole device (hipDeviceSynchronize: other streams' and contexts' work too)
+ *     before freeing the old buffer — rr_ctx_reserve sizes it up front so a hot path never
+ *     grows — and under graph capture it fails instead.
  * Plain C: no HIP or torch types in any signature.  Streams are passed as void* (hipStream_t).
  */
 #ifndef RR_SERDES_H

@@ -90,7 +90,8 @@ void rr_ctx_destroy(rr_ctx *c) {
 
 /* Grow the scratch.  Kernels of earlier calls — on whatever stream, or replays of a captured
  * graph — may still be using the old buffer: growing (rare: rr_ctx_reserve sizes it up front)
- * waits for the device.  (Round 4 recorded an event after every call for this wait: one HIP call
+ * waits for the whole device (hipDeviceSynchronize: every stream on it, other contexts', torch's
+ * and RCCL's work included — rr_ctx_reserve is the way to never pay it on a hot path).  (Round 4 recorded an event after every call for this wait: one HIP call
  * more per call, on the path small batches are bound by.)  Growing allocates, which a stream
  * under graph capture cannot do: size the scratch with rr_ctx_reserve before capturing. */
 int rr_ensure_scratch(rr_ctx *c, uint64_t words, hipStream_t stream) {
@@ -126,7 +127,12 @@ static int is_capturing(hipStream_t stream) {
 }
 static int ensure_dsums(rr_ctx *c, uint64_t dec_words, uint64_t enc_words, hipStream_t stream) {
     if (c->dsums && dec_words <= c->dsums_dec && enc_words <= c->dsums_enc) {
-        if (c->dsums_dirty && !is_capturing(stream)) {
+        /* a failed call left sums non-zero: a captured call would bake them into its graph (its
+         * first replay's offsets wrong), so it is refused until an uncaptured call re-zeroes them
+         *  */
+        if (c->dsums_dirty && is_capturing(stream))
+            return fail(RR_API_EINVAL, "a failed call left the context's sums dirty: make one call outside the capture first");
+        if (c->dsums_dirty) {
             HIPCHK(hipMemsetAsync(c->dsums, 0, (c->dsums_enc + 3 * c->dsums_dec) * sizeof(uint64_t), stream));
             c->dsums_dirty = 0;
             c->dext[0] = c->dext[1] = 0;
@@ -203,8 +209,8 @@ int rr_decode_batch(rr_ctx *c, const rr_blob_batch *in, rr_flat_batch *out, rr_t
     if (!aligned16(in->data) || !aligned16(out->arena)) return fail(RR_API_EINVAL, "data/arena not 16-byte aligned");
     if (in->data_cap & 15) return fail(RR_API_EINVAL, "data_cap must be a multiple of 16");
     if (out->arena_cap < in->data_cap) return fail(RR_API_EINVAL, "arena_cap < data_cap");
+    HIPCHK(hipSetDevice(c->device));   /* (the launch helpers' per-device facts: this context's device) */
     if (SMALL_DEC(c, in->n, in->data_cap)) {   /* one launch, no scratch */
-        HIPCHK(hipSetDevice(c->device));
         HIPCHK(rr_launch_decode_small(in->data, in->offsets, in->n, out->values, out->elems, out->elem_cap, out->arena,
                                       in->data_cap, d_totals, NULL, 0, (hipStream_t)stream));
         return RR_API_OK;
@@ -250,8 +256,8 @@ int rr_encode_batch(rr_ctx *c, const rr_flat_batch *in, rr_blob_batch *out, rr_t
     if (!out->offsets) return fail(RR_API_EINVAL, "NULL offsets");
     if (in->n && (!in->values || !out->data)) return fail(RR_API_EINVAL, "NULL buffer");
     if ((uintptr_t)out->data & 15) return fail(RR_API_EINVAL, "out->data must be 16-byte aligned");
+    HIPCHK(hipSetDevice(c->device));
     if (SMALL_ENC(c, in->n, out->data_cap)) {   /* one launch, no scratch */
-        HIPCHK(hipSetDevice(c->device));
         HIPCHK(rr_launch_encode_small(in->values, in->elems, in->elem_cap, in->arena, in->arena_cap, in->n, out->data,
                                       out->data_cap, out->offsets, d_totals, NULL, 0, (hipStream_t)stream));
         return RR_API_OK;

@@ -330,6 +330,9 @@ __device__ __forceinline__ void fold_totals(const uint64_t *__restrict__ stats, 
 //                     (heaviest class first) walked from the stage by the waves; the window's
 //                     marked values fixed at its end, its totals added atomically.
 
+#ifndef RR_ABLATE   // timing-only ablations (tools/, wrong results; the decode's 1-4 below): count_kernel 5 no
+#define RR_ABLATE 0       // List stage or walk, 6 the stage lands but no walk
+#endif
 // ---- K1: reservation + class per value ------------------------------------------------
 // reserve(i) = the descriptor slots value i owns (rr_format.h): header fields only, plus the
 // length chain of a List.  Equal to the decoded count for every valid blob.
@@ -568,6 +571,10 @@ __global__ __launch_bounds__(CNT_NT) void count_kernel(const uint8_t *__restrict
     // global load per element made the wave's longest List its critical path).  A List longer
     // than the stage walks from global memory.
     const uint32_t lane = lane_id(), wave = tid / RR_WAVE;
+#if RR_ABLATE == 5   // timing only (wrong results): no List staging, no walk
+    if (i < n && c == C_LIST) r = (b1 - o_hi) >> 4;
+    if (0)
+#endif
     {
         const uint64_t L = b1 - o_hi, s0 = (o_hi + 5) & ~15ull;
         const bool lst = i < n && c == C_LIST && L > 5;
@@ -592,6 +599,10 @@ __global__ __launch_bounds__(CNT_NT) void count_kernel(const uint8_t *__restrict
                                                          16, 0, 0);
             }
             __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the pack has landed (this wave's own stage)
+#if RR_ABLATE == 6   // timing only (wrong results): the stage lands, no walk
+            if (inpack) r = L >> 4 | (lstage[wave][16 * ex] & 1);
+            else
+#endif
             if (inpack)
                 r = list_count_lds((uint32_t)(uintptr_t)(lds_cptr)(lstage[wave] + 16 * ex + ((o_hi + 5) & 15)) - 5u, (uint32_t)L);
             todo &= ~pack;
@@ -1084,9 +1095,6 @@ extern "C" int rr_probe_set(void *p) { return hipMemcpyToSymbol(HIP_SYMBOL(g_pro
 #endif
 // Timing-only ablations (tools/, wrong results): -DRR_ABLATE=1 copy + stage only, 2 + the class
 // sort (no batches), 3 no arena copy, 4 no descriptor stores (rr_decode_class.h).
-#ifndef RR_ABLATE
-#define RR_ABLATE 0
-#endif
 
 // Window granules (16 B) per thread loaded before the first_val -> offsets / class-byte loads
 // (the rest after the class bytes): measured 8 before 6 % slower, none before 2 % slower.
@@ -1136,6 +1144,10 @@ __global__ __launch_bounds__(NW * RR_WAVE) __attribute__((amdgpu_waves_per_eu(DE
           const uint64_t prt0 = __builtin_amdgcn_s_memrealtime();
           if (threadIdx.x < PROBE_WORDS) prb[threadIdx.x] = 0;)
     const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid / RR_WAVE;
+    // (A persistent form — the resident grid walking windows b, b + grid, ..., no workgroup
+    // teardown and dispatch between a CU slot's windows, ~1.6 us of idle slot each — costs 61
+    // spilled VGPRs at the 128 cap, a 2-window unrolled form 57: decode_kernel 285 -> 366 us,
+    // round 6, profiles/r6_decode_persist_ab.txt.)
     const uint32_t tile = blockIdx.x;
     if (tid == 0) nfix = 0;   // (ordered before the batches by the sort's first barrier)
     // 0. the loads of the window's first slot go out first (reduced under the sort)
@@ -2896,9 +2908,33 @@ static uint64_t scan_tiles(uint64_t n) { return (n + SCAN_TILE - 1) / SCAN_TILE;
 // windows instead of 13.2 of 72 KiB), and a small batch spreads over every CU instead of a
 // few full windows (config 1 at 100K values: 512 windows of 13.7 KiB instead of 98).
 constexpr uint64_t DEC_WMIN = 1024;
+// Per-device launch facts: the calling thread's current device, which every entry
+// point of rr_api.c sets to its context's device first; one slot per device id, filled by
+// whichever thread gets there first (racing threads store the same value)
+constexpr int RR_MAX_DEV = 64;
+static uint32_t dev_cache(uint32_t (&cache)[RR_MAX_DEV], uint32_t (*query)(void)) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    uint32_t *slot = &cache[(uint32_t)dev % RR_MAX_DEV];
+    uint32_t v = __atomic_load_n(slot, __ATOMIC_RELAXED);
+    if (!v) {
+        v = query();
+        __atomic_store_n(slot, v, __ATOMIC_RELAXED);
+    }
+    return v;
+}
+static uint32_t q_dec_slots(void) { return resident_grid(DECODE_KERNEL, DEC_NW * RR_WAVE, false); }
+static uint32_t q_cus(void) {
+    int dev = 0, c = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
+    return c > 0 ? (uint32_t)c : 1u;
+}
+static uint32_t g_dec_slots[RR_MAX_DEV], g_cus[RR_MAX_DEV];
+static uint32_t dec_slots(void) { return dev_cache(g_dec_slots, q_dec_slots); }
+static uint32_t dev_cus(void) { return dev_cache(g_cus, q_cus); }
 static uint32_t dec_win(uint64_t data_cap) {
-    static uint64_t slots = 0;
-    if (!slots) slots = resident_grid(DECODE_KERNEL, DEC_NW * RR_WAVE, false);
+    const uint64_t slots = dec_slots();
     const uint64_t per_gen = slots * DEC_W, gens = (data_cap + per_gen - 1) / per_gen;
     uint64_t w = gens ? (data_cap + gens * slots - 1) / (gens * slots) : DEC_WMIN;
     w = (w + 15) & ~15ull;
@@ -2935,13 +2971,7 @@ extern "C" hipError_t rr_launch_decode(const uint8_t *blob, const uint64_t *offs
     // 30K values -16 % / -10 %; at 200K config-1 values (781 a window) two per CU stay faster
     // (profiles/r5_small_windows_ab.txt).  Fewer windows than dec_windows(data_cap): the scratch
     // and the sums sized from data_cap still cover them.
-    static uint64_t cus = 0;
-    if (!cus) {
-        int dev = 0, c = 0;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
-        cus = c > 0 ? (uint64_t)c : 1;
-    }
+    const uint64_t cus = dev_cus();
     if (data_cap <= cus * DEC_W && n <= cus * DEC_NW * RR_WAVE) {
         uint64_t w = ((data_cap + cus - 1) / cus + 15) & ~15ull;
         w = w < DEC_WMIN ? DEC_WMIN : w;

@@ -20,6 +20,8 @@ VARIANTS = [
     ("rr_kernels.hip", "-DRR_ABLATE=2"),
     ("rr_kernels.hip", "-DRR_ABLATE=3"),
     ("rr_kernels.hip", "-DRR_ABLATE=4"),
+    ("rr_kernels.hip", "-DRR_ABLATE=5"),
+    ("rr_kernels.hip", "-DRR_ABLATE=6"),
     ("rr_kernels.hip", "-DRR_DEC_W=65536"),
     ("rr_kernels.hip", "-DRR_DEC_SLACK=8192"),
     ("rr_kernels.hip", "-DRR_DEC_NW=4"),

@@ -276,9 +276,10 @@ def test_handoff_under_uneven_load(engine_small):
         s.synchronize()
         load.close()
     assert checked == 6 * len(cases)
+    # (how many calls returned while the load was still queued depends on host launch speed
+    # against the GPU's drain rate, not on correctness: reported, not asserted — ADVICE r5)
     print(f"decode calls beside the load: median {1e6 * sorted(lat)[len(lat) // 2]:.1f} us, max {1e6 * max(lat):.1f} us; "
           f"{busy} of {checked} returned while the load was still queued")
-    assert busy >= checked // 2, f"only {busy} of {checked} calls ran beside a loaded GPU"
 
 
 def test_failed_second_launch_resets_sums(engine):

@@ -8,6 +8,6 @@ while [ $# -ge 2 ]; do
   mkdir -p ../../build/var_$name
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 $flags -c rr_kernels.hip -o ../../build/var_$name/k.o
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 $flags -c rr_snappy.hip -o ../../build/var_$name/s.o
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../librr_serdes_$name.so ../../build/var_$name/k.o ../../build/var_$name/s.o ../../build/csrc/rr_api.o ../../build/csrc/rr_shard.o ../../build/csrc/rr_snappy_api.o ../../build/csrc/rr_rdb.o ../../build/csrc/rr_kv.o ../../build/csrc/rr_gen.o -L/opt/rocm/lib -lrccl -lm
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../librr_serdes_$name.so ../../build/var_$name/k.o ../../build/var_$name/s.o ../../build/csrc/rr_api.o ../../build/csrc/rr_shard.o ../../build/csrc/rr_snappy_api.o ../../build/csrc/rr_rdb.o ../../build/csrc/rr_kv.o ../../build/csrc/rr_gen.o ../../build/csrc/rr_host.o -L/opt/rocm/lib -lrccl -lm
   echo built librr_serdes_$name.so
 done
