@@ -663,6 +663,56 @@ struct Out {
     }
 };
 
+// The compressor's hash table (CompressFragment's `table`, snappy.cc:468-486): ts u16 entries,
+// all zero at the fragment's start, table[h] = the last position stored under hash h.
+// RR_SNZ_SPARSE = 0: that dense array, 2 * ts bytes of LDS (32 KiB for a 16 KiB block: 5 waves per
+// CU).  Otherwise the same map as an open-addressing table of RR_SNZ_SPARSE u32 entries
+// ((h + 1) << 16 | position, 0 empty; linear probing from h's low bits): a fragment stores only as
+// many hashes as its probes touch — a few hundred for an incompressible 16 KiB block — so 16 KiB
+// of LDS holds it and a CU runs twice the waves.  Lookups return what the dense array would
+// (0 for a hash never stored); a fragment that would fill more than 3/4 of the entries is
+// abandoned (its block goes to a second pass with the dense array), so every output byte is the
+// dense compressor's.
+#ifndef RR_SNZ_SPARSE
+#define RR_SNZ_SPARSE 4096
+#endif
+constexpr uint32_t SPT = RR_SNZ_SPARSE, SPT_LIMIT = SPT - SPT / 4;
+template <bool SPARSE>
+struct HTab {
+    lds_u16 *d;   // dense
+    lds_u32 *t;   // sparse
+    __device__ __forceinline__ uint32_t get(uint32_t h) const {
+        if (!SPARSE) return d[h];
+        uint32_t i = h & (SPT - 1);
+        const uint32_t key = h + 1;
+        for (;;) {
+            const uint32_t e = t[i];
+            if (e == 0) return 0u;
+            if ((e >> 16) == key) return e & 0xFFFFu;
+            i = (i + 1) & (SPT - 1);
+        }
+    }
+    // table[h] = pos; 1 when this claimed an empty entry.  Lanes storing together hold distinct
+    // hashes (the round's last writer of each), or all the same (the uniform steps)
+    __device__ __forceinline__ uint32_t put(uint32_t h, uint32_t pos) {
+        if (!SPARSE) { d[h] = (uint16_t)pos; return 0u; }
+        const uint32_t key = h + 1, nv = (key << 16) | pos;
+        uint32_t i = h & (SPT - 1);
+        for (;;) {
+            const uint32_t e = t[i];
+            if (e == 0) {
+                uint32_t exp = 0;
+                if (__atomic_compare_exchange_n(&t[i], &exp, nv, false, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) return 1u;
+                if ((exp >> 16) == key) { t[i] = nv; return 0u; }   // (a lane of the same store got there first)
+            } else if ((e >> 16) == key) {
+                t[i] = nv;
+                return 0u;
+            }
+            i = (i + 1) & (SPT - 1);
+        }
+    }
+};
+
 // FindMatchLength: bytes equal at a + i and b + i, for b + i < lim; 64 lanes a step
 __device__ __forceinline__ uint32_t match_len(const Frag &F, uint32_t a, uint32_t b, uint32_t lim) {
     const uint32_t l = lane_id();
@@ -677,9 +727,14 @@ __device__ __forceinline__ uint32_t match_len(const Frag &F, uint32_t a, uint32_
 #ifndef RR_SNZ_K   // most probes a compressor step-1 round evaluates at once (1: the serial loop)
 #define RR_SNZ_K 16
 #endif
-__device__ void compress_fragment(const Frag &F, uint32_t fn, lds_u16 *table, uint32_t ts, Out &O) {
+template <bool SPARSE>
+__device__ bool compress_fragment(const Frag &F, uint32_t fn, HTab<SPARSE> table, uint32_t ts, Out &O) {
     const uint32_t shift = 32 - log2floor(ts);
-    uint32_t ip = 0, next_emit = 0;
+    uint32_t ip = 0, next_emit = 0, used = 0;   // used: sparse entries claimed
+    auto claimed = [&](uint32_t c) __attribute__((always_inline)) {
+        if (SPARSE) used += (uint32_t)__popcll(__ballot(c != 0));
+        return SPARSE && used > SPT_LIMIT;
+    };
     if (fn >= MARGIN) {
         const uint32_t ip_limit = fn - MARGIN;
         uint32_t next_hash = hash32(F.ld32(++ip), shift);
@@ -735,7 +790,7 @@ __device__ void compress_fragment(const Frag &F, uint32_t fn, lds_u16 *table, ui
                     }
 #endif
                     const uint32_t Pp = (uint32_t)__shfl((int)P, prev < 0 ? (int)lane : prev, WAVE);
-                    const uint32_t c = prev >= 0 ? Pp : (uint32_t)table[act ? H : 0];
+                    const uint32_t c = prev >= 0 ? Pp : table.get(act ? H : 0);
                     const bool m = valid && x == F.ld32(c);
                     const uint64_t stop = __ballot(act && (!valid || m));
                     const uint32_t sl = stop ? (uint32_t)__builtin_ctzll(stop) : K;
@@ -749,7 +804,9 @@ __device__ void compress_fragment(const Frag &F, uint32_t fn, lds_u16 *table, ui
                     // the compressor at 4 waves per CU: 29.9 -> 30.5 GB/s on config 4.)
                     const bool tell = commit && prev >= 0;
                     const int over = __builtin_amdgcn_ds_permute((tell ? prev : (int)WAVE - 1) * 4, tell ? 1 : 0);
-                    if (commit && !over) table[H] = (uint16_t)P;
+                    uint32_t cl = 0;
+                    if (commit && !over) cl = table.put(H, P);
+                    if (claimed(cl)) return false;
                     if (sl < K) {
                         if (!hit) goto remainder;
                         ip = rdl(P, sl);
@@ -771,8 +828,8 @@ __device__ void compress_fragment(const Frag &F, uint32_t fn, lds_u16 *table, ui
                 next_ip = ip + between;
                 if (next_ip > ip_limit) goto remainder;
                 next_hash = hash32(F.ld32(next_ip), shift);
-                cand = table[h];
-                table[h] = (uint16_t)ip;
+                cand = table.get(h);
+                if (claimed(table.put(h, ip))) return false;
                 if (F.ld32(ip) == F.ld32(cand)) break;
             }
 #endif
@@ -786,12 +843,12 @@ __device__ void compress_fragment(const Frag &F, uint32_t fn, lds_u16 *table, ui
                 next_emit = ip;
                 if (ip >= ip_limit) goto remainder;
                 const uint32_t prev = F.ld32(ip - 1);
-                table[hash32(prev, shift)] = (uint16_t)(ip - 1);
+                if (claimed(table.put(hash32(prev, shift), ip - 1))) return false;
                 cur = F.ld32(ip);
                 const uint32_t ch = hash32(cur, shift);
-                cand = table[ch];
+                cand = table.get(ch);
                 cbytes = F.ld32(cand);
-                table[ch] = (uint16_t)ip;
+                if (claimed(table.put(ch, ip))) return false;
             } while (cur == cbytes);
             next_hash = hash32(F.ld32(ip + 1), shift);
             ++ip;
@@ -799,18 +856,25 @@ __device__ void compress_fragment(const Frag &F, uint32_t fn, lds_u16 *table, ui
     }
 remainder:
     if (next_emit < fn) O.literal(F, next_emit, fn - next_emit);
+    return true;
 }
 
+// SPARSE: the first pass (sparse tables; a block whose fragment overflows its table gets size
+// RR_SNZ_REDO); !SPARSE after it: the dense pass over the blocks marked RR_SNZ_REDO only
+// (SPT == 0: the dense pass over every block, the one pass)
+constexpr uint64_t RR_SNZ_REDO = ~0ull;
+template <bool SPARSE>
 __global__ __launch_bounds__(WAVE) void snz_comp_kernel(const uint8_t *__restrict__ in, uint64_t in_cap,
                                                         const uint64_t *__restrict__ in_offs, uint64_t n,
                                                         uint8_t *__restrict__ slots,
                                                         const uint64_t *__restrict__ slot_offs,
                                                         uint64_t *__restrict__ sizes, uint32_t fcap) {
     extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
-    lds_u16 *table = (lds_u16 *)sm;
-    lds_u8 *ib = (lds_u8 *)sm + 2 * TAB_MAX;
+    HTab<SPARSE> table{(lds_u16 *)sm, (lds_u32 *)sm};
+    lds_u8 *ib = (lds_u8 *)sm + (SPARSE ? 4 * SPT : 2 * TAB_MAX);
     const uint32_t lane = lane_id();
     for (uint64_t b = blockIdx.x; b < n; b += gridDim.x) {
+        if (!SPARSE && SPT != 0 && sizes[b] != RR_SNZ_REDO) continue;   // (the dense pass: marked blocks only)
         const uint64_t c0 = in_offs[b], len = in_offs[b + 1] - c0;
         const uint32_t s0 = (uint32_t)(c0 & 3);
         Frag F;
@@ -834,7 +898,8 @@ __global__ __launch_bounds__(WAVE) void snz_comp_kernel(const uint8_t *__restric
         for (uint64_t f = 0; f < len; f += FRAG) {
             const uint32_t fn = (uint32_t)(len - f < FRAG ? len - f : FRAG);
             const uint32_t ts = table_size(fn);
-            for (uint32_t k = lane; k < ts / 2; k += WAVE) ((lds_u32 *)table)[k] = 0;
+            if (SPARSE) for (uint32_t k = lane; k < SPT; k += WAVE) table.t[k] = 0;
+            else for (uint32_t k = lane; k < ts / 2; k += WAVE) ((lds_u32 *)table.d)[k] = 0;
             F.g = s0 + (uint32_t)f;
             F.sh = (uint32_t)((c0 + f) & 15);
             F.lds = F.sh + fn + 8 <= fcap;
@@ -857,9 +922,12 @@ __global__ __launch_bounds__(WAVE) void snz_comp_kernel(const uint8_t *__restric
                     if (q < ng) reinterpret_cast<__attribute__((address_space(3))) u32x4_t *>(ib)[q] = v[k];
                 }
             }
-            compress_fragment(F, fn, table, ts, O);
+            if (!compress_fragment<SPARSE>(F, fn, table, ts, O)) {
+                O.op = ~0u;   // (abandoned: the dense pass redoes the whole block)
+                break;
+            }
         }
-        if (lane == 0) sizes[b] = O.op;
+        if (lane == 0) sizes[b] = O.op == ~0u ? RR_SNZ_REDO : O.op;
     }
 }
 
@@ -934,9 +1002,14 @@ extern "C" hipError_t rr_launch_snappy_compress(const uint8_t *in, uint64_t in_c
     hipLaunchKernelGGL(snz_bound_kernel, g, dim3(256), 0, stream, in_offs, n, slot_offs, lb, (uint32_t)lbw);
     hipError_t e = rr_launch_scan_u64(slot_offs, n, lb, err, stream);
     if (e != hipSuccess) return e;
-    if (n) {
+    if (n && SPT != 0) {   // sparse tables (16 KiB: 10 waves per CU), then the dense pass over the blocks they could not hold
+        hipLaunchKernelGGL(snz_comp_kernel<true>, dim3(grid_for(n, 1u << 20)), dim3(WAVE), 4 * SPT + SNZ_FRAG_LDS, stream, in,
+                           in_cap, in_offs, n, slots, (const uint64_t *)slot_offs, out_offs, SNZ_FRAG_LDS);
+        hipLaunchKernelGGL(snz_comp_kernel<false>, dim3(grid_for(n, 2048)), dim3(WAVE), 2 * TAB_MAX + SNZ_FRAG_LDS, stream, in,
+                           in_cap, in_offs, n, slots, (const uint64_t *)slot_offs, out_offs, SNZ_FRAG_LDS);
+    } else if (n) {
         const uint32_t smem = 2 * TAB_MAX + SNZ_FRAG_LDS;   // (5 waves per CU at the default fragment size)
-        hipLaunchKernelGGL(snz_comp_kernel, dim3(grid_for(n, 1u << 20)), dim3(WAVE), smem, stream, in, in_cap, in_offs, n, slots,
+        hipLaunchKernelGGL(snz_comp_kernel<false>, dim3(grid_for(n, 1u << 20)), dim3(WAVE), smem, stream, in, in_cap, in_offs, n, slots,
                            (const uint64_t *)slot_offs, out_offs, SNZ_FRAG_LDS);
     }
     hipLaunchKernelGGL(snz_sizes_kernel, g, dim3(256), 0, stream, out_offs, n, lb, (uint32_t)lbw);
