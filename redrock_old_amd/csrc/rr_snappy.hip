@@ -665,16 +665,21 @@ struct Out {
 
 // The compressor's hash table (CompressFragment's `table`, snappy.cc:468-486): ts u16 entries,
 // all zero at the fragment's start, table[h] = the last position stored under hash h.
-// RR_SNZ_SPARSE = 0: that dense array, 2 * ts bytes of LDS (32 KiB for a 16 KiB block: 5 waves per
-// CU).  Otherwise the same map as an open-addressing table of RR_SNZ_SPARSE u32 entries
-// ((h + 1) << 16 | position, 0 empty; linear probing from h's low bits): a fragment stores only as
-// many hashes as its probes touch — a few hundred for an incompressible 16 KiB block — so 16 KiB
-// of LDS holds it and a CU runs twice the waves.  Lookups return what the dense array would
+// RR_SNZ_SPARSE = 0 (the default): that dense array, 2 * ts bytes of LDS (32 KiB for a 16 KiB
+// block: 5 waves per CU).  Otherwise the same map as an open-addressing table of RR_SNZ_SPARSE u32
+// entries ((h + 1) << 16 | position, 0 empty; linear probing from h's low bits): a fragment stores
+// only as many hashes as its probes touch — a few hundred for an incompressible 16 KiB block — so
+// 16 KiB of LDS holds it and a CU runs twice the waves.  Lookups return what the dense array would
 // (0 for a hash never stored); a fragment that would fill more than 3/4 of the entries is
 // abandoned (its block goes to a second pass with the dense array), so every output byte is the
-// dense compressor's.
+// dense compressor's (the snappy suite is bit-exact either way).  Measured, round 6
+// (profiles/r6_snappy_sparse_ab.txt): incompressible config 2 247 -> 358 GB/s (4096 entries) /
+// 450 (2048), but config 4 33.1 -> 17.9 / 23.9 and config 3 13.9 -> 10.0 / 12.4 GB/s — their
+// repeated ziplist fields make copies, each copy restarts the probe schedule at stride 1, so a
+// block's table fills (the dense second pass then redoes it) and the probe loops and CAS inserts
+// cost more than the doubled occupancy wins.  Not the default.
 #ifndef RR_SNZ_SPARSE
-#define RR_SNZ_SPARSE 4096
+#define RR_SNZ_SPARSE 0
 #endif
 constexpr uint32_t SPT = RR_SNZ_SPARSE, SPT_LIMIT = SPT - SPT / 4;
 template <bool SPARSE>
@@ -1002,7 +1007,7 @@ extern "C" hipError_t rr_launch_snappy_compress(const uint8_t *in, uint64_t in_c
     hipLaunchKernelGGL(snz_bound_kernel, g, dim3(256), 0, stream, in_offs, n, slot_offs, lb, (uint32_t)lbw);
     hipError_t e = rr_launch_scan_u64(slot_offs, n, lb, err, stream);
     if (e != hipSuccess) return e;
-    if (n && SPT != 0) {   // sparse tables (16 KiB: 10 waves per CU), then the dense pass over the blocks they could not hold
+    if (n && SPT != 0) {   // sparse tables (RR_SNZ_SPARSE), then the dense pass over the blocks they could not hold
         hipLaunchKernelGGL(snz_comp_kernel<true>, dim3(grid_for(n, 1u << 20)), dim3(WAVE), 4 * SPT + SNZ_FRAG_LDS, stream, in,
                            in_cap, in_offs, n, slots, (const uint64_t *)slot_offs, out_offs, SNZ_FRAG_LDS);
         hipLaunchKernelGGL(snz_comp_kernel<false>, dim3(grid_for(n, 2048)), dim3(WAVE), 2 * TAB_MAX + SNZ_FRAG_LDS, stream, in,

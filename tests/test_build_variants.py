@@ -32,7 +32,7 @@ VARIANTS = [
     ("rr_snappy.hip", "-DRR_SNZ_K=1"),
     ("rr_snappy.hip", "-DRR_SNZ_K=32"),
     ("rr_snappy.hip", "-DRR_SNZ_SPEC=0"),
-    ("rr_snappy.hip", "-DRR_SNZ_SPARSE=0"),
+    ("rr_snappy.hip", "-DRR_SNZ_SPARSE=4096"),
     ("rr_snappy.hip", "-DRR_SNZ_SPARSE=2048 -DRR_SNZ_K=1"),
     ("rr_snappy.hip", "-DRR_PROBE"),
 ]
