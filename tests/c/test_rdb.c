@@ -176,11 +176,32 @@ static int bench(size_t k, char **keys, size_t *lens, int *dbis) {
     t_serial_des = now() - t0;
     stop(&s, fq, fr, th);
 #endif
+    /* the product paths of a child linked with the shim: desObject is the host codec (f1) —
+     * the unchanged serial child (rock.c:527-550), and the pipelined RAW batch */
+    start(&s, &fq, &fr, 0, NULL, &th);
+    t0 = now();
+    for (size_t i = 0; i < k; i++) {
+        size_t vlen = 0;
+        wr(fq, &dbis[i], sizeof(int)); wr(fq, &lens[i], sizeof(size_t)); wr(fq, keys[i], lens[i]);
+        rd(fr, &vlen, sizeof vlen);
+        char *v = malloc(vlen ? vlen : 1);
+        rd(fr, v, vlen);
+        decrRefCount(desObject(v, vlen));
+        free(v);
+    }
+    const double t_serial_shim = now() - t0;
+    stop(&s, fq, fr, th);
     start(&s, &fq, &fr, 0, NULL, &th);
     rr_rdb_blobs b;
     t0 = now();
     rr_rdb_request_batch(fq, fr, dbis, (const char *const *)keys, lens, k, &b);
     const double t_batch = now() - t0;
+    double t_batch_shim;
+    {
+        const double t1 = now();
+        for (size_t i = 0; i < k; i++) decrRefCount(desObject(b.data + b.offsets[i], b.offsets[i + 1] - b.offsets[i]));
+        t_batch_shim = t_batch + (now() - t1);
+    }
 #ifdef RR_RDB_BENCH_ORACLE
     {   /* the pipelined RAW batch + the child's CPU desObject on every value */
         uint64_t nbad = 0;
@@ -217,6 +238,8 @@ static int bench(size_t k, char **keys, size_t *lens, int *dbis) {
            "\"batch_fetch_keys_per_s\": %.0f, \"flat_restore_keys_per_s\": %.0f",
            k, (unsigned long long)bytes, gen.n ? "generated batch" : "golden fixtures", k / t_serial, k / t_batch,
            k / t_flat);
+    printf(", \"serial_fetch_shim_desobject_keys_per_s\": %.0f, \"batch_fetch_shim_desobject_keys_per_s\": %.0f",
+           k / t_serial_shim, k / t_batch_shim);
     if (t_serial_des > 0)
         printf(", \"serial_fetch_cpu_desobject_keys_per_s\": %.0f, \"batch_fetch_cpu_desobject_keys_per_s\": %.0f",
                k / t_serial_des, k / t_batch_des);
