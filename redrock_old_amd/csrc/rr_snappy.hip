@@ -936,16 +936,43 @@ __global__ __launch_bounds__(WAVE) void snz_comp_kernel(const uint8_t *__restric
     }
 }
 
-__global__ __launch_bounds__(WAVE) void snz_pack_kernel(const uint8_t *__restrict__ slots,
-                                                        const uint64_t *__restrict__ slot_offs, uint64_t n,
-                                                        uint8_t *__restrict__ out,
-                                                        const uint64_t *__restrict__ out_offs) {
+// A wave per block, four blocks a workgroup.  The packed destination is split at its 16-byte
+// boundaries: the head and tail (< 16 bytes each) a byte a lane, the body as aligned 16-byte
+// stores from unaligned 16-byte loads of the slot (gfx950 serves an unaligned global load),
+// PACK_U loads a lane in flight before their stores.  (Round 5 and before: a byte a lane,
+// ~0.9 TB/s of copy; config 2's blocks barely compress, so that was a quarter of its call.)
+constexpr uint32_t PACK_WPB = 4, PACK_U = 4;
+typedef uint32_t u32x4_ua __attribute__((ext_vector_type(4), aligned(1)));
+__global__ __launch_bounds__(PACK_WPB * WAVE) void snz_pack_kernel(const uint8_t *__restrict__ slots,
+                                                                   const uint64_t *__restrict__ slot_offs, uint64_t n,
+                                                                   uint8_t *__restrict__ out,
+                                                                   const uint64_t *__restrict__ out_offs) {
     const uint32_t lane = lane_id();
-    for (uint64_t b = blockIdx.x; b < n; b += gridDim.x) {
+    const uint64_t step = (uint64_t)gridDim.x * PACK_WPB;
+    for (uint64_t b = (uint64_t)blockIdx.x * PACK_WPB + threadIdx.x / WAVE; b < n; b += step) {
+        const uint64_t o0 = out_offs[b], len = out_offs[b + 1] - o0;
         const uint8_t *s = slots + slot_offs[b];
-        uint8_t *d = out + out_offs[b];
-        const uint64_t len = out_offs[b + 1] - out_offs[b];
-        for (uint64_t k = lane; k < len; k += WAVE) d[k] = s[k];
+        uint8_t *d = out + o0;
+        const uint64_t h0 = (16 - (o0 & 15)) & 15, h = h0 < len ? h0 : len;
+        const uint64_t body = (len - h) & ~15ull, t0 = h + body;
+        if (lane < h) d[lane] = s[lane];
+        if (lane < len - t0) d[t0 + lane] = s[t0 + lane];
+        const u32x4_ua *sv = reinterpret_cast<const u32x4_ua *>(s + h);
+        u32x4_t *dv = reinterpret_cast<u32x4_t *>(d + h);
+        const uint64_t nv = body >> 4;
+        for (uint64_t k0 = 0; k0 < nv; k0 += PACK_U * WAVE) {
+            u32x4_t v[PACK_U];
+#pragma unroll
+            for (uint32_t u = 0; u < PACK_U; ++u) {
+                const uint64_t k = k0 + u * WAVE + lane;
+                if (k < nv) v[u] = sv[k];
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < PACK_U; ++u) {
+                const uint64_t k = k0 + u * WAVE + lane;
+                if (k < nv) dv[k] = v[u];
+            }
+        }
     }
 }
 
@@ -1020,7 +1047,7 @@ extern "C" hipError_t rr_launch_snappy_compress(const uint8_t *in, uint64_t in_c
     hipLaunchKernelGGL(snz_sizes_kernel, g, dim3(256), 0, stream, out_offs, n, lb, (uint32_t)lbw);
     e = rr_launch_scan_u64(out_offs, n, lb, err, stream);
     if (e != hipSuccess || n == 0) return e != hipSuccess ? e : hipGetLastError();
-    hipLaunchKernelGGL(snz_pack_kernel, dim3(grid_for(n, 1u << 20)), dim3(WAVE), 0, stream, slots,
+    hipLaunchKernelGGL(snz_pack_kernel, dim3(grid_for((n + PACK_WPB - 1) / PACK_WPB, 1u << 20)), dim3(PACK_WPB * WAVE), 0, stream, slots,
                        (const uint64_t *)slot_offs, n, out, (const uint64_t *)out_offs);
     return hipGetLastError();
 }
