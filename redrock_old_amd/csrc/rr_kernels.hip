@@ -331,8 +331,8 @@ __device__ __forceinline__ void fold_totals(const uint64_t *__restrict__ stats, 
 //                     marked values fixed at its end, its totals added atomically.
 
 #ifndef RR_ABLATE   // timing-only ablations (tools/, wrong results; the decode's 1-4 below): count_kernel 5 no
-#define RR_ABLATE 0       // List stage or walk, 6 the stage lands but no walk
-#endif
+#define RR_ABLATE 0       // List stage or walk, 6 the stage lands but no walk; enc_emit_kernel 7 no header,
+#endif                    // length or decimal field writes, 8 no payload copies, 9 no decimals, 10 no task fields
 // ---- K1: reservation + class per value ------------------------------------------------
 // reserve(i) = the descriptor slots value i owns (rr_format.h): header fields only, plus the
 // length chain of a List.  Equal to the decoded count for every valid blob.
@@ -2237,6 +2237,10 @@ struct Img {
 constexpr uint64_t JQ_SRC = (1ull << 40) - 1;
 
 
+// copy pieces: 2^ENC_PS-byte image blocks (round 6: 16-byte pieces, one aligned load each and four
+// pieces a thread in flight, measured within noise of 64-byte pieces: encode config 4 0.3748 vs
+// 0.3754 ms, configs 3 and 2 +1 %; profiles/r6_encode_pieces_ab.txt)
+constexpr uint32_t ENC_PS = 6;
 // waves per SIMD the emit kernel is built for (74 VGPRs, no spills; 5: E4 345 us, 6: 307 us)
 constexpr int ENC_WPE = 6;
 template <uint32_t W, uint32_t NT, uint32_t RCAP>
@@ -2257,8 +2261,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(ENC_WPE))) v
     // block 0 folds E1's and E3's tile totals into the call's totals before its window (a
     // separate finalize launch's work, hidden under the other windows: encode cfg 4 -1 %)
     if (tot && blockIdx.x == 0) fold_totals(stats, ntiles, offsets, n, tot, err);
-    static_assert(RCAP >= 2 && W / 64 + RCAP < 65536, "run piece bases are 16-bit");
-    constexpr uint32_t RTOP = 1u << (31 - __builtin_clz(RCAP - 1));   // largest power of two < RCAP
+    static_assert(RCAP >= 2 && (W >> ENC_PS) + RCAP < 65536, "run piece bases are 16-bit");
     __shared__ uint4 img4[W / 16];
     __shared__ uint64_t rq_a[RCAP];        // run: arena offset | length << 40
     __shared__ uint32_t rq_dp[RCAP];       // run: image offset | first piece (pieces of earlier runs) << 16
@@ -2316,7 +2319,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(ENC_WPE))) v
         src += want ? d0 - pos : 0;
         const uint32_t dst = want ? (uint32_t)(d0 - w0) : 0, l = want ? (uint32_t)(d1 - d0) : 0;
         const bool queued = want && src + l <= JQ_SRC;
-        const uint32_t np = queued ? ((dst + l - 1) >> 6) - (dst >> 6) + 1 : 0;
+        const uint32_t np = queued ? ((dst + l - 1) >> ENC_PS) - (dst >> ENC_PS) + 1 : 0;
         const uint64_t mine = queued ? (1ull | ((uint64_t)np << 32)) : 0;
         // (the two 32-bit fields scanned apart in DPP: a wave's runs and pieces stay far below 2^32)
         const uint64_t incl = (uint64_t)wave_incl_scan_u32(queued ? 1u : 0u) |
@@ -2361,7 +2364,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(ENC_WPE))) v
                                    : type == RR_TYPE_SET_HT ? ne : (uint64_t)(ne / 2);
                 for (uint32_t f = 0; f < 2; ++f) {
                     const uint32_t nb = f == 0 ? 5u : fnb;
-                    if (nb) I.field(a + 5 * f, f == 0 ? (type | ((uint64_t)(x.y & RR_LRU_MASK) << 8)) : fv8, nb);
+                    if (nb && RR_ABLATE != 7) I.field(a + 5 * f, f == 0 ? (type | ((uint64_t)(x.y & RR_LRU_MASK) << 8)) : fv8, nb);
                 }
                 tasks = (type == RR_TYPE_HASH_ZIPLIST || type == RR_TYPE_ZSET_ZIPLIST) ? 1u : ne;
                 sv_pos[tid] = a + enc_hdr(type);
@@ -2430,9 +2433,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(ENC_WPE))) v
                 else if (type == RR_TYPE_LIST_QUICKLIST) { fval = es - 4; fnb = 4; hdr = 4; pay = e.kind != RR_K_INT; }
                 else if (type == RR_TYPE_SET_INTSET) { fval = e.data; fnb = enc; pay = false; }
                 else if (type == RR_TYPE_ZSET_SKIPLIST && (k & 1)) { fval = e.data; pay = false; }
-                if (fnb) I.field(p, fval, fnb);
+                if (fnb && RR_ABLATE != 7 && RR_ABLATE != 10) I.field(p, fval, fnb);
                 EPROBE(asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); const uint64_t rw1 = rr_stamp(); tw1 += rw1 - rs1;)
-                if (type == RR_TYPE_LIST_QUICKLIST && !pay) I.decimal(p + 4, (int64_t)e.data, (uint32_t)(es - 4));
+                if (type == RR_TYPE_LIST_QUICKLIST && !pay && RR_ABLATE != 7 && RR_ABLATE != 9) I.decimal(p + 4, (int64_t)e.data, (uint32_t)(es - 4));
                 EPROBE(asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); const uint64_t rw2 = rr_stamp(); tw2 += rw2 - rw1;)
                 ppos = p + hdr;
             }
@@ -2455,23 +2458,54 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(ENC_WPE))) v
     // the run's k-th 64-byte image block
     const uint32_t nr = (uint32_t)sh_nrp < RCAP ? (uint32_t)sh_nrp : RCAP;
     const uint32_t npc = sh_pend != 0xFFFFFFFFu ? sh_pend : (uint32_t)(sh_nrp >> 32);
-    auto piece = [&](uint32_t b, uint64_t &ps, uint32_t &pd, uint32_t &pl) {
-        uint32_t lo = 0;   // (steps from the largest power of two below RCAP: every index reachable)
+    // piece -> run map in the rounds' value arrays (free now): each queued run writes its index at
+    // its first piece, then a block-wide running max fills the pieces after it (heads increase
+    // along the map, the zeros between them never win) — one LDS read per piece instead of a
+    // binary search of the runs' first pieces (9 dependent LDS reads per piece).  Round 6: encode
+    // config 4 0.382 -> 0.371 ms and 0.384 -> 0.372 on one box, config 2 -1.5 %, config 3 within
+    // noise (profiles/r6_encode_pieces_ab.txt)
+    uint16_t *const pmap = reinterpret_cast<uint16_t *>(sv_raw);
+    static_assert(8 * NT >= (W >> ENC_PS) + RCAP && 16 * NT <= sizeof(sv_raw), "piece map: 8 pieces a thread");
+    if (npc) {   // (block-uniform)
+        reinterpret_cast<uint4 *>(pmap)[tid] = make_uint4(0, 0, 0, 0);
+        lds_barrier();
+        for (uint32_t r = tid; r < nr; r += NT) pmap[rq_dp[r] >> 16] = (uint16_t)r;
+        lds_barrier();
+        const uint4 q = reinterpret_cast<const uint4 *>(pmap)[tid];
+        const uint32_t qw[4] = {q.x, q.y, q.z, q.w};
+        uint32_t m[8];
 #pragma unroll
-        for (uint32_t s = RTOP; s > 0; s >>= 1)
-            if (lo + s < nr && (rq_dp[lo + s] >> 16) <= b) lo += s;
+        for (uint32_t k = 0; k < 8; ++k) m[k] = (qw[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
+#pragma unroll
+        for (uint32_t k = 1; k < 8; ++k) m[k] = max(m[k], m[k - 1]);
+        const uint32_t im = wave_incl_max_u32(m[7]);
+        const uint32_t wv = tid / RR_WAVE;
+        if (lane_id() == RR_WAVE - 1) wsum[0][wv] = im;
+        lds_barrier();
+        uint32_t carry = wave_from_prev(im);   // (lane 0: 0; every lane runs the DPP)
+#pragma unroll
+        for (uint32_t k = 0; k < NT / RR_WAVE; ++k) carry = k < wv ? max(carry, (uint32_t)wsum[0][k]) : carry;
+#pragma unroll
+        for (uint32_t k = 0; k < 8; ++k) m[k] = max(carry, m[k]);
+        reinterpret_cast<uint4 *>(pmap)[tid] = make_uint4(m[0] | m[1] << 16, m[2] | m[3] << 16, m[4] | m[5] << 16, m[6] | m[7] << 16);
+        lds_barrier();
+    }
+    auto piece = [&](uint32_t b, uint64_t &ps, uint32_t &pd, uint32_t &pl) {
+        const uint32_t lo = pmap[b];
         const uint64_t a = rq_a[lo];
-        const uint32_t dp = rq_dp[lo], dst = dp & 0xFFFF, l = (uint32_t)(a >> 40), k = b - (dp >> 16);
-        const uint32_t d0 = k == 0 ? dst : ((dst >> 6) + k) << 6;
-        const uint32_t e1 = (((dst >> 6) + k + 1) << 6), e = e1 < dst + l ? e1 : dst + l;
+        const uint32_t dp = rq_dp[lo], dst = dp & 0xFFFF, l = (uint32_t)(a >> 40),
+                       k = b - (dp >> 16);
+        const uint32_t d0 = k == 0 ? dst : ((dst >> ENC_PS) + k) << ENC_PS;
+        const uint32_t e1 = (((dst >> ENC_PS) + k + 1) << ENC_PS), e = e1 < dst + l ? e1 : dst + l;
         ps = (a & JQ_SRC) + (d0 - dst);
         pd = d0;
-        pl = e > d0 ? e - d0 : 0;   // (inside one 64-byte block by construction)
+        pl = e > d0 ? e - d0 : 0;   // (inside one 2^ENC_PS-byte block by construction)
     };
     // Every run aligned with its image offset mod 16 (any arena that keeps the blob layout, the
     // decode's mirror arena included): pieces move whole granules (RR_AL_LOAD / RR_AL_STORE).
     // A window with any other run takes the byte plan below for all its pieces.
-    if (sh_unal == 0) {
+    if (RR_ABLATE == 8) {   // timing only (wrong results): no payload copies
+    } else if (sh_unal == 0) {
         for (uint32_t j = tid; j < npc; j += 2 * NT) {
             const bool two = j + NT < npc;
             uint64_t s0, s1 = 0;
