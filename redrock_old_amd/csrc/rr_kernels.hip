@@ -2102,16 +2102,15 @@ struct Img {
     uint8_t *img;
     uint64_t w0;
     uint64_t span;
-    __device__ __forceinline__ void put(uint64_t pos, uint32_t b) const {
-        const uint64_t d = pos - w0;
-        if (d < span) img[d] = (uint8_t)b;
-    }
-    // little-endian field of nb (<= 8) bytes
+    // little-endian field of nb (<= 8) bytes, clipped to the window with no byte loop: the bytes
+    // before w0 shifted out, those past the span cut from the length.  (Until round 6 a byte loop
+    // handled the window's two straddling values, inlined at every call site: the emit kernel
+    // took 79 VGPRs instead of 72, and encode config 4 / 3 ran 2.6 % slower;
+    // profiles/r6_encode_pieces_ab.txt)
     __device__ __forceinline__ void field(uint64_t pos, uint64_t v, uint32_t nb) const {
-        const uint64_t d = pos - w0;
-        if (d < span && d + nb <= span) lds_or(img, (uint32_t)d, v, nb);
-        else
-            for (uint32_t i = 0; i < nb; ++i) put(pos + i, (uint32_t)(v >> (8 * i)) & 0xFF);
+        const int64_t d = (int64_t)(pos - w0), e = d + (int64_t)nb;
+        const int64_t lo = d > 0 ? d : 0, hi = e < (int64_t)span ? e : (int64_t)span;
+        if (hi > lo) lds_or(img, (uint32_t)lo, v >> (8 * (uint32_t)(lo - d)), (uint32_t)(hi - lo));
     }
     // sdsll2str(x) (sds.c:450-479), l characters at pos: |x| as three 8-digit chunks, each
     // turned into 8 ASCII digits at once (SWAR), the 24-character string shifted right past
