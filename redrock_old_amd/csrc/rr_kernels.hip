@@ -2112,6 +2112,25 @@ struct Img {
         const int64_t lo = d > 0 ? d : 0, hi = e < (int64_t)span ? e : (int64_t)span;
         if (hi > lo) lds_or(img, (uint32_t)lo, v >> (8 * (uint32_t)(lo - d)), (uint32_t)(hi - lo));
     }
+    // the same with the bytes before `from` dropped too
+    __device__ __forceinline__ void field_from(uint64_t pos, uint64_t v, uint32_t nb, uint64_t from) const {
+        const int64_t d = (int64_t)(pos - w0), e = d + (int64_t)nb, f = (int64_t)(from - w0);
+        int64_t lo = d > f ? d : f;
+        lo = lo > 0 ? lo : 0;
+        const int64_t hi = e < (int64_t)span ? e : (int64_t)span;
+        if (hi > lo) lds_or(img, (uint32_t)lo, v >> (8 * (uint32_t)(lo - d)), (uint32_t)(hi - lo));
+    }
+    // chunk c (0: the last 8 digits, 1: the 8 before, 2: the first 3) of sdsll2str(x) at pos, l
+    // characters: the chunk's 8 digits right-aligned at their place, the leading zeros dropped by
+    // the clip at the first digit; chunk 0 also writes the sign
+    __device__ __forceinline__ void decimal_chunk(uint64_t pos, int64_t x, uint32_t l, uint32_t c) const {
+        const uint64_t u = x < 0 ? 0ull - (uint64_t)x : (uint64_t)x;
+        const uint64_t q = u / 100000000ull, q2 = q / 100000000ull;
+        const uint64_t ch = c == 0 ? u - q * 100000000ull : c == 1 ? q - q2 * 100000000ull : q2;
+        const uint64_t end = pos + l, from = pos + (x < 0 ? 1u : 0u);
+        field_from(end - 8 * (c + 1), swar8((uint32_t)ch), 8, from);
+        if (c == 0 && x < 0) field(pos, '-', 1);
+    }
     // sdsll2str(x) (sds.c:450-479), l characters at pos: |x| as three 8-digit chunks, each
     // turned into 8 ASCII digits at once (SWAR), the 24-character string shifted right past
     // its leading zeros (first character in byte 0), the sign prepended, then stored as up to
@@ -2271,6 +2290,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(ENC_WPE))) v
     uint64_t *const sv_pos = sv_raw;
     uint32_t *const sv_el = reinterpret_cast<uint32_t *>(sv_raw + NT), *const sv_te = sv_el + NT;
     __shared__ uint64_t wsum[2][NT / RR_WAVE];
+    __shared__ uint8_t dsrc[NT / RR_WAVE][RR_WAVE / 3 + 1];   // a wave's decimal lanes, in lane order
     __shared__ uint64_t sh_nrp;            // runs reserved | pieces reserved << 32
     __shared__ uint32_t sh_pend;           // pieces of the queued runs, when the queue overflowed
     __shared__ uint32_t sh_unal;           // some queued run is not aligned with its image offset mod 16
@@ -2421,6 +2441,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(ENC_WPE))) v
             EPROBE(const uint64_t rs1 = rr_stamp(); tsc += rs1 - rs0;)
             bool pay = false;
             uint64_t ppos = 0;
+            [[maybe_unused]] bool isd = false;
+            [[maybe_unused]] uint64_t dpos = 0;
+            [[maybe_unused]] uint32_t dlen = 0;
             if (act) {
                 const uint64_t p = sv_pos[j] + ex;
                 // one fixed field, then a decimal or a payload (single call sites keep the
@@ -2434,9 +2457,32 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(ENC_WPE))) v
                 else if (type == RR_TYPE_ZSET_SKIPLIST && (k & 1)) { fval = e.data; pay = false; }
                 if (fnb && RR_ABLATE != 7 && RR_ABLATE != 10) I.field(p, fval, fnb);
                 EPROBE(asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); const uint64_t rw1 = rr_stamp(); tw1 += rw1 - rs1;)
-                if (type == RR_TYPE_LIST_QUICKLIST && !pay && RR_ABLATE != 7 && RR_ABLATE != 9) I.decimal(p + 4, (int64_t)e.data, (uint32_t)(es - 4));
+                if (type == RR_TYPE_LIST_QUICKLIST && !pay) { isd = true; dpos = p + 4; dlen = (uint32_t)(es - 4); }
                 EPROBE(asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); const uint64_t rw2 = rr_stamp(); tw2 += rw2 - rw1;)
                 ppos = p + hdr;
+            }
+            // integer List elements' decimals: a wave with at most 21 spreads each one's three
+            // 8-digit chunks over three lanes (one SWAR conversion a lane instead of three: the
+            // decimals were ~20 % of the kernel's VALU); lane 3i + c takes chunk c of the wave's
+            // i-th decimal, whose lane it finds through a per-wave LDS list.  Round 6: E4 297.5 ->
+            // 282.7 us, encode config 4 -2.3 % (profiles/r6_encode_pieces_ab.txt)
+            {
+                const uint64_t dm = __ballot(isd);
+                const uint32_t nd = (uint32_t)__popcll(dm);
+                if (nd && nd <= RR_WAVE / 3 && RR_ABLATE != 7 && RR_ABLATE != 9) {   // (wave-uniform)
+                    const uint32_t ln = lane_id(), wv = tid / RR_WAVE;
+                    if (isd) dsrc[wv][__builtin_amdgcn_mbcnt_hi((uint32_t)(dm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)dm, 0u))] = (uint8_t)ln;
+                    const uint32_t i = ln / 3, c = ln - 3 * i;
+                    const uint32_t src = i < nd ? dsrc[wv][i] : ln;
+                    const int64_t x = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute((int)(4 * src), (int)(uint32_t)e.data)) |
+                                                ((uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute((int)(4 * src), (int)(uint32_t)(e.data >> 32)) << 32));
+                    const uint64_t xp = ((uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute((int)(4 * src), (int)(uint32_t)dpos)) |
+                                        ((uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute((int)(4 * src), (int)(uint32_t)(dpos >> 32)) << 32);
+                    const uint32_t xl = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4 * src), (int)dlen);
+                    if (i < nd) I.decimal_chunk(xp, x, xl, c);
+                } else if (isd && RR_ABLATE != 7 && RR_ABLATE != 9) {
+                    I.decimal(dpos, (int64_t)e.data, dlen);
+                }
             }
             payload(pay, ppos, e.data, e.len);
             run += rt;
