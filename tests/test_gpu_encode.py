@@ -234,3 +234,37 @@ def test_host_encode_pipelined_matches_one_call(engine, layout):
     assert np.array_equal(out, data[:nb]) and t2["bytes"] == nb
     for cap in (int(offs[30000]) + 5, int(offs[59000]), nb // 7):
         _check_against_oracle(engine, v, e, a, data_cap=cap)
+
+
+def test_list_decimals_both_wave_paths(engine):
+    """Integer List elements (sdsll2str, sds.c:450-479) through the emit kernel's two decimal
+    paths: a wave holding at most 21 integers spreads each one's three 8-digit chunks over three
+    lanes, a wave with more writes each on its own lane.  All-integer Lists (every task of a wave an
+    integer), Lists mixing integers and strings (a few a wave), a List of 3,000 integers whose
+    decimals straddle the 16 KiB output windows, and the boundary values of every chunk: decode
+    equal to the oracle, encode(decode(b)) == b byte for byte."""
+    rng = np.random.default_rng(2026)
+    edges = [0, 1, -1, 9, 10, -10, 99, 100, 10**8 - 1, 10**8, -(10**8), 10**8 + 1, 10**16 - 1, 10**16,
+             -(10**16), 10**16 + 7, 2**63 - 1, -(2**63), 1234567890123456789, -999999999999999999]
+    def ints(k):
+        out = []
+        for _ in range(k):
+            b = int(rng.integers(0, 64))
+            m = int(rng.integers(0, 2**63, dtype=np.uint64)) >> (63 - b) if b else 0
+            out.append(-m if rng.integers(0, 2) else m)
+        return out
+    blobs = []
+    for i in range(40):   # all integers: more than 21 a wave
+        blobs.append(l_list(i, [str(x).encode() for x in edges + ints(60)]))
+    for i in range(40, 80):   # mixed: a few integers a wave
+        items = []
+        for x in edges[(i % 5):(i % 5) + 6]:
+            items += [str(x).encode(), b"s" * int(rng.integers(1, 40)), b"abc-" + str(i).encode()]
+        blobs.append(l_list(i, items))
+    blobs.append(l_list(80, [str(x).encode() for x in ints(3000) + edges]))   # crosses windows
+    data, offs = batch_from_blobs(blobs)
+    ov, oe, oa, ot = cpu.decode(data, offs)
+    assert (ov["status"] == 0).all()
+    v, e, a, t = engine.decode_host(data, offs)
+    out, ooffs, t2 = _check_against_oracle(engine, v, e, a)
+    assert np.array_equal(ooffs, offs) and np.array_equal(out[:int(offs[-1])], data[:int(offs[-1])])
