@@ -2422,6 +2422,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(ENC_WPE))) v
             pe = ElemV{0, 0, 0};
             if (t < tt) {
                 // last value j with tb[j] <= t
+                // (a per-chunk LDS task -> value map instead, built with a block-wide max fill:
+                // encode config 4 +8-10 %, the fill's three barriers a chunk cost more than the
+                // search's dependent reads; round 6, profiles/r6_encode_pieces_ab.txt)
                 uint32_t lo = 0;
 #pragma unroll
                 for (uint32_t s = NT / 2; s > 0; s >>= 1)
