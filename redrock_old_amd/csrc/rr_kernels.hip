@@ -1117,6 +1117,116 @@ constexpr uint32_t DEC_KE = 2;
 // told so (left to itself it takes 137 for the hash-table walk and the CU holds one workgroup).
 constexpr int DEC_WPE = 4;
 
+// The one-launch decode's words in the context's sums (zero on entry, zero again when the call's
+// last window is done): [6] a wait that never ended (the error word), then per window its
+// look-back word (ONE_RUN once it runs, ONE_AGG | its reservations once it knows them) and its
+// end word (ONE_AGG | n_bad << 40 | payload).
+constexpr uint32_t ONE_HDR = 8;
+constexpr uint64_t ONE_AGG = 1ull << 63, ONE_RUN = 1ull << 62, ONE_VAL = ONE_RUN - 1;
+__host__ __device__ constexpr uint64_t one_words(uint64_t nwin) { return ONE_HDR + 2 * nwin; }
+
+// The window's values [v[0], v[1]) and their first offsets f[0], f[1]: count_kernel's first_val
+// of the window and of the next, i.e. min{i <= n : i == n or offsets[i] >= T} for T = tile * win
+// and (tile + 1) * win.  Round 1 reads NT consecutive offsets from just before the guess
+// n * T / data_cap (exact for evenly sized values: config 1's windows resolve both bounds in this
+// one round, and the window's own offsets come out of the same samples, a[0, NT) from position
+// *base); a bound outside them narrows by NT / 2 samples a round.  a: 3 * NT u64 of LDS,
+// cnt: 2 * NW u64.
+// issue(): the caller's loads, issued right behind the first samples (vmcnt retires in order, so
+// the samples are waited for without them).
+template <uint32_t NT, typename F>
+__device__ __forceinline__ void one_locate(const uint64_t *__restrict__ offsets, uint64_t n, uint32_t win,
+                                           uint64_t data_cap, uint32_t tile, uint64_t on, uint64_t *a, uint64_t *cnt,
+                                           uint64_t (&v)[2], uint64_t (&f)[2], uint64_t &base, F &&issue) {
+    constexpr uint32_t H = NT / 2, NWV = NT / RR_WAVE;
+    const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid / RR_WAVE;
+    const uint64_t T[2] = {(uint64_t)tile * win, (uint64_t)(tile + 1) * win};
+    const uint64_t g = (uint64_t)((double)n * (double)T[0] / (double)(data_cap ? data_cap : 1));
+    base = rfl64(g > NT / 8 ? (g - NT / 8 < n ? g - NT / 8 : n) : 0);
+    const uint64_t q1 = base + tid < n ? base + tid : n;
+    const uint64_t a1 = q1 < n ? offsets[q1] : on;
+    issue();
+    a[tid] = a1;
+    const uint64_t m0 = __ballot(q1 < n && a1 < T[0]), m1 = __ballot(q1 < n && a1 < T[1]);
+    if (lane == 0) cnt[wave] = (uint64_t)__popcll(m0) | ((uint64_t)__popcll(m1) << 32);
+    lds_barrier();
+    uint64_t lo[2], hi[2], oh[2];
+    {
+        uint32_t c[2] = {0, 0};
+#pragma unroll
+        for (uint32_t w = 0; w < NWV; ++w) { c[0] += (uint32_t)cnt[w]; c[1] += (uint32_t)(cnt[w] >> 32); }
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {   // (position j of the samples: min(base + j, n))
+            const uint64_t qc = base + c[k] < n ? base + c[k] : n;
+            lo[k] = c[k] ? qc : 0;   // (samples 0 .. c - 1 lie below T: the bound is past them)
+            hi[k] = c[k] < NT ? qc : n;
+            oh[k] = rfl64(c[k] < NT ? a[c[k]] : on);
+        }
+    }
+    // later rounds (rare): threads [0, H) search T[0], [H, NT) T[1]; buffers 1 and 2 alternate
+    for (uint32_t r = 1; lo[0] < hi[0] || lo[1] < hi[1]; ++r) {
+        const uint32_t k = tid / H, j = tid % H, b = 1 + (r & 1);
+        const uint64_t span = hi[k] - lo[k];
+        const uint64_t p = span <= H ? lo[k] + j : lo[k] + span * j / H;
+        const bool valid = p < hi[k];
+        const uint64_t x = valid ? offsets[p] : 0;
+        a[b * NT + tid] = x;
+        const uint64_t m = __ballot(valid && x < T[k]);
+        if (lane == 0) cnt[(r & 1) * NWV + wave] = (uint64_t)__popcll(m);
+        lds_barrier();
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            if (lo[kk] >= hi[kk]) continue;
+            uint32_t c = 0;
+#pragma unroll
+            for (uint32_t w = 0; w < NWV / 2; ++w) c += (uint32_t)cnt[(r & 1) * NWV + kk * (NWV / 2) + w];
+            const uint64_t sp = hi[kk] - lo[kk];
+            const uint32_t nv = sp <= H ? (uint32_t)sp : H;   // the valid samples
+            auto pos = [&](uint32_t q) { return sp <= H ? lo[kk] + q : lo[kk] + sp * q / H; };
+            const uint64_t nlo = c ? pos(c - 1) + 1 : lo[kk];
+            if (c < nv) { hi[kk] = rfl64(pos(c)); oh[kk] = rfl64(a[b * NT + kk * H + c]); }
+            lo[kk] = rfl64(nlo);
+        }
+    }
+    v[0] = rfl64(lo[0]); v[1] = rfl64(lo[1]);
+    f[0] = oh[0]; f[1] = oh[1];
+}
+
+// The same bound by one wave alone, 64 samples a round (the look-back's help below)
+__device__ __forceinline__ uint64_t wave_lower_bound(const uint64_t *__restrict__ offsets, uint64_t n, uint64_t T) {
+    uint64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint64_t sp = hi - lo;
+        const uint32_t j = lane_id(), nv = sp <= RR_WAVE ? (uint32_t)sp : RR_WAVE;
+        auto pos = [&](uint32_t q) { return sp <= RR_WAVE ? lo + q : lo + sp * q / RR_WAVE; };
+        const uint64_t p = pos(j);
+        const uint32_t c = (uint32_t)__popcll(__ballot(j < nv && offsets[p] < T));
+        const uint64_t nlo = c ? pos(c - 1) + 1 : lo;
+        if (c < nv) hi = pos(c);
+        lo = nlo;
+    }
+    return lo;
+}
+
+// A window's reservations (unsaturated, as count_kernel's window sums), by one wave from global
+// memory: the look-back's help for a window that has not started (its workgroup not yet
+// dispatched), so that a window never waits on one that is not running.
+__device__ uint64_t one_window_sum(const uint8_t *__restrict__ blob, const uint64_t *__restrict__ offsets, uint64_t n,
+                                   uint32_t win, uint32_t p) {
+    const uint64_t v0 = wave_lower_bound(offsets, n, (uint64_t)p * win);
+    const uint64_t v1 = wave_lower_bound(offsets, n, (uint64_t)(p + 1) * win);
+    uint64_t sum = 0;
+    for (uint64_t v = v0 + lane_id(); v < v1; v += RR_WAVE) {
+        const uint64_t o = offsets[v], o1 = offsets[v + 1];
+        uint32_t d[6], c;
+        uint64_t r;
+        head24(blob, o, o1, d);
+        reserve_classify(blob + o, o1 - o, d, r, c);
+        sum += r;
+    }
+    return wave_sum(sum);
+}
+
 // Workgroup per byte WINDOW of W bytes: window t owns the values whose first byte lies in
 // [t*W, (t+1)*W) (first_val from K1).  The workgroup
 //   1. loads the window (buffer resources: no exec-mask branches; loads past the range read
@@ -1134,14 +1244,19 @@ constexpr int DEC_WPE = 4;
 // windows before it (two loads per lane: the groups before its group, the windows before it in
 // its group); each chunk scans its values' reservations in LDS (eloc) while it sorts them, so
 // no scan launch runs between count_kernel and this kernel.
-template <uint32_t W, uint32_t SLACK, uint32_t NW, uint32_t PMAX>
+//
+// ONE (a batch of one generation of windows, no count_kernel): the window's index comes from an
+// atomic ticket and its values from two lower-bound searches of offsets (one_locate); it
+// classifies its values from the stage itself (count_kernel's rule) and finds its first slot by
+// a decoupled look-back over the earlier windows (rr_device.h); the call's totals gather in the
+// context's words and the last window to finish stores them and leaves the words zero (one_words).
+template <uint32_t W, uint32_t SLACK, uint32_t NW, uint32_t PMAX, bool ONE = false>
 __global__ __launch_bounds__(NW * RR_WAVE) __attribute__((amdgpu_waves_per_eu(DEC_WPE))) void decode_kernel(
     const uint8_t *__restrict__ blob, uint64_t data_cap, const uint64_t *__restrict__ offsets, uint64_t n,
-    const uint32_t *__restrict__ first_val, const uint64_t *__restrict__ first_off, const uint8_t *__restrict__ cls,
-    const uint32_t *__restrict__ counts,
+    const uint32_t *__restrict__ first_val, const uint64_t *__restrict__ first_off, uint8_t *__restrict__ cls, uint32_t *__restrict__ counts,
     const uint64_t *wtot, const uint64_t *gtot, rr_value *__restrict__ values,
     rr_elem *__restrict__ elems, uint64_t elem_cap, uint8_t *__restrict__ arena, uint32_t nwin, uint32_t win,
-    rr_totals *tot) {
+    rr_totals *tot, uint64_t *one, uint64_t *zero_words, uint64_t nzero) {
     constexpr uint32_t NT = NW * RR_WAVE, STAGE = W + SLACK;
     static_assert(PMAX == NT, "a chunk is one value per thread (the slot scan)");
     static_assert(W % 16 == 0 && SLACK % 16 == 0, "tile shape");
@@ -1155,7 +1270,7 @@ __global__ __launch_bounds__(NW * RR_WAVE) __attribute__((amdgpu_waves_per_eu(DE
     __shared__ uint32_t next_batch;
     __shared__ uint64_t red[2][NW];
     PROBE(__shared__ uint64_t prb[PROBE_WORDS]; uint64_t pt0 = __builtin_amdgcn_s_memtime(), pt1 = 0, pt2 = 0;
-          const uint64_t prt0 = __builtin_amdgcn_s_memrealtime();
+          const uint64_t prt0 = __builtin_amdgcn_s_memrealtime(); uint64_t pa = 0, pb = 0, pc = 0;
           if (threadIdx.x < PROBE_WORDS) prb[threadIdx.x] = 0;)
     const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid / RR_WAVE;
     // (A persistent form — the resident grid walking windows b, b + grid, ..., no workgroup
@@ -1164,39 +1279,85 @@ __global__ __launch_bounds__(NW * RR_WAVE) __attribute__((amdgpu_waves_per_eu(DE
     // round 6, profiles/r6_decode_persist_ab.txt.)
     const uint32_t tile = blockIdx.x;
     if (tid == 0) nfix = 0;   // (ordered before the batches by the sort's first barrier)
-    // 0. the loads of the window's first slot go out first (reduced under the sort)
-    const uint32_t grp = tile / WGROUP, gi = tile % WGROUP;
-    uint64_t pre = tid < gi ? wtot[(uint64_t)grp * WGROUP + tid] : 0;
-    for (uint32_t k = tid; k < grp; k += NT) pre += gtot[k];
-    const uint64_t padded = (offsets[n] + 15) & ~15ull;
+    __shared__ rr_totals s_fix;   // (ONE: the fixup's adjustments of the window's totals)
+    if (ONE && tid < 4) reinterpret_cast<uint64_t *>(&s_fix)[tid] = 0;
+    uint64_t *const state = one + ONE_HDR, *const fin = state + nwin;   // (ONE)
     const uint64_t W0 = (uint64_t)tile * win;   // (win <= W: the call's window size, launch_decode)
-    const uint64_t W1 = W0 + win < padded ? W0 + win : padded;
-    // the arena copy starts at the call's first value (a call over a slice of a larger buffer —
-    // the chunks of rr_decode_batch_host — copies only its own bytes); the stage always lies
-    // past it (S0 >= offsets[v_lo] >= offsets[0])
-    const uint64_t A0 = W0 > (offsets[0] & ~15ull) ? W0 : (offsets[0] & ~15ull);
-    // the window's own granules [A0, W1) first: their range needs only offsets[0] and
-    // offsets[n], not first_val -> offsets, so the loads go out at the window's start; the
-    // stage's tail [W1, ov_te) (the last values' bytes past the window) follows.  The arena gets
-    // [A0, W1) (stores past it are dropped); granule A0 / 16 + tid + k * NT is at byte offset
-    // 16 (tid + k NT)
     constexpr uint32_t KM = W / 16 / NT;   // granules per thread of a whole window
-    static_assert(W % (16 * NT) == 0, "window granules per thread");
-    const uint64_t ov_a = A0 >> 4, ov_w1 = W1 >> 4;
-    const uint32_t ov_mb = ov_w1 > ov_a ? (uint32_t)((ov_w1 - ov_a) * 16) : 0u;
-    const rsrc_t ov_RM = make_rsrc(blob + A0, ov_mb);
-    const rsrc_t ov_RA = make_rsrc(arena + A0, ov_mb);
-    // KE granules per thread go out before the first_val -> offsets / class-byte loads, the rest
-    // after the class bytes: the sort waits (vmcnt, in issue order) for the class bytes and
-    // therefore for the early granules only
-    constexpr uint32_t KE = DEC_KE < KM ? DEC_KE : KM;
+    static_assert(W % 16 == 0 && W % (16 * NT) == 0, "window granules per thread");
     u32x4 ov_m[KM];
+    uint64_t pre = 0, padded, W1, A0, ov_a, v_lo, v_hi, f_lo, f_hi, sbase = 0;
+    uint32_t ov_mb;
+    rsrc_t ov_RM;
+    uint32_t cls0 = C_N, cnt0 = 0;
+    if constexpr (ONE) {
+        if (tid == 0) lb_store(&state[tile], ONE_RUN);   // (the look-back waits only on windows that run)
+        // count_kernel's other duty: the other half of the context's sums, a slice per window
+        const uint64_t per = (nzero + gridDim.x - 1) / gridDim.x, z0 = (uint64_t)blockIdx.x * per;
+        const uint64_t z1 = z0 + per < nzero ? z0 + per : nzero;
+        for (uint64_t k = z0 + tid; k < z1; k += NT) zero_words[k] = 0;
+        // the window's granules [W0, W0 + win) go out right behind the search's first samples
+        // (bounded by data_cap, not offsets[n]: no round trip first; granules past the batch are
+        // not staged and their arena stores are dropped, below)
+        const uint64_t LE = W0 + win < data_cap ? W0 + win : data_cap;
+        ov_a = W0 >> 4;
+        ov_mb = LE > W0 ? (uint32_t)(LE - W0) : 0u;
+        ov_RM = make_rsrc(blob + W0, ov_mb);
+        const uint64_t on = offsets[n];
+        uint64_t vv[2], ff[2];
+        one_locate<NT>(offsets, n, win, data_cap, tile, on, reinterpret_cast<uint64_t *>(stage), &wpart[0][0], vv, ff,
+                       sbase, [&]() __attribute__((always_inline)) {
 #pragma unroll
-    for (uint32_t k = 0; k < KE; ++k)
-        ov_m[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ov_RM, (int)((tid + k * NT) * 16), 0, 0));
-    // (the values' first offsets come with first_val: one round trip, not first_val -> offsets)
-    const uint64_t v_lo = first_val[tile], v_hi = first_val[tile + 1];
-    const uint64_t f_lo = first_off[tile], f_hi = first_off[tile + 1];
+                           for (uint32_t k = 0; k < KM; ++k)
+                               ov_m[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                                       ov_RM, (int)((tid + k * NT) * 16), 0, 0));
+                       });
+        PROBE(pa = __builtin_amdgcn_s_memtime();)
+        v_lo = vv[0]; v_hi = vv[1]; f_lo = ff[0]; f_hi = ff[1];
+        padded = (on + 15) & ~15ull;
+        W1 = W0 + win < padded ? W0 + win : padded;
+        A0 = W0 > (offsets[0] & ~15ull) ? W0 : (offsets[0] & ~15ull);
+    } else {
+        // 0. the loads of the window's first slot go out first (reduced under the sort)
+        const uint32_t grp = tile / WGROUP, gi = tile % WGROUP;
+        pre = tid < gi ? wtot[(uint64_t)grp * WGROUP + tid] : 0;
+        for (uint32_t k = tid; k < grp; k += NT) pre += gtot[k];
+        padded = (offsets[n] + 15) & ~15ull;
+        W1 = W0 + win < padded ? W0 + win : padded;
+        // the arena copy starts at the call's first value (a call over a slice of a larger buffer —
+        // the chunks of rr_decode_batch_host — copies only its own bytes); the stage always lies
+        // past it (S0 >= offsets[v_lo] >= offsets[0])
+        A0 = W0 > (offsets[0] & ~15ull) ? W0 : (offsets[0] & ~15ull);
+        // the window's own granules [A0, W1) first: their range needs only offsets[0] and
+        // offsets[n], not first_val -> offsets, so the loads go out at the window's start; the
+        // stage's tail [W1, ov_te) (the last values' bytes past the window) follows.  The arena
+        // gets [A0, W1) (stores past it are dropped); granule A0 / 16 + tid + k * NT is at byte
+        // offset 16 (tid + k NT)
+        ov_a = A0 >> 4;
+        ov_mb = (W1 >> 4) > ov_a ? (uint32_t)(((W1 >> 4) - ov_a) * 16) : 0u;
+        ov_RM = make_rsrc(blob + A0, ov_mb);
+        // KE granules per thread go out before the first_val -> offsets / class-byte loads, the
+        // rest after the class bytes: the sort waits (vmcnt, in issue order) for the class bytes
+        // and therefore for the early granules only
+        constexpr uint32_t KE = DEC_KE < KM ? DEC_KE : KM;
+#pragma unroll
+        for (uint32_t k = 0; k < KE; ++k)
+            ov_m[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ov_RM, (int)((tid + k * NT) * 16), 0, 0));
+        // (the values' first offsets come with first_val: one round trip, not first_val -> offsets)
+        v_lo = first_val[tile]; v_hi = first_val[tile + 1];
+        f_lo = first_off[tile]; f_hi = first_off[tile + 1];
+        // the first chunk's class bytes and reservations, loaded before the rest of the window so
+        // their latency hides under it
+        cls0 = v_lo + tid < v_hi ? (uint32_t)cls[v_lo + tid] : C_N;
+        cnt0 = v_lo + tid < v_hi ? counts[v_lo + tid] : 0u;
+#pragma unroll
+        for (uint32_t k = KE; k < KM; ++k)
+            ov_m[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ov_RM, (int)((tid + k * NT) * 16), 0, 0));
+    }
+    const uint64_t ov_w1 = W1 >> 4;
+    // the arena gets [A0, W1): in the ONE form the loads start at W0, so granules below A0 (the
+    // call's first value, in window 0 or in a slice of a larger buffer) are dropped
+    const rsrc_t ov_RA = make_rsrc(arena + ov_a * 16, ov_w1 > ov_a ? (uint32_t)((ov_w1 - ov_a) * 16) : 0u);
     uint64_t S0 = W0, S1 = W0;
     if (v_hi > v_lo) {
         S0 = f_lo & ~15ull;
@@ -1210,14 +1371,14 @@ __global__ __launch_bounds__(NW * RR_WAVE) __attribute__((amdgpu_waves_per_eu(DE
     const uint64_t ov_t0 = ov_w1 > ov_a ? ov_w1 : ov_a;
     const bool staged = S1 - S0 <= STAGE && (S1 >> 4) <= ov_t0 + (uint64_t)KT * NT;
     const uint64_t cap = elem_cap < 0xFFFFFFFFull ? elem_cap : 0xFFFFFFFFull;   // elem_base is 32-bit
-
-    // the first chunk's class bytes and reservations, loaded before the rest of the window so
-    // their latency hides under it
-    const uint32_t cls0 = v_lo + tid < v_hi ? (uint32_t)cls[v_lo + tid] : C_N;
-    const uint32_t cnt0 = v_lo + tid < v_hi ? counts[v_lo + tid] : 0u;
-#pragma unroll
-    for (uint32_t k = KE; k < KM; ++k)
-        ov_m[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ov_RM, (int)((tid + k * NT) * 16), 0, 0));
+    // (ONE: the first chunk's offsets, from the search's first samples when they hold them)
+    uint64_t o_v = 0, o_v1 = 0;
+    if constexpr (ONE) {
+        const uint64_t *a = reinterpret_cast<const uint64_t *>(stage);
+        const uint64_t i0 = v_lo + tid < n ? v_lo + tid : n, i1 = v_lo + tid + 1 < n ? v_lo + tid + 1 : n;
+        o_v = i0 >= sbase && i0 - sbase < NT ? a[i0 - sbase] : offsets[i0];
+        o_v1 = i1 >= sbase && i1 - sbase < NT ? a[i1 - sbase] : offsets[i1];
+    }
     // the stage's tail, also in flight under the sort
     const uint64_t ov_te = (staged && S1 > W1 ? S1 : W1) >> 4;
     const rsrc_t ov_RT = make_rsrc(blob + ov_t0 * 16, ov_te > ov_t0 ? (uint32_t)((ov_te - ov_t0) * 16) : 0u);
@@ -1226,8 +1387,10 @@ __global__ __launch_bounds__(NW * RR_WAVE) __attribute__((amdgpu_waves_per_eu(DE
     for (uint32_t k = 0; k < KT; ++k)
         ov_t[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ov_RT, (int)((tid + k * NT) * 16), 0, 0));
 
-    pre = wave_sum_fast(pre);
-    if (lane == 0) wpart[0][wave] = pre;   // (read after the sort's first barrier)
+    if constexpr (!ONE) {
+        pre = wave_sum_fast(pre);
+        if (lane == 0) wpart[0][wave] = pre;   // (read after the sort's first barrier)
+    }
     auto first_slot = [&]() __attribute__((always_inline)) {
         uint64_t s = 0;
 #pragma unroll
@@ -1246,11 +1409,12 @@ __global__ __launch_bounds__(NW * RR_WAVE) __attribute__((amdgpu_waves_per_eu(DE
     auto ov_finish = [&]() __attribute__((always_inline)) {
 #pragma unroll
         for (uint32_t k = 0; k < KM; ++k) {
-            if (RR_ABLATE != 3)
-                __builtin_amdgcn_raw_buffer_store_b128(ov_m[k], ov_RA, (int)((tid + k * NT) * 16), 0, 2 /* nt */);
             // (a window smaller than W: the main loads' granules past W1 read zeros, and the
             // tail loads bring those stage slots)
             const uint64_t g = ov_a + tid + (uint64_t)k * NT;
+            // (ONE: granules below A0 go to an offset past the resource, which drops the store)
+            const int so = ONE && g < (A0 >> 4) ? 0x7FFFFFF0 : (int)((tid + k * NT) * 16);
+            if (RR_ABLATE != 3) __builtin_amdgcn_raw_buffer_store_b128(ov_m[k], ov_RA, so, 0, 2 /* nt */);
             ov_lds[g < ov_w1 ? ov_slot(g) : STAGE / 16] = ov_m[k];
         }
         // the stage's tail [W1, ov_te): LDS only
@@ -1265,6 +1429,20 @@ __global__ __launch_bounds__(NW * RR_WAVE) __attribute__((amdgpu_waves_per_eu(DE
     const bool far = (!staged && S1 - S0 > 0xFFFFFF00ull) || ((S1 - S0) / 2 + (v_hi - v_lo)) * 16 >= NOSLOT;
     const LdsSrc lsrc{(lds_cptr)stage};
     const GlbSrc gsrc{make_rsrc(blob + S0, (uint32_t)(data_cap - S0 < 0xFFFFFFFFull ? data_cap - S0 : 0xFFFFFFFFull))};
+    // ONE: a value's reservation and class (count_kernel's rule: reserve_classify, a List's
+    // length chain) from the stage once it has landed, or from global memory for a window that
+    // is not staged
+    auto one_class = [&](uint64_t o, uint64_t o1, uint64_t &r, uint32_t &c) __attribute__((always_inline)) {
+        uint32_t d[6];
+        if (staged) {
+            const uint32_t q = (uint32_t)(o - S0);
+            lsrc.get<6>(q, d);   // (reads up to 28 bytes past q: inside the stage's slack)
+            reserve_classify(lsrc.S + q, o1 - o, d, r, c);
+        } else {
+            head24(blob, o, o1, d);
+            reserve_classify(blob + o, o1 - o, d, r, c);
+        }
+    };
 
     uint64_t bad = 0, pay = 0, eb0 = 0, run = 0;   // run: the slots of the earlier chunks
     const uint64_t v_end = RR_ABLATE == 1 ? v_lo : v_hi;
@@ -1278,8 +1456,10 @@ __global__ __launch_bounds__(NW * RR_WAVE) __attribute__((amdgpu_waves_per_eu(DE
         lds_barrier();   // also: the previous chunk's batches are done
         PROBE(if (c0 == v_lo) pt1 = __builtin_amdgcn_s_memtime();)
         const uint32_t i = tid;
-        const uint32_t ci = c0 == v_lo ? cls0 : i < nv ? (uint32_t)cls[c0 + i] : C_N;
-        const uint32_t ri = c0 == v_lo ? cnt0 : i < nv ? counts[c0 + i] : 0u;
+        uint32_t ci, ri;
+        // (ONE: a later chunk's classes and reservations were stored by the window's first pass)
+        ci = c0 == v_lo ? cls0 : i < nv ? (uint32_t)cls[c0 + i] : C_N;
+        ri = c0 == v_lo ? cnt0 : i < nv ? counts[c0 + i] : 0u;
         const uint32_t myc = i < nv ? (far ? C_EXACT : ci) : C_N;
         if (wave * RR_WAVE < nv) {   // (wave-uniform)
 #pragma unroll
@@ -1330,11 +1510,95 @@ __global__ __launch_bounds__(NW * RR_WAVE) __attribute__((amdgpu_waves_per_eu(DE
         return rfl64(ctot);   // (wave-uniform: kept in SGPRs)
     };
     uint64_t ctot = 0;
-    if (v_end > v_lo) {
-        ctot = sort_chunk(v_lo);   // (with the window's loads still in flight)
-        eb0 = rfl64(first_slot());   // (the waves' sums are behind the sort's first barrier)
+    if constexpr (ONE) {
+        // the stage first, then the classes and reservations from it; the window's sum (of the
+        // unsaturated reservations, as count_kernel's window sums) published before the sort and
+        // the look-back resolved after it
+        lds_barrier();   // (every wave has read its offsets from the search's samples)
+        ov_finish();
+        lds_barrier();
+        PROBE(pb = __builtin_amdgcn_s_memtime();)
+        uint64_t ragg = 0;
+        if (v_lo + tid < v_hi) {
+            one_class(o_v, o_v1, ragg, cls0);
+            cnt0 = (uint32_t)(ragg < 0xFFFFFFFFull ? ragg : 0xFFFFFFFFull);
+        }
+        if (v_hi - v_lo > PMAX) {   // a window of more than one chunk: the later chunks' classes
+            for (uint64_t c0 = v_lo + PMAX; c0 < v_hi; c0 += PMAX) {   // and reservations kept in the scratch
+                if (c0 + tid < v_hi) {
+                    uint64_t r;
+                    uint32_t c;
+                    one_class(offsets[c0 + tid], offsets[c0 + tid + 1], r, c);
+                    ragg += r;
+                    cls[c0 + tid] = (uint8_t)c;
+                    counts[c0 + tid] = (uint32_t)(r < 0xFFFFFFFFull ? r : 0xFFFFFFFFull);
+                }
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (read back by other waves of the window)
+        }
+        ragg = wave_sum_fast(ragg);
+        if (lane == 0) red[0][wave] = ragg;
+        lds_barrier();
+        uint64_t agg = 0;
+#pragma unroll
+        for (uint32_t w = 0; w < NW; ++w) agg += red[0][w];
+        // the window's look-back word, then the sort; then every earlier window's word, a thread
+        // each (at most 511: one generation): a window that has not published yet but runs is
+        // waited for; one not running yet (its workgroup not dispatched) is summed here instead,
+        // by wave 0 from global memory (one_window_sum), so no window waits on one that does not run
+        if (tid == 0) lb_store(&state[tile], ONE_RUN | ONE_AGG | agg);
+        if (v_end > v_lo) ctot = sort_chunk(v_lo);
+        __shared__ uint64_t lbw[2][2][NW];   // [round parity][waiting, to help][wave]
+        uint64_t got = 0;
+        bool have = tid >= tile;
+        for (uint32_t it = 0;; ++it) {
+            bool help = false;
+            if (!have) {
+                const uint64_t x = lb_load(&state[tid]);
+                if (x & ONE_AGG) { got = x & ONE_VAL; have = true; }
+                else help = !(x & ONE_RUN);
+            }
+            const uint32_t b = it & 1;
+            const uint64_t wm = __ballot(!have), hm = __ballot(help);
+            if (lane == 0) { lbw[b][0][wave] = wm; lbw[b][1][wave] = hm; }
+            lds_barrier();
+            uint64_t anyw = 0, anyh = 0;
+#pragma unroll
+            for (uint32_t w = 0; w < NW; ++w) { anyw |= lbw[b][0][w]; anyh |= lbw[b][1][w]; }
+            if (!anyw) break;
+            if (it > (1u << 22)) {   // bounded: never hang the GPU (the call reports bytes = ~0)
+                if (tid == 0) lb_store(one + 6, 1);
+                break;
+            }
+            if (anyh) {
+                if (wave == 0) {
+                    for (uint32_t w = 0; w < NW; ++w)
+                        for (uint64_t m = lbw[b][1][w]; m; m &= m - 1) {
+                            const uint32_t q = w * RR_WAVE + (uint32_t)__builtin_ctzll(m);
+                            const uint64_t sq = one_window_sum(blob, offsets, n, win, q);
+                            if (lane == 0) lb_store(&state[q], ONE_AGG | sq);
+                        }
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (visible before the next round)
+                }
+            } else {
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        got = wave_sum_fast(got);
+        if (lane == 0) red[1][wave] = got;
+        lds_barrier();
+        uint64_t e = 0;
+#pragma unroll
+        for (uint32_t w = 0; w < NW; ++w) e += red[1][w];
+        eb0 = rfl64(e);
+        PROBE(pc = __builtin_amdgcn_s_memtime();)
+    } else {
+        if (v_end > v_lo) {
+            ctot = sort_chunk(v_lo);       // (with the window's loads still in flight)
+            eb0 = rfl64(first_slot());     // (the waves' sums are behind the sort's first barrier)
+        }
+        ov_finish();                       // they have landed under the sort
     }
-    ov_finish();                         // they have landed under the sort
     for (uint64_t c0 = v_lo; c0 < v_end; c0 += PMAX) {
         if (c0 != v_lo) {
             lds_barrier();   // every wave is done with the previous chunk's batches
@@ -1402,9 +1666,58 @@ __global__ __launch_bounds__(NW * RR_WAVE) __attribute__((amdgpu_waves_per_eu(DE
     //    in the stage's LDS once every wave's records and descriptors are visible to the others
     if (nfix) {
         __syncthreads();
-        fixup_window<NT>(blob, v_lo, v_hi, values, elems, tot, stage);
+        fixup_window<NT>(blob, v_lo, v_hi, values, elems, ONE ? &s_fix : tot, stage);
+        if (ONE) lds_barrier();   // (s_fix complete)
     }
-    if (tid == 0) {
+    if constexpr (ONE) {
+        // the window's totals into its end word; the call's last window waits for every other
+        // window's, stores the call's totals and leaves the call's words zero (every look-back is
+        // over once every window has ended)
+        uint64_t tb = 0, tp = 0;
+#pragma unroll
+        for (uint32_t w = 0; w < NW; ++w) { tb += red[0][w]; tp += red[1][w]; }
+        tb += s_fix.n_bad;
+        tp += s_fix.payload;   // (u64 wrap: the fixup's adjustments are negative)
+        if (tile != nwin - 1) {
+            if (tid == 0) lb_store(&fin[tile], ONE_AGG | tb << 40 | (tp & ((1ull << 40) - 1)));
+        } else {
+            uint64_t xb = 0, xp = 0;
+            if (tid < tile) {
+                uint64_t x = 0;
+                for (uint32_t sp = 0; !((x = lb_load(&fin[tid])) & ONE_AGG); ++sp) {
+                    if (sp > (1u << 22)) { lb_store(one + 6, 1); break; }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                xb = (x & ~ONE_AGG) >> 40;
+                xp = x & ((1ull << 40) - 1);
+            }
+            lds_barrier();   // (every wave is past its reads of red)
+            xb = wave_sum_fast(xb);
+            xp = wave_sum_fast(xp);
+            if (lane == 0) { red[0][wave] = xb; red[1][wave] = xp; }
+            lds_barrier();
+            if (tid == 0) {
+                for (uint32_t w = 0; w < NW; ++w) { tb += red[0][w]; tp += red[1][w]; }
+                const uint64_t err = lb_load(one + 6);
+                if (tot) {
+                    tot->n_elems = eb0 + run + ctot;
+                    tot->bytes = err ? ~0ull : offsets[n];   // (a wait that never ended)
+                    tot->n_bad = tb;
+                    tot->payload = tp;
+                }
+                lb_store(one + 6, 0);
+            }
+            if (tid < nwin) { lb_store(&state[tid], 0); lb_store(&fin[tid], 0); }
+        }
+        // (probe: [0] locate, [1] stage .. first slot, [2] the rest, [24] locate .. stage landed)
+        PROBE(if (tid == 0) {
+              prb[0] = pa - pt0; prb[1] = pc - pa; prb[2] = __builtin_amdgcn_s_memtime() - pc; prb[24] = pb - pa;
+              prb[28] = v_hi - v_lo; prb[27] = prt0; prb[30] = __builtin_amdgcn_s_memrealtime();
+              prb[31] = (uint64_t)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11)) |
+                        ((uint64_t)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (15 << 11)) << 32);
+              prb[29] = staged; if (g_probe) for (uint32_t i = 0; i < PROBE_WORDS; ++i) g_probe[(uint64_t)tile * PROBE_WORDS + i] = prb[i]; })
+    }
+    if (!ONE && tid == 0) {
         uint64_t tb = 0, tp = 0;
         for (uint32_t w = 0; w < NW; ++w) { tb += red[0][w]; tp += red[1][w]; }
         // the window's {bad, payload} straight into the call's totals (zeroed by count_kernel):
@@ -2981,6 +3294,16 @@ extern "C" hipError_t rr_launch_encode_small(const rr_value *values, const rr_el
 constexpr uint32_t DEC_W = RR_DEC_W, DEC_NW = RR_DEC_NW;
 // (values per sort chunk: one per thread, the chunk's slot scan)
 #define DECODE_KERNEL decode_kernel<RR_DEC_W, RR_DEC_SLACK, RR_DEC_NW, RR_DEC_NW * RR_WAVE>
+#define DECODE_ONE decode_kernel<RR_DEC_W, RR_DEC_SLACK, RR_DEC_NW, RR_DEC_NW * RR_WAVE, true>
+// (RR_DEC_ONE=0 in the environment: the two-launch form for every batch — A/B runs only)
+static bool dec_one(void) {
+    static int v = -1;
+    if (v < 0) {
+        const char *e = getenv("RR_DEC_ONE");
+        v = !(e && e[0] == '0');
+    }
+    return v != 0;
+}
 
 
 // Resident workgroup count for a persistent launch: occupancy query minus one block per CU
@@ -3053,10 +3376,11 @@ extern "C" uint64_t rr_decode_scratch_words(uint64_t data_cap, uint64_t n) {
     const uint64_t nw = dec_windows(data_cap);
     return RR_SCRATCH_HDR + (n + 2) / 2 + (nw + 2) / 2 + (nw + 1) + (n + 7) / 8 + 2;
 }
-// The sums (one half of the context's double buffer): [window sums, nwin] [group sums, nwin / WGROUP + 1]
+// The sums (one half of the context's double buffer): [window sums, nwin] [group sums, nwin / WGROUP + 1],
+// or the one-launch form's words (one_words(nwin) <= this)
 extern "C" uint64_t rr_decode_sums_words(uint64_t data_cap) {
-    const uint64_t nw = dec_windows(data_cap);
-    return nw + dec_groups(nw);
+    const uint64_t nw = dec_windows(data_cap), two = nw + dec_groups(nw);
+    return two > one_words(nw) ? two : one_words(nw);
 }
 
 extern "C" hipError_t rr_launch_decode(const uint8_t *blob, const uint64_t *offsets, uint64_t n, rr_value *values,
@@ -3078,12 +3402,21 @@ extern "C" hipError_t rr_launch_decode(const uint8_t *blob, const uint64_t *offs
             nw = (uint32_t)(data_cap / win + 1);
         }
     }
+    // A batch of one generation of windows: one launch (decode_kernel's ONE form) instead of
+    // count_kernel + decode_kernel.  (The debug hook that withholds the second launch keeps the
+    // two-launch form, which it tests.)
     uint64_t *wtot = sums;
     uint64_t *gtot = wtot + nw;
     uint32_t *counts = reinterpret_cast<uint32_t *>(scratch + RR_SCRATCH_HDR);
     uint32_t *first_val = counts + ((n + 2) & ~1ull);
     uint64_t *first_off = reinterpret_cast<uint64_t *>(first_val + ((nw + 2) & ~1u));
     uint8_t *cls = reinterpret_cast<uint8_t *>(first_off + nw + 1);
+    if (!first_only && nw <= dec_slots() && nw <= DEC_NW * RR_WAVE && dec_one()) {   // (a look-back thread per earlier window)
+        hipLaunchKernelGGL((DECODE_ONE), dim3(nw), dim3(DEC_NW * RR_WAVE), 0, stream, blob, data_cap, offsets, n,
+                           nullptr, nullptr, cls, counts, nullptr, nullptr, values, elems, elem_cap, arena, nw, win,
+                           totals, sums, zero, nzero);
+        return hipGetLastError();
+    }
     if (data_cap < (1ull << 32))
         hipLaunchKernelGGL(count_kernel<true>, dim3((uint32_t)((n + 1 + 255) / 256)), dim3(256), 0, stream, blob, offsets, n,
                            first_val, first_off, nw, win, counts, cls, wtot, gtot, zero, nzero, totals);
@@ -3092,7 +3425,8 @@ extern "C" hipError_t rr_launch_decode(const uint8_t *blob, const uint64_t *offs
                            n, first_val, first_off, nw, win, counts, cls, wtot, gtot, zero, nzero, totals);
     if (first_only) return hipGetLastError();
     hipLaunchKernelGGL((DECODE_KERNEL), dim3(nw), dim3(DEC_NW * RR_WAVE), 0, stream, blob, data_cap, offsets, n,
-                       first_val, first_off, cls, counts, wtot, gtot, values, elems, elem_cap, arena, nw, win, totals);
+                       first_val, first_off, cls, counts, wtot, gtot, values, elems, elem_cap, arena, nw, win, totals,
+                       nullptr, nullptr, 0);
     return hipGetLastError();
 }
 

@@ -44,6 +44,9 @@ print(f"cfg {cfg}: {nwin} windows, staged {int(p[:, 29].sum())}, values/window {
 print("phase cycles per window (mean / p90):  copy %.0f / %.0f   sort %.0f / %.0f   batches %.0f / %.0f" % (
     p[:, 0].mean(), np.percentile(p[:, 0], 90), p[:, 1].mean(), np.percentile(p[:, 1], 90),
     p[:, 2].mean(), np.percentile(p[:, 2], 90)))
+if p[:, 24].any():   # the one-launch form: copy = locate, sort = stage .. first slot
+    print("one-launch: locate %.0f   locate .. stage landed %.0f   stage .. first slot %.0f   (cycles, mean)" % (
+        p[:, 0].mean(), p[:, 24].mean(), (p[:, 1] - p[:, 24]).mean()))
 for c, nm in enumerate(names):
     nbat = p[:, 3 + NC + c].sum()
     if nbat:
