@@ -125,6 +125,8 @@ def lib():
         L.rr_ctx_set_options.argtypes = [vp, C.c_uint]
     if hasattr(L, "rr_debug_fail_second"):   # test hook, not in rr_serdes.h
         L.rr_debug_fail_second.argtypes = [vp]
+    if hasattr(L, "rr_debug_one_help"):   # test hook, not in rr_serdes.h
+        L.rr_debug_one_help.argtypes = [vp]
     L.rr_last_error.restype = C.c_char_p
     L.rr_decode_batch.argtypes = [vp, C.POINTER(BlobBatch), C.POINTER(FlatBatch), vp, vp]
     L.rr_encode_batch.argtypes = [vp, C.POINTER(FlatBatch), C.POINTER(BlobBatch), vp, vp]
@@ -376,6 +378,11 @@ class Engine:
     def debug_fail_second(self):
         """Test hook: the next pipeline call launches only its first kernel and fails."""
         _check(self._L.rr_debug_fail_second(self._ctx))
+
+    def debug_one_help(self):
+        """Test hook: the next one-launch decode sums every earlier window itself (the look-back's
+        help for windows whose workgroups have not started)."""
+        _check(self._L.rr_debug_one_help(self._ctx))
 
     def reserve(self, n: int, nbytes: int = 0):
         _check(self._L.rr_ctx_reserve(self._ctx, n, nbytes))

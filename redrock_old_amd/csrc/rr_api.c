@@ -180,6 +180,13 @@ int rr_debug_fail_second(rr_ctx *c) {
     c->fail_second = 1;
     return RR_API_OK;
 }
+/* test hook (not in rr_serdes.h): the context's next one-launch decode sums every earlier
+ * window itself, as for windows whose workgroups have not started (the look-back's help path) */
+int rr_debug_one_help(rr_ctx *c) {
+    if (!c) return fail(RR_API_EINVAL, "ctx is NULL");
+    c->fail_second = 2;
+    return RR_API_OK;
+}
 #define SMALL_DEC(c, n, cap) (!((c)->options & RR_CTX_NO_SMALL) && rr_small_decode_fits((n), (cap)))
 #define SMALL_ENC(c, n, cap) (!((c)->options & RR_CTX_NO_SMALL) && rr_small_encode_fits((n), (cap)))
 
@@ -241,9 +248,9 @@ int rr_decode_batch(rr_ctx *c, const rr_blob_batch *in, rr_flat_batch *out, rr_t
                                           out->arena, c->scratch, use, zero, nzero, in->data_cap, d_totals,
                                           (hipStream_t)stream, first_only);
     rc = mark_scratch(c, (hipStream_t)stream);
-    if (e != hipSuccess || first_only) {
+    if (e != hipSuccess || first_only == 1) {
         c->dsums_dirty = 1;
-        return first_only ? fail(RR_API_EHIP, "decode: second launch withheld (rr_debug_fail_second)")
+        return first_only == 1 ? fail(RR_API_EHIP, "decode: second launch withheld (rr_debug_fail_second)")
                           : fail(RR_API_EHIP, "decode launch: %s", hipGetErrorString(e));
     }
     return rc;
@@ -265,7 +272,7 @@ int rr_encode_batch(rr_ctx *c, const rr_flat_batch *in, rr_blob_batch *out, rr_t
     int rc = ensure_scratch(c, rr_encode_scratch_words(in->n, out->data_cap), (hipStream_t)stream);
     if (!rc) rc = ensure_dsums(c, 0, rr_encode_sums_words(in->n), (hipStream_t)stream);
     if (rc) return rc;
-    const int first_only = c->fail_second;
+    const int first_only = c->fail_second == 1;   /* (2: the decode's help hook, not an encode's) */
     c->fail_second = 0;
     const hipError_t e = rr_launch_encode(in->values, in->elems, in->elem_cap, in->arena, in->arena_cap, in->n,
                                           out->data, out->data_cap, out->offsets, c->scratch, c->dsums, d_totals,

@@ -23,7 +23,8 @@ struct rr_ctx {
     uint64_t dext[2];                /* words each decode half holds non-zero (its last call's sums) */
     int dphase;                      /* the half the next decode call uses */
     int dsums_dirty;                 /* a call failed midway: re-zero the whole buffer first */
-    int fail_second;             /* test hook (rr_debug_fail_second): the next pipeline call stops after its first kernel */
+    int fail_second;             /* test hooks: 1 (rr_debug_fail_second) the next pipeline call stops after its first
+                                    kernel; 2 (rr_debug_one_help) the next one-launch decode helps every window */
     /* device staging for host entry points */
     void *d_in, *d_off, *d_vals, *d_elems, *d_arena, *d_out, *d_ooff;
     size_t c_in, c_off, c_vals, c_elems, c_arena, c_out, c_ooff;

@@ -1256,7 +1256,7 @@ __global__ __launch_bounds__(NW * RR_WAVE) __attribute__((amdgpu_waves_per_eu(DE
     const uint32_t *__restrict__ first_val, const uint64_t *__restrict__ first_off, uint8_t *__restrict__ cls, uint32_t *__restrict__ counts,
     const uint64_t *wtot, const uint64_t *gtot, rr_value *__restrict__ values,
     rr_elem *__restrict__ elems, uint64_t elem_cap, uint8_t *__restrict__ arena, uint32_t nwin, uint32_t win,
-    rr_totals *tot, uint64_t *one, uint64_t *zero_words, uint64_t nzero) {
+    rr_totals *tot, uint64_t *one, uint64_t *zero_words, uint64_t nzero, uint32_t help_all) {
     constexpr uint32_t NT = NW * RR_WAVE, STAGE = W + SLACK;
     static_assert(PMAX == NT, "a chunk is one value per thread (the slot scan)");
     static_assert(W % 16 == 0 && SLACK % 16 == 0, "tile shape");
@@ -1554,9 +1554,10 @@ __global__ __launch_bounds__(NW * RR_WAVE) __attribute__((amdgpu_waves_per_eu(DE
         for (uint32_t it = 0;; ++it) {
             bool help = false;
             if (!have) {
-                const uint64_t x = lb_load(&state[tid]);
+                const uint64_t x = lb_load(&state[tid]);   // (after the sort: issued before it, the
+                                                           // first read finds fewer words, 14.0 -> 15.1 us)
                 if (x & ONE_AGG) { got = x & ONE_VAL; have = true; }
-                else help = !(x & ONE_RUN);
+                else help = help_all || !(x & ONE_RUN);   // (help_all: the test hook's forced help)
             }
             const uint32_t b = it & 1;
             const uint64_t wm = __ballot(!have), hm = __ballot(help);
@@ -3411,10 +3412,10 @@ extern "C" hipError_t rr_launch_decode(const uint8_t *blob, const uint64_t *offs
     uint32_t *first_val = counts + ((n + 2) & ~1ull);
     uint64_t *first_off = reinterpret_cast<uint64_t *>(first_val + ((nw + 2) & ~1u));
     uint8_t *cls = reinterpret_cast<uint8_t *>(first_off + nw + 1);
-    if (!first_only && nw <= dec_slots() && nw <= DEC_NW * RR_WAVE && dec_one()) {   // (a look-back thread per earlier window)
+    if (first_only != 1 && nw <= dec_slots() && nw <= DEC_NW * RR_WAVE && dec_one()) {   // (a look-back thread per earlier window)
         hipLaunchKernelGGL((DECODE_ONE), dim3(nw), dim3(DEC_NW * RR_WAVE), 0, stream, blob, data_cap, offsets, n,
                            nullptr, nullptr, cls, counts, nullptr, nullptr, values, elems, elem_cap, arena, nw, win,
-                           totals, sums, zero, nzero);
+                           totals, sums, zero, nzero, (uint32_t)(first_only == 2));
         return hipGetLastError();
     }
     if (data_cap < (1ull << 32))
@@ -3423,10 +3424,10 @@ extern "C" hipError_t rr_launch_decode(const uint8_t *blob, const uint64_t *offs
     else
         hipLaunchKernelGGL(count_kernel<false>, dim3((uint32_t)((n + 1 + 255) / 256)), dim3(256), 0, stream, blob, offsets,
                            n, first_val, first_off, nw, win, counts, cls, wtot, gtot, zero, nzero, totals);
-    if (first_only) return hipGetLastError();
+    if (first_only == 1) return hipGetLastError();
     hipLaunchKernelGGL((DECODE_KERNEL), dim3(nw), dim3(DEC_NW * RR_WAVE), 0, stream, blob, data_cap, offsets, n,
                        first_val, first_off, cls, counts, wtot, gtot, values, elems, elem_cap, arena, nw, win, totals,
-                       nullptr, nullptr, 0);
+                       nullptr, nullptr, 0, 0u);
     return hipGetLastError();
 }
 

@@ -303,3 +303,20 @@ def test_failed_second_launch_resets_sums(engine):
     assert t2 == xt and np.array_equal(ooffs, xoffs) and np.array_equal(out, xo)
     v, e, a, t = engine.decode_host(data, offs)   # (and the decode after the encode's failure)
     assert_flat_equal((v, e), (ov, oe), "decode after a withheld encode launch")
+
+
+@pytest.mark.parametrize("cfg,n", [(1, 100000), (4, 30000), (3, 20000), (2, 6000)])
+def test_one_launch_help_path(engine, cfg, n):
+    """The one-launch decode (decode_kernel's ONE form, a batch of one window generation): with
+    the test hook every window sums all earlier windows itself (one_window_sum, the look-back's
+    help for windows whose workgroups have not started) instead of reading their words; the
+    records, descriptors, arena and totals equal the oracle's, and the next call (no hook) is
+    exact too, so the call left its words zero."""
+    data, offs = rr.gen_batch(cfg, n, seed=97 + cfg)
+    ov, oe, oa, ot = cpu.decode(data, offs)
+    for hook in (True, False):
+        if hook:
+            engine.debug_one_help()
+        v, e, a, t = engine.decode_host(data, offs)
+        assert_flat_equal((v, e), (ov, oe), f"cfg {cfg} help {hook}")
+        assert t == ot and np.array_equal(a, oa[:len(a)]), (cfg, hook)
