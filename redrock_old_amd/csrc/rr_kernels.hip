@@ -320,7 +320,8 @@ __device__ __forceinline__ void fold_totals(const uint64_t *__restrict__ stats, 
 }
 
 // ---------------------------------------------------------------------------------------- decode
-// A memset and two launches, no inter-workgroup waits:
+// Two launches, no inter-workgroup waits (a batch of one window generation: decode_kernel's ONE
+// form alone, which does count_kernel's part in each window):
 //   K1 count_kernel   thread per value: its descriptor reservation (rr_format.h) and its walk
 //                     class (rr_decode_class.h; header checks done here), first_val per byte
 //                     window, the reservations summed per window and per group of windows;
@@ -1245,11 +1246,12 @@ __device__ uint64_t one_window_sum(const uint8_t *__restrict__ blob, const uint6
 // its group); each chunk scans its values' reservations in LDS (eloc) while it sorts them, so
 // no scan launch runs between count_kernel and this kernel.
 //
-// ONE (a batch of one generation of windows, no count_kernel): the window's index comes from an
-// atomic ticket and its values from two lower-bound searches of offsets (one_locate); it
-// classifies its values from the stage itself (count_kernel's rule) and finds its first slot by
-// a decoupled look-back over the earlier windows (rr_device.h); the call's totals gather in the
-// context's words and the last window to finish stores them and leaves the words zero (one_words).
+// ONE (a batch of one generation of windows, no count_kernel): the window finds its values by
+// two lower-bound searches of offsets (one_locate), classifies them from its stage itself
+// (count_kernel's rule) and finds its first slot by a flat look-back over the earlier windows'
+// words, waiting only on windows that run (one not dispatched yet is summed here); each window
+// stores its totals in its end word and the last window stores the call's totals and leaves the
+// words zero (one_words).
 template <uint32_t W, uint32_t SLACK, uint32_t NW, uint32_t PMAX, bool ONE = false>
 __global__ __launch_bounds__(NW * RR_WAVE) __attribute__((amdgpu_waves_per_eu(DEC_WPE))) void decode_kernel(
     const uint8_t *__restrict__ blob, uint64_t data_cap, const uint64_t *__restrict__ offsets, uint64_t n,
