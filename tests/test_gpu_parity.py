@@ -775,3 +775,21 @@ def test_config5_per_gpu_shard_at_full_size(engine):
     assert int(gv["elem_base"].max()) + int(gv["n_elems"][gv["elem_base"].argmax()]) == elem_add + shard_descs
     assert int(ge["data"][ref].max()) > 40_000_000_000
     assert_flat_equal((gv, ge), (ov, oe), "config 5 last shard rebased to its whole-batch position")
+
+
+@pytest.mark.parametrize("cfg,n", [(1, 500_000), (2, 60_000), (4, 65_000), (3, 45_000)])
+def test_one_launch_full_generation(engine, cfg, n):
+    """Device-resident batches of one full window generation (up to 512 windows of ~68 KiB) take
+    the one-launch decode (decode_kernel's ONE form): config 1 at 500K values puts ~980 values in
+    a window (two sort chunks: the later chunk's classes kept in the scratch), config 2's Zipf
+    strings leave windows unstaged, configs 3 / 4 the grouped walks.  Records, descriptors,
+    totals and payloads equal the oracle's; the round trip re-encodes the batch."""
+    data, offs = rr.gen_batch(cfg, n)
+    nb = int(offs[-1])
+    v, e, a, tot = _device_decode(data, offs)
+    ov, oe, oa, ot = cpu.decode(data, offs, nthreads=8)
+    assert_flat_equal((v, e), (ov, oe), f"cfg {cfg} one launch")
+    assert (int(tot[0]), int(tot[1]), int(tot[2]), int(tot[3])) == (ot["n_elems"], ot["bytes"], ot["n_bad"], ot["payload"])
+    assert _payload_equal(e, a, oa)
+    out, ooffs, _ = engine.encode_host(v, e, a)
+    assert np.array_equal(ooffs, offs) and out.tobytes() == data[:nb].tobytes()
