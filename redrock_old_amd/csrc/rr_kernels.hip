@@ -769,6 +769,10 @@ __device__ __forceinline__ uint32_t class_vpb(uint32_t c) {
 // class batch order: heaviest walks first (longest-job-first over the window's waves; hash-first
 // instead of ziplist-first measured within noise)
 __constant__ uint32_t CLASS_ORDER[C_N] = {C_ZL, C_SL, C_HH, C_HT, C_LIST, C_EXACT, C_IS, C_STR};
+__device__ __forceinline__ constexpr uint32_t class_at(uint32_t k) {   // CLASS_ORDER[k] for a constant k
+    return k == 0 ? C_ZL : k == 1 ? C_SL : k == 2 ? C_HH : k == 3 ? C_HT : k == 4 ? C_LIST : k == 5 ? C_EXACT
+                                                                                              : k == 6 ? C_IS : C_STR;
+}
 
 // One single-class batch, run by the whole wave: lane < cnt (active) decodes value v (byte
 // offsets relative to the source, whose byte 0 is batch offset B).  The walks run the wave in
@@ -1101,7 +1105,7 @@ __device__ __forceinline__ uint64_t rfl64(uint64_t x) {
 // cycles / counts / lanes into a buffer set by rr_probe_set (PROBE_WORDS u64 per window).
 // Diagnostics only; the product build has none of it.
 #ifdef RR_PROBE
-constexpr uint32_t PROBE_WORDS = 32;
+constexpr uint32_t PROBE_WORDS = 36;   // ([32, 36): the one-launch form's phases)
 __device__ uint64_t *g_probe;
 extern "C" int rr_probe_set(void *p) { return hipMemcpyToSymbol(HIP_SYMBOL(g_probe), &p, sizeof(p)) == hipSuccess ? 0 : -1; }
 #define PROBE(...) __VA_ARGS__
@@ -1268,11 +1272,11 @@ __global__ __launch_bounds__(NW * RR_WAVE) __attribute__((amdgpu_waves_per_eu(DE
     __shared__ uint16_t perm[PMAX];
     __shared__ uint32_t eloc[PMAX + 1];   // chunk-relative first slot of each value, then the chunk's slots
     __shared__ uint64_t wpart[2][NW];     // wave sums: [0] the window's first slot, [1] the chunk's slot scan
-    __shared__ uint32_t ccount[C_N], cbase[C_N], ccur[C_N], bpre[C_N + 1];
+    __shared__ uint32_t ccount[C_N], cbase[C_N], bpre[C_N + 1], wcnt[NW][C_N];
     __shared__ uint32_t next_batch;
     __shared__ uint64_t red[2][NW];
     PROBE(__shared__ uint64_t prb[PROBE_WORDS]; uint64_t pt0 = __builtin_amdgcn_s_memtime(), pt1 = 0, pt2 = 0;
-          const uint64_t prt0 = __builtin_amdgcn_s_memrealtime(); uint64_t pa = 0, pb = 0, pc = 0;
+          const uint64_t prt0 = __builtin_amdgcn_s_memrealtime(); uint64_t pa = 0, pb = 0, pc = 0, pd = 0, pe = 0; uint32_t pit = 0;
           if (threadIdx.x < PROBE_WORDS) prb[threadIdx.x] = 0;)
     const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid / RR_WAVE;
     // (A persistent form — the resident grid walking windows b, b + grid, ..., no workgroup
@@ -1448,43 +1452,55 @@ __global__ __launch_bounds__(NW * RR_WAVE) __attribute__((amdgpu_waves_per_eu(DE
 
     uint64_t bad = 0, pay = 0, eb0 = 0, run = 0;   // run: the slots of the earlier chunks
     const uint64_t v_end = RR_ABLATE == 1 ? v_lo : v_hi;
-    // 2. counting sort of a chunk of values by class (ballot per class, one LDS atomic per
-    //    class per wave-round) into perm, class bases and batch prefixes; and the scan of the
-    //    chunk's reservations into eloc (returns the chunk's slots)
+    // 2. counting sort of a chunk of values by class into perm, class bases and batch prefixes,
+    //    and the scan of the chunk's reservations into eloc (returns the chunk's slots).  One
+    //    barrier: each wave's class counts go to LDS (a ballot per class), then every wave finds
+    //    its own class bases from them (lane c: class c's total and its part in earlier waves, the
+    //    bases in batch order by readlane) and places its values with no atomics (three barriers
+    //    and a returning LDS atomic per class and wave before: config 1's one-launch windows sort
+    //    in 3.9K cycles instead of 5.6K; config 4 at 1M values 0.348-0.353 -> 0.332-0.334 ms).
     auto sort_chunk = [&](uint64_t c0) __attribute__((always_inline)) -> uint64_t {
         const uint32_t nv = (uint32_t)(v_hi - c0 < PMAX ? v_hi - c0 : PMAX);
-        if (tid < C_N) { ccount[tid] = 0; ccur[tid] = 0; }
         if (tid == 0) next_batch = 0;
-        lds_barrier();   // also: the previous chunk's batches are done
         PROBE(if (c0 == v_lo) pt1 = __builtin_amdgcn_s_memtime();)
         const uint32_t i = tid;
-        uint32_t ci, ri;
         // (ONE: a later chunk's classes and reservations were stored by the window's first pass)
-        ci = c0 == v_lo ? cls0 : i < nv ? (uint32_t)cls[c0 + i] : C_N;
-        ri = c0 == v_lo ? cnt0 : i < nv ? counts[c0 + i] : 0u;
+        const uint32_t ci = c0 == v_lo ? cls0 : i < nv ? (uint32_t)cls[c0 + i] : C_N;
+        const uint32_t ri = c0 == v_lo ? cnt0 : i < nv ? counts[c0 + i] : 0u;
         const uint32_t myc = i < nv ? (far ? C_EXACT : ci) : C_N;
-        if (wave * RR_WAVE < nv) {   // (wave-uniform)
+        uint32_t cntc = 0;   // lane c < C_N: this wave's values of class c
+        uint64_t mm = 0;     // the wave's ballot of my class
 #pragma unroll
-            for (uint32_t c = 0; c < C_N; ++c) {
-                const uint64_t m = __ballot(myc == c);
-                if (m && lane == 0) atomicAdd(&ccount[c], (uint32_t)__popcll(m));
-            }
+        for (uint32_t c = 0; c < C_N; ++c) {
+            const uint64_t m = __ballot(myc == c);
+            cntc = lane == c ? (uint32_t)__popcll(m) : cntc;
+            mm = myc == c ? m : mm;
         }
+        if (lane < C_N) wcnt[wave][lane] = cntc;
         const uint64_t incl = wave_incl_scan_fast((uint64_t)ri);
         if (lane == RR_WAVE - 1) wpart[1][wave] = incl;
         lds_barrier();
-        if (tid == 0) {
-            uint32_t s = 0, bs = 0;
-            for (uint32_t k = 0; k < C_N; ++k) {
-                const uint32_t c = CLASS_ORDER[k];
-                const uint32_t vpb = class_vpb(c);
-                cbase[c] = s;
-                bpre[k] = bs;
-                s += ccount[c];
-                bs += (ccount[c] + vpb - 1) / vpb;
+        uint32_t tot_c = 0, below_c = 0;   // lane c < C_N: class c's total, and in earlier waves
+        if (lane < C_N) {
+#pragma unroll
+            for (uint32_t w = 0; w < NW; ++w) {
+                const uint32_t x = wcnt[w][lane];
+                tot_c += x;
+                below_c += w < wave ? x : 0u;
             }
-            bpre[C_N] = bs;
         }
+        uint32_t base_c = 0, s = 0, bs = 0;   // lane c: class c's first perm slot
+#pragma unroll
+        for (uint32_t k = 0; k < C_N; ++k) {
+            const uint32_t c = class_at(k), vpb = class_vpb(c);
+            const uint32_t t = (uint32_t)__builtin_amdgcn_readlane((int)tot_c, (int)c);
+            base_c = lane == c ? s : base_c;
+            if (tid == 0) { cbase[c] = s; ccount[c] = t; bpre[k] = bs; }   // (the batch loop's)
+            s += t;
+            bs += (t + vpb - 1) / vpb;
+        }
+        if (tid == 0) bpre[C_N] = bs;
+        const uint32_t myb = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((myc & (RR_WAVE - 1)) * 4), (int)(base_c + below_c));
         uint64_t wpre = 0, ctot = 0;
 #pragma unroll
         for (uint32_t w = 0; w < NW; ++w) {
@@ -1494,21 +1510,11 @@ __global__ __launch_bounds__(NW * RR_WAVE) __attribute__((amdgpu_waves_per_eu(DE
         }
         // (u32, saturated: slots past 2^32 - 1 fail capacity whatever their exact place)
         const uint64_t mine = wpre + incl - ri;
-        if (i < nv) eloc[i] = (uint32_t)(mine < 0xFFFFFFFFull ? mine : 0xFFFFFFFFull);
-        if (tid == 0) eloc[nv] = (uint32_t)(ctot < 0xFFFFFFFFull ? ctot : 0xFFFFFFFFull);
-        lds_barrier();
-        if (wave * RR_WAVE < nv) {
-#pragma unroll
-            for (uint32_t c = 0; c < C_N; ++c) {
-                const uint64_t m = __ballot(myc == c);
-                if (m) {
-                    uint32_t at = 0;
-                    if (lane == 0) at = atomicAdd(&ccur[c], (uint32_t)__popcll(m));
-                    at = __builtin_amdgcn_readfirstlane(at);   // (lane 0 took the atomic)
-                    if (myc == c) perm[cbase[c] + at + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = (uint16_t)i;
-                }
-            }
+        if (i < nv) {
+            eloc[i] = (uint32_t)(mine < 0xFFFFFFFFull ? mine : 0xFFFFFFFFull);
+            perm[myb + (uint32_t)__popcll(mm & ((1ull << lane) - 1))] = (uint16_t)i;
         }
+        if (tid == 0) eloc[nv] = (uint32_t)(ctot < 0xFFFFFFFFull ? ctot : 0xFFFFFFFFull);
         return rfl64(ctot);   // (wave-uniform: kept in SGPRs)
     };
     uint64_t ctot = 0;
@@ -1549,7 +1555,9 @@ __global__ __launch_bounds__(NW * RR_WAVE) __attribute__((amdgpu_waves_per_eu(DE
         // waited for; one not running yet (its workgroup not dispatched) is summed here instead,
         // by wave 0 from global memory (one_window_sum), so no window waits on one that does not run
         if (tid == 0) lb_store(&state[tile], ONE_RUN | ONE_AGG | agg);
+        PROBE(pd = __builtin_amdgcn_s_memtime();)
         if (v_end > v_lo) ctot = sort_chunk(v_lo);
+        PROBE(pe = __builtin_amdgcn_s_memtime();)
         __shared__ uint64_t lbw[2][2][NW];   // [round parity][waiting, to help][wave]
         uint64_t got = 0;
         bool have = tid >= tile;
@@ -1568,6 +1576,7 @@ __global__ __launch_bounds__(NW * RR_WAVE) __attribute__((amdgpu_waves_per_eu(DE
             uint64_t anyw = 0, anyh = 0;
 #pragma unroll
             for (uint32_t w = 0; w < NW; ++w) { anyw |= lbw[b][0][w]; anyh |= lbw[b][1][w]; }
+            PROBE(pit = it + 1;)
             if (!anyw) break;
             if (it > (1u << 22)) {   // bounded: never hang the GPU (the call reports bytes = ~0)
                 if (tid == 0) lb_store(one + 6, 1);
@@ -1712,9 +1721,10 @@ __global__ __launch_bounds__(NW * RR_WAVE) __attribute__((amdgpu_waves_per_eu(DE
             }
             if (tid < nwin) { lb_store(&state[tid], 0); lb_store(&fin[tid], 0); }
         }
-        // (probe: [0] locate, [1] stage .. first slot, [2] the rest, [24] locate .. stage landed)
+        // (probe: [0] locate, [1] stage .. first slot, [2] the rest, [32] locate .. stage landed,
+        //  [33] classification + publish, [34] the first chunk's sort, [35] look-back rounds)
         PROBE(if (tid == 0) {
-              prb[0] = pa - pt0; prb[1] = pc - pa; prb[2] = __builtin_amdgcn_s_memtime() - pc; prb[24] = pb - pa;
+              prb[0] = pa - pt0; prb[1] = pc - pa; prb[2] = __builtin_amdgcn_s_memtime() - pc; prb[32] = pb - pa; prb[33] = pd - pb; prb[34] = pe - pd; prb[35] = pit;
               prb[28] = v_hi - v_lo; prb[27] = prt0; prb[30] = __builtin_amdgcn_s_memrealtime();
               prb[31] = (uint64_t)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11)) |
                         ((uint64_t)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (15 << 11)) << 32);
