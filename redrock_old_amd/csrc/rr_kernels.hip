@@ -768,8 +768,7 @@ __device__ __forceinline__ uint32_t class_vpb(uint32_t c) {
 }
 // class batch order: heaviest walks first (longest-job-first over the window's waves; hash-first
 // instead of ziplist-first measured within noise)
-__constant__ uint32_t CLASS_ORDER[C_N] = {C_ZL, C_SL, C_HH, C_HT, C_LIST, C_EXACT, C_IS, C_STR};
-__device__ __forceinline__ constexpr uint32_t class_at(uint32_t k) {   // CLASS_ORDER[k] for a constant k
+__device__ __forceinline__ constexpr uint32_t class_at(uint32_t k) {   // {ZL, SL, HH, HT, LIST, EXACT, IS, STR}[k]
     return k == 0 ? C_ZL : k == 1 ? C_SL : k == 2 ? C_HH : k == 3 ? C_HT : k == 4 ? C_LIST : k == 5 ? C_EXACT
                                                                                               : k == 6 ? C_IS : C_STR;
 }
@@ -1272,7 +1271,8 @@ __global__ __launch_bounds__(NW * RR_WAVE) __attribute__((amdgpu_waves_per_eu(DE
     __shared__ uint16_t perm[PMAX];
     __shared__ uint32_t eloc[PMAX + 1];   // chunk-relative first slot of each value, then the chunk's slots
     __shared__ uint64_t wpart[2][NW];     // wave sums: [0] the window's first slot, [1] the chunk's slot scan
-    __shared__ uint32_t ccount[C_N], cbase[C_N], bpre[C_N + 1], wcnt[NW][C_N];
+    __shared__ uint32_t ccount[C_N], cbase[C_N], wcnt[NW][C_N];
+    __shared__ uint64_t bend;   // the batch prefix ends in batch order, a byte each (<= 72 batches a chunk)
     __shared__ uint32_t next_batch;
     __shared__ uint64_t red[2][NW];
     PROBE(__shared__ uint64_t prb[PROBE_WORDS]; uint64_t pt0 = __builtin_amdgcn_s_memtime(), pt1 = 0, pt2 = 0;
@@ -1490,16 +1490,19 @@ __global__ __launch_bounds__(NW * RR_WAVE) __attribute__((amdgpu_waves_per_eu(DE
             }
         }
         uint32_t base_c = 0, s = 0, bs = 0;   // lane c: class c's first perm slot
+        uint64_t be = 0;
 #pragma unroll
         for (uint32_t k = 0; k < C_N; ++k) {
             const uint32_t c = class_at(k), vpb = class_vpb(c);
             const uint32_t t = (uint32_t)__builtin_amdgcn_readlane((int)tot_c, (int)c);
             base_c = lane == c ? s : base_c;
-            if (tid == 0) { cbase[c] = s; ccount[c] = t; bpre[k] = bs; }   // (the batch loop's)
+            if (tid == 0) { cbase[c] = s; ccount[c] = t; }   // (the batch loop's)
             s += t;
             bs += (t + vpb - 1) / vpb;
+            be |= (uint64_t)bs << (8 * k);
         }
-        if (tid == 0) bpre[C_N] = bs;
+        static_assert(PMAX / 8 + C_N < 256, "batch prefix ends fit a byte (vpb >= 8)");
+        if (tid == 0) bend = be;
         const uint32_t myb = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((myc & (RR_WAVE - 1)) * 4), (int)(base_c + below_c));
         uint64_t wpre = 0, ctot = 0;
 #pragma unroll
@@ -1625,18 +1628,26 @@ __global__ __launch_bounds__(NW * RR_WAVE) __attribute__((amdgpu_waves_per_eu(DE
 
         PROBE(if (c0 == v_lo) pt2 = __builtin_amdgcn_s_memtime();)
         // 3. single-class batches, taken dynamically by the waves
-        const uint32_t nb = RR_ABLATE == 2 ? 0u : bpre[C_N];
+        const uint64_t be = rfl64(bend);   // (uniform: SGPRs)
+        const uint32_t nb = RR_ABLATE == 2 ? 0u : (uint32_t)(be >> 56);
         for (;;) {
             uint32_t bi = 0;
             if (lane == 0) bi = atomicAdd(&next_batch, 1u);
             bi = __builtin_amdgcn_readfirstlane(bi);
             if (bi >= nb) break;
-            uint32_t k = 0;
-            while (bi >= bpre[k + 1]) ++k;
-            const uint32_t c = CLASS_ORDER[k];
+            // the batch's class from the packed prefix ends by scalar compares, not an LDS read per
+            // class passed (round 6: config 3 at 1M 0.445 -> 0.438 ms, config 1 at 100K 13.5 -> 13.2 us)
+            uint32_t k = 0, b0 = 0;   // (bi < nb)
+#pragma unroll
+            for (int j = 0; j < C_N - 1; ++j) {
+                const uint32_t e = (uint32_t)(be >> (8 * j)) & 0xFFu;
+                b0 = bi >= e ? e : b0;
+                k += bi >= e;
+            }
+            const uint32_t c = class_at(k);
             const uint32_t vpb = class_vpb(c);
-            const uint32_t first = cbase[c] + (bi - bpre[k]) * vpb;
-            const uint32_t cnt = min(ccount[c] - (bi - bpre[k]) * vpb, vpb);
+            const uint32_t first = cbase[c] + (bi - b0) * vpb;
+            const uint32_t cnt = min(ccount[c] - (bi - b0) * vpb, vpb);
             PROBE(const uint64_t tb0 = __builtin_amdgcn_s_memtime();)
             // lanes per value: the chained classes 64 / cnt (grouped walks; a power of two for
             // Lists, ziplists and hash tables, so a value's lanes lie in one DPP row), hash
