@@ -115,9 +115,11 @@ int rr_ensure_scratch(rr_ctx *c, uint64_t words, hipStream_t stream) {
 
 /* The zero-between-calls sums (rr_internal.h): the encode's group sums, E4's block 0 zeroes
  * what E3 read; the decode's window and group sums, double-buffered — each call adds into one
- * half while its count_kernel zeroes what the previous call left in the other — plus a half for
- * graph-captured decodes, which a captured zeroing kernel re-zeroes at every replay.  So no kernel has to
- * learn that it finishes last (round 4 found that with a returning atomic at every window's end).
+ * half while its count_kernel (or the one-launch decode) zeroes what the previous call left in the
+ * other — plus a half for graph-captured decodes, which a captured zeroing kernel re-zeroes at every
+ * replay.  So no two-launch kernel has to learn that it finishes last (round 4 found that with a
+ * returning atomic at every window's end); the one-launch form's last window by index gathers the
+ * others' end words and leaves its words zero itself.
  * Zeroed once when (re)allocated; like the scratch, growing waits on the previous call and is
  * refused under graph capture.  A call that failed midway leaves dsums_dirty: the next call
  * zeroes the whole buffer first. */
@@ -235,7 +237,7 @@ int rr_decode_batch(rr_ctx *c, const rr_blob_batch *in, rr_flat_batch *out, rr_t
     if (capturing) {   /* the graph's own half, re-zeroed by a captured kernel at every replay */
         use = half[2];
         HIPCHK(rr_launch_zero_words(use, nsums, (hipStream_t)stream));
-    } else {           /* this call's half; its count_kernel zeroes what the previous call left in the other */
+    } else {           /* this call's half; the call zeroes what the previous call left in the other */
         const int x = c->dphase, y = 1 - x;
         use = half[x];
         zero = half[y];

@@ -18,9 +18,11 @@ extern "C" {
 #endif
 
 /* sums: rr_decode_sums_words(data_cap) words, zero on entry (count_kernel adds the window and
- * group sums into them, decode_kernel reads them); zero / nzero: words the call's count_kernel
- * zeroes on the way (the other half of the context's double buffer).  first_only (test hook):
- * launch only the first kernel. */
+ * group sums into them, decode_kernel reads them; a batch of one window generation runs
+ * decode_kernel's one-launch form alone, which keeps its look-back and end words there and leaves
+ * them zero); zero / nzero: words the call zeroes on the way (the other half of the context's
+ * double buffer).  first_only (test hooks): 1 launch only count_kernel (the two-launch form);
+ * 2 the one-launch form sums every earlier window itself (its look-back's help path). */
 hipError_t rr_launch_decode(const uint8_t *blob, const uint64_t *offsets, uint64_t n, rr_value *values,
                             rr_elem *elems, uint64_t elem_cap, uint8_t *arena, uint64_t *scratch, uint64_t *sums,
                             uint64_t *zero, uint64_t nzero, uint64_t data_cap, rr_totals *totals, hipStream_t stream,
