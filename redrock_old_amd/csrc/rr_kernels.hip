@@ -1104,7 +1104,7 @@ __device__ __forceinline__ uint64_t rfl64(uint64_t x) {
 // cycles / counts / lanes into a buffer set by rr_probe_set (PROBE_WORDS u64 per window).
 // Diagnostics only; the product build has none of it.
 #ifdef RR_PROBE
-constexpr uint32_t PROBE_WORDS = 36;   // ([32, 36): the one-launch form's phases)
+constexpr uint32_t PROBE_WORDS = 37;   // ([32, 36): the one-launch form's phases, [36] batch start -> offsets)
 __device__ uint64_t *g_probe;
 extern "C" int rr_probe_set(void *p) { return hipMemcpyToSymbol(HIP_SYMBOL(g_probe), &p, sizeof(p)) == hipSuccess ? 0 : -1; }
 #define PROBE(...) __VA_ARGS__
@@ -1668,6 +1668,11 @@ __global__ __launch_bounds__(NW * RR_WAVE) __attribute__((amdgpu_waves_per_eu(DE
                 eb_v = e1 == 0xFFFFFFFFu ? 1ull << 40 : eb_c + e0;   // (saturated: past every capacity)
                 r_v = e1 - e0;
             }
+            PROBE({   // cycles from the batch's start until its values' offsets are in registers
+                const uint64_t ox = active ? offsets[v] : 0ull;
+                const uint64_t tof = __builtin_amdgcn_s_memtime() - tb0 + (ox == ~0ull ? 1u : 0u);
+                if (lane == 0) atomicAdd((unsigned long long *)&prb[36], (unsigned long long)tof);
+            })
             const Acc a = staged ? run_batch(lsrc, c, active, v, G, g, S0, E, eb_c, blob, offsets, eb_v, r_v, values,
                                              elems, cap, &nfix)
                                  : run_batch(gsrc, c, active, v, G, g, S0, E, eb_c, blob, offsets, eb_v, r_v, values,

@@ -28,14 +28,14 @@ d_arena = torch.empty((nb + 15) & ~15, dtype=torch.uint8, device=dev)
 d_tot = torch.zeros(4, dtype=torch.int64, device=dev)
 # (the call's windows are sized at run time, at least 1 KiB: room for that many)
 nmax = len(data) // 1024 + 2
-probe = torch.zeros(nmax * 36, dtype=torch.int64, device=dev)   # (PROBE_WORDS)
+probe = torch.zeros(nmax * 37, dtype=torch.int64, device=dev)   # (PROBE_WORDS)
 L = rr.lib()
 L.rr_probe_set.argtypes = [C.c_void_p]
 assert L.rr_probe_set(C.c_void_p(probe.data_ptr())) == 0
 for _ in range(3):
     eng.decode_device(d_data, d_offs, d_vals, d_elems, d_arena, d_tot)
 torch.cuda.synchronize()
-p = probe.cpu().numpy().reshape(nmax, 36).astype(np.float64)
+p = probe.cpu().numpy().reshape(nmax, 37).astype(np.float64)
 p = p[(p[:, 0] + p[:, 1] + p[:, 2]) > 0]   # the windows the call ran
 nwin = len(p)
 names = ["STR", "IS", "LIST", "HTSET", "SL", "ZL", "EXACT", "HTHASH"]   # rr_decode_class.h classes
@@ -49,6 +49,10 @@ if p[:, 35].any():   # the one-launch form ([35] its look-back rounds): copy = l
         p[:, 0].mean(), p[:, 32].mean(), (p[:, 1] - p[:, 32]).mean()))
     print("  of which: classify + publish %.0f   first chunk's sort %.0f   look-back %.0f (rounds %.2f, max %d)" % (
         p[:, 33].mean(), p[:, 34].mean(), (p[:, 1] - p[:, 32] - p[:, 33] - p[:, 34]).mean(), p[:, 35].mean(), p[:, 35].max()))
+nbt = p[:, 3 + NC:3 + 2 * NC].sum()
+if p[:, 36].any() and nbt:
+    print("batch start -> its values' offsets in registers: %.0f cycles a batch, %.0f a window (of %.0f batch cycles)" % (
+        p[:, 36].sum() / nbt, p[:, 36].mean(), p[:, 2].mean()))
 for c, nm in enumerate(names):
     nbat = p[:, 3 + NC + c].sum()
     if nbat:
@@ -58,4 +62,4 @@ for c, nm in enumerate(names):
 # XCC_ID << 32) for tools/timeline.py
 out = os.environ.get("PROBE_OUT")
 if out:
-    np.save(out, probe.cpu().numpy().reshape(nmax, 36)[:nwin])
+    np.save(out, probe.cpu().numpy().reshape(nmax, 37)[:nwin])
