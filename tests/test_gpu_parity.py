@@ -793,3 +793,36 @@ def test_one_launch_full_generation(engine, cfg, n):
     assert _payload_equal(e, a, oa)
     out, ooffs, _ = engine.encode_host(v, e, a)
     assert np.array_equal(ooffs, offs) and out.tobytes() == data[:nb].tobytes()
+
+
+@pytest.mark.parametrize("cfg,n,slack", [(1, 100_000, 3), (4, 20_000, 8)])
+def test_one_launch_data_cap_past_the_batch(engine, cfg, n, slack):
+    """A device batch whose buffer (data_cap) runs far past its last value, the tail filled with
+    random bytes: the one-launch form guesses its values from data_cap, so its windows past the
+    data own no values and the search's guess is off; records, descriptors, totals and the
+    arena's [offsets[0], offsets[n]) equal the oracle's, and no byte past the batch is copied."""
+    import torch
+    data, offs = rr.gen_batch(cfg, n)
+    nb = int(offs[-1])
+    cap_b = ((nb + 15) & ~15) * slack
+    dev = torch.device("cuda:0")
+    host = np.random.default_rng(5).integers(0, 256, cap_b, dtype=np.uint8)
+    host[:nb] = data[:nb]
+    d_data = torch.from_numpy(host).to(dev)
+    d_offs = torch.from_numpy(offs.view(np.int64)).to(dev)
+    cap = rr.elem_bound(n, nb)
+    d_vals = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
+    d_elems = torch.zeros(cap * 16, dtype=torch.uint8, device=dev)
+    d_arena = torch.zeros(cap_b, dtype=torch.uint8, device=dev)
+    d_tot = torch.zeros(4, dtype=torch.int64, device=dev)
+    engine.decode_device(d_data, d_offs, d_vals, d_elems, d_arena, d_tot)
+    torch.cuda.synchronize()
+    tot = d_tot.cpu().numpy().view(np.uint64)
+    v = d_vals.cpu().numpy().view(rr.VALUE_DT)
+    e = d_elems.cpu().numpy().view(rr.ELEM_DT)[:int(tot[0])]
+    a = d_arena.cpu().numpy()
+    ov, oe, oa, ot = cpu.decode(data, offs, nthreads=8)
+    assert_flat_equal((v, e), (ov, oe), f"cfg {cfg} data_cap x{slack}")
+    assert (int(tot[0]), int(tot[1]), int(tot[2]), int(tot[3])) == (ot["n_elems"], ot["bytes"], ot["n_bad"], ot["payload"])
+    assert _payload_equal(e, a, oa)
+    assert not a[(nb + 15) & ~15:].any(), "bytes past the batch copied into the arena"
